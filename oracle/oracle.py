@@ -1,0 +1,186 @@
+"""ctypes binding of oracle/build/libst_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference path (st_oracle.c) is the parity checker
+for the MI355X product.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'build', 'libst_oracle.so')
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags='C')
+_lib = None
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c_d, c_u64, c_i = ctypes.c_double, ctypes.c_uint64, ctypes.c_int
+        vp = ctypes.c_void_p
+        L.st_o_exp.restype = c_d
+        L.st_o_exp.argtypes = [c_d]
+        L.st_o_log.restype = c_d
+        L.st_o_log.argtypes = [c_d]
+        for f in ('st_o_quat_from_euler', 'st_o_mat4_trs', 'st_o_mat3_from_quat', 'st_o_rotate_sh',
+                  'st_o_transform', 'st_o_filter_finite', 'st_o_morton_order', 'st_o_pack_compressed',
+                  'st_o_kmeans', 'st_o_cluster1d', 'st_o_sog'):
+            getattr(L, f).restype = c_i
+        L.st_o_filter_finite.restype = c_u64
+        L.st_o_quat_from_euler.argtypes = [c_d, c_d, c_d, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def mulberry32(seed, n):
+    """The Math.random replacement stream used by tests/golden/gen/make_golden.js."""
+    i = np.arange(1, n + 1, dtype=np.uint64)
+    a = ((np.uint64(seed) + i * np.uint64(0x6D2B79F5)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    with np.errstate(over='ignore'):
+        t = (a ^ (a >> np.uint32(15))) * (a | np.uint32(1))
+        t = t ^ (t + (t ^ (t >> np.uint32(7))) * (t | np.uint32(61)))
+    return (t ^ (t >> np.uint32(14))).astype(np.float64) / 4294967296.0
+
+
+def exp(x):
+    return lib().st_o_exp(float(x))
+
+
+def log(x):
+    return lib().st_o_log(float(x))
+
+
+def transform_params(t=(0.0, 0.0, 0.0), euler=None, quat=None, s=1.0):
+    """PlayCanvas Mat4.setTRS / Mat3.setFromQuat / RotateSH as transform() builds them."""
+    L = lib()
+    q = np.array([0, 0, 0, 1], np.float64) if quat is None else np.asarray(quat, np.float64).copy()
+    if euler is not None:
+        L.st_o_quat_from_euler(float(euler[0]), float(euler[1]), float(euler[2]), _p(q))
+    m4 = np.zeros(16, np.float32)
+    m3 = np.zeros(9, np.float32)
+    L.st_o_mat4_trs(_p(np.asarray(t, np.float64)), _p(q), ctypes.c_double(s), _p(m4))
+    L.st_o_mat3_from_quat(_p(q), _p(m3))
+    sh1, sh2, sh3 = np.zeros(9), np.zeros(25), np.zeros(49)
+    L.st_o_rotate_sh(_p(m3), _p(sh1), _p(sh2), _p(sh3))
+    return dict(quat=q, mat4=m4, mat3=m3, sh1=sh1, sh2=sh2, sh3=sh3, s=float(s))
+
+
+def transform(cols, params, sh_coeffs):
+    """In-place transform of a dict of float32 columns (transform.ts:12-65)."""
+    L = lib()
+    g = lambda k: cols.get(k)
+    has = lambda ks: all(k in cols for k in ks)
+    x = _p(g('x')) if has(('x', 'y', 'z')) else None
+    y = _p(g('y')) if x else None
+    z = _p(g('z')) if x else None
+    rot = _ptrs([cols[f'rot_{i}'] for i in range(4)]) if has([f'rot_{i}' for i in range(4)]) else None
+    sc = _ptrs([cols[f'scale_{i}'] for i in range(3)]) if has([f'scale_{i}' for i in range(3)]) else None
+    sh = _ptrs([cols[f'f_rest_{i}'] for i in range(sh_coeffs * 3)]) if sh_coeffs else None
+    n = len(next(iter(cols.values())))
+    L.st_o_transform(ctypes.c_uint64(n), x, y, z, rot, sc, sh, ctypes.c_int(sh_coeffs), _p(params['mat4']),
+                     _p(params['quat']), ctypes.c_double(params['s']), _p(params['sh1']), _p(params['sh2']),
+                     _p(params['sh3']))
+
+
+def filter_finite(col_list):
+    n = len(col_list[0])
+    out = np.zeros(n, np.uint32)
+    m = lib().st_o_filter_finite(ctypes.c_uint64(n), ctypes.c_int(len(col_list)), _ptrs(col_list), _p(out))
+    return out[:m]
+
+
+def morton_order(x, y, z):
+    n = len(x)
+    idx = np.arange(n, dtype=np.uint32)
+    lib().st_o_morton_order(_p(x), _p(y), _p(z), _p(idx), ctypes.c_uint64(n))
+    return idx
+
+
+MEMBERS = ['x', 'y', 'z', 'scale_0', 'scale_1', 'scale_2', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity',
+           'rot_0', 'rot_1', 'rot_2', 'rot_3']
+
+
+def pack_compressed(cols, order, nsh):
+    n = len(order)
+    nch = (n + 255) // 256
+    chunk = np.zeros(nch * 18, np.float32)
+    vertex = np.zeros(n * 4, np.uint32)
+    sh = np.zeros(n * nsh, np.uint8)
+    shc = [cols[f'f_rest_{k}'] for k in range(nsh)]
+    lib().st_o_pack_compressed(ctypes.c_uint64(n), _ptrs([cols[m] for m in MEMBERS]),
+                               _ptrs(shc) if nsh else None, ctypes.c_int(nsh), _p(order), _p(chunk),
+                               _p(vertex), _p(sh))
+    return chunk, vertex, sh
+
+
+def kmeans(col_list, k, iters, draws):
+    d = len(col_list)
+    n = len(col_list[0])
+    kk = k if n >= k else n
+    cent = np.zeros(d * kk, np.float32)
+    labels = np.zeros(n, np.uint32)
+    used = ctypes.c_uint64(0)
+    rc = lib().st_o_kmeans(_ptrs(col_list), ctypes.c_int(d), ctypes.c_uint64(n), ctypes.c_int(k),
+                           ctypes.c_int(iters), _p(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                           _p(cent), _p(labels))
+    return rc, cent.reshape(d, kk), labels, used.value
+
+
+def cluster1d(col_list, iters, draws):
+    n = len(col_list[0])
+    cent = np.zeros(256, np.float32)
+    labels = np.zeros(n * len(col_list), np.uint8)
+    used = ctypes.c_uint64(0)
+    rc = lib().st_o_cluster1d(_ptrs(col_list), ctypes.c_int(len(col_list)), ctypes.c_uint64(n),
+                              ctypes.c_int(iters), _p(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                              _p(cent), _p(labels))
+    return rc, cent, labels.reshape(len(col_list), n), used.value
+
+
+class SogMeta(ctypes.Structure):
+    _fields_ = [('width', ctypes.c_int), ('height', ctypes.c_int),
+                ('means_min', ctypes.c_double * 3), ('means_max', ctypes.c_double * 3),
+                ('scales_codebook', ctypes.c_float * 256), ('sh0_codebook', ctypes.c_float * 256),
+                ('sh_bands', ctypes.c_int), ('palette_size', ctypes.c_int),
+                ('shn_codebook', ctypes.c_float * 256), ('shn_width', ctypes.c_int), ('shn_height', ctypes.c_int)]
+
+
+def sog(cols, sh_coeffs, iters, draws):
+    n = len(cols['x'])
+    w = int(np.ceil(np.sqrt(n) / 4) * 4)
+    h = int(np.ceil(n / w / 4) * 4)
+    tex = {k: np.zeros(w * h * 4, np.uint8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
+    pal = 65536
+    cent = np.zeros(64 * max(sh_coeffs, 1) * ((pal + 63) // 64) * 4, np.uint8)
+    meta = SogMeta()
+    used = ctypes.c_uint64(0)
+    shc = [cols[f'f_rest_{k}'] for k in range(3 * sh_coeffs)]
+    rc = lib().st_o_sog(ctypes.c_uint64(n), _ptrs([cols[m] for m in MEMBERS]), _ptrs(shc) if sh_coeffs else None,
+                        ctypes.c_int(sh_coeffs), ctypes.c_int(iters), _p(draws), ctypes.c_uint64(len(draws)),
+                        ctypes.byref(used), ctypes.byref(meta), _p(tex['means_l']), _p(tex['means_u']),
+                        _p(tex['quats']), _p(tex['scales']), _p(tex['sh0']), _p(cent), _p(tex['shN_labels']))
+    out = {k: v.reshape(h, w, 4) for k, v in tex.items()}
+    if sh_coeffs:
+        out['shN_centroids'] = cent[:meta.shn_width * meta.shn_height * 4].reshape(meta.shn_height, meta.shn_width, 4)
+    else:
+        del out['shN_labels']
+    return rc, out, meta, used.value
