@@ -1,0 +1,153 @@
+/*
+ * st_abi.h -- C-ABI of the MI355X splat-transform hot path (libsplat_hip.so).
+ *
+ * Plain pointers and sizes only.  Each entry point replaces one reference seam
+ * (file:line into praveenpenumaka/splat-transform src/):
+ *
+ *   st_transform / st_dev_transform         transform(dataTable, t, r, s)      transform.ts:12-65
+ *   st_quat_from_euler                      Quat.setFromEulerAngles             process.ts:75-79
+ *   st_transform_params_make                Mat4.setTRS + Mat3.setFromQuat +
+ *                                           new RotateSH(mat3)                  transform.ts:13-15,
+ *                                                                               rotate-sh.ts:49-149
+ *   st_filter_finite / st_dev_filter_finite filter(dt, isFinite-all) indices    process.ts:47-61,84-95
+ *   st_dev_permute_rows                     DataTable.permuteRows               data-table.ts:135-149
+ *   st_dev_concat_rows                      combine() column copy               index.ts:158-210
+ *   st_morton_order / st_dev_morton_order   generateOrdering(dataTable, idx)    ordering.ts:4-110
+ *   st_pack_compressed / st_dev_...         writeCompressedPly chunk loop +
+ *                                           CompressedChunk.pack                write-compressed-ply.ts:56-109,
+ *                                                                               compressed-chunk.ts:44-180
+ *   st_kmeans / st_dev_kmeans               kmeans(points, k, iters) --no-gpu   k-means.ts:137-201,
+ *                                                                               kd-tree.ts:9-100
+ *   st_cluster1d / st_dev_cluster1d         cluster1d(dataTable, iters)         write-sog.ts:56-99
+ *   st_sog / st_dev_sog                     writeSog texture + meta generation  write-sog.ts:110-370
+ *   st_dev_kmeans_* (step API)              one k-means iteration split at the
+ *                                           centroid-sum exchange (multi-GPU)   k-means.ts:164-192
+ *
+ * Conventions
+ *  - Columns are SoA float32 arrays of n rows (the reference's Float32Array
+ *    columns, read-ply.ts:148-150).  st_* entry points take HOST pointers and
+ *    copy through HBM; st_dev_* take DEVICE pointers and run on the context's
+ *    stream (asynchronously unless the function must return a count).
+ *  - Math.random: k-means draws are supplied by the caller as a buffer of
+ *    doubles in [0,1) in the order the reference consumes them; `used`
+ *    returns how many were consumed.  ST_ERR_DRAWS if the buffer is short.
+ *  - Every function returns ST_OK (0) or a negative st_status; the message is
+ *    available from st_last_error() (thread-local).  Data anomalies that the
+ *    reference tolerates (NaN quantises to 0, degenerate extents skip the
+ *    Morton sort) are not errors.  Inputs that crash the reference's k-means
+ *    (non-finite points) return ST_ERR_NONFINITE.
+ */
+#ifndef ST_ABI_H
+#define ST_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ST_ABI_VERSION 1
+
+enum st_status {
+    ST_OK = 0,
+    ST_ERR_ARG = -1,
+    ST_ERR_HIP = -2,
+    ST_ERR_NONFINITE = -3,
+    ST_ERR_DRAWS = -4,
+    ST_ERR_NOMEM = -5,
+    ST_ERR_UNSUPPORTED = -6,
+    ST_ERR_INTERNAL = -7
+};
+
+typedef struct st_ctx st_ctx;
+
+/* SoA table of float32 columns (borrowed for the duration of a call). */
+typedef struct {
+    uint64_t n;                 /* rows */
+    int32_t ncol;               /* columns */
+    const char *const *names;   /* PLY property names: x y z f_dc_0 f_rest_k opacity scale_i rot_i ... */
+    float *const *cols;         /* column base pointers (host or device, per entry point) */
+} st_table;
+
+/* Host-side constants of one transform() call: Mat4.setTRS (f32 storage),
+ * the quaternion r, the uniform scale s and the RotateSH band matrices
+ * (row-major, f64) built from Mat3.setFromQuat(r). */
+typedef struct {
+    float m4[16];
+    double r[4]; /* x, y, z, w */
+    double s;
+    double sh1[9];
+    double sh2[25];
+    double sh3[49];
+} st_transform_params;
+
+typedef struct {
+    int32_t width, height;          /* means/quats/scales/sh0/shN_labels textures (RGBA8) */
+    double means_min[3], means_max[3];
+    float scales_codebook[256];
+    float sh0_codebook[256];
+    int32_t sh_bands;               /* 0..3 */
+    int32_t palette_size;           /* shN.count */
+    float shn_codebook[256];
+    int32_t shn_width, shn_height;  /* shN_centroids texture */
+} st_sog_meta;
+
+typedef struct {
+    uint8_t *means_l, *means_u, *quats, *scales, *sh0; /* width*height*4 each */
+    uint8_t *shn_centroids;                           /* shn_width*shn_height*4 (NULL if sh_bands==0) */
+    uint8_t *shn_labels;                              /* width*height*4 (NULL if sh_bands==0) */
+} st_sog_textures;
+
+/* ---- runtime ------------------------------------------------------------ */
+int st_abi_version(void);
+const char *st_last_error(void);
+int st_device_count(int32_t *count);
+int st_ctx_create(int32_t device, st_ctx **out);
+void st_ctx_destroy(st_ctx *ctx);
+/* Run on a caller-owned hipStream_t (e.g. torch.cuda.current_stream()); NULL restores the context's own stream. */
+int st_ctx_set_stream(st_ctx *ctx, void *hip_stream);
+int st_ctx_synchronize(st_ctx *ctx);
+/* Per-stage device timing (hipEvents) of the last st_*sog / st_*kmeans call, JSON text. */
+const char *st_ctx_last_timings(st_ctx *ctx);
+
+/* ---- host constants ------------------------------------------------------ */
+int st_quat_from_euler(double ex_deg, double ey_deg, double ez_deg, double q_xyzw[4]);
+int st_transform_params_make(const double t[3], const double r_xyzw[4], double s, st_transform_params *out);
+/* SOG texture geometry (write-sog.ts:117-118, :310, :319) */
+int st_sog_geometry(uint64_t n, int32_t sh_coeffs, int32_t *width, int32_t *height,
+                    int32_t *palette_size, int32_t *shn_width, int32_t *shn_height);
+
+/* ---- host-memory entry points ---------------------------------------------- */
+int st_transform(st_ctx *ctx, const st_table *table, const st_transform_params *p);
+int st_filter_finite(st_ctx *ctx, const st_table *table, uint32_t *out_idx, uint64_t *out_n);
+int st_morton_order(st_ctx *ctx, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
+int st_pack_compressed(st_ctx *ctx, const st_table *table, const uint32_t *order,
+                       float *chunk, uint32_t *vertex, uint8_t *sh);
+int st_kmeans(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n, int32_t k, int32_t iters,
+              const double *draws, uint64_t ndraws, uint64_t *used, float *centroids, uint32_t *labels);
+int st_cluster1d(st_ctx *ctx, const float *const *cols, int32_t ncols, uint64_t n, int32_t iters,
+                 const double *draws, uint64_t ndraws, uint64_t *used, float *centroids256, uint8_t *labels);
+int st_sog(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
+           uint64_t *used, st_sog_meta *meta, const st_sog_textures *out);
+
+/* ---- device-memory entry points (device pointers, context stream) ---------- */
+int st_dev_transform(st_ctx *ctx, const st_table *table, const st_transform_params *p);
+int st_dev_filter_finite(st_ctx *ctx, const st_table *table, uint32_t *out_idx, uint64_t *out_n);
+int st_dev_permute_rows(st_ctx *ctx, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst);
+int st_dev_concat_rows(st_ctx *ctx, const st_table *const *srcs, int32_t nsrc, const st_table *dst);
+int st_dev_morton_order(st_ctx *ctx, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
+int st_dev_pack_compressed(st_ctx *ctx, const st_table *table, const uint32_t *order,
+                           float *chunk, uint32_t *vertex, uint8_t *sh);
+/* draws stay on the host (the reference's Math.random lives there) */
+int st_dev_kmeans(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n, int32_t k, int32_t iters,
+                  const double *draws, uint64_t ndraws, uint64_t *used, float *centroids, uint32_t *labels);
+int st_dev_cluster1d(st_ctx *ctx, const float *const *cols, int32_t ncols, uint64_t n, int32_t iters,
+                     const double *draws, uint64_t ndraws, uint64_t *used, float *centroids256, uint8_t *labels);
+int st_dev_sog(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
+               uint64_t *used, st_sog_meta *meta, const st_sog_textures *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ST_ABI_H */

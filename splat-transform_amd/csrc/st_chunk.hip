@@ -1,0 +1,202 @@
+// st_chunk.hip -- compressed-PLY chunk packing (write-compressed-ply.ts:56-109,
+// CompressedChunk.pack compressed-chunk.ts:44-180).
+//
+// One 256-thread workgroup per 256-splat chunk, one lane per splat of the
+// Morton order.  Per-chunk min/max use Math.min/Math.max semantics (NaN
+// propagates, -0 < +0) through wave64 shuffles + LDS; the quantisers run in
+// f64 exactly as the JS; the final partial chunk is padded with its last
+// splat (write-compressed-ply.ts:90-93).  HBM traffic per splat: 14 gathered
+// floats + 3C SH floats in, 16 B vertex + 3C bytes SH out.
+#include "st_internal.h"
+#include "st_jsmath.h"
+
+namespace st {
+namespace {
+
+constexpr double SH_C0 = 0.28209479177387814;
+
+__device__ inline float jmin(float a, float b) {
+    if (a != a || b != b) return __builtin_nanf("");
+    if (a == b) return __builtin_signbit(a) ? a : b;
+    return a < b ? a : b;
+}
+__device__ inline float jmax(float a, float b) {
+    if (a != a || b != b) return __builtin_nanf("");
+    if (a == b) return __builtin_signbit(a) ? b : a;
+    return a > b ? a : b;
+}
+
+// JS min and max over the 256 lanes of the block for NV values each
+template <int NV>
+__device__ inline void block_minmax(float (&mn)[NV], float (&mx)[NV]) {
+    __shared__ float smn[NV][4], smx[NV][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[v] = jmin(mn[v], __shfl_xor(mn[v], o, 64));
+            mx[v] = jmax(mx[v], __shfl_xor(mx[v], o, 64));
+        }
+        if (lane == 0) {
+            smn[v][w] = mn[v];
+            smx[v][w] = mx[v];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        mn[v] = jmin(jmin(smn[v][0], smn[v][1]), jmin(smn[v][2], smn[v][3]));
+        mx[v] = jmax(jmax(smx[v][0], smx[v][1]), jmax(smx[v][2], smx[v][3]));
+    }
+    __syncthreads();
+}
+
+__device__ inline double normalize01(double x, double mn, double mx) {
+    if (x <= mn) return 0;
+    if (x >= mx) return 1;
+    return (mx - mn < 0.00001) ? 0 : (x - mn) / (mx - mn);
+}
+
+__device__ inline uint32_t pack_unorm(double value, int bits) {
+    const double t = (double)((1 << bits) - 1);
+    return (uint32_t)js::to_int32(js::max_(0, js::min_(t, __builtin_floor(value * t + 0.5))));
+}
+
+__device__ inline uint32_t pack111011(double x, double y, double z) {
+    return (pack_unorm(x, 11) << 21) | (pack_unorm(y, 10) << 11) | pack_unorm(z, 11);
+}
+
+__device__ inline uint32_t pack8888(double x, double y, double z, double w) {
+    return (pack_unorm(x, 8) << 24) | (pack_unorm(y, 8) << 16) | (pack_unorm(z, 8) << 8) | pack_unorm(w, 8);
+}
+
+// packRot: Quat(x=rot_0, y=rot_1, z=rot_2, w=rot_3).normalize(), smallest-three 2+10+10+10
+__device__ inline uint32_t pack_rot(double x, double y, double z, double w) {
+    double len = __builtin_sqrt(x * x + y * y + z * z + w * w);
+    double a[4];
+    if (len == 0) {
+        a[0] = a[1] = a[2] = 0;
+        a[3] = 1;
+    } else {
+        len = 1 / len;
+        a[0] = x * len;
+        a[1] = y * len;
+        a[2] = z * len;
+        a[3] = w * len;
+    }
+    int largest = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (__builtin_fabs(a[i]) > __builtin_fabs(a[largest])) largest = i;
+    if (a[largest] < 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = -a[i];
+    }
+    const double norm = __builtin_sqrt(2.0) * 0.5;
+    uint32_t result = (uint32_t)largest;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i != largest) result = (result << 10) | pack_unorm(a[i] * norm + 0.5, 10);
+    return result;
+}
+
+struct ChunkArgs {
+    const float *m[14];  // x y z scale_0..2 f_dc_0..2 opacity rot_0..3
+    const float *const *sh;
+    int nsh;
+    uint64_t n;
+    const uint32_t *order;
+    float *chunk;
+    uint4 *vertex;
+    uint8_t *sh_out;
+};
+
+__global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
+    enum { X, Y, Z, S0, S1, S2, R, G, B, OP, Q0, Q1, Q2, Q3 };
+    const uint64_t c = blockIdx.x;
+    const uint64_t base = c * 256;
+    const uint32_t num = (uint32_t)((a.n < base + 256 ? a.n : base + 256) - base);
+    const uint32_t j = threadIdx.x;
+    const bool real = j < num;
+    const uint32_t row = a.order[base + (real ? j : num - 1)];
+    float d[14];
+#pragma unroll
+    for (int m = 0; m < 14; ++m) d[m] = a.m[m][row];
+    // 8-bit SH (write-compressed-ply.ts:83-87)
+    if (real && a.nsh) {
+        uint8_t *o = a.sh_out + (base + j) * (uint64_t)a.nsh;
+        for (int k = 0; k < a.nsh; ++k) {
+            const double nv = (double)a.sh[k][row] / 8 + 0.5;
+            o[k] = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+        }
+    }
+    float mn[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
+    float mx[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
+    block_minmax<6>(mn, mx);
+    double smn[3], smx[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // clamp(v, -20, 20) = Math.max(-20, Math.min(20, v))
+        smn[i] = js::max_(-20, js::min_(20, (double)mn[3 + i]));
+        smx[i] = js::max_(-20, js::min_(20, (double)mx[3 + i]));
+    }
+    const float col[3] = {(float)((double)d[R] * SH_C0 + 0.5), (float)((double)d[G] * SH_C0 + 0.5),
+                          (float)((double)d[B] * SH_C0 + 0.5)};
+    float cmn[3] = {col[0], col[1], col[2]}, cmx[3] = {col[0], col[1], col[2]};
+    block_minmax<3>(cmn, cmx);
+    if (real) {
+        uint4 v;
+        v.x = pack111011(normalize01(d[X], mn[0], mx[0]), normalize01(d[Y], mn[1], mx[1]),
+                         normalize01(d[Z], mn[2], mx[2]));
+        v.y = pack_rot(d[Q0], d[Q1], d[Q2], d[Q3]);
+        v.z = pack111011(normalize01(d[S0], smn[0], smx[0]), normalize01(d[S1], smn[1], smx[1]),
+                         normalize01(d[S2], smn[2], smx[2]));
+        v.w = pack8888(normalize01(col[0], cmn[0], cmx[0]), normalize01(col[1], cmn[1], cmx[1]),
+                       normalize01(col[2], cmn[2], cmx[2]), js::sigmoid(d[OP]));
+        a.vertex[base + j] = v;
+    }
+    if (j < 18) {
+        const double cd[18] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2], smn[0], smn[1], smn[2],
+                               smx[0], smx[1], smx[2], cmn[0], cmn[1], cmn[2], cmx[0], cmx[1], cmx[2]};
+        a.chunk[c * 18 + j] = (float)cd[j];
+    }
+}
+
+}  // namespace
+
+void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
+                         uint8_t *sh) {
+    const uint64_t n = t->n;
+    if (n == 0) return;
+    static const char *members[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
+                                      "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    ChunkArgs a{};
+    for (int i = 0; i < 14; ++i) {
+        a.m[i] = col_or_null(t, members[i]);
+        ST_REQUIRE(a.m[i], ST_ERR_ARG, std::string("pack_compressed: missing column ") + members[i]);
+    }
+    const int C = sh_coeffs_of(t);
+    a.nsh = 3 * C;
+    if (a.nsh) {
+        ST_REQUIRE(sh, ST_ERR_ARG, "pack_compressed: sh output is NULL");
+        std::vector<float *> p(a.nsh);
+        char nm[32];
+        for (int i = 0; i < a.nsh; ++i) {
+            snprintf(nm, sizeof nm, "f_rest_%d", i);
+            p[i] = col_or_null(t, nm);
+        }
+        auto **d = wsT<float *>(c, "chunk.sh", a.nsh);
+        ST_HIP(hipMemcpyAsync(d, p.data(), sizeof(float *) * a.nsh, hipMemcpyHostToDevice, c->stream));
+        a.sh = d;
+    }
+    a.n = n;
+    a.order = order;
+    a.chunk = chunk;
+    a.vertex = reinterpret_cast<uint4 *>(vertex);
+    a.sh_out = sh;
+    const uint64_t nchunks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
+    ST_LAUNCH_CHECK();
+}
+
+}  // namespace st

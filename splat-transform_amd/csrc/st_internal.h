@@ -1,0 +1,125 @@
+// st_internal.h -- shared runtime pieces of libsplat_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/st_abi.h"
+
+namespace st {
+
+// ---------------------------------------------------------------------------
+// errors: internal code throws st::Error, the extern "C" boundary converts it
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string &msg);
+
+#define ST_HIP(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            throw ::st::Error(ST_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define ST_LAUNCH_CHECK() ST_HIP(hipGetLastError())
+
+#define ST_REQUIRE(cond, code, msg)                  \
+    do {                                             \
+        if (!(cond)) throw ::st::Error((code), (msg)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// grow-only device workspace, one buffer per named slot
+struct Workspace {
+    struct Buf {
+        void *ptr = nullptr;
+        size_t bytes = 0;
+    };
+    std::map<std::string, Buf> bufs;
+    void *get(const std::string &slot, size_t bytes);
+    void release();
+};
+
+struct StageTimer {
+    hipEvent_t ev;
+    std::string name;
+};
+
+}  // namespace st
+
+struct st_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    st::Workspace ws;
+    // pinned host staging for small readbacks
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
+    std::vector<st::StageTimer> marks;
+    bool timing = false;
+    std::string last_timings = "{}";
+};
+
+namespace st {
+
+inline void *ws(st_ctx *c, const std::string &slot, size_t bytes) { return c->ws.get(slot, bytes); }
+template <typename T>
+inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
+    return static_cast<T *>(c->ws.get(slot, count * sizeof(T) + 16));
+}
+void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
+void use_device(st_ctx *c);
+void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
+
+inline unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u << 30) {
+    uint64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------------------
+// primitives (st_prims.hip)
+
+// exclusive scan of n u32 values (out may alias in); returns nothing, total written to *d_total if not null
+void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *d_total);
+
+// stable LSD radix sort of (key, value) pairs on bits [begin_bit, end_bit)
+void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
+                    const std::string &tag);
+void radix_sort_u64(st_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
+                    const std::string &tag);
+
+// iota
+void iota_u32(st_ctx *c, uint32_t *out, uint64_t n);
+
+// column lookups on an st_table
+int find_col(const st_table *t, const char *name);
+float *col_or_null(const st_table *t, const char *name);
+int sh_coeffs_of(const st_table *t);  // band rule: transform.ts:20 / write-sog.ts:296
+
+// module entry points (device pointers)
+void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p);
+uint64_t filter_finite_dev(st_ctx *c, const st_table *t, uint32_t *out_idx);
+void permute_rows_dev(st_ctx *c, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst);
+void concat_rows_dev(st_ctx *c, const st_table *const *srcs, int nsrc, const st_table *dst);
+void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
+void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
+                         uint8_t *sh);
+// returns draws consumed
+uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
+                    uint64_t ndraws, float *centroids, uint32_t *labels);
+uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, int iters, const double *draws,
+                       uint64_t ndraws, float *centroids256, uint8_t *labels);
+uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
+                 const st_sog_textures *out);
+
+}  // namespace st

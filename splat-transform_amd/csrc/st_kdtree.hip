@@ -1,0 +1,238 @@
+// st_kdtree.hip -- the reference's KdTree tie-break for exact-distance ties.
+//
+// When two centroids are at exactly the same f64 distance from a point (e.g.
+// a re-seeded centroid equal to another), the reference's answer is whichever
+// KdTree.findNearest meets first (kd-tree.ts:39-68: nearer child first, strict
+// `<`, prune on distance^2 >= best).  This file rebuilds that tree on the device
+// and walks it for the (rare) tied points only.
+//
+// Tree build (kd-tree.ts:73-99): the recursion only permutes `indices` inside
+// segments whose boundaries depend on K alone -- depth L sorts every segment of
+// length >= 2 by axis L % D (stable), then splits [lo,hi) at mid = lo+(len>>1)
+// (len 2: node lo, right child lo+1).  So each depth is one stable radix sort of
+// (segment rank, coordinate) over the active positions; the segment layout is
+// precomputed on the host per K.
+// Walk: one thread per tied point over the implicit tree, with every exact
+// distance precomputed by a wave-parallel kernel, so each visit is O(1).
+#include <memory>
+#include <unordered_map>
+
+#include "st_jsmath.h"
+#include "st_kmeans.h"
+
+namespace st {
+namespace {
+
+using namespace km;
+
+struct Level {
+    uint32_t count;      // active positions at this depth
+    uint32_t seg_bits;   // bits of the segment rank
+    uint32_t *pos;       // device: active positions (ascending)
+    uint32_t *rank;      // device: segment rank of each active position
+};
+
+struct KdLayout {
+    int k = 0;
+    std::vector<Level> levels;
+    std::vector<void *> allocs;
+    ~KdLayout() {
+        for (void *p : allocs) (void)hipFree(p);
+    }
+};
+
+// host: the segment structure of KdTree.build for k centroids
+std::unique_ptr<KdLayout> make_layout(int k) {
+    auto L = std::make_unique<KdLayout>();
+    L->k = k;
+    std::vector<std::pair<uint32_t, uint32_t>> segs = {{0u, (uint32_t)k}}, next;
+    while (!segs.empty()) {
+        std::vector<uint32_t> pos, rank;
+        uint32_t r = 0;
+        next.clear();
+        for (auto s : segs) {
+            const uint32_t len = s.second - s.first;
+            if (len >= 2) {
+                for (uint32_t p = s.first; p < s.second; ++p) {
+                    pos.push_back(p);
+                    rank.push_back(r);
+                }
+                ++r;
+            }
+            if (len == 2) {
+                // right child is a single leaf: nothing further to sort
+            } else if (len >= 3) {
+                const uint32_t mid = s.first + (len >> 1);
+                next.push_back({s.first, mid});
+                next.push_back({mid + 1, s.second});
+            }
+        }
+        if (!pos.empty()) {
+            Level lv{};
+            lv.count = (uint32_t)pos.size();
+            uint32_t bits = 0;
+            while ((1u << bits) < r) ++bits;
+            lv.seg_bits = bits;
+            ST_HIP(hipMalloc(&lv.pos, pos.size() * 4));
+            ST_HIP(hipMalloc(&lv.rank, rank.size() * 4));
+            L->allocs.push_back(lv.pos);
+            L->allocs.push_back(lv.rank);
+            ST_HIP(hipMemcpy(lv.pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice));
+            ST_HIP(hipMemcpy(lv.rank, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
+            L->levels.push_back(lv);
+        }
+        segs.swap(next);
+    }
+    return L;
+}
+
+__global__ __launch_bounds__(256) void k_level_keys(const float *__restrict__ cen, int k, int axis,
+                                                    const uint32_t *__restrict__ S, const uint32_t *__restrict__ pos,
+                                                    const uint32_t *__restrict__ rank, uint32_t m,
+                                                    uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        const uint32_t ci = S[pos[j]];
+        keys[j] = ((uint64_t)rank[j] << 32) | sortkey_(cen[(uint64_t)axis * k + ci]);
+        vals[j] = ci;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_level_scatter(const uint32_t *__restrict__ pos,
+                                                       const uint32_t *__restrict__ vals, uint32_t m,
+                                                       uint32_t *__restrict__ S) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) S[pos[j]] = vals[j];
+}
+
+// exact distances of one tied point to every centroid (kd-tree.ts:26-35)
+__global__ __launch_bounds__(256) void k_all_dist(const float *const *cols, int d, const float *__restrict__ cen,
+                                                  int k, const uint32_t *__restrict__ tie_pts, uint32_t first,
+                                                  double *__restrict__ dist) {
+    const uint32_t t = blockIdx.y;
+    const uint32_t p = tie_pts[first + t];
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < (uint32_t)k; c += gridDim.x * blockDim.x) {
+        double l = 0;
+        for (int i = 0; i < d; ++i) {
+            const double v = (double)cen[(uint64_t)i * k + c] - (double)cols[i][p];
+            l += v * v;
+        }
+        dist[(uint64_t)t * k + c] = l;
+    }
+}
+
+struct Frame {
+    uint32_t lo, hi, depth;
+};
+
+__device__ inline void seg_split(uint32_t lo, uint32_t hi, uint32_t &node, uint32_t &llo, uint32_t &lhi,
+                                 uint32_t &rlo, uint32_t &rhi) {
+    const uint32_t len = hi - lo;
+    if (len == 1) {
+        node = lo;
+        llo = lhi = rlo = rhi = 0;
+    } else if (len == 2) {
+        node = lo;
+        llo = lhi = 0;
+        rlo = lo + 1;
+        rhi = lo + 2;
+    } else {
+        node = lo + (len >> 1);
+        llo = lo;
+        lhi = node;
+        rlo = node + 1;
+        rhi = hi;
+    }
+}
+
+__global__ void k_kd_walk(const float *const *cols, int d, const float *__restrict__ cen, int k,
+                          const uint32_t *__restrict__ S, const uint32_t *__restrict__ tie_pts, uint32_t first,
+                          uint32_t count, const double *__restrict__ dist, uint32_t *__restrict__ labels) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint32_t p = tie_pts[first + t];
+    const double *dd = dist + (uint64_t)t * k;
+    double mind = __builtin_inf();
+    uint32_t mini = 0xffffffffu;
+    Frame stack[64];
+    int sp = 0;
+    uint32_t clo = 0, chi = (uint32_t)k, cdepth = 0;
+    bool descend = true;
+    while (true) {
+        if (descend) {
+            while (chi > clo) {
+                stack[sp++] = Frame{clo, chi, cdepth};
+                uint32_t node, llo, lhi, rlo, rhi;
+                seg_split(clo, chi, node, llo, lhi, rlo, rhi);
+                const int axis = (int)(cdepth % (uint32_t)d);
+                const double distance = (double)cols[axis][p] - (double)cen[(uint64_t)axis * k + S[node]];
+                if (distance > 0) {
+                    clo = rlo;
+                    chi = rhi;
+                } else {
+                    clo = llo;
+                    chi = lhi;
+                }
+                ++cdepth;
+            }
+        }
+        if (sp == 0) break;
+        const Frame f = stack[--sp];
+        uint32_t node, llo, lhi, rlo, rhi;
+        seg_split(f.lo, f.hi, node, llo, lhi, rlo, rhi);
+        const int axis = (int)(f.depth % (uint32_t)d);
+        const uint32_t ci = S[node];
+        const double distance = (double)cols[axis][p] - (double)cen[(uint64_t)axis * k + ci];
+        const double thisd = dd[ci];
+        if (thisd < mind) {
+            mind = thisd;
+            mini = ci;
+        }
+        const uint32_t olo = (distance > 0) ? llo : rlo, ohi = (distance > 0) ? lhi : rhi;
+        if (distance * distance < mind && ohi > olo) {
+            clo = olo;
+            chi = ohi;
+            cdepth = f.depth + 1;
+            descend = true;
+        } else {
+            descend = false;
+        }
+    }
+    labels[p] = mini;
+}
+
+}  // namespace
+
+void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels) {
+    (void)n;
+    static thread_local std::unordered_map<int64_t, std::unique_ptr<KdLayout>> layouts;
+    auto &L = layouts[((int64_t)c->device << 32) | (uint32_t)k];
+    if (!L) L = make_layout(k);
+    auto *S = wsT<uint32_t>(c, "kd.S", (size_t)k);
+    auto *keys = wsT<uint64_t>(c, "kd.keys", (size_t)k);
+    auto *vals = wsT<uint32_t>(c, "kd.vals", (size_t)k);
+    iota_u32(c, S, (uint64_t)k);
+    for (size_t lv = 0; lv < L->levels.size(); ++lv) {
+        const Level &v = L->levels[lv];
+        const int axis = (int)(lv % (size_t)d);
+        hipLaunchKernelGGL(k_level_keys, dim3(grid_for(v.count, 256, 1024)), dim3(256), 0, c->stream, cen, k, axis, S,
+                           v.pos, v.rank, v.count, keys, vals);
+        ST_LAUNCH_CHECK();
+        radix_sort_u64(c, keys, vals, v.count, 0, 32 + (int)v.seg_bits, "kd.rs");
+        hipLaunchKernelGGL(k_level_scatter, dim3(grid_for(v.count, 256, 1024)), dim3(256), 0, c->stream, v.pos, vals,
+                           v.count, S);
+        ST_LAUNCH_CHECK();
+    }
+    const uint32_t batch = 64;
+    auto *dist = wsT<double>(c, "kd.dist", (size_t)batch * k);
+    for (uint32_t first = 0; first < nties; first += batch) {
+        const uint32_t cnt = (nties - first < batch) ? (nties - first) : batch;
+        hipLaunchKernelGGL(k_all_dist, dim3(grid_for(k, 256, 64), cnt), dim3(256), 0, c->stream, dcols, d, cen, k,
+                           tie_pts, first, dist);
+        ST_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_kd_walk, dim3((cnt + 63) / 64), dim3(64), 0, c->stream, dcols, d, cen, k, S, tie_pts,
+                           first, cnt, dist, labels);
+        ST_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace st

@@ -1,0 +1,51 @@
+// st_kmeans.h -- internal interfaces shared by the k-means translation units.
+#pragma once
+
+#include "st_internal.h"
+
+namespace st {
+namespace km {
+
+enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u };
+
+// device-resident k-means state (one per call)
+struct State {
+    uint64_t cursor;  // Math.random draws consumed so far
+    uint32_t err;
+    uint32_t amb;     // ambiguous points this iteration (D > 1)
+    uint32_t ties;    // exact-distance ties this iteration (D > 1)
+    uint32_t pad;
+};
+
+__host__ __device__ inline uint32_t fkey_(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float fkey_inv_(uint32_t k) {
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    return __builtin_bit_cast(float, u);
+}
+// stable-sort key of a centroid coordinate under the comparator `a - b`
+// (k-means / kd-tree sort callbacks): -0 and +0 compare equal
+__host__ __device__ inline uint32_t sortkey_(float f) { return fkey_(f == 0.0f ? 0.0f : f); }
+
+}  // namespace km
+
+// shared by the 1-D and N-D loops
+void reseed_empty(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *start,
+                  const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen);
+// start[c] = first index with sorted_labels >= c, start[k] = n
+void bounds_from_sorted(st_ctx *c, const uint32_t *sorted_labels, uint64_t n, int k, uint32_t *start);
+void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t *sorted_labels, uint32_t *members,
+                 uint32_t *start);
+
+void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
+                   const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
+void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
+                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
+
+// KdTree tie-break for exact-distance ties (st_kdtree.hip)
+void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels);
+
+}  // namespace st

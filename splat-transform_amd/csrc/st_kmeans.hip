@@ -1,0 +1,228 @@
+// st_kmeans.hip -- kmeans() on the --no-gpu semantics (k-means.ts:137-201).
+//
+// Parity target: labels = exact nearest centroid under the reference's f64
+// distance with the KdTree's traversal tie-break (kd-tree.ts:22-71), means =
+// f64 running sums in ascending point order (calcAverage, k-means.ts:41-63),
+// empty clusters re-seeded from the caller's Math.random stream in ascending
+// cluster order, labels from the last assign and centroids after the last
+// update.
+//
+// Assign, D == 1: the KdTree over 1-D centroids is the implicit BST over the
+//   stably sorted centroid values, so every point walks it exactly as
+//   findNearest does (same pruning, same tie-break).
+// Assign, D > 1 (SH palette, K up to 65,536): score(c) = |c|^2 - 2 p.c on the
+//   matrix cores as a bf16x3 split GEMM (v_mfma_f32_32x32x16_bf16, K-dim
+//   3*roundup(D+3,16)), a running top-2 per point in the epilogue, and a
+//   rigorous per-point error bound W_p.  A point whose runner-up is > W_p
+//   behind is decided; the rest (~1%) gather every centroid within W_p and
+//   resolve them with the reference's exact f64 distance; exact ties go to a
+//   KdTree traversal (st_kdtree.hip).
+// Update: stable radix sort of (label, point) gives each cluster its members
+//   in ascending order; 1-D clusters sum in parallel when an exactness
+//   certificate proves every partial sum is representable (then any order
+//   equals the sequential sum), otherwise sequentially.
+#include "st_internal.h"
+#include "st_jsmath.h"
+#include "st_kmeans.h"
+
+namespace st {
+namespace km {
+
+// ---------------------------------------------------------------------------
+// common kernels
+
+__global__ __launch_bounds__(256) void k_nonfinite(const float *const *cols, int d, uint64_t n, uint32_t *flag) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t bad = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        for (int c = 0; c < d; ++c) bad |= js::isfinitef_(cols[c][i]) ? 0u : 1u;
+    if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// initializeCentroids1D (k-means.ts:23-39)
+__global__ __launch_bounds__(256) void k_minmax1d(const float *v, uint64_t n, uint32_t *mm) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        lo = fminf(lo, v[i]);
+        hi = fmaxf(hi, v[i]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], fkey_(lo));
+        atomicMax(&mm[1], fkey_(hi));
+    }
+}
+
+__global__ void k_init1d(const uint32_t *mm, float *cen, int k) {
+    const double m = fkey_inv_(mm[0]), M = fkey_inv_(mm[1]);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x)
+        cen[i] = (float)(m + (M - m) * i / (k - 1));
+}
+
+// centroids[c][i] = points[c][rows[i]]
+__global__ __launch_bounds__(256) void k_gather_init(const float *const *cols, int d, const uint32_t *rows, int k,
+                                                     float *cen) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) {
+        const uint32_t r = rows[i];
+        for (int c = 0; c < d; ++c) cen[(uint64_t)c * k + i] = cols[c][r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// update: cluster boundaries in the label-sorted member list
+__global__ __launch_bounds__(256) void k_bounds(const uint32_t *__restrict__ sorted_labels, uint64_t n, int k,
+                                                uint32_t *__restrict__ start) {
+    // start[c] = first position with label >= c ; start[k] = n
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c <= k; c += gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            uint64_t mid = (lo + hi) >> 1;
+            if (sorted_labels[mid] < (uint32_t)c) lo = mid + 1; else hi = mid;
+        }
+        start[c] = (uint32_t)lo;
+    }
+}
+
+// re-seed empty clusters (k-means.ts:174-178): the j-th empty cluster (ascending)
+// takes draw cursor+j; rank comes from an exclusive scan of the empty flags
+__global__ __launch_bounds__(256) void k_empty_flags(const uint32_t *start, int k, uint32_t *flags) {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < k; c += gridDim.x * blockDim.x)
+        flags[c] = (start[c + 1] == start[c]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_reseed(const float *const *cols, int d, uint64_t n, int k,
+                                                const uint32_t *flags, const uint32_t *rank, const double *draws,
+                                                uint64_t ndraws, State *st, float *cen) {
+    const uint64_t cursor = st->cursor;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < k; c += gridDim.x * blockDim.x) {
+        if (!flags[c]) continue;
+        const uint64_t di = cursor + rank[c];
+        if (di >= ndraws) {
+            atomicOr(&st->err, ERR_DRAWS);
+            continue;
+        }
+        const uint64_t row = (uint64_t)__builtin_floor(draws[di] * (double)n);
+        for (int j = 0; j < d; ++j) cen[(uint64_t)j * k + c] = cols[j][row];
+    }
+}
+
+__global__ void k_advance_cursor(State *st, const uint32_t *total_empty) { st->cursor += *total_empty; }
+
+}  // namespace km
+
+using namespace km;
+
+// ---------------------------------------------------------------------------
+static void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
+    auto *flag = wsT<uint32_t>(c, "km.nf", 1);
+    ST_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_nonfinite, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c->stream, dcols, d, n, flag);
+    ST_LAUNCH_CHECK();
+    auto *h = static_cast<uint32_t *>(pinned(c, 16));
+    ST_HIP(hipMemcpyAsync(h, flag, 4, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    ST_REQUIRE(h[0] == 0, ST_ERR_NONFINITE,
+               "kmeans: non-finite point (the reference's KdTree returns index -1 and k-means.ts:131 throws)");
+}
+
+// reseed + cursor bookkeeping shared by both update paths
+void reseed_empty(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *start,
+                  const double *ddraws, uint64_t ndraws, State *dstate, float *cen) {
+    auto *flags = wsT<uint32_t>(c, "km.eflags", (size_t)k + 1);
+    auto *rank = wsT<uint32_t>(c, "km.erank", (size_t)k + 1);
+    hipLaunchKernelGGL(k_empty_flags, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, start, k, flags);
+    scan_u32(c, flags, rank, (uint64_t)k, rank + k);
+    hipLaunchKernelGGL(k_reseed, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, n, k, flags, rank,
+                       ddraws, ndraws, dstate, cen);
+    hipLaunchKernelGGL(k_advance_cursor, dim3(1), dim3(1), 0, c->stream, dstate, rank + k);
+    ST_LAUNCH_CHECK();
+}
+
+void bounds_from_sorted(st_ctx *c, const uint32_t *sorted_labels, uint64_t n, int k, uint32_t *start) {
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)k + 1, 256, 1024)), dim3(256), 0, c->stream, sorted_labels,
+                       n, k, start);
+    ST_LAUNCH_CHECK();
+}
+
+void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t *sorted_labels, uint32_t *members,
+                 uint32_t *start) {
+    ST_HIP(hipMemcpyAsync(sorted_labels, labels, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    iota_u32(c, members, n);
+    int bits = 1;
+    while ((1ull << bits) < (uint64_t)k) ++bits;
+    radix_sort_u32(c, sorted_labels, members, n, 0, bits, "km.ms");
+    bounds_from_sorted(c, sorted_labels, n, k, start);
+}
+
+uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
+                    uint64_t ndraws, float *cen, uint32_t *labels) {
+    ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans: n must be < 2^31 per device");
+    if (n < (uint64_t)k) {  // k-means.ts:139-144
+        for (int j = 0; j < d; ++j)
+            ST_HIP(hipMemcpyAsync(cen + (uint64_t)j * n, cols[j], n * sizeof(float), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        iota_u32(c, labels, n);
+        return 0;
+    }
+    auto **dcols = wsT<const float *>(c, "km.cols", (size_t)d);
+    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
+    check_finite(c, dcols, d, n);
+    mark(c, "km.check");
+
+    // Math.random stream: uploaded once, consumed on device in reference order
+    const uint64_t nd = ndraws ? ndraws : 1;
+    auto *ddraws = wsT<double>(c, "km.draws", nd);
+    if (ndraws) ST_HIP(hipMemcpyAsync(ddraws, draws, ndraws * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    auto *dstate = static_cast<State *>(ws(c, "km.state", sizeof(State)));
+    State hs{};
+    uint64_t init_used = 0;
+    if (d == 1) {
+        auto *mm = wsT<uint32_t>(c, "km.mm", 2);
+        const uint32_t init_mm[2] = {0xffffffffu, 0u};
+        ST_HIP(hipMemcpyAsync(mm, init_mm, 8, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_minmax1d, dim3(grid_for(n, 256, 1024)), dim3(256), 0, c->stream, cols[0], n, mm);
+        hipLaunchKernelGGL(k_init1d, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, mm, cen, k);
+        ST_LAUNCH_CHECK();
+    } else {
+        // initializeCentroids (k-means.ts:8-20): k distinct rows by rejection on the
+        // host-owned Math.random stream; the rows are then gathered on the device.
+        std::vector<uint32_t> rows(k);
+        std::vector<uint8_t> chosen(n, 0);
+        uint64_t cur = 0;
+        for (int i = 0; i < k; ++i) {
+            uint64_t cand;
+            do {
+                ST_REQUIRE(cur < ndraws, ST_ERR_DRAWS, "kmeans: Math.random draws exhausted during initialisation");
+                cand = (uint64_t)std::floor(draws[cur++] * (double)n);
+            } while (chosen[cand]);
+            chosen[cand] = 1;
+            rows[i] = (uint32_t)cand;
+        }
+        init_used = cur;
+        auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
+        ST_HIP(hipMemcpyAsync(drows, rows.data(), sizeof(uint32_t) * k, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_gather_init, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, drows, k,
+                           cen);
+        ST_LAUNCH_CHECK();
+    }
+    hs.cursor = init_used;
+    ST_HIP(hipMemcpyAsync(dstate, &hs, sizeof(State), hipMemcpyHostToDevice, c->stream));
+    mark(c, "km.init");
+
+    if (d == 1)
+        kmeans1d_loop(c, cols[0], dcols, n, k, iters, ddraws, ndraws, dstate, cen, labels);
+    else
+        kmeansnd_loop(c, cols, dcols, d, n, k, iters, ddraws, ndraws, dstate, cen, labels);
+
+    ST_HIP(hipMemcpyAsync(&hs, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
+    ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");
+    return hs.cursor;
+}
+
+}  // namespace st

@@ -1,0 +1,221 @@
+// st_kmeans1d.hip -- 1-D k-means (cluster1d's K=256 codebooks, write-sog.ts:56-99).
+//
+// Assign: the reference rebuilds a KdTree over the centroids every iteration
+// (k-means.ts:104).  With one column every level sorts by the same key, so the
+// tree is the implicit BST over the stably sorted centroid values: segment
+// [lo,hi) has its node at lo+(len>>1) (len 2: node lo, right child lo+1).  Each
+// point walks that tree exactly like KdTree.findNearest (kd-tree.ts:39-68):
+// nearer child first, strict `<` on the f64 squared distance, prune when
+// distance^2 >= best.  This reproduces the reference's tie-break bit-for-bit.
+//
+// Update: a stable sort by label lays each cluster's values out contiguously in
+// ascending point order.  One workgroup per cluster sums them in f64: in
+// parallel when every value is a multiple of 2^e and sum|x| < 2^(e+53) (then
+// every partial sum is exact, so any order equals calcAverage's sequential
+// sum), otherwise in the reference's order.
+#include "st_jsmath.h"
+#include "st_kmeans.h"
+
+namespace st {
+namespace {
+
+using namespace km;
+
+constexpr int KD1_LDS = 4096;  // centroids kept in LDS up to this K
+
+__global__ __launch_bounds__(256) void k_sortkeys(const float *cen, int k, uint32_t *keys, uint32_t *vals) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) {
+        keys[i] = sortkey_(cen[i]);
+        vals[i] = (uint32_t)i;
+    }
+}
+
+struct Seg {
+    uint32_t lo, hi;
+};
+
+// node / children of an implicit-tree segment
+__device__ inline void seg_node(Seg s, uint32_t &node, Seg &left, Seg &right) {
+    const uint32_t len = s.hi - s.lo;
+    if (len == 1) {
+        node = s.lo;
+        left = right = Seg{0, 0};
+    } else if (len == 2) {
+        node = s.lo;
+        left = Seg{0, 0};
+        right = Seg{s.lo + 1, s.lo + 2};
+    } else {
+        const uint32_t mid = s.lo + (len >> 1);
+        node = mid;
+        left = Seg{s.lo, mid};
+        right = Seg{mid + 1, s.hi};
+    }
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void k_kd1_assign(const float *__restrict__ pts, uint64_t n,
+                                                    const float *__restrict__ cen, const uint32_t *__restrict__ order,
+                                                    int k, uint32_t *__restrict__ labels) {
+    __shared__ float sv[LDS ? KD1_LDS : 1];
+    __shared__ uint32_t si[LDS ? KD1_LDS : 1];
+    if (LDS) {
+        for (int i = threadIdx.x; i < k; i += blockDim.x) {
+            const uint32_t o = order[i];
+            si[i] = o;
+            sv[i] = cen[o];
+        }
+        __syncthreads();
+    }
+    auto val = [&](uint32_t pos) -> float { return LDS ? sv[pos] : cen[order[pos]]; };
+    auto idx = [&](uint32_t pos) -> uint32_t { return LDS ? si[pos] : order[pos]; };
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double p = pts[i];
+        double mind = __builtin_inf();
+        uint32_t mini = 0xffffffffu;
+        Seg stack[24];
+        int sp = 0;
+        Seg cur{0, (uint32_t)k};
+        bool descend = true;
+        while (true) {
+            if (descend) {
+                // go down the `next` chain, remembering each frame
+                while (cur.hi > cur.lo) {
+                    stack[sp++] = cur;
+                    uint32_t node;
+                    Seg l, r;
+                    seg_node(cur, node, l, r);
+                    const double distance = p - (double)val(node);
+                    cur = (distance > 0) ? r : l;
+                }
+            }
+            if (sp == 0) break;
+            const Seg f = stack[--sp];
+            uint32_t node;
+            Seg l, r;
+            seg_node(f, node, l, r);
+            const double cv = val(node);
+            const double distance = p - cv;
+            const double v = cv - p;
+            const double thisd = 0.0 + v * v;
+            if (thisd < mind) {
+                mind = thisd;
+                mini = idx(node);
+            }
+            const Seg other = (distance > 0) ? l : r;
+            if (distance * distance < mind && other.hi > other.lo) {
+                cur = other;
+                descend = true;
+            } else {
+                descend = false;
+            }
+        }
+        labels[i] = mini;
+    }
+}
+
+// pairs for the member sort: key = label, val = value bits (ascending point order kept)
+__global__ __launch_bounds__(256) void k_pairs1d(const float *pts, const uint32_t *labels, uint64_t n,
+                                                 uint32_t *keys, uint32_t *vals) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        keys[i] = labels[i];
+        vals[i] = __builtin_bit_cast(uint32_t, pts[i]);
+    }
+}
+
+// exponent of the unit in the last place of an f32 (value is a multiple of 2^ulpexp)
+__device__ inline int ulp_exp(float x) {
+    const uint32_t e = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;
+    return e == 0 ? -149 : (int)e - 150;
+}
+
+__global__ __launch_bounds__(256) void k_sum1d(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
+                                               int k, float *__restrict__ cen) {
+    const int cl = blockIdx.x;
+    const uint32_t s0 = start[cl], s1 = start[cl + 1];
+    if (s1 == s0) return;  // empty: re-seeded separately
+    __shared__ double red_s[4], red_a[4];
+    __shared__ int red_e[4];
+    __shared__ double seq_sum;
+    double sum = 0, sabs = 0;
+    int emin = 1 << 20;
+    for (uint32_t j = s0 + threadIdx.x; j < s1; j += blockDim.x) {
+        const float x = __builtin_bit_cast(float, vals[j]);
+        sum += (double)x;
+        sabs += (double)__builtin_fabsf(x);
+        if (x != 0.0f) emin = min(emin, ulp_exp(x));
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        sabs += __shfl_xor(sabs, o, 64);
+        emin = min(emin, __shfl_xor(emin, o, 64));
+    }
+    if (lane == 0) {
+        red_s[w] = sum;
+        red_a[w] = sabs;
+        red_e[w] = emin;
+    }
+    __syncthreads();
+    sum = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);
+    sabs = (red_a[0] + red_a[1]) + (red_a[2] + red_a[3]);
+    emin = min(min(red_e[0], red_e[1]), min(red_e[2], red_e[3]));
+    const uint32_t count = s1 - s0;
+    // certificate: sum|x| (bounded above with slack for its own rounding) < 2^(emin+53)
+    const bool exact = (sabs == 0.0) || (sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin + 53));
+    if (!exact) {
+        // sequential sum in ascending point order (calcAverage)
+        if (w == 0) {
+            double s = 0;
+            for (uint32_t j0 = s0; j0 < s1; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const double v = (j < s1) ? (double)__builtin_bit_cast(float, vals[j]) : 0.0;
+                const uint32_t m = (s1 - j0 < 64u) ? (s1 - j0) : 64u;
+                for (uint32_t t = 0; t < m; ++t) s += __shfl(v, (int)t, 64);
+            }
+            if (lane == 0) seq_sum = s;
+        }
+        __syncthreads();
+        sum = seq_sum;
+    }
+    if (threadIdx.x == 0) cen[cl] = (float)(sum / (double)count);
+}
+
+}  // namespace
+
+void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
+                   const double *ddraws, uint64_t ndraws, State *dstate, float *cen, uint32_t *labels) {
+    auto *ckeys = wsT<uint32_t>(c, "k1.ckeys", (size_t)k);
+    auto *corder = wsT<uint32_t>(c, "k1.corder", (size_t)k);
+    auto *keys = wsT<uint32_t>(c, "k1.keys", n);
+    auto *vals = wsT<uint32_t>(c, "k1.vals", n);
+    auto *start = wsT<uint32_t>(c, "k1.start", (size_t)k + 1);
+    int kbits = 1;
+    while ((1ull << kbits) < (uint64_t)k) ++kbits;
+    for (int it = 0; it < iters; ++it) {
+        // KdTree build == stable sort of the centroid values (kd-tree.ts:73-99)
+        hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
+        ST_LAUNCH_CHECK();
+        radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
+        const unsigned g = grid_for(n, 256, 256 * 16);
+        if (k <= KD1_LDS)
+            hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+        else
+            hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+        ST_LAUNCH_CHECK();
+        mark(c, "k1.assign");
+        // update
+        hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,
+                           vals);
+        ST_LAUNCH_CHECK();
+        radix_sort_u32(c, keys, vals, n, 0, kbits, "k1.msort");
+        bounds_from_sorted(c, keys, n, k, start);
+        hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen);
+        ST_LAUNCH_CHECK();
+        reseed_empty(c, dcols, 1, n, k, start, ddraws, ndraws, dstate, cen);
+        mark(c, "k1.update");
+    }
+}
+
+}  // namespace st

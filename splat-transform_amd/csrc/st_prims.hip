@@ -1,0 +1,243 @@
+// st_prims.hip -- device-wide primitives: exclusive scan and stable LSD radix sort.
+//
+// Radix sort: 8-bit digits, reduce-then-scan per pass.  A block owns a tile of
+// 4096 keys; each of its four waves owns a contiguous quarter, visited in 16
+// rows of 64 lanes, so (wave, row, lane) order == input order.  Within a row a
+// key's stable rank among equal digits comes from 8 ballots (wave64 match),
+// per-wave digit counters live in LDS, and a per-digit prefix over the waves
+// plus the global (digit, block) offset gives the output slot.  Stability is
+// what ordering.ts:82-83 (V8's stable TypedArray.sort) and the in-cluster
+// member order of k-means.ts:123-135 require.
+#include "st_internal.h"
+
+namespace st {
+
+namespace {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+__device__ inline uint32_t wave_inclusive_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// exclusive scan of the 256 per-thread values of a block; returns block total via *total
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t wsum[SCAN_THREADS / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_THREADS / 64; ++i) {
+        if (i < w) before += wsum[i];
+        tot += wsum[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return before + inc - v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t *__restrict__ in, uint64_t n,
+                                                              uint32_t *__restrict__ partial) {
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i)
+        if (base + i < n) s += in[base + i];
+    uint32_t tot;
+    block_exclusive_scan(s, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(const uint32_t *in, uint64_t n, uint32_t *out,
+                                                            const uint32_t *__restrict__ partial_ex,
+                                                            uint32_t *d_total, int write_total) {
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        v[i] = (base + i < n) ? in[base + i] : 0u;
+        s += v[i];
+    }
+    uint32_t tot;
+    uint32_t ex = block_exclusive_scan(s, &tot) + (partial_ex ? partial_ex[blockIdx.x] : 0u);
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        if (base + i < n) out[base + i] = ex;
+        ex += v[i];
+    }
+    if (write_total && d_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_THREADS - 1) *d_total = ex;
+}
+
+__global__ void k_iota(uint32_t *out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)i;
+}
+
+// ---------------------------------------------------------------------------
+constexpr int RS_THREADS = 256;
+constexpr int RS_ROWS = 16;
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_TILE = RS_THREADS * RS_ROWS;  // 4096
+constexpr int RS_WAVE_SPAN = 64 * RS_ROWS;     // 1024
+
+template <typename K>
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K *__restrict__ keys, uint64_t n, int shift, int bits,
+                                                        uint32_t *__restrict__ hist, uint32_t nblocks) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll 4
+    for (int r = 0; r < RS_ROWS; ++r) {
+        const uint64_t e = base + (uint64_t)r * RS_THREADS + threadIdx.x;
+        if (e < n) atomicAdd(&h[(uint32_t)(keys[e] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+template <typename K>
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                           uint64_t n, int shift, int bits,
+                                                           const uint32_t *__restrict__ offs, uint32_t nblocks,
+                                                           K *__restrict__ okeys, uint32_t *__restrict__ ovals) {
+    __shared__ uint32_t wcount[RS_WAVES][256];
+    __shared__ uint32_t wbase[RS_WAVES][256];
+    __shared__ uint32_t goff[256];
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wcount[0][0])[i] = 0;
+    goff[threadIdx.x] = offs[(uint64_t)threadIdx.x * nblocks + blockIdx.x];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t mask = (1u << bits) - 1u;
+    const uint64_t wbase_e = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WAVE_SPAN;
+    K k[RS_ROWS];
+    uint32_t v[RS_ROWS];
+    uint32_t off[RS_ROWS];
+    uint32_t dg[RS_ROWS];
+#pragma unroll
+    for (int r = 0; r < RS_ROWS; ++r) {
+        const uint64_t e = wbase_e + (uint64_t)r * 64 + lane;
+        const bool valid = e < n;
+        k[r] = valid ? keys[e] : (K)0;
+        v[r] = valid ? vals[e] : 0u;
+        const uint32_t d = (uint32_t)(k[r] >> shift) & mask;
+        dg[r] = d;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t before = valid ? wcount[w][d] : 0u;
+        off[r] = before + rank;
+        const bool leader = valid && ((peers & lt) == 0);
+        if (leader) wcount[w][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < RS_WAVES; ++i) {
+            wbase[i][d] = s;
+            s += wcount[i][d];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ROWS; ++r) {
+        const uint64_t e = wbase_e + (uint64_t)r * 64 + lane;
+        if (e < n) {
+            const uint32_t pos = goff[dg[r]] + wbase[w][dg[r]] + off[r];
+            okeys[pos] = k[r];
+            ovals[pos] = v[r];
+        }
+    }
+}
+
+template <typename K>
+void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
+                     const std::string &tag) {
+    if (n <= 1 || end_bit <= begin_bit) return;
+    ST_REQUIRE(n < (1ull << 32), ST_ERR_ARG, "radix sort: n must be < 2^32");
+    const uint32_t nblocks = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    K *k2 = wsT<K>(c, tag + ".k2", n);
+    uint32_t *v2 = wsT<uint32_t>(c, tag + ".v2", n);
+    uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", (uint64_t)256 * nblocks);
+    K *ka = keys, *kb = k2;
+    uint32_t *va = vals, *vb = v2;
+    int passes = 0;
+    for (int shift = begin_bit; shift < end_bit; shift += 8) {
+        const int bits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
+        hipLaunchKernelGGL(k_rs_hist<K>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, n, shift, bits, hist,
+                           nblocks);
+        ST_LAUNCH_CHECK();
+        scan_u32(c, hist, hist, (uint64_t)256 * nblocks, nullptr);
+        hipLaunchKernelGGL(k_rs_scatter<K>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, va, n, shift, bits,
+                           hist, nblocks, kb, vb);
+        ST_LAUNCH_CHECK();
+        std::swap(ka, kb);
+        std::swap(va, vb);
+        ++passes;
+    }
+    if (passes & 1) {
+        ST_HIP(hipMemcpyAsync(keys, ka, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
+        ST_HIP(hipMemcpyAsync(vals, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    }
+}
+
+}  // namespace
+
+void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *d_total) {
+    if (n == 0) {
+        if (d_total) ST_HIP(hipMemsetAsync(d_total, 0, sizeof(uint32_t), c->stream));
+        return;
+    }
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (nb == 1) {
+        hipLaunchKernelGGL(k_scan_down, dim3(1), dim3(SCAN_THREADS), 0, c->stream, in, n, out, nullptr, d_total, 1);
+        ST_LAUNCH_CHECK();
+        return;
+    }
+    // per-level partial buffers keyed by size class so nested scans do not collide
+    std::string tag = "scan.p" + std::to_string(nb);
+    uint32_t *partial = wsT<uint32_t>(c, tag, nb + 1);
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, c->stream, in, n, partial);
+    ST_LAUNCH_CHECK();
+    scan_u32(c, partial, partial, nb, partial + nb);
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, c->stream, in, n, out, partial,
+                       nullptr, 0);
+    ST_LAUNCH_CHECK();
+    if (d_total) ST_HIP(hipMemcpyAsync(d_total, partial + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+}
+
+void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
+    radix_sort_impl<uint32_t>(c, keys, vals, n, b0, b1, tag);
+}
+
+void radix_sort_u64(st_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
+    radix_sort_impl<uint64_t>(c, keys, vals, n, b0, b1, tag);
+}
+
+void iota_u32(st_ctx *c, uint32_t *out, uint64_t n) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c->stream, out, n);
+    ST_LAUNCH_CHECK();
+}
+
+}  // namespace st

@@ -1,0 +1,303 @@
+// st_runtime.hip -- context, workspace, error plumbing, table helpers.
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+#include "st_internal.h"
+
+namespace st {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+
+void *Workspace::get(const std::string &slot, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    Buf &b = bufs[slot];
+    if (b.bytes < bytes) {
+        if (b.ptr) ST_HIP(hipFree(b.ptr));
+        b.ptr = nullptr;
+        b.bytes = 0;
+        size_t want = bytes + bytes / 8;  // headroom for slowly growing sizes
+        hipError_t e = hipMalloc(&b.ptr, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(ST_ERR_NOMEM, "workspace '" + slot + "': hipMalloc(" + std::to_string(want) + ") failed");
+        }
+        b.bytes = want;
+    }
+    return b.ptr;
+}
+
+void Workspace::release() {
+    for (auto &kv : bufs)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    bufs.clear();
+}
+
+void *pinned(st_ctx *c, size_t bytes) {
+    if (c->pinned_bytes < bytes) {
+        if (c->pinned) ST_HIP(hipHostFree(c->pinned));
+        c->pinned = nullptr;
+        ST_HIP(hipHostMalloc(&c->pinned, bytes, hipHostMallocDefault));
+        c->pinned_bytes = bytes;
+    }
+    return c->pinned;
+}
+
+void use_device(st_ctx *c) { ST_HIP(hipSetDevice(c->device)); }
+
+void mark(st_ctx *c, const char *name) {
+    if (!c->timing) return;
+    StageTimer t;
+    t.name = name;
+    ST_HIP(hipEventCreate(&t.ev));
+    ST_HIP(hipEventRecord(t.ev, c->stream));
+    c->marks.push_back(t);
+}
+
+static void begin_timing(st_ctx *c) {
+    c->timing = getenv("ST_TIMING") != nullptr;
+    for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
+    c->marks.clear();
+    mark(c, "begin");
+}
+
+static void end_timing(st_ctx *c) {
+    if (!c->timing) return;
+    mark(c, "end");
+    ST_HIP(hipEventSynchronize(c->marks.back().ev));
+    std::ostringstream os;
+    os << "{";
+    for (size_t i = 1; i < c->marks.size(); ++i) {
+        float ms = 0;
+        ST_HIP(hipEventElapsedTime(&ms, c->marks[i - 1].ev, c->marks[i].ev));
+        os << (i > 1 ? ", " : "") << "\"" << c->marks[i].name << "\": " << ms;
+    }
+    os << "}";
+    c->last_timings = os.str();
+    if (getenv("ST_TIMING_PRINT")) fprintf(stderr, "[st timing] %s\n", c->last_timings.c_str());
+}
+
+int find_col(const st_table *t, const char *name) {
+    for (int i = 0; i < t->ncol; ++i)
+        if (t->names[i] && strcmp(t->names[i], name) == 0) return i;
+    return -1;
+}
+
+float *col_or_null(const st_table *t, const char *name) {
+    int i = find_col(t, name);
+    return i < 0 ? nullptr : t->cols[i];
+}
+
+int sh_coeffs_of(const st_table *t) {
+    // { '9': 1, '24': 2, '-1': 3 }[index of first missing f_rest_i] ?? 0
+    int first_missing = -1;
+    char nm[32];
+    for (int i = 0; i < 45; ++i) {
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        if (find_col(t, nm) < 0) {
+            first_missing = i;
+            break;
+        }
+    }
+    switch (first_missing) {
+        case 9: return 3;
+        case 24: return 8;
+        case -1: return 15;
+        default: return 0;
+    }
+}
+
+}  // namespace st
+
+// ---------------------------------------------------------------------------
+// extern "C" boundary
+using namespace st;
+
+template <typename F>
+static int guarded(F &&f) {
+    try {
+        f();
+        return ST_OK;
+    } catch (const st::Error &e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_last_error("host allocation failed");
+        return ST_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return ST_ERR_INTERNAL;
+    }
+}
+
+#define ST_ARG(cond, msg) ST_REQUIRE(cond, ST_ERR_ARG, msg)
+
+static void check_table(const st_table *t) {
+    ST_ARG(t != nullptr, "table is NULL");
+    ST_ARG(t->ncol >= 0 && (t->ncol == 0 || (t->names && t->cols)), "table: bad column arrays");
+    for (int i = 0; i < t->ncol; ++i) ST_ARG(t->cols[i] != nullptr || t->n == 0, "table: NULL column pointer");
+}
+
+extern "C" {
+
+int st_abi_version(void) { return ST_ABI_VERSION; }
+
+const char *st_last_error(void) { return g_last_error.c_str(); }
+
+int st_device_count(int32_t *count) {
+    return guarded([&] {
+        ST_ARG(count, "count is NULL");
+        int n = 0;
+        ST_HIP(hipGetDeviceCount(&n));
+        *count = n;
+    });
+}
+
+int st_ctx_create(int32_t device, st_ctx **out) {
+    return guarded([&] {
+        ST_ARG(out, "out is NULL");
+        int n = 0;
+        ST_HIP(hipGetDeviceCount(&n));
+        ST_REQUIRE(n > 0, ST_ERR_HIP, "no HIP device visible (the MI355X product path has no CPU fallback)");
+        ST_ARG(device >= 0 && device < n, "device index out of range");
+        hipDeviceProp_t prop;
+        ST_HIP(hipGetDeviceProperties(&prop, device));
+        ST_REQUIRE(strncmp(prop.gcnArchName, "gfx950", 6) == 0, ST_ERR_UNSUPPORTED,
+                   std::string("libsplat_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
+        auto *c = new st_ctx();
+        c->device = device;
+        ST_HIP(hipSetDevice(device));
+        ST_HIP(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        c->stream = c->own_stream;
+        *out = c;
+    });
+}
+
+void st_ctx_destroy(st_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->ws.release();
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int st_ctx_set_stream(st_ctx *c, void *s) {
+    return guarded([&] {
+        ST_ARG(c, "ctx is NULL");
+        c->stream = s ? (hipStream_t)s : c->own_stream;
+    });
+}
+
+int st_ctx_synchronize(st_ctx *c) {
+    return guarded([&] {
+        ST_ARG(c, "ctx is NULL");
+        use_device(c);
+        ST_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+const char *st_ctx_last_timings(st_ctx *c) { return c ? c->last_timings.c_str() : "{}"; }
+
+// ---- device entry points --------------------------------------------------
+int st_dev_transform(st_ctx *c, const st_table *t, const st_transform_params *p) {
+    return guarded([&] {
+        ST_ARG(c && p, "NULL argument");
+        check_table(t);
+        use_device(c);
+        transform_dev(c, t, p);
+    });
+}
+
+int st_dev_filter_finite(st_ctx *c, const st_table *t, uint32_t *out_idx, uint64_t *out_n) {
+    return guarded([&] {
+        ST_ARG(c && out_n, "NULL argument");
+        check_table(t);
+        use_device(c);
+        *out_n = filter_finite_dev(c, t, out_idx);
+    });
+}
+
+int st_dev_permute_rows(st_ctx *c, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst) {
+    return guarded([&] {
+        ST_ARG(c && (idx || m == 0), "NULL argument");
+        check_table(src);
+        check_table(dst);
+        ST_ARG(dst->ncol == src->ncol && dst->n == m, "permute_rows: dst must have src's columns and m rows");
+        use_device(c);
+        permute_rows_dev(c, src, idx, m, dst);
+    });
+}
+
+int st_dev_concat_rows(st_ctx *c, const st_table *const *srcs, int32_t nsrc, const st_table *dst) {
+    return guarded([&] {
+        ST_ARG(c && srcs && nsrc > 0, "NULL argument");
+        for (int i = 0; i < nsrc; ++i) check_table(srcs[i]);
+        check_table(dst);
+        use_device(c);
+        concat_rows_dev(c, srcs, nsrc, dst);
+    });
+}
+
+int st_dev_morton_order(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *idx, uint64_t n) {
+    return guarded([&] {
+        ST_ARG(c && ((x && y && z && idx) || n == 0), "NULL argument");
+        use_device(c);
+        morton_order_dev(c, x, y, z, idx, n);
+    });
+}
+
+int st_dev_pack_compressed(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
+                           uint8_t *sh) {
+    return guarded([&] {
+        ST_ARG(c && ((order && chunk && vertex) || t->n == 0), "NULL argument");
+        check_table(t);
+        use_device(c);
+        pack_compressed_dev(c, t, order, chunk, vertex, sh);
+    });
+}
+
+int st_dev_kmeans(st_ctx *c, const float *const *cols, int32_t d, uint64_t n, int32_t k, int32_t iters,
+                  const double *draws, uint64_t ndraws, uint64_t *used, float *centroids, uint32_t *labels) {
+    return guarded([&] {
+        ST_ARG(c && cols && d > 0 && k > 0 && iters >= 0 && centroids && labels, "bad argument");
+        ST_ARG(draws || ndraws == 0, "draws is NULL");
+        use_device(c);
+        begin_timing(c);
+        uint64_t u = kmeans_dev(c, cols, d, n, k, iters, draws, ndraws, centroids, labels);
+        end_timing(c);
+        if (used) *used = u;
+    });
+}
+
+int st_dev_cluster1d(st_ctx *c, const float *const *cols, int32_t ncols, uint64_t n, int32_t iters,
+                     const double *draws, uint64_t ndraws, uint64_t *used, float *centroids, uint8_t *labels) {
+    return guarded([&] {
+        ST_ARG(c && cols && ncols > 0 && centroids && labels, "bad argument");
+        use_device(c);
+        begin_timing(c);
+        uint64_t u = cluster1d_dev(c, cols, ncols, n, iters, draws, ndraws, centroids, labels);
+        end_timing(c);
+        if (used) *used = u;
+    });
+}
+
+int st_dev_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+               st_sog_meta *meta, const st_sog_textures *out) {
+    return guarded([&] {
+        ST_ARG(c && meta && out, "NULL argument");
+        check_table(t);
+        use_device(c);
+        begin_timing(c);
+        uint64_t u = sog_dev(c, t, iters, draws, ndraws, meta, out);
+        end_timing(c);
+        if (used) *used = u;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,330 @@
+// st_sog.hip -- writeSog texture + meta generation (write-sog.ts:110-370) and
+// cluster1d (write-sog.ts:56-99), device-resident end to end.
+//
+// Order of work and of Math.random consumption follows writeSog exactly:
+// Morton order -> means_l/u -> quats -> cluster1d(scales) -> cluster1d(f_dc)
+// + opacity -> kmeans(SH, paletteSize) -> cluster1d(centroids) -> shN
+// textures.  Texels beyond n stay zero (the reference's zero-initialised
+// Uint8Arrays).  WebP encoding / ZIP packaging stay on the host (out of the
+// device pipeline).
+#include <cmath>
+
+#include "st_jsmath.h"
+#include "st_kmeans.h"
+
+namespace st {
+namespace {
+
+using namespace km;
+
+__global__ __launch_bounds__(256) void k_concat1d(const float *const *cols, int ncols, uint64_t n, float *out) {
+    const uint64_t total = n * (uint64_t)ncols;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride)
+        out[i] = cols[i / n][i % n];
+}
+
+__global__ void k_sort_codebook(const float *cen, uint32_t *keys, uint32_t *vals) {
+    const int i = threadIdx.x;
+    keys[i] = sortkey_(cen[i]);
+    vals[i] = (uint32_t)i;
+}
+
+__global__ void k_finish_codebook(const float *cen, const uint32_t *order, float *sorted, uint32_t *inv) {
+    const int i = threadIdx.x;
+    sorted[i] = cen[order[i]];
+    inv[order[i]] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_remap_labels(const uint32_t *lab, const uint32_t *inv, uint64_t total,
+                                                      uint8_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride)
+        out[i] = (uint8_t)inv[lab[i]];
+}
+
+// NaN-ignoring min/max (write-sog.ts:15-31: `if (value < min)` skips NaN)
+__global__ __launch_bounds__(256) void k_minmax3(const float *x, const float *y, const float *z, uint64_t n,
+                                                 uint32_t *mm) {
+    const float *c[3] = {x, y, z};
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = c[a][i];
+            if (v == v) {
+                const uint32_t k = fkey_(v);
+                lo[a] = k < lo[a] ? k : lo[a];
+                hi[a] = k > hi[a] ? k : hi[a];
+            }
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t t0 = __shfl_xor(lo[a], o, 64), t1 = __shfl_xor(hi[a], o, 64);
+            lo[a] = t0 < lo[a] ? t0 : lo[a];
+            hi[a] = t1 > hi[a] ? t1 : hi[a];
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&mm[a], lo[a]);
+            atomicMax(&mm[3 + a], hi[a]);
+        }
+    }
+}
+
+struct MeansArgs {
+    const float *c[3];
+    double mn[3], mx[3];
+};
+
+__global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint32_t *__restrict__ idx, uint64_t n,
+                                                  uint32_t *__restrict__ ml, uint32_t *__restrict__ mu) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t r = idx[i];
+        uint32_t lw = 0xff000000u, up = 0xff000000u;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double v = 65535 * (js::log_transform((double)a.c[k][r]) - a.mn[k]) / (a.mx[k] - a.mn[k]);
+            const int32_t iv = js::to_int32(v);
+            lw |= (uint32_t)(iv & 0xff) << (8 * k);
+            up |= (uint32_t)((iv >> 8) & 0xff) << (8 * k);
+        }
+        ml[i] = lw;
+        mu[i] = up;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_quats_tex(const float *__restrict__ q0, const float *__restrict__ q1,
+                                                  const float *__restrict__ q2, const float *__restrict__ q3,
+                                                  const uint32_t *__restrict__ idx, uint64_t n,
+                                                  uint32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t r = idx[i];
+        double q[4] = {q0[r], q1[r], q2[r], q3[r]};
+        const double l = __builtin_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = q[j] / l;
+        int mc = 0;
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+            if (__builtin_fabs(q[j]) > __builtin_fabs(q[mc])) mc = j;
+        if (q[mc] < 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] *= -1;
+        }
+        const double sqrt2 = __builtin_sqrt(2.0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] *= sqrt2;
+        uint32_t px = (uint32_t)(252 + mc) << 24;
+        int k = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j == mc) continue;
+            px |= (uint32_t)js::to_uint8(255 * (q[j] * 0.5 + 0.5)) << (8 * k);
+            ++k;
+        }
+        out[i] = px;
+    }
+}
+
+// writeTableData (write-sog.ts:142-157): rgb from u8 label columns, alpha = 4th column or 255
+__global__ __launch_bounds__(256) void k_table_tex(const uint8_t *__restrict__ l0, const uint8_t *__restrict__ l1,
+                                                  const uint8_t *__restrict__ l2, const float *__restrict__ opacity,
+                                                  const uint32_t *__restrict__ idx, uint64_t n,
+                                                  uint32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t r = idx[i];
+        uint32_t a = 255;
+        if (opacity) a = js::to_uint8(js::max_(0, js::min_(255, js::sigmoid(opacity[r]) * 255)));
+        out[i] = (uint32_t)l0[r] | ((uint32_t)l1[r] << 8) | ((uint32_t)l2[r] << 16) | (a << 24);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_shn_labels_tex(const uint32_t *__restrict__ labels,
+                                                       const uint32_t *__restrict__ idx, uint64_t n,
+                                                       uint32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t label = labels[idx[i]];
+        out[i] = (label & 0xffu) | (((label >> 8) & 0xffu) << 8) | 0xff000000u;
+    }
+}
+
+// shN_centroids (write-sog.ts:319-335): centroid i, coefficient j -> texel i*C + j
+__global__ __launch_bounds__(256) void k_shn_centroids_tex(const uint8_t *__restrict__ cl, int C, int pal,
+                                                          uint32_t *__restrict__ out) {
+    const uint64_t total = (uint64_t)pal * C;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const uint64_t i = t / C, j = t % C;
+        out[t] = (uint32_t)cl[j * pal + i] | ((uint32_t)cl[(C + j) * pal + i] << 8) |
+                 ((uint32_t)cl[(2 * C + j) * pal + i] << 16) | 0xff000000u;
+    }
+}
+
+int palette_of(uint64_t n) {
+    int lg = 0;
+    while ((2ull << lg) <= n) ++lg;  // floor(log2 n)
+    const int p = lg - 10;           // floor(log2(n / 1024))
+    if (p >= 6) return 64 * 1024;
+    if (p >= 0) return (1 << p) * 1024;
+    return 1024 >> (-p);
+}
+
+}  // namespace
+
+uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, int iters, const double *draws,
+                       uint64_t ndraws, float *centroids256, uint8_t *labels) {
+    const uint64_t total = n * (uint64_t)ncols;
+    ST_REQUIRE(total >= 256, ST_ERR_ARG,
+               "cluster1d: fewer than 256 values (the reference's kmeans returns a plain Array and .subarray throws)");
+    auto **dcols = wsT<const float *>(c, "c1.cols", (size_t)ncols);
+    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * ncols, hipMemcpyHostToDevice, c->stream));
+    auto *data = wsT<float>(c, "c1.data", total);
+    hipLaunchKernelGGL(k_concat1d, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, dcols, ncols, n, data);
+    ST_LAUNCH_CHECK();
+    auto *cen = wsT<float>(c, "c1.cen", 256);
+    auto *lab = wsT<uint32_t>(c, "c1.lab", total);
+    const float *one[1] = {data};
+    const uint64_t used = kmeans_dev(c, one, 1, total, 256, iters, draws, ndraws, cen, lab);
+    auto *keys = wsT<uint32_t>(c, "c1.keys", 256);
+    auto *order = wsT<uint32_t>(c, "c1.order", 256);
+    auto *inv = wsT<uint32_t>(c, "c1.inv", 256);
+    hipLaunchKernelGGL(k_sort_codebook, dim3(1), dim3(256), 0, c->stream, cen, keys, order);
+    radix_sort_u32(c, keys, order, 256, 0, 32, "c1.rs");
+    hipLaunchKernelGGL(k_finish_codebook, dim3(1), dim3(256), 0, c->stream, cen, order, centroids256, inv);
+    hipLaunchKernelGGL(k_remap_labels, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, lab, inv, total,
+                       labels);
+    ST_LAUNCH_CHECK();
+    return used;
+}
+
+uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
+                 const st_sog_textures *out) {
+    const uint64_t n = t->n;
+    ST_REQUIRE(n > 0, ST_ERR_ARG, "sog: empty table");
+    ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "sog: n must be < 2^31 per device");
+    static const char *members[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
+                                      "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    const float *m[14];
+    for (int i = 0; i < 14; ++i) {
+        m[i] = col_or_null(t, members[i]);
+        ST_REQUIRE(m[i], ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
+    }
+    const int C = sh_coeffs_of(t);
+    int32_t W, H, pal, cw, chh;
+    st_sog_geometry(n, C, &W, &H, &pal, &cw, &chh);
+    const uint64_t texels = (uint64_t)W * H;
+    *meta = st_sog_meta{};
+    meta->width = W;
+    meta->height = H;
+    for (uint8_t *p : {out->means_l, out->means_u, out->quats, out->scales, out->sh0})
+        ST_REQUIRE(p, ST_ERR_ARG, "sog: texture output is NULL");
+    for (uint8_t *p : {out->means_l, out->means_u, out->quats, out->scales, out->sh0})
+        ST_HIP(hipMemsetAsync(p, 0, texels * 4, c->stream));
+
+    // Morton order (write-sog.ts:42-49)
+    auto *idx = wsT<uint32_t>(c, "sog.idx", n);
+    iota_u32(c, idx, n);
+    morton_order_dev(c, m[0], m[1], m[2], idx, n);
+    mark(c, "sog.morton");
+    const unsigned g = grid_for(n, 256, 8192);
+
+    // means (write-sog.ts:161-187)
+    auto *mm = wsT<uint32_t>(c, "sog.mm", 6);
+    const uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0};
+    ST_HIP(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_minmax3, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, m[0], m[1], m[2], n, mm);
+    ST_LAUNCH_CHECK();
+    uint32_t hmm[6];
+    ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    MeansArgs ma{};
+    for (int a = 0; a < 3; ++a) {
+        ma.c[a] = m[a];
+        const double lo = hmm[a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[a]);
+        const double hi = hmm[3 + a] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[3 + a]);
+        ma.mn[a] = js::log_transform(lo);
+        ma.mx[a] = js::log_transform(hi);
+        meta->means_min[a] = ma.mn[a];
+        meta->means_max[a] = ma.mx[a];
+    }
+    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, idx, n, (uint32_t *)out->means_l,
+                       (uint32_t *)out->means_u);
+    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13], idx, n,
+                       (uint32_t *)out->quats);
+    ST_LAUNCH_CHECK();
+    mark(c, "sog.means_quats");
+
+    uint64_t cursor = 0;
+    auto *lab = wsT<uint8_t>(c, "sog.lab", n * 3);
+    auto *cb = wsT<float>(c, "sog.cb", 256);
+    // scales (write-sog.ts:245-251)
+    cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
+    ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
+                       (const float *)nullptr, idx, n, (uint32_t *)out->scales);
+    ST_LAUNCH_CHECK();
+    mark(c, "sog.scales");
+    // colour + opacity (write-sog.ts:253-268)
+    cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
+    ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9], idx, n,
+                       (uint32_t *)out->sh0);
+    ST_LAUNCH_CHECK();
+    mark(c, "sog.sh0");
+
+    meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
+    if (C > 0) {
+        ST_REQUIRE(out->shn_centroids && out->shn_labels, ST_ERR_ARG, "sog: shN texture outputs are NULL");
+        meta->palette_size = pal;
+        meta->shn_width = cw;
+        meta->shn_height = chh;
+        const int D = 3 * C;
+        std::vector<const float *> sh(D);
+        char nm[32];
+        for (int i = 0; i < D; ++i) {
+            snprintf(nm, sizeof nm, "f_rest_%d", i);
+            sh[i] = col_or_null(t, nm);
+        }
+        auto *cen = wsT<float>(c, "sog.shcen", (size_t)pal * D);
+        auto *labels = wsT<uint32_t>(c, "sog.shlab", n);
+        cursor += kmeans_dev(c, sh.data(), D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels);
+        mark(c, "sog.shkmeans");
+        std::vector<const float *> ccols(D);
+        for (int i = 0; i < D; ++i) ccols[i] = cen + (uint64_t)i * pal;
+        auto *cl = wsT<uint8_t>(c, "sog.cl", (size_t)pal * D);
+        cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cb, cl);
+        ST_HIP(hipMemcpyAsync(meta->shn_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemsetAsync(out->shn_centroids, 0, (size_t)cw * chh * 4, c->stream));
+        ST_HIP(hipMemsetAsync(out->shn_labels, 0, texels * 4, c->stream));
+        hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
+                           cl, C, pal, (uint32_t *)out->shn_centroids);
+        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, idx, n,
+                           (uint32_t *)out->shn_labels);
+        ST_LAUNCH_CHECK();
+        mark(c, "sog.shn");
+    }
+    ST_HIP(hipStreamSynchronize(c->stream));
+    return cursor;
+}
+
+}  // namespace st
+
+extern "C" int st_sog_geometry(uint64_t n, int32_t C, int32_t *w, int32_t *h, int32_t *pal, int32_t *cw,
+                               int32_t *ch) {
+    if (n == 0) return ST_ERR_ARG;
+    const int W = (int)(std::ceil(std::sqrt((double)n) / 4) * 4);
+    const int H = (int)(std::ceil((double)n / W / 4) * 4);
+    const int P = C > 0 ? st::palette_of(n) : 0;
+    if (w) *w = W;
+    if (h) *h = H;
+    if (pal) *pal = P;
+    if (cw) *cw = 64 * C;
+    if (ch) *ch = C > 0 ? (P + 63) / 64 : 0;
+    return ST_OK;
+}

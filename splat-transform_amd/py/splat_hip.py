@@ -1,0 +1,289 @@
+"""ctypes binding of libsplat_hip.so (the C-ABI in include/st_abi.h).
+
+Used by the tests, bench.py and __graft_entry__.  Host-array entry points take
+numpy arrays; ``dev_*`` entry points take torch CUDA (HIP) tensors and pass
+their device pointers, running on torch's current stream.  There is no CPU
+fallback: constructing a Context without a gfx950 device raises.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, 'lib', 'libsplat_hip.so')
+
+ST_OK = 0
+_lib = None
+
+
+class StError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f'st error {code}: {msg}')
+        self.code = code
+
+
+class Table(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_uint64), ('ncol', ctypes.c_int32),
+                ('names', ctypes.POINTER(ctypes.c_char_p)), ('cols', ctypes.POINTER(ctypes.c_void_p))]
+
+
+class TransformParams(ctypes.Structure):
+    _fields_ = [('m4', ctypes.c_float * 16), ('r', ctypes.c_double * 4), ('s', ctypes.c_double),
+                ('sh1', ctypes.c_double * 9), ('sh2', ctypes.c_double * 25), ('sh3', ctypes.c_double * 49)]
+
+
+class SogMeta(ctypes.Structure):
+    _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
+                ('means_min', ctypes.c_double * 3), ('means_max', ctypes.c_double * 3),
+                ('scales_codebook', ctypes.c_float * 256), ('sh0_codebook', ctypes.c_float * 256),
+                ('sh_bands', ctypes.c_int32), ('palette_size', ctypes.c_int32),
+                ('shn_codebook', ctypes.c_float * 256), ('shn_width', ctypes.c_int32), ('shn_height', ctypes.c_int32)]
+
+
+class SogTextures(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shn_centroids', 'shn_labels')]
+
+
+EXPORTS = [
+    'st_abi_version', 'st_last_error', 'st_device_count', 'st_ctx_create', 'st_ctx_destroy', 'st_ctx_set_stream',
+    'st_ctx_synchronize', 'st_ctx_last_timings', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
+    'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
+    'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
+    'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
+]
+
+
+def build(jobs=8):
+    subprocess.check_call(['make', '-s', '-C', PKG, f'-j{jobs}'])
+
+
+def lib():
+    """Load libsplat_hip.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'{LIB_PATH} missing: build it with `make -C {PKG}` (hipcc, gfx950)')
+        L = ctypes.CDLL(LIB_PATH)
+        for name in EXPORTS:
+            getattr(L, name)
+        L.st_last_error.restype = ctypes.c_char_p
+        L.st_ctx_last_timings.restype = ctypes.c_char_p
+        L.st_ctx_destroy.restype = None
+        for name in EXPORTS:
+            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy'):
+                getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != ST_OK:
+        raise StError(rc, lib().st_last_error().decode())
+
+
+def _vp(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _ptr(t):
+    """device pointer of a torch tensor or numpy host array"""
+    if t is None:
+        return None
+    if hasattr(t, 'data_ptr'):
+        return ctypes.c_void_p(t.data_ptr())
+    return ctypes.c_void_p(t.ctypes.data)
+
+
+def make_table(cols):
+    """st_table over a dict name -> float32 array (numpy host or torch device); keeps refs alive"""
+    names = list(cols.keys())
+    n = len(cols[names[0]]) if names else 0
+    c_names = (ctypes.c_char_p * len(names))(*[s.encode() for s in names])
+    c_cols = (ctypes.c_void_p * len(names))(*[_ptr(cols[k]).value for k in names])
+    t = Table(n, len(names), ctypes.cast(c_names, ctypes.POINTER(ctypes.c_char_p)),
+              ctypes.cast(c_cols, ctypes.POINTER(ctypes.c_void_p)))
+    t._keep = (c_names, c_cols, cols)
+    return t
+
+
+def quat_from_euler(ex, ey, ez):
+    q = (ctypes.c_double * 4)()
+    check(lib().st_quat_from_euler(ctypes.c_double(ex), ctypes.c_double(ey), ctypes.c_double(ez), q))
+    return np.array(q[:])
+
+
+def transform_params(t=(0.0, 0.0, 0.0), r=(0.0, 0.0, 0.0, 1.0), s=1.0):
+    p = TransformParams()
+    check(lib().st_transform_params_make((ctypes.c_double * 3)(*t), (ctypes.c_double * 4)(*r), ctypes.c_double(s),
+                                         ctypes.byref(p)))
+    return p
+
+
+def action_params(kind, value):
+    """process.ts:71-83: translate / rotate (Euler degrees) / scale"""
+    if kind == 'translate':
+        return transform_params(t=value)
+    if kind == 'rotate':
+        return transform_params(r=quat_from_euler(*value))
+    if kind == 'scale':
+        return transform_params(s=float(value))
+    raise ValueError(kind)
+
+
+def sog_geometry(n, sh_coeffs):
+    v = [ctypes.c_int32() for _ in range(5)]
+    check(lib().st_sog_geometry(ctypes.c_uint64(n), ctypes.c_int32(sh_coeffs), *[ctypes.byref(x) for x in v]))
+    return tuple(x.value for x in v)
+
+
+def device_count():
+    n = ctypes.c_int32(0)
+    check(lib().st_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    def __init__(self, device=0):
+        self.h = ctypes.c_void_p()
+        check(lib().st_ctx_create(ctypes.c_int32(device), ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().st_ctx_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle):
+        check(lib().st_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def synchronize(self):
+        check(lib().st_ctx_synchronize(self.h))
+
+    def timings(self):
+        return lib().st_ctx_last_timings(self.h).decode()
+
+    # ---- host-memory seams ----------------------------------------------------
+    def transform(self, cols, params):
+        t = make_table(cols)
+        check(lib().st_transform(self.h, ctypes.byref(t), ctypes.byref(params)))
+
+    def filter_finite(self, cols):
+        t = make_table(cols)
+        out = np.zeros(t.n, np.uint32)
+        m = ctypes.c_uint64(0)
+        check(lib().st_filter_finite(self.h, ctypes.byref(t), _vp(out), ctypes.byref(m)))
+        return out[:m.value]
+
+    def morton_order(self, x, y, z, indices=None):
+        n = len(x)
+        idx = np.arange(n, dtype=np.uint32) if indices is None else np.ascontiguousarray(indices, np.uint32).copy()
+        check(lib().st_morton_order(self.h, _vp(x), _vp(y), _vp(z), _vp(idx), ctypes.c_uint64(n)))
+        return idx
+
+    def pack_compressed(self, cols, order, nsh):
+        t = make_table(cols)
+        n = t.n
+        chunk = np.zeros(((n + 255) // 256) * 18, np.float32)
+        vertex = np.zeros(n * 4, np.uint32)
+        sh = np.zeros(max(n * nsh, 1), np.uint8)
+        check(lib().st_pack_compressed(self.h, ctypes.byref(t), _vp(np.ascontiguousarray(order, np.uint32)),
+                                       _vp(chunk), _vp(vertex), _vp(sh)))
+        return chunk, vertex, sh[:n * nsh]
+
+    def kmeans(self, col_list, k, iters, draws):
+        d, n = len(col_list), len(col_list[0])
+        kk = min(k, n)
+        cent = np.zeros(d * kk, np.float32)
+        labels = np.zeros(n, np.uint32)
+        used = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * d)(*[c.ctypes.data for c in col_list])
+        check(lib().st_kmeans(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(n), ctypes.c_int32(k),
+                              ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                              _vp(cent), _vp(labels)))
+        return cent.reshape(d, kk), labels, used.value
+
+    def cluster1d(self, col_list, iters, draws):
+        n = len(col_list[0])
+        cent = np.zeros(256, np.float32)
+        labels = np.zeros(n * len(col_list), np.uint8)
+        used = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * len(col_list))(*[c.ctypes.data for c in col_list])
+        check(lib().st_cluster1d(self.h, ptrs, ctypes.c_int32(len(col_list)), ctypes.c_uint64(n),
+                                 ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                                 _vp(cent), _vp(labels)))
+        return cent, labels.reshape(len(col_list), n), used.value
+
+    def sog(self, cols, iters, draws):
+        t = make_table(cols)
+        C = sum(1 for k in cols if k.startswith('f_rest_')) // 3
+        C = {9: 3, 24: 8, 45: 15}.get(3 * C, 0) if C else 0
+        W, H, pal, cw, ch = sog_geometry(t.n, C)
+        tex = {k: np.zeros(W * H * 4, np.uint8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0')}
+        if C:
+            tex['shN_labels'] = np.zeros(W * H * 4, np.uint8)
+            tex['shN_centroids'] = np.zeros(cw * ch * 4, np.uint8)
+        out = SogTextures(tex['means_l'].ctypes.data, tex['means_u'].ctypes.data, tex['quats'].ctypes.data,
+                          tex['scales'].ctypes.data, tex['sh0'].ctypes.data,
+                          tex['shN_centroids'].ctypes.data if C else None,
+                          tex['shN_labels'].ctypes.data if C else None)
+        meta = SogMeta()
+        used = ctypes.c_uint64(0)
+        check(lib().st_sog(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)),
+                           ctypes.byref(used), ctypes.byref(meta), ctypes.byref(out)))
+        res = {k: v.reshape(H, W, 4) for k, v in tex.items() if k != 'shN_centroids'}
+        if C:
+            res['shN_centroids'] = tex['shN_centroids'].reshape(ch, cw, 4)
+        return res, meta, used.value
+
+    # ---- device-memory seams (torch tensors) --------------------------------------
+    def dev_transform(self, cols, params):
+        t = make_table(cols)
+        check(lib().st_dev_transform(self.h, ctypes.byref(t), ctypes.byref(params)))
+
+    def dev_morton_order(self, x, y, z, idx):
+        check(lib().st_dev_morton_order(self.h, _ptr(x), _ptr(y), _ptr(z), _ptr(idx), ctypes.c_uint64(len(idx))))
+
+    def dev_pack_compressed(self, cols, order, chunk, vertex, sh):
+        t = make_table(cols)
+        check(lib().st_dev_pack_compressed(self.h, ctypes.byref(t), _ptr(order), _ptr(chunk), _ptr(vertex),
+                                           _ptr(sh)))
+
+    def dev_filter_finite(self, cols, out_idx):
+        t = make_table(cols)
+        m = ctypes.c_uint64(0)
+        check(lib().st_dev_filter_finite(self.h, ctypes.byref(t), _ptr(out_idx), ctypes.byref(m)))
+        return m.value
+
+    def dev_permute_rows(self, src, idx, m, dst):
+        ts, td = make_table(src), make_table(dst)
+        check(lib().st_dev_permute_rows(self.h, ctypes.byref(ts), _ptr(idx), ctypes.c_uint64(m), ctypes.byref(td)))
+
+    def dev_kmeans(self, col_list, k, iters, draws, centroids, labels):
+        d, n = len(col_list), len(col_list[0])
+        used = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_kmeans(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(n), ctypes.c_int32(k),
+                                  ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                                  _ptr(centroids), _ptr(labels)))
+        return used.value
+
+    def dev_sog(self, cols, iters, draws, tex):
+        """tex: dict of device uint8 tensors (see sog_geometry for sizes)"""
+        t = make_table(cols)
+        out = SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                            ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        meta = SogMeta()
+        used = ctypes.c_uint64(0)
+        check(lib().st_dev_sog(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws),
+                               ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                               ctypes.byref(out)))
+        return meta, used.value

@@ -1,0 +1,80 @@
+"""CPU-side checks of the product library: it loads, exports every symbol the
+C-ABI header declares, and its host-only constants (PlayCanvas math restated,
+RotateSH matrices, SOG geometry) match the reference's golden vectors.
+No compute call that needs a GPU is made here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import splat_hip as sh
+from golden_io import Golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, 'include', 'st_abi.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(st_[a-z0-9_]+)\s*\(', src)))
+
+
+@pytest.fixture(scope='module')
+def L():
+    if not os.path.exists(sh.LIB_PATH):
+        sh.build()
+    return sh.lib()
+
+
+def test_library_exports_every_declared_symbol(L):
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(sh.EXPORTS)
+    assert L.st_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object(L):
+    blob = open(sh.LIB_PATH, 'rb').read()
+    assert b'amdgcn-amd-amdhsa--gfx950' in blob
+
+
+def test_quat_and_transform_params_match_reference(L):
+    g = Golden('transform')
+    for li, acts in enumerate(g.meta['actions']):
+        for ai, act in enumerate(acts):
+            p = sh.action_params(act['kind'], act['value'])
+            q = np.array(p.r[:])
+            assert np.array_equal(q.view(np.uint64), g[f'p{li}_{ai}_quat'].view(np.uint64))
+            assert np.array_equal(np.array(p.m4[:], np.float32).view(np.uint32), g[f'p{li}_{ai}_mat4'].view(np.uint32))
+            rot = g[f'p{li}_{ai}_shrot']
+            assert np.array_equal(np.array(p.sh1[:]), rot[0:3, 0:3].ravel())
+            assert np.array_equal(np.array(p.sh2[:]), rot[3:8, 3:8].ravel())
+            assert np.array_equal(np.array(p.sh3[:]), rot[8:15, 8:15].ravel())
+
+
+def test_sog_geometry_matches_reference(L):
+    g = Golden('sog')
+    for case in g.meta['cases']:
+        n = case['n']
+        name = case['name']
+        C = {'sh0': 0, 'sh1': 3, 'sh2': 8, 'sh3': 15}[name]
+        W, H, pal, cw, ch = sh.sog_geometry(n, C)
+        assert g[f'{name}_means_l'].shape == (H, W, 4)
+        if C:
+            assert pal == case['meta']['shN']['count']
+            assert g[f'{name}_shN_centroids'].shape == (ch, cw, 4)
+    # paletteSize = min(64, 2^floor(log2(n/1024))) * 1024
+    for n, want in [(1024, 1024), (2047, 1024), (2048, 2048), (65535, 32768), (65536, 65536), (10**7, 65536),
+                    (700, 512), (1, 1)]:
+        assert sh.sog_geometry(n, 15)[2] == want, n
+
+
+def test_context_without_gpu_fails_loudly(L):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    with pytest.raises(sh.StError):
+        sh.Context(0)

@@ -1,0 +1,140 @@
+"""Parity of the HIP path (through the C-ABI) against the reference's golden
+vectors and the pinned CPU restatement.  Integer / byte / index outputs must
+be bit-exact; float outputs of the transform are compared bit-exactly too
+(NaN as NaN), which is stricter than the 1e-5 relative bound north_star states.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import splat_hip as sh
+from golden_io import Golden
+from test_oracle_golden import same_bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    return sh.Context(0)
+
+
+@pytest.mark.parametrize('band', [0, 1, 2, 3])
+def test_transform_golden(ctx, band):
+    g = Golden('transform')
+    for li, acts in enumerate(g.meta['actions']):
+        cols = g.table(f'b{band}_in_')
+        for act in acts:
+            ctx.transform(cols, sh.action_params(act['kind'], act['value']))
+        for k in cols:
+            key = f'b{band}_a{li}_{k}'
+            if key in g:
+                same_bits(cols[k], g[key])
+
+
+def test_transform_large_vs_oracle(ctx):
+    rng = np.random.default_rng(1003)
+    n = 200_000
+    names = ['x', 'y', 'z'] + [f'f_rest_{i}' for i in range(45)] + ['scale_0', 'scale_1', 'scale_2'] + \
+        [f'rot_{i}' for i in range(4)]
+    cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in names}
+    ref = {k: v.copy() for k, v in cols.items()}
+    op = oracle.transform_params(euler=(0, 45, 0))
+    oracle.transform(ref, op, 15)
+    ctx.transform(cols, sh.action_params('rotate', (0, 45, 0)))
+    for k in names:
+        same_bits(cols[k], ref[k])
+
+
+def test_morton_golden(ctx):
+    g = Golden('ordering')
+    for name in g.meta['cases']:
+        got = ctx.morton_order(g[f'{name}_x'], g[f'{name}_y'], g[f'{name}_z'])
+        same_bits(got, g[f'{name}_order'])
+
+
+@pytest.mark.parametrize('n,frac', [(300_000, 0.05), (1_000_000, 0.2)])
+def test_morton_large_vs_oracle(ctx, n, frac):
+    rng = np.random.default_rng(1000 + n)
+    x, y, z = (rng.normal(0, 10, n).astype(np.float32) for _ in range(3))
+    m = rng.random(n) < frac
+    for a in (x, y, z):
+        a[m] = (1 + rng.random(m.sum()) * 1e-3).astype(np.float32)
+    got = ctx.morton_order(x, y, z)
+    want = oracle.morton_order(x, y, z)
+    same_bits(got, want)
+
+
+def test_compressed_ply_golden(ctx):
+    g = Golden('compressed_ply')
+    for name in g.meta['cases']:
+        cols = g.table(f'{name}_in_')
+        nsh = sum(1 for c in cols if c.startswith('f_rest_'))
+        order = ctx.morton_order(cols['x'], cols['y'], cols['z'])
+        chunk, vertex, shb = ctx.pack_compressed(cols, order, nsh)
+        same_bits(chunk, g[f'{name}_chunk'])
+        same_bits(vertex, g[f'{name}_vertex'])
+        same_bits(shb, g[f'{name}_sh'])
+
+
+def test_filter_nan_golden(ctx):
+    g = Golden('filter_combine')
+    cols = g.table('in_')
+    keep = ctx.filter_finite(cols)
+    out = g.table('out_')
+    for k in cols:
+        same_bits(cols[k][keep], out[k])
+
+
+def test_kmeans_golden(ctx):
+    g = Golden('kmeans')
+    for case in g.meta['cases']:
+        name = case['name']
+        cols = [g[f'{name}_p{j}'] for j in range(case['d'])]
+        draws = oracle.mulberry32(case['seed'], case['draws'] + 16)
+        cent, labels, used = ctx.kmeans(cols, case['k'], case['iters'], draws)
+        assert used == case['draws'], name
+        for j in range(case['d']):
+            same_bits(cent[j], g[f'{name}_c{j}'])
+        same_bits(labels, g[f'{name}_labels'])
+
+
+def test_cluster1d_golden(ctx):
+    g = Golden('kmeans')
+    m = g.meta['cluster1d']
+    cols = [g[f'cluster1d_p{j}'] for j in range(3)]
+    cent, labels, used = ctx.cluster1d(cols, m['iters'], oracle.mulberry32(m['seed'], 1000))
+    assert used == m['draws']
+    same_bits(cent, g['cluster1d_centroids'])
+    for j in range(3):
+        same_bits(labels[j], g[f'cluster1d_l{j}'])
+
+
+def test_sog_golden(ctx):
+    g = Golden('sog')
+    for case in g.meta['cases']:
+        name = case['name']
+        cols = g.table(f'{name}_in_')
+        tex, meta, used = ctx.sog(cols, case['iters'], oracle.mulberry32(case['seed'], case['draws'] + 64))
+        assert used == case['draws'], name
+        for k, v in tex.items():
+            same_bits(v, g[f'{name}_{k}'])
+        ref = case['meta']
+        assert list(meta.means_min) == ref['means']['mins']
+        assert list(meta.means_max) == ref['means']['maxs']
+        same_bits(np.array(meta.scales_codebook, np.float32), np.array(ref['scales']['codebook'], np.float32))
+        same_bits(np.array(meta.sh0_codebook, np.float32), np.array(ref['sh0']['codebook'], np.float32))
+        if 'shN' in ref:
+            same_bits(np.array(meta.shn_codebook, np.float32), np.array(ref['shN']['codebook'], np.float32))
+
+
+@pytest.mark.parametrize('n,d,k,iters', [(20_000, 45, 1024, 2), (30_000, 9, 2048, 2), (60_000, 1, 256, 4)])
+def test_kmeans_vs_oracle(ctx, n, d, k, iters):
+    rng = np.random.default_rng(n + d)
+    cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
+    draws = oracle.mulberry32(n + k, 4 * k * (iters + 1) + 64)
+    cent, labels, used = ctx.kmeans(cols, k, iters, draws)
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, iters, draws)
+    assert rc == 0 and used == oused
+    same_bits(labels, olabels)
+    same_bits(cent, ocent)
