@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py -- Msplats/s PLY->SOG (SH-3, 10 k-means iters) on MI355X.
+
+One step = the whole SOG device pipeline of write-sog.ts:110-370 over one
+synthetic SH-3 splat table already resident in HBM: Morton order, means /
+quats textures, cluster1d(scales), cluster1d(f_dc) + opacity, the SH palette
+k-means (K = 65,536, 10 iterations), the codebook cluster1d and the shN
+textures.  WebP / ZIP encoding of the textures is host work outside the
+device pipeline and is not in the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S]
+
+N > 1 is launched by torch.distributed.run: one process per GPU, each rank
+holds its own shard of S splats (weak scaling) and runs the pipeline on it.
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
+(the MFMA assign sweep, measured with HIP events on its own stream) and the
+CPU-oracle baseline timed on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
+
+MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
+HBM_TBPS = 8.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--splats', type=int, default=10_000_000, help='splats per GPU')
+    ap.add_argument('--iters', type=int, default=10, help='k-means iterations (reference default 10)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-assign-sample', type=int, default=1000)
+    ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
+    return ap.parse_args()
+
+
+def synth_table(n, seed, device):
+    """SURVEY.md 8d distributions: 95% positions ~N(0,10^2), 5% in a 1e-3 cube
+    (forces equal-key Morton runs > 256); f_dc ~N(0,1); f_rest ~N(0,0.1^2);
+    opacity ~N(0,2^2); scale ~U(-7,-2); rot ~N(0,1)^4 (not normalised)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    f = dict(device=device, dtype=torch.float32)
+    cols = {}
+    cube = torch.rand(n, generator=g, **f) < 0.05
+    for a, off in zip('xyz', (1.0, -2.0, 3.0)):
+        v = torch.randn(n, generator=g, **f) * 10
+        c = off + torch.rand(n, generator=g, **f) * 1e-3
+        cols[a] = torch.where(cube, c, v).contiguous()
+    for i in range(3):
+        cols[f'f_dc_{i}'] = torch.randn(n, generator=g, **f)
+    for i in range(45):
+        cols[f'f_rest_{i}'] = torch.randn(n, generator=g, **f) * 0.1
+    cols['opacity'] = torch.randn(n, generator=g, **f) * 2
+    for i in range(3):
+        cols[f'scale_{i}'] = torch.rand(n, generator=g, **f) * 5 - 7
+    for i in range(4):
+        cols[f'rot_{i}'] = torch.randn(n, generator=g, **f)
+    return cols
+
+
+def cpu_baseline(args):
+    """Time the CPU restatement (oracle/, the reference algorithm in C, 1 thread)
+    on a bounded sample and extrapolate to the bench workload."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import numpy as np
+
+    import oracle
+    oracle.build()
+    rng = np.random.default_rng(1002)
+    K, D = 65536, 45
+    # (a) one clusterKdTreeCpu pass at K = 65,536 over a point sample; centroids are data rows
+    data = [rng.normal(0, 0.1, K + args.cpu_assign_sample).astype(np.float32) for _ in range(D)]
+    cen = np.stack([c[:K] for c in data])
+    pts = [c[K:] for c in data]
+    t0 = time.perf_counter()
+    rc, _ = oracle.kmeans_assign(pts, cen)
+    ta = (time.perf_counter() - t0) / args.cpu_assign_sample
+    # (b) everything else: the SH0 writeSog pipeline (Morton, means/quats, two cluster1d k-means of
+    # 10 iterations, textures) on a splat sample
+    n = args.cpu_rest_sample
+    names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'scale_0', 'scale_1', 'scale_2',
+             'rot_0', 'rot_1', 'rot_2', 'rot_3']
+    cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in names}
+    t0 = time.perf_counter()
+    oracle.sog(cols, 0, args.iters, oracle.mulberry32(3, 200_000))
+    tb = (time.perf_counter() - t0) / n
+    per_splat = args.iters * ta + tb
+    return {
+        'value': 1e-6 / per_splat,
+        'unit': 'Msplats/s',
+        'cores': 1,
+        'kind': 'port',
+        'sample': (f'oracle/ C restatement, 1 thread: KdTree assign at K=65536, D=45 timed on '
+                   f'{args.cpu_assign_sample} points ({ta * 1e3:.2f} ms/point/iter) x {args.iters} iters + SH0 '
+                   f'writeSog pipeline timed on {n} splats ({tb * 1e6:.2f} us/splat); extrapolated per splat'),
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import splat_hip as sh
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', init_method='env://')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    ctx = sh.Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    n = args.splats
+    cols = synth_table(n, 1002 + rank, dev)
+    W, H, pal, cw, ch = sh.sog_geometry(n, 15)
+    u8 = dict(device=dev, dtype=torch.uint8)
+    tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
+    tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
+    # the host's Math.random stream (any uniform [0,1) doubles; the reference uses Math.random)
+    draws = np.random.default_rng(42 + rank).random(2 * 65536 * (args.iters + 2))
+    torch.cuda.synchronize()
+
+    def step():
+        return ctx.dev_sog(cols, args.iters, draws, tex)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_profiling(True)
+    ctx.reset_kernel_stats()
+    os.environ.pop('ST_TIMING', None)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        meta, used = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
+    ctx.set_profiling(False)
+
+    # one more step with per-stage event marks (outside the timed region)
+    os.environ['ST_TIMING'] = '1'
+    step()
+    torch.cuda.synchronize()
+    stages = json.loads(ctx.timings())
+    os.environ.pop('ST_TIMING', None)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    total_splats = n * world * args.steps
+    value = total_splats / elapsed / 1e6
+    avg_sweep_s = (sweep_ms / max(sweep_launches, 1)) / 1e3
+    D = 45
+    flops_per_launch = 2.0 * n * pal * D  # nearest-centroid dot products, one assign pass
+    achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+    out = {
+        'metric': 'Msplats/sec PLY->SOG (SH-3, 10 k-means iters)',
+        'value': value,
+        'unit': 'Msplats/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64+f32 (bit-exact JS semantics); bf16x3 MFMA for the assign prefilter',
+        'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seed 1002+rank), resident in HBM',
+        'config': {'workload': f'writeSog SH3 {n} splats/GPU, {args.iters} k-means iters, paletteSize {pal}',
+                   'splats_per_gpu': n, 'sh_bands': 3, 'palette_size': pal, 'iterations': args.iters,
+                   'parallelism': f'dp{world}'},
+        'roofline': {
+            'kernel': 'k_sweep<KS=9> (v_mfma_f32_32x32x16_bf16 nearest-centroid assign)',
+            'bound': 'mfma',
+            'achieved': achieved,
+            'peak': MFMA_BF16_DENSE_TFLOPS,
+            'unit': 'TFLOP/s',
+            'frac': (achieved / MFMA_BF16_DENSE_TFLOPS) if achieved else None,
+            'traffic': None,
+            'algorithmic_flops_per_launch': flops_per_launch,
+            'avg_launch_ms': avg_sweep_s * 1e3,
+            'launches': sweep_launches,
+        },
+        'cpu_baseline': cpu,
+        'stages_ms': stages,
+        'draws_used_per_step': used,
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

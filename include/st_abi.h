@@ -110,6 +110,12 @@ int st_ctx_set_stream(st_ctx *ctx, void *hip_stream);
 int st_ctx_synchronize(st_ctx *ctx);
 /* Per-stage device timing (hipEvents) of the last st_*sog / st_*kmeans call, JSON text. */
 const char *st_ctx_last_timings(st_ctx *ctx);
+/* Kernel profiling: when enabled, the library brackets its named hot kernels
+ * ("kn.sweep", "mo.sort", ...) with hipEvents on the context stream; stats
+ * accumulate until st_ctx_reset_kernel_stats.  Query after a synchronize. */
+int st_ctx_set_profiling(st_ctx *ctx, int32_t enable);
+int st_ctx_reset_kernel_stats(st_ctx *ctx);
+int st_ctx_kernel_stats(st_ctx *ctx, const char *name, double *total_ms, uint64_t *launches);
 
 /* ---- host constants ------------------------------------------------------ */
 int st_quat_from_euler(double ex_deg, double ey_deg, double ez_deg, double q_xyzw[4]);

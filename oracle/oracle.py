@@ -145,6 +145,16 @@ def kmeans(col_list, k, iters, draws):
     return rc, cent.reshape(d, kk), labels, used.value
 
 
+def kmeans_assign(col_list, centroids):
+    """centroids: (d, k) float32"""
+    d, n = len(col_list), len(col_list[0])
+    cen = np.ascontiguousarray(centroids, np.float32)
+    labels = np.zeros(n, np.uint32)
+    rc = lib().st_o_kmeans_assign(_ptrs(col_list), ctypes.c_int(d), ctypes.c_uint64(n), _p(cen),
+                                  ctypes.c_int(cen.shape[1]), _p(labels))
+    return rc, labels
+
+
 def cluster1d(col_list, iters, draws):
     n = len(col_list[0])
     cent = np.zeros(256, np.float32)

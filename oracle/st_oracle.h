@@ -58,6 +58,11 @@ int st_o_kmeans(const float *const *cols, int d, uint64_t n, int k, int iters,
                 const double *draws, uint64_t ndraws, uint64_t *used,
                 float *centroids, uint32_t *labels);
 
+/* One clusterKdTreeCpu pass (k-means.ts:103-121): KdTree over the given
+ * centroids (d columns of k) + findNearest for every point.  Used to time
+ * the CPU baseline of the assign step. */
+int st_o_kmeans_assign(const float *const *cols, int d, uint64_t n, const float *centroids, int k, uint32_t *labels);
+
 /* cluster1d (write-sog.ts:56-99): centroids[256] sorted ascending, labels u8 (ncols x n). */
 int st_o_cluster1d(const float *const *cols, int ncols, uint64_t n, int iters,
                    const double *draws, uint64_t ndraws, uint64_t *used,

@@ -195,6 +195,7 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     a.vertex = reinterpret_cast<uint4 *>(vertex);
     a.sh_out = sh;
     const uint64_t nchunks = (n + 255) / 256;
+    KTimer kt(c, "chunk.pack");
     hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();
 }

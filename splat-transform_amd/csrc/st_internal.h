@@ -66,6 +66,14 @@ struct st_ctx {
     std::vector<st::StageTimer> marks;
     bool timing = false;
     std::string last_timings = "{}";
+    // kernel profiling (st_ctx_set_profiling)
+    bool profiling = false;
+    struct KEv {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<KEv> kevents;
+    std::vector<hipEvent_t> event_pool;
 };
 
 namespace st {
@@ -78,6 +86,15 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
 void use_device(st_ctx *c);
 void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
+
+// brackets one kernel launch with hipEvents when profiling is enabled
+struct KTimer {
+    st_ctx *c;
+    hipEvent_t a = nullptr, b = nullptr;
+    const char *name;
+    KTimer(st_ctx *ctx, const char *nm);
+    ~KTimer();
+};
 
 inline unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u << 30) {
     uint64_t g = (work + per_block - 1) / per_block;

@@ -174,9 +174,6 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     mark(c, "km.check");
 
     // Math.random stream: uploaded once, consumed on device in reference order
-    const uint64_t nd = ndraws ? ndraws : 1;
-    auto *ddraws = wsT<double>(c, "km.draws", nd);
-    if (ndraws) ST_HIP(hipMemcpyAsync(ddraws, draws, ndraws * sizeof(double), hipMemcpyHostToDevice, c->stream));
     auto *dstate = static_cast<State *>(ws(c, "km.state", sizeof(State)));
     State hs{};
     uint64_t init_used = 0;
@@ -211,6 +208,11 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     }
     hs.cursor = init_used;
     ST_HIP(hipMemcpyAsync(dstate, &hs, sizeof(State), hipMemcpyHostToDevice, c->stream));
+    // re-seeds consume at most k draws per iteration: upload only that window of the stream
+    const uint64_t window = std::min<uint64_t>(ndraws, init_used + (uint64_t)k * (uint64_t)iters);
+    auto *ddraws = wsT<double>(c, "km.draws", window ? window : 1);
+    if (window) ST_HIP(hipMemcpyAsync(ddraws, draws, window * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    ndraws = window;
     mark(c, "km.init");
 
     if (d == 1)

@@ -199,6 +199,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         ST_LAUNCH_CHECK();
         radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
         const unsigned g = grid_for(n, 256, 256 * 16);
+        KTimer kt(c, "k1.assign");
         if (k <= KD1_LDS)
             hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
         else

@@ -422,6 +422,7 @@ struct Sweep {
                      State *st) {
         const uint32_t per_block = 4 * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
+        KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, PT, 0>), grid, dim3(256), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
                            cmax, (const uint32_t *)nullptr, labels, thr, amb, st, (uint32_t *)nullptr,
                            (uint32_t *)nullptr);
@@ -431,6 +432,7 @@ struct Sweep {
                         uint32_t ctiles, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
         const uint32_t per_block = 4 * PT;
         const dim3 grid((atiles + per_block - 1) / per_block);
+        KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, PT, 1>), grid, dim3(256), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
                            (uint32_t *)nullptr, thr_slot, (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand);
@@ -524,6 +526,7 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         mark(c, "kn.exact");
         // update
         member_sort(c, labels, n, k, sorted_labels, members, start);
+        KTimer kt(c, "kn.sumnd");
         hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen);
         ST_LAUNCH_CHECK();
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);

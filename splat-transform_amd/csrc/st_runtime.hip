@@ -57,6 +57,29 @@ void mark(st_ctx *c, const char *name) {
     c->marks.push_back(t);
 }
 
+static hipEvent_t pool_event(st_ctx *c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    ST_HIP(hipEventCreate(&e));
+    return e;
+}
+
+KTimer::KTimer(st_ctx *ctx, const char *nm) : c(ctx), name(nm) {
+    if (!c->profiling) return;
+    a = pool_event(c);
+    b = pool_event(c);
+    ST_HIP(hipEventRecord(a, c->stream));
+}
+
+KTimer::~KTimer() {
+    if (!a) return;
+    if (hipEventRecord(b, c->stream) == hipSuccess) c->kevents.push_back({name, a, b});
+}
+
 static void begin_timing(st_ctx *c) {
     c->timing = getenv("ST_TIMING") != nullptr;
     for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
@@ -183,6 +206,11 @@ void st_ctx_destroy(st_ctx *c) {
     c->ws.release();
     if (c->pinned) (void)hipHostFree(c->pinned);
     for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
+    for (auto &k : c->kevents) {
+        (void)hipEventDestroy(k.a);
+        (void)hipEventDestroy(k.b);
+    }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -203,6 +231,45 @@ int st_ctx_synchronize(st_ctx *c) {
 }
 
 const char *st_ctx_last_timings(st_ctx *c) { return c ? c->last_timings.c_str() : "{}"; }
+
+int st_ctx_set_profiling(st_ctx *c, int32_t enable) {
+    return guarded([&] {
+        ST_ARG(c, "ctx is NULL");
+        c->profiling = enable != 0;
+    });
+}
+
+int st_ctx_reset_kernel_stats(st_ctx *c) {
+    return guarded([&] {
+        ST_ARG(c, "ctx is NULL");
+        use_device(c);
+        ST_HIP(hipStreamSynchronize(c->stream));
+        for (auto &k : c->kevents) {
+            c->event_pool.push_back(k.a);
+            c->event_pool.push_back(k.b);
+        }
+        c->kevents.clear();
+    });
+}
+
+int st_ctx_kernel_stats(st_ctx *c, const char *name, double *total_ms, uint64_t *launches) {
+    return guarded([&] {
+        ST_ARG(c && name && total_ms && launches, "NULL argument");
+        use_device(c);
+        double t = 0;
+        uint64_t cnt = 0;
+        for (auto &k : c->kevents) {
+            if (k.name != name) continue;
+            ST_HIP(hipEventSynchronize(k.b));
+            float ms = 0;
+            ST_HIP(hipEventElapsedTime(&ms, k.a, k.b));
+            t += ms;
+            ++cnt;
+        }
+        *total_ms = t;
+        *launches = cnt;
+    });
+}
 
 // ---- device entry points --------------------------------------------------
 int st_dev_transform(st_ctx *c, const st_table *t, const st_transform_params *p) {

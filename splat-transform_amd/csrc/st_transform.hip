@@ -155,6 +155,7 @@ void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p) {
     for (int i = 0; i < 9; ++i) a.sh1[i] = p->sh1[i];
     for (int i = 0; i < 25; ++i) a.sh2[i] = p->sh2[i];
     for (int i = 0; i < 49; ++i) a.sh3[i] = p->sh3[i];
+    KTimer kt(c, "transform");
     switch (C) {
         case 0: launch_transform<0>(c, a, pos, rot, scl); break;
         case 3: launch_transform<3>(c, a, pos, rot, scl); break;

@@ -50,7 +50,8 @@ class SogTextures(ctypes.Structure):
 
 EXPORTS = [
     'st_abi_version', 'st_last_error', 'st_device_count', 'st_ctx_create', 'st_ctx_destroy', 'st_ctx_set_stream',
-    'st_ctx_synchronize', 'st_ctx_last_timings', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
+    'st_ctx_synchronize', 'st_ctx_last_timings', 'st_ctx_set_profiling', 'st_ctx_reset_kernel_stats',
+    'st_ctx_kernel_stats', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
@@ -170,6 +171,19 @@ class Context:
 
     def timings(self):
         return lib().st_ctx_last_timings(self.h).decode()
+
+    def set_profiling(self, on=True):
+        check(lib().st_ctx_set_profiling(self.h, ctypes.c_int32(1 if on else 0)))
+
+    def reset_kernel_stats(self):
+        check(lib().st_ctx_reset_kernel_stats(self.h))
+
+    def kernel_stats(self, name):
+        """(total_ms, launches) of a named library kernel since the last reset (HIP events, ctx stream)"""
+        ms = ctypes.c_double(0)
+        cnt = ctypes.c_uint64(0)
+        check(lib().st_ctx_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
 
     # ---- host-memory seams ----------------------------------------------------
     def transform(self, cols, params):
