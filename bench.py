@@ -158,6 +158,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
+    kstats = {}
+    for name in ('kn.sweep', 'kn.collect', 'kn.exact', 'kn.sumnd', 'k1.assign'):
+        ms, cnt = ctx.kernel_stats(name)
+        kstats[name] = {'avg_ms': ms / max(cnt, 1), 'launches': cnt}
     ctx.set_profiling(False)
 
     # one more step with per-stage event marks (outside the timed region)
@@ -208,6 +212,7 @@ def main():
         },
         'cpu_baseline': cpu,
         'stages_ms': stages,
+        'kernels': kstats,
         'draws_used_per_step': used,
     }
     print(json.dumps(out))

@@ -14,7 +14,7 @@ struct State {
     uint32_t err;
     uint32_t amb;     // ambiguous points this iteration (D > 1)
     uint32_t ties;    // exact-distance ties this iteration (D > 1)
-    uint32_t pad;
+    uint32_t overflow;  // ambiguous points whose candidate list overflowed (exact scan of all K)
 };
 
 __host__ __device__ inline uint32_t fkey_(float f) {

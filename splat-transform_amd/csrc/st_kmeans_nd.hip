@@ -3,28 +3,32 @@
 // The SH palette step (write-sog.ts:313): points = the 3C f_rest columns
 // (D = 45 at SH3), K = paletteSize (65,536 from 64k splats up).
 //
-// Score on MFMA.  score(c) = |c|^2 - 2 p.c is the nearest-centroid key for a
-// fixed point.  With a power-of-two scale sigma (max|x|*sigma in [1,2)) each
-// scaled coordinate is split into bf16 pieces x = hi + lo + r (|r| <= 2^-16|x|)
-// and one 32x32x16 bf16 MFMA chain over a K-dim of 3*KP (KP = roundup(D+3,16))
-// evaluates
-//     A[c] = [ c_hi | n1 n2 n3 | c_lo | c_hi ]      (centroid rows, n = |c|^2 in 3 bf16)
-//     B[p] = [ -2p_hi | 1 1 1  | -2p_hi | -2p_lo ]   (point columns)
-//     A.B  = |c|^2 - 2(p_hi c_hi + p_hi c_lo + p_lo c_hi)
-// Bound (products exact in f32; <= 3KP+KS f32 roundings, assumed truncating):
-//     |score_mfma - score| <= E_p = 2e-4 |p| cmax + 3e-5 cmax^2 + 1e-30   (scaled units)
-// A running top-2 (m1, i1, m2) per point: if m2 > m1 + W_p (W_p = 2 E_p + 2 delta_p,
-// delta_p covers the reference's own f64 rounding) then i1 IS the reference's
-// nearest centroid and no exact tie exists.  Otherwise the point is ambiguous:
-// a second sweep collects every centroid with score <= m1 + W_p (a superset of
-// the exact argmin set) and the exact f64 distance of kd-tree.ts:26-35 picks.
+// Score on MFMA.  score(c) = |c|^2 - 2 p.c orders the centroids of a fixed
+// point exactly like the reference's distance.  Coordinates are scaled by a
+// power of two sigma (max|x|*sigma in [1,2), exact) and rounded to fp16; one
+// v_mfma_f32_32x32x16_f16 chain over a K-dim of KP = roundup(D+3, 16) computes
+//     A[c] = [ c~ | n1 n2 n3 ]   (centroid rows; n = |sigma c|^2 split in fp16)
+//     B[p] = [ -2 p~ | 1 1 1 ]   (point columns)
+// Products are exact in f32, so (|x - x~| <= 2^-11 |x| + e_abs)
+//     |score_mfma - score| <= E = A |p| cmax + B cmax^2 + e_abs-terms + key truncation
+// with e_abs = 2^-25 when the matrix cores keep fp16 denormals (probed once per
+// context) and 2^-14 otherwise.  A running top-2 per point in the epilogue (the
+// centroid's row is packed into the 4 low mantissa bits of the score, so one
+// v_med3 + one v_min per score track both, and one compare per tile records the
+// tile of the minimum) decides the point when m2 > m1 + W_p (W_p = 2E + 2 delta_p,
+// delta_p = the reference's own f64 rounding).  Otherwise the point is
+// ambiguous (~11% at SH3): a second sweep collects every centroid with
+// score <= m1 + W_p (a superset of the exact argmin set) and the exact f64
+// distance of kd-tree.ts:26-35 decides; exact ties go to the KdTree walk.
 //
-// Tiling (gfx950, wave64): workgroup = 4 waves; each wave owns PT tiles of 32
-// points whose B fragments stay in VGPRs for the whole centroid sweep; 32-row
+// Tiling (gfx950, wave64): workgroup = 4 waves, each wave owns PT = 4 tiles of
+// 32 points whose B fragments stay in VGPRs for the whole sweep; 32-row
 // centroid tiles (pre-laid-out in fragment order, KS x 1 KiB each) stream
-// through a double-buffered LDS ring; C/D layout puts the point on the lane
-// (col = lane&31) and 16 centroids per lane-half in registers, so the top-2
-// update is lane-local: v_med3 / v_cmp / v_min / v_cndmask per score.
+// through a double-buffered LDS ring, CT_STAGE tiles per barrier.  The C/D
+// layout puts the point on the lane (col = lane & 31) and 16 centroid rows per
+// lane-half in registers, so the top-2 update is lane-local.
+#include <cmath>
+
 #include "st_jsmath.h"
 #include "st_kmeans.h"
 
@@ -33,22 +37,57 @@ namespace {
 
 using namespace km;
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int CT_STAGE = 2;    // centroid tiles per LDS stage
+constexpr int PT = 4;          // point tiles per wave
+constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
-constexpr float ERR_A = 2.0e-4f, ERR_B = 3.0e-5f, ERR_ABS = 1.0e-30f, REL64 = 1.0e-13f;
 
 __host__ __device__ inline int kp_of(int d) { return ((d + 3) + 15) / 16 * 16; }
 
-// ---- bf16 helpers (RNE on finite values) ----------------------------------
-__device__ inline uint16_t bf16_bits(float f) {
-    uint32_t u = __builtin_bit_cast(uint32_t, f);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
+// fp16 RNE of a finite float (scaled values are < 2^16)
+__device__ inline uint16_t h_bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ inline float h_val(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+
+struct Bound {
+    float a, b, ec, ep, rel;  // E = a|p|cm + b cm^2 + ec (|p| + cm) + ep; delta = rel (|p| + cm)^2
+};
+
+// error-bound constants for a given dimension and fp16-denormal behaviour
+Bound make_bound(int d, bool denorm) {
+    const double u = std::ldexp(1.0, -11);          // fp16 RNE relative half-ulp
+    const double e_abs = denorm ? std::ldexp(1.0, -25) : std::ldexp(1.0, -14);
+    const double gam = (d + 3 + 3) * std::ldexp(1.0, -23);  // f32 accumulation, truncation-safe
+    const double trunc = 16 * std::ldexp(1.0, -23);         // 4 low bits replaced by the row id
+    Bound B{};
+    // rounding of p and c (x2 for the -2 factor) + accumulation + key truncation, 5% slack
+    B.a = (float)((2 * 2 * u * (1 + u) + 2.01 * gam + 2 * trunc) * 1.05);
+    B.b = (float)((1.01 * gam + std::ldexp(1.0, -22) + trunc) * 1.05);
+    B.ec = (float)(2 * std::sqrt((double)d) * e_abs * (1 + u) * 1.05);
+    B.ep = (float)((2 * d * e_abs * e_abs + 3 * e_abs) * 1.05 + 1e-30);
+    B.rel = 1.0e-13f;
+    return B;
 }
-__device__ inline float bf16_val(uint16_t h) { return __builtin_bit_cast(float, (uint32_t)h << 16); }
+
+__device__ inline float wbound(const Bound &B, float pn, float cm) {
+    const float e = B.a * pn * cm + B.b * cm * cm + B.ec * (pn + cm) + B.ep;
+    const float s = pn + cm;
+    return (2.0f * e + 2.0f * B.rel * s * s) * 1.0001f;
+}
+
+// does v_mfma_f32_32x32x16_f16 keep fp16 denormal inputs?
+__global__ void k_probe_denorm(float *out) {
+    const int lane = threadIdx.x;
+    f16x8 a = {}, b = {};
+    if (lane == 0) {
+        a[0] = __builtin_bit_cast(_Float16, (uint16_t)0x0010u);  // 2^-20
+        b[0] = (_Float16)1.0f;
+    }
+    f32x16 acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+    if (lane == 0) out[0] = acc[0];
+}
 
 // ---- preparation kernels ------------------------------------------------------
 __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d, uint64_t n, uint32_t *out) {
@@ -60,149 +99,133 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
     if ((threadIdx.x & 63) == 0) atomicMax(out, __builtin_bit_cast(uint32_t, m));
 }
 
-// point B fragments: pfrag[t][s][lane] = 8 bf16 of B[k = 16s + 8h + j][p = 32t + (lane&31)]
+// point B fragments: pfrag[t][s][lane] = 8 fp16 of B[k = 16s + 8h + j][p = 32t + (lane&31)];
+// one thread per (point, k-step, half); also |sigma p| (rounded up) and the AoS f32 copy
 __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
-                                                     int ks, float sigma, uint4 *pfrag, float *pnorm,
-                                                     float *aos) {
-    const int kp = kp_of(d);
-    const uint64_t total = (uint64_t)ntiles * 32;
+                                                     int ks, float sigma, uint4 *pfrag, float *pnorm, float *aos) {
+    const uint64_t total = (uint64_t)ntiles * 32 * ks * 2;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += stride) {
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += stride) {
+        const uint64_t p = q % ((uint64_t)ntiles * 32);
+        const int sh = (int)(q / ((uint64_t)ntiles * 32));  // s * 2 + h
+        const int s = sh >> 1, h = sh & 1;
         const bool valid = p < n;
-        uint16_t hi[64], lo[64];
-        double nn = 0;
-        for (int c = 0; c < kp; ++c) {
-            float v = 0.f;
-            if (valid && c < d) {
-                const float raw = cols[c][p];
-                aos[p * d + c] = raw;
-                v = raw * sigma;
-            }
-            const uint16_t h = bf16_bits(v);
-            hi[c] = h;
-            lo[c] = bf16_bits(v - bf16_val(h));
-            nn += (double)v * (double)v;
-        }
-        if (valid) pnorm[p] = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
-        const uint32_t t = (uint32_t)(p >> 5), col = (uint32_t)(p & 31);
-        for (int s = 0; s < ks; ++s)
-            for (int h = 0; h < 2; ++h) {
-                uint16_t e[8];
-                for (int j = 0; j < 8; ++j) {
-                    const int k = 16 * s + 8 * h + j;
-                    const int piece = k / kp, dim = k % kp;
-                    uint16_t bits;
-                    if (dim < d) {
-                        const uint16_t src = (piece == 2) ? lo[dim] : hi[dim];
-                        bits = bf16_bits(-2.0f * bf16_val(src));  // exact (power-of-two scale)
-                    } else if (piece == 0 && dim < d + 3) {
-                        bits = valid ? (uint16_t)0x3f80u : (uint16_t)0;  // 1.0
-                    } else {
-                        bits = 0;
-                    }
-                    e[j] = bits;
+        uint16_t e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * s + 8 * h + j;
+            uint16_t bits = 0;
+            if (k < d) {
+                if (valid) {
+                    const float raw = cols[k][p];
+                    aos[p * d + k] = raw;
+                    bits = h_bits(-2.0f * h_val(h_bits(raw * sigma)));  // -2 p~ exactly
                 }
-                uint4 q;
-                q.x = e[0] | ((uint32_t)e[1] << 16);
-                q.y = e[2] | ((uint32_t)e[3] << 16);
-                q.z = e[4] | ((uint32_t)e[5] << 16);
-                q.w = e[6] | ((uint32_t)e[7] << 16);
-                pfrag[((uint64_t)t * ks + s) * 64 + h * 32 + col] = q;
+            } else if (k < d + 3) {
+                bits = valid ? (uint16_t)0x3c00u : (uint16_t)0;  // 1.0
             }
+            e[j] = bits;
+        }
+        uint4 v;
+        v.x = e[0] | ((uint32_t)e[1] << 16);
+        v.y = e[2] | ((uint32_t)e[3] << 16);
+        v.z = e[4] | ((uint32_t)e[5] << 16);
+        v.w = e[6] | ((uint32_t)e[7] << 16);
+        pfrag[((p >> 5) * ks + s) * 64 + h * 32 + (p & 31)] = v;
+        if (sh == 0 && valid) {
+            double nn = 0;
+            for (int c = 0; c < d; ++c) {
+                const double x = (double)(cols[c][p] * sigma);
+                nn += x * x;
+            }
+            pnorm[p] = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+        }
     }
 }
 
-// centroid A fragments + cmax; rows >= k are padding that can never win
+// centroid A fragments + cmax; one thread per centroid row; rows >= k can never win
 __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
                                                         float sigma, uint4 *cfrag, uint32_t *cmax_bits) {
-    const int kp = kp_of(d);
     const uint32_t total = ctiles * 32;
     float mymax = 0.f;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < total; r += gridDim.x * blockDim.x) {
         const bool valid = r < (uint32_t)k;
-        uint16_t hi[64], lo[64];
         double nn = 0;
-        for (int c = 0; c < kp; ++c) {
-            const float v = (valid && c < d) ? cen[(uint64_t)c * k + r] * sigma : 0.f;
-            const uint16_t h = bf16_bits(v);
-            hi[c] = h;
-            lo[c] = bf16_bits(v - bf16_val(h));
-            nn += (double)v * (double)v;
+        for (int c = 0; c < d; ++c) {
+            const double x = valid ? (double)(cen[(uint64_t)c * k + r] * sigma) : 0.0;
+            nn += x * x;
         }
-        if (!valid) nn = 1.0e30;  // padding rows: score 1e30
-        // n = n1 + n2 + n3 to ~2^-24 relative
-        const float f0 = (float)nn;
-        const uint16_t n1 = bf16_bits(f0);
-        const double r1 = nn - (double)bf16_val(n1);
-        const uint16_t n2 = bf16_bits((float)r1);
-        const double r2 = r1 - (double)bf16_val(n2);
-        const uint16_t n3 = bf16_bits((float)r2);
-        if (valid) mymax = fmaxf(mymax, (float)(__builtin_sqrt(nn) * (1.0 + 1e-6)));
+        uint16_t n1, n2, n3;
+        if (valid) {
+            n1 = h_bits((float)nn);
+            const double r1 = nn - (double)h_val(n1);
+            n2 = h_bits((float)r1);
+            const double r2 = r1 - (double)h_val(n2);
+            n3 = h_bits((float)r2);
+            mymax = fmaxf(mymax, (float)(__builtin_sqrt(nn) * (1.0 + 1e-6)));
+        } else {
+            n1 = h_bits(60000.0f);  // padding: score ~6e4 >> any real score (< 200)
+            n2 = n3 = 0;
+        }
         const uint32_t t = r >> 5, row = r & 31;
         for (int s = 0; s < ks; ++s)
             for (int h = 0; h < 2; ++h) {
                 uint16_t e[8];
+#pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int kk = 16 * s + 8 * h + j;
-                    const int piece = kk / kp, dim = kk % kp;
                     uint16_t bits = 0;
-                    if (dim < d) bits = (piece == 1) ? lo[dim] : hi[dim];
-                    else if (piece == 0 && dim == d) bits = n1;
-                    else if (piece == 0 && dim == d + 1) bits = n2;
-                    else if (piece == 0 && dim == d + 2) bits = n3;
+                    if (kk < d) bits = valid ? h_bits(cen[(uint64_t)kk * k + r] * sigma) : (uint16_t)0;
+                    else if (kk == d) bits = n1;
+                    else if (kk == d + 1) bits = n2;
+                    else if (kk == d + 2) bits = n3;
                     e[j] = bits;
                 }
-                uint4 q;
-                q.x = e[0] | ((uint32_t)e[1] << 16);
-                q.y = e[2] | ((uint32_t)e[3] << 16);
-                q.z = e[4] | ((uint32_t)e[5] << 16);
-                q.w = e[6] | ((uint32_t)e[7] << 16);
-                cfrag[((uint64_t)t * ks + s) * 64 + h * 32 + row] = q;
+                uint4 v;
+                v.x = e[0] | ((uint32_t)e[1] << 16);
+                v.y = e[2] | ((uint32_t)e[3] << 16);
+                v.z = e[4] | ((uint32_t)e[5] << 16);
+                v.w = e[6] | ((uint32_t)e[7] << 16);
+                cfrag[((uint64_t)t * ks + s) * 64 + h * 32 + row] = v;
             }
     }
     for (int o = 32; o > 0; o >>= 1) mymax = fmaxf(mymax, __shfl_xor(mymax, o, 64));
     if ((threadIdx.x & 63) == 0) atomicMax(cmax_bits, __builtin_bit_cast(uint32_t, mymax));
 }
 
-__device__ inline float wbound(float pn, float cm) {
-    const float e = ERR_A * pn * cm + ERR_B * cm * cm + ERR_ABS;
-    const float s = pn + cm;
-    return (2.0f * e + 2.0f * REL64 * s * s) * 1.0001f;
-}
-
 // ---- the MFMA sweep -------------------------------------------------------------
-// MODE 0: main assign (top-2, decide or flag ambiguous)
-// MODE 1: collect candidates for ambiguous points (score <= thr)
-template <int KS, int PT, int MODE>
-__global__ __launch_bounds__(256, 2) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
-                                                  const uint4 *__restrict__ cfrag, uint32_t ctiles,
-                                                  const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
-                                                  const uint32_t *__restrict__ amb_ids,  // MODE 1: slot -> point
-                                                  uint32_t *__restrict__ labels, float *__restrict__ thr,
-                                                  uint32_t *__restrict__ amb, State *st,
-                                                  uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand) {
+// MODE 0: main assign (top-2; decide or flag ambiguous)
+// MODE 1: collect candidates of ambiguous points (score <= thr)
+template <int KS, int MODE>
+__global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
+                                               const uint4 *__restrict__ cfrag, uint32_t ctiles,
+                                               const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
+                                               const Bound bnd, uint32_t *__restrict__ labels,
+                                               float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
+                                               uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
+    constexpr int PER_THREAD = (STAGE_U4 + 255) / 256;
     __shared__ uint4 lds[2][STAGE_U4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const uint32_t tile0 = (blockIdx.x * 4 + w) * PT;
 
-    bf16x8 b[PT][KS];
+    f16x8 b[PT][KS];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         const uint32_t tt = tile0 + t;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             uint4 q = (tt < ntiles) ? pfrag[((uint64_t)tt * KS + s) * 64 + lane] : make_uint4(0, 0, 0, 0);
-            b[t][s] = __builtin_bit_cast(bf16x8, q);
+            b[t][s] = __builtin_bit_cast(f16x8, q);
         }
     }
     float m1[PT], m2[PT], th[PT];
-    uint32_t i1[PT];
+    uint32_t t1[PT];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         m1[t] = __builtin_inff();
         m2[t] = __builtin_inff();
-        i1[t] = 0;
+        t1[t] = 0;
         th[t] = -__builtin_inff();
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -211,24 +234,21 @@ __global__ __launch_bounds__(256, 2) void k_sweep(const uint4 *__restrict__ pfra
     }
 
     const uint32_t nstages = (ctiles + CT_STAGE - 1) / CT_STAGE;
-    const uint4 *src = cfrag;
     const uint32_t total_u4 = ctiles * KS * 64;
-    // prologue: stage 0
-    for (uint32_t i = threadIdx.x; i < STAGE_U4; i += 256) lds[0][i] = (i < total_u4) ? src[i] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)STAGE_U4; i += 256)
+        lds[0][i] = (i < total_u4) ? cfrag[i] : make_uint4(0, 0, 0, 0);
     __syncthreads();
     for (uint32_t sg = 0; sg < nstages; ++sg) {
         const int cur = sg & 1;
-        // prefetch next stage into registers
-        constexpr int PER_THREAD = (STAGE_U4 + 255) / 256;
         uint4 nxt[PER_THREAD];
         const uint32_t nbase = (sg + 1) * STAGE_U4;
 #pragma unroll
         for (int q = 0; q < PER_THREAD; ++q) {
             const uint32_t i = threadIdx.x + q * 256;
-            nxt[q] = (sg + 1 < nstages && i < (uint32_t)STAGE_U4 && nbase + i < total_u4) ? src[nbase + i]
+            nxt[q] = (sg + 1 < nstages && i < (uint32_t)STAGE_U4 && nbase + i < total_u4) ? cfrag[nbase + i]
                                                                                           : make_uint4(0, 0, 0, 0);
         }
-#pragma unroll
+#pragma unroll 2
         for (int ct = 0; ct < CT_STAGE; ++ct) {
             const uint32_t ctile = sg * CT_STAGE + ct;
             f32x16 acc[PT];
@@ -236,26 +256,32 @@ __global__ __launch_bounds__(256, 2) void k_sweep(const uint4 *__restrict__ pfra
             for (int t = 0; t < PT; ++t) acc[t] = f32x16{};
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                const bf16x8 a = __builtin_bit_cast(bf16x8, lds[cur][(ct * KS + s) * 64 + lane]);
+                const f16x8 a = __builtin_bit_cast(f16x8, lds[cur][(ct * KS + s) * 64 + lane]);
 #pragma unroll
-                for (int t = 0; t < PT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[t][s], acc[t], 0, 0, 0);
+                for (int t = 0; t < PT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[t][s], acc[t], 0, 0, 0);
             }
             if (ctile < ctiles) {
-                const uint32_t cb = ctile * 32 + 4 * h;
 #pragma unroll
                 for (int t = 0; t < PT; ++t) {
+                    if (MODE == 0) {
+                        const float before = m1[t];
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float sc = acc[t][r];
-                        const uint32_t ci = cb + (r & 3) + 8 * (r >> 2);
-                        if (MODE == 0) {
-                            m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], sc);
-                            const bool lt = sc < m1[t];
-                            m1[t] = lt ? sc : m1[t];
-                            i1[t] = lt ? ci : i1[t];
-                        } else {
-                            if (sc <= th[t]) {
+                        for (int r = 0; r < 16; ++r) {
+                            // score with the row id r in its 4 low mantissa bits.  NB: read the vector
+                            // element by value first: __builtin_bit_cast on an ext_vector element
+                            // lvalue silently reads element 0 (hipcc / ROCm 7.2).
+                            const float sc = acc[t][r];
+                            const float key = __uint_as_float((__float_as_uint(sc) & ~0xFu) | (uint32_t)r);
+                            m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], key);
+                            m1[t] = fminf(m1[t], key);
+                        }
+                        t1[t] = (m1[t] < before) ? ctile : t1[t];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            if (acc[t][r] <= th[t]) {
                                 const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
+                                const uint32_t ci = ctile * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
                                 const uint32_t pos = atomicAdd(&cand_cnt[slot], 1u);
                                 if (pos < CAND_CAP) cand[(uint64_t)slot * CAND_CAP + pos] = ci;
                             }
@@ -279,15 +305,17 @@ __global__ __launch_bounds__(256, 2) void k_sweep(const uint4 *__restrict__ pfra
     const float cm = __builtin_bit_cast(float, *cmax_bits);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
+        const uint32_t rid = __builtin_bit_cast(uint32_t, m1[t]) & 0xFu;
+        const uint32_t i1 = t1[t] * 32 + 4 * h + (rid & 3) + 8 * (rid >> 2);
         const float om1 = __shfl_xor(m1[t], 32, 64), om2 = __shfl_xor(m2[t], 32, 64);
-        const uint32_t oi1 = __shfl_xor(i1[t], 32, 64);
+        const uint32_t oi1 = __shfl_xor(i1, 32, 64);
         const float nm1 = fminf(m1[t], om1);
         const float nm2 = fminf(fmaxf(m1[t], om1), fminf(m2[t], om2));
-        const uint32_t ni1 = (m1[t] < om1) ? i1[t] : ((om1 < m1[t]) ? oi1 : min(i1[t], oi1));
+        const uint32_t ni1 = (m1[t] <= om1) ? i1 : oi1;
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
         bool is_amb = false;
         if (h == 0 && p < npts) {
-            const float W = wbound(pnorm[p], cm);
+            const float W = wbound(bnd, pnorm[p], cm);
             if (nm2 > nm1 + W) {
                 labels[p] = ni1;
             } else {
@@ -349,6 +377,7 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     const float *prow = aos + (uint64_t)p * d;
     const uint32_t cnt = cand_cnt[a];
     const bool overflow = cnt > CAND_CAP;
+    if (overflow && lane == 0) atomicAdd(&st->overflow, 1u);
     double best = __builtin_inf();
     uint32_t bidx = 0xffffffffu;
     const uint32_t limit = overflow ? (uint32_t)k : cnt;
@@ -416,46 +445,51 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
 
 template <int KS>
 struct Sweep {
-    static constexpr int PT = 2;
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
-                     const float *pnorm, const uint32_t *cmax, uint32_t *labels, float *thr, uint32_t *amb,
-                     State *st) {
+                     const float *pnorm, const uint32_t *cmax, const Bound &bnd, uint32_t *labels, float *thr,
+                     uint32_t *amb, State *st) {
         const uint32_t per_block = 4 * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
-        hipLaunchKernelGGL((k_sweep<KS, PT, 0>), grid, dim3(256), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
-                           cmax, (const uint32_t *)nullptr, labels, thr, amb, st, (uint32_t *)nullptr,
-                           (uint32_t *)nullptr);
+        hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(256), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
+                           cmax, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr);
         ST_LAUNCH_CHECK();
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
-                        uint32_t ctiles, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
+                        uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
         const uint32_t per_block = 4 * PT;
         const dim3 grid((atiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.collect");
-        hipLaunchKernelGGL((k_sweep<KS, PT, 1>), grid, dim3(256), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
-                           (const float *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
-                           (uint32_t *)nullptr, thr_slot, (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand);
+        hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(256), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
+                           (const float *)nullptr, (const uint32_t *)nullptr, bnd, (uint32_t *)nullptr, thr_slot,
+                           (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand);
         ST_LAUNCH_CHECK();
     }
 };
 
-template <int KS>
-void run_main(st_ctx *c, int ks_dummy, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag,
-              uint32_t ctiles, const float *pnorm, const uint32_t *cmax, uint32_t *labels, float *thr, uint32_t *amb,
-              State *st) {
-    (void)ks_dummy;
-    Sweep<KS>::main(c, pfrag, ntiles, n, cfrag, ctiles, pnorm, cmax, labels, thr, amb, st);
+bool probe_denorm(st_ctx *c) {
+    static thread_local std::map<int, bool> cache;
+    auto it = cache.find(c->device);
+    if (it != cache.end()) return it->second;
+    auto *d = wsT<float>(c, "kn.probe", 1);
+    hipLaunchKernelGGL(k_probe_denorm, dim3(1), dim3(64), 0, c->stream, d);
+    ST_LAUNCH_CHECK();
+    float v = 0;
+    ST_HIP(hipMemcpyAsync(&v, d, 4, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    const bool keep = (v == std::ldexp(1.0f, -20));
+    cache[c->device] = keep;
+    return keep;
 }
 
 }  // namespace
 
 #define ST_KS_DISPATCH(KSV, CALL) \
     switch (KSV) {                \
-        case 3: { constexpr int KS = 3; CALL; } break;   \
-        case 6: { constexpr int KS = 6; CALL; } break;   \
-        case 9: { constexpr int KS = 9; CALL; } break;   \
-        case 12: { constexpr int KS = 12; CALL; } break; \
+        case 1: { constexpr int KS = 1; CALL; } break; \
+        case 2: { constexpr int KS = 2; CALL; } break; \
+        case 3: { constexpr int KS = 3; CALL; } break; \
+        case 4: { constexpr int KS = 4; CALL; } break; \
         default: throw Error(ST_ERR_UNSUPPORTED, "kmeans: dimension too large for the MFMA assign (D <= 61)"); \
     }
 
@@ -463,7 +497,7 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
     ST_REQUIRE(d <= 61, ST_ERR_UNSUPPORTED, "kmeans: D > 61 not supported by the MFMA assign");
     ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
-    const int kp = kp_of(d), ks = 3 * kp / 16;
+    const int ks = kp_of(d) / 16;
     const uint32_t ntiles = (uint32_t)((n + 31) / 32);
     const uint32_t ctiles = (uint32_t)((k + 31) / 32);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
@@ -478,6 +512,7 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits
     auto *h = static_cast<State *>(pinned(c, sizeof(State)));
+    const Bound bnd = make_bound(d, probe_denorm(c));
 
     // scale: max|x| * sigma in [1, 2)
     ST_HIP(hipMemsetAsync(scal, 0, 16, c->stream));
@@ -489,8 +524,8 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     const float amax = __builtin_bit_cast(float, amax_bits);
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
-    hipLaunchKernelGGL(k_point_frags, dim3(grid_for((uint64_t)ntiles * 32, 256, 8192)), dim3(256), 0, c->stream,
-                       dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, aos);
+    hipLaunchKernelGGL(k_point_frags, dim3(grid_for((uint64_t)ntiles * 32 * ks * 2, 256, 16384)), dim3(256), 0,
+                       c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, aos);
     ST_LAUNCH_CHECK();
     mark(c, "kn.prep");
 
@@ -499,9 +534,9 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0,
                            c->stream, cen, d, k, ctiles, ks, sigma, cfrag, scal + 1);
         ST_LAUNCH_CHECK();
-        ST_HIP(hipMemsetAsync(&dstate->amb, 0, 8, c->stream));  // amb + ties
-        ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, labels, thr,
-                                            amb, dstate)));
+        ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
+        ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
+                                            thr, amb, dstate)));
         mark(c, "kn.assign");
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
@@ -515,20 +550,38 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
             hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, c->stream,
                                pfrag, amb, thr, namb, ks, afrag, thr_slot, cand_cnt);
             ST_LAUNCH_CHECK();
-            ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, thr_slot, cand_cnt, cand)));
-            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, cen, k, amb, namb,
-                               cand_cnt, cand, labels, ties, dstate);
-            ST_LAUNCH_CHECK();
+            ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt,
+                                                   cand)));
+            {
+                KTimer kt(c, "kn.exact");
+                hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, cen, k, amb, namb,
+                                   cand_cnt, cand, labels, ties, dstate);
+                ST_LAUNCH_CHECK();
+            }
             ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
             ST_HIP(hipStreamSynchronize(c->stream));
+            if (getenv("ST_DEBUG")) {
+                uint32_t cmb = 0;
+                float pn0 = 0, thr0 = 0;
+                ST_HIP(hipMemcpy(&cmb, scal + 1, 4, hipMemcpyDeviceToHost));
+                ST_HIP(hipMemcpy(&pn0, pnorm, 4, hipMemcpyDeviceToHost));
+                ST_HIP(hipMemcpy(&thr0, thr, 4, hipMemcpyDeviceToHost));
+                fprintf(stderr,
+                        "[st kmeans] it=%d n=%llu k=%d ambiguous=%u ties=%u overflow=%u sigma=%g cmax=%g |p0|=%g "
+                        "thr0=%g bound a=%g b=%g ec=%g ep=%g\n",
+                        it, (unsigned long long)n, k, namb, h->ties, h->overflow, sigma,
+                        __builtin_bit_cast(float, cmb), pn0, thr0, bnd.a, bnd.b, bnd.ec, bnd.ep);
+            }
             if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
         }
         mark(c, "kn.exact");
         // update
         member_sort(c, labels, n, k, sorted_labels, members, start);
-        KTimer kt(c, "kn.sumnd");
-        hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen);
-        ST_LAUNCH_CHECK();
+        {
+            KTimer kt(c, "kn.sumnd");
+            hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen);
+            ST_LAUNCH_CHECK();
+        }
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "kn.update");
     }
