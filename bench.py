@@ -26,7 +26,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
 
-MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
+MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA peak (MI355X_MICROARCH.md)
 HBM_TBPS = 8.0
 
 
@@ -193,18 +193,18 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'f64+f32 (bit-exact JS semantics); bf16x3 MFMA for the assign prefilter',
+        'dtype': 'f64+f32 (bit-exact JS semantics); fp16 MFMA (f32 accumulate) for the assign prefilter',
         'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seed 1002+rank), resident in HBM',
         'config': {'workload': f'writeSog SH3 {n} splats/GPU, {args.iters} k-means iters, paletteSize {pal}',
                    'splats_per_gpu': n, 'sh_bands': 3, 'palette_size': pal, 'iterations': args.iters,
                    'parallelism': f'dp{world}'},
         'roofline': {
-            'kernel': 'k_sweep<KS=9> (v_mfma_f32_32x32x16_bf16 nearest-centroid assign)',
+            'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-2 per splat)',
             'bound': 'mfma',
             'achieved': achieved,
-            'peak': MFMA_BF16_DENSE_TFLOPS,
+            'peak': MFMA_F16_DENSE_TFLOPS,
             'unit': 'TFLOP/s',
-            'frac': (achieved / MFMA_BF16_DENSE_TFLOPS) if achieved else None,
+            'frac': (achieved / MFMA_F16_DENSE_TFLOPS) if achieved else None,
             'traffic': None,
             'algorithmic_flops_per_launch': flops_per_launch,
             'avg_launch_ms': avg_sweep_s * 1e3,

@@ -130,14 +130,21 @@ __device__ inline int ulp_exp(float x) {
     return e == 0 ? -149 : (int)e - 150;
 }
 
+// calcAverage (k-means.ts:41-63) for one cluster: the reference adds the members' values
+// in ascending point order into one f64.  When every partial sum is exactly representable
+// (certificate: sum|x| < 2^(emin+53), emin = the smallest ulp exponent among the values)
+// the order is immaterial and the block sums in parallel; otherwise the cluster is
+// flagged and k_sum1d_seq replays the sequential sum.
 __global__ __launch_bounds__(256) void k_sum1d(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
-                                               int k, float *__restrict__ cen) {
+                                               int k, float *__restrict__ cen, uint32_t *__restrict__ seq_flag) {
     const int cl = blockIdx.x;
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    if (s1 == s0) return;  // empty: re-seeded separately
+    if (s1 == s0) {  // empty: re-seeded separately
+        if (threadIdx.x == 0) seq_flag[cl] = 0;
+        return;
+    }
     __shared__ double red_s[4], red_a[4];
     __shared__ int red_e[4];
-    __shared__ double seq_sum;
     double sum = 0, sabs = 0;
     int emin = 1 << 20;
     for (uint32_t j = s0 + threadIdx.x; j < s1; j += blockDim.x) {
@@ -158,28 +165,60 @@ __global__ __launch_bounds__(256) void k_sum1d(const uint32_t *__restrict__ vals
         red_e[w] = emin;
     }
     __syncthreads();
+    if (threadIdx.x != 0) return;
     sum = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);
     sabs = (red_a[0] + red_a[1]) + (red_a[2] + red_a[3]);
     emin = min(min(red_e[0], red_e[1]), min(red_e[2], red_e[3]));
-    const uint32_t count = s1 - s0;
-    // certificate: sum|x| (bounded above with slack for its own rounding) < 2^(emin+53)
+    // sum|x| bounded above with slack for its own rounding
     const bool exact = (sabs == 0.0) || (sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin + 53));
-    if (!exact) {
-        // sequential sum in ascending point order (calcAverage)
-        if (w == 0) {
-            double s = 0;
-            for (uint32_t j0 = s0; j0 < s1; j0 += 64) {
-                const uint32_t j = j0 + lane;
-                const double v = (j < s1) ? (double)__builtin_bit_cast(float, vals[j]) : 0.0;
-                const uint32_t m = (s1 - j0 < 64u) ? (s1 - j0) : 64u;
-                for (uint32_t t = 0; t < m; ++t) s += __shfl(v, (int)t, 64);
-            }
-            if (lane == 0) seq_sum = s;
+    seq_flag[cl] = exact ? 0u : 1u;
+    if (exact) cen[cl] = (float)(sum / (double)(s1 - s0));
+}
+
+// the sequential f64 sum of a flagged cluster: one lane walks the members in order, the
+// loads run PF x 16 bytes ahead of the dependent add chain
+__global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
+                                                  const uint32_t *__restrict__ seq_flag, float *__restrict__ cen) {
+    const int cl = blockIdx.x;
+    if (!seq_flag[cl] || threadIdx.x != 0) return;
+    const uint32_t s0 = start[cl], s1 = start[cl + 1];
+    double s = 0;
+    uint32_t j = s0;
+    for (; j < s1 && (j & 3u); ++j) s += (double)__builtin_bit_cast(float, vals[j]);
+    const uint32_t nq = (s1 - j) >> 2;
+    // a zero the compiler cannot see keeps the (uniform) loads on the vector path: scalar
+    // loads would each need an lgkmcnt(0) wait and serialise the chain
+    uint32_t opaque0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(opaque0));
+    const uint4 *q = reinterpret_cast<const uint4 *>(vals + j) + opaque0;
+    constexpr uint32_t PF = 16;
+    uint4 buf[PF];
+#pragma unroll
+    for (uint32_t u = 0; u < PF; ++u) buf[u] = (u < nq) ? q[u] : make_uint4(0, 0, 0, 0);
+    uint32_t i = 0;
+    for (; i + PF <= nq; i += PF) {
+#pragma unroll
+        for (uint32_t u = 0; u < PF; ++u) {
+            const uint4 v = buf[u];
+            buf[u] = (i + u + PF < nq) ? q[i + u + PF] : make_uint4(0, 0, 0, 0);
+            s += (double)__builtin_bit_cast(float, v.x);
+            s += (double)__builtin_bit_cast(float, v.y);
+            s += (double)__builtin_bit_cast(float, v.z);
+            s += (double)__builtin_bit_cast(float, v.w);
         }
-        __syncthreads();
-        sum = seq_sum;
     }
-    if (threadIdx.x == 0) cen[cl] = (float)(sum / (double)count);
+#pragma unroll
+    for (uint32_t u = 0; u < PF; ++u) {  // buf[u] holds quad i + u
+        if (i + u < nq) {
+            const uint4 v = buf[u];
+            s += (double)__builtin_bit_cast(float, v.x);
+            s += (double)__builtin_bit_cast(float, v.y);
+            s += (double)__builtin_bit_cast(float, v.z);
+            s += (double)__builtin_bit_cast(float, v.w);
+        }
+    }
+    for (j += nq * 4; j < s1; ++j) s += (double)__builtin_bit_cast(float, vals[j]);
+    cen[cl] = (float)(s / (double)(s1 - s0));
 }
 
 }  // namespace
@@ -191,6 +230,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     auto *keys = wsT<uint32_t>(c, "k1.keys", n);
     auto *vals = wsT<uint32_t>(c, "k1.vals", n);
     auto *start = wsT<uint32_t>(c, "k1.start", (size_t)k + 1);
+    auto *seq_flag = wsT<uint32_t>(c, "k1.seqflag", (size_t)k);
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
     for (int it = 0; it < iters; ++it) {
@@ -199,12 +239,16 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         ST_LAUNCH_CHECK();
         radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
         const unsigned g = grid_for(n, 256, 256 * 16);
-        KTimer kt(c, "k1.assign");
-        if (k <= KD1_LDS)
-            hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
-        else
-            hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
-        ST_LAUNCH_CHECK();
+        {
+            KTimer kt(c, "k1.assign");
+            if (k <= KD1_LDS)
+                hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
+                                   labels);
+            else
+                hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
+                                   labels);
+            ST_LAUNCH_CHECK();
+        }
         mark(c, "k1.assign");
         // update
         hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,
@@ -212,8 +256,13 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         ST_LAUNCH_CHECK();
         radix_sort_u32(c, keys, vals, n, 0, kbits, "k1.msort");
         bounds_from_sorted(c, keys, n, k, start);
-        hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen);
-        ST_LAUNCH_CHECK();
+        {
+            KTimer kt(c, "k1.sum");
+            hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen, seq_flag);
+            ST_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_sum1d_seq, dim3(k), dim3(64), 0, c->stream, vals, start, seq_flag, cen);
+            ST_LAUNCH_CHECK();
+        }
         reseed_empty(c, dcols, 1, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "k1.update");
     }

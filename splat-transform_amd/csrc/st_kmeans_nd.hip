@@ -10,13 +10,13 @@
 //     A[c] = [ c~ | n1 n2 n3 ]   (centroid rows; n = |sigma c|^2 split in fp16)
 //     B[p] = [ -2 p~ | 1 1 1 ]   (point columns)
 // Products are exact in f32, so (|x - x~| <= 2^-11 |x| + e_abs)
-//     |score_mfma - score| <= E = A |p| cmax + B cmax^2 + e_abs-terms + key truncation
+//     |score_mfma - score| <= E = A |p| cmax + B cmax^2 + e_abs-terms
 // with e_abs = 2^-25 when the matrix cores keep fp16 denormals (probed once per
-// context) and 2^-14 otherwise.  A running top-2 per point in the epilogue (the
-// centroid's row is packed into the 4 low mantissa bits of the score, so one
-// v_med3 + one v_min per score track both, and one compare per tile records the
-// tile of the minimum) decides the point when m2 > m1 + W_p (W_p = 2E + 2 delta_p,
-// delta_p = the reference's own f64 rounding).  Otherwise the point is
+// context) and 2^-14 otherwise.  A running top-2 per point in the epilogue (one
+// v_med3 + one v_min per score, one compare per tile to record the tile of the
+// minimum) decides the point when m2 > m1 + W_p (W_p = 2E + 2 delta_p, delta_p =
+// the reference's own f64 rounding); k_fixrow then finds the row inside that
+// tile with the exact f64 distance.  Otherwise the point is
 // ambiguous (~11% at SH3): a second sweep collects every centroid with
 // score <= m1 + W_p (a superset of the exact argmin set) and the exact f64
 // distance of kd-tree.ts:26-35 decides; exact ties go to the KdTree walk.
@@ -28,6 +28,7 @@
 // layout puts the point on the lane (col = lane & 31) and 16 centroid rows per
 // lane-half in registers, so the top-2 update is lane-local.
 #include <cmath>
+#include <utility>
 
 #include "st_jsmath.h"
 #include "st_kmeans.h"
@@ -36,6 +37,16 @@ namespace st {
 namespace {
 
 using namespace km;
+
+// compile-time loop: f(std::integral_constant<int, 0>{}) ... f(integral_constant<N - 1>{})
+template <typename F, int... I>
+__device__ inline void static_for_(F &f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ inline void static_for(F &&f) {
+    static_for_(f, std::make_integer_sequence<int, N>{});
+}
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -59,11 +70,10 @@ Bound make_bound(int d, bool denorm) {
     const double u = std::ldexp(1.0, -11);          // fp16 RNE relative half-ulp
     const double e_abs = denorm ? std::ldexp(1.0, -25) : std::ldexp(1.0, -14);
     const double gam = (d + 3 + 3) * std::ldexp(1.0, -23);  // f32 accumulation, truncation-safe
-    const double trunc = 16 * std::ldexp(1.0, -23);         // 4 low bits replaced by the row id
     Bound B{};
-    // rounding of p and c (x2 for the -2 factor) + accumulation + key truncation, 5% slack
-    B.a = (float)((2 * 2 * u * (1 + u) + 2.01 * gam + 2 * trunc) * 1.05);
-    B.b = (float)((1.01 * gam + std::ldexp(1.0, -22) + trunc) * 1.05);
+    // rounding of p and c (x2 for the -2 factor) + accumulation, 5% slack
+    B.a = (float)((2 * 2 * u * (1 + u) + 2.01 * gam) * 1.05);
+    B.b = (float)((1.01 * gam + std::ldexp(1.0, -22)) * 1.05);
     B.ec = (float)(2 * std::sqrt((double)d) * e_abs * (1 + u) * 1.05);
     B.ep = (float)((2 * d * e_abs * e_abs + 3 * e_abs) * 1.05 + 1e-30);
     B.rel = 1.0e-13f;
@@ -196,6 +206,12 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
 // ---- the MFMA sweep -------------------------------------------------------------
 // MODE 0: main assign (top-2; decide or flag ambiguous)
 // MODE 1: collect candidates of ambiguous points (score <= thr)
+//
+// Software pipeline over "slots" (one centroid tile x one point tile = KS MFMAs): the
+// epilogue of the previous slot is cut into KS slices, slice s issued right behind
+// MFMA s of this slot and fenced with sched_barrier, so each MFMA's 32 cycles on the
+// matrix pipe cover ~10 VALU ops of the same wave.  Each lane keeps two top-2 chains
+// per point tile (rows 0-7 and 8-15 of its half) for instruction-level parallelism.
 template <int KS, int MODE>
 __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
@@ -204,7 +220,8 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
-    constexpr int PER_THREAD = (STAGE_U4 + 255) / 256;
+    static_assert(STAGE_U4 % 256 == 0, "stage must split evenly over the workgroup");
+    constexpr int PER_THREAD = STAGE_U4 / 256;
     __shared__ uint4 lds[2][STAGE_U4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const uint32_t tile0 = (blockIdx.x * 4 + w) * PT;
@@ -219,13 +236,20 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
             b[t][s] = __builtin_bit_cast(f16x8, q);
         }
     }
-    float m1[PT], m2[PT], th[PT];
-    uint32_t t1[PT];
+    // -inf the compiler cannot see: med3(x, s, ninf) = min(x, s) stays one v_med3 instead of
+    // being folded into v_min plus two NaN canonicalisations
+    float ninf;
+    asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(ninf));
+    float m1[PT][2], m2[PT][2], th[PT];
+    uint32_t t1[PT][2];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-        m1[t] = __builtin_inff();
-        m2[t] = __builtin_inff();
-        t1[t] = 0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            m1[t][c] = __builtin_inff();
+            m2[t][c] = __builtin_inff();
+            t1[t][c] = 0;
+        }
         th[t] = -__builtin_inff();
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -233,93 +257,143 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
         }
     }
 
-    const uint32_t nstages = (ctiles + CT_STAGE - 1) / CT_STAGE;
-    const uint32_t total_u4 = ctiles * KS * 64;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)STAGE_U4; i += 256)
-        lds[0][i] = (i < total_u4) ? cfrag[i] : make_uint4(0, 0, 0, 0);
+    // slice q of the epilogue of scores sc (point tile t, centroid tile ctile)
+    float snap[2], mn = 0.f;
+    auto slice = [&](const f32x16 &sc, int t, uint32_t ctile, auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int STEPS = 8;  // row pairs (r, r + 8)
+        constexpr int r0 = q * STEPS / KS, r1 = (q + 1) * STEPS / KS;
+        if (MODE == 0) {
+            if (q == 0) {
+                snap[0] = m1[t][0];
+                snap[1] = m1[t][1];
+            }
+#pragma unroll
+            for (int r = r0; r < r1; ++r) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float v = sc[r + 8 * c];
+                    m2[t][c] = __builtin_amdgcn_fmed3f(m1[t][c], m2[t][c], v);
+                    m1[t][c] = __builtin_amdgcn_fmed3f(m1[t][c], v, ninf);
+                }
+            }
+            if (q == KS - 1) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) t1[t][c] = (m1[t][c] < snap[c]) ? ctile : t1[t][c];
+            }
+        } else {
+            // candidates are rare (a handful of the K centroids per point): test the tile's
+            // minimum first, scan its rows only when it reaches the threshold
+            if (q == 0) mn = __builtin_inff();
+#pragma unroll
+            for (int r = r0; r < r1; ++r) {
+                mn = __builtin_amdgcn_fmed3f(mn, sc[r], ninf);
+                mn = __builtin_amdgcn_fmed3f(mn, sc[r + 8], ninf);
+            }
+            if (q == KS - 1 && mn <= th[t]) {
+                const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (sc[r] <= th[t]) {
+                        const uint32_t ci = ctile * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+                        const uint32_t pos = atomicAdd(&cand_cnt[slot], 1u);
+                        if (pos < CAND_CAP) cand[(uint64_t)slot * CAND_CAP + pos] = ci;
+                    }
+                }
+            }
+        }
+    };
+
+    // ctiles is a multiple of CT_STAGE (the tail is padded with never-winning rows)
+    const uint32_t nstages = ctiles / CT_STAGE;
+#pragma unroll
+    for (int q = 0; q < PER_THREAD; ++q) lds[0][threadIdx.x + q * 256] = cfrag[threadIdx.x + q * 256];
     __syncthreads();
+    // one score buffer per point tile: slot t of a centroid tile writes buf[t] while the
+    // epilogue drains buf[(t + 1) % PT], written PT - 1 slots earlier -- long enough for
+    // the MFMA results to have landed, so the VALU never waits on the matrix pipe
+    static_assert(PT == 4, "the score-buffer rotation assumes 4 point tiles per wave");
+    f32x16 buf[PT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) buf[t][r] = __builtin_inff();  // no-op slots before the first
+    uint32_t tile_prev = 0;  // centroid tile of the previous ct iteration
     for (uint32_t sg = 0; sg < nstages; ++sg) {
         const int cur = sg & 1;
         uint4 nxt[PER_THREAD];
         const uint32_t nbase = (sg + 1) * STAGE_U4;
 #pragma unroll
-        for (int q = 0; q < PER_THREAD; ++q) {
-            const uint32_t i = threadIdx.x + q * 256;
-            nxt[q] = (sg + 1 < nstages && i < (uint32_t)STAGE_U4 && nbase + i < total_u4) ? cfrag[nbase + i]
-                                                                                          : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll 2
-        for (int ct = 0; ct < CT_STAGE; ++ct) {
-            const uint32_t ctile = sg * CT_STAGE + ct;
-            f32x16 acc[PT];
+        for (int q = 0; q < PER_THREAD; ++q)
+            nxt[q] = (sg + 1 < nstages) ? cfrag[nbase + threadIdx.x + q * 256] : make_uint4(0, 0, 0, 0);
+        // A fragments ping-pong between two register sets: tile ct + 1 is read from LDS while
+        // tile ct's MFMAs run (the read at the stage's last tile re-reads it, unused)
+        f16x8 a0[KS], a1[KS];
 #pragma unroll
-            for (int t = 0; t < PT; ++t) acc[t] = f32x16{};
+        for (int s = 0; s < KS; ++s) a0[s] = __builtin_bit_cast(f16x8, lds[cur][s * 64 + lane]);
+        auto tile_step = [&](uint32_t ct, f16x8 (&a)[KS], f16x8 (&an)[KS]) {
+            const uint32_t tile_cur = sg * CT_STAGE + ct;
+            const uint32_t ctn = (ct + 1 < (uint32_t)CT_STAGE) ? ct + 1 : ct;
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const f16x8 a = __builtin_bit_cast(f16x8, lds[cur][(ct * KS + s) * 64 + lane]);
-#pragma unroll
-                for (int t = 0; t < PT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[t][s], acc[t], 0, 0, 0);
-            }
-            if (ctile < ctiles) {
-#pragma unroll
-                for (int t = 0; t < PT; ++t) {
-                    if (MODE == 0) {
-                        const float before = m1[t];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            // score with the row id r in its 4 low mantissa bits.  NB: read the vector
-                            // element by value first: __builtin_bit_cast on an ext_vector element
-                            // lvalue silently reads element 0 (hipcc / ROCm 7.2).
-                            const float sc = acc[t][r];
-                            const float key = __uint_as_float((__float_as_uint(sc) & ~0xFu) | (uint32_t)r);
-                            m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], key);
-                            m1[t] = fminf(m1[t], key);
-                        }
-                        t1[t] = (m1[t] < before) ? ctile : t1[t];
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            if (acc[t][r] <= th[t]) {
-                                const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
-                                const uint32_t ci = ctile * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
-                                const uint32_t pos = atomicAdd(&cand_cnt[slot], 1u);
-                                if (pos < CAND_CAP) cand[(uint64_t)slot * CAND_CAP + pos] = ci;
-                            }
-                        }
-                    }
-                }
-            }
+            for (int s = 0; s < KS; ++s) an[s] = __builtin_bit_cast(f16x8, lds[cur][(ctn * KS + s) * 64 + lane]);
+            static_for<PT>([&](auto tc_) {
+                constexpr int t = decltype(tc_)::value;
+                constexpr int td = (t + 1) % PT;  // point tile whose scores drain in this slot
+                const uint32_t tile_d = (td > t) ? tile_prev : tile_cur;
+                f32x16 acc = {};
+                static_for<KS>([&](auto sc_) {
+                    constexpr int s = decltype(sc_)::value;
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], b[t][s], acc, 0, 0, 0);
+                    slice(buf[td], td, tile_d, sc_);
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+                buf[t] = acc;
+            });
+            tile_prev = tile_cur;
+        };
+        static_assert(CT_STAGE % 2 == 0, "ping-pong over pairs of centroid tiles");
+#pragma unroll 1
+        for (uint32_t ct = 0; ct < (uint32_t)CT_STAGE; ct += 2) {
+            tile_step(ct, a0, a1);
+            tile_step(ct + 1, a1, a0);
         }
         if (sg + 1 < nstages) {
             __syncthreads();
 #pragma unroll
-            for (int q = 0; q < PER_THREAD; ++q) {
-                const uint32_t i = threadIdx.x + q * 256;
-                if (i < (uint32_t)STAGE_U4) lds[cur ^ 1][i] = nxt[q];
-            }
+            for (int q = 0; q < PER_THREAD; ++q) lds[cur ^ 1][threadIdx.x + q * 256] = nxt[q];
             __syncthreads();
         }
     }
+    // drain the last centroid tile's slots 1..PT-1 (slot 0 drained in slot PT-1)
+    static_for<PT - 1>([&](auto tc_) {
+        constexpr int td = decltype(tc_)::value + 1;
+        static_for<KS>([&](auto sc_) { slice(buf[td], td, tile_prev, sc_); });
+    });
     if (MODE == 1) return;
 
     const float cm = __builtin_bit_cast(float, *cmax_bits);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-        const uint32_t rid = __builtin_bit_cast(uint32_t, m1[t]) & 0xFu;
-        const uint32_t i1 = t1[t] * 32 + 4 * h + (rid & 3) + 8 * (rid >> 2);
-        const float om1 = __shfl_xor(m1[t], 32, 64), om2 = __shfl_xor(m2[t], 32, 64);
-        const uint32_t oi1 = __shfl_xor(i1, 32, 64);
-        const float nm1 = fminf(m1[t], om1);
-        const float nm2 = fminf(fmaxf(m1[t], om1), fminf(m2[t], om2));
-        const uint32_t ni1 = (m1[t] <= om1) ? i1 : oi1;
+        // merge the two chains of this lane-half, then the two halves of the point
+        const float a1 = m1[t][0], b1 = m1[t][1];
+        const float hm1 = fminf(a1, b1);
+        const float hm2 = fminf(fmaxf(a1, b1), fminf(m2[t][0], m2[t][1]));
+        // code = (tile, lane-half, chain) of the minimum; k_fixrow scans that chain's 8 rows
+        const uint32_t hcode = (a1 <= b1) ? (t1[t][0] * 4u + 2u * (uint32_t)h) : (t1[t][1] * 4u + 2u * (uint32_t)h + 1u);
+        const float om1 = __shfl_xor(hm1, 32, 64), om2 = __shfl_xor(hm2, 32, 64);
+        const uint32_t ocode = __shfl_xor(hcode, 32, 64);
+        const float nm1 = fminf(hm1, om1);
+        const float nm2 = fminf(fmaxf(hm1, om1), fminf(hm2, om2));
+        const uint32_t code = (hm1 <= om1) ? hcode : ocode;
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
         bool is_amb = false;
         if (h == 0 && p < npts) {
             const float W = wbound(bnd, pnorm[p], cm);
             if (nm2 > nm1 + W) {
-                labels[p] = ni1;
+                labels[p] = code;  // k_fixrow turns the code into the centroid index
             } else {
                 is_amb = true;
+                labels[p] = 0xffffffffu;
                 thr[p] = nm1 + W;
             }
         }
@@ -362,6 +436,33 @@ __device__ inline double ref_dist(const float *__restrict__ cen, int k, uint32_t
         l += v * v;
     }
     return l;
+}
+
+// decided points: the sweep left (tile, lane-half, chain) of the minimum in labels[p];
+// 8 lanes per point take the exact f64 distance of that chain's 8 rows and keep the
+// argmin.  The margin m2 > m1 + W_p covers both the MFMA and the reference rounding,
+// so the minimum is strict and equals the one the reference's KdTree returns.
+__global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float *__restrict__ cen,
+                                                int k, uint32_t n, uint32_t *__restrict__ labels) {
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+    const int j = threadIdx.x & 7;
+    if (p >= n) return;  // uniform per 8-lane group
+    const uint32_t code = labels[p];
+    if (code == 0xffffffffu) return;  // ambiguous: k_exact decides
+    const int r = 8 * (int)(code & 1) + j;  // accumulator register of the chain
+    const uint32_t c = (code >> 2) * 32 + 4 * ((code >> 1) & 1) + (r & 3) + 8 * (r >> 2);
+    double best = (c < (uint32_t)k) ? ref_dist(cen, k, c, aos + p * d, d) : __builtin_inf();
+    uint32_t bidx = c;
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o, 64);
+        const uint32_t oi = __shfl_xor(bidx, o, 64);
+        if (ob < best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+    }
+    if (j == 0) labels[p] = bidx;
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
@@ -499,9 +600,10 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
     const int ks = kp_of(d) / 16;
     const uint32_t ntiles = (uint32_t)((n + 31) / 32);
-    const uint32_t ctiles = (uint32_t)((k + 31) / 32);
+    // centroid tiles, padded to whole LDS stages with rows that can never win (k_centroid_frags)
+    const uint32_t ctiles = (uint32_t)(((k + 31) / 32 + CT_STAGE - 1) / CT_STAGE * CT_STAGE);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
-    auto *cfrag = wsT<uint4>(c, "kn.cfrag", ((size_t)ctiles + CT_STAGE) * ks * 64);
+    auto *cfrag = wsT<uint4>(c, "kn.cfrag", (size_t)ctiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
     auto *thr = wsT<float>(c, "kn.thr", n);
@@ -537,6 +639,12 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
         ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
                                             thr, amb, dstate)));
+        {
+            KTimer kt(c, "kn.fixrow");
+            hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 8 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cen,
+                               k, (uint32_t)n, labels);
+            ST_LAUNCH_CHECK();
+        }
         mark(c, "kn.assign");
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
@@ -588,3 +696,4 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
 }
 
 }  // namespace st
+

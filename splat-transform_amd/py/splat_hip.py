@@ -13,7 +13,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, 'lib', 'libsplat_hip.so')
+# ST_LIB overrides the library path (kernel-variant experiments under tools/)
+LIB_PATH = os.environ.get('ST_LIB') or os.path.join(PKG, 'lib', 'libsplat_hip.so')
 
 ST_OK = 0
 _lib = None
