@@ -30,7 +30,6 @@
 #include <cmath>
 #include <utility>
 
-#include "st_jsmath.h"
 #include "st_kmeans.h"
 
 namespace st {
@@ -240,16 +239,14 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     // being folded into v_min plus two NaN canonicalisations
     float ninf;
     asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(ninf));
-    float m1[PT][2], m2[PT][2], th[PT];
-    uint32_t t1[PT][2];
+    // per point tile: top-2 of the tile minima seen by this lane-half, and the tile of the best
+    float m1[PT], m2[PT], th[PT];
+    uint32_t t1[PT];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            m1[t][c] = __builtin_inff();
-            m2[t][c] = __builtin_inff();
-            t1[t][c] = 0;
-        }
+        m1[t] = __builtin_inff();
+        m2[t] = __builtin_inff();
+        t1[t] = 0;
         th[t] = -__builtin_inff();
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -257,40 +254,24 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
         }
     }
 
-    // slice q of the epilogue of scores sc (point tile t, centroid tile ctile)
-    float snap[2], mn = 0.f;
+    // slice q of the epilogue of scores sc (point tile t, centroid tile ctile): the minimum
+    // of the lane-half's 16 rows (v_min3 tree), then, in the last slice, the running top-2
+    // of tile minima.  Two rows of one tile never compete here: k_fixrow settles the
+    // winning tile's rows with the exact distance.
+    float mn = 0.f;
     auto slice = [&](const f32x16 &sc, int t, uint32_t ctile, auto qc) {
         constexpr int q = decltype(qc)::value;
-        constexpr int STEPS = 8;  // row pairs (r, r + 8)
-        constexpr int r0 = q * STEPS / KS, r1 = (q + 1) * STEPS / KS;
-        if (MODE == 0) {
-            if (q == 0) {
-                snap[0] = m1[t][0];
-                snap[1] = m1[t][1];
-            }
+        constexpr int r0 = q * 16 / KS, r1 = (q + 1) * 16 / KS;
+        if (q == 0) mn = sc[0];
 #pragma unroll
-            for (int r = r0; r < r1; ++r) {
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const float v = sc[r + 8 * c];
-                    m2[t][c] = __builtin_amdgcn_fmed3f(m1[t][c], m2[t][c], v);
-                    m1[t][c] = __builtin_amdgcn_fmed3f(m1[t][c], v, ninf);
-                }
-            }
-            if (q == KS - 1) {
-#pragma unroll
-                for (int c = 0; c < 2; ++c) t1[t][c] = (m1[t][c] < snap[c]) ? ctile : t1[t][c];
-            }
-        } else {
-            // candidates are rare (a handful of the K centroids per point): test the tile's
-            // minimum first, scan its rows only when it reaches the threshold
-            if (q == 0) mn = __builtin_inff();
-#pragma unroll
-            for (int r = r0; r < r1; ++r) {
-                mn = __builtin_amdgcn_fmed3f(mn, sc[r], ninf);
-                mn = __builtin_amdgcn_fmed3f(mn, sc[r + 8], ninf);
-            }
-            if (q == KS - 1 && mn <= th[t]) {
+        for (int r = (q == 0 ? 1 : r0); r < r1; ++r) mn = fminf(mn, sc[r]);
+        if (q == KS - 1) {
+            if (MODE == 0) {
+                m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], mn);
+                t1[t] = (mn < m1[t]) ? ctile : t1[t];
+                m1[t] = fminf(m1[t], mn);
+            } else if (mn <= th[t]) {
+                // candidates are rare (a handful of the K centroids per point)
                 const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -374,17 +355,12 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     const float cm = __builtin_bit_cast(float, *cmax_bits);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-        // merge the two chains of this lane-half, then the two halves of the point
-        const float a1 = m1[t][0], b1 = m1[t][1];
-        const float hm1 = fminf(a1, b1);
-        const float hm2 = fminf(fmaxf(a1, b1), fminf(m2[t][0], m2[t][1]));
-        // code = (tile, lane-half, chain) of the minimum; k_fixrow scans that chain's 8 rows
-        const uint32_t hcode = (a1 <= b1) ? (t1[t][0] * 4u + 2u * (uint32_t)h) : (t1[t][1] * 4u + 2u * (uint32_t)h + 1u);
-        const float om1 = __shfl_xor(hm1, 32, 64), om2 = __shfl_xor(hm2, 32, 64);
-        const uint32_t ocode = __shfl_xor(hcode, 32, 64);
-        const float nm1 = fminf(hm1, om1);
-        const float nm2 = fminf(fmaxf(hm1, om1), fminf(hm2, om2));
-        const uint32_t code = (hm1 <= om1) ? hcode : ocode;
+        // merge the two lane-halves of the point; code = (tile, lane-half) of the minimum
+        const float om1 = __shfl_xor(m1[t], 32, 64), om2 = __shfl_xor(m2[t], 32, 64);
+        const uint32_t ot1 = __shfl_xor(t1[t], 32, 64);
+        const float nm1 = fminf(m1[t], om1);
+        const float nm2 = fminf(fmaxf(m1[t], om1), fminf(m2[t], om2));
+        const uint32_t code = (m1[t] <= om1) ? (t1[t] * 2u + (uint32_t)h) : (ot1 * 2u + (uint32_t)(h ^ 1));
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
         bool is_amb = false;
         if (h == 0 && p < npts) {
@@ -438,23 +414,25 @@ __device__ inline double ref_dist(const float *__restrict__ cen, int k, uint32_t
     return l;
 }
 
-// decided points: the sweep left (tile, lane-half, chain) of the minimum in labels[p];
-// 8 lanes per point take the exact f64 distance of that chain's 8 rows and keep the
-// argmin.  The margin m2 > m1 + W_p covers both the MFMA and the reference rounding,
-// so the minimum is strict and equals the one the reference's KdTree returns.
+// decided points: the sweep left (tile, lane-half) of the minimum in labels[p]; every
+// other tile's rows score above m1 + W_p, so their reference distances exceed that of
+// the best row, and the argmin lies among this lane-half's 16 rows.  16 lanes per point
+// take the exact f64 distance of kd-tree.ts:26-35 for those rows; a unique minimum is
+// the reference's answer, an exact tie goes to the KdTree walk (kd_resolve_ties).
 __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float *__restrict__ cen,
-                                                int k, uint32_t n, uint32_t *__restrict__ labels) {
-    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
-    const int j = threadIdx.x & 7;
-    if (p >= n) return;  // uniform per 8-lane group
+                                                int k, uint32_t n, uint32_t *__restrict__ labels,
+                                                uint32_t *__restrict__ ties, State *st) {
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int r = threadIdx.x & 15;
+    if (p >= n) return;  // uniform per 16-lane group
     const uint32_t code = labels[p];
     if (code == 0xffffffffu) return;  // ambiguous: k_exact decides
-    const int r = 8 * (int)(code & 1) + j;  // accumulator register of the chain
-    const uint32_t c = (code >> 2) * 32 + 4 * ((code >> 1) & 1) + (r & 3) + 8 * (r >> 2);
-    double best = (c < (uint32_t)k) ? ref_dist(cen, k, c, aos + p * d, d) : __builtin_inf();
+    const uint32_t c = (code >> 1) * 32 + 4 * (code & 1) + (r & 3) + 8 * (r >> 2);
+    const double mine = (c < (uint32_t)k) ? ref_dist(cen, k, c, aos + p * d, d) : __builtin_inf();
+    double best = mine;
     uint32_t bidx = c;
 #pragma unroll
-    for (int o = 4; o > 0; o >>= 1) {
+    for (int o = 8; o > 0; o >>= 1) {
         const double ob = __shfl_xor(best, o, 64);
         const uint32_t oi = __shfl_xor(bidx, o, 64);
         if (ob < best || (ob == best && oi < bidx)) {
@@ -462,7 +440,14 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
             bidx = oi;
         }
     }
-    if (j == 0) labels[p] = bidx;
+    const uint32_t eq = (mine == best) ? 1u : 0u;
+    uint32_t cnt = eq;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (r == 0) {
+        labels[p] = bidx;  // provisional on a tie; the KdTree pass decides
+        if (cnt > 1) ties[atomicAdd(&st->ties, 1u)] = (uint32_t)p;
+    }
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
@@ -641,8 +626,8 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
                                             thr, amb, dstate)));
         {
             KTimer kt(c, "kn.fixrow");
-            hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 8 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cen,
-                               k, (uint32_t)n, labels);
+            hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d,
+                               cen, k, (uint32_t)n, labels, ties, dstate);
             ST_LAUNCH_CHECK();
         }
         mark(c, "kn.assign");
@@ -680,8 +665,9 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
                         it, (unsigned long long)n, k, namb, h->ties, h->overflow, sigma,
                         __builtin_bit_cast(float, cmb), pn0, thr0, bnd.a, bnd.b, bnd.ec, bnd.ep);
             }
-            if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
         }
+        // exact ties from k_fixrow and k_exact: the KdTree walk decides
+        if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
         mark(c, "kn.exact");
         // update
         member_sort(c, labels, n, k, sorted_labels, members, start);
