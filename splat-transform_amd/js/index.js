@@ -1,0 +1,189 @@
+'use strict';
+// splat-hip host module: the reference's hot-path functions, same names,
+// argument meaning and in-place mutation, executed on MI355X through the N-API
+// addon (../napi/addon.c) over the C-ABI (include/st_abi.h).  Plain JS for
+// Node >= 12 (no `??`, no `?.`).  A DataTable is anything shaped like the
+// reference's (src/data-table.ts:5-150): {columns: [{name, data}], numRows,
+// getColumnByName(name), hasColumn(name)}; the Column/DataTable classes below
+// are a minimal stand-in for standalone use.
+//
+//   transform(dataTable, t, r, s)           transform.ts:12-65
+//   generateOrdering(dataTable, indices)    ordering.ts:4-110
+//   filterNaN(dataTable)                    process.ts:84-95 (+ filter :47-61)
+//   packCompressed(dataTable)               write-compressed-ply.ts:56-109 (the chunk loop)
+//   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
+//   cluster1d(dataTable, iterations)        write-sog.ts:56-99
+//   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
+//
+// Math.random: the device consumes the reference's draws in the reference's
+// order.  Draws are taken from Math.random up front; the ones a call did not
+// consume are kept in `pending` and served first to the next call, so the
+// process-wide stream is exactly what the reference would have consumed.
+
+const path = require('path');
+
+const addon = require(path.join(__dirname, '..', 'napi', 'build', 'addon.node'));
+
+class Column {
+    constructor(name, data) {
+        this.name = name;
+        this.data = data;
+    }
+}
+
+class DataTable {
+    constructor(columns) {
+        if (columns.length === 0) throw new Error('DataTable must have at least one column');
+        for (let i = 1; i < columns.length; ++i) {
+            if (columns[i].data.length !== columns[0].data.length) {
+                throw new Error(`Column ${columns[i].name} has a different number of rows`);
+            }
+        }
+        this.columns = columns;
+    }
+    get numRows() { return this.columns[0].data.length; }
+    get numColumns() { return this.columns.length; }
+    getColumn(i) { return this.columns[i]; }
+    getColumnByName(name) { return this.columns.find(c => c.name === name); }
+    hasColumn(name) { return this.columns.some(c => c.name === name); }
+    getColumnNames() { return this.columns.map(c => c.name); }
+}
+
+// ---- Math.random stream --------------------------------------------------------
+let pending = [];
+
+const takeDraws = (count) => {
+    const out = new Float64Array(count);
+    let i = 0;
+    for (; i < count && i < pending.length; ++i) out[i] = pending[i];
+    for (; i < count; ++i) out[i] = Math.random();
+    pending = pending.slice(Math.min(count, pending.length));
+    return out;
+};
+
+const giveBack = (draws, used) => {
+    pending = Array.from(draws.subarray(used)).concat(pending);
+};
+
+// run fn(draws) with enough draws; a short buffer (ST_ERR_DRAWS) is retried with
+// a longer one that starts with the same values, so the stream is unchanged
+const withDraws = (estimate, fn) => {
+    let count = Math.max(estimate, 64);
+    for (;;) {
+        const draws = takeDraws(count);
+        try {
+            const res = fn(draws);
+            giveBack(draws, res.used);
+            return res;
+        } catch (e) {
+            giveBack(draws, 0);
+            if (!/status -4\)/.test(e.message)) throw e;
+            count *= 2;
+        }
+    }
+};
+
+// ---- helpers ---------------------------------------------------------------------
+const f32Columns = (dataTable) => {
+    const cols = [];
+    const names = [];
+    for (const c of dataTable.columns) {
+        if (!(c.data instanceof Float32Array)) continue;
+        cols.push(c.data);
+        names.push(c.name);
+    }
+    return { cols, names };
+};
+
+const shCoeffsOf = (dataTable) => {
+    // band detection rule of transform.ts:20 / write-compressed-ply.ts:32
+    const idx = [9, 24, -1];
+    const miss = (() => {
+        for (let i = 0; i < 45; ++i) if (!dataTable.hasColumn(`f_rest_${i}`)) return i;
+        return -1;
+    })();
+    const band = idx.indexOf(miss) + 1;
+    return [0, 3, 8, 15][band];
+};
+
+// ---- the path ------------------------------------------------------------------------
+// t: {x, y, z} (Vec3), r: {x, y, z, w} (Quat), s: number -- mutates the columns in place
+const transform = (dataTable, t, r, s) => {
+    const { cols, names } = f32Columns(dataTable);
+    addon.transform(cols, names, [t.x, t.y, t.z], [r.x, r.y, r.z, r.w], s);
+};
+
+const quatFromEuler = (x, y, z) => {
+    const q = addon.quatFromEuler(x, y, z);
+    return { x: q[0], y: q[1], z: q[2], w: q[3] };
+};
+
+const generateOrdering = (dataTable, indices) => {
+    const x = dataTable.getColumnByName('x').data;
+    const y = dataTable.getColumnByName('y').data;
+    const z = dataTable.getColumnByName('z').data;
+    return addon.mortonOrder(x, y, z, indices);
+};
+
+// rows whose every column is finite, in order (filterNaN)
+const filterNaN = (dataTable) => {
+    const { cols } = f32Columns(dataTable);
+    const keep = addon.filterFinite(cols);
+    return new DataTable(dataTable.columns.map((c) => {
+        const out = new c.data.constructor(keep.length);
+        for (let i = 0; i < keep.length; ++i) out[i] = c.data[keep[i]];
+        return new Column(c.name, out);
+    }));
+};
+
+// the chunk / vertex / sh arrays writeCompressedPly writes after its header
+const packCompressed = (dataTable) => {
+    const n = dataTable.numRows;
+    const order = new Uint32Array(n);
+    for (let i = 0; i < n; ++i) order[i] = i;
+    generateOrdering(dataTable, order);
+    const { cols, names } = f32Columns(dataTable);
+    return addon.packCompressed(cols, names, order, 3 * shCoeffsOf(dataTable));
+};
+
+const kmeans = (points, k, iterations) => {
+    const cols = points.columns.map(c => c.data);
+    const n = points.numRows;
+    const res = withDraws(k * (iterations + 1) + 1024, draws => addon.kmeans(cols, k, iterations, draws));
+    const kk = Math.min(k, n);
+    const centroids = new DataTable(points.columns.map((c, i) =>
+        new Column(c.name, res.centroids.slice(i * kk, (i + 1) * kk))));
+    return Promise.resolve({ centroids, labels: res.labels });
+};
+
+const cluster1d = (dataTable, iterations) => {
+    const cols = dataTable.columns.map(c => c.data);
+    const n = dataTable.numRows;
+    const res = withDraws(256 * (iterations + 1) + 64, draws => addon.cluster1d(cols, iterations, draws));
+    const labels = new DataTable(dataTable.columns.map((c, i) =>
+        new Column(c.name, res.labels.slice(i * n, (i + 1) * n))));
+    const centroids = new DataTable([new Column('data', res.centroids)]);
+    return Promise.resolve({ centroids, labels });
+};
+
+// writeSog's device work: the seven RGBA textures and the meta.json fields
+const sogTextures = (dataTable, iterations) => {
+    const { cols, names } = f32Columns(dataTable);
+    const k = 65536;
+    return Promise.resolve(withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
+        draws => addon.sog(cols, names, iterations, draws)));
+};
+
+module.exports = {
+    Column,
+    DataTable,
+    addon,
+    transform,
+    quatFromEuler,
+    generateOrdering,
+    filterNaN,
+    packCompressed,
+    kmeans,
+    cluster1d,
+    sogTextures
+};

@@ -1,0 +1,508 @@
+/*
+ * addon.c -- N-API (v8, Node >= 12) binding of libsplat_hip.so for the
+ * reference's Node host.  Thin: it borrows the TypedArray storage of the
+ * caller's DataTable columns for the duration of one call (no copies on the
+ * JS side), forwards to the C-ABI in include/st_abi.h and turns a negative
+ * st_status into a thrown JS Error carrying st_last_error().
+ *
+ * Exports (js/index.js wraps them in the reference's signatures):
+ *   version() -> number                       st_abi_version
+ *   deviceCount() -> number                   st_device_count
+ *   transform(cols, names, t[3], r[4], s)     st_transform_params_make + st_transform
+ *                                             (transform.ts:12-65)
+ *   quatFromEuler(ex, ey, ez) -> [x,y,z,w]    Quat.setFromEulerAngles (process.ts:75-79)
+ *   filterFinite(cols) -> Uint32Array         filterNaN's row predicate (process.ts:84-95)
+ *   mortonOrder(x, y, z, indices)             generateOrdering (ordering.ts:4-110), in place
+ *   packCompressed(cols, names, order, nsh)   writeCompressedPly chunk loop
+ *        -> {chunk, vertex, sh}               (write-compressed-ply.ts:56-109)
+ *   kmeans(cols, k, iters, draws)             kmeans --no-gpu (k-means.ts:137-201)
+ *        -> {centroids, labels, used}
+ *   cluster1d(cols, iters, draws)             cluster1d (write-sog.ts:56-99)
+ *        -> {centroids, labels, used}
+ *   sog(cols, names, iters, draws)            writeSog textures + meta (write-sog.ts:110-370)
+ *        -> {meta fields, textures, used}
+ */
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "st_abi.h"
+
+static st_ctx *g_ctx = NULL;
+
+#define NAPI_OK(call)                                                   \
+    do {                                                                \
+        if ((call) != napi_ok) {                                        \
+            napi_throw_error(env, NULL, "splat-hip: N-API call failed"); \
+            goto fail;                                                  \
+        }                                                               \
+    } while (0)
+
+static napi_value throw_st(napi_env env, int rc) {
+    char buf[600];
+    snprintf(buf, sizeof buf, "splat-hip: %s (status %d)", st_last_error(), rc);
+    napi_throw_error(env, NULL, buf);
+    return NULL;
+}
+
+static int get_ctx(napi_env env, st_ctx **out) {
+    if (!g_ctx) {
+        int rc = st_ctx_create(0, &g_ctx);
+        if (rc != ST_OK) {
+            g_ctx = NULL;
+            throw_st(env, rc);
+            return 0;
+        }
+    }
+    *out = g_ctx;
+    return 1;
+}
+
+/* TypedArray storage of `v`; type-checked */
+static void *ta_data(napi_env env, napi_value v, napi_typedarray_type want, size_t *len) {
+    bool is_ta = false;
+    napi_typedarray_type type;
+    size_t length = 0, off = 0;
+    void *data = NULL;
+    napi_value ab;
+    if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta ||
+        napi_get_typedarray_info(env, v, &type, &length, &data, &ab, &off) != napi_ok || type != want) {
+        napi_throw_type_error(env, NULL, "splat-hip: wrong TypedArray type");
+        return NULL;
+    }
+    if (len) *len = length;
+    return data;
+}
+
+static double num(napi_env env, napi_value v) {
+    double d = 0;
+    napi_get_value_double(env, v, &d);
+    return d;
+}
+
+/* array of Float32Array -> float* list (caller frees); n = common length */
+static float **f32_list(napi_env env, napi_value arr, uint32_t *count, uint64_t *n) {
+    uint32_t m = 0;
+    if (napi_get_array_length(env, arr, &m) != napi_ok) {
+        napi_throw_type_error(env, NULL, "splat-hip: expected an array of Float32Array columns");
+        return NULL;
+    }
+    float **p = (float **)calloc(m ? m : 1, sizeof(float *));
+    *n = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        napi_value e;
+        size_t len = 0;
+        napi_get_element(env, arr, i, &e);
+        p[i] = (float *)ta_data(env, e, napi_float32_array, &len);
+        if (!p[i]) {
+            free(p);
+            return NULL;
+        }
+        if (i == 0) *n = len;
+        else if (len != *n) {
+            free(p);
+            napi_throw_range_error(env, NULL, "splat-hip: columns differ in length");
+            return NULL;
+        }
+    }
+    *count = m;
+    return p;
+}
+
+static char **str_list(napi_env env, napi_value arr, uint32_t m) {
+    char **s = (char **)calloc(m ? m : 1, sizeof(char *));
+    for (uint32_t i = 0; i < m; ++i) {
+        napi_value e;
+        size_t len = 0;
+        napi_get_element(env, arr, i, &e);
+        napi_get_value_string_utf8(env, e, NULL, 0, &len);
+        s[i] = (char *)malloc(len + 1);
+        napi_get_value_string_utf8(env, e, s[i], len + 1, &len);
+    }
+    return s;
+}
+
+static void free_strs(char **s, uint32_t m) {
+    if (!s) return;
+    for (uint32_t i = 0; i < m; ++i) free(s[i]);
+    free(s);
+}
+
+static napi_value new_typed(napi_env env, napi_typedarray_type type, size_t elems, size_t esize, void **data) {
+    napi_value ab, ta;
+    if (napi_create_arraybuffer(env, elems * esize, data, &ab) != napi_ok) return NULL;
+    if (napi_create_typedarray(env, type, elems, ab, 0, &ta) != napi_ok) return NULL;
+    return ta;
+}
+
+static void set_named(napi_env env, napi_value obj, const char *k, napi_value v) {
+    napi_set_named_property(env, obj, k, v);
+}
+
+static napi_value make_num(napi_env env, double d) {
+    napi_value v;
+    napi_create_double(env, d, &v);
+    return v;
+}
+
+/* ---- exports -------------------------------------------------------------- */
+static napi_value js_version(napi_env env, napi_callback_info info) {
+    (void)info;
+    return make_num(env, st_abi_version());
+}
+
+static napi_value js_device_count(napi_env env, napi_callback_info info) {
+    (void)info;
+    int32_t n = 0;
+    if (st_device_count(&n) != ST_OK) n = 0;
+    return make_num(env, n);
+}
+
+static napi_value js_quat_from_euler(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out;
+    double q[4];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    st_quat_from_euler(num(env, argv[0]), num(env, argv[1]), num(env, argv[2]), q);
+    NAPI_OK(napi_create_array_with_length(env, 4, &out));
+    for (uint32_t i = 0; i < 4; ++i) napi_set_element(env, out, i, make_num(env, q[i]));
+    return out;
+fail:
+    return NULL;
+}
+
+/* transform(cols, names, t[3], r[4], s): mutates the Float32Array columns in place */
+static napi_value js_transform(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5], e;
+    uint32_t m = 0;
+    uint64_t n = 0;
+    float **cols = NULL;
+    char **names = NULL;
+    st_ctx *ctx;
+    double t[3], r[4];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    names = str_list(env, argv[1], m);
+    for (uint32_t i = 0; i < 3; ++i) {
+        napi_get_element(env, argv[2], i, &e);
+        t[i] = num(env, e);
+    }
+    for (uint32_t i = 0; i < 4; ++i) {
+        napi_get_element(env, argv[3], i, &e);
+        r[i] = num(env, e);
+    }
+    {
+        st_transform_params p;
+        st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+        int rc = st_transform_params_make(t, r, num(env, argv[4]), &p);
+        if (rc == ST_OK && get_ctx(env, &ctx)) rc = st_transform(ctx, &tab, &p);
+        else if (rc == ST_OK) goto fail;
+        free(cols);
+        free_strs(names, m);
+        if (rc != ST_OK) return throw_st(env, rc);
+    }
+    return NULL;
+fail:
+    free(cols);
+    free_strs(names, m);
+    return NULL;
+}
+
+static napi_value js_filter_finite(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out;
+    uint32_t m = 0;
+    uint64_t n = 0, kept = 0;
+    float **cols;
+    st_ctx *ctx;
+    void *buf;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    {
+        uint32_t *idx = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+        st_table tab = {n, (int32_t)m, NULL, cols};
+        int rc = get_ctx(env, &ctx) ? st_filter_finite(ctx, &tab, idx, &kept) : 1;
+        free(cols);
+        if (rc != ST_OK) {
+            free(idx);
+            return rc == 1 ? NULL : throw_st(env, rc);
+        }
+        out = new_typed(env, napi_uint32_array, kept, 4, &buf);
+        memcpy(buf, idx, kept * 4);
+        free(idx);
+    }
+    return out;
+fail:
+    return NULL;
+}
+
+/* mortonOrder(x, y, z, indices): reorders `indices` in place, returns it */
+static napi_value js_morton(napi_env env, napi_callback_info info) {
+    size_t argc = 4, nx = 0, ny = 0, nz = 0, ni = 0;
+    napi_value argv[4];
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    {
+        float *x = (float *)ta_data(env, argv[0], napi_float32_array, &nx);
+        float *y = (float *)ta_data(env, argv[1], napi_float32_array, &ny);
+        float *z = (float *)ta_data(env, argv[2], napi_float32_array, &nz);
+        uint32_t *idx = (uint32_t *)ta_data(env, argv[3], napi_uint32_array, &ni);
+        if (!x || !y || !z || !idx) return NULL;
+        if (nx != ny || nx != nz || ni != nx) {
+            /* writeCompressedPly / writeSog order all rows (write-compressed-ply.ts:61-65, write-sog.ts:42-49) */
+            napi_throw_range_error(env, NULL, "splat-hip: x/y/z/indices lengths differ");
+            return NULL;
+        }
+        if (!get_ctx(env, &ctx)) return NULL;
+        int rc = st_morton_order(ctx, x, y, z, idx, (uint64_t)ni);
+        if (rc != ST_OK) return throw_st(env, rc);
+    }
+    return argv[3];
+fail:
+    return NULL;
+}
+
+static napi_value js_pack_compressed(napi_env env, napi_callback_info info) {
+    size_t argc = 4, no = 0;
+    napi_value argv[4], out;
+    uint32_t m = 0;
+    uint64_t n = 0;
+    float **cols = NULL;
+    char **names = NULL;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    names = str_list(env, argv[1], m);
+    {
+        uint32_t *order = (uint32_t *)ta_data(env, argv[2], napi_uint32_array, &no);
+        int32_t nsh = (int32_t)num(env, argv[3]);
+        void *chunk, *vertex, *sh;
+        const uint64_t nch = (no + 255) / 256;
+        napi_value tch, tvx, tsh;
+        if (!order) goto fail;
+        if (no != n) {
+            napi_throw_range_error(env, NULL, "splat-hip: order must name every row");
+            goto fail;
+        }
+        tch = new_typed(env, napi_float32_array, nch * 18, 4, &chunk);
+        tvx = new_typed(env, napi_uint32_array, no * 4, 4, &vertex);
+        tsh = new_typed(env, napi_uint8_array, no * (uint64_t)nsh, 1, &sh);
+        if (!get_ctx(env, &ctx)) goto fail;
+        {
+            st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+            int rc = st_pack_compressed(ctx, &tab, order, (float *)chunk, (uint32_t *)vertex, (uint8_t *)sh);
+            if (rc != ST_OK) {
+                free(cols);
+                free_strs(names, m);
+                return throw_st(env, rc);
+            }
+        }
+        NAPI_OK(napi_create_object(env, &out));
+        set_named(env, out, "chunk", tch);
+        set_named(env, out, "vertex", tvx);
+        set_named(env, out, "sh", tsh);
+    }
+    free(cols);
+    free_strs(names, m);
+    return out;
+fail:
+    free(cols);
+    free_strs(names, m);
+    return NULL;
+}
+
+static napi_value js_kmeans(napi_env env, napi_callback_info info) {
+    size_t argc = 4, nd = 0;
+    napi_value argv[4], out;
+    uint32_t d = 0;
+    uint64_t n = 0, used = 0;
+    float **cols;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &d, &n))) return NULL;
+    {
+        const int32_t k = (int32_t)num(env, argv[1]), iters = (int32_t)num(env, argv[2]);
+        double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);
+        const uint64_t kk = (uint64_t)k < n ? (uint64_t)k : n;
+        void *cen, *lab;
+        napi_value tc, tl;
+        if (!draws) {
+            free(cols);
+            return NULL;
+        }
+        tc = new_typed(env, napi_float32_array, kk * d, 4, &cen);
+        tl = new_typed(env, napi_uint32_array, n, 4, &lab);
+        if (!get_ctx(env, &ctx)) {
+            free(cols);
+            return NULL;
+        }
+        int rc = st_kmeans(ctx, (const float *const *)cols, (int32_t)d, n, k, iters, draws, nd, &used, (float *)cen,
+                           (uint32_t *)lab);
+        free(cols);
+        if (rc != ST_OK) return throw_st(env, rc);
+        NAPI_OK(napi_create_object(env, &out));
+        set_named(env, out, "centroids", tc); /* column-major: d columns of kk values */
+        set_named(env, out, "labels", tl);
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    return out;
+fail:
+    return NULL;
+}
+
+static napi_value js_cluster1d(napi_env env, napi_callback_info info) {
+    size_t argc = 3, nd = 0;
+    napi_value argv[3], out;
+    uint32_t m = 0;
+    uint64_t n = 0, used = 0;
+    float **cols;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    {
+        const int32_t iters = (int32_t)num(env, argv[1]);
+        double *draws = (double *)ta_data(env, argv[2], napi_float64_array, &nd);
+        void *cen, *lab;
+        napi_value tc, tl;
+        if (!draws) {
+            free(cols);
+            return NULL;
+        }
+        tc = new_typed(env, napi_float32_array, 256, 4, &cen);
+        tl = new_typed(env, napi_uint8_array, n * m, 1, &lab);
+        if (!get_ctx(env, &ctx)) {
+            free(cols);
+            return NULL;
+        }
+        int rc = st_cluster1d(ctx, (const float *const *)cols, (int32_t)m, n, iters, draws, nd, &used, (float *)cen,
+                              (uint8_t *)lab);
+        free(cols);
+        if (rc != ST_OK) return throw_st(env, rc);
+        NAPI_OK(napi_create_object(env, &out));
+        set_named(env, out, "centroids", tc);
+        set_named(env, out, "labels", tl); /* m column blocks of n bytes */
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    return out;
+fail:
+    return NULL;
+}
+
+static napi_value f32_copy(napi_env env, const float *src, size_t n) {
+    void *d;
+    napi_value v = new_typed(env, napi_float32_array, n, 4, &d);
+    memcpy(d, src, n * 4);
+    return v;
+}
+
+static napi_value js_sog(napi_env env, napi_callback_info info) {
+    size_t argc = 4, nd = 0;
+    napi_value argv[4], out, tex;
+    uint32_t m = 0;
+    uint64_t n = 0, used = 0;
+    float **cols = NULL;
+    char **names = NULL;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    names = str_list(env, argv[1], m);
+    {
+        const int32_t iters = (int32_t)num(env, argv[2]);
+        double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);
+        int32_t W = 0, H = 0, pal = 0, cw = 0, ch = 0, sh = 0;
+        st_sog_meta meta;
+        st_sog_textures t;
+        void *p[7];
+        napi_value tv[7];
+        static const char *tn[7] = {"means_l", "means_u", "quats", "scales", "sh0", "shN_centroids", "shN_labels"};
+        if (!draws) goto fail;
+        for (uint32_t i = 0; i < m; ++i)
+            if (strcmp(names[i], "f_rest_44") == 0) sh = 15;
+            else if (strcmp(names[i], "f_rest_23") == 0 && sh < 8) sh = 8;
+            else if (strcmp(names[i], "f_rest_8") == 0 && sh < 3) sh = 3;
+        if (st_sog_geometry(n, sh, &W, &H, &pal, &cw, &ch) != ST_OK) {
+            napi_throw_range_error(env, NULL, "splat-hip: empty table");
+            goto fail;
+        }
+        for (int i = 0; i < 7; ++i) {
+            const size_t bytes = (i == 5) ? (size_t)cw * ch * 4 : (size_t)W * H * 4;
+            tv[i] = new_typed(env, napi_uint8_array, bytes, 1, &p[i]);
+        }
+        t.means_l = (uint8_t *)p[0];
+        t.means_u = (uint8_t *)p[1];
+        t.quats = (uint8_t *)p[2];
+        t.scales = (uint8_t *)p[3];
+        t.sh0 = (uint8_t *)p[4];
+        t.shn_centroids = cw ? (uint8_t *)p[5] : NULL;
+        t.shn_labels = cw ? (uint8_t *)p[6] : NULL;
+        if (!get_ctx(env, &ctx)) goto fail;
+        {
+            st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+            int rc = st_sog(ctx, &tab, iters, draws, nd, &used, &meta, &t);
+            if (rc != ST_OK) {
+                free(cols);
+                free_strs(names, m);
+                return throw_st(env, rc);
+            }
+        }
+        NAPI_OK(napi_create_object(env, &out));
+        NAPI_OK(napi_create_object(env, &tex));
+        for (int i = 0; i < 7; ++i)
+            if (i < 5 || cw) set_named(env, tex, tn[i], tv[i]);
+        set_named(env, out, "textures", tex);
+        set_named(env, out, "width", make_num(env, meta.width));
+        set_named(env, out, "height", make_num(env, meta.height));
+        {
+            napi_value mins, maxs;
+            napi_create_array_with_length(env, 3, &mins);
+            napi_create_array_with_length(env, 3, &maxs);
+            for (uint32_t i = 0; i < 3; ++i) {
+                napi_set_element(env, mins, i, make_num(env, meta.means_min[i]));
+                napi_set_element(env, maxs, i, make_num(env, meta.means_max[i]));
+            }
+            set_named(env, out, "meansMins", mins);
+            set_named(env, out, "meansMaxs", maxs);
+        }
+        set_named(env, out, "scalesCodebook", f32_copy(env, meta.scales_codebook, 256));
+        set_named(env, out, "sh0Codebook", f32_copy(env, meta.sh0_codebook, 256));
+        set_named(env, out, "shBands", make_num(env, meta.sh_bands));
+        set_named(env, out, "paletteSize", make_num(env, meta.palette_size));
+        set_named(env, out, "shNCodebook", f32_copy(env, meta.shn_codebook, 256));
+        set_named(env, out, "shNWidth", make_num(env, meta.shn_width));
+        set_named(env, out, "shNHeight", make_num(env, meta.shn_height));
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    free(cols);
+    free_strs(names, m);
+    return out;
+fail:
+    free(cols);
+    free_strs(names, m);
+    return NULL;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    static const struct {
+        const char *name;
+        napi_callback fn;
+    } fns[] = {{"version", js_version},
+               {"deviceCount", js_device_count},
+               {"quatFromEuler", js_quat_from_euler},
+               {"transform", js_transform},
+               {"filterFinite", js_filter_finite},
+               {"mortonOrder", js_morton},
+               {"packCompressed", js_pack_compressed},
+               {"kmeans", js_kmeans},
+               {"cluster1d", js_cluster1d},
+               {"sog", js_sog}};
+    for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
+        napi_value f;
+        if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok) return NULL;
+        napi_set_named_property(env, exports, fns[i].name, f);
+    }
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

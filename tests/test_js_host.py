@@ -1,0 +1,98 @@
+"""The Node host side (splat-transform_amd/js + napi/addon.node): the reference's
+function signatures over the C-ABI.  CPU: the addon loads, exports the entry
+points, and fails loudly without a GPU (no CPU fallback).  GPU: the host module
+driven like the reference's writers reproduces the oracle bit for bit."""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ADDON = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
+NODE = shutil.which('node')
+
+pytestmark = pytest.mark.skipif(NODE is None, reason='node not installed')
+
+
+@pytest.fixture(scope='module')
+def addon_built():
+    import splat_hip as sh
+    if not os.path.exists(sh.LIB_PATH):
+        sh.build()
+    if not os.path.exists(ADDON):
+        subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'splat-transform_amd', 'napi')])
+    return ADDON
+
+
+def node(script):
+    return subprocess.run([NODE, '-e', script], cwd=ROOT, capture_output=True, text=True, timeout=120)
+
+
+def test_addon_exports(addon_built):
+    r = node("const h=require('./splat-transform_amd/js'); console.log(JSON.stringify(Object.keys(h.addon).sort()),"
+             " h.addon.version())")
+    assert r.returncode == 0, r.stderr
+    keys, ver = r.stdout.strip().rsplit(' ', 1)
+    assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
+                                       'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog'])
+    assert ver == '1'
+
+
+def test_quat_from_euler_matches_oracle(addon_built):
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    r = node("const h=require('./splat-transform_amd/js'); console.log(JSON.stringify(h.quatFromEuler(10, 45, -30)))")
+    assert r.returncode == 0, r.stderr
+    q = json.loads(r.stdout)
+    want = oracle.transform_params(euler=(10, 45, -30))['quat']
+    assert [q['x'], q['y'], q['z'], q['w']] == list(want)
+
+
+@pytest.mark.skipif(os.path.exists('/dev/kfd') and os.access('/dev/kfd', os.R_OK), reason='a GPU is present')
+def test_no_cpu_fallback(addon_built):
+    r = node("const h=require('./splat-transform_amd/js'); const t=new h.DataTable([new h.Column('x', new Float32Array(4))]);"
+             " try { h.transform(t, {x:0,y:0,z:0}, {x:0,y:0,z:0,w:1}, 2); console.log('RAN') }"
+             " catch (e) { console.log('THREW ' + e.message) }")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith('THREW splat-hip:'), r.stdout
+
+
+@pytest.mark.gpu
+def test_host_roundtrip_matches_oracle(addon_built, tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    rng = np.random.default_rng(77)
+    n, k, iters, seed = 20000, 256, 2, 91
+    names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+        ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
+    cols = {c: rng.normal(0, 1, n).astype(np.float32) for c in names}
+    for i in range(45):
+        cols[f'f_rest_{i}'] *= np.float32(0.1)
+    for c in names:
+        cols[c].tofile(tmp_path / f'{c}.f32')
+    (tmp_path / 'manifest.json').write_text(json.dumps(
+        {'columns': names, 'euler': [0, 45, 0], 'k': k, 'iters': iters, 'seed': seed}))
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'host_roundtrip.js'), str(tmp_path)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+    ref = {c: v.copy() for c, v in cols.items()}
+    oracle.transform(ref, oracle.transform_params(euler=(0, 45, 0)), 15)
+    for c in names:
+        got = np.fromfile(tmp_path / f't_{c}.f32', np.float32)
+        assert np.array_equal(got.view(np.uint32), ref[c].view(np.uint32)), c
+    order = oracle.morton_order(ref['x'], ref['y'], ref['z'])
+    chunk, vertex, shb = oracle.pack_compressed(ref, order, 45)
+    assert np.array_equal(np.fromfile(tmp_path / 'chunk.f32', np.float32).view(np.uint32), chunk.view(np.uint32))
+    assert np.array_equal(np.fromfile(tmp_path / 'vertex.u32', np.uint32), vertex)
+    assert np.array_equal(np.fromfile(tmp_path / 'sh.u8', np.uint8), shb)
+    pts = [ref[f'f_rest_{i}'] for i in range(45)]
+    rc, cen, labels, used = oracle.kmeans(pts, k, iters, oracle.mulberry32(seed, 1 << 16))
+    assert rc == 0
+    assert np.array_equal(np.fromfile(tmp_path / 'labels.u32', np.uint32), labels)
+    assert np.array_equal(np.fromfile(tmp_path / 'centroids.f32', np.float32).view(np.uint32),
+                          cen.reshape(-1).view(np.uint32))
