@@ -10,8 +10,11 @@ device pipeline and is not in the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S]
 
-N > 1 is launched by torch.distributed.run: one process per GPU, each rank
-holds its own shard of S splats (weak scaling) and runs the pipeline on it.
+N > 1 is launched by torch.distributed.run: one process per GPU, each rank holds
+a shard of S splats of one N*S-splat table (weak scaling) and the job writes the
+SOG of the whole table: k-means exchanges the centroid sums over RCCL every
+iteration (exact, splat_dist.py), Morton all-gathers x/y/z, textures reduce to
+rank 0.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
 (the MFMA assign sweep, measured with HIP events on its own stream) and the
@@ -38,6 +41,8 @@ def parse():
     ap.add_argument('--splats', type=int, default=10_000_000, help='splats per GPU')
     ap.add_argument('--iters', type=int, default=10, help='k-means iterations (reference default 10)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo to '
+                    'rehearse several ranks on one GPU)')
     ap.add_argument('--cpu-assign-sample', type=int, default=1000)
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     return ap.parse_args()
@@ -119,24 +124,41 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
-        dist.init_process_group('nccl', init_method='env://')
+        dist.init_process_group(args.backend, init_method='env://')
+    local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
+    # one real stream for the library and the torch glue (st_ctx_set_stream(NULL) would select the
+    # context's own stream, and torch's legacy default stream has handle 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx = sh.Context(local)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx.set_stream(stream.cuda_stream)
     n = args.splats
     cols = synth_table(n, 1002 + rank, dev)
-    W, H, pal, cw, ch = sh.sog_geometry(n, 15)
-    u8 = dict(device=dev, dtype=torch.uint8)
-    tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
-    tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
-    # the host's Math.random stream (any uniform [0,1) doubles; the reference uses Math.random)
-    draws = np.random.default_rng(42 + rank).random(2 * 65536 * (args.iters + 2))
-    torch.cuda.synchronize()
+    # the host's Math.random stream (any uniform [0,1) doubles; the reference uses Math.random):
+    # one stream for the whole job, identical on every rank
+    draws = np.random.default_rng(42).random(2 * 65536 * (args.iters + 2))
+    W, H, pal, cw, ch = sh.sog_geometry(n * world, 15)
+    if world == 1:
+        u8 = dict(device=dev, dtype=torch.uint8)
+        tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
+        tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
 
-    def step():
-        return ctx.dev_sog(cols, args.iters, draws, tex)
+        def step():
+            return ctx.dev_sog(cols, args.iters, draws, tex)
+    else:
+        # rows sharded in rank order; kmeans/cluster1d exchange centroid sums over RCCL, Morton
+        # all-gathers x/y/z, textures reduce to rank 0 (splat_dist.py)
+        import splat_dist
+        ops = splat_dist.HipOps(ctx, dev)
+        comm = splat_dist.Comm()
+
+        def step():
+            _, _, used = splat_dist.write_sog(ops, comm, cols, args.iters, draws)
+            return None, used
+    torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -159,17 +181,19 @@ def main():
         elapsed = t.item()
     sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
     kstats = {}
-    for name in ('kn.sweep', 'kn.collect', 'kn.exact', 'kn.sumnd', 'k1.assign'):
+    for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum'):
         ms, cnt = ctx.kernel_stats(name)
         kstats[name] = {'avg_ms': ms / max(cnt, 1), 'launches': cnt}
     ctx.set_profiling(False)
 
-    # one more step with per-stage event marks (outside the timed region)
-    os.environ['ST_TIMING'] = '1'
-    step()
-    torch.cuda.synchronize()
-    stages = json.loads(ctx.timings())
-    os.environ.pop('ST_TIMING', None)
+    # one more step with per-stage event marks (outside the timed region; single device only)
+    stages = None
+    if world == 1:
+        os.environ['ST_TIMING'] = '1'
+        step()
+        torch.cuda.synchronize()
+        stages = json.loads(ctx.timings())
+        os.environ.pop('ST_TIMING', None)
 
     if rank != 0:
         if world > 1:
@@ -195,9 +219,10 @@ def main():
         'vs_baseline': None,
         'dtype': 'f64+f32 (bit-exact JS semantics); fp16 MFMA (f32 accumulate) for the assign prefilter',
         'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seed 1002+rank), resident in HBM',
-        'config': {'workload': f'writeSog SH3 {n} splats/GPU, {args.iters} k-means iters, paletteSize {pal}',
-                   'splats_per_gpu': n, 'sh_bands': 3, 'palette_size': pal, 'iterations': args.iters,
-                   'parallelism': f'dp{world}'},
+        'config': {'workload': f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters, '
+                               f'paletteSize {pal}',
+                   'splats_per_gpu': n, 'splats_total': n * world, 'sh_bands': 3, 'palette_size': pal,
+                   'iterations': args.iters, 'parallelism': f'rowshard{world}' if world > 1 else 'single'},
         'roofline': {
             'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-2 per splat)',
             'bound': 'mfma',

@@ -57,6 +57,13 @@ struct StageTimer {
 
 struct st_ctx {
     int device = 0;
+    // the N-D k-means point set prepared by nd_prepare (fp16 scale and shape)
+    float kn_sigma = 1.0f;
+    uint64_t kn_n = 0;
+    int kn_d = 0;
+    // the last st_dev_kmeans_partials call (member lists kept for st_dev_kmeans_seqsum)
+    int ds_nseg = 0, ds_k = 0, ds_d = 0;
+    uint64_t ds_n = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     st::Workspace ws;
@@ -138,5 +145,23 @@ uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t 
                        uint64_t ndraws, float *centroids256, uint8_t *labels);
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
                  const st_sog_textures *out);
+void codebook_dev(st_ctx *c, const float *cen, const uint32_t *lab, uint64_t total, float *centroids256,
+                  uint8_t *labels);
+void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const double lo[3], const double hi[3],
+                     const uint8_t *scale_lab, const uint8_t *color_lab, const uint32_t *shn_lab, st_sog_meta *meta,
+                     const st_sog_textures *out);
+void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *out);
+
+// multi-GPU building blocks (st_dist.hip)
+void minmax_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, double *lo, double *hi);
+void dist_prepare(st_ctx *c, const float *const *cols, int d, uint64_t n);
+void dist_assign(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen, uint32_t *labels);
+void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
+                   double *sums, double *sabs, int32_t *emin, uint32_t *counts);
+void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running);
+uint32_t dist_finish(st_ctx *c, int d, int k, const double *sums, const double *sabs, const int32_t *emin,
+                     const uint32_t *counts, float *cen, uint32_t *pending);
+void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npairs, const double *running,
+                  const uint32_t *counts, float *cen);
 
 }  // namespace st

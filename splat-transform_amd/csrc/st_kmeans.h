@@ -25,6 +25,16 @@ __host__ __device__ inline float fkey_inv_(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return __builtin_bit_cast(float, u);
 }
+// exponent of the unit in the last place of an f32 (the value is a multiple of 2^ulp_exp)
+__device__ inline int ulp_exp(float x) {
+    const uint32_t e = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;
+    return e == 0 ? -149 : (int)e - 150;
+}
+// certificate that every partial sum of a set of f32 values is exact in f64: all are
+// multiples of 2^emin and |partial sums| <= sum|x| < 2^(emin + 53) (slack for sum|x|'s own rounding)
+__host__ __device__ inline bool sum_is_exact(double sabs, int emin) {
+    return sabs == 0.0 || sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin + 53);
+}
 // stable-sort key of a centroid coordinate under the comparator `a - b`
 // (k-means / kd-tree sort callbacks): -0 and +0 compare equal
 __host__ __device__ inline uint32_t sortkey_(float f) { return fkey_(f == 0.0f ? 0.0f : f); }
@@ -43,6 +53,13 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                    const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
+
+// step form of the loops (shared with the distributed step API, st_dist.hip)
+void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n);  // workspace: kn.pfrag/kn.pnorm/kn.aos
+void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
+               km::State *dstate);
+void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels);
+void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n);
 
 // KdTree tie-break for exact-distance ties (st_kdtree.hip)
 void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,

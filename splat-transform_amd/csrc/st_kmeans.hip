@@ -117,7 +117,7 @@ __global__ void k_advance_cursor(State *st, const uint32_t *total_empty) { st->c
 using namespace km;
 
 // ---------------------------------------------------------------------------
-static void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
+void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     auto *flag = wsT<uint32_t>(c, "km.nf", 1);
     ST_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
     hipLaunchKernelGGL(k_nonfinite, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c->stream, dcols, d, n, flag);

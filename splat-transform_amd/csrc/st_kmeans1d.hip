@@ -124,11 +124,6 @@ __global__ __launch_bounds__(256) void k_pairs1d(const float *pts, const uint32_
     }
 }
 
-// exponent of the unit in the last place of an f32 (value is a multiple of 2^ulpexp)
-__device__ inline int ulp_exp(float x) {
-    const uint32_t e = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;
-    return e == 0 ? -149 : (int)e - 150;
-}
 
 // calcAverage (k-means.ts:41-63) for one cluster: the reference adds the members' values
 // in ascending point order into one f64.  When every partial sum is exactly representable
@@ -170,7 +165,7 @@ __global__ __launch_bounds__(256) void k_sum1d(const uint32_t *__restrict__ vals
     sabs = (red_a[0] + red_a[1]) + (red_a[2] + red_a[3]);
     emin = min(min(red_e[0], red_e[1]), min(red_e[2], red_e[3]));
     // sum|x| bounded above with slack for its own rounding
-    const bool exact = (sabs == 0.0) || (sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin + 53));
+    const bool exact = sum_is_exact(sabs, emin);
     seq_flag[cl] = exact ? 0u : 1u;
     if (exact) cen[cl] = (float)(sum / (double)(s1 - s0));
 }
@@ -223,10 +218,25 @@ __global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ v
 
 }  // namespace
 
-void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
-                   const double *ddraws, uint64_t ndraws, State *dstate, float *cen, uint32_t *labels) {
+// one exact 1-D assign: KdTree build == stable sort of the centroid values
+// (kd-tree.ts:73-99), then the walk simulation
+void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels) {
     auto *ckeys = wsT<uint32_t>(c, "k1.ckeys", (size_t)k);
     auto *corder = wsT<uint32_t>(c, "k1.corder", (size_t)k);
+    hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
+    ST_LAUNCH_CHECK();
+    radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
+    const unsigned g = grid_for(n, 256, 256 * 16);
+    KTimer kt(c, "k1.assign");
+    if (k <= KD1_LDS)
+        hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+    else
+        hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+    ST_LAUNCH_CHECK();
+}
+
+void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
+                   const double *ddraws, uint64_t ndraws, State *dstate, float *cen, uint32_t *labels) {
     auto *keys = wsT<uint32_t>(c, "k1.keys", n);
     auto *vals = wsT<uint32_t>(c, "k1.vals", n);
     auto *start = wsT<uint32_t>(c, "k1.start", (size_t)k + 1);
@@ -234,21 +244,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
     for (int it = 0; it < iters; ++it) {
-        // KdTree build == stable sort of the centroid values (kd-tree.ts:73-99)
-        hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
-        ST_LAUNCH_CHECK();
-        radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
-        const unsigned g = grid_for(n, 256, 256 * 16);
-        {
-            KTimer kt(c, "k1.assign");
-            if (k <= KD1_LDS)
-                hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
-                                   labels);
-            else
-                hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
-                                   labels);
-            ST_LAUNCH_CHECK();
-        }
+        assign1d(c, pts, n, k, cen, labels);
         mark(c, "k1.assign");
         // update
         hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,

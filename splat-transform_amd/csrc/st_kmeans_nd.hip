@@ -579,28 +579,15 @@ bool probe_denorm(st_ctx *c) {
         default: throw Error(ST_ERR_UNSUPPORTED, "kmeans: dimension too large for the MFMA assign (D <= 61)"); \
     }
 
-void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
-                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
+// ---- steps: prepare the point set once, then one exact assign per iteration -------
+void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     ST_REQUIRE(d <= 61, ST_ERR_UNSUPPORTED, "kmeans: D > 61 not supported by the MFMA assign");
-    ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
     const int ks = kp_of(d) / 16;
     const uint32_t ntiles = (uint32_t)((n + 31) / 32);
-    // centroid tiles, padded to whole LDS stages with rows that can never win (k_centroid_frags)
-    const uint32_t ctiles = (uint32_t)(((k + 31) / 32 + CT_STAGE - 1) / CT_STAGE * CT_STAGE);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
-    auto *cfrag = wsT<uint4>(c, "kn.cfrag", (size_t)ctiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
-    auto *thr = wsT<float>(c, "kn.thr", n);
-    auto *amb = wsT<uint32_t>(c, "kn.amb", n);
-    auto *ties = wsT<uint32_t>(c, "kn.ties", n);
-    auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
-    auto *members = wsT<uint32_t>(c, "kn.members", n);
-    auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits
-    auto *h = static_cast<State *>(pinned(c, sizeof(State)));
-    const Bound bnd = make_bound(d, probe_denorm(c));
-
     // scale: max|x| * sigma in [1, 2)
     ST_HIP(hipMemsetAsync(scal, 0, 16, c->stream));
     hipLaunchKernelGGL(k_absmax, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, dcols, d, n, scal);
@@ -614,61 +601,87 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     hipLaunchKernelGGL(k_point_frags, dim3(grid_for((uint64_t)ntiles * 32 * ks * 2, 256, 16384)), dim3(256), 0,
                        c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, aos);
     ST_LAUNCH_CHECK();
+    c->kn_sigma = sigma;
+    c->kn_n = n;
+    c->kn_d = d;
     mark(c, "kn.prep");
+}
 
-    for (int it = 0; it < iters; ++it) {
-        ST_HIP(hipMemsetAsync(scal + 1, 0, 4, c->stream));
-        hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0,
-                           c->stream, cen, d, k, ctiles, ks, sigma, cfrag, scal + 1);
+void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
+               km::State *dstate) {
+    ST_REQUIRE(c->kn_n == n && c->kn_d == d, ST_ERR_ARG, "kmeans assign: point set not prepared");
+    ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
+    const int ks = kp_of(d) / 16;
+    const uint32_t ntiles = (uint32_t)((n + 31) / 32);
+    // centroid tiles, padded to whole LDS stages with rows that can never win (k_centroid_frags)
+    const uint32_t ctiles = (uint32_t)(((k + 31) / 32 + CT_STAGE - 1) / CT_STAGE * CT_STAGE);
+    auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
+    auto *pnorm = wsT<float>(c, "kn.pnorm", n);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+    auto *scal = wsT<uint32_t>(c, "kn.scal", 4);
+    auto *cfrag = wsT<uint4>(c, "kn.cfrag", (size_t)ctiles * ks * 64);
+    auto *thr = wsT<float>(c, "kn.thr", n);
+    auto *amb = wsT<uint32_t>(c, "kn.amb", n);
+    auto *ties = wsT<uint32_t>(c, "kn.ties", n);
+    auto *h = static_cast<State *>(pinned(c, sizeof(State)));
+    const Bound bnd = make_bound(d, probe_denorm(c));
+    const float sigma = c->kn_sigma;
+
+    ST_HIP(hipMemsetAsync(scal + 1, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
+                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1);
+    ST_LAUNCH_CHECK();
+    ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
+    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
+                                        thr, amb, dstate)));
+    {
+        KTimer kt(c, "kn.fixrow");
+        hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cen, k,
+                           (uint32_t)n, labels, ties, dstate);
         ST_LAUNCH_CHECK();
-        ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
-        ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
-                                            thr, amb, dstate)));
+    }
+    mark(c, "kn.assign");
+    ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t namb = h->amb;
+    if (namb) {
+        const uint32_t atiles = (namb + 31) / 32;
+        auto *afrag = wsT<uint4>(c, "kn.afrag", (size_t)atiles * ks * 64);
+        auto *thr_slot = wsT<float>(c, "kn.thrslot", (size_t)atiles * 32);
+        auto *cand_cnt = wsT<uint32_t>(c, "kn.ccnt", (size_t)atiles * 32);
+        auto *cand = wsT<uint32_t>(c, "kn.cand", (size_t)namb * CAND_CAP);
+        hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, c->stream,
+                           pfrag, amb, thr, namb, ks, afrag, thr_slot, cand_cnt);
+        ST_LAUNCH_CHECK();
+        ST_KS_DISPATCH(ks,
+                       (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt, cand)));
         {
-            KTimer kt(c, "kn.fixrow");
-            hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d,
-                               cen, k, (uint32_t)n, labels, ties, dstate);
+            KTimer kt(c, "kn.exact");
+            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, cen, k, amb, namb,
+                               cand_cnt, cand, labels, ties, dstate);
             ST_LAUNCH_CHECK();
         }
-        mark(c, "kn.assign");
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
-        const uint32_t namb = h->amb;
-        if (namb) {
-            const uint32_t atiles = (namb + 31) / 32;
-            auto *afrag = wsT<uint4>(c, "kn.afrag", (size_t)atiles * ks * 64);
-            auto *thr_slot = wsT<float>(c, "kn.thrslot", (size_t)atiles * 32);
-            auto *cand_cnt = wsT<uint32_t>(c, "kn.ccnt", (size_t)atiles * 32);
-            auto *cand = wsT<uint32_t>(c, "kn.cand", (size_t)namb * CAND_CAP);
-            hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, c->stream,
-                               pfrag, amb, thr, namb, ks, afrag, thr_slot, cand_cnt);
-            ST_LAUNCH_CHECK();
-            ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt,
-                                                   cand)));
-            {
-                KTimer kt(c, "kn.exact");
-                hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, cen, k, amb, namb,
-                                   cand_cnt, cand, labels, ties, dstate);
-                ST_LAUNCH_CHECK();
-            }
-            ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipStreamSynchronize(c->stream));
-            if (getenv("ST_DEBUG")) {
-                uint32_t cmb = 0;
-                float pn0 = 0, thr0 = 0;
-                ST_HIP(hipMemcpy(&cmb, scal + 1, 4, hipMemcpyDeviceToHost));
-                ST_HIP(hipMemcpy(&pn0, pnorm, 4, hipMemcpyDeviceToHost));
-                ST_HIP(hipMemcpy(&thr0, thr, 4, hipMemcpyDeviceToHost));
-                fprintf(stderr,
-                        "[st kmeans] it=%d n=%llu k=%d ambiguous=%u ties=%u overflow=%u sigma=%g cmax=%g |p0|=%g "
-                        "thr0=%g bound a=%g b=%g ec=%g ep=%g\n",
-                        it, (unsigned long long)n, k, namb, h->ties, h->overflow, sigma,
-                        __builtin_bit_cast(float, cmb), pn0, thr0, bnd.a, bnd.b, bnd.ec, bnd.ep);
-            }
-        }
-        // exact ties from k_fixrow and k_exact: the KdTree walk decides
-        if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
-        mark(c, "kn.exact");
+    }
+    if (getenv("ST_DEBUG"))
+        fprintf(stderr, "[st kmeans] n=%llu k=%d ambiguous=%u ties=%u overflow=%u sigma=%g\n", (unsigned long long)n,
+                k, namb, h->ties, h->overflow, sigma);
+    // exact ties from k_fixrow and k_exact: the KdTree walk decides
+    if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
+    mark(c, "kn.exact");
+}
+
+void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
+                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
+    (void)cols;
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+    auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
+    auto *members = wsT<uint32_t>(c, "kn.members", n);
+    auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
+    nd_prepare(c, dcols, d, n);
+    for (int it = 0; it < iters; ++it) {
+        nd_assign(c, dcols, d, n, k, cen, labels, dstate);
         // update
         member_sort(c, labels, n, k, sorted_labels, members, start);
         {

@@ -367,4 +367,98 @@ int st_dev_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws,
     });
 }
 
+
+// ---- multi-GPU building blocks ------------------------------------------------------
+int st_dev_minmax(st_ctx *c, const float *const *cols, int32_t ncols, uint64_t n, double *lo, double *hi) {
+    return guarded([&] {
+        ST_ARG(c && cols && ncols > 0 && lo && hi, "bad argument");
+        use_device(c);
+        minmax_dev(c, cols, ncols, n, lo, hi);
+    });
+}
+
+int st_dev_kmeans_prepare(st_ctx *c, const float *const *cols, int32_t d, uint64_t n) {
+    return guarded([&] {
+        ST_ARG(c && cols && d > 0 && n > 0, "bad argument");
+        use_device(c);
+        dist_prepare(c, cols, d, n);
+    });
+}
+
+int st_dev_kmeans_assign(st_ctx *c, const float *const *cols, int32_t d, uint64_t n, int32_t k,
+                         const float *centroids, uint32_t *labels) {
+    return guarded([&] {
+        ST_ARG(c && cols && d > 0 && n > 0 && k > 0 && centroids && labels, "bad argument");
+        use_device(c);
+        dist_assign(c, cols, d, n, k, centroids, labels);
+    });
+}
+
+int st_dev_kmeans_partials(st_ctx *c, const float *const *cols, int32_t d, uint64_t n, int32_t nseg, int32_t k,
+                           const uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
+    return guarded([&] {
+        ST_ARG(c && cols && d > 0 && n > 0 && k > 0 && labels && sums && sabs && emin && counts, "bad argument");
+        use_device(c);
+        dist_partials(c, cols, d, n, nseg, k, labels, sums, sabs, emin, counts);
+    });
+}
+
+int st_dev_kmeans_seqsum(st_ctx *c, int32_t d, int32_t k, int32_t seg, const uint32_t *pairs, uint32_t npairs,
+                         double *running) {
+    return guarded([&] {
+        ST_ARG(c && (npairs == 0 || (pairs && running)), "bad argument");
+        use_device(c);
+        dist_seqsum(c, d, k, seg, pairs, npairs, running);
+    });
+}
+
+int st_dev_kmeans_finish(st_ctx *c, int32_t d, int32_t k, const double *sums, const double *sabs,
+                         const int32_t *emin, const uint32_t *counts, float *centroids, uint32_t *pending,
+                         uint32_t *npending) {
+    return guarded([&] {
+        ST_ARG(c && d > 0 && k > 0 && sums && sabs && emin && counts && centroids && pending && npending,
+               "bad argument");
+        use_device(c);
+        *npending = dist_finish(c, d, k, sums, sabs, emin, counts, centroids, pending);
+    });
+}
+
+int st_dev_kmeans_average(st_ctx *c, int32_t d, int32_t k, const uint32_t *pairs, uint32_t npairs,
+                          const double *running, const uint32_t *counts, float *centroids) {
+    return guarded([&] {
+        ST_ARG(c && d > 0 && k > 0 && (npairs == 0 || (pairs && running)) && counts && centroids, "bad argument");
+        use_device(c);
+        dist_average(c, d, k, pairs, npairs, running, counts, centroids);
+    });
+}
+
+int st_dev_cluster1d_codebook(st_ctx *c, const float *centroids, const uint32_t *labels, uint64_t total,
+                              float *codebook256, uint8_t *labels8) {
+    return guarded([&] {
+        ST_ARG(c && centroids && codebook256 && (total == 0 || (labels && labels8)), "bad argument");
+        use_device(c);
+        codebook_dev(c, centroids, labels, total, codebook256, labels8);
+    });
+}
+
+int st_dev_sog_scatter(st_ctx *c, const st_table *local, const uint32_t *pos, const double lo[3], const double hi[3],
+                       const uint8_t *scale_labels, const uint8_t *color_labels, const uint32_t *shn_labels,
+                       st_sog_meta *meta, const st_sog_textures *out) {
+    return guarded([&] {
+        ST_ARG(c && (pos || local->n == 0) && lo && hi && meta && out, "bad argument");
+        check_table(local);
+        use_device(c);
+        sog_scatter_dev(c, local, pos, lo, hi, scale_labels, color_labels, shn_labels, meta, out);
+    });
+}
+
+int st_dev_sog_shn_centroids(st_ctx *c, const uint8_t *codebook_labels, int32_t sh_coeffs, int32_t palette,
+                             uint8_t *out) {
+    return guarded([&] {
+        ST_ARG(c && codebook_labels && sh_coeffs > 0 && palette > 0 && out, "bad argument");
+        use_device(c);
+        shn_centroids_dev(c, codebook_labels, sh_coeffs, palette, out);
+    });
+}
+
 }  // extern "C"

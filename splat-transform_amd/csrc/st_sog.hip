@@ -78,11 +78,21 @@ struct MeansArgs {
     double mn[3], mx[3];
 };
 
-__global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint32_t *__restrict__ idx, uint64_t n,
+// Texture kernels run in two forms: gather (texel i <- row idx[i], the single-device
+// writeSog) or scatter (local row i -> texel pos[i], one shard of a multi-GPU writeSog)
+__device__ inline void tex_slot(const uint32_t *idx, const uint32_t *pos, uint64_t i, uint32_t &row, uint64_t &o) {
+    row = pos ? (uint32_t)i : idx[i];
+    o = pos ? (uint64_t)pos[i] : i;
+}
+
+__global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint32_t *__restrict__ idx,
+                                                  const uint32_t *__restrict__ pos, uint64_t n,
                                                   uint32_t *__restrict__ ml, uint32_t *__restrict__ mu) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t r = idx[i];
+        uint32_t r;
+        uint64_t o;
+        tex_slot(idx, pos, i, r, o);
         uint32_t lw = 0xff000000u, up = 0xff000000u;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -91,18 +101,20 @@ __global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint
             lw |= (uint32_t)(iv & 0xff) << (8 * k);
             up |= (uint32_t)((iv >> 8) & 0xff) << (8 * k);
         }
-        ml[i] = lw;
-        mu[i] = up;
+        ml[o] = lw;
+        mu[o] = up;
     }
 }
 
 __global__ __launch_bounds__(256) void k_quats_tex(const float *__restrict__ q0, const float *__restrict__ q1,
                                                   const float *__restrict__ q2, const float *__restrict__ q3,
-                                                  const uint32_t *__restrict__ idx, uint64_t n,
-                                                  uint32_t *__restrict__ out) {
+                                                  const uint32_t *__restrict__ idx, const uint32_t *__restrict__ pos,
+                                                  uint64_t n, uint32_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t r = idx[i];
+        uint32_t r;
+        uint64_t o;
+        tex_slot(idx, pos, i, r, o);
         double q[4] = {q0[r], q1[r], q2[r], q3[r]};
         const double l = __builtin_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
 #pragma unroll
@@ -126,31 +138,37 @@ __global__ __launch_bounds__(256) void k_quats_tex(const float *__restrict__ q0,
             px |= (uint32_t)js::to_uint8(255 * (q[j] * 0.5 + 0.5)) << (8 * k);
             ++k;
         }
-        out[i] = px;
+        out[o] = px;
     }
 }
 
 // writeTableData (write-sog.ts:142-157): rgb from u8 label columns, alpha = 4th column or 255
 __global__ __launch_bounds__(256) void k_table_tex(const uint8_t *__restrict__ l0, const uint8_t *__restrict__ l1,
                                                   const uint8_t *__restrict__ l2, const float *__restrict__ opacity,
-                                                  const uint32_t *__restrict__ idx, uint64_t n,
-                                                  uint32_t *__restrict__ out) {
+                                                  const uint32_t *__restrict__ idx, const uint32_t *__restrict__ pos,
+                                                  uint64_t n, uint32_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t r = idx[i];
+        uint32_t r;
+        uint64_t o;
+        tex_slot(idx, pos, i, r, o);
         uint32_t a = 255;
         if (opacity) a = js::to_uint8(js::max_(0, js::min_(255, js::sigmoid(opacity[r]) * 255)));
-        out[i] = (uint32_t)l0[r] | ((uint32_t)l1[r] << 8) | ((uint32_t)l2[r] << 16) | (a << 24);
+        out[o] = (uint32_t)l0[r] | ((uint32_t)l1[r] << 8) | ((uint32_t)l2[r] << 16) | (a << 24);
     }
 }
 
 __global__ __launch_bounds__(256) void k_shn_labels_tex(const uint32_t *__restrict__ labels,
-                                                       const uint32_t *__restrict__ idx, uint64_t n,
+                                                       const uint32_t *__restrict__ idx,
+                                                       const uint32_t *__restrict__ pos, uint64_t n,
                                                        uint32_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t label = labels[idx[i]];
-        out[i] = (label & 0xffu) | (((label >> 8) & 0xffu) << 8) | 0xff000000u;
+        uint32_t r;
+        uint64_t o;
+        tex_slot(idx, pos, i, r, o);
+        const uint32_t label = labels[r];
+        out[o] = (label & 0xffu) | (((label >> 8) & 0xffu) << 8) | 0xff000000u;
     }
 }
 
@@ -191,16 +209,70 @@ uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t 
     auto *lab = wsT<uint32_t>(c, "c1.lab", total);
     const float *one[1] = {data};
     const uint64_t used = kmeans_dev(c, one, 1, total, 256, iters, draws, ndraws, cen, lab);
+    codebook_dev(c, cen, lab, total, centroids256, labels);
+    return used;
+}
+
+// cluster1d's codebook (write-sog.ts:69-88): centroids sorted ascending (stable,
+// `a - b` comparator), labels remapped to the sorted order as bytes
+void codebook_dev(st_ctx *c, const float *cen, const uint32_t *lab, uint64_t total, float *centroids256,
+                  uint8_t *labels) {
     auto *keys = wsT<uint32_t>(c, "c1.keys", 256);
     auto *order = wsT<uint32_t>(c, "c1.order", 256);
     auto *inv = wsT<uint32_t>(c, "c1.inv", 256);
     hipLaunchKernelGGL(k_sort_codebook, dim3(1), dim3(256), 0, c->stream, cen, keys, order);
     radix_sort_u32(c, keys, order, 256, 0, 32, "c1.rs");
     hipLaunchKernelGGL(k_finish_codebook, dim3(1), dim3(256), 0, c->stream, cen, order, centroids256, inv);
-    hipLaunchKernelGGL(k_remap_labels, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, lab, inv, total,
-                       labels);
+    if (total)
+        hipLaunchKernelGGL(k_remap_labels, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, lab, inv, total,
+                           labels);
     ST_LAUNCH_CHECK();
-    return used;
+}
+
+// one shard's texels of a multi-GPU writeSog: local rows at their global sorted
+// positions `pos`; lo/hi are the global NaN-ignoring extents of x, y, z
+void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const double lo[3], const double hi[3],
+                     const uint8_t *scale_lab, const uint8_t *color_lab, const uint32_t *shn_lab, st_sog_meta *meta,
+                     const st_sog_textures *out) {
+    const uint64_t n = t->n;
+    static const char *members[8] = {"x", "y", "z", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    const float *m[8];
+    for (int i = 0; i < 8; ++i) {
+        m[i] = col_or_null(t, members[i]);
+        ST_REQUIRE(m[i], ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
+    }
+    MeansArgs ma{};
+    for (int a = 0; a < 3; ++a) {
+        ma.c[a] = m[a];
+        ma.mn[a] = js::log_transform(lo[a]);
+        ma.mx[a] = js::log_transform(hi[a]);
+        meta->means_min[a] = ma.mn[a];
+        meta->means_max[a] = ma.mx[a];
+    }
+    if (!n) return;
+    const unsigned g = grid_for(n, 256, 8192);
+    if (out->means_l && out->means_u)
+        hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
+                           (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+    if (out->quats)
+        hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[4], m[5], m[6], m[7],
+                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
+    if (out->scales && scale_lab)
+        hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, scale_lab, scale_lab + n, scale_lab + 2 * n,
+                           (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
+    if (out->sh0 && color_lab)
+        hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, color_lab, color_lab + n, color_lab + 2 * n,
+                           m[3], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+    if (out->shn_labels && shn_lab)
+        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, shn_lab, (const uint32_t *)nullptr,
+                           pos, n, (uint32_t *)out->shn_labels);
+    ST_LAUNCH_CHECK();
+}
+
+void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *out) {
+    hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
+                       cl, C, pal, (uint32_t *)out);
+    ST_LAUNCH_CHECK();
 }
 
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
@@ -253,10 +325,10 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
         meta->means_min[a] = ma.mn[a];
         meta->means_max[a] = ma.mx[a];
     }
-    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, idx, n, (uint32_t *)out->means_l,
-                       (uint32_t *)out->means_u);
-    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13], idx, n,
-                       (uint32_t *)out->quats);
+    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, idx, (const uint32_t *)nullptr, n,
+                       (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13], idx,
+                       (const uint32_t *)nullptr, n, (uint32_t *)out->quats);
     ST_LAUNCH_CHECK();
     mark(c, "sog.means_quats");
 
@@ -267,14 +339,14 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
     hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
-                       (const float *)nullptr, idx, n, (uint32_t *)out->scales);
+                       (const float *)nullptr, idx, (const uint32_t *)nullptr, n, (uint32_t *)out->scales);
     ST_LAUNCH_CHECK();
     mark(c, "sog.scales");
     // colour + opacity (write-sog.ts:253-268)
     cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9], idx, n,
-                       (uint32_t *)out->sh0);
+    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9], idx,
+                       (const uint32_t *)nullptr, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
 
@@ -304,8 +376,8 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
         ST_HIP(hipMemsetAsync(out->shn_labels, 0, texels * 4, c->stream));
         hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
                            cl, C, pal, (uint32_t *)out->shn_centroids);
-        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, idx, n,
-                           (uint32_t *)out->shn_labels);
+        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, idx,
+                           (const uint32_t *)nullptr, n, (uint32_t *)out->shn_labels);
         ST_LAUNCH_CHECK();
         mark(c, "sog.shn");
     }

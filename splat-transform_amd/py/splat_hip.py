@@ -17,6 +17,7 @@ PKG = os.path.dirname(HERE)
 LIB_PATH = os.environ.get('ST_LIB') or os.path.join(PKG, 'lib', 'libsplat_hip.so')
 
 ST_OK = 0
+ST_ERR_ARG, ST_ERR_HIP, ST_ERR_NONFINITE, ST_ERR_DRAWS = -1, -2, -3, -4
 _lib = None
 
 
@@ -56,6 +57,9 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
+    'st_dev_minmax', 'st_dev_kmeans_prepare', 'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
+    'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
+    'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
 ]
 
 
@@ -291,6 +295,15 @@ class Context:
                                   _ptr(centroids), _ptr(labels)))
         return used.value
 
+    def dev_cluster1d(self, col_list, iters, draws, centroids, labels):
+        n = len(col_list[0])
+        used = ctypes.c_uint64(0)
+        ptrs = (ctypes.c_void_p * len(col_list))(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_cluster1d(self.h, ptrs, ctypes.c_int32(len(col_list)), ctypes.c_uint64(n),
+                                     ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)),
+                                     ctypes.byref(used), _ptr(centroids), _ptr(labels)))
+        return used.value
+
     def dev_sog(self, cols, iters, draws, tex):
         """tex: dict of device uint8 tensors (see sog_geometry for sizes)"""
         t = make_table(cols)
@@ -302,3 +315,61 @@ class Context:
                                ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
                                ctypes.byref(out)))
         return meta, used.value
+
+    # ---- multi-GPU building blocks (device tensors; see splat_dist.py) ----------------
+    def dev_minmax(self, cols):
+        m = len(cols)
+        lo, hi = (ctypes.c_double * m)(), (ctypes.c_double * m)()
+        ptrs = (ctypes.c_void_p * m)(*[c.data_ptr() for c in cols])
+        check(lib().st_dev_minmax(self.h, ptrs, ctypes.c_int32(m), ctypes.c_uint64(len(cols[0])), lo, hi))
+        return list(lo), list(hi)
+
+    def dev_kmeans_prepare(self, col_list):
+        d, n = len(col_list), len(col_list[0])
+        ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_kmeans_prepare(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(n)))
+
+    def dev_kmeans_assign(self, col_list, k, centroids, labels):
+        d, n = len(col_list), len(col_list[0])
+        ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_kmeans_assign(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(n), ctypes.c_int32(k),
+                                         _ptr(centroids), _ptr(labels)))
+
+    def dev_kmeans_partials(self, col_list, nseg, k, labels, sums, sabs, emin, counts):
+        d, n = len(col_list), len(col_list[0])
+        ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_kmeans_partials(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(n), ctypes.c_int32(nseg),
+                                           ctypes.c_int32(k), _ptr(labels), _ptr(sums), _ptr(sabs), _ptr(emin),
+                                           _ptr(counts)))
+
+    def dev_kmeans_seqsum(self, d, k, seg, pairs, running):
+        check(lib().st_dev_kmeans_seqsum(self.h, ctypes.c_int32(d), ctypes.c_int32(k), ctypes.c_int32(seg),
+                                         _ptr(pairs), ctypes.c_uint32(len(pairs)), _ptr(running)))
+
+    def dev_kmeans_finish(self, d, k, sums, sabs, emin, counts, centroids, pending):
+        np_ = ctypes.c_uint32(0)
+        check(lib().st_dev_kmeans_finish(self.h, ctypes.c_int32(d), ctypes.c_int32(k), _ptr(sums), _ptr(sabs),
+                                         _ptr(emin), _ptr(counts), _ptr(centroids), _ptr(pending), ctypes.byref(np_)))
+        return np_.value
+
+    def dev_kmeans_average(self, d, k, pairs, running, counts, centroids):
+        check(lib().st_dev_kmeans_average(self.h, ctypes.c_int32(d), ctypes.c_int32(k), _ptr(pairs),
+                                          ctypes.c_uint32(len(pairs)), _ptr(running), _ptr(counts), _ptr(centroids)))
+
+    def dev_cluster1d_codebook(self, centroids, labels, codebook, labels8):
+        check(lib().st_dev_cluster1d_codebook(self.h, _ptr(centroids), _ptr(labels), ctypes.c_uint64(len(labels)),
+                                              _ptr(codebook), _ptr(labels8)))
+
+    def dev_sog_scatter(self, cols, pos, lo, hi, scale_labels, color_labels, shn_labels, tex):
+        t = make_table(cols)
+        out = SogTextures(*[(tex[k].data_ptr() if tex.get(k) is not None else None) for k in
+                            ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        meta = SogMeta()
+        check(lib().st_dev_sog_scatter(self.h, ctypes.byref(t), _ptr(pos), (ctypes.c_double * 3)(*lo),
+                                       (ctypes.c_double * 3)(*hi), _ptr(scale_labels), _ptr(color_labels),
+                                       _ptr(shn_labels), ctypes.byref(meta), ctypes.byref(out)))
+        return meta
+
+    def dev_sog_shn_centroids(self, codebook_labels, sh_coeffs, palette, out):
+        check(lib().st_dev_sog_shn_centroids(self.h, _ptr(codebook_labels), ctypes.c_int32(sh_coeffs),
+                                             ctypes.c_int32(palette), _ptr(out)))
