@@ -78,10 +78,11 @@ __global__ __launch_bounds__(256) void k_partials_nd(const float *__restrict__ a
     const uint32_t s0 = start[sc], s1 = start[sc + 1];
     if (lane == 0) counts[sc] = s1 - s0;
     if (lane >= d) return;
+    const int ld = aos_ld(d);
     double sum = 0, sa = 0;
     int em = 1 << 20;
     for (uint32_t j = s0; j < s1; ++j) {
-        const float v = aos[(uint64_t)members[j] * d + lane];
+        const float v = aos[(uint64_t)members[j] * ld + lane];
         sum += (double)v;
         sa += (double)__builtin_fabsf(v);
         if (v != 0.0f) em = min(em, ulp_exp(v));
@@ -139,8 +140,9 @@ __global__ __launch_bounds__(64) void k_seqsum_nd(const float *__restrict__ aos,
     if (p >= npairs) return;
     const uint32_t pair = pairs[p], cl = pair / d, dim = pair % d;
     const uint32_t sc = (uint32_t)seg * k + cl;
+    const int ld = aos_ld(d);
     double s = running[p];
-    for (uint32_t j = start[sc]; j < start[sc + 1]; ++j) s += (double)aos[(uint64_t)members[j] * d + dim];
+    for (uint32_t j = start[sc]; j < start[sc + 1]; ++j) s += (double)aos[(uint64_t)members[j] * ld + dim];
     running[p] = s;
 }
 
@@ -266,7 +268,7 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
                            sabs, emin, counts);
     } else {
         ST_REQUIRE(c->kn_n == n && c->kn_d == d, ST_ERR_ARG, "kmeans partials: point set not prepared");
-        auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+        auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
         hipLaunchKernelGGL(k_partials_nd, dim3((unsigned)((nk + 3) / 4)), dim3(256), 0, c->stream, aos, d, payload,
                            start, k, nseg, sums, sabs, emin, counts);
     }
@@ -287,7 +289,7 @@ void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32
     if (d == 1) {
         hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, running);
     } else {
-        auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+        auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
         hipLaunchKernelGGL(k_seqsum_nd, dim3((npairs + 63) / 64), dim3(64), 0, c->stream, aos, d, payload, start, k,
                            seg, pairs, npairs, running);
     }

@@ -25,6 +25,9 @@ __host__ __device__ inline float fkey_inv_(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return __builtin_bit_cast(float, u);
 }
+// row stride of the f32 AoS copies of points and centroids (16-byte rows, zero padded)
+__host__ __device__ inline int aos_ld(int d) { return (d + 3) & ~3; }
+
 // exponent of the unit in the last place of an f32 (the value is a multiple of 2^ulp_exp)
 __device__ inline int ulp_exp(float x) {
     const uint32_t e = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
 
 // point B fragments: pfrag[t][s][lane] = 8 fp16 of B[k = 16s + 8h + j][p = 32t + (lane&31)];
 // one thread per (point, k-step, half); also |sigma p| (rounded up) and the AoS f32 copy
+// (row stride aos_ld(d), zero padded)
 __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
                                                      int ks, float sigma, uint4 *pfrag, float *pnorm, float *aos) {
     const uint64_t total = (uint64_t)ntiles * 32 * ks * 2;
@@ -119,6 +120,7 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
         const int sh = (int)(q / ((uint64_t)ntiles * 32));  // s * 2 + h
         const int s = sh >> 1, h = sh & 1;
         const bool valid = p < n;
+        const int ld = aos_ld(d);
         uint16_t e[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -127,11 +129,12 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
             if (k < d) {
                 if (valid) {
                     const float raw = cols[k][p];
-                    aos[p * d + k] = raw;
+                    aos[p * ld + k] = raw;
                     bits = h_bits(-2.0f * h_val(h_bits(raw * sigma)));  // -2 p~ exactly
                 }
-            } else if (k < d + 3) {
-                bits = valid ? (uint16_t)0x3c00u : (uint16_t)0;  // 1.0
+            } else {
+                if (k < d + 3) bits = valid ? (uint16_t)0x3c00u : (uint16_t)0;  // 1.0
+                if (k < ld && valid) aos[p * ld + k] = 0.0f;                    // row padding
             }
             e[j] = bits;
         }
@@ -152,13 +155,27 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
     }
 }
 
-// centroid A fragments + cmax; one thread per centroid row; rows >= k can never win
+// centroid A fragments + cmax + the AoS f32 copy of the centroids (exact distances);
+// one thread per centroid row; rows >= k can never win
 __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
-                                                        float sigma, uint4 *cfrag, uint32_t *cmax_bits) {
+                                                        float sigma, uint4 *cfrag, uint32_t *cmax_bits, float *caos,
+                                                        float2 *cfix) {
     const uint32_t total = ctiles * 32;
+    const int ld = aos_ld(d);
     float mymax = 0.f;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < total; r += gridDim.x * blockDim.x) {
         const bool valid = r < (uint32_t)k;
+        if (valid) {
+            for (int c = 0; c < ld; ++c) caos[(uint64_t)r * ld + c] = c < d ? cen[(uint64_t)c * k + r] : 0.0f;
+            // k_fixrow layout: [tile][lane-half][dim pair][16 rows] float2, so the 16 lanes of a
+            // point read one whole 128-byte line per dimension pair
+            const uint32_t row = r & 31, hh = (row >> 2) & 1, r16 = (row & 3) | ((row >> 3) << 2);
+            for (int q = 0; q < ld / 2; ++q) {
+                const float a = 2 * q < d ? cen[(uint64_t)(2 * q) * k + r] : 0.0f;
+                const float b = 2 * q + 1 < d ? cen[(uint64_t)(2 * q + 1) * k + r] : 0.0f;
+                cfix[(((uint64_t)(r >> 5) * 2 + hh) * (ld / 2) + q) * 16 + r16] = make_float2(a, b);
+            }
+        }
         double nn = 0;
         for (int c = 0; c < d; ++c) {
             const double x = valid ? (double)(cen[(uint64_t)c * k + r] * sigma) : 0.0;
@@ -403,12 +420,22 @@ __global__ __launch_bounds__(256) void k_gather_amb(const uint4 *__restrict__ pf
     }
 }
 
-// kd-tree.ts:26-35 distance (c - p per dimension, sequential f64 sum)
-__device__ inline double ref_dist(const float *__restrict__ cen, int k, uint32_t c, const float *__restrict__ prow,
-                                  int d) {
+// kd-tree.ts:26-35 distance (c - p per dimension, sequential f64 sum) of two
+// zero-padded AoS rows; the padding adds +0 to a non-negative sum, so the result is
+// the reference's for the first d dimensions
+__device__ inline double ref_dist(const float *__restrict__ crow, const float *__restrict__ prow, int ld) {
+    const float4 *c4 = reinterpret_cast<const float4 *>(crow);
+    const float4 *p4 = reinterpret_cast<const float4 *>(prow);
     double l = 0;
-    for (int i = 0; i < d; ++i) {
-        const double v = (double)cen[(uint64_t)i * k + c] - (double)prow[i];
+    for (int q = 0; q < ld / 4; ++q) {
+        const float4 a = c4[q], b = p4[q];
+        double v = (double)a.x - (double)b.x;
+        l += v * v;
+        v = (double)a.y - (double)b.y;
+        l += v * v;
+        v = (double)a.z - (double)b.z;
+        l += v * v;
+        v = (double)a.w - (double)b.w;
         l += v * v;
     }
     return l;
@@ -417,18 +444,63 @@ __device__ inline double ref_dist(const float *__restrict__ cen, int k, uint32_t
 // decided points: the sweep left (tile, lane-half) of the minimum in labels[p]; every
 // other tile's rows score above m1 + W_p, so their reference distances exceed that of
 // the best row, and the argmin lies among this lane-half's 16 rows.  16 lanes per point
-// take the exact f64 distance of kd-tree.ts:26-35 for those rows; a unique minimum is
-// the reference's answer, an exact tie goes to the KdTree walk (kd_resolve_ties).
-__global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float *__restrict__ cen,
-                                                int k, uint32_t n, uint32_t *__restrict__ labels,
-                                                uint32_t *__restrict__ ties, State *st) {
+// (one row each) screen with an f32 distance and a rigorous bound that covers both the
+// f32 evaluation and the reference's f64 one: when exactly one row's interval reaches
+// the lowest upper end, it is the reference's answer.  Otherwise the candidate rows take
+// the exact f64 distance of kd-tree.ts:26-35; a unique minimum decides, an exact tie
+// goes to the KdTree walk (kd_resolve_ties).
+__global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
+                                                const float *__restrict__ caos, int k, uint32_t n,
+                                                uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                State *st) {
+    const int ld = aos_ld(d);
     const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     const int r = threadIdx.x & 15;
     if (p >= n) return;  // uniform per 16-lane group
     const uint32_t code = labels[p];
     if (code == 0xffffffffu) return;  // ambiguous: k_exact decides
     const uint32_t c = (code >> 1) * 32 + 4 * (code & 1) + (r & 3) + 8 * (r >> 2);
-    const double mine = (c < (uint32_t)k) ? ref_dist(cen, k, c, aos + p * d, d) : __builtin_inf();
+    const bool valid = c < (uint32_t)k;
+    const float *prow = aos + p * ld;
+    // f32 screen: |s - T| <= (d + 2) u T for fma accumulation of fl(c - p)^2 (u = 2^-24), plus
+    // underflow; the reference's f64 error is far below the (d + 4) u margin used
+    float s = 0.f;
+    if (valid) {
+        // padded dimensions hold 0 in both rows: they add +0
+        const float4 *p4 = reinterpret_cast<const float4 *>(prow);
+        const float2 *crow = cfix + (uint64_t)(code >> 1) * 2 * (ld / 2) * 16 + (uint64_t)(code & 1) * (ld / 2) * 16 + r;
+        for (int q = 0; q < ld / 4; ++q) {
+            const float4 pv = p4[q];
+            const float2 c0 = crow[(2 * q) * 16], c1 = crow[(2 * q + 1) * 16];
+            float v = c0.x - pv.x;
+            s = __builtin_fmaf(v, v, s);
+            v = c0.y - pv.y;
+            s = __builtin_fmaf(v, v, s);
+            v = c1.x - pv.z;
+            s = __builtin_fmaf(v, v, s);
+            v = c1.y - pv.w;
+            s = __builtin_fmaf(v, v, s);
+        }
+    }
+    const float rel = (float)(d + 4) * 0x1p-24f, ab = (float)(d + 2) * 0x1p-126f;
+    const float lo = valid ? s - (s * rel + ab) : __builtin_inff();
+    const float hi = valid ? s + (s * rel + ab) : __builtin_inff();
+    float mh = hi;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
+    bool cand = valid && lo <= mh;  // NaN/inf screens fall through to the exact path
+    uint32_t ncand = cand ? 1u : 0u;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
+    if (ncand == 1) {
+        uint32_t w = cand ? c : 0xffffffffu;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
+        if (r == 0) labels[p] = w;
+        return;
+    }
+    if (ncand == 0) cand = valid;
+    const double mine = cand ? ref_dist(caos + (uint64_t)c * ld, prow, ld) : __builtin_inf();
     double best = mine;
     uint32_t bidx = c;
 #pragma unroll
@@ -440,7 +512,7 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
             bidx = oi;
         }
     }
-    const uint32_t eq = (mine == best) ? 1u : 0u;
+    const uint32_t eq = (cand && mine == best) ? 1u : 0u;
     uint32_t cnt = eq;
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
@@ -451,7 +523,7 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
-__global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, int d, const float *__restrict__ cen,
+__global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, int d, const float *__restrict__ caos,
                                                int k, const uint32_t *__restrict__ amb, uint32_t namb,
                                                const uint32_t *__restrict__ cand_cnt,
                                                const uint32_t *__restrict__ cand, uint32_t *__restrict__ labels,
@@ -460,7 +532,8 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     const uint32_t a = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (a >= namb) return;
     const uint32_t p = amb[a];
-    const float *prow = aos + (uint64_t)p * d;
+    const int ld = aos_ld(d);
+    const float *prow = aos + (uint64_t)p * ld;
     const uint32_t cnt = cand_cnt[a];
     const bool overflow = cnt > CAND_CAP;
     if (overflow && lane == 0) atomicAdd(&st->overflow, 1u);
@@ -469,7 +542,7 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     const uint32_t limit = overflow ? (uint32_t)k : cnt;
     for (uint32_t j = lane; j < limit; j += 64) {
         const uint32_t c = overflow ? j : cand[(uint64_t)a * CAND_CAP + j];
-        const double dd = ref_dist(cen, k, c, prow, d);
+        const double dd = ref_dist(caos + (uint64_t)c * ld, prow, ld);
         if (dd < best || (dd == best && c < bidx)) {
             best = dd;
             bidx = c;
@@ -482,7 +555,7 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     uint32_t lowest = 0xffffffffu;
     for (uint32_t j = lane; j < limit; j += 64) {
         const uint32_t c = overflow ? j : cand[(uint64_t)a * CAND_CAP + j];
-        if (ref_dist(cen, k, c, prow, d) == m) {
+        if (ref_dist(caos + (uint64_t)c * ld, prow, ld) == m) {
             ++mine;
             lowest = min(lowest, c);
         }
@@ -514,18 +587,19 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     if (cl >= (uint32_t)k) return;
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
     if (s0 == s1 || lane >= d) return;
+    const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
     for (; j + 4 <= s1; j += 4) {
         const uint32_t m0 = members[j], m1 = members[j + 1], m2 = members[j + 2], m3 = members[j + 3];
-        const float v0 = aos[(uint64_t)m0 * d + lane], v1 = aos[(uint64_t)m1 * d + lane];
-        const float v2 = aos[(uint64_t)m2 * d + lane], v3 = aos[(uint64_t)m3 * d + lane];
+        const float v0 = aos[(uint64_t)m0 * ld + lane], v1 = aos[(uint64_t)m1 * ld + lane];
+        const float v2 = aos[(uint64_t)m2 * ld + lane], v3 = aos[(uint64_t)m3 * ld + lane];
         sum += (double)v0;
         sum += (double)v1;
         sum += (double)v2;
         sum += (double)v3;
     }
-    for (; j < s1; ++j) sum += (double)aos[(uint64_t)members[j] * d + lane];
+    for (; j < s1; ++j) sum += (double)aos[(uint64_t)members[j] * ld + lane];
     cen[(uint64_t)lane * k + cl] = (float)(sum / (double)(s1 - s0));
 }
 
@@ -586,7 +660,7 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     const uint32_t ntiles = (uint32_t)((n + 31) / 32);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
-    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits
     // scale: max|x| * sigma in [1, 2)
     ST_HIP(hipMemsetAsync(scal, 0, 16, c->stream));
@@ -617,7 +691,7 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     const uint32_t ctiles = (uint32_t)(((k + 31) / 32 + CT_STAGE - 1) / CT_STAGE * CT_STAGE);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
-    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);
     auto *cfrag = wsT<uint4>(c, "kn.cfrag", (size_t)ctiles * ks * 64);
     auto *thr = wsT<float>(c, "kn.thr", n);
@@ -628,16 +702,18 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     const float sigma = c->kn_sigma;
 
     ST_HIP(hipMemsetAsync(scal + 1, 0, 4, c->stream));
+    auto *caos = wsT<float>(c, "kn.caos", (size_t)k * aos_ld(d));
+    auto *cfix = wsT<float2>(c, "kn.cfix", (size_t)ctiles * 32 * (aos_ld(d) / 2));
     hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
-                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1);
+                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix);
     ST_LAUNCH_CHECK();
     ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
                                         thr, amb, dstate)));
     {
         KTimer kt(c, "kn.fixrow");
-        hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cen, k,
-                           (uint32_t)n, labels, ties, dstate);
+        hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cfix,
+                           caos, k, (uint32_t)n, labels, ties, dstate);
         ST_LAUNCH_CHECK();
     }
     mark(c, "kn.assign");
@@ -657,7 +733,7 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
                        (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt, cand)));
         {
             KTimer kt(c, "kn.exact");
-            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, cen, k, amb, namb,
+            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, caos, k, amb, namb,
                                cand_cnt, cand, labels, ties, dstate);
             ST_LAUNCH_CHECK();
         }
@@ -675,7 +751,7 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
     (void)cols;
-    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
     auto *members = wsT<uint32_t>(c, "kn.members", n);
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
