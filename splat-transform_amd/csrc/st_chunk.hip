@@ -5,8 +5,9 @@
 // Morton order.  Per-chunk min/max use Math.min/Math.max semantics (NaN
 // propagates, -0 < +0) through wave64 shuffles + LDS; the quantisers run in
 // f64 exactly as the JS; the final partial chunk is padded with its last
-// splat (write-compressed-ply.ts:90-93).  HBM traffic per splat: 14 gathered
-// floats + 3C SH floats in, 16 B vertex + 3C bytes SH out.
+// splat (write-compressed-ply.ts:90-93).  HBM traffic per splat: the column
+// transpose (14 + 3C floats read, the padded row written), one gathered row,
+// 16 B vertex + 3C bytes SH out.
 #include "st_internal.h"
 #include "st_jsmath.h"
 
@@ -101,10 +102,37 @@ __device__ inline uint32_t pack_rot(double x, double y, double z, double w) {
     return result;
 }
 
+// Rows are gathered through the Morton order, i.e. at random.  Gathering 59 SoA
+// columns would touch one cache line per (splat, column); the columns are first
+// transposed (streaming, coalesced) into 16-byte-aligned AoS rows of RL floats
+// ([14 members][3C SH][pad]) so a gathered row is RL*4 contiguous bytes.
+struct TransposeArgs {
+    const float *src[64];
+    int ncol, rl;
+    uint64_t n;
+    float *rows;
+};
+
+// 64 rows per block through LDS: coalesced column reads, coalesced row writes
+__global__ __launch_bounds__(256) void k_rows_aos(const TransposeArgs a) {
+    __shared__ float tile[64 * 64];
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const int t = threadIdx.x;
+    for (int e = t; e < 64 * a.rl; e += 256) {
+        const int col = e / 64, r = e % 64;
+        const uint64_t row = r0 + r;
+        tile[r * a.rl + col] = (col < a.ncol && row < a.n) ? a.src[col][row] : 0.0f;
+    }
+    __syncthreads();
+    const uint64_t nrows = (a.n - r0 < 64) ? (a.n - r0) : 64;
+    float4 *dst = reinterpret_cast<float4 *>(a.rows + r0 * a.rl);
+    const float4 *s4 = reinterpret_cast<const float4 *>(tile);
+    for (uint64_t e = t; e < nrows * a.rl / 4; e += 256) dst[e] = s4[e];
+}
+
 struct ChunkArgs {
-    const float *m[14];  // x y z scale_0..2 f_dc_0..2 opacity rot_0..3
-    const float *const *sh;
-    int nsh;
+    const float *rows;  // AoS rows: x y z scale_0..2 f_dc_0..2 opacity rot_0..3, then the SH
+    int rl, nsh;
     uint64_t n;
     const uint32_t *order;
     float *chunk;
@@ -114,22 +142,38 @@ struct ChunkArgs {
 
 __global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
     enum { X, Y, Z, S0, S1, S2, R, G, B, OP, Q0, Q1, Q2, Q3 };
+    __shared__ uint32_t sh_stage[256 * 45 / 4];
     const uint64_t c = blockIdx.x;
     const uint64_t base = c * 256;
     const uint32_t num = (uint32_t)((a.n < base + 256 ? a.n : base + 256) - base);
     const uint32_t j = threadIdx.x;
     const bool real = j < num;
     const uint32_t row = a.order[base + (real ? j : num - 1)];
-    float d[14];
+    const float4 *r4 = reinterpret_cast<const float4 *>(a.rows + (uint64_t)row * a.rl);
+    float d[16];
 #pragma unroll
-    for (int m = 0; m < 14; ++m) d[m] = a.m[m][row];
-    // 8-bit SH (write-compressed-ply.ts:83-87)
-    if (real && a.nsh) {
-        uint8_t *o = a.sh_out + (base + j) * (uint64_t)a.nsh;
-        for (int k = 0; k < a.nsh; ++k) {
-            const double nv = (double)a.sh[k][row] / 8 + 0.5;
-            o[k] = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = r4[q];
+        d[4 * q] = v.x;
+        d[4 * q + 1] = v.y;
+        d[4 * q + 2] = v.z;
+        d[4 * q + 3] = v.w;
+    }
+    // 8-bit SH (write-compressed-ply.ts:83-87), staged in LDS for coalesced stores
+    if (a.nsh) {
+        uint8_t *stage = reinterpret_cast<uint8_t *>(sh_stage);
+        if (real) {
+            for (int k = 0; k < a.nsh; ++k) {
+                const double nv = (double)a.rows[(uint64_t)row * a.rl + 14 + k] / 8 + 0.5;
+                stage[j * a.nsh + k] = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+            }
         }
+        __syncthreads();
+        uint8_t *o = a.sh_out + base * (uint64_t)a.nsh;
+        const uint32_t bytes = num * (uint32_t)a.nsh;
+        // chunk bases are multiples of 256 * nsh bytes, so o is 4-byte aligned
+        for (uint32_t e = j; e < bytes / 4; e += 256) reinterpret_cast<uint32_t *>(o)[e] = sh_stage[e];
+        for (uint32_t e = (bytes / 4) * 4 + j; e < bytes; e += 256) o[e] = stage[e];
     }
     float mn[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
     float mx[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
@@ -170,25 +214,27 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     if (n == 0) return;
     static const char *members[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
                                       "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
-    ChunkArgs a{};
+    TransposeArgs ta{};
     for (int i = 0; i < 14; ++i) {
-        a.m[i] = col_or_null(t, members[i]);
-        ST_REQUIRE(a.m[i], ST_ERR_ARG, std::string("pack_compressed: missing column ") + members[i]);
+        ta.src[i] = col_or_null(t, members[i]);
+        ST_REQUIRE(ta.src[i], ST_ERR_ARG, std::string("pack_compressed: missing column ") + members[i]);
     }
     const int C = sh_coeffs_of(t);
-    a.nsh = 3 * C;
-    if (a.nsh) {
-        ST_REQUIRE(sh, ST_ERR_ARG, "pack_compressed: sh output is NULL");
-        std::vector<float *> p(a.nsh);
-        char nm[32];
-        for (int i = 0; i < a.nsh; ++i) {
-            snprintf(nm, sizeof nm, "f_rest_%d", i);
-            p[i] = col_or_null(t, nm);
-        }
-        auto **d = wsT<float *>(c, "chunk.sh", a.nsh);
-        ST_HIP(hipMemcpyAsync(d, p.data(), sizeof(float *) * a.nsh, hipMemcpyHostToDevice, c->stream));
-        a.sh = d;
+    const int nsh = 3 * C;
+    if (nsh) ST_REQUIRE(sh, ST_ERR_ARG, "pack_compressed: sh output is NULL");
+    char nm[32];
+    for (int i = 0; i < nsh; ++i) {
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        ta.src[14 + i] = col_or_null(t, nm);
     }
+    ta.ncol = 14 + nsh;
+    ta.rl = (ta.ncol + 3) & ~3;
+    ta.n = n;
+    ta.rows = wsT<float>(c, "chunk.rows", n * (uint64_t)ta.rl);
+    ChunkArgs a{};
+    a.rows = ta.rows;
+    a.rl = ta.rl;
+    a.nsh = nsh;
     a.n = n;
     a.order = order;
     a.chunk = chunk;
@@ -196,6 +242,7 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     a.sh_out = sh;
     const uint64_t nchunks = (n + 255) / 256;
     KTimer kt(c, "chunk.pack");
+    hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, c->stream, ta);
     hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();
 }

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""HBM-bound stages of the path at BASELINE config 3 (10M SH-3 splats, -r 0,45,0,
+--filterNaN -> .compressed.ply), each timed with HIP events on the library's stream
+and priced against the 8 TB/s HBM peak with its ALGORITHMIC bytes per splat:
+
+  transform (a3/a4)       440 B  read+write x,y,z, rot_0..3, scale_0..2, f_rest_0..44 (f32)
+  filter_finite (a6)      252 B  read 62 columns + write the kept index
+  permute_rows (a6)       496 B  gather 62 columns + write them
+  morton_order (a8)        92 B  SURVEY 8d: extents 12 + keys 12+4 + 4-pass 8-bit LSD on 8-B pairs 64
+  pack_compressed (a9/10) 301 B  gather 14+45 columns, write vertex 16 B + sh 45 B + chunk
+
+Prints one JSON object (also written to gpurun_out/paths.json)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
+
+import torch
+
+import splat_hip as sh
+
+HBM = 8.0e12
+
+
+def main(n=10_000_000, reps=5):
+    dev = torch.device('cuda', 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx = sh.Context(0)
+    ctx.set_stream(stream.cuda_stream)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1003)
+    names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+        ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3', 'nx', 'ny', 'nz']
+    cols = {k: torch.randn(n, generator=g, device=dev) for k in names}
+    # 0.1% of rows get a NaN/Inf in a random column
+    bad = torch.randperm(n, generator=g, device=dev)[: n // 1000]
+    which = torch.randint(0, len(names), (bad.numel(),), generator=g, device=dev)
+    for j, k in enumerate(names):
+        rows = bad[which == j]
+        cols[k][rows[: rows.numel() // 2]] = float('nan')
+        cols[k][rows[rows.numel() // 2:]] = float('inf')
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()  # warm
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        best = []
+        for _ in range(reps):
+            ev[0].record(stream)
+            fn()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            best.append(ev[0].elapsed_time(ev[1]))
+        return sorted(best)[len(best) // 2]
+
+    out = {'splats': n, 'hbm_peak_GBps': HBM / 1e9, 'stages': {}}
+
+    def report(name, ms, bytes_per_splat, rows=n):
+        gbs = bytes_per_splat * rows / (ms / 1e3) / 1e9
+        out['stages'][name] = {'ms': ms, 'alg_bytes_per_splat': bytes_per_splat, 'achieved_GBps': gbs,
+                               'frac_hbm': gbs / (HBM / 1e9)}
+
+    params = sh.action_params('rotate', (0, 45, 0))
+    report('transform', timed(lambda: ctx.dev_transform(cols, params)), 440)
+    idx = torch.empty(n, dtype=torch.int32, device=dev)
+    kept = [0]
+
+    def filt():
+        kept[0] = ctx.dev_filter_finite(cols, idx)
+    report('filter_finite', timed(filt), 62 * 4 + 4)
+    m = kept[0]
+    dst = {k: torch.empty(m, device=dev) for k in names}
+    report('permute_rows', timed(lambda: ctx.dev_permute_rows(cols, idx, m, dst)), 62 * 8, rows=m)
+    order = torch.empty(m, dtype=torch.int32, device=dev)
+
+    def morton():
+        order.copy_(torch.arange(m, dtype=torch.int32, device=dev))
+        ctx.dev_morton_order(dst['x'], dst['y'], dst['z'], order)
+    report('morton_order', timed(morton), 92, rows=m)
+    chunk = torch.empty((m + 255) // 256 * 18, device=dev)
+    vertex = torch.empty(m * 4, dtype=torch.int32, device=dev)
+    shb = torch.empty(m * 45, dtype=torch.uint8, device=dev)
+    pack_cols = {k: v for k, v in dst.items() if not k.startswith('n')}
+    report('pack_compressed', timed(lambda: ctx.dev_pack_compressed(pack_cols, order, chunk, vertex, shb)), 301,
+           rows=m)
+
+    # the whole config-3 device pipeline (inputs resident, outputs in HBM)
+    def pipeline():
+        ctx.dev_transform(cols, params)
+        mm = ctx.dev_filter_finite(cols, idx)
+        ctx.dev_permute_rows(cols, idx, mm, dst)
+        morton()
+        ctx.dev_pack_compressed(pack_cols, order, chunk, vertex, shb)
+    ms = timed(pipeline)
+    out['config3'] = {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'kept': m}
+    os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+    with open(os.path.join(ROOT, 'gpurun_out', 'paths.json'), 'w') as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == '__main__':
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000)
