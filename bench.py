@@ -206,6 +206,13 @@ def main():
     flops_per_launch = 2.0 * n * pal * D  # nearest-centroid dot products, one assign pass
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+    # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
+    # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
+    traffic, tsrc = None, None
+    tfile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_traffic.json')
+    if os.path.exists(tfile) and n == 10_000_000:
+        traffic = json.load(open(tfile))['hbm_bytes_per_launch']
+        tsrc = os.path.relpath(tfile, ROOT)
     out = {
         'metric': 'Msplats/sec PLY->SOG (SH-3, 10 k-means iters)',
         'value': value,
@@ -230,7 +237,9 @@ def main():
             'peak': MFMA_F16_DENSE_TFLOPS,
             'unit': 'TFLOP/s',
             'frac': (achieved / MFMA_F16_DENSE_TFLOPS) if achieved else None,
-            'traffic': None,
+            'traffic': traffic,
+            'traffic_unit': 'bytes per launch',
+            'traffic_source': tsrc,
             'algorithmic_flops_per_launch': flops_per_launch,
             'avg_launch_ms': avg_sweep_s * 1e3,
             'launches': sweep_launches,
