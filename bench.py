@@ -181,7 +181,8 @@ def main():
         elapsed = t.item()
     sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
     kstats = {}
-    for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum'):
+    for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum',
+                 'chunk.pack'):
         ms, cnt = ctx.kernel_stats(name)
         kstats[name] = {'avg_ms': ms / max(cnt, 1), 'launches': cnt}
     ctx.set_profiling(False)

@@ -15,6 +15,7 @@ struct State {
     uint32_t amb;     // ambiguous points this iteration (D > 1)
     uint32_t ties;    // exact-distance ties this iteration (D > 1)
     uint32_t overflow;  // ambiguous points whose candidate list overflowed (exact scan of all K)
+    uint32_t pairs;     // points whose candidates lie in two tile-halves (k_fixpair)
 };
 
 __host__ __device__ inline uint32_t fkey_(float f) {

@@ -234,7 +234,8 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
                                                const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
                                                const Bound bnd, uint32_t *__restrict__ labels,
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
-                                               uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand) {
+                                               uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
+                                               uint32_t *__restrict__ pair_pts, uint2 *__restrict__ pair_codes) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
     static_assert(STAGE_U4 % 256 == 0, "stage must split evenly over the workgroup");
     constexpr int PER_THREAD = STAGE_U4 / 256;
@@ -256,14 +257,17 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     // being folded into v_min plus two NaN canonicalisations
     float ninf;
     asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(ninf));
-    // per point tile: top-2 of the tile minima seen by this lane-half, and the tile of the best
-    float m1[PT], m2[PT], th[PT];
-    uint32_t t1[PT];
+    // per point tile: top-3 of the tile minima seen by this lane-half and the tiles of the
+    // best two
+    float m1[PT], m2[PT], m3[PT], th[PT];
+    uint32_t t1[PT], t2[PT];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         m1[t] = __builtin_inff();
         m2[t] = __builtin_inff();
+        m3[t] = __builtin_inff();
         t1[t] = 0;
+        t2[t] = 0;
         th[t] = -__builtin_inff();
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -272,9 +276,9 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     }
 
     // slice q of the epilogue of scores sc (point tile t, centroid tile ctile): the minimum
-    // of the lane-half's 16 rows (v_min3 tree), then, in the last slice, the running top-2
-    // of tile minima.  Two rows of one tile never compete here: k_fixrow settles the
-    // winning tile's rows with the exact distance.
+    // of the lane-half's 16 rows (v_min3 tree), then, in the last slice, the running top-3
+    // of tile minima.  Two rows of one tile never compete here: k_fixrow / k_fixpair settle
+    // the winning tile-halves' rows with the exact distance.
     float mn = 0.f;
     auto slice = [&](const f32x16 &sc, int t, uint32_t ctile, auto qc) {
         constexpr int q = decltype(qc)::value;
@@ -284,8 +288,15 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
         for (int r = (q == 0 ? 1 : r0); r < r1; ++r) mn = fminf(mn, sc[r]);
         if (q == KS - 1) {
             if (MODE == 0) {
+                // selects on scalar temporaries (a select between two array elements is
+                // lowered through scratch memory)
+                const bool lt1 = mn < m1[t], lt2 = mn < m2[t];
+                const uint32_t o1 = t1[t], o2 = t2[t];
+                const uint32_t n2 = lt2 ? ctile : o2;
+                t2[t] = lt1 ? o1 : n2;
+                t1[t] = lt1 ? ctile : o1;
+                m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], mn);
                 m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], mn);
-                t1[t] = (mn < m1[t]) ? ctile : t1[t];
                 m1[t] = fminf(m1[t], mn);
             } else if (mn <= th[t]) {
                 // candidates are rare (a handful of the K centroids per point)
@@ -372,22 +383,42 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     const float cm = __builtin_bit_cast(float, *cmax_bits);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-        // merge the two lane-halves of the point; code = (tile, lane-half) of the minimum
-        const float om1 = __shfl_xor(m1[t], 32, 64), om2 = __shfl_xor(m2[t], 32, 64);
-        const uint32_t ot1 = __shfl_xor(t1[t], 32, 64);
-        const float nm1 = fminf(m1[t], om1);
-        const float nm2 = fminf(fmaxf(m1[t], om1), fminf(m2[t], om2));
-        const uint32_t code = (m1[t] <= om1) ? (t1[t] * 2u + (uint32_t)h) : (ot1 * 2u + (uint32_t)(h ^ 1));
+        // merge the two lane-halves' top-3 (sorted) into the point's top-3; codes =
+        // (tile, lane-half) of the best two
+        const float a1 = m1[t], a2 = m2[t], a3 = m3[t];
+        const float b1 = __shfl_xor(a1, 32, 64), b2 = __shfl_xor(a2, 32, 64), b3 = __shfl_xor(a3, 32, 64);
+        const uint32_t ca1 = t1[t] * 2u + (uint32_t)h, ca2 = t2[t] * 2u + (uint32_t)h;
+        const uint32_t cb1 = __shfl_xor(ca1, 32, 64), cb2 = __shfl_xor(ca2, 32, 64);
+        const float nm1 = fminf(a1, b1);
+        const float nm2 = fminf(fmaxf(a1, b1), fminf(a2, b2));
+        const float nm3 = fminf(fminf(a3, b3), fminf(fmaxf(a2, b1), fmaxf(a1, b2)));
+        const uint32_t code1 = (a1 <= b1) ? ca1 : cb1;
+        const uint32_t code2 = (a1 <= b1) ? ((a2 <= b1) ? ca2 : cb1) : ((b2 < a1) ? cb2 : ca1);
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
-        bool is_amb = false;
+        bool is_amb = false, is_pair = false;
         if (h == 0 && p < npts) {
             const float W = wbound(bnd, pnorm[p], cm);
             if (nm2 > nm1 + W) {
-                labels[p] = code;  // k_fixrow turns the code into the centroid index
+                labels[p] = code1;  // k_fixrow turns the code into the centroid index
+            } else if (nm3 > nm1 + W) {
+                is_pair = true;  // every candidate lies in the two best tile-halves
+                labels[p] = 0xfffffffeu;
             } else {
                 is_amb = true;
                 labels[p] = 0xffffffffu;
                 thr[p] = nm1 + W;
+            }
+        }
+        const uint64_t pmask = __ballot(is_pair);
+        if (pmask) {
+            uint32_t base = 0;
+            const int leader = __builtin_ctzll(pmask);
+            if (lane == leader) base = atomicAdd(&st->pairs, (uint32_t)__popcll(pmask));
+            base = __shfl(base, leader, 64);
+            if (is_pair) {
+                const uint32_t i = base + __popcll(pmask & ((1ull << lane) - 1));
+                pair_pts[i] = p;
+                pair_codes[i] = make_uint2(code1, code2);
             }
         }
         const uint64_t mask = __ballot(is_amb);
@@ -449,17 +480,15 @@ __device__ inline double ref_dist(const float *__restrict__ crow, const float *_
 // the lowest upper end, it is the reference's answer.  Otherwise the candidate rows take
 // the exact f64 distance of kd-tree.ts:26-35; a unique minimum decides, an exact tie
 // goes to the KdTree walk (kd_resolve_ties).
-__global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
-                                                const float *__restrict__ caos, int k, uint32_t n,
-                                                uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
-                                                State *st) {
+// G lanes per point (16 rows of one tile-half, or 32 rows of two), lane r scoring row
+// r % 16 of tile-half code(r / 16)
+template <int G>
+__device__ inline void fix_group(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
+                                 const float *__restrict__ caos, int k, uint64_t p, int r, uint32_t code,
+                                 uint32_t *__restrict__ labels, uint32_t *__restrict__ ties, State *st) {
     const int ld = aos_ld(d);
-    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-    const int r = threadIdx.x & 15;
-    if (p >= n) return;  // uniform per 16-lane group
-    const uint32_t code = labels[p];
-    if (code == 0xffffffffu) return;  // ambiguous: k_exact decides
-    const uint32_t c = (code >> 1) * 32 + 4 * (code & 1) + (r & 3) + 8 * (r >> 2);
+    const int rr = r & 15;
+    const uint32_t c = (code >> 1) * 32 + 4 * (code & 1) + (rr & 3) + 8 * (rr >> 2);
     const bool valid = c < (uint32_t)k;
     const float *prow = aos + p * ld;
     // f32 screen: |s - T| <= (d + 2) u T for fma accumulation of fl(c - p)^2 (u = 2^-24), plus
@@ -468,7 +497,7 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
     if (valid) {
         // padded dimensions hold 0 in both rows: they add +0
         const float4 *p4 = reinterpret_cast<const float4 *>(prow);
-        const float2 *crow = cfix + (uint64_t)(code >> 1) * 2 * (ld / 2) * 16 + (uint64_t)(code & 1) * (ld / 2) * 16 + r;
+        const float2 *crow = cfix + (uint64_t)(code >> 1) * 2 * (ld / 2) * 16 + (uint64_t)(code & 1) * (ld / 2) * 16 + rr;
         for (int q = 0; q < ld / 4; ++q) {
             const float4 pv = p4[q];
             const float2 c0 = crow[(2 * q) * 16], c1 = crow[(2 * q + 1) * 16];
@@ -487,15 +516,15 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
     const float hi = valid ? s + (s * rel + ab) : __builtin_inff();
     float mh = hi;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
+    for (int o = G / 2; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
     bool cand = valid && lo <= mh;  // NaN/inf screens fall through to the exact path
     uint32_t ncand = cand ? 1u : 0u;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
+    for (int o = G / 2; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
     if (ncand == 1) {
         uint32_t w = cand ? c : 0xffffffffu;
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
+        for (int o = G / 2; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
         if (r == 0) labels[p] = w;
         return;
     }
@@ -504,7 +533,7 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
     double best = mine;
     uint32_t bidx = c;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
+    for (int o = G / 2; o > 0; o >>= 1) {
         const double ob = __shfl_xor(best, o, 64);
         const uint32_t oi = __shfl_xor(bidx, o, 64);
         if (ob < best || (ob == best && oi < bidx)) {
@@ -515,11 +544,37 @@ __global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, i
     const uint32_t eq = (cand && mine == best) ? 1u : 0u;
     uint32_t cnt = eq;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    for (int o = G / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if (r == 0) {
         labels[p] = bidx;  // provisional on a tie; the KdTree pass decides
         if (cnt > 1) ties[atomicAdd(&st->ties, 1u)] = (uint32_t)p;
     }
+}
+
+// decided points (one tile-half): 16 lanes per point
+__global__ __launch_bounds__(256) void k_fixrow(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
+                                                const float *__restrict__ caos, int k, uint32_t n,
+                                                uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                State *st) {
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    if (p >= n) return;  // uniform per 16-lane group
+    const uint32_t code = labels[p];
+    if (code >= 0xfffffffeu) return;  // pair (k_fixpair) or ambiguous (k_exact)
+    fix_group<16>(aos, d, cfix, caos, k, p, threadIdx.x & 15, code, labels, ties, st);
+}
+
+// pair points (two tile-halves): 32 lanes per point
+__global__ __launch_bounds__(256) void k_fixpair(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
+                                                 const float *__restrict__ caos, int k,
+                                                 const uint32_t *__restrict__ pair_pts,
+                                                 const uint2 *__restrict__ pair_codes, uint32_t npairs,
+                                                 uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                 State *st) {
+    const uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 5;
+    if (i >= npairs) return;  // uniform per 32-lane group
+    const int r = threadIdx.x & 31;
+    const uint2 cc = pair_codes[i];
+    fix_group<32>(aos, d, cfix, caos, k, pair_pts[i], r, r < 16 ? cc.x : cc.y, labels, ties, st);
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
@@ -607,12 +662,13 @@ template <int KS>
 struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
                      const float *pnorm, const uint32_t *cmax, const Bound &bnd, uint32_t *labels, float *thr,
-                     uint32_t *amb, State *st) {
+                     uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
         const uint32_t per_block = 4 * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(256), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
-                           cmax, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr);
+                           cmax, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
+                           pair_codes);
         ST_LAUNCH_CHECK();
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
@@ -622,7 +678,8 @@ struct Sweep {
         KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(256), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const uint32_t *)nullptr, bnd, (uint32_t *)nullptr, thr_slot,
-                           (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand);
+                           (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
+                           (uint2 *)nullptr);
         ST_LAUNCH_CHECK();
     }
 };
@@ -707,18 +764,27 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
                        cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix);
     ST_LAUNCH_CHECK();
-    ST_HIP(hipMemsetAsync(&dstate->amb, 0, 12, c->stream));  // amb + ties + overflow
+    auto *pair_pts = wsT<uint32_t>(c, "kn.pairpts", n);
+    auto *pair_codes = wsT<uint2>(c, "kn.paircodes", n);
+    ST_HIP(hipMemsetAsync(&dstate->amb, 0, 16, c->stream));  // amb + ties + overflow + pairs
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
-                                        thr, amb, dstate)));
+                                        thr, amb, dstate, pair_pts, pair_codes)));
     {
         KTimer kt(c, "kn.fixrow");
         hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cfix,
                            caos, k, (uint32_t)n, labels, ties, dstate);
         ST_LAUNCH_CHECK();
     }
-    mark(c, "kn.assign");
     ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t npair = h->pairs;
+    if (npair) {
+        KTimer kt(c, "kn.fixpair");
+        hipLaunchKernelGGL(k_fixpair, dim3((npair * 32 + 255) / 256), dim3(256), 0, c->stream, aos, d, cfix, caos, k,
+                           pair_pts, pair_codes, npair, labels, ties, dstate);
+        ST_LAUNCH_CHECK();
+    }
+    mark(c, "kn.assign");
     const uint32_t namb = h->amb;
     if (namb) {
         const uint32_t atiles = (namb + 31) / 32;
@@ -739,10 +805,19 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
         }
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
+        if (getenv("ST_DEBUG")) {  // candidate-count histogram of the ambiguous points
+            std::vector<uint32_t> cc(namb);
+            ST_HIP(hipMemcpy(cc.data(), cand_cnt, namb * 4, hipMemcpyDeviceToHost));
+            uint64_t hist[6] = {0, 0, 0, 0, 0, 0};
+            for (uint32_t v : cc) ++hist[v < 5 ? v : 5];
+            fprintf(stderr, "[st kmeans] candidates per ambiguous point: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5+:%llu\n",
+                    (unsigned long long)hist[0], (unsigned long long)hist[1], (unsigned long long)hist[2],
+                    (unsigned long long)hist[3], (unsigned long long)hist[4], (unsigned long long)hist[5]);
+        }
     }
     if (getenv("ST_DEBUG"))
-        fprintf(stderr, "[st kmeans] n=%llu k=%d ambiguous=%u ties=%u overflow=%u sigma=%g\n", (unsigned long long)n,
-                k, namb, h->ties, h->overflow, sigma);
+        fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
+                (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
     // exact ties from k_fixrow and k_exact: the KdTree walk decides
     if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
     mark(c, "kn.exact");
