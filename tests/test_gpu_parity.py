@@ -138,3 +138,22 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters):
     assert rc == 0 and used == oused
     same_bits(labels, olabels)
     same_bits(cent, ocent)
+
+
+@pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
+def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac):
+    """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
+    hold tiny members, so the sequential f64 sum rounds -- a few events (k_sum1d_replay) or
+    many (the sequential fallback)."""
+    rng = np.random.default_rng(77)
+    n = 300_000
+    cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
+    for c in cols:
+        tiny = rng.random(n) < tiny_frac
+        c[tiny] *= np.float32(1e-9)
+    draws = oracle.mulberry32(5, 1 << 14)
+    cent, labels, used = ctx.cluster1d(cols, 4, draws)
+    rc, ocent, olabels, oused = oracle.cluster1d(cols, 4, draws)
+    assert rc == 0 and used == oused
+    assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
+    assert np.array_equal(labels, olabels)
