@@ -176,9 +176,10 @@ int st_dev_kmeans_assign(st_ctx *ctx, const float *const *cols, int32_t d, uint6
 /* per (segment, dim, cluster): f64 sum in ascending point order, sum|x|, smallest ulp exponent; counts */
 int st_dev_kmeans_partials(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n, int32_t nseg, int32_t k,
                            const uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts);
-/* continue running[i] (pair = cluster*d + dim) over this rank's members of segment seg */
+/* continue running[i] (pair = cluster*d + dim) over this rank's members of segment seg, exactly as the
+ * sequential f64 sum; emin / sabs are the global (reduced) partials [d][k] */
 int st_dev_kmeans_seqsum(st_ctx *ctx, int32_t d, int32_t k, int32_t seg, const uint32_t *pairs, uint32_t npairs,
-                         double *running);
+                         double *running, const int32_t *emin, const double *sabs);
 /* global (reduced) partials -> centroids where the sum is certified exact; the rest listed in pending
  * (ascending pair order, *npending on the host); clusters with count 0 are left untouched */
 int st_dev_kmeans_finish(st_ctx *ctx, int32_t d, int32_t k, const double *sums, const double *sabs,

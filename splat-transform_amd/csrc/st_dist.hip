@@ -22,6 +22,7 @@
 
 #include "st_jsmath.h"
 #include "st_kmeans.h"
+#include "st_replay.h"
 
 namespace st {
 namespace {
@@ -146,11 +147,31 @@ __global__ __launch_bounds__(64) void k_seqsum_nd(const float *__restrict__ aos,
     running[p] = s;
 }
 
-// 1-D: one wave per pending cluster, lane 0 walks the contiguous label-sorted values
+// 1-D: the exact replay (st_replay.h) of each pending cluster's sum over this segment,
+// starting from its running value; one RT-thread block per pair.  Pairs the replay
+// cannot take are flagged for k_seqsum_1d.
+__global__ __launch_bounds__(RT) void k_seqsum_1d_replay(const uint32_t *__restrict__ vals,
+                                                         const uint32_t *__restrict__ start, int k, int seg,
+                                                         const uint32_t *__restrict__ pairs,
+                                                         double *__restrict__ running,
+                                                         const int32_t *__restrict__ emin,
+                                                         const double *__restrict__ sabs, __int128 *__restrict__ cand_all,
+                                                         uint32_t *__restrict__ flag) {
+    const uint32_t p = blockIdx.x, cl = pairs[p];
+    const uint32_t sc = (uint32_t)seg * k + cl;
+    double out = 0;
+    const bool ok = replay_sum(vals, start[sc], start[sc + 1], emin[cl], sabs[cl], running[p],
+                               cand_all + (uint64_t)p * CAND_MAX, &out);
+    if (threadIdx.x != 0) return;
+    flag[p] = ok ? 0u : 1u;
+    if (ok) running[p] = out;
+}
+
+// 1-D fallback: one wave per flagged pending cluster, lane 0 walks the contiguous values
 __global__ __launch_bounds__(64) void k_seqsum_1d(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
                                                   int k, int seg, const uint32_t *__restrict__ pairs,
-                                                  double *__restrict__ running) {
-    if (threadIdx.x != 0) return;
+                                                  const uint32_t *__restrict__ flag, double *__restrict__ running) {
+    if (threadIdx.x != 0 || !flag[blockIdx.x]) return;
     const uint32_t p = blockIdx.x;
     const uint32_t sc = (uint32_t)seg * k + pairs[p];
     uint32_t opaque0;  // keeps the loads on the vector path (see k_sum1d_seq)
@@ -279,7 +300,8 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
     c->ds_n = n;
 }
 
-void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running) {
+void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running,
+                 const int32_t *emin, const double *sabs) {
     ST_REQUIRE(c->ds_d == d && c->ds_k == k && seg >= 0 && seg < c->ds_nseg, ST_ERR_ARG,
                "kmeans seqsum: no matching partials on this context");
     if (!npairs) return;
@@ -287,7 +309,13 @@ void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32
     auto *payload = wsT<uint32_t>(c, "ds.payload", n);
     auto *start = wsT<uint32_t>(c, "ds.start", nk + 1);
     if (d == 1) {
-        hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, running);
+        auto *cand = wsT<__int128>(c, "ds.cands", (size_t)npairs * CAND_MAX);
+        auto *flag = wsT<uint32_t>(c, "ds.sflag", npairs);
+        hipLaunchKernelGGL(k_seqsum_1d_replay, dim3(npairs), dim3(RT), 0, c->stream, payload, start, k, seg, pairs,
+                           running, emin, sabs, cand, flag);
+        ST_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, flag,
+                           running);
     } else {
         auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
         hipLaunchKernelGGL(k_seqsum_nd, dim3((npairs + 63) / 64), dim3(64), 0, c->stream, aos, d, payload, start, k,

@@ -158,7 +158,8 @@ void dist_prepare(st_ctx *c, const float *const *cols, int d, uint64_t n);
 void dist_assign(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen, uint32_t *labels);
 void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
                    double *sums, double *sabs, int32_t *emin, uint32_t *counts);
-void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running);
+void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running,
+                 const int32_t *emin, const double *sabs);
 uint32_t dist_finish(st_ctx *c, int d, int k, const double *sums, const double *sabs, const int32_t *emin,
                      const uint32_t *counts, float *cen, uint32_t *pending);
 void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npairs, const double *running,

@@ -404,11 +404,11 @@ int st_dev_kmeans_partials(st_ctx *c, const float *const *cols, int32_t d, uint6
 }
 
 int st_dev_kmeans_seqsum(st_ctx *c, int32_t d, int32_t k, int32_t seg, const uint32_t *pairs, uint32_t npairs,
-                         double *running) {
+                         double *running, const int32_t *emin, const double *sabs) {
     return guarded([&] {
-        ST_ARG(c && (npairs == 0 || (pairs && running)), "bad argument");
+        ST_ARG(c && (npairs == 0 || (pairs && running && emin && sabs)), "bad argument");
         use_device(c);
-        dist_seqsum(c, d, k, seg, pairs, npairs, running);
+        dist_seqsum(c, d, k, seg, pairs, npairs, running, emin, sabs);
     });
 }
 

@@ -139,8 +139,8 @@ class HipOps:
         self.ctx.dev_kmeans_partials(pts, nseg, k, labels, sums, sabs, emin, counts)
         return sums, sabs, emin, counts
 
-    def seqsum(self, d, k, seg, pairs, running):
-        self.ctx.dev_kmeans_seqsum(d, k, seg, pairs, running)
+    def seqsum(self, d, k, seg, pairs, running, emin, sabs):
+        self.ctx.dev_kmeans_seqsum(d, k, seg, pairs, running, emin, sabs)
 
     def finish(self, d, k, sums, sabs, emin, counts, cen):
         pending = self.empty((d * k,), torch.int32)
@@ -286,7 +286,7 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
             running = ops.zeros((pending.numel(),), torch.float64)
             for r, seg in P.segments():
                 if r == comm.rank:
-                    ops.seqsum(d, k, seg, pending, running)
+                    ops.seqsum(d, k, seg, pending, running, E, A)
                 comm.broadcast(running, r)
             ops.average(d, k, pending, running, C, cen)
         empty = (C == 0).nonzero().flatten().tolist()

@@ -342,9 +342,10 @@ class Context:
                                            ctypes.c_int32(k), _ptr(labels), _ptr(sums), _ptr(sabs), _ptr(emin),
                                            _ptr(counts)))
 
-    def dev_kmeans_seqsum(self, d, k, seg, pairs, running):
+    def dev_kmeans_seqsum(self, d, k, seg, pairs, running, emin, sabs):
         check(lib().st_dev_kmeans_seqsum(self.h, ctypes.c_int32(d), ctypes.c_int32(k), ctypes.c_int32(seg),
-                                         _ptr(pairs), ctypes.c_uint32(len(pairs)), _ptr(running)))
+                                         _ptr(pairs), ctypes.c_uint32(len(pairs)), _ptr(running), _ptr(emin),
+                                         _ptr(sabs)))
 
     def dev_kmeans_finish(self, d, k, sums, sabs, emin, counts, centroids, pending):
         np_ = ctypes.c_uint32(0)

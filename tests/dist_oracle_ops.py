@@ -74,7 +74,7 @@ class OracleOps:
         self.vals, self.d = vals, d
         return (torch.from_numpy(sums), torch.from_numpy(sabs), torch.from_numpy(emin), torch.from_numpy(counts))
 
-    def seqsum(self, d, k, seg, pairs, running):
+    def seqsum(self, d, k, seg, pairs, running, emin=None, sabs=None):
         for p, pair in enumerate(pairs.tolist()):
             c, j = divmod(pair, d)
             acc = float(running[p])
