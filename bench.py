@@ -232,7 +232,7 @@ def main():
                    'splats_per_gpu': n, 'splats_total': n * world, 'sh_bands': 3, 'palette_size': pal,
                    'iterations': args.iters, 'parallelism': f'rowshard{world}' if world > 1 else 'single'},
         'roofline': {
-            'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-2 per splat)',
+            'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-3 tile minima per splat)',
             'bound': 'mfma',
             'achieved': achieved,
             'peak': MFMA_F16_DENSE_TFLOPS,

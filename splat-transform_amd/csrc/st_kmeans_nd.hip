@@ -12,21 +12,23 @@
 // Products are exact in f32, so (|x - x~| <= 2^-11 |x| + e_abs)
 //     |score_mfma - score| <= E = A |p| cmax + B cmax^2 + e_abs-terms
 // with e_abs = 2^-25 when the matrix cores keep fp16 denormals (probed once per
-// context) and 2^-14 otherwise.  A running top-2 per point in the epilogue (one
-// v_med3 + one v_min per score, one compare per tile to record the tile of the
-// minimum) decides the point when m2 > m1 + W_p (W_p = 2E + 2 delta_p, delta_p =
-// the reference's own f64 rounding); k_fixrow then finds the row inside that
-// tile with the exact f64 distance.  Otherwise the point is
-// ambiguous (~11% at SH3): a second sweep collects every centroid with
+// context) and 2^-14 otherwise.  The epilogue keeps, per point and lane-half, the
+// running top-3 of the 16-row tile minima (a v_min3 tree per tile, then two v_med3 +
+// one v_min) and the tiles of the best two.  m2 > m1 + W_p (W_p = 2E + 2 delta_p,
+// delta_p = the reference's own f64 rounding) decides the point: k_fixrow finds the
+// row inside the best tile-half with the exact f64 distance.  m3 > m1 + W_p puts
+// every candidate in the best two tile-halves: k_fixpair settles those 32 rows.
+// Otherwise the point is ambiguous (~2% at SH3): a second sweep collects every centroid with
 // score <= m1 + W_p (a superset of the exact argmin set) and the exact f64
 // distance of kd-tree.ts:26-35 decides; exact ties go to the KdTree walk.
 //
 // Tiling (gfx950, wave64): workgroup = 4 waves, each wave owns PT = 4 tiles of
 // 32 points whose B fragments stay in VGPRs for the whole sweep; 32-row
 // centroid tiles (pre-laid-out in fragment order, KS x 1 KiB each) stream
-// through a double-buffered LDS ring, CT_STAGE tiles per barrier.  The C/D
+// through a double-buffered LDS ring, CT_STAGE tiles per barrier, filled by
+// global_load_lds DMA (no VGPRs held for the prefetch).  The C/D
 // layout puts the point on the lane (col = lane & 31) and 16 centroid rows per
-// lane-half in registers, so the top-2 update is lane-local.
+// lane-half in registers, so the top-3 update is lane-local.
 #include <cmath>
 #include <utility>
 
@@ -51,6 +53,8 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int PT = 4;          // point tiles per wave
+constexpr int NW = 4;          // waves per workgroup (they share the LDS centroid stages)
+constexpr int WG = 64 * NW;    // threads per workgroup
 constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
 
@@ -220,16 +224,16 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
 }
 
 // ---- the MFMA sweep -------------------------------------------------------------
-// MODE 0: main assign (top-2; decide or flag ambiguous)
+// MODE 0: main assign (top-3 of tile minima; decided / pair / ambiguous)
 // MODE 1: collect candidates of ambiguous points (score <= thr)
 //
 // Software pipeline over "slots" (one centroid tile x one point tile = KS MFMAs): the
 // epilogue of the previous slot is cut into KS slices, slice s issued right behind
 // MFMA s of this slot and fenced with sched_barrier, so each MFMA's 32 cycles on the
-// matrix pipe cover ~10 VALU ops of the same wave.  Each lane keeps two top-2 chains
-// per point tile (rows 0-7 and 8-15 of its half) for instruction-level parallelism.
+// matrix pipe cover ~10 VALU ops of the same wave.  Occupancy is 2 waves per SIMD
+// (~190 VGPRs: B fragments 48, score buffers 64, A ping-pong 24, top-3 state 20).
 template <int KS, int MODE>
-__global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
+__global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
                                                const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
                                                const Bound bnd, uint32_t *__restrict__ labels,
@@ -237,11 +241,11 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
                                                uint32_t *__restrict__ pair_pts, uint2 *__restrict__ pair_codes) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
-    static_assert(STAGE_U4 % 256 == 0, "stage must split evenly over the workgroup");
-    constexpr int PER_THREAD = STAGE_U4 / 256;
+    constexpr int PER_THREAD = (STAGE_U4 + WG - 1) / WG;
+    static_assert(STAGE_U4 % 64 == 0, "a stage is whole wave-instructions");
     __shared__ uint4 lds[2][STAGE_U4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const uint32_t tile0 = (blockIdx.x * 4 + w) * PT;
+    const uint32_t tile0 = (blockIdx.x * NW + w) * PT;
 
     f16x8 b[PT][KS];
 #pragma unroll
@@ -290,14 +294,18 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
             if (MODE == 0) {
                 // selects on scalar temporaries (a select between two array elements is
                 // lowered through scratch memory)
-                const bool lt1 = mn < m1[t], lt2 = mn < m2[t];
-                const uint32_t o1 = t1[t], o2 = t2[t];
-                const uint32_t n2 = lt2 ? ctile : o2;
-                t2[t] = lt1 ? o1 : n2;
-                t1[t] = lt1 ? ctile : o1;
-                m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], mn);
-                m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], mn);
-                m1[t] = fminf(m1[t], mn);
+                // a tile minimum >= m3 leaves the top-3 unchanged; late in the sweep most
+                // wave-wide slots have none below it, so the update is skipped
+                if (__builtin_expect(__ballot(mn < m3[t]) != 0, 0)) {
+                    const bool lt1 = mn < m1[t], lt2 = mn < m2[t];
+                    const uint32_t o1 = t1[t], o2 = t2[t];
+                    const uint32_t n2 = lt2 ? ctile : o2;
+                    t2[t] = lt1 ? o1 : n2;
+                    t1[t] = lt1 ? ctile : o1;
+                    m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], mn);
+                    m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], mn);
+                    m1[t] = fminf(m1[t], mn);
+                }
             } else if (mn <= th[t]) {
                 // candidates are rare (a handful of the K centroids per point)
                 const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -315,8 +323,20 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
 
     // ctiles is a multiple of CT_STAGE (the tail is padded with never-winning rows)
     const uint32_t nstages = ctiles / CT_STAGE;
+    // centroid stages move global -> LDS by DMA (global_load_lds_dwordx4: no VGPR staging,
+    // one wave-instruction fills 1 KiB at a wave-uniform base + 16 B per lane)
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(w) * 64;
+    auto stage_in = [&](int buf, uint32_t sg_) {
+        const uint4 *src = cfrag + (uint64_t)sg_ * STAGE_U4 + threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < PER_THREAD; ++q) lds[0][threadIdx.x + q * 256] = cfrag[threadIdx.x + q * 256];
+        for (int q = 0; q < PER_THREAD; ++q)
+            if (STAGE_U4 % WG == 0 || wbase + q * WG < (uint32_t)STAGE_U4)
+                __builtin_amdgcn_global_load_lds(src + q * WG,
+                                                 (__attribute__((address_space(3))) void *)&lds[buf][wbase + q * WG],
+                                                 16, 0, 0);
+    };
+    stage_in(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // one score buffer per point tile: slot t of a centroid tile writes buf[t] while the
     // epilogue drains buf[(t + 1) % PT], written PT - 1 slots earlier -- long enough for
@@ -330,11 +350,8 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
     uint32_t tile_prev = 0;  // centroid tile of the previous ct iteration
     for (uint32_t sg = 0; sg < nstages; ++sg) {
         const int cur = sg & 1;
-        uint4 nxt[PER_THREAD];
-        const uint32_t nbase = (sg + 1) * STAGE_U4;
-#pragma unroll
-        for (int q = 0; q < PER_THREAD; ++q)
-            nxt[q] = (sg + 1 < nstages) ? cfrag[nbase + threadIdx.x + q * 256] : make_uint4(0, 0, 0, 0);
+        // the other buffer was last read in stage sg - 1, which ended with a barrier
+        if (sg + 1 < nstages) stage_in(cur ^ 1, sg + 1);
         // A fragments ping-pong between two register sets: tile ct + 1 is read from LDS while
         // tile ct's MFMAs run (the read at the stage's last tile re-reads it, unused)
         f16x8 a0[KS], a1[KS];
@@ -367,9 +384,7 @@ __global__ __launch_bounds__(256) void k_sweep(const uint4 *__restrict__ pfrag, 
             tile_step(ct + 1, a1, a0);
         }
         if (sg + 1 < nstages) {
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < PER_THREAD; ++q) lds[cur ^ 1][threadIdx.x + q * 256] = nxt[q];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
     }
@@ -663,20 +678,20 @@ struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
                      const float *pnorm, const uint32_t *cmax, const Bound &bnd, uint32_t *labels, float *thr,
                      uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
-        const uint32_t per_block = 4 * PT;
+        const uint32_t per_block = NW * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
-        hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(256), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
+        hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(WG), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
                            cmax, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
                            pair_codes);
         ST_LAUNCH_CHECK();
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
                         uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
-        const uint32_t per_block = 4 * PT;
+        const uint32_t per_block = NW * PT;
         const dim3 grid((atiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.collect");
-        hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(256), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
+        hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const uint32_t *)nullptr, bnd, (uint32_t *)nullptr, thr_slot,
                            (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
                            (uint2 *)nullptr);
