@@ -26,6 +26,12 @@
  *                                           labels                              write-sog.ts:69-88
  *   st_dev_sog_scatter / _shn_centroids     one shard's texels of writeSog      write-sog.ts:142-239,
  *                                                                               :319-348
+ *   st_webp_lossless / st_dev_webp_lossless WebPEncodeLosslessRGBA (libwebp)   lib/webp_encode.c:19-29,
+ *                                                                               utils/webp.ts:19-41
+ *   st_dev_crc32                            Crc.update / value                  serialize/crc.ts:1-28
+ *   st_zip_store                            ZipWriter (store, descriptors)      serialize/zip-writer.ts:35-135
+ *   st_sog_meta_json                        JSON.stringify(meta)                write-sog.ts:271-293,350-361
+ *   st_sog_bundle / st_dev_sog_bundle       writeSog to a .sog bundle           write-sog.ts:110-140,361-366
  *
  * Conventions
  *  - Columns are SoA float32 arrays of n rows (the reference's Float32Array
@@ -197,6 +203,36 @@ int st_dev_sog_scatter(st_ctx *ctx, const st_table *local, const uint32_t *pos, 
                        st_sog_meta *meta, const st_sog_textures *out);
 int st_dev_sog_shn_centroids(st_ctx *ctx, const uint8_t *codebook_labels, int32_t sh_coeffs, int32_t palette,
                              uint8_t *out);
+
+/* ---- WebP lossless, CRC-32, the .sog container ---------------
+ * WebP: a valid lossless VP8L stream (predictor transform + canonical prefix
+ * codes) that decodes to exactly the input RGBA; parity is at the decoded-pixel
+ * level, the bytes differ from libwebp's.  Images are 1..16384 on each side. */
+/* worst-case .webp size for a width x height image (0 if out of range) */
+uint64_t st_webp_max_size(int32_t width, int32_t height);
+/* device RGBA8 (stride bytes per row, multiple of 4) -> device .webp bytes (cap >= st_webp_max_size) */
+int st_dev_webp_lossless(st_ctx *ctx, const uint8_t *rgba, int32_t width, int32_t height, int32_t stride,
+                         uint8_t *out, uint64_t cap, uint64_t *size);
+/* host form of WebPEncodeLosslessRGBA: *out is malloc'd, release with st_free */
+int st_webp_lossless(st_ctx *ctx, const uint8_t *rgba, int32_t width, int32_t height, int32_t stride,
+                     uint8_t **out, uint64_t *size);
+/* zlib-compatible CRC-32 of n device bytes, continuing from crc_in (0 = fresh; crc.ts value()) */
+int st_dev_crc32(st_ctx *ctx, const uint8_t *data, uint64_t n, uint32_t crc_in, uint32_t *out);
+/* host: the store-only ZIP of zip-writer.ts (entries in order, CRCs given); *out malloc'd */
+int st_zip_store(const char *const *names, const uint8_t *const *data, const uint64_t *sizes,
+                 const uint32_t *crcs, int32_t count, uint16_t dos_time, uint16_t dos_date,
+                 uint8_t **out, uint64_t *out_size);
+/* host: meta.json text of writeSog (JS number formatting); *out malloc'd, NUL-terminated */
+int st_sog_meta_json(const st_sog_meta *meta, uint64_t count, char **out, uint64_t *out_size);
+/* the .sog archive of textures resident on the device (st_dev_sog's outputs):
+ * WebP encode + CRC on the device, ZIP layout on the host.  dos_time/dos_date are
+ * the ZipWriter's clock fields (zip-writer.ts:39-41).  *out malloc'd (st_free). */
+int st_dev_sog_bundle(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
+                      uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);
+/* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */
+int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
+                  uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);
+void st_free(void *p);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "st_internal.h"
+#include "st_webp.h"
 
 namespace st {
 namespace {
@@ -214,6 +215,35 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
             to_host(c, out->shn_centroids, dt.shn_centroids, (uint64_t)cw * chh * 4);
         }
         ST_HIP(hipStreamSynchronize(c->stream));
+        if (used) *used = u;
+    });
+}
+
+// writeSog to a .sog bundle (write-sog.ts:110-370 with the ZipWriter of :112-114):
+// the archive bytes, malloc'd (st_free)
+int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                  uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
+    return guarded_h([&] {
+        ST_ARGH(c && t && out && out_size, "NULL argument");
+        use_device(c);
+        DevTable d = upload(c, t, {}, "h.s");
+        const int C = sh_coeffs_of(t);
+        int32_t W, H, pal, cw, chh;
+        ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
+        const uint64_t tex = (uint64_t)W * H * 4;
+        st_sog_textures dt{};
+        dt.means_l = wsT<uint8_t>(c, "h.s.ml", tex);
+        dt.means_u = wsT<uint8_t>(c, "h.s.mu", tex);
+        dt.quats = wsT<uint8_t>(c, "h.s.q", tex);
+        dt.scales = wsT<uint8_t>(c, "h.s.sc", tex);
+        dt.sh0 = wsT<uint8_t>(c, "h.s.sh0", tex);
+        if (C) {
+            dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
+            dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
+        }
+        st_sog_meta meta{};
+        const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, &meta, &dt);
+        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, out, out_size);
         if (used) *used = u;
     });
 }

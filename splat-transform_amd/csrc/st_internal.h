@@ -36,6 +36,24 @@ void set_last_error(const std::string &msg);
         if (!(cond)) throw ::st::Error((code), (msg)); \
     } while (0)
 
+// runs f at the extern "C" boundary: st::Error -> its code + st_last_error()
+template <typename F>
+inline int guard(F &&f) {
+    try {
+        f();
+        return ST_OK;
+    } catch (const Error &e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_last_error("host allocation failed");
+        return ST_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return ST_ERR_INTERNAL;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // grow-only device workspace, one buffer per named slot
 struct Workspace {

@@ -1,0 +1,244 @@
+// st_vp8l.cpp -- VP8L prefix codes and header bits (host; see st_vp8l.h).
+//
+// Bitstream layout follows the WebP lossless format (RFC 9649): signature 0x2f,
+// 14-bit width-1 / height-1, alpha hint, version 0; transforms; colour-cache bit;
+// meta-prefix bit (main image only); five prefix codes (green + length prefixes,
+// red, blue, alpha, distance); the entropy-coded pixels.
+#include "st_vp8l.h"
+
+#include <algorithm>
+#include <queue>
+#include <stdexcept>
+
+namespace st {
+namespace vp8l {
+
+void BitWriter::put(uint32_t v, int n) {
+    if (n == 0) return;
+    acc |= (uint64_t)(v & ((n == 32) ? 0xffffffffu : ((1u << n) - 1))) << nacc;
+    nacc += n;
+    nbits += (uint64_t)n;
+    while (nacc >= 8) {
+        buf.push_back((uint8_t)acc);
+        acc >>= 8;
+        nacc -= 8;
+    }
+}
+
+std::vector<uint8_t> BitWriter::bytes() const {
+    std::vector<uint8_t> b = buf;
+    if (nacc) b.push_back((uint8_t)acc);
+    return b;
+}
+
+// Huffman over the used symbols with counts raised to at least `floor`; depths out
+static int huffman_depths(const std::vector<std::pair<uint64_t, int>> &used, uint64_t floor_,
+                          std::vector<int> &depth) {
+    const int m = (int)used.size();
+    // nodes 0..m-1 leaves, then internal nodes; parent links give the depths
+    std::vector<int> parent(2 * m, -1);
+    typedef std::pair<uint64_t, int> Item;  // (weight, node): ties by node id, deterministic
+    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+    for (int i = 0; i < m; ++i) pq.push({std::max(used[i].first, floor_), i});
+    int next = m;
+    while (pq.size() > 1) {
+        Item a = pq.top();
+        pq.pop();
+        Item b = pq.top();
+        pq.pop();
+        parent[a.second] = next;
+        parent[b.second] = next;
+        pq.push({a.first + b.first, next});
+        ++next;
+    }
+    int maxd = 0;
+    depth.assign(m, 0);
+    for (int i = 0; i < m; ++i) {
+        int d = 0;
+        for (int p = parent[i]; p >= 0; p = parent[p]) ++d;
+        depth[i] = d;
+        maxd = std::max(maxd, d);
+    }
+    return maxd;
+}
+
+void huffman_lengths(const uint64_t *counts, int n, int limit, uint8_t *len) {
+    std::vector<std::pair<uint64_t, int>> used;
+    for (int s = 0; s < n; ++s) {
+        len[s] = 0;
+        if (counts[s]) used.push_back({counts[s], s});
+    }
+    if (used.empty()) return;
+    if (used.size() == 1) {
+        len[used[0].second] = 1;
+        return;
+    }
+    // raising small counts flattens the tree until it fits the length limit (the
+    // result is still a full binary tree, i.e. a complete code)
+    std::vector<int> depth;
+    for (uint64_t floor_ = 1;; floor_ *= 2) {
+        if (huffman_depths(used, floor_, depth) <= limit) break;
+    }
+    for (size_t i = 0; i < used.size(); ++i) len[used[i].second] = (uint8_t)depth[i];
+}
+
+// canonical codes (shorter first, ascending symbol within a length), bit-reversed
+static void canonical(const uint8_t *len, int n, uint16_t *rev) {
+    int bl[kMaxCodeLen + 2] = {0};
+    for (int s = 0; s < n; ++s) bl[len[s]]++;
+    bl[0] = 0;
+    uint32_t next[kMaxCodeLen + 2] = {0};
+    uint32_t code = 0;
+    for (int b = 1; b <= kMaxCodeLen + 1; ++b) {
+        code = (code + bl[b - 1]) << 1;
+        next[b] = code;
+    }
+    for (int s = 0; s < n; ++s) {
+        rev[s] = 0;
+        const int l = len[s];
+        if (!l) continue;
+        const uint32_t c = next[l]++;
+        uint32_t r = 0;
+        for (int i = 0; i < l; ++i) r |= ((c >> i) & 1u) << (l - 1 - i);
+        rev[s] = (uint16_t)r;
+    }
+}
+
+static const int kCodeLengthOrder[19] = {17, 18, 0, 1, 2, 3, 4, 5, 16, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+
+Code write_code(BitWriter &bw, const uint64_t *counts, int alphabet) {
+    Code c;
+    c.len.assign(alphabet, 0);
+    c.rev.assign(alphabet, 0);
+    std::vector<int> used;
+    for (int s = 0; s < alphabet; ++s)
+        if (counts[s]) used.push_back(s);
+    if (used.empty()) used.push_back(0);  // an unused alphabet: one zero-bit symbol
+    if (used.size() <= 2 && used.back() < 256) {
+        // simple code: 1 or 2 symbols, lengths 0 or 1
+        bw.put(1, 1);
+        bw.put((uint32_t)used.size() - 1, 1);
+        if (used[0] < 2) {
+            bw.put(0, 1);
+            bw.put((uint32_t)used[0], 1);
+        } else {
+            bw.put(1, 1);
+            bw.put((uint32_t)used[0], 8);
+        }
+        if (used.size() == 2) {
+            bw.put((uint32_t)used[1], 8);
+            c.len[used[0]] = 1;
+            c.len[used[1]] = 1;
+            c.rev[used[1]] = 1;  // ascending symbols: used[0] < used[1] gets code 0
+        }
+        return c;
+    }
+    // normal code
+    huffman_lengths(counts, alphabet, kMaxCodeLen, c.len.data());
+    canonical(c.len.data(), alphabet, c.rev.data());
+    // run-length tokens over the code lengths: 0..15 literal, 16 repeat previous
+    // non-zero 3..6, 17 zeros 3..10, 18 zeros 11..138
+    struct Tok {
+        uint8_t sym, extra_bits;
+        uint8_t extra;
+    };
+    std::vector<Tok> toks;
+    for (int i = 0; i < alphabet;) {
+        const int v = c.len[i];
+        int run = 1;
+        while (i + run < alphabet && c.len[i + run] == v) ++run;
+        i += run;
+        if (v == 0) {
+            while (run > 0) {
+                if (run >= 11) {
+                    const int r = std::min(run, 138);
+                    toks.push_back({18, 7, (uint8_t)(r - 11)});
+                    run -= r;
+                } else if (run >= 3) {
+                    const int r = std::min(run, 10);
+                    toks.push_back({17, 3, (uint8_t)(r - 3)});
+                    run -= r;
+                } else {
+                    toks.push_back({0, 0, 0});
+                    --run;
+                }
+            }
+        } else {
+            toks.push_back({(uint8_t)v, 0, 0});
+            --run;
+            while (run >= 3) {
+                const int r = std::min(run, 6);
+                toks.push_back({16, 2, (uint8_t)(r - 3)});
+                run -= r;
+            }
+            while (run-- > 0) toks.push_back({(uint8_t)v, 0, 0});
+        }
+    }
+    uint64_t tc[19] = {0};
+    for (auto &t : toks) tc[t.sym]++;
+    uint8_t cl[19];
+    huffman_lengths(tc, 19, 7, cl);
+    uint16_t crev[19];
+    canonical(cl, 19, crev);
+    int nused = 0;
+    for (int s = 0; s < 19; ++s) nused += cl[s] != 0;
+    int ncl = 4;
+    for (int i = 0; i < 19; ++i)
+        if (cl[kCodeLengthOrder[i]]) ncl = std::max(ncl, i + 1);
+    bw.put(0, 1);  // normal code
+    bw.put((uint32_t)(ncl - 4), 4);
+    for (int i = 0; i < ncl; ++i) bw.put(cl[kCodeLengthOrder[i]], 3);
+    bw.put(0, 1);  // max_symbol = alphabet size
+    for (auto &t : toks) {
+        // a one-symbol code-length code is read with zero bits
+        if (nused > 1) bw.put(crev[t.sym], cl[t.sym]);
+        bw.put(t.extra, t.extra_bits);
+    }
+    return c;
+}
+
+void build_header(int width, int height, bool alpha_used, const uint32_t *hist, const uint8_t *modes, Header &out) {
+    if (width < 1 || height < 1 || width > 16384 || height > 16384)
+        throw std::invalid_argument("vp8l: image size out of range");
+    BitWriter &bw = out.bw;
+    bw.put(0x2f, 8);
+    bw.put((uint32_t)(width - 1), 14);
+    bw.put((uint32_t)(height - 1), 14);
+    bw.put(alpha_used ? 1 : 0, 1);
+    bw.put(0, 3);
+    // predictor transform with its sub-image (entropy-coded image: green = mode)
+    bw.put(1, 1);
+    bw.put(0, 2);
+    bw.put(kPredBits - 2, 3);
+    const int bw_ = (width + (1 << kPredBits) - 1) >> kPredBits;
+    const int bh_ = (height + (1 << kPredBits) - 1) >> kPredBits;
+    {
+        std::vector<uint64_t> g(kGreenAlphabet, 0), zero(256, 0), dist(kDistAlphabet, 0);
+        for (int i = 0; i < bw_ * bh_; ++i) g[modes[i]]++;
+        zero[0] = 1;
+        bw.put(0, 1);  // no colour cache
+        Code cg = write_code(bw, g.data(), kGreenAlphabet);
+        write_code(bw, zero.data(), 256);  // red 0
+        write_code(bw, zero.data(), 256);  // blue 0
+        write_code(bw, zero.data(), 256);  // alpha 0
+        write_code(bw, dist.data(), kDistAlphabet);
+        for (int i = 0; i < bw_ * bh_; ++i) bw.put(cg.rev[modes[i]], cg.len[modes[i]]);
+    }
+    bw.put(0, 1);  // no more transforms
+    // main image
+    bw.put(0, 1);  // no colour cache
+    bw.put(0, 1);  // one prefix-code group
+    out.tab.assign(4 * 256, 0);
+    std::vector<uint64_t> dist(kDistAlphabet, 0);
+    for (int ch = 0; ch < 4; ++ch) {
+        const int alphabet = ch == 0 ? kGreenAlphabet : 256;
+        std::vector<uint64_t> cnt(alphabet, 0);
+        for (int s = 0; s < 256; ++s) cnt[s] = hist[ch * 256 + s];
+        Code code = write_code(bw, cnt.data(), alphabet);
+        for (int s = 0; s < 256; ++s) out.tab[ch * 256 + s] = ((uint32_t)code.len[s] << 16) | code.rev[s];
+    }
+    write_code(bw, dist.data(), kDistAlphabet);
+}
+
+}  // namespace vp8l
+}  // namespace st

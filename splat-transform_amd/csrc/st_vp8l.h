@@ -1,0 +1,62 @@
+// st_vp8l.h -- host side of the WebP lossless (VP8L) encoder: prefix-code
+// construction and the bitstream header.  The per-pixel work (predictor choice,
+// residuals, histograms, the entropy-coded pixel stream) runs on the device
+// (st_webp.hip); the host turns four 256-bin histograms into canonical prefix
+// codes and writes the few hundred header bits in front of the pixel stream.
+//
+// Replaces the reference's WebPEncodeLosslessRGBA (lib/webp_encode.c:19-29,
+// called from utils/webp.ts:19-41 by write-sog.ts:120-140).  Parity is at the
+// decoded-RGBA level: any valid lossless VP8L stream of the same
+// pixels is a drop-in; the byte stream itself differs from libwebp's.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace st {
+namespace vp8l {
+
+constexpr int kPredBits = 4;           // predictor blocks of 16 x 16 pixels
+constexpr int kGreenAlphabet = 280;    // 256 literals + 24 length prefixes (no colour cache)
+constexpr int kDistAlphabet = 40;
+constexpr int kMaxCodeLen = 15;
+
+// LSB-first bit writer (the VP8L bit order)
+struct BitWriter {
+    std::vector<uint8_t> buf;
+    uint64_t acc = 0;
+    int nacc = 0;
+    uint64_t nbits = 0;
+    void put(uint32_t v, int n);
+    // the bytes written so far, the last one partial (zero high bits)
+    std::vector<uint8_t> bytes() const;
+};
+
+// one prefix code: per symbol the emitted length (0 for a one-symbol code) and the
+// canonical code with its bits reversed (VP8L reads codes MSB-first from an LSB-first stream)
+struct Code {
+    std::vector<uint8_t> len;
+    std::vector<uint16_t> rev;
+};
+
+// length-limited Huffman code lengths for counts[0..n) (a complete code when >= 2 symbols)
+void huffman_lengths(const uint64_t *counts, int n, int limit, uint8_t *len);
+
+// build the code for counts[0..alphabet) and append its description to bw
+// (simple code for <= 2 used symbols below 256, normal code otherwise)
+Code write_code(BitWriter &bw, const uint64_t *counts, int alphabet);
+
+// The header bits of one image: everything before the main image's pixel
+// stream (VP8L signature, size, predictor transform with its entropy-coded
+// sub-image, colour-cache and meta-code flags, the five prefix codes).
+// hist: residual histograms in channel order G, R, B, A (256 bins each);
+// modes: the predictor sub-image (one byte per 16 x 16 block, row-major).
+// tab (out): 4 x 256 device table entries (len << 16 | reversed code), G, R, B, A.
+struct Header {
+    BitWriter bw;
+    std::vector<uint32_t> tab;
+};
+void build_header(int width, int height, bool alpha_used, const uint32_t *hist, const uint8_t *modes, Header &out);
+
+}  // namespace vp8l
+}  // namespace st

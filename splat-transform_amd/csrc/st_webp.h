@@ -1,0 +1,51 @@
+// st_webp.h -- device WebP lossless encode, CRC-32, and the SOG container (internal).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "st_internal.h"
+
+namespace st {
+
+struct WebpJob {
+    const uint8_t *rgba;  // device, RGBA8 rows
+    int w, h, stride;     // stride in bytes (multiple of 4)
+    uint8_t *out;         // device, >= webp_max_size(w, h) bytes, 4-byte aligned
+    uint64_t cap;
+    uint64_t size;        // out: bytes of the .webp file
+};
+
+uint64_t webp_max_size(int w, int h);
+// encodes every job (three stream synchronisations for the whole batch)
+void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs);
+// zlib-compatible CRC-32 of cnt device buffers (crc_in: running value, 0 for a fresh CRC)
+void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const uint32_t *crc_in, int cnt,
+               uint32_t *crcs);
+
+// the whole .sog archive (WebP-encoded textures + meta.json, zip-writer.ts layout) of
+// textures resident on the device; *out is malloc'd (st_free)
+void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
+                    uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size);
+
+// ---- host: the .sog container (st_zip.cpp) ----------------------------------
+// JSON text of a JS number (Number::toString as JSON.stringify emits it; non-finite -> null)
+std::string js_number(double v);
+// meta.json of writeSog (write-sog.ts:271-293, 350-361)
+std::string sog_meta_json(const st_sog_meta &m, uint64_t count);
+
+struct ZipEntry {
+    std::string name;
+    uint64_t size;
+    uint32_t crc;
+};
+// the store-only archive of serialize/zip-writer.ts: per entry a local header, the
+// data and a data descriptor; then the central directory and the end record.
+uint64_t zip_size(const std::vector<ZipEntry> &entries);
+// writes everything but the entries' data into buf (zip_size bytes); data_off[i] = where
+// entry i's bytes go
+void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf,
+               uint64_t *data_off);
+
+}  // namespace st

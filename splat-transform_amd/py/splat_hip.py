@@ -60,6 +60,8 @@ EXPORTS = [
     'st_dev_minmax', 'st_dev_kmeans_prepare', 'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
+    'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
+    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_sog_bundle', 'st_free',
 ]
 
 
@@ -79,8 +81,10 @@ def lib():
         L.st_last_error.restype = ctypes.c_char_p
         L.st_ctx_last_timings.restype = ctypes.c_char_p
         L.st_ctx_destroy.restype = None
+        L.st_free.restype = None
+        L.st_webp_max_size.restype = ctypes.c_uint64
         for name in EXPORTS:
-            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy'):
+            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy', 'st_free', 'st_webp_max_size'):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -144,6 +148,39 @@ def sog_geometry(n, sh_coeffs):
     v = [ctypes.c_int32() for _ in range(5)]
     check(lib().st_sog_geometry(ctypes.c_uint64(n), ctypes.c_int32(sh_coeffs), *[ctypes.byref(x) for x in v]))
     return tuple(x.value for x in v)
+
+
+def _take(buf, size):
+    """copy a malloc'd library buffer into bytes and release it"""
+    try:
+        return ctypes.string_at(buf, size.value)
+    finally:
+        lib().st_free(buf)
+
+
+def webp_max_size(w, h):
+    return lib().st_webp_max_size(ctypes.c_int32(w), ctypes.c_int32(h))
+
+
+def zip_store(entries, dos_time, dos_date):
+    """store-only ZIP of [(name, bytes, crc)] in the layout of serialize/zip-writer.ts (host)"""
+    n = len(entries)
+    names = (ctypes.c_char_p * n)(*[e[0].encode() for e in entries])
+    bufs = [ctypes.create_string_buffer(bytes(e[1]), len(e[1]) or 1) for e in entries]
+    data = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    sizes = (ctypes.c_uint64 * n)(*[len(e[1]) for e in entries])
+    crcs = (ctypes.c_uint32 * n)(*[e[2] for e in entries])
+    out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+    check(lib().st_zip_store(names, data, sizes, crcs, ctypes.c_int32(n), ctypes.c_uint16(dos_time),
+                             ctypes.c_uint16(dos_date), ctypes.byref(out), ctypes.byref(size)))
+    return _take(out, size)
+
+
+def sog_meta_json(meta, count):
+    """meta.json text of writeSog for an SogMeta (host)"""
+    out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+    check(lib().st_sog_meta_json(ctypes.byref(meta), ctypes.c_uint64(count), ctypes.byref(out), ctypes.byref(size)))
+    return _take(out, size)
 
 
 def device_count():
@@ -263,7 +300,52 @@ class Context:
             res['shN_centroids'] = tex['shN_centroids'].reshape(ch, cw, 4)
         return res, meta, used.value
 
+    def webp_lossless(self, rgba):
+        """WebPEncodeLosslessRGBA of a host (H, W, 4) uint8 array -> .webp bytes"""
+        rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+        h, w = rgba.shape[:2]
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        check(lib().st_webp_lossless(self.h, _vp(rgba), ctypes.c_int32(w), ctypes.c_int32(h), ctypes.c_int32(w * 4),
+                                     ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size)
+
+    def sog_bundle(self, cols, iters, draws, dos_time, dos_date):
+        """writeSog to a .sog bundle: (archive bytes, draws used)"""
+        t = make_table(cols)
+        used = ctypes.c_uint64(0)
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        check(lib().st_sog_bundle(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws),
+                                  ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.c_uint16(dos_time),
+                                  ctypes.c_uint16(dos_date), ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size), used.value
+
     # ---- device-memory seams (torch tensors) --------------------------------------
+    def dev_webp_lossless(self, rgba, out):
+        """rgba: device uint8 (H, W, 4) tensor; out: device uint8 tensor of >= webp_max_size bytes"""
+        h, w = rgba.shape[:2]
+        size = ctypes.c_uint64(0)
+        check(lib().st_dev_webp_lossless(self.h, _ptr(rgba), ctypes.c_int32(w), ctypes.c_int32(h),
+                                         ctypes.c_int32(rgba.stride(0)), _ptr(out), ctypes.c_uint64(out.numel()),
+                                         ctypes.byref(size)))
+        return size.value
+
+    def dev_crc32(self, data, n=None, crc_in=0):
+        out = ctypes.c_uint32(0)
+        n = data.numel() if n is None else n
+        check(lib().st_dev_crc32(self.h, _ptr(data), ctypes.c_uint64(n), ctypes.c_uint32(crc_in),
+                                 ctypes.byref(out)))
+        return out.value
+
+    def dev_sog_bundle(self, meta, count, tex, dos_time, dos_date):
+        """the .sog archive bytes of device textures (dict as for dev_sog) and their SogMeta"""
+        t = SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                          ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        check(lib().st_dev_sog_bundle(self.h, ctypes.byref(meta), ctypes.c_uint64(count), ctypes.byref(t),
+                                      ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
+                                      ctypes.byref(size)))
+        return _take(out, size)
+
     def dev_transform(self, cols, params):
         t = make_table(cols)
         check(lib().st_dev_transform(self.h, ctypes.byref(t), ctypes.byref(params)))

@@ -402,6 +402,39 @@ cases.sog = async () => {
     fx.save();
 };
 
+// .sog bundle (write-sog.ts:110-140,361-366 + serialize/zip-writer.ts + crc.ts): the
+// whole ZIP with a pinned clock, so the container layout, the CRC-32 of every entry
+// and the raw meta.json text are fixed.  Entries hold the identity WebP stand-in's
+// payload (16-byte 'RGBA' header + pixels; see build_ref.py).
+cases.sog_bundle = async () => {
+    const fx = new Fixture('sog_bundle');
+    const specs = [['b_sh1', 2048, 3, 2, 31, 0.0], ['b_sh0', 1500, 0, 2, 32, 0.05]];
+    const clock = [2024, 4, 17, 13, 37, 42];  // local time: dosTime/dosDate fixed
+    fx.meta.cases = [];
+    const RealDate = Date;
+    for (const [name, n, shc, iters, seed, cube] of specs) {
+        const { names, cols } = makeSplats(n, shc, 400 + n, { cubeFrac: cube });
+        const table = toTable(names, cols);
+        addTable(fx, `${name}_in_`, table);
+        const dir = fs.mkdtempSync('/tmp/st_sogb_');
+        const outPath = path.join(dir, 'scene.sog');
+        const fh = await fs.promises.open(outPath, 'w');
+        seedRandom(seed);
+        global.Date = class extends RealDate { constructor(...a) { super(...(a.length ? a : clock)); } };
+        try {
+            await quiet(() => writeSog(fh, table, outPath, iters, 'cpu'));
+        } finally {
+            global.Date = RealDate;
+        }
+        await fh.close();
+        const zip = fs.readFileSync(outPath);
+        fx.meta.cases.push({ name, n, iters, seed, draws: drawCount, clock });
+        fx.add(`${name}_zip`, new Uint8Array(zip.buffer, zip.byteOffset, zip.length));
+        fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
+    }
+    fx.save();
+};
+
 cases.filter_combine = () => {
     const fx = new Fixture('filter_combine');
     const { names, cols } = makeSplats(500, 15, 77);

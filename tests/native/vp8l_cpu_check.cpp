@@ -1,0 +1,143 @@
+// TEST INFRASTRUCTURE ONLY: a scalar host emulation of the device VP8L kernels
+// (st_webp.hip: predictor choice, residuals, histograms, pixel stream) around the
+// product's own header/prefix-code builder (st_vp8l.cpp), so the bitstream format
+// can be checked on a machine without a GPU (tests/test_webp_cpu.py decodes the
+// output with Pillow/libwebp).  Never linked into libsplat_hip.
+//
+//   vp8l_cpu_check in.rgba W H out.webp
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../splat-transform_amd/csrc/st_vp8l.h"
+
+using namespace st::vp8l;
+
+static uint32_t ch(uint32_t v, int c) { return (v >> (8 * c)) & 0xffu; }
+static uint32_t avg2(uint32_t a, uint32_t b) { return (((a ^ b) & 0xfefefefeu) >> 1) + (a & b); }
+static uint32_t clamp_full(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r = 0;
+    for (int k = 0; k < 4; ++k) {
+        int v = (int)ch(a, k) + (int)ch(b, k) - (int)ch(c, k);
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        r |= (uint32_t)v << (8 * k);
+    }
+    return r;
+}
+static uint32_t clamp_half(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int x = (int)ch(a, k), y = (int)ch(b, k);
+        int v = x + (x - y) / 2;
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        r |= (uint32_t)v << (8 * k);
+    }
+    return r;
+}
+static uint32_t sel(uint32_t L, uint32_t T, uint32_t TL) {
+    int pl = 0, pt = 0;
+    for (int k = 0; k < 4; ++k) {
+        pl += abs((int)ch(T, k) - (int)ch(TL, k));
+        pt += abs((int)ch(L, k) - (int)ch(TL, k));
+    }
+    return pl < pt ? L : T;
+}
+static uint32_t pred(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
+    switch (m) {
+        case 0: return 0xff000000u;
+        case 1: return L;
+        case 2: return T;
+        case 3: return TR;
+        case 4: return TL;
+        case 5: return avg2(avg2(L, TR), T);
+        case 6: return avg2(L, TL);
+        case 7: return avg2(L, T);
+        case 8: return avg2(TL, T);
+        case 9: return avg2(T, TR);
+        case 10: return avg2(avg2(L, TL), avg2(T, TR));
+        case 11: return sel(L, T, TL);
+        case 12: return clamp_full(L, T, TL);
+        default: return clamp_half(avg2(L, T), TL);
+    }
+}
+static uint32_t sub(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int k = 0; k < 4; ++k) r |= ((ch(a, k) - ch(b, k)) & 0xffu) << (8 * k);
+    return r;
+}
+
+int main(int argc, char **argv) {
+    if (argc != 5) return 2;
+    const int w = atoi(argv[2]), h = atoi(argv[3]);
+    std::vector<uint8_t> rgba((size_t)w * h * 4);
+    FILE *f = fopen(argv[1], "rb");
+    if (!f || fread(rgba.data(), 1, rgba.size(), f) != rgba.size()) return 3;
+    fclose(f);
+    std::vector<uint32_t> argb((size_t)w * h);
+    bool alpha = false;
+    for (size_t i = 0; i < argb.size(); ++i) {
+        const uint8_t *p = &rgba[i * 4];
+        argb[i] = ((uint32_t)p[3] << 24) | ((uint32_t)p[0] << 16) | ((uint32_t)p[1] << 8) | p[2];
+        alpha = alpha || p[3] != 255;
+    }
+    auto at = [&](int x, int y) { return argb[(size_t)y * w + x]; };
+    const int B = 1 << kPredBits, bw = (w + B - 1) / B, bh = (h + B - 1) / B;
+    std::vector<uint8_t> modes((size_t)bw * bh);
+    std::vector<uint32_t> res((size_t)w * h);
+    for (int by = 0; by < bh; ++by)
+        for (int bx = 0; bx < bw; ++bx) {
+            uint64_t cost[14] = {0};
+            for (int y = by * B; y < std::min(h, by * B + B); ++y)
+                for (int x = bx * B; x < std::min(w, bx * B + B); ++x) {
+                    if (x == 0 || y == 0) continue;
+                    const uint32_t TR = (x + 1 < w) ? at(x + 1, y - 1) : at(0, y);
+                    for (int m = 0; m < 14; ++m) {
+                        const uint32_t r = sub(at(x, y), pred(m, at(x - 1, y), at(x, y - 1), at(x - 1, y - 1), TR));
+                        for (int k = 0; k < 4; ++k) cost[m] += ch(r, k) < 128 ? ch(r, k) : 256 - ch(r, k);
+                    }
+                }
+            int best = 0;
+            for (int m = 1; m < 14; ++m)
+                if (cost[m] < cost[best]) best = m;
+            modes[(size_t)by * bw + bx] = (uint8_t)best;
+        }
+    std::vector<uint32_t> hist(4 * 256, 0);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            uint32_t p;
+            if (y == 0)
+                p = x == 0 ? 0xff000000u : at(x - 1, y);
+            else if (x == 0)
+                p = at(x, y - 1);
+            else {
+                const uint32_t TR = (x + 1 < w) ? at(x + 1, y - 1) : at(0, y);
+                p = pred(modes[(size_t)(y / B) * bw + x / B], at(x - 1, y), at(x, y - 1), at(x - 1, y - 1), TR);
+            }
+            const uint32_t r = sub(at(x, y), p);
+            res[(size_t)y * w + x] = r;
+            hist[0 * 256 + ch(r, 1)]++;
+            hist[1 * 256 + ch(r, 2)]++;
+            hist[2 * 256 + ch(r, 0)]++;
+            hist[3 * 256 + ch(r, 3)]++;
+        }
+    Header hd;
+    build_header(w, h, alpha, hist.data(), modes.data(), hd);
+    BitWriter &bw_ = hd.bw;
+    for (uint32_t r : res) {
+        const uint32_t e[4] = {hd.tab[0 * 256 + ch(r, 1)], hd.tab[1 * 256 + ch(r, 2)], hd.tab[2 * 256 + ch(r, 0)],
+                               hd.tab[3 * 256 + ch(r, 3)]};
+        for (int k = 0; k < 4; ++k) bw_.put(e[k] & 0xffffu, (int)(e[k] >> 16));
+    }
+    std::vector<uint8_t> body = bw_.bytes();
+    const uint32_t vsz = (uint32_t)body.size(), pad = vsz & 1, riff = 4 + 8 + vsz + pad;
+    FILE *o = fopen(argv[4], "wb");
+    fwrite("RIFF", 1, 4, o);
+    fwrite(&riff, 4, 1, o);
+    fwrite("WEBPVP8L", 1, 8, o);
+    fwrite(&vsz, 4, 1, o);
+    fwrite(body.data(), 1, body.size(), o);
+    if (pad) fputc(0, o);
+    fclose(o);
+    return 0;
+}

@@ -1,0 +1,167 @@
+"""The .sog container on the host (no GPU): ZIP layout, CRC-32, meta.json text and
+the VP8L header/prefix-code builder.
+
+Pinned by tests/golden/sog_bundle.* -- the reference's own writeSog writing a .sog
+(serialize/zip-writer.ts, crc.ts, write-sog.ts:271-366) with a fixed clock; its
+entries hold the identity WebP stand-in's payload (tests/golden/gen/build_ref.py).
+"""
+import io
+import os
+import shutil
+import subprocess
+import zipfile
+import zlib
+
+import numpy as np
+import pytest
+
+import sog_container as oc
+import splat_hip as sh
+from golden_io import Golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = Golden('sog_bundle')
+CASES = [c['name'] for c in G.meta['cases']]
+
+
+def _case(name):
+    c = next(c for c in G.meta['cases'] if c['name'] == name)
+    z = G[name + '_zip'].tobytes()
+    return c, z
+
+
+def _clock(c):
+    y, mo, d, hh, mm, ss = c['clock']
+    return oc.dos_clock(y, mo, d, hh, mm, ss)
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_oracle_zip_matches_reference_bytes(name):
+    c, z = _case(name)
+    zf = zipfile.ZipFile(io.BytesIO(z))
+    assert zf.testzip() is None
+    entries = [(i.filename, zf.read(i.filename)) for i in zf.infolist()]
+    t, d = _clock(c)
+    assert oc.zip_store(entries, t, d) == z
+    for (nm, data), info in zip(entries, zf.infolist()):
+        assert oc.crc32(data) == zlib.crc32(data) == info.CRC
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_product_zip_store_matches_reference_bytes(name):
+    c, z = _case(name)
+    zf = zipfile.ZipFile(io.BytesIO(z))
+    entries = [(i.filename, zf.read(i.filename), i.CRC) for i in zf.infolist()]
+    t, d = _clock(c)
+    assert sh.zip_store(entries, t, d) == z
+
+
+def _meta_struct(m):
+    meta = sh.SogMeta()
+    for k in range(3):
+        meta.means_min[k] = m['means']['mins'][k]
+        meta.means_max[k] = m['means']['maxs'][k]
+    for k in range(256):
+        meta.scales_codebook[k] = m['scales']['codebook'][k]
+        meta.sh0_codebook[k] = m['sh0']['codebook'][k]
+    if 'shN' in m:
+        meta.sh_bands = m['shN']['bands']
+        meta.palette_size = m['shN']['count']
+        for k in range(256):
+            meta.shn_codebook[k] = m['shN']['codebook'][k]
+    return meta
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_meta_json_text_matches_reference(name):
+    import json
+    c, z = _case(name)
+    text = zipfile.ZipFile(io.BytesIO(z)).read('meta.json')
+    m = json.loads(text)
+    # the codebooks are float32 values: the struct stores them exactly
+    assert sh.sog_meta_json(_meta_struct(m), m['count']) == text
+    shn = m.get('shN', {})
+    assert oc.sog_meta_json(m['count'], m['means']['mins'], m['means']['maxs'], m['scales']['codebook'],
+                            m['sh0']['codebook'], shn.get('bands', 0), shn.get('count', 0),
+                            shn.get('codebook')) == text
+
+
+EDGE = [1e-7, 1.5e-7, 1e-6, 1.25e-6, 0.1, 0.000123, 1e21, 1e20, 123456789012345680000.0, 1.7976931348623157e308,
+        5e-324, 2.2250738585072014e-308, -0.0, 0.5, 3.0, -2.5e-10, 4.35, 2 ** 53, 2 ** 70, 1 / 3, float('nan'),
+        float('inf'), -float('inf'), 9.999999999999999e22, 1e-5]
+
+
+def test_js_number_formatting_edge_values():
+    # product formatter (through meta.json) against the restatement of Number::toString
+    vals = EDGE + [0.0] * ((6 - len(EDGE) % 6) % 6)
+    for i in range(0, len(vals), 6):
+        meta = sh.SogMeta()
+        for k in range(3):
+            meta.means_min[k] = vals[i + k]
+            meta.means_max[k] = vals[i + 3 + k]
+        cb = [0.0] * 256
+        want = oc.sog_meta_json(7, vals[i:i + 3], vals[i + 3:i + 6], cb, cb)
+        assert sh.sog_meta_json(meta, 7) == want
+    # spot checks of the restatement against ECMAScript's published outputs
+    assert [oc.js_number(v) for v in (1e-7, 1e21, 1e20, 0.000001, -0.0, 1.5, 100.0, 2 ** 70)] == \
+        ['1e-7', '1e+21', '100000000000000000000', '0.000001', '0', '1.5', '100', '1.1805916207174113e+21']
+
+
+# ---- VP8L header / prefix codes (product host code) + a scalar emulation of the kernels
+HARNESS = '/tmp/st_vp8l_cpu_check'
+
+
+def _harness():
+    src = os.path.join(ROOT, 'tests', 'native', 'vp8l_cpu_check.cpp')
+    lib_src = os.path.join(ROOT, 'splat-transform_amd', 'csrc', 'st_vp8l.cpp')
+    if shutil.which('g++') is None:
+        pytest.skip('g++ not available')
+    if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < max(os.path.getmtime(src),
+                                                                     os.path.getmtime(lib_src)):
+        subprocess.check_call(['g++', '-O2', '-std=c++17', '-o', HARNESS, src, lib_src])
+    return HARNESS
+
+
+def _roundtrip(img, tmp_path):
+    from PIL import Image
+    h, w, _ = img.shape
+    src, dst = tmp_path / 'in.rgba', tmp_path / 'out.webp'
+    np.ascontiguousarray(img, np.uint8).tofile(src)
+    subprocess.check_call([_harness(), str(src), str(w), str(h), str(dst)])
+    return np.array(Image.open(dst).convert('RGBA'))
+
+
+def _images():
+    rng = np.random.default_rng(5)
+    x = np.arange(96)
+    gx, gy = np.meshgrid(x, x[:70])
+    grad = np.stack([gx * 3 % 256, gy * 2 % 256, (gx + gy) % 256, np.full_like(gx, 255)], -1)
+    opaque = rng.integers(0, 256, (61, 45, 4))
+    opaque[..., 3] = 255
+    return {
+        'random': rng.integers(0, 256, (37, 53, 4)),
+        'constant': np.full((20, 30, 4), 7),
+        'gradient': grad,
+        'two_colours': rng.integers(0, 2, (16, 16, 4)) * 255,
+        '1x1': rng.integers(0, 256, (1, 1, 4)),
+        '1xN': rng.integers(0, 256, (1, 77, 4)),
+        'Nx1': rng.integers(0, 256, (50, 1, 4)),
+        'opaque_noise': opaque,
+        'sparse_palette': rng.choice([0, 17, 200, 255], size=(33, 70, 4)),
+    }
+
+
+@pytest.mark.parametrize('kind', list(_images().keys()))
+def test_vp8l_header_decodes(kind, tmp_path):
+    img = _images()[kind].astype(np.uint8)
+    assert np.array_equal(_roundtrip(img, tmp_path), img)
+
+
+def test_vp8l_header_decodes_sog_textures(tmp_path):
+    g = Golden('sog')
+    for case in g.meta['cases']:
+        for f in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels'):
+            key = f"{case['name']}_{f}"
+            if key in g:
+                img = g[key]
+                assert np.array_equal(_roundtrip(img, tmp_path), img), key
