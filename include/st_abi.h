@@ -229,6 +229,10 @@ int st_sog_meta_json(const st_sog_meta *meta, uint64_t count, char **out, uint64
  * the ZipWriter's clock fields (zip-writer.ts:39-41).  *out malloc'd (st_free). */
 int st_dev_sog_bundle(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);
+/* as st_dev_sog_bundle, but *out borrows the context's pinned archive buffer (valid
+ * until the next bundle call on ctx; no copy) -- what a writer hands to write(2) */
+int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
+                           uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *size);
 /* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */
 int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                   uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);

@@ -2,6 +2,7 @@
 // into HBM, run the device path, copy results back.  These mirror the
 // reference seams one-for-one for callers that hold host TypedArrays (the
 // N-API addon, ctypes); callers that keep tables resident use st_dev_*.
+#include <cstdlib>
 #include <cstring>
 
 #include "st_internal.h"
@@ -243,7 +244,14 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
         }
         st_sog_meta meta{};
         const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, &meta, &dt);
-        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, out, out_size);
+        const uint8_t *view;
+        uint64_t nb;
+        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, &view, &nb);
+        uint8_t *buf = (uint8_t *)std::malloc(nb);
+        ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
+        std::memcpy(buf, view, nb);
+        *out = buf;
+        *out_size = nb;
         if (used) *used = u;
     });
 }

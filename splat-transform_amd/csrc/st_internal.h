@@ -88,6 +88,9 @@ struct st_ctx {
     // pinned host staging for small readbacks
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
+    // pinned host buffer of the last .sog archive (st_dev_sog_bundle*)
+    void *archive = nullptr;
+    size_t archive_bytes = 0;
     std::vector<st::StageTimer> marks;
     bool timing = false;
     std::string last_timings = "{}";
@@ -109,6 +112,7 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
     return static_cast<T *>(c->ws.get(slot, count * sizeof(T) + 16));
 }
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
+void *archive_buf(st_ctx *c, size_t bytes);  // host pinned archive buffer (reused, grow-only)
 void use_device(st_ctx *c);
 void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
 

@@ -46,6 +46,18 @@ void *pinned(st_ctx *c, size_t bytes) {
     return c->pinned;
 }
 
+void *archive_buf(st_ctx *c, size_t bytes) {
+    if (c->archive_bytes < bytes) {
+        if (c->archive) ST_HIP(hipHostFree(c->archive));
+        c->archive = nullptr;
+        c->archive_bytes = 0;
+        const size_t want = bytes + bytes / 8;
+        ST_HIP(hipHostMalloc(&c->archive, want, hipHostMallocDefault));
+        c->archive_bytes = want;
+    }
+    return c->archive;
+}
+
 void use_device(st_ctx *c) { ST_HIP(hipSetDevice(c->device)); }
 
 void mark(st_ctx *c, const char *name) {
@@ -205,6 +217,7 @@ void st_ctx_destroy(st_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     c->ws.release();
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->archive) (void)hipHostFree(c->archive);
     for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
     for (auto &k : c->kevents) {
         (void)hipEventDestroy(k.a);

@@ -25,9 +25,10 @@ void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const u
                uint32_t *crcs);
 
 // the whole .sog archive (WebP-encoded textures + meta.json, zip-writer.ts layout) of
-// textures resident on the device; *out is malloc'd (st_free)
+// textures resident on the device, in the context's pinned archive buffer (valid until
+// the next bundle call on this context)
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
-                    uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size);
+                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size);
 
 // ---- host: the .sog container (st_zip.cpp) ----------------------------------
 // JSON text of a JS number (Number::toString as JSON.stringify emits it; non-finite -> null)

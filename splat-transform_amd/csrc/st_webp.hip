@@ -18,9 +18,10 @@
 //   k_vp8l_emit     each group assembles its bit run in LDS (atomicOr at the run's
 //                   own bit alignment) and stores whole words; the two edge words
 //                   it shares with its neighbours are OR-ed in        read 4 B, write ~bits/8
-// CRC-32: each thread takes the zlib CRC of a 4 KiB span and shifts it to the end
+// CRC-32: each thread takes the zlib CRC of a 2 KiB span (slicing-by-8) and shifts it to the end
 // of the buffer (multiplication by x^(8m) mod P, zlib's crc32_combine identity);
 // the XOR of all shifted CRCs is the CRC of the buffer.
+#include <cstdlib>
 #include <cstring>
 
 #include "st_internal.h"
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
 
 // ---- CRC-32 (zlib polynomial, reflected) ---------------------------------------
 constexpr uint32_t CRC_POLY = 0xedb88320u;
-constexpr uint32_t CRC_SPAN = 4096;  // bytes per thread
+constexpr uint32_t CRC_SPAN = 2048;  // bytes per thread
 
 __host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
     uint32_t m = 1u << 31, p = 0;
@@ -352,13 +353,14 @@ __host__ __device__ inline uint32_t x2nmodp(const uint32_t *x2n, uint64_t n, uns
 
 __global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ data, uint64_t n, uint32_t init,
                                                uint32_t *__restrict__ out) {
-    __shared__ uint32_t tbl[256];
+    // slicing-by-8: tbl[k][b] = CRC of byte b followed by k zero bytes
+    __shared__ uint32_t tbl[8][256];
     __shared__ uint32_t x2n[32];
     __shared__ uint32_t red[4];
     {
         uint32_t c = threadIdx.x;
         for (int k = 0; k < 8; ++k) c = (c & 1) ? (CRC_POLY ^ (c >> 1)) : (c >> 1);
-        tbl[threadIdx.x] = c;
+        tbl[0][threadIdx.x] = c;
     }
     if (threadIdx.x == 0) {
         uint32_t p = 1u << 30;  // x^1
@@ -366,28 +368,29 @@ __global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ data,
         for (int i = 1; i < 32; ++i) x2n[i] = p = multmodp(p, p);
     }
     __syncthreads();
+    for (int k = 1; k < 8; ++k) {
+        const uint32_t v = tbl[k - 1][threadIdx.x];
+        tbl[k][threadIdx.x] = (v >> 8) ^ tbl[0][v & 0xff];
+        __syncthreads();
+    }
     const uint64_t s0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * CRC_SPAN;
     uint32_t contrib = 0;
     if (s0 < n) {
         const uint64_t s1 = (s0 + CRC_SPAN < n) ? s0 + CRC_SPAN : n;
         uint32_t c = 0xffffffffu;
         uint64_t i = s0;
-        // 16-byte loads over the aligned middle of the span
-        for (; i < s1 && (((uintptr_t)data + i) & 15); ++i) c = (c >> 8) ^ tbl[(c ^ data[i]) & 0xff];
+        for (; i < s1 && (((uintptr_t)data + i) & 15); ++i) c = (c >> 8) ^ tbl[0][(c ^ data[i]) & 0xff];
+        auto step8 = [&](uint32_t lo, uint32_t hi) {
+            c ^= lo;
+            c = tbl[7][c & 0xff] ^ tbl[6][(c >> 8) & 0xff] ^ tbl[5][(c >> 16) & 0xff] ^ tbl[4][c >> 24] ^
+                tbl[3][hi & 0xff] ^ tbl[2][(hi >> 8) & 0xff] ^ tbl[1][(hi >> 16) & 0xff] ^ tbl[0][hi >> 24];
+        };
         for (; i + 16 <= s1; i += 16) {
             const uint4 q = *(const uint4 *)(data + i);
-            const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint32_t wd = wds[k];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    c = (c >> 8) ^ tbl[(c ^ wd) & 0xff];
-                    wd >>= 8;
-                }
-            }
+            step8(q.x, q.y);
+            step8(q.z, q.w);
         }
-        for (; i < s1; ++i) c = (c >> 8) ^ tbl[(c ^ data[i]) & 0xff];
+        for (; i < s1; ++i) c = (c >> 8) ^ tbl[0][(c ^ data[i]) & 0xff];
         c ^= 0xffffffffu;
         // crc(A B) = crc(A) * x^(8|B|) xor crc(B): shift this span's CRC to the end of the buffer
         contrib = multmodp(x2nmodp(x2n, n - s1, 3), c);
@@ -557,7 +560,7 @@ void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const u
 namespace st {
 
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
-                    uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
+                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size) {
     // entries in write-sog.ts order (:186-187, :239, :251, :268, :335, :348, :364)
     struct Img {
         const char *name;
@@ -583,8 +586,21 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
     }
     webp_encode_dev(c, jobs.data(), ni);
     const std::string mj = sog_meta_json(meta, count);
+    std::vector<ZipEntry> es;
+    for (int i = 0; i < ni; ++i) es.push_back({imgs[i].name, jobs[i].size, 0});
+    es.push_back({"meta.json", mj.size(), 0});
+    const uint64_t total = zip_size(es);
+    ST_REQUIRE(total < (1ull << 32), ST_ERR_ARG, "sog bundle: archive exceeds 4 GiB (no zip64, as the reference)");
+    uint8_t *buf = (uint8_t *)archive_buf(c, total);
+    std::vector<uint64_t> off(es.size());
+    zip_write(es, dos_time, dos_date, buf, off.data());  // offsets; headers rewritten with the CRCs below
+    // entry bytes go straight into the pinned archive while the CRC kernels run
+    std::memcpy(buf + off[ni], mj.data(), mj.size());
     uint8_t *dmeta = wsT<uint8_t>(c, "sb.meta", mj.size());
-    ST_HIP(hipMemcpyAsync(dmeta, mj.data(), mj.size(), hipMemcpyHostToDevice, c->stream));
+    ST_HIP(hipMemcpyAsync(dmeta, buf + off[ni], mj.size(), hipMemcpyHostToDevice, c->stream));
+    for (int i = 0; i < ni; ++i)
+        if (jobs[i].size)
+            ST_HIP(hipMemcpyAsync(buf + off[i], jobs[i].out, jobs[i].size, hipMemcpyDeviceToHost, c->stream));
     std::vector<const uint8_t *> ptrs;
     std::vector<uint64_t> lens;
     for (auto &j : jobs) {
@@ -594,30 +610,9 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
     ptrs.push_back(dmeta);
     lens.push_back(mj.size());
     std::vector<uint32_t> zero(ptrs.size(), 0), crcs(ptrs.size(), 0);
-    crc32_dev(c, ptrs.data(), lens.data(), zero.data(), (int)ptrs.size(), crcs.data());
-    std::vector<ZipEntry> es;
-    for (int i = 0; i < ni; ++i) es.push_back({imgs[i].name, jobs[i].size, crcs[i]});
-    es.push_back({"meta.json", mj.size(), crcs[ni]});
-    const uint64_t total = zip_size(es);
-    ST_REQUIRE(total < (1ull << 32), ST_ERR_ARG, "sog bundle: archive exceeds 4 GiB (no zip64, as the reference)");
-    uint8_t *buf = (uint8_t *)std::malloc(total);
-    ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
-    std::vector<uint64_t> off(es.size());
+    crc32_dev(c, ptrs.data(), lens.data(), zero.data(), (int)ptrs.size(), crcs.data());  // synchronises
+    for (size_t i = 0; i < es.size(); ++i) es[i].crc = crcs[i];
     zip_write(es, dos_time, dos_date, buf, off.data());
-    for (int i = 0; i < ni; ++i)
-        if (jobs[i].size) {
-            hipError_t e = hipMemcpyAsync(buf + off[i], jobs[i].out, jobs[i].size, hipMemcpyDeviceToHost, c->stream);
-            if (e != hipSuccess) {
-                std::free(buf);
-                ST_HIP(e);
-            }
-        }
-    std::memcpy(buf + off[ni], mj.data(), mj.size());
-    hipError_t e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) {
-        std::free(buf);
-        ST_HIP(e);
-    }
     *out = buf;
     *out_size = total;
 }
@@ -680,6 +675,22 @@ int st_dev_crc32(st_ctx *c, const uint8_t *data, uint64_t n, uint32_t crc_in, ui
 
 int st_dev_sog_bundle(st_ctx *c, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size) {
+    return guard([&] {
+        ST_REQUIRE(c && meta && tex && out && size, ST_ERR_ARG, "NULL argument");
+        use_device(c);
+        const uint8_t *view;
+        uint64_t n;
+        sog_bundle_dev(c, *meta, count, *tex, dos_time, dos_date, &view, &n);
+        uint8_t *buf = (uint8_t *)std::malloc(n);
+        ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
+        std::memcpy(buf, view, n);
+        *out = buf;
+        *size = n;
+    });
+}
+
+int st_dev_sog_bundle_view(st_ctx *c, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
+                           uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *size) {
     return guard([&] {
         ST_REQUIRE(c && meta && tex && out && size, ST_ERR_ARG, "NULL argument");
         use_device(c);

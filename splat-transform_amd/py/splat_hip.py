@@ -61,7 +61,7 @@ EXPORTS = [
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
-    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_sog_bundle', 'st_free',
+    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
 ]
 
 
@@ -335,6 +335,16 @@ class Context:
         check(lib().st_dev_crc32(self.h, _ptr(data), ctypes.c_uint64(n), ctypes.c_uint32(crc_in),
                                  ctypes.byref(out)))
         return out.value
+
+    def dev_sog_bundle_view(self, meta, count, tex, dos_time, dos_date):
+        """as dev_sog_bundle without the copy: (address, size) of the context's pinned archive"""
+        t = SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                          ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        check(lib().st_dev_sog_bundle_view(self.h, ctypes.byref(meta), ctypes.c_uint64(count), ctypes.byref(t),
+                                           ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
+                                           ctypes.byref(size)))
+        return out.value, size.value
 
     def dev_sog_bundle(self, meta, count, tex, dos_time, dos_date):
         """the .sog archive bytes of device textures (dict as for dev_sog) and their SogMeta"""

@@ -135,3 +135,23 @@ def test_sog_bundle_vs_reference(ctx, name):
     # the archive is the reference's layout around our entries
     entries = [(i.filename, got.read(i.filename)) for i in gi]
     assert oc.zip_store(entries, t, d) == z
+
+
+def test_sog_bundle_device_view_matches_copy(ctx):
+    g = Golden('sog_bundle')
+    c = next(c for c in g.meta['cases'] if c['name'] == 'b_sh1')
+    cols = {k: torch.from_numpy(v).cuda() for k, v in g.table('b_sh1_in_').items()}
+    draws = oracle.mulberry32(c['seed'], c['draws'] + 64)
+    W, H, pal, cw, ch = sh.sog_geometry(c['n'], 3)
+    u8 = dict(device='cuda', dtype=torch.uint8)
+    tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
+    tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
+    meta, used = ctx.dev_sog(cols, c['iters'], draws, tex)
+    assert used == c['draws']
+    t, d = oc.dos_clock(*c['clock'])
+    z = ctx.dev_sog_bundle(meta, c['n'], tex, t, d)
+    addr, size = ctx.dev_sog_bundle_view(meta, c['n'], tex, t, d)
+    import ctypes
+    assert ctypes.string_at(addr, size) == z
+    host, _ = ctx.sog_bundle(g.table('b_sh1_in_'), c['iters'], draws, t, d)
+    assert host == z
