@@ -5,8 +5,11 @@ One step = the whole SOG device pipeline of write-sog.ts:110-370 over one
 synthetic SH-3 splat table already resident in HBM: Morton order, means /
 quats textures, cluster1d(scales), cluster1d(f_dc) + opacity, the SH palette
 k-means (K = 65,536, 10 iterations), the codebook cluster1d and the shN
-textures.  WebP / ZIP encoding of the textures is host work outside the
-device pipeline and is not in the timed region.
+textures (the headline is the device pipeline).  The .sog
+container stage -- WebP lossless encode of the seven textures, CRC-32 and the
+ZIP layout (st_dev_sog_bundle_view, archive in pinned host memory) -- is timed
+right after on the same textures and reported in "container" with the
+end-to-end rate.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S]
 
@@ -155,8 +158,11 @@ def main():
         ops = splat_dist.HipOps(ctx, dev)
         comm = splat_dist.Comm()
 
+        last = {}
+
         def step():
-            _, _, used = splat_dist.write_sog(ops, comm, cols, args.iters, draws)
+            t_, m_, used = splat_dist.write_sog(ops, comm, cols, args.iters, draws)
+            last.update(tex=t_, meta=m_)
             return None, used
     torch.cuda.synchronize()
 
@@ -200,6 +206,25 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    # the .sog container of this step's textures on rank 0 (outside the headline's timed region)
+    if world == 1:
+        bmeta, btex, bcount = meta, tex, n
+    else:
+        import splat_dist
+        bmeta, btex, bcount = splat_dist.meta_struct(last['meta']), last['tex'], n * world
+    ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)  # warm: workspace + pinned archive
+    ctx.set_profiling(True)
+    ctx.reset_kernel_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, archive_bytes = ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)
+    container_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    ckern = {}
+    for name in ('webp.predict', 'webp.hist', 'webp.bits', 'webp.emit', 'crc32'):
+        ms, cnt = ctx.kernel_stats(name)
+        ckern[name] = ms / args.steps
+    ctx.set_profiling(False)
     total_splats = n * world * args.steps
     value = total_splats / elapsed / 1e6
     avg_sweep_s = (sweep_ms / max(sweep_launches, 1)) / 1e3
@@ -246,6 +271,15 @@ def main():
             'launches': sweep_launches,
         },
         'cpu_baseline': cpu,
+        'container': {
+            'what': 'st_dev_sog_bundle_view: WebP lossless x7 + CRC-32 + ZIP of this step\'s textures, archive in '
+                    'pinned host memory (rank 0)',
+            'ms': container_ms,
+            'archive_bytes': archive_bytes,
+            'kernel_ms': ckern,
+            'end_to_end_ms_per_step': elapsed / args.steps * 1e3 + container_ms,
+            'end_to_end_Msplats_per_s': (n * world) / (elapsed / args.steps + container_ms / 1e3) / 1e6,
+        },
         'stages_ms': stages,
         'kernels': kstats,
         'draws_used_per_step': used,

@@ -370,3 +370,31 @@ def _sh_coeffs(cols):
     # band rule of transform.ts:20 / write-sog.ts:296
     miss = next((i for i in range(45) if f'f_rest_{i}' not in cols), -1)
     return [0, 3, 8, 15][{9: 1, 24: 2, -1: 3}.get(miss, 0)]
+
+
+def meta_struct(meta):
+    """the SogMeta (st_abi.h) of write_sog's meta dict, for the .sog bundle on rank 0"""
+    m = sh.SogMeta()
+    m.width, m.height = meta['width'], meta['height']
+    for k in range(3):
+        m.means_min[k] = meta['means_min'][k]
+        m.means_max[k] = meta['means_max'][k]
+    for k in range(256):
+        m.scales_codebook[k] = float(meta['scales_codebook'][k])
+        m.sh0_codebook[k] = float(meta['sh0_codebook'][k])
+        if meta['sh_bands']:
+            m.shn_codebook[k] = float(meta['shn_codebook'][k])
+    m.sh_bands, m.palette_size = meta['sh_bands'], meta['palette_size']
+    m.shn_width, m.shn_height = meta['shn_width'], meta['shn_height']
+    return m
+
+
+def write_sog_bundle(ops, comm, cols, iters, draws, dos_time, dos_date):
+    """writeSog to a .sog archive (write-sog.ts:110-370 + zip-writer.ts) for the global table:
+    the textures of write_sog, then WebP + CRC + ZIP on rank 0's device.  Returns the archive
+    bytes on rank 0 (None elsewhere) and the draws consumed."""
+    tex, meta, used = write_sog(ops, comm, cols, iters, draws)
+    if tex is None:
+        return None, used
+    return ops.ctx.dev_sog_bundle(meta_struct(meta), meta['count'], tex, dos_time, dos_date), used
+

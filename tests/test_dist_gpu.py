@@ -56,7 +56,9 @@ def _rank(rank, world, port, n, seed, iters, q):
     tex, meta, used = splat_dist.write_sog(ops, comm, cols, iters, draws)
     torch.cuda.synchronize()
     if rank == 0:
-        q.put(dict(tex={k: v.cpu().numpy() for k, v in tex.items()}, meta=meta, used=used))
+        # the .sog archive of the gathered textures (WebP + CRC + ZIP on rank 0's device)
+        z = ctx.dev_sog_bundle(splat_dist.meta_struct(meta), meta['count'], tex, 0x6a2b, 0x58b1)
+        q.put(dict(tex={k: v.cpu().numpy() for k, v in tex.items()}, meta=meta, used=used, zip=z))
     dist.destroy_process_group()
     ctx.close()
 
@@ -99,4 +101,6 @@ def test_two_rank_write_sog_matches_single_device():
     assert list(m['means_min']) == list(meta.means_min) and list(m['means_max']) == list(meta.means_max)
     for k in ('scales_codebook', 'sh0_codebook', 'shn_codebook'):
         assert np.array_equal(np.asarray(m[k]).view(np.uint32), np.array(getattr(meta, k), np.float32).view(np.uint32)), k
+    # identical .sog archive
+    assert ctx.dev_sog_bundle(meta, n, tex, 0x6a2b, 0x58b1) == res['zip']
     ctx.close()
