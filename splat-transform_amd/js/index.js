@@ -14,6 +14,8 @@
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
 //   cluster1d(dataTable, iterations)        write-sog.ts:56-99
 //   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
+//   writeSogBundle(dataTable, iterations)   write-sog.ts:110-370 to a .sog (WebP + CRC + ZIP on the device)
+//   WebpEncoder                             utils/webp.ts:19-41 (encodeLosslessRGBA)
 //
 // Math.random: the device consumes the reference's draws in the reference's
 // order.  Draws are taken from Math.random up front; the ones a call did not
@@ -174,6 +176,29 @@ const sogTextures = (dataTable, iterations) => {
         draws => addon.sog(cols, names, iterations, draws)));
 };
 
+// utils/webp.ts:19-41: same class shape; the stream is a valid lossless WebP of the same
+// pixels (encoded on the device), not libwebp's bytes
+class WebpEncoder {
+    static async create() { return new WebpEncoder(); }
+
+    encodeLosslessRGBA(rgba, width, height, stride = width * 4) {
+        return addon.webpLossless(rgba, width, height, stride);
+    }
+}
+
+// writeSog to a .sog bundle (write-sog.ts:110-370 with its ZipWriter): the archive bytes.
+// The ZIP clock is taken like zip-writer.ts:39-41 when the archive is written.
+const writeSogBundle = (dataTable, iterations) => {
+    const { cols, names } = f32Columns(dataTable);
+    const k = 65536;
+    const date = new Date();
+    const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
+    const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
+    const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
+        draws => addon.sogBundle(cols, names, iterations, draws, dosTime, dosDate));
+    return Promise.resolve(res.archive);
+};
+
 module.exports = {
     Column,
     DataTable,
@@ -185,5 +210,7 @@ module.exports = {
     packCompressed,
     kmeans,
     cluster1d,
-    sogTextures
+    sogTextures,
+    WebpEncoder,
+    writeSogBundle
 };

@@ -21,6 +21,11 @@
  *        -> {centroids, labels, used}
  *   sog(cols, names, iters, draws)            writeSog textures + meta (write-sog.ts:110-370)
  *        -> {meta fields, textures, used}
+ *   webpLossless(rgba, w, h, stride) -> Buffer WebpEncoder.encodeLosslessRGBA (utils/webp.ts:19-41,
+ *                                             lib/webp_encode.c:19-29)
+ *   sogBundle(cols, names, iters, draws, dosTime, dosDate)
+ *        -> {archive: Buffer, used}           writeSog to a .sog (write-sog.ts:110-370 +
+ *                                             serialize/zip-writer.ts)
  */
 #include <node_api.h>
 #include <stdio.h>
@@ -483,6 +488,75 @@ fail:
     return NULL;
 }
 
+static napi_value js_webp_lossless(napi_env env, napi_callback_info info) {
+    size_t argc = 4, len = 0;
+    napi_value argv[4], out;
+    st_ctx *ctx;
+    uint8_t *webp = NULL;
+    uint64_t size = 0;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    {
+        const uint8_t *rgba = (const uint8_t *)ta_data(env, argv[0], napi_uint8_array, &len);
+        const int32_t w = (int32_t)num(env, argv[1]), h = (int32_t)num(env, argv[2]);
+        const int32_t stride = argc > 3 ? (int32_t)num(env, argv[3]) : w * 4;
+        if (!rgba) return NULL;
+        if (w < 1 || h < 1 || stride < w * 4 || (uint64_t)stride * (uint64_t)(h - 1) + (uint64_t)w * 4 > len) {
+            napi_throw_range_error(env, NULL, "splat-hip: rgba buffer smaller than width x height");
+            return NULL;
+        }
+        if (!get_ctx(env, &ctx)) return NULL;
+        int rc = st_webp_lossless(ctx, rgba, w, h, stride, &webp, &size);
+        if (rc != ST_OK) return throw_st(env, rc);
+        NAPI_OK(napi_create_buffer_copy(env, size, webp, NULL, &out));
+        st_free(webp);
+        return out;
+    }
+fail:
+    st_free(webp);
+    return NULL;
+}
+
+static napi_value js_sog_bundle(napi_env env, napi_callback_info info) {
+    size_t argc = 6, nd = 0;
+    napi_value argv[6], out, buf;
+    uint32_t m = 0;
+    uint64_t n = 0, used = 0, size = 0;
+    float **cols = NULL;
+    char **names = NULL;
+    uint8_t *zip = NULL;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
+    names = str_list(env, argv[1], m);
+    {
+        const int32_t iters = (int32_t)num(env, argv[2]);
+        double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);
+        const uint16_t dos_time = (uint16_t)num(env, argv[4]), dos_date = (uint16_t)num(env, argv[5]);
+        if (!draws) goto fail;
+        if (!get_ctx(env, &ctx)) goto fail;
+        st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+        int rc = st_sog_bundle(ctx, &tab, iters, draws, nd, &used, dos_time, dos_date, &zip, &size);
+        if (rc != ST_OK) {
+            free(cols);
+            free_strs(names, m);
+            return throw_st(env, rc);
+        }
+        NAPI_OK(napi_create_buffer_copy(env, size, zip, NULL, &buf));
+        NAPI_OK(napi_create_object(env, &out));
+        set_named(env, out, "archive", buf);
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    st_free(zip);
+    free(cols);
+    free_strs(names, m);
+    return out;
+fail:
+    st_free(zip);
+    free(cols);
+    free_strs(names, m);
+    return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     static const struct {
         const char *name;
@@ -496,7 +570,9 @@ static napi_value init(napi_env env, napi_value exports) {
                {"packCompressed", js_pack_compressed},
                {"kmeans", js_kmeans},
                {"cluster1d", js_cluster1d},
-               {"sog", js_sog}};
+               {"sog", js_sog},
+               {"webpLossless", js_webp_lossless},
+               {"sogBundle", js_sog_bundle}};
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;
         if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok) return NULL;

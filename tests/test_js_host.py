@@ -38,7 +38,8 @@ def test_addon_exports(addon_built):
     assert r.returncode == 0, r.stderr
     keys, ver = r.stdout.strip().rsplit(' ', 1)
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
-                                       'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog'])
+                                       'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
+                                       'webpLossless', 'sogBundle'])
     assert ver == '1'
 
 
@@ -96,3 +97,44 @@ def test_host_roundtrip_matches_oracle(addon_built, tmp_path):
     assert np.array_equal(np.fromfile(tmp_path / 'labels.u32', np.uint32), labels)
     assert np.array_equal(np.fromfile(tmp_path / 'centroids.f32', np.float32).view(np.uint32),
                           cen.reshape(-1).view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_js_sog_bundle_matches_reference(addon_built, tmp_path):
+    import io
+    import struct
+    import zipfile
+    from PIL import Image
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import sog_container as oc
+    from golden_io import Golden
+    g = Golden('sog_bundle')
+    c = next(c for c in g.meta['cases'] if c['name'] == 'b_sh1')
+    cols = g.table('b_sh1_in_')
+    for k, v in cols.items():
+        v.astype(np.float32).tofile(tmp_path / f'{k}.f32')
+    img = np.random.default_rng(3).integers(0, 256, (45, 67, 4), dtype=np.uint8)
+    img.tofile(tmp_path / 'img.rgba')
+    (tmp_path / 'manifest.json').write_text(json.dumps(
+        {'columns': list(cols), 'seed': c['seed'], 'iters': c['iters'], 'clock': c['clock'], 'w': 67, 'h': 45}))
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'sog_bundle.js'), str(tmp_path)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    z = (tmp_path / 'out.sog').read_bytes()
+    ref = zipfile.ZipFile(io.BytesIO(g['b_sh1_zip'].tobytes()))
+    got = zipfile.ZipFile(io.BytesIO(z))
+    assert got.testzip() is None
+    assert [i.filename for i in got.infolist()] == [i.filename for i in ref.infolist()]
+    assert [i.date_time for i in got.infolist()] == [i.date_time for i in ref.infolist()]
+    assert got.read('meta.json') == ref.read('meta.json')
+    for i in ref.infolist():
+        if i.filename.endswith('.webp'):
+            p = ref.read(i.filename)
+            w, h, n = struct.unpack('<III', p[4:16])
+            want = np.frombuffer(p[16:16 + n], np.uint8).reshape(h, w, 4)
+            assert np.array_equal(np.array(Image.open(io.BytesIO(got.read(i.filename))).convert('RGBA')), want)
+    t, d = oc.dos_clock(*c['clock'])
+    assert oc.zip_store([(i.filename, got.read(i.filename)) for i in got.infolist()], t, d) == z
+    dec = np.array(Image.open(tmp_path / 'img.webp').convert('RGBA'))
+    assert np.array_equal(dec, img)
