@@ -32,6 +32,10 @@
  *   st_zip_store                            ZipWriter (store, descriptors)      serialize/zip-writer.ts:35-135
  *   st_sog_meta_json                        JSON.stringify(meta)                write-sog.ts:271-293,350-361
  *   st_sog_bundle / st_dev_sog_bundle       writeSog to a .sog bundle           write-sog.ts:110-140,361-366
+ *   st_ply_read_header / _parse_header      readPly header search + parseHeader readers/read-ply.ts:54-137
+ *   st_ply_read / st_dev_ply_read           readPly element rows -> columns     read-ply.ts:139-188
+ *   st_dev_ply_transpose                    (the same, rows already in HBM)     read-ply.ts:165-182
+ *   st_decompress_ply / st_dev_...          decompressPly                       readers/decompress-ply.ts:82-232
  *
  * Conventions
  *  - Columns are SoA float32 arrays of n rows (the reference's Float32Array
@@ -102,6 +106,31 @@ typedef struct {
     float shn_codebook[256];
     int32_t shn_width, shn_height;  /* shN_centroids texture */
 } st_sog_meta;
+
+/* PLY header (readers/read-ply.ts:7-26); property types of read-ply.ts:28-40 */
+enum st_ply_type {
+    ST_PLY_CHAR = 1, ST_PLY_UCHAR, ST_PLY_SHORT, ST_PLY_USHORT, ST_PLY_INT, ST_PLY_UINT, ST_PLY_FLOAT, ST_PLY_DOUBLE
+};
+#define ST_PLY_MAX_ELEMENTS 16
+#define ST_PLY_MAX_PROPS 256
+#define ST_PLY_NAME 64
+typedef struct {
+    char name[ST_PLY_NAME];
+    int32_t type; /* st_ply_type */
+} st_ply_property;
+typedef struct {
+    char name[ST_PLY_NAME];
+    uint64_t count;
+    int32_t nprops;
+    st_ply_property props[ST_PLY_MAX_PROPS];
+} st_ply_element;
+typedef struct {
+    uint64_t header_bytes;   /* bytes up to and including "\nend_header\n" */
+    int32_t nelements;
+    int32_t ncomments;
+    char comments[8192];     /* the comment texts, '\n'-separated */
+    st_ply_element elements[ST_PLY_MAX_ELEMENTS];
+} st_ply_header;
 
 typedef struct {
     uint8_t *means_l, *means_u, *quats, *scales, *sh0; /* width*height*4 each */
@@ -237,6 +266,28 @@ int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count,
 int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                   uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);
 void st_free(void *p);
+
+/* ---- PLY ingest and the compressed-PLY reader ----------------
+ * Same header grammar and errors as readPly (binary little-endian bodies; the
+ * "format" line is not checked, as in the reference).  A body shorter than the
+ * header declares is an error here (the reference silently keeps stale bytes). */
+int st_ply_parse_header(const uint8_t *data, uint64_t len, st_ply_header *out);
+int st_ply_read_header(int32_t fd, st_ply_header *out);   /* pread of the first <= 128 KiB */
+uint64_t st_ply_row_bytes(const st_ply_header *h, int32_t element);
+/* element rows (row_bytes each, 4-byte aligned, device) -> per-property device columns */
+int st_dev_ply_transpose(st_ctx *ctx, const st_ply_header *h, int32_t element, const uint8_t *rows,
+                         uint64_t nrows, void *const *cols);
+/* element `element` of the file fd -> device columns (pinned double-buffered chunks, H2D, transpose) */
+int st_dev_ply_read(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, void *const *cols);
+/* the same into host columns (readPly's TypedArrays) */
+int st_ply_read(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, void *const *host_cols);
+/* decompressPly: chunk = the 18 float columns min_x..max_b in decompress-ply.ts:14-33 order,
+ * vertex = packed_position, packed_rotation, packed_scale, packed_color; sh = nsh (0/9/24/45)
+ * uint8 f_rest columns; out = x y z f_dc_0..2 opacity rot_0..3 scale_0..2 then f_rest_0.. */
+int st_dev_decompress_ply(st_ctx *ctx, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                          const uint8_t *const *sh, int32_t nsh, float *const *out);
+int st_decompress_ply(st_ctx *ctx, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                      const uint8_t *const *sh, int32_t nsh, float *const *out);
 
 #ifdef __cplusplus
 }

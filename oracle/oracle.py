@@ -194,3 +194,24 @@ def sog(cols, sh_coeffs, iters, draws):
     else:
         del out['shN_labels']
     return rc, out, meta, used.value
+
+
+CHUNK_COLS = ['min_x', 'min_y', 'min_z', 'max_x', 'max_y', 'max_z', 'min_scale_x', 'min_scale_y', 'min_scale_z',
+              'max_scale_x', 'max_scale_y', 'max_scale_z', 'min_r', 'min_g', 'min_b', 'max_r', 'max_g', 'max_b']
+VERTEX_COLS = ['packed_position', 'packed_rotation', 'packed_scale', 'packed_color']
+DECOMP_COLS = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'rot_0', 'rot_1', 'rot_2', 'rot_3',
+               'scale_0', 'scale_1', 'scale_2']
+
+
+def decompress_ply(chunk, vertex, sh):
+    """decompressPly (decompress-ply.ts:82-232) -> dict of float32 columns"""
+    n = len(vertex['packed_position'])
+    ch = [np.ascontiguousarray(chunk[k], np.float32) for k in CHUNK_COLS]
+    vx = [np.ascontiguousarray(vertex[k], np.uint32) for k in VERTEX_COLS]
+    sv = [np.ascontiguousarray(a, np.uint8) for a in sh]
+    names = DECOMP_COLS + [f'f_rest_{i}' for i in range(len(sv))]
+    out = {k: np.empty(n, np.float32) for k in names}
+    lib().st_o_decompress_ply(ctypes.c_uint64(n), _ptrs(ch), _ptrs(vx), _ptrs(sv) if sv else None,
+                              ctypes.c_int(len(sv)), _ptrs([out[k] for k in names]))
+    return out
+

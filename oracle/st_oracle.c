@@ -996,3 +996,64 @@ done:
     free(indices);
     return rc;
 }
+
+/* ---- compressed-PLY reader (readers/decompress-ply.ts:82-232) ------------------
+ * chunk: the 18 chunk columns in the order of decompress-ply.ts:14-33 (min_x .. max_b);
+ * vertex: packed_position, packed_rotation, packed_scale, packed_color;
+ * out: 14 columns x, y, z, f_dc_0..2, opacity, rot_0..3, scale_0..2 (decompress-ply.ts:112-128),
+ * then nsh f_rest columns. */
+static inline double dp_unorm(uint32_t v, int bits) {
+    const uint32_t t = (1u << bits) - 1;  /* decompress-ply.ts:132-135 */
+    return (double)(v & t) / (double)t;
+}
+static inline double dp_lerp(double a, double b, double t) { return a * (1 - t) + b * t; }
+
+void st_o_decompress_ply(uint64_t n, const float *const chunk[18], const uint32_t *const vertex[4],
+                         const uint8_t *const *sh, int nsh, float *const *out) {
+    const double SH_C0 = 0.28209479177387814;
+    const double norm = 1.0 / (sqrt(2) * 0.5);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t ci = i / 256;
+        const uint32_t pp = vertex[0][i], pr = vertex[1][i], ps = vertex[2][i], pc = vertex[3][i];
+        /* unpack111011 (:136-140) */
+        const double px = dp_unorm(pp >> 21, 11), py = dp_unorm(pp >> 11, 10), pz = dp_unorm(pp, 11);
+        const double sx = dp_unorm(ps >> 21, 11), sy = dp_unorm(ps >> 11, 10), sz = dp_unorm(ps, 11);
+        /* unpack8888 (:141-146) */
+        const double cx = dp_unorm(pc >> 24, 8), cy = dp_unorm(pc >> 16, 8), cz = dp_unorm(pc >> 8, 8),
+                     cw = dp_unorm(pc, 8);
+        /* unpackRot (:147-163) */
+        const double a = (dp_unorm(pr >> 20, 10) - 0.5) * norm;
+        const double b = (dp_unorm(pr >> 10, 10) - 0.5) * norm;
+        const double c = (dp_unorm(pr, 10) - 0.5) * norm;
+        const double m = sqrt(fmax(0, 1.0 - (a * a + b * b + c * c)));
+        double r[4];
+        switch (pr >> 30) {
+            case 0: r[0] = m; r[1] = a; r[2] = b; r[3] = c; break;
+            case 1: r[0] = a; r[1] = m; r[2] = b; r[3] = c; break;
+            case 2: r[0] = a; r[1] = b; r[2] = m; r[3] = c; break;
+            default: r[0] = a; r[1] = b; r[2] = c; r[3] = m; break;
+        }
+        /* :183-216 */
+        out[0][i] = (float)dp_lerp(chunk[0][ci], chunk[3][ci], px);
+        out[1][i] = (float)dp_lerp(chunk[1][ci], chunk[4][ci], py);
+        out[2][i] = (float)dp_lerp(chunk[2][ci], chunk[5][ci], pz);
+        const double cr = dp_lerp(chunk[12][ci], chunk[15][ci], cx);
+        const double cg = dp_lerp(chunk[13][ci], chunk[16][ci], cy);
+        const double cb = dp_lerp(chunk[14][ci], chunk[17][ci], cz);
+        out[3][i] = (float)((cr - 0.5) / SH_C0);
+        out[4][i] = (float)((cg - 0.5) / SH_C0);
+        out[5][i] = (float)((cb - 0.5) / SH_C0);
+        out[6][i] = (float)(-st_o_log(1 / cw - 1));
+        for (int k = 0; k < 4; ++k) out[7 + k][i] = (float)r[k];
+        out[11][i] = (float)dp_lerp(chunk[6][ci], chunk[9][ci], sx);
+        out[12][i] = (float)dp_lerp(chunk[7][ci], chunk[10][ci], sy);
+        out[13][i] = (float)dp_lerp(chunk[8][ci], chunk[11][ci], sz);
+    }
+    /* :219-229 */
+    for (int k = 0; k < nsh; ++k)
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint8_t v = sh[k][i];
+            const double t = (v == 0) ? 0 : (v == 255) ? 1 : (v + 0.5) / 256;
+            out[14 + k][i] = (float)((t - 0.5) * 8);
+        }
+}

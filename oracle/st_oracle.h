@@ -87,6 +87,10 @@ int st_o_sog(uint64_t n, const float *const m14[14], const float *const *sh, int
              uint8_t *means_l, uint8_t *means_u, uint8_t *quats, uint8_t *scales, uint8_t *sh0,
              uint8_t *shn_centroids, uint8_t *shn_labels);
 
+/* compressed-PLY reader (decompress-ply.ts:82-232): see st_oracle.c */
+void st_o_decompress_ply(uint64_t n, const float *const chunk[18], const uint32_t *const vertex[4],
+                         const uint8_t *const *sh, int nsh, float *const *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,9 @@ struct st_ctx {
     // pinned host buffer of the last .sog archive (st_dev_sog_bundle*)
     void *archive = nullptr;
     size_t archive_bytes = 0;
+    // pinned host chunks of the PLY reader
+    void *io = nullptr;
+    size_t io_bytes = 0;
     std::vector<st::StageTimer> marks;
     bool timing = false;
     std::string last_timings = "{}";
@@ -113,6 +116,7 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
 }
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
 void *archive_buf(st_ctx *c, size_t bytes);  // host pinned archive buffer (reused, grow-only)
+void *io_buf(st_ctx *c, size_t bytes);       // host pinned file-chunk buffer (reused, grow-only)
 void use_device(st_ctx *c);
 void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
 
@@ -173,6 +177,11 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
                      const uint8_t *scale_lab, const uint8_t *color_lab, const uint32_t *shn_lab, st_sog_meta *meta,
                      const st_sog_textures *out);
 void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *out);
+
+// PLY ingest / compressed-PLY reader (st_ply.hip)
+void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols);
+void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                        const uint8_t *const *sh, int nsh, float *const *out);
 
 // multi-GPU building blocks (st_dist.hip)
 void minmax_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, double *lo, double *hi);

@@ -1,0 +1,480 @@
+// st_ply.hip -- PLY ingest and the compressed-PLY reader on the device (SURVEY.md 8f
+// ranks 2 and 4).
+//
+//   header         readers/read-ply.ts:111-137 (search for "\nend_header\n" within
+//                  128 KiB), parseHeader :54-110 (host; same accepted grammar and errors)
+//   body           read-ply.ts:142-188 copies each row's properties into per-property
+//                  TypedArrays.  Here: the element's rows stream file -> pinned chunk ->
+//                  HBM (double-buffered, the pread of chunk k+1 overlapping the copy and
+//                  transpose of chunk k) and k_ply_cols turns rows into columns:
+//                  RB rows per workgroup staged in LDS with coalesced 4-byte loads, then
+//                  one thread per (property, row) assembles the value's bytes and stores
+//                  it (consecutive threads = consecutive rows of one column: coalesced).
+//                  HBM traffic 2 x row bytes per row.
+//   decompress     readers/decompress-ply.ts:82-232: one thread per splat, f64 JS
+//                  semantics (lerp, unorm unpacking, Math.sqrt, V8's Math.log), f32
+//                  stores; SH bytes -> floats.                   read 16 B + D, write 56 + 4D B
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "st_internal.h"
+#include "st_jsmath.h"
+
+namespace st {
+namespace {
+
+int type_size(int t) {
+    switch (t) {
+        case ST_PLY_CHAR:
+        case ST_PLY_UCHAR: return 1;
+        case ST_PLY_SHORT:
+        case ST_PLY_USHORT: return 2;
+        case ST_PLY_INT:
+        case ST_PLY_UINT:
+        case ST_PLY_FLOAT: return 4;
+        case ST_PLY_DOUBLE: return 8;
+        default: return 0;
+    }
+}
+
+int type_of(const std::string &s) {
+    static const char *names[] = {"char", "uchar", "short", "ushort", "int", "uint", "float", "double"};
+    for (int i = 0; i < 8; ++i)
+        if (s == names[i]) return ST_PLY_CHAR + i;
+    return 0;
+}
+
+// JS parseInt(s, 10); false for NaN
+bool js_parse_int(const std::string &s, long long &v) {
+    size_t i = 0;
+    while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\r' || s[i] == '\v' || s[i] == '\f')) ++i;
+    bool neg = false;
+    if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+    size_t j = i;
+    long long x = 0;
+    while (j < s.size() && s[j] >= '0' && s[j] <= '9') {
+        if (x < (1ll << 53)) x = x * 10 + (s[j] - '0');
+        ++j;
+    }
+    if (j == i) return false;
+    v = neg ? -x : x;
+    return true;
+}
+
+void parse_header(const uint8_t *data, uint64_t len, st_ply_header *h) {
+    std::memset(h, 0, sizeof *h);
+    static const char magic[4] = {'p', 'l', 'y', '\n'};
+    static const char end[12] = {'\n', 'e', 'n', 'd', '_', 'h', 'e', 'a', 'd', 'e', 'r', '\n'};
+    ST_REQUIRE(len >= 16, ST_ERR_ARG, "ply: failed to read file header");
+    ST_REQUIRE(std::memcmp(data, magic, 4) == 0, ST_ERR_ARG, "ply: invalid file header");
+    // the reader grows the header byte by byte from 16 bytes until it ends with "\nend_header\n"
+    uint64_t hs = 0;
+    const uint64_t lim = len < 128 * 1024 ? len : 128 * 1024;
+    for (uint64_t k = 17; k <= lim; ++k)
+        if (std::memcmp(data + k - 12, end, 12) == 0) {
+            hs = k;
+            break;
+        }
+    ST_REQUIRE(hs, ST_ERR_ARG, "ply: failed to read file header");
+    h->header_bytes = hs;
+    // split on '\n', drop empty lines, skip the first line
+    std::vector<std::string> lines;
+    std::string cur;
+    for (uint64_t i = 0; i < hs; ++i) {
+        if (data[i] == '\n') {
+            if (!cur.empty()) lines.push_back(cur);
+            cur.clear();
+        } else {
+            cur.push_back((char)data[i]);
+        }
+    }
+    if (!cur.empty()) lines.push_back(cur);
+    st_ply_element *el = nullptr;
+    std::string comments;
+    for (size_t li = 1; li < lines.size(); ++li) {
+        std::vector<std::string> w;
+        size_t a = 0;
+        const std::string &ln = lines[li];
+        for (;;) {
+            const size_t b = ln.find(' ', a);
+            w.push_back(ln.substr(a, b == std::string::npos ? std::string::npos : b - a));
+            if (b == std::string::npos) break;
+            a = b + 1;
+        }
+        if (w[0] == "ply" || w[0] == "format" || w[0] == "end_header") continue;
+        if (w[0] == "comment") {
+            if (!comments.empty()) comments += '\n';
+            comments += ln.size() > 8 ? ln.substr(8) : std::string();
+            h->ncomments++;
+        } else if (w[0] == "element") {
+            ST_REQUIRE(w.size() == 3, ST_ERR_ARG, "ply: invalid ply header");
+            ST_REQUIRE(h->nelements < ST_PLY_MAX_ELEMENTS, ST_ERR_UNSUPPORTED, "ply: too many elements");
+            ST_REQUIRE(w[1].size() < ST_PLY_NAME, ST_ERR_UNSUPPORTED, "ply: element name too long");
+            el = &h->elements[h->nelements++];
+            std::memcpy(el->name, w[1].c_str(), w[1].size() + 1);
+            long long cnt = 0;
+            if (!js_parse_int(w[2], cnt)) cnt = 0;  // parseInt NaN: an empty element
+            ST_REQUIRE(cnt >= 0, ST_ERR_ARG, "ply: invalid typed array length");
+            el->count = (uint64_t)cnt;
+        } else if (w[0] == "property") {
+            ST_REQUIRE(el && w.size() == 3 && type_of(w[1]), ST_ERR_ARG, "ply: invalid ply header");
+            ST_REQUIRE(el->nprops < ST_PLY_MAX_PROPS, ST_ERR_UNSUPPORTED, "ply: too many properties");
+            ST_REQUIRE(w[2].size() < ST_PLY_NAME, ST_ERR_UNSUPPORTED, "ply: property name too long");
+            st_ply_property &p = el->props[el->nprops++];
+            std::memcpy(p.name, w[2].c_str(), w[2].size() + 1);
+            p.type = type_of(w[1]);
+        } else {
+            throw Error(ST_ERR_ARG, "ply: unrecognized header value '" + w[0] + "' in ply header");
+        }
+    }
+    ST_REQUIRE(comments.size() < sizeof h->comments, ST_ERR_UNSUPPORTED, "ply: comments too long");
+    std::memcpy(h->comments, comments.c_str(), comments.size() + 1);
+}
+
+uint32_t row_bytes(const st_ply_element &e) {
+    uint32_t r = 0;
+    for (int p = 0; p < e.nprops; ++p) r += type_size(e.props[p].type);
+    return r;
+}
+
+struct PropSlot {
+    uint32_t offset;  // byte offset in the row
+    uint32_t size;    // 1, 2, 4, 8
+};
+
+constexpr uint32_t LDS_ROWS_BYTES = 48 * 1024;
+
+// rows [0, nrows) of the staged chunk -> columns at rows [row0, row0 + nrows)
+__global__ __launch_bounds__(256) void k_ply_cols(const uint8_t *__restrict__ rows, uint64_t nrows, uint32_t R,
+                                                  uint32_t RB, const PropSlot *__restrict__ props, int nprops,
+                                                  void *const *__restrict__ cols, uint64_t row0) {
+    extern __shared__ uint32_t lds32[];
+    const uint8_t *lds8 = (const uint8_t *)lds32;
+    const uint64_t r0 = (uint64_t)blockIdx.x * RB;
+    const uint32_t nr = (uint32_t)((nrows - r0) < RB ? (nrows - r0) : RB);
+    // RB is a multiple of 4, so every block starts 4-byte aligned; a partial last word is
+    // read byte by byte (never past the rows)
+    const uint32_t bytes = nr * R, words = bytes / 4;
+    const uint32_t *src = (const uint32_t *)(rows + r0 * R);
+    for (uint32_t i = threadIdx.x; i < words; i += 256) lds32[i] = src[i];
+    if (threadIdx.x == 0 && (bytes & 3)) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < (bytes & 3); ++k) v |= (uint32_t)rows[r0 * R + words * 4 + k] << (8 * k);
+        lds32[words] = v;
+    }
+    __syncthreads();
+    const uint32_t total = nr * (uint32_t)nprops;
+    for (uint32_t e = threadIdx.x; e < total; e += 256) {
+        const uint32_t p = e / nr, r = e - p * nr;
+        const PropSlot ps = props[p];
+        const uint32_t off = r * R + ps.offset;
+        uint64_t v = 0;
+        for (uint32_t k = 0; k < ps.size; ++k) v |= (uint64_t)lds8[off + k] << (8 * k);
+        const uint64_t row = row0 + r0 + r;
+        switch (ps.size) {
+            case 1: ((uint8_t *)cols[p])[row] = (uint8_t)v; break;
+            case 2: ((uint16_t *)cols[p])[row] = (uint16_t)v; break;
+            case 4: ((uint32_t *)cols[p])[row] = (uint32_t)v; break;
+            default: ((uint64_t *)cols[p])[row] = v; break;
+        }
+    }
+}
+
+struct Transposer {
+    st_ctx *c;
+    uint32_t R, RB;
+    int nprops;
+    PropSlot *d_props;
+    void **d_cols;
+    Transposer(st_ctx *ctx, const st_ply_element &e, void *const *cols, const std::string &tag) : c(ctx) {
+        R = row_bytes(e);
+        nprops = e.nprops;
+        RB = R ? (LDS_ROWS_BYTES / R) & ~3u : 64;
+        ST_REQUIRE(R == 0 || RB >= 4, ST_ERR_UNSUPPORTED, "ply: rows longer than 12 KiB");
+        if (RB > 256) RB = 256;
+        std::vector<PropSlot> ps(nprops);
+        uint32_t off = 0;
+        for (int p = 0; p < nprops; ++p) {
+            ps[p] = {off, (uint32_t)type_size(e.props[p].type)};
+            off += ps[p].size;
+        }
+        d_props = wsT<PropSlot>(c, tag + ".props", nprops ? nprops : 1);
+        d_cols = wsT<void *>(c, tag + ".cols", nprops ? nprops : 1);
+        if (nprops) {
+            ST_HIP(hipMemcpyAsync(d_props, ps.data(), sizeof(PropSlot) * nprops, hipMemcpyHostToDevice, c->stream));
+            ST_HIP(hipMemcpyAsync(d_cols, cols, sizeof(void *) * nprops, hipMemcpyHostToDevice, c->stream));
+        }
+    }
+    void run(const uint8_t *rows, uint64_t nrows, uint64_t row0) {
+        if (!nrows || !nprops) return;
+        KTimer kt(c, "ply.cols");
+        hipLaunchKernelGGL(k_ply_cols, dim3((unsigned)((nrows + RB - 1) / RB)), dim3(256), (RB * R + 3) & ~3u,
+                           c->stream, rows, nrows, R, RB, d_props, nprops, (void *const *)d_cols, row0);
+        ST_LAUNCH_CHECK();
+    }
+};
+
+// ---- compressed PLY -------------------------------------------------------------
+struct DecompArgs {
+    const float *chunk[18];
+    const uint32_t *vertex[4];
+    float *out[14];
+};
+
+__device__ inline double unorm(uint32_t v, int bits) {
+    const uint32_t t = (1u << bits) - 1;
+    return (double)(v & t) / (double)t;
+}
+__device__ inline double lerp(double a, double b, double t) { return a * (1 - t) + b * t; }
+
+__global__ __launch_bounds__(256) void k_decompress(DecompArgs A, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t ci = i / 256;
+    const uint32_t pp = A.vertex[0][i], pr = A.vertex[1][i], ps = A.vertex[2][i], pc = A.vertex[3][i];
+    const double px = unorm(pp >> 21, 11), py = unorm(pp >> 11, 10), pz = unorm(pp, 11);
+    const double sx = unorm(ps >> 21, 11), sy = unorm(ps >> 11, 10), sz = unorm(ps, 11);
+    const double cx = unorm(pc >> 24, 8), cy = unorm(pc >> 16, 8), cz = unorm(pc >> 8, 8), cw = unorm(pc, 8);
+    const double norm = 1.0 / (__builtin_sqrt(2.0) * 0.5);
+    const double a = (unorm(pr >> 20, 10) - 0.5) * norm;
+    const double b = (unorm(pr >> 10, 10) - 0.5) * norm;
+    const double c = (unorm(pr, 10) - 0.5) * norm;
+    const double s2 = 1.0 - (a * a + b * b + c * c);
+    const double m = __builtin_sqrt(s2 > 0 ? s2 : 0.0);  // Math.max(0, x) of a finite x
+    const uint32_t which = pr >> 30;
+    const double r0 = which == 0 ? m : a;
+    const double r1 = which == 0 ? a : (which == 1 ? m : b);
+    const double r2 = which <= 1 ? b : (which == 2 ? m : c);
+    const double r3 = which <= 2 ? c : m;
+    A.out[0][i] = (float)lerp(A.chunk[0][ci], A.chunk[3][ci], px);
+    A.out[1][i] = (float)lerp(A.chunk[1][ci], A.chunk[4][ci], py);
+    A.out[2][i] = (float)lerp(A.chunk[2][ci], A.chunk[5][ci], pz);
+    const double SH_C0 = 0.28209479177387814;
+    A.out[3][i] = (float)((lerp(A.chunk[12][ci], A.chunk[15][ci], cx) - 0.5) / SH_C0);
+    A.out[4][i] = (float)((lerp(A.chunk[13][ci], A.chunk[16][ci], cy) - 0.5) / SH_C0);
+    A.out[5][i] = (float)((lerp(A.chunk[14][ci], A.chunk[17][ci], cz) - 0.5) / SH_C0);
+    A.out[6][i] = (float)(-js::log(1 / cw - 1));
+    A.out[7][i] = (float)r0;
+    A.out[8][i] = (float)r1;
+    A.out[9][i] = (float)r2;
+    A.out[10][i] = (float)r3;
+    A.out[11][i] = (float)lerp(A.chunk[6][ci], A.chunk[9][ci], sx);
+    A.out[12][i] = (float)lerp(A.chunk[7][ci], A.chunk[10][ci], sy);
+    A.out[13][i] = (float)lerp(A.chunk[8][ci], A.chunk[11][ci], sz);
+}
+
+constexpr int SH_MAX = 45;
+struct ShArgs {
+    const uint8_t *sh[SH_MAX];
+    float *out[SH_MAX];
+};
+
+__global__ __launch_bounds__(256) void k_decompress_sh(ShArgs A, int nsh, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    for (int k = 0; k < nsh; ++k) {
+        const uint32_t v = A.sh[k][i];
+        const double t = (v == 0) ? 0.0 : (v == 255) ? 1.0 : (v + 0.5) / 256;
+        A.out[k][i] = (float)((t - 0.5) * 8);
+    }
+}
+
+}  // namespace
+
+void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                        const uint8_t *const *sh, int nsh, float *const *out) {
+    ST_REQUIRE(nsh == 0 || nsh == 9 || nsh == 24 || nsh == 45, ST_ERR_ARG,
+               "decompress: SH column count must be 0, 9, 24 or 45 (decompress-ply.ts:62)");
+    if (!n) return;
+    DecompArgs A{};
+    for (int k = 0; k < 18; ++k) A.chunk[k] = chunk[k];
+    for (int k = 0; k < 4; ++k) A.vertex[k] = vertex[k];
+    for (int k = 0; k < 14; ++k) A.out[k] = out[k];
+    {
+        KTimer kt(c, "ply.decompress");
+        hipLaunchKernelGGL(k_decompress, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, A, n);
+        ST_LAUNCH_CHECK();
+    }
+    if (nsh) {
+        ShArgs S{};
+        for (int k = 0; k < nsh; ++k) {
+            S.sh[k] = sh[k];
+            S.out[k] = out[14 + k];
+        }
+        hipLaunchKernelGGL(k_decompress_sh, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, S, nsh, n);
+        ST_LAUNCH_CHECK();
+    }
+}
+
+// one element of a PLY file (fd) into device columns, streamed through pinned chunks
+void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols) {
+    ST_REQUIRE(element >= 0 && element < h.nelements, ST_ERR_ARG, "ply: element index out of range");
+    uint64_t off = h.header_bytes;
+    for (int e = 0; e < element; ++e) off += h.elements[e].count * row_bytes(h.elements[e]);
+    const st_ply_element &el = h.elements[element];
+    Transposer tp(c, el, cols, "ply");
+    const uint64_t R = tp.R, total = el.count * R;
+    if (!total) return;
+    // chunks of whole LDS blocks, ~32 MiB (ST_PLY_CHUNK overrides the byte target: tests)
+    uint64_t target = 32ull << 20;
+    if (const char *e = std::getenv("ST_PLY_CHUNK")) target = std::strtoull(e, nullptr, 10);
+    const uint64_t per = (uint64_t)tp.RB * R;
+    const uint64_t chunk_rows = (target / per > 0 ? target / per : 1) * tp.RB;
+    const uint64_t chunk_bytes = chunk_rows * R;
+    uint8_t *pin = (uint8_t *)io_buf(c, 2 * (chunk_bytes + 64));
+    uint8_t *stage[2] = {wsT<uint8_t>(c, "ply.stage0", chunk_bytes + 64), wsT<uint8_t>(c, "ply.stage1", chunk_bytes + 64)};
+    hipEvent_t ev[2];
+    ST_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    ST_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    bool pending[2] = {false, false};
+    try {
+        uint64_t row = 0;
+        for (int k = 0; row < el.count; ++k) {
+            const int b = k & 1;
+            const uint64_t nr = (el.count - row) < chunk_rows ? (el.count - row) : chunk_rows;
+            const uint64_t bytes = nr * R;
+            uint8_t *hb = pin + b * (chunk_bytes + 64);
+            if (pending[b]) ST_HIP(hipEventSynchronize(ev[b]));  // the copy out of hb is done
+            uint64_t got = 0;
+            while (got < bytes) {
+                const ssize_t r = pread(fd, hb + got, bytes - got, (off_t)(off + row * R + got));
+                ST_REQUIRE(r > 0, ST_ERR_ARG, "ply: file shorter than its header declares");
+                got += (uint64_t)r;
+            }
+            ST_HIP(hipMemcpyAsync(stage[b], hb, bytes, hipMemcpyHostToDevice, c->stream));
+            ST_HIP(hipEventRecord(ev[b], c->stream));
+            pending[b] = true;
+            tp.run(stage[b], nr, row);
+            row += nr;
+        }
+        ST_HIP(hipStreamSynchronize(c->stream));
+    } catch (...) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipEventDestroy(ev[0]);
+        (void)hipEventDestroy(ev[1]);
+        throw;
+    }
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+}
+
+}  // namespace st
+
+using namespace st;
+
+extern "C" {
+
+int st_ply_parse_header(const uint8_t *data, uint64_t len, st_ply_header *out) {
+    return guard([&] {
+        ST_REQUIRE(data && out, ST_ERR_ARG, "NULL argument");
+        parse_header(data, len, out);
+    });
+}
+
+int st_ply_read_header(int32_t fd, st_ply_header *out) {
+    return guard([&] {
+        ST_REQUIRE(out && fd >= 0, ST_ERR_ARG, "bad argument");
+        std::vector<uint8_t> buf(128 * 1024);
+        uint64_t got = 0;
+        for (;;) {
+            const ssize_t r = pread(fd, buf.data() + got, buf.size() - got, (off_t)got);
+            if (r <= 0) break;
+            got += (uint64_t)r;
+            if (got == buf.size()) break;
+        }
+        parse_header(buf.data(), got, out);
+    });
+}
+
+uint64_t st_ply_row_bytes(const st_ply_header *h, int32_t element) {
+    if (!h || element < 0 || element >= h->nelements) return 0;
+    return row_bytes(h->elements[element]);
+}
+
+int st_dev_ply_transpose(st_ctx *c, const st_ply_header *h, int32_t element, const uint8_t *rows, uint64_t nrows,
+                         void *const *cols) {
+    return guard([&] {
+        ST_REQUIRE(c && h && rows && cols && element >= 0 && element < h->nelements, ST_ERR_ARG, "bad argument");
+        ST_REQUIRE(((uintptr_t)rows & 3) == 0, ST_ERR_ARG, "ply: rows must be 4-byte aligned");
+        use_device(c);
+        Transposer tp(c, h->elements[element], cols, "plyt");
+        tp.run(rows, nrows, 0);
+    });
+}
+
+int st_dev_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, void *const *cols) {
+    return guard([&] {
+        ST_REQUIRE(c && h && cols && fd >= 0, ST_ERR_ARG, "bad argument");
+        use_device(c);
+        ply_read_dev(c, fd, *h, element, cols);
+    });
+}
+
+int st_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, void *const *host_cols) {
+    return guard([&] {
+        ST_REQUIRE(c && h && host_cols && fd >= 0 && element >= 0 && element < h->nelements, ST_ERR_ARG,
+                   "bad argument");
+        use_device(c);
+        const st_ply_element &el = h->elements[element];
+        std::vector<void *> dcols(el.nprops);
+        for (int p = 0; p < el.nprops; ++p)
+            dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * type_size(el.props[p].type) + 8);
+        ply_read_dev(c, fd, *h, element, dcols.data());
+        for (int p = 0; p < el.nprops; ++p)
+            if (el.count)
+                ST_HIP(hipMemcpyAsync(host_cols[p], dcols[p], el.count * type_size(el.props[p].type),
+                                      hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+int st_dev_decompress_ply(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                          const uint8_t *const *sh, int32_t nsh, float *const *out) {
+    return guard([&] {
+        ST_REQUIRE(c && chunk && vertex && out && (nsh == 0 || sh), ST_ERR_ARG, "NULL argument");
+        use_device(c);
+        decompress_ply_dev(c, n, chunk, vertex, sh, nsh, out);
+    });
+}
+
+int st_decompress_ply(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
+                      const uint8_t *const *sh, int32_t nsh, float *const *out) {
+    return guard([&] {
+        ST_REQUIRE(c && chunk && vertex && out && (nsh == 0 || sh), ST_ERR_ARG, "NULL argument");
+        ST_REQUIRE(nsh == 0 || nsh == 9 || nsh == 24 || nsh == 45, ST_ERR_ARG,
+                   "decompress: SH column count must be 0, 9, 24 or 45 (decompress-ply.ts:62)");
+        use_device(c);
+        const uint64_t nch = (n + 255) / 256;
+        std::vector<const float *> dchunk(18);
+        std::vector<const uint32_t *> dvert(4);
+        std::vector<const uint8_t *> dsh(nsh);
+        std::vector<float *> dout(14 + nsh);
+        for (int k = 0; k < 18; ++k) {
+            float *d = wsT<float>(c, "dph.ch" + std::to_string(k), nch);
+            if (nch) ST_HIP(hipMemcpyAsync(d, chunk[k], nch * 4, hipMemcpyHostToDevice, c->stream));
+            dchunk[k] = d;
+        }
+        for (int k = 0; k < 4; ++k) {
+            uint32_t *d = wsT<uint32_t>(c, "dph.v" + std::to_string(k), n);
+            if (n) ST_HIP(hipMemcpyAsync(d, vertex[k], n * 4, hipMemcpyHostToDevice, c->stream));
+            dvert[k] = d;
+        }
+        for (int k = 0; k < nsh; ++k) {
+            uint8_t *d = wsT<uint8_t>(c, "dph.s" + std::to_string(k), n);
+            if (n) ST_HIP(hipMemcpyAsync(d, sh[k], n, hipMemcpyHostToDevice, c->stream));
+            dsh[k] = d;
+        }
+        for (int k = 0; k < 14 + nsh; ++k) dout[k] = wsT<float>(c, "dph.o" + std::to_string(k), n);
+        decompress_ply_dev(c, n, dchunk.data(), dvert.data(), dsh.data(), nsh, dout.data());
+        for (int k = 0; k < 14 + nsh; ++k)
+            if (n) ST_HIP(hipMemcpyAsync(out[k], dout[k], n * 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+}  // extern "C"

@@ -58,6 +58,17 @@ void *archive_buf(st_ctx *c, size_t bytes) {
     return c->archive;
 }
 
+void *io_buf(st_ctx *c, size_t bytes) {
+    if (c->io_bytes < bytes) {
+        if (c->io) ST_HIP(hipHostFree(c->io));
+        c->io = nullptr;
+        c->io_bytes = 0;
+        ST_HIP(hipHostMalloc(&c->io, bytes, hipHostMallocDefault));
+        c->io_bytes = bytes;
+    }
+    return c->io;
+}
+
 void use_device(st_ctx *c) { ST_HIP(hipSetDevice(c->device)); }
 
 void mark(st_ctx *c, const char *name) {
@@ -218,6 +229,7 @@ void st_ctx_destroy(st_ctx *c) {
     c->ws.release();
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->archive) (void)hipHostFree(c->archive);
+    if (c->io) (void)hipHostFree(c->io);
     for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
     for (auto &k : c->kevents) {
         (void)hipEventDestroy(k.a);

@@ -50,6 +50,35 @@ class SogTextures(ctypes.Structure):
                 ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shn_centroids', 'shn_labels')]
 
 
+PLY_TYPES = {1: ('char', np.int8), 2: ('uchar', np.uint8), 3: ('short', np.int16), 4: ('ushort', np.uint16),
+             5: ('int', np.int32), 6: ('uint', np.uint32), 7: ('float', np.float32), 8: ('double', np.float64)}
+
+
+class PlyProperty(ctypes.Structure):
+    _fields_ = [('name', ctypes.c_char * 64), ('type', ctypes.c_int32)]
+
+
+class PlyElement(ctypes.Structure):
+    _fields_ = [('name', ctypes.c_char * 64), ('count', ctypes.c_uint64), ('nprops', ctypes.c_int32),
+                ('props', PlyProperty * 256)]
+
+
+class PlyHeader(ctypes.Structure):
+    _fields_ = [('header_bytes', ctypes.c_uint64), ('nelements', ctypes.c_int32), ('ncomments', ctypes.c_int32),
+                ('comments', ctypes.c_char * 8192), ('elements', PlyElement * 16)]
+
+    def layout(self):
+        """[(element name, count, [(prop name, numpy dtype)])]"""
+        out = []
+        for e in self.elements[:self.nelements]:
+            out.append((e.name.decode(), e.count,
+                        [(p.name.decode(), PLY_TYPES[p.type][1]) for p in e.props[:e.nprops]]))
+        return out
+
+    def comment_list(self):
+        return self.comments.decode().split('\n') if self.ncomments else []
+
+
 EXPORTS = [
     'st_abi_version', 'st_last_error', 'st_device_count', 'st_ctx_create', 'st_ctx_destroy', 'st_ctx_set_stream',
     'st_ctx_synchronize', 'st_ctx_last_timings', 'st_ctx_set_profiling', 'st_ctx_reset_kernel_stats',
@@ -62,6 +91,8 @@ EXPORTS = [
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
     'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
+    'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
+    'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
 ]
 
 
@@ -83,8 +114,10 @@ def lib():
         L.st_ctx_destroy.restype = None
         L.st_free.restype = None
         L.st_webp_max_size.restype = ctypes.c_uint64
+        L.st_ply_row_bytes.restype = ctypes.c_uint64
         for name in EXPORTS:
-            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy', 'st_free', 'st_webp_max_size'):
+            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy', 'st_free', 'st_webp_max_size',
+                            'st_ply_row_bytes'):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -181,6 +214,21 @@ def sog_meta_json(meta, count):
     out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
     check(lib().st_sog_meta_json(ctypes.byref(meta), ctypes.c_uint64(count), ctypes.byref(out), ctypes.byref(size)))
     return _take(out, size)
+
+
+CHUNK_COLS = ['min_x', 'min_y', 'min_z', 'max_x', 'max_y', 'max_z', 'min_scale_x', 'min_scale_y', 'min_scale_z',
+              'max_scale_x', 'max_scale_y', 'max_scale_z', 'min_r', 'min_g', 'min_b', 'max_r', 'max_g', 'max_b']
+VERTEX_COLS = ['packed_position', 'packed_rotation', 'packed_scale', 'packed_color']
+DECOMP_COLS = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'rot_0', 'rot_1', 'rot_2', 'rot_3',
+               'scale_0', 'scale_1', 'scale_2']
+
+
+def ply_parse_header(data):
+    """readPly's header (read-ply.ts:54-137) from the first bytes of a file (host)"""
+    h = PlyHeader()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    check(lib().st_ply_parse_header(buf, ctypes.c_uint64(len(data)), ctypes.byref(h)))
+    return h
 
 
 def device_count():
@@ -309,6 +357,38 @@ class Context:
                                      ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size)
 
+    def read_ply(self, path):
+        """readPly (read-ply.ts:111-191) -> (comments, [(element, {prop: numpy column})]); rows go through HBM"""
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = PlyHeader()
+            check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+            out = []
+            for ei, (name, count, props) in enumerate(h.layout()):
+                cols = {pn: np.empty(count, dt) for pn, dt in props}
+                ptrs = (ctypes.c_void_p * max(len(props), 1))(*[cols[pn].ctypes.data for pn, _ in props])
+                check(lib().st_ply_read(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(ei), ptrs))
+                out.append((name, cols))
+            return h.comment_list(), out
+        finally:
+            os.close(fd)
+
+    def decompress_ply(self, chunk, vertex, sh):
+        """decompressPly (decompress-ply.ts:82-232): chunk/vertex dicts of numpy columns, sh list of uint8
+        columns -> dict of float32 columns in the reference's order"""
+        n = len(vertex['packed_position'])
+        keep = [np.ascontiguousarray(chunk[k], np.float32) for k in CHUNK_COLS]
+        cp = (ctypes.c_void_p * 18)(*[a.ctypes.data for a in keep])
+        vk = [np.ascontiguousarray(vertex[k], np.uint32) for k in VERTEX_COLS]
+        vp = (ctypes.c_void_p * 4)(*[a.ctypes.data for a in vk])
+        sk = [np.ascontiguousarray(a, np.uint8) for a in sh]
+        sp = (ctypes.c_void_p * max(len(sk), 1))(*[a.ctypes.data for a in sk])
+        names = DECOMP_COLS + [f'f_rest_{i}' for i in range(len(sk))]
+        out = {k: np.empty(n, np.float32) for k in names}
+        op = (ctypes.c_void_p * len(names))(*[out[k].ctypes.data for k in names])
+        check(lib().st_decompress_ply(self.h, ctypes.c_uint64(n), cp, vp, sp, ctypes.c_int32(len(sk)), op))
+        return out
+
     def sog_bundle(self, cols, iters, draws, dos_time, dos_date):
         """writeSog to a .sog bundle: (archive bytes, draws used)"""
         t = make_table(cols)
@@ -355,6 +435,35 @@ class Context:
                                       ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
                                       ctypes.byref(size)))
         return _take(out, size)
+
+    def read_ply_dev(self, path, device='cuda'):
+        """readPly into device columns: (comments, [(element, {prop: torch tensor})])"""
+        import torch
+        tmap = {np.int8: torch.int8, np.uint8: torch.uint8, np.int16: torch.int16, np.uint16: torch.uint16,
+                np.int32: torch.int32, np.uint32: torch.uint32, np.float32: torch.float32, np.float64: torch.float64}
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = PlyHeader()
+            check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+            out = []
+            for ei, (name, count, props) in enumerate(h.layout()):
+                cols = {pn: torch.empty(count, dtype=tmap[dt], device=device) for pn, dt in props}
+                ptrs = (ctypes.c_void_p * max(len(props), 1))(*[cols[pn].data_ptr() for pn, _ in props])
+                check(lib().st_dev_ply_read(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(ei), ptrs))
+                out.append((name, cols))
+            return h.comment_list(), out
+        finally:
+            os.close(fd)
+
+    def dev_decompress_ply(self, chunk, vertex, sh, out):
+        """device form of decompress_ply: torch tensors in, `out` dict of float32 tensors (DECOMP_COLS + f_rest_*)"""
+        n = vertex['packed_position'].numel()
+        cp = (ctypes.c_void_p * 18)(*[chunk[k].data_ptr() for k in CHUNK_COLS])
+        vp = (ctypes.c_void_p * 4)(*[vertex[k].data_ptr() for k in VERTEX_COLS])
+        sp = (ctypes.c_void_p * max(len(sh), 1))(*[a.data_ptr() for a in sh])
+        names = DECOMP_COLS + [f'f_rest_{i}' for i in range(len(sh))]
+        op = (ctypes.c_void_p * len(names))(*[out[k].data_ptr() for k in names])
+        check(lib().st_dev_decompress_ply(self.h, ctypes.c_uint64(n), cp, vp, sp, ctypes.c_int32(len(sh)), op))
 
     def dev_transform(self, cols, params):
         t = make_table(cols)

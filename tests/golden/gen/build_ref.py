@@ -34,6 +34,7 @@ FILES = [
     'utils/math', 'utils/rotate-sh', 'utils/kd-tree', 'utils/k-means',
     'writers/write-compressed-ply', 'writers/write-sog',
     'serialize/crc', 'serialize/writer', 'serialize/zip-writer',
+    'readers/read-ply', 'readers/decompress-ply',
 ]
 
 EXTRA_EXPORTS = {
@@ -109,6 +110,10 @@ def main():
     shutil.copy(os.path.join(HERE, 'pc_math.js'), os.path.join(OUT, '__stubs/playcanvas.js'))
     for rel in FILES:
         src = open(os.path.join(REF, 'src', rel + '.ts')).read()
+        # type-only imports have no runtime part
+        src = re.sub(r'^import type [^;]*;\n', '', src, flags=re.M)
+        # non-null assertions `x!.y`
+        src = re.sub(r'([\w\)\]])!\.', r'\1.', src)
         js = strip(src)
         js = lower_modules(js, make_resolver(rel))
         js = lower_nullish(js)

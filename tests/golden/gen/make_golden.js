@@ -32,6 +32,8 @@ const { kmeans } = require(path.join(REF, 'utils/k-means.js'));
 const { writeCompressedPly } = require(path.join(REF, 'writers/write-compressed-ply.js'));
 const { writeSog, cluster1d } = require(path.join(REF, 'writers/write-sog.js'));
 const { combine } = require(path.join(REF, 'index.js'));
+const { readPly } = require(path.join(REF, 'readers/read-ply.js'));
+const { isCompressedPly, decompressPly } = require(path.join(REF, 'readers/decompress-ply.js'));
 const pc = require(path.join(REF, '__stubs/playcanvas.js'));
 
 // ---------------------------------------------------------------------------
@@ -432,6 +434,70 @@ cases.sog_bundle = async () => {
         fx.add(`${name}_zip`, new Uint8Array(zip.buffer, zip.byteOffset, zip.length));
         fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
     }
+    fx.save();
+};
+
+// PLY ingest (readers/read-ply.ts:111-191) and the compressed-PLY reader
+// (readers/decompress-ply.ts:6-232): a mixed-type two-element PLY, and the
+// compressed files of the compressed_ply cases read back and decompressed.
+cases.ply_io = async () => {
+    const fx = new Fixture('ply_io');
+    const dir = fs.mkdtempSync('/tmp/st_ply_');
+    const readFile = async (bytes) => {
+        const p = path.join(dir, 'f.ply');
+        fs.writeFileSync(p, bytes);
+        const fh = await fs.promises.open(p, 'r');
+        try { return await readPly(fh); } finally { await fh.close(); }
+    };
+    // (1) mixed property types, comments, two elements
+    const g = new Gen(611);
+    const props = [['float', 'x', 4], ['double', 'd', 8], ['uchar', 'u', 1], ['char', 'c', 1], ['short', 's', 2],
+        ['ushort', 'us', 2], ['int', 'i', 4], ['uint', 'ui', 4], ['float', 'y', 4]];
+    const nv = 1500, ne = 7;
+    const header = ['ply', 'format binary_little_endian 1.0', 'comment made by make_golden.js', 'comment second',
+        `element vertex ${nv}`].concat(props.map(p => `property ${p[0]} ${p[1]}`))
+        .concat([`element extra ${ne}`, 'property float a', 'property uchar b', 'end_header']).join('\n') + '\n';
+    const rowV = props.reduce((t, p) => t + p[2], 0), rowE = 5;
+    const body = Buffer.alloc(nv * rowV + ne * rowE);
+    let o = 0;
+    for (let r = 0; r < nv; ++r) {
+        body.writeFloatLE(g.normal(0, 10), o); o += 4;
+        body.writeDoubleLE(g.normal(0, 1e6), o); o += 8;
+        body.writeUInt8(g.int(256), o); o += 1;
+        body.writeInt8(g.int(256) - 128, o); o += 1;
+        body.writeInt16LE(g.int(65536) - 32768, o); o += 2;
+        body.writeUInt16LE(g.int(65536), o); o += 2;
+        body.writeInt32LE((g.int(65536) << 16) | g.int(65536), o); o += 4;
+        body.writeUInt32LE(((g.int(65536) << 16) | g.int(65536)) >>> 0, o); o += 4;
+        body.writeFloatLE(r === 3 ? NaN : g.normal(), o); o += 4;
+    }
+    for (let r = 0; r < ne; ++r) {
+        body.writeFloatLE(r * 0.25, o); o += 4;
+        body.writeUInt8(200 + r, o); o += 1;
+    }
+    const file = Buffer.concat([Buffer.from(header, 'ascii'), body]);
+    fx.add('mixed_file', new Uint8Array(file.buffer, file.byteOffset, file.length));
+    const ply = await readFile(file);
+    fx.meta.mixed = { comments: ply.comments, elements: ply.elements.map(e => ({
+        name: e.name, rows: e.dataTable.numRows,
+        columns: e.dataTable.columns.map(c => [c.name, c.dataType]) })) };
+    for (const e of ply.elements) for (const c of e.dataTable.columns) fx.add(`mixed_${e.name}_${c.name}`, c.data);
+    // (2) the compressed PLY files of the compressed_ply fixture, read and decompressed
+    const cp = JSON.parse(fs.readFileSync(path.join(OUT, 'compressed_ply.json'), 'utf8'));
+    const blob = fs.readFileSync(path.join(OUT, 'compressed_ply.bin'));
+    const part = (k) => { const a = cp.arrays[k]; return blob.subarray(a.offset, a.offset + a.nbytes); };
+    fx.meta.compressed = [];
+    for (const name of cp.meta.cases) {
+        const f = Buffer.concat([part(`${name}_header`), part(`${name}_chunk`), part(`${name}_vertex`), part(`${name}_sh`)]);
+        const cply = await readFile(f);
+        const ok = isCompressedPly(cply);
+        fx.meta.compressed.push({ name, isCompressed: ok });
+        if (!ok) continue;
+        const out = decompressPly(cply);
+        fx.meta[`${name}_columns`] = out.columns.map(c => c.name);
+        for (const c of out.columns) fx.add(`${name}_dec_${c.name}`, c.data);
+    }
+    fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
     fx.save();
 };
 
