@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "st_internal.h"
@@ -148,6 +149,7 @@ struct PropSlot {
 };
 
 constexpr uint32_t LDS_ROWS_BYTES = 48 * 1024;
+constexpr int kReaders = 8;  // pread threads per file chunk
 
 // rows [0, nrows) of the staged chunk -> columns at rows [row0, row0 + nrows)
 __global__ __launch_bounds__(256) void k_ply_cols(const uint8_t *__restrict__ rows, uint64_t nrows, uint32_t R,
@@ -320,8 +322,8 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
     Transposer tp(c, el, cols, "ply");
     const uint64_t R = tp.R, total = el.count * R;
     if (!total) return;
-    // chunks of whole LDS blocks, ~32 MiB (ST_PLY_CHUNK overrides the byte target: tests)
-    uint64_t target = 32ull << 20;
+    // chunks of whole LDS blocks, ~64 MiB (ST_PLY_CHUNK overrides the byte target: tests)
+    uint64_t target = 64ull << 20;
     if (const char *e = std::getenv("ST_PLY_CHUNK")) target = std::strtoull(e, nullptr, 10);
     const uint64_t per = (uint64_t)tp.RB * R;
     const uint64_t chunk_rows = (target / per > 0 ? target / per : 1) * tp.RB;
@@ -340,12 +342,32 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
             const uint64_t bytes = nr * R;
             uint8_t *hb = pin + b * (chunk_bytes + 64);
             if (pending[b]) ST_HIP(hipEventSynchronize(ev[b]));  // the copy out of hb is done
-            uint64_t got = 0;
-            while (got < bytes) {
-                const ssize_t r = pread(fd, hb + got, bytes - got, (off_t)(off + row * R + got));
-                ST_REQUIRE(r > 0, ST_ERR_ARG, "ply: file shorter than its header declares");
-                got += (uint64_t)r;
+            // page-cache copies are per-thread memcpy bound: several readers per chunk
+            const uint64_t base = off + row * R;
+            const int nt = bytes >= (8ull << 20) ? kReaders : 1;
+            std::vector<std::thread> th;
+            std::vector<int> ok(nt, 1);
+            for (int t = 0; t < nt; ++t) {
+                const uint64_t a0 = bytes * t / nt, a1 = bytes * (t + 1) / nt;
+                auto job = [&, t, a0, a1] {
+                    uint64_t got = a0;
+                    while (got < a1) {
+                        const ssize_t r = pread(fd, hb + got, a1 - got, (off_t)(base + got));
+                        if (r <= 0) {
+                            ok[t] = 0;
+                            return;
+                        }
+                        got += (uint64_t)r;
+                    }
+                };
+                if (nt == 1)
+                    job();
+                else
+                    th.emplace_back(job);
             }
+            for (auto &x : th) x.join();
+            for (int t = 0; t < nt; ++t)
+                ST_REQUIRE(ok[t], ST_ERR_ARG, "ply: file shorter than its header declares");
             ST_HIP(hipMemcpyAsync(stage[b], hb, bytes, hipMemcpyHostToDevice, c->stream));
             ST_HIP(hipEventRecord(ev[b], c->stream));
             pending[b] = true;
