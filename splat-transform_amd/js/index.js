@@ -16,6 +16,8 @@
 //   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
 //   writeSogBundle(dataTable, iterations)   write-sog.ts:110-370 to a .sog (WebP + CRC + ZIP on the device)
 //   WebpEncoder                             utils/webp.ts:19-41 (encodeLosslessRGBA)
+//   readPly(fileHandle)                     readers/read-ply.ts:111-191
+//   isCompressedPly / decompressPly(ply)    readers/decompress-ply.ts:6-232
 //
 // Math.random: the device consumes the reference's draws in the reference's
 // order.  Draws are taken from Math.random up front; the ones a call did not
@@ -199,6 +201,63 @@ const writeSogBundle = (dataTable, iterations) => {
     return Promise.resolve(res.archive);
 };
 
+// readers/read-ply.ts:111-191: {comments, elements: [{name, dataTable}]} from an open FileHandle
+// (rows stream through pinned memory into HBM and are transposed to columns there)
+const readPly = (fileHandle) => {
+    const r = addon.readPly(fileHandle.fd);
+    return Promise.resolve({
+        comments: r.comments,
+        elements: r.elements.map(e => ({
+            name: e.name,
+            dataTable: new DataTable(e.columns.map(c => new Column(c.name, c.data)))
+        }))
+    });
+};
+
+const CHUNK_PROPS = ['min_x', 'min_y', 'min_z', 'max_x', 'max_y', 'max_z', 'min_scale_x', 'min_scale_y',
+    'min_scale_z', 'max_scale_x', 'max_scale_y', 'max_scale_z', 'min_r', 'min_g', 'min_b', 'max_r', 'max_g', 'max_b'];
+const VERTEX_PROPS = ['packed_position', 'packed_rotation', 'packed_scale', 'packed_color'];
+
+// readers/decompress-ply.ts:6-80 (schema check, host)
+const isCompressedPly = (ply) => {
+    const has = (dt, names, ctor) => names.every((n) => {
+        const c = dt.getColumnByName(n);
+        return c && c.data instanceof ctor;
+    });
+    const ne = ply.elements.length;
+    if (ne !== 2 && ne !== 3) return false;
+    const chunk = ply.elements.find(e => e.name === 'chunk');
+    if (!chunk || !has(chunk.dataTable, CHUNK_PROPS, Float32Array)) return false;
+    const vertex = ply.elements.find(e => e.name === 'vertex');
+    if (!vertex || !has(vertex.dataTable, VERTEX_PROPS, Uint32Array)) return false;
+    if (Math.ceil(vertex.dataTable.numRows / 256) !== chunk.dataTable.numRows) return false;
+    if (ne === 3) {
+        const sh = ply.elements.find(e => e.name === 'sh');
+        if (!sh) return false;
+        const d = sh.dataTable;
+        if ([9, 24, 45].indexOf(d.numColumns) === -1) return false;
+        for (let i = 0; i < d.numColumns; ++i) {
+            const c = d.getColumnByName(`f_rest_${i}`);
+            if (!c || !(c.data instanceof Uint8Array)) return false;
+        }
+        if (d.numRows !== vertex.dataTable.numRows) return false;
+    }
+    return true;
+};
+
+// readers/decompress-ply.ts:82-232 (decoded on the device)
+const decompressPly = (ply) => {
+    const chunk = ply.elements.find(e => e.name === 'chunk').dataTable;
+    const vertex = ply.elements.find(e => e.name === 'vertex').dataTable;
+    const shEl = ply.elements.find(e => e.name === 'sh');
+    const shCols = shEl ? shEl.dataTable.columns : [];
+    const out = addon.decompressPly(CHUNK_PROPS.map(n => chunk.getColumnByName(n).data),
+        VERTEX_PROPS.map(n => vertex.getColumnByName(n).data), shCols.map(c => c.data));
+    const names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'rot_0', 'rot_1', 'rot_2', 'rot_3',
+        'scale_0', 'scale_1', 'scale_2'].concat(shCols.map(c => c.name));
+    return new DataTable(out.map((d, i) => new Column(names[i], d)));
+};
+
 module.exports = {
     Column,
     DataTable,
@@ -212,5 +271,8 @@ module.exports = {
     cluster1d,
     sogTextures,
     WebpEncoder,
-    writeSogBundle
+    writeSogBundle,
+    readPly,
+    isCompressedPly,
+    decompressPly
 };

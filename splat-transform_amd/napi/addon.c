@@ -26,6 +26,10 @@
  *   sogBundle(cols, names, iters, draws, dosTime, dosDate)
  *        -> {archive: Buffer, used}           writeSog to a .sog (write-sog.ts:110-370 +
  *                                             serialize/zip-writer.ts)
+ *   readPly(fd) -> {comments, elements:       readPly (readers/read-ply.ts:111-191)
+ *        [{name, columns: [{name, data}]}]}
+ *   decompressPly(chunk[18], vertex[4], sh[]) decompressPly (readers/decompress-ply.ts:82-232)
+ *        -> Float32Array[14 + sh.length]
  */
 #include <node_api.h>
 #include <stdio.h>
@@ -557,6 +561,149 @@ fail:
     return NULL;
 }
 
+static napi_value js_read_ply(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out, els, comments;
+    st_ctx *ctx;
+    st_ply_header *h = NULL;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    {
+        const int32_t fd = (int32_t)num(env, argv[0]);
+        static const napi_typedarray_type tt[9] = {napi_uint8_array, napi_int8_array, napi_uint8_array,
+                                                   napi_int16_array, napi_uint16_array, napi_int32_array,
+                                                   napi_uint32_array, napi_float32_array, napi_float64_array};
+        static const size_t ts[9] = {1, 1, 1, 2, 2, 4, 4, 4, 8};
+        h = (st_ply_header *)calloc(1, sizeof *h);
+        if (!h) goto fail;
+        int rc = st_ply_read_header(fd, h);
+        if (rc != ST_OK) {
+            free(h);
+            return throw_st(env, rc);
+        }
+        if (!get_ctx(env, &ctx)) goto fail;
+        NAPI_OK(napi_create_object(env, &out));
+        NAPI_OK(napi_create_array_with_length(env, (size_t)h->ncomments, &comments));
+        {
+            const char *c = h->comments;
+            for (int32_t i = 0; i < h->ncomments; ++i) {
+                const char *e = strchr(c, '\n');
+                const size_t len = e ? (size_t)(e - c) : strlen(c);
+                napi_value sv;
+                napi_create_string_utf8(env, c, len, &sv);
+                napi_set_element(env, comments, (uint32_t)i, sv);
+                c = e ? e + 1 : c + len;
+            }
+        }
+        NAPI_OK(napi_create_array_with_length(env, (size_t)h->nelements, &els));
+        for (int32_t ei = 0; ei < h->nelements; ++ei) {
+            const st_ply_element *el = &h->elements[ei];
+            napi_value eo, cols, nm;
+            void *ptrs[ST_PLY_MAX_PROPS];
+            napi_create_object(env, &eo);
+            napi_create_string_utf8(env, el->name, NAPI_AUTO_LENGTH, &nm);
+            set_named(env, eo, "name", nm);
+            napi_create_array_with_length(env, (size_t)el->nprops, &cols);
+            for (int32_t p = 0; p < el->nprops; ++p) {
+                napi_value co, pn, ta = new_typed(env, tt[el->props[p].type], (size_t)el->count,
+                                                  ts[el->props[p].type], &ptrs[p]);
+                if (!ta) goto fail;
+                napi_create_object(env, &co);
+                napi_create_string_utf8(env, el->props[p].name, NAPI_AUTO_LENGTH, &pn);
+                set_named(env, co, "name", pn);
+                set_named(env, co, "data", ta);
+                napi_set_element(env, cols, (uint32_t)p, co);
+            }
+            rc = st_ply_read(ctx, fd, h, ei, ptrs);
+            if (rc != ST_OK) {
+                free(h);
+                return throw_st(env, rc);
+            }
+            set_named(env, eo, "columns", cols);
+            napi_set_element(env, els, (uint32_t)ei, eo);
+        }
+        set_named(env, out, "comments", comments);
+        set_named(env, out, "elements", els);
+    }
+    free(h);
+    return out;
+fail:
+    free(h);
+    return NULL;
+}
+
+/* array of TypedArrays of one type -> data pointers; n = common length */
+static void **ta_list(napi_env env, napi_value arr, napi_typedarray_type want, uint32_t expect, uint64_t *n) {
+    uint32_t m = 0;
+    if (napi_get_array_length(env, arr, &m) != napi_ok || (expect && m != expect)) {
+        napi_throw_type_error(env, NULL, "splat-hip: wrong column list");
+        return NULL;
+    }
+    void **p = (void **)calloc(m ? m : 1, sizeof(void *));
+    for (uint32_t i = 0; i < m; ++i) {
+        napi_value e;
+        size_t len = 0;
+        napi_get_element(env, arr, i, &e);
+        p[i] = ta_data(env, e, want, &len);
+        if (!p[i]) {
+            free(p);
+            return NULL;
+        }
+        if (n) *n = len;
+    }
+    return p;
+}
+
+static napi_value js_decompress_ply(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out;
+    void **chunk = NULL, **vertex = NULL, **sh = NULL;
+    uint64_t nch = 0, n = 0, nsv = 0;
+    uint32_t nsh = 0;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(chunk = ta_list(env, argv[0], napi_float32_array, 18, &nch))) goto fail;
+    if (!(vertex = ta_list(env, argv[1], napi_uint32_array, 4, &n))) goto fail;
+    NAPI_OK(napi_get_array_length(env, argv[2], &nsh));
+    if (!(sh = ta_list(env, argv[2], napi_uint8_array, 0, &nsv))) goto fail;
+    if (nch != (n + 255) / 256 || (nsh && nsv != n)) {
+        napi_throw_range_error(env, NULL, "splat-hip: chunk/vertex/sh lengths do not match");
+        goto fail;
+    }
+    {
+        float *o[14 + 45];
+        napi_value tv[14 + 45];
+        if (nsh > 45) {
+            napi_throw_range_error(env, NULL, "splat-hip: at most 45 SH columns");
+            goto fail;
+        }
+        NAPI_OK(napi_create_array_with_length(env, 14 + nsh, &out));
+        for (uint32_t k = 0; k < 14 + nsh; ++k) {
+            void *d;
+            tv[k] = new_typed(env, napi_float32_array, (size_t)n, 4, &d);
+            o[k] = (float *)d;
+            napi_set_element(env, out, k, tv[k]);
+        }
+        if (!get_ctx(env, &ctx)) goto fail;
+        int rc = st_decompress_ply(ctx, n, (const float *const *)chunk, (const uint32_t *const *)vertex,
+                                   (const uint8_t *const *)sh, (int32_t)nsh, o);
+        if (rc != ST_OK) {
+            free(chunk);
+            free(vertex);
+            free(sh);
+            return throw_st(env, rc);
+        }
+    }
+    free(chunk);
+    free(vertex);
+    free(sh);
+    return out;
+fail:
+    free(chunk);
+    free(vertex);
+    free(sh);
+    return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     static const struct {
         const char *name;
@@ -572,7 +719,9 @@ static napi_value init(napi_env env, napi_value exports) {
                {"cluster1d", js_cluster1d},
                {"sog", js_sog},
                {"webpLossless", js_webp_lossless},
-               {"sogBundle", js_sog_bundle}};
+               {"sogBundle", js_sog_bundle},
+               {"readPly", js_read_ply},
+               {"decompressPly", js_decompress_ply}};
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;
         if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok) return NULL;

@@ -39,7 +39,7 @@ def test_addon_exports(addon_built):
     keys, ver = r.stdout.strip().rsplit(' ', 1)
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
                                        'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
-                                       'webpLossless', 'sogBundle'])
+                                       'webpLossless', 'sogBundle', 'readPly', 'decompressPly'])
     assert ver == '1'
 
 
@@ -138,3 +138,29 @@ def test_js_sog_bundle_matches_reference(addon_built, tmp_path):
     assert oc.zip_store([(i.filename, got.read(i.filename)) for i in got.infolist()], t, d) == z
     dec = np.array(Image.open(tmp_path / 'img.webp').convert('RGBA'))
     assert np.array_equal(dec, img)
+
+
+@pytest.mark.gpu
+def test_js_read_ply_and_decompress_match_reference(addon_built, tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from golden_io import Golden
+    from test_ply_cpu import compressed_file
+    g = Golden('ply_io')
+    (tmp_path / 'mixed.ply').write_bytes(g['mixed_file'].tobytes())
+    (tmp_path / 'comp.ply').write_bytes(compressed_file('sh3'))
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'ply_read.js'), str(tmp_path)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    summ = json.loads((tmp_path / 'summary.json').read_text())
+    assert summ['mixed']['comments'] == g.meta['mixed']['comments']
+    assert not summ['mixed']['compressed'] and summ['comp']['compressed']
+    for e in g.meta['mixed']['elements']:
+        for k, _ in e['columns']:
+            ref = g[f"mixed_{e['name']}_{k}"]
+            got = np.fromfile(tmp_path / f"mixed_{e['name']}_{k}.bin", ref.dtype)
+            assert np.array_equal(got.view(f'u{ref.dtype.itemsize}'), ref.view(f'u{ref.dtype.itemsize}')), k
+    assert summ['comp']['decoded'] == g.meta['sh3_columns']
+    for k in g.meta['sh3_columns']:
+        ref = g[f'sh3_dec_{k}']
+        got = np.fromfile(tmp_path / f'comp_dec_{k}.bin', np.float32)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
