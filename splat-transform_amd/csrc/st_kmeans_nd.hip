@@ -113,49 +113,66 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
 }
 
 // point B fragments: pfrag[t][s][lane] = 8 fp16 of B[k = 16s + 8h + j][p = 32t + (lane&31)];
-// one thread per (point, k-step, half); also |sigma p| (rounded up) and the AoS f32 copy
-// (row stride aos_ld(d), zero padded)
+// also |sigma p| (rounded up) and the AoS f32 copy (row stride aos_ld(d), zero padded).
+// One workgroup per 256 points: the d column slices land in LDS (coalesced reads), then
+// the AoS rows and the 8 point tiles' fragments leave as contiguous runs (coalesced writes).
+constexpr int PF_PTS = 256;            // points per workgroup (8 tiles)
+constexpr int PF_LDS_LD = PF_PTS + 1;  // LDS column stride: row-wise reads hit distinct banks
 __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
                                                      int ks, float sigma, uint4 *pfrag, float *pnorm, float *aos) {
-    const uint64_t total = (uint64_t)ntiles * 32 * ks * 2;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += stride) {
-        const uint64_t p = q % ((uint64_t)ntiles * 32);
-        const int sh = (int)(q / ((uint64_t)ntiles * 32));  // s * 2 + h
-        const int s = sh >> 1, h = sh & 1;
-        const bool valid = p < n;
-        const int ld = aos_ld(d);
+    __shared__ float x[61 * PF_LDS_LD];  // d <= 61
+    const uint64_t p0 = (uint64_t)blockIdx.x * PF_PTS;
+    const int j = threadIdx.x;
+    const bool valid = p0 + j < n;
+    for (int k = 0; k < d; ++k) x[k * PF_LDS_LD + j] = valid ? cols[k][p0 + j] : 0.0f;
+    __syncthreads();
+    if (valid) {
+        double nn = 0;
+        for (int k = 0; k < d; ++k) {
+            const double v = (double)(x[k * PF_LDS_LD + j] * sigma);
+            nn += v * v;
+        }
+        pnorm[p0 + j] = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+    }
+    // AoS rows: one float4 per thread-step over the workgroup's contiguous row block
+    const int ld = aos_ld(d), q4 = ld / 4;
+    const uint32_t rows = (uint32_t)min((uint64_t)PF_PTS, n - min(n, p0));
+    float4 *dst = reinterpret_cast<float4 *>(aos + p0 * ld);
+    for (uint32_t f = j; f < rows * q4; f += 256) {
+        const uint32_t r = f / q4, c = (f % q4) * 4;
+        float4 v;
+        v.x = c + 0 < (uint32_t)d ? x[(c + 0) * PF_LDS_LD + r] : 0.0f;
+        v.y = c + 1 < (uint32_t)d ? x[(c + 1) * PF_LDS_LD + r] : 0.0f;
+        v.z = c + 2 < (uint32_t)d ? x[(c + 2) * PF_LDS_LD + r] : 0.0f;
+        v.w = c + 3 < (uint32_t)d ? x[(c + 3) * PF_LDS_LD + r] : 0.0f;
+        dst[f] = v;
+    }
+    // fragments of the 8 tiles (contiguous: tile-major, then k-step, then lane)
+    const uint32_t t0 = blockIdx.x * (PF_PTS / 32);
+    const uint32_t tiles = min((uint32_t)(PF_PTS / 32), ntiles - t0);
+    for (uint32_t f = j; f < tiles * ks * 64; f += 256) {
+        const uint32_t t = f / (ks * 64), rem = f % (ks * 64);
+        const int st = (int)(rem / 64), h = (int)((rem % 64) / 32), l = (int)(rem % 32);
+        const uint32_t r = t * 32 + l;
+        const bool pv = p0 + r < n;
         uint16_t e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = 16 * s + 8 * h + j;
+        for (int jj = 0; jj < 8; ++jj) {
+            const int k = 16 * st + 8 * h + jj;
             uint16_t bits = 0;
             if (k < d) {
-                if (valid) {
-                    const float raw = cols[k][p];
-                    aos[p * ld + k] = raw;
-                    bits = h_bits(-2.0f * h_val(h_bits(raw * sigma)));  // -2 p~ exactly
-                }
-            } else {
-                if (k < d + 3) bits = valid ? (uint16_t)0x3c00u : (uint16_t)0;  // 1.0
-                if (k < ld && valid) aos[p * ld + k] = 0.0f;                    // row padding
+                if (pv) bits = h_bits(-2.0f * h_val(h_bits(x[k * PF_LDS_LD + r] * sigma)));  // -2 p~ exactly
+            } else if (k < d + 3) {
+                bits = pv ? (uint16_t)0x3c00u : (uint16_t)0;  // 1.0
             }
-            e[j] = bits;
+            e[jj] = bits;
         }
         uint4 v;
         v.x = e[0] | ((uint32_t)e[1] << 16);
         v.y = e[2] | ((uint32_t)e[3] << 16);
         v.z = e[4] | ((uint32_t)e[5] << 16);
         v.w = e[6] | ((uint32_t)e[7] << 16);
-        pfrag[((p >> 5) * ks + s) * 64 + h * 32 + (p & 31)] = v;
-        if (sh == 0 && valid) {
-            double nn = 0;
-            for (int c = 0; c < d; ++c) {
-                const double x = (double)(cols[c][p] * sigma);
-                nn += x * x;
-            }
-            pnorm[p] = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
-        }
+        pfrag[(uint64_t)(t0 + t) * ks * 64 + rem] = v;
     }
 }
 
@@ -497,13 +514,23 @@ __device__ inline double ref_dist(const float *__restrict__ crow, const float *_
 // goes to the KdTree walk (kd_resolve_ties).
 // G lanes per point (16 rows of one tile-half, or 32 rows of two), lane r scoring row
 // r % 16 of tile-half code(r / 16)
+// centroid index of row rr (0..15) of tile-half `code` (the MFMA C/D row layout)
+__device__ inline uint32_t code_row(uint32_t code, int rr) {
+    return (code >> 1) * 32 + 4 * (code & 1) + (rr & 3) + 8 * (rr >> 2);
+}
+
+template <int G>
+__device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
+                                  const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
+                                  uint32_t *__restrict__ ties, State *st);
+
 template <int G>
 __device__ inline void fix_group(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
                                  const float *__restrict__ caos, int k, uint64_t p, int r, uint32_t code,
                                  uint32_t *__restrict__ labels, uint32_t *__restrict__ ties, State *st) {
     const int ld = aos_ld(d);
     const int rr = r & 15;
-    const uint32_t c = (code >> 1) * 32 + 4 * (code & 1) + (rr & 3) + 8 * (rr >> 2);
+    const uint32_t c = code_row(code, rr);
     const bool valid = c < (uint32_t)k;
     const float *prow = aos + p * ld;
     // f32 screen: |s - T| <= (d + 2) u T for fma accumulation of fl(c - p)^2 (u = 2^-24), plus
@@ -526,6 +553,17 @@ __device__ inline void fix_group(const float *__restrict__ aos, int d, const flo
             s = __builtin_fmaf(v, v, s);
         }
     }
+    fix_decide<G>(s, valid, c, d, caos, prow, p, r, labels, ties, st);
+}
+
+// the decision of a G-lane group from each lane's f32 screen s of row c: a unique interval
+// minimum decides; otherwise the exact f64 distances of the surviving rows
+template <int G>
+__device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
+                                  const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
+                                  uint32_t *__restrict__ ties, State *st) {
+    const int ld = aos_ld(d);
+    // the screen's error: (d + 2) u T for any summation order of the d non-negative terms
     const float rel = (float)(d + 4) * 0x1p-24f, ab = (float)(d + 2) * 0x1p-126f;
     const float lo = valid ? s - (s * rel + ab) : __builtin_inff();
     const float hi = valid ? s + (s * rel + ab) : __builtin_inff();
@@ -590,6 +628,131 @@ __global__ __launch_bounds__(256) void k_fixpair(const float *__restrict__ aos, 
     const int r = threadIdx.x & 31;
     const uint2 cc = pair_codes[i];
     fix_group<32>(aos, d, cfix, caos, k, pair_pts[i], r, r < 16 ? cc.x : cc.y, labels, ties, st);
+}
+
+// ---- decided points grouped by tile-half ------------------------------------------
+// At K = 65,536 there are 4,096 tile-halves and ~2,000 decided points per half.  A
+// counting sort groups the points by their half (k_code_hist, scan, k_code_scatter; the
+// order inside a group is immaterial), then k_fixrow_b keeps each lane's centroid row in
+// VGPRs across a run of points of one half: centroid rows are read once per run instead of
+// 3 KiB per point from L2.
+constexpr int FB_MAX_CODES = 8192;  // LDS histogram limit (2 x 4,096 tiles = K <= 131,072)
+constexpr int FB_TILE = 4096;        // points per k_code_scatter round (16 per thread)
+constexpr int FB_RUN = 32;           // consecutive grouped points per 16-lane group
+
+__global__ __launch_bounds__(256) void k_code_hist(const uint32_t *__restrict__ labels, uint32_t n, uint32_t ncodes,
+                                                   uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[FB_MAX_CODES];
+    for (uint32_t i = threadIdx.x; i < ncodes; i += 256) h[i] = 0;
+    __syncthreads();
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+        const uint32_t code = labels[p];
+        if (code < ncodes) atomicAdd(&h[code], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ncodes; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// cursor = exclusive scan of the histogram; each round ranks its points per code in LDS,
+// reserves one range per code with a global atomic, and writes the point indices
+__global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict__ labels, uint32_t n, uint32_t ncodes,
+                                                      uint32_t *__restrict__ cursor, uint32_t *__restrict__ grouped) {
+    __shared__ uint32_t h[FB_MAX_CODES];
+    constexpr int PER = FB_TILE / 256;
+    for (uint32_t base = blockIdx.x * FB_TILE; base < n; base += gridDim.x * FB_TILE) {
+        for (uint32_t i = threadIdx.x; i < ncodes; i += 256) h[i] = 0;
+        __syncthreads();
+        uint32_t code[PER], rank[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t p = base + j * 256 + threadIdx.x;
+            code[j] = p < n ? labels[p] : 0xffffffffu;
+            rank[j] = code[j] < ncodes ? atomicAdd(&h[code[j]], 1u) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < ncodes; i += 256)
+            if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (code[j] < ncodes) grouped[h[code[j]] + rank[j]] = base + j * 256 + threadIdx.x;
+        __syncthreads();
+    }
+}
+
+// lane q of a 16-lane DPP row reads x from lane Q of its row (row_newbcast); folded into
+// the consuming VALU op (v_sub_f32_dpp)
+template <int Q>
+__device__ inline float row_bcast(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x150 + Q, 0xf, 0xf, true));
+}
+
+// 16 lanes (one DPP row) per point over runs of FB_RUN grouped points; lane rr holds row rr
+// of the current tile-half in VGPRs (LD floats, zero padded) and reloads it when the half
+// changes.  The run's point indices and codes are loaded up front (lane rr holds points rr
+// and 16 + rr) and handed out by shuffles.  A point row is loaded once per group -- lane q
+// holds its float4 q -- and broadcast inside the row by DPP, so the vector-memory path
+// moves 192 B per point instead of 16 x 192 B; the next point's row is in flight while
+// this one is scored.  (c - p)^2 is taken as (p - c)^2: the same rounded square.
+template <int LD>
+__global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos, int d, const float *__restrict__ caos,
+                                                  int k, const uint32_t *__restrict__ grouped,
+                                                  const uint32_t *__restrict__ ndecided,
+                                                  uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                  State *st) {
+    static_assert(FB_RUN == 32, "two run slots per lane");
+    static_assert(LD / 4 <= 16, "one float4 of the point row per lane");
+    const uint32_t nd = *ndecided;
+    const uint32_t grp = (blockIdx.x * 256 + threadIdx.x) >> 4;
+    const uint32_t j0 = grp * FB_RUN;
+    if (j0 >= nd) return;  // uniform per 16-lane group
+    const int cnt = (int)min(nd - j0, (uint32_t)FB_RUN);
+    const int rr = threadIdx.x & 15;
+    const int gl = (threadIdx.x & 63) & ~15;  // first lane of this group in the wave
+    const uint32_t pa = rr < cnt ? grouped[j0 + rr] : 0u;
+    const uint32_t pb = 16 + rr < cnt ? grouped[j0 + 16 + rr] : 0u;
+    const uint32_t ca = rr < cnt ? labels[pa] : 0u;
+    const uint32_t cb = 16 + rr < cnt ? labels[pb] : 0u;
+    auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
+    auto code_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? ca : cb, gl + (i & 15), 64); };
+    auto slice = [&](uint32_t pt) {
+        return rr < LD / 4 ? reinterpret_cast<const float4 *>(aos + (uint64_t)pt * LD)[rr]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 row[LD / 4];
+    uint32_t have = 0xffffffffu, c = 0;
+    bool valid = false;
+    uint32_t p = point_of(0);
+    float4 cur = slice(p);
+    for (int i = 0; i < cnt; ++i) {
+        const uint32_t code = code_of(i);
+        const uint32_t pn = point_of(i + 1 < cnt ? i + 1 : i);
+        if (code != have) {  // uniform per group
+            have = code;
+            c = code_row(code, rr);
+            valid = c < (uint32_t)k;
+            const float4 *src = reinterpret_cast<const float4 *>(caos + (uint64_t)(valid ? c : 0) * LD);
+#pragma unroll
+            for (int q = 0; q < LD / 4; ++q) row[q] = src[q];
+        }
+        const float4 nxt = slice(pn);
+        float s0 = 0.f, s1 = 0.f;  // two chains: the screen bound holds for any summation order
+        static_for<LD / 4>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            float v = row_bcast<q>(cur.x) - row[q].x;
+            s0 = __builtin_fmaf(v, v, s0);
+            v = row_bcast<q>(cur.y) - row[q].y;
+            s1 = __builtin_fmaf(v, v, s1);
+            v = row_bcast<q>(cur.z) - row[q].z;
+            s0 = __builtin_fmaf(v, v, s0);
+            v = row_bcast<q>(cur.w) - row[q].w;
+            s1 = __builtin_fmaf(v, v, s1);
+        });
+        fix_decide<16>(s0 + s1, valid, c, d, caos, aos + (uint64_t)p * LD, p, rr, labels, ties, st);
+        cur = nxt;
+        p = pn;
+    }
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
@@ -660,14 +823,14 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
-    for (; j + 4 <= s1; j += 4) {
-        const uint32_t m0 = members[j], m1 = members[j + 1], m2 = members[j + 2], m3 = members[j + 3];
-        const float v0 = aos[(uint64_t)m0 * ld + lane], v1 = aos[(uint64_t)m1 * ld + lane];
-        const float v2 = aos[(uint64_t)m2 * ld + lane], v3 = aos[(uint64_t)m3 * ld + lane];
-        sum += (double)v0;
-        sum += (double)v1;
-        sum += (double)v2;
-        sum += (double)v3;
+    // 16 member rows in flight per wave (the adds stay in ascending point order)
+    constexpr int U = 16;
+    for (; j + U <= s1; j += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum += (double)v[u];
     }
     for (; j < s1; ++j) sum += (double)aos[(uint64_t)members[j] * ld + lane];
     cen[(uint64_t)lane * k + cl] = (float)(sum / (double)(s1 - s0));
@@ -744,7 +907,7 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     const float amax = __builtin_bit_cast(float, amax_bits);
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
-    hipLaunchKernelGGL(k_point_frags, dim3(grid_for((uint64_t)ntiles * 32 * ks * 2, 256, 16384)), dim3(256), 0,
+    hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(256), 0,
                        c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, aos);
     ST_LAUNCH_CHECK();
     c->kn_sigma = sigma;
@@ -784,7 +947,35 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     ST_HIP(hipMemsetAsync(&dstate->amb, 0, 16, c->stream));  // amb + ties + overflow + pairs
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
                                         thr, amb, dstate, pair_pts, pair_codes)));
-    {
+    const uint32_t ncodes = ctiles * 2;
+    const int ld = aos_ld(d);
+    if (ncodes <= (uint32_t)FB_MAX_CODES && (ld == 48 || ld == 24 || ld == 12) && !getenv("ST_FIXROW_L2")) {
+        // group the decided points by tile-half, then settle them with register-resident rows
+        KTimer kt(c, "kn.fixrow");
+        auto *hist = wsT<uint32_t>(c, "kn.fbhist", ncodes);
+        auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
+        auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
+        auto *grouped = wsT<uint32_t>(c, "kn.fbpts", n);
+        ST_HIP(hipMemsetAsync(hist, 0, ncodes * sizeof(uint32_t), c->stream));
+        hipLaunchKernelGGL(k_code_hist, dim3(grid_for(n, 256 * 64, 512)), dim3(256), 0, c->stream, labels,
+                           (uint32_t)n, ncodes, hist);
+        ST_LAUNCH_CHECK();
+        scan_u32(c, hist, cursor, ncodes, ndec);
+        hipLaunchKernelGGL(k_code_scatter, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream, labels,
+                           (uint32_t)n, ncodes, cursor, grouped);
+        ST_LAUNCH_CHECK();
+        const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
+        if (ld == 48)
+            hipLaunchKernelGGL(k_fixrow_b<48>, g, dim3(256), 0, c->stream, aos, d, caos, k, grouped, ndec, labels,
+                               ties, dstate);
+        else if (ld == 24)
+            hipLaunchKernelGGL(k_fixrow_b<24>, g, dim3(256), 0, c->stream, aos, d, caos, k, grouped, ndec, labels,
+                               ties, dstate);
+        else
+            hipLaunchKernelGGL(k_fixrow_b<12>, g, dim3(256), 0, c->stream, aos, d, caos, k, grouped, ndec, labels,
+                               ties, dstate);
+        ST_LAUNCH_CHECK();
+    } else {
         KTimer kt(c, "kn.fixrow");
         hipLaunchKernelGGL(k_fixrow, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, c->stream, aos, d, cfix,
                            caos, k, (uint32_t)n, labels, ties, dstate);

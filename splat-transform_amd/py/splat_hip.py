@@ -8,6 +8,7 @@ fallback: constructing a Context without a gfx950 device raises.
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 
@@ -239,6 +240,11 @@ def device_count():
 
 class Context:
     def __init__(self, device=0):
+        # PyTorch-ROCm ships its own HIP runtime next to the one this library links; when both
+        # live in one process, torch's must initialise first (the other order leaves torch
+        # without a device).  Device tensors are still shared through plain pointers.
+        if 'torch' in sys.modules:
+            sys.modules['torch'].cuda.init()
         self.h = ctypes.c_void_p()
         check(lib().st_ctx_create(ctypes.c_int32(device), ctypes.byref(self.h)))
 

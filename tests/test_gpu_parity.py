@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope='module')
 def ctx():
+    import torch  # noqa: F401  (initialised before the library's runtime: see splat_hip.Context)
     return sh.Context(0)
 
 
@@ -157,3 +158,44 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac):
     assert rc == 0 and used == oused
     assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
     assert np.array_equal(labels, olabels)
+
+
+@pytest.mark.parametrize('n,k,dup', [(40_000, 65536, 0.0), (30_000, 65536, 0.3), (20_000, 131072, 0.0)])
+def test_nd_assign_full_palette_argmin(ctx, n, k, dup):
+    """One assign pass at the SOG palette size (K = 65,536 / 131,072, D = 45) against a
+    brute-force f64 distance computed on the device in the reference's own order
+    (kd-tree.ts:26-35: l += (c - p)^2 sequentially over the dimensions, each op rounded
+    like a JS number): every label must reach the exact minimum.  dup > 0 makes a share of
+    the points copies of centroids (distance 0 and near-ties between neighbouring rows)."""
+    import torch
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(n + k)
+    d = 45
+    cen = (torch.randn(d, k, generator=g, device=dev) * 0.05).contiguous()
+    pts = torch.randn(d, n, generator=g, device=dev) * 0.1
+    if dup:
+        m = int(n * dup)
+        pick = torch.randint(0, k, (m,), generator=g, device=dev)
+        pts[:, :m] = cen[:, pick] + torch.randn(d, m, generator=g, device=dev) * 1e-4
+    cols = [pts[j].contiguous() for j in range(d)]
+    labels = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.dev_kmeans_prepare(cols)
+    ctx.dev_kmeans_assign(cols, k, cen, labels)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    lab = labels.long()
+    cd = cen.double()
+    bad = 0
+    for s in range(0, n, 512):
+        e = min(n, s + 512)
+        pd = torch.stack([c[s:e] for c in cols]).double()
+        dist = torch.zeros(e - s, k, dtype=torch.float64, device=dev)
+        for j in range(d):
+            v = cd[j][None, :] - pd[j][:, None]
+            dist += v * v
+        mn = dist.min(1).values
+        got = dist.gather(1, lab[s:e, None]).squeeze(1)
+        bad += int((got != mn).sum().item())
+    assert bad == 0, f'{bad} labels miss the exact f64 minimum'
