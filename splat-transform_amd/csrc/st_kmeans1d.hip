@@ -53,6 +53,51 @@ __device__ inline void seg_node(Seg s, uint32_t &node, Seg &left, Seg &right) {
     }
 }
 
+// KdTree.findNearest over the implicit tree (the reference's visit order and strict `<`)
+template <typename V, typename I>
+__device__ inline uint32_t kd1_walk(double p, int k, V val, I idx) {
+    double mind = __builtin_inf();
+    uint32_t mini = 0xffffffffu;
+    Seg stack[24];
+    int sp = 0;
+    Seg cur{0, (uint32_t)k};
+    bool descend = true;
+    while (true) {
+        if (descend) {
+            // go down the `next` chain, remembering each frame
+            while (cur.hi > cur.lo) {
+                stack[sp++] = cur;
+                uint32_t node;
+                Seg l, r;
+                seg_node(cur, node, l, r);
+                const double distance = p - (double)val(node);
+                cur = (distance > 0) ? r : l;
+            }
+        }
+        if (sp == 0) break;
+        const Seg f = stack[--sp];
+        uint32_t node;
+        Seg l, r;
+        seg_node(f, node, l, r);
+        const double cv = val(node);
+        const double distance = p - cv;
+        const double v = cv - p;
+        const double thisd = 0.0 + v * v;
+        if (thisd < mind) {
+            mind = thisd;
+            mini = idx(node);
+        }
+        const Seg other = (distance > 0) ? l : r;
+        if (distance * distance < mind && other.hi > other.lo) {
+            cur = other;
+            descend = true;
+        } else {
+            descend = false;
+        }
+    }
+    return mini;
+}
+
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_kd1_assign(const float *__restrict__ pts, uint64_t n,
                                                     const float *__restrict__ cen, const uint32_t *__restrict__ order,
@@ -70,48 +115,75 @@ __global__ __launch_bounds__(256) void k_kd1_assign(const float *__restrict__ pt
     auto val = [&](uint32_t pos) -> float { return LDS ? sv[pos] : cen[order[pos]]; };
     auto idx = [&](uint32_t pos) -> uint32_t { return LDS ? si[pos] : order[pos]; };
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const double p = pts[i];
-        double mind = __builtin_inf();
-        uint32_t mini = 0xffffffffu;
-        Seg stack[24];
-        int sp = 0;
-        Seg cur{0, (uint32_t)k};
-        bool descend = true;
-        while (true) {
-            if (descend) {
-                // go down the `next` chain, remembering each frame
-                while (cur.hi > cur.lo) {
-                    stack[sp++] = cur;
-                    uint32_t node;
-                    Seg l, r;
-                    seg_node(cur, node, l, r);
-                    const double distance = p - (double)val(node);
-                    cur = (distance > 0) ? r : l;
-                }
-            }
-            if (sp == 0) break;
-            const Seg f = stack[--sp];
-            uint32_t node;
-            Seg l, r;
-            seg_node(f, node, l, r);
-            const double cv = val(node);
-            const double distance = p - cv;
-            const double v = cv - p;
-            const double thisd = 0.0 + v * v;
-            if (thisd < mind) {
-                mind = thisd;
-                mini = idx(node);
-            }
-            const Seg other = (distance > 0) ? l : r;
-            if (distance * distance < mind && other.hi > other.lo) {
-                cur = other;
-                descend = true;
-            } else {
-                descend = false;
-            }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        labels[i] = kd1_walk((double)pts[i], k, val, idx);
+}
+
+// The same answer without the walk.  With one dimension every centroid is a value on a
+// line, and the rounded distance (c - p)^2 is monotone in |c - p| on each side of p, so
+// the minimum is reached at the last centroid <= p (L) or the first > p (R).  If it is
+// reached there only -- the rounded distances of L, R and of their outer neighbours differ
+// from it -- it is the unique minimum, which the KdTree walk finds in any visit order.
+// Otherwise (duplicate centroid values, equal rounded distances) the point takes the walk.
+// R is located through a uniform grid of KD1_CELLS cells over [c_min, c_max]: a monotone
+// cell map puts every centroid of a smaller cell below p and of a larger one above it.
+constexpr int KD1_CELLS = 1024;
+__global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict__ pts, uint64_t n,
+                                                         const float *__restrict__ cen,
+                                                         const uint32_t *__restrict__ order, int k,
+                                                         uint32_t *__restrict__ labels) {
+    __shared__ float sv[KD1_LDS];
+    __shared__ uint32_t si[KD1_LDS];
+    __shared__ uint16_t cc[KD1_LDS];
+    __shared__ uint32_t first[KD1_CELLS + 1];
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+        const uint32_t o = order[i];
+        si[i] = o;
+        sv[i] = cen[o];
+    }
+    __syncthreads();
+    const float lo = sv[0], hi = sv[k - 1];
+    const float span = hi - lo;
+    const float inv = (span > 0.f && span < __builtin_inff()) ? (float)KD1_CELLS / span : 0.f;
+    auto cell = [&](float x) -> int {
+        const float t = (x - lo) * inv;
+        return (int)__builtin_fminf(__builtin_fmaxf(t, 0.f), (float)(KD1_CELLS - 1));
+    };
+    for (int i = threadIdx.x; i < k; i += blockDim.x) cc[i] = (uint16_t)cell(sv[i]);
+    __syncthreads();
+    for (int g = threadIdx.x; g <= KD1_CELLS; g += blockDim.x) {  // first[g] = #{i : cc[i] < g}
+        int a = 0, b = k;
+        while (a < b) {
+            const int m = (a + b) >> 1;
+            if ((int)cc[m] < g) a = m + 1;
+            else b = m;
         }
-        labels[i] = mini;
+        first[g] = (uint32_t)a;
+    }
+    __syncthreads();
+    auto dist = [&](int pos, double p) {
+        const double v = (double)sv[pos] - p;
+        return 0.0 + v * v;
+    };
+    auto val = [&](uint32_t pos) -> float { return sv[pos]; };
+    auto idx = [&](uint32_t pos) -> uint32_t { return si[pos]; };
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float pf = pts[i];
+        const double p = pf;
+        const int g = cell(pf);
+        int u = (int)first[g];
+        const int ue = (int)first[g + 1];
+        while (u < ue && sv[u] <= pf) ++u;  // R = u: the first centroid > p
+        const int L = u - 1, R = u;
+        const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
+        const double dr = R < k ? dist(R, p) : __builtin_inf();
+        const double m = __builtin_fmin(dl, dr);
+        const bool tie = dl == dr || (L >= 1 && dist(L - 1, p) == m) || (R + 1 < k && dist(R + 1, p) == m);
+        uint32_t lab;
+        if (!tie) lab = si[dl < dr ? L : R];
+        else lab = kd1_walk(p, k, val, idx);
+        labels[i] = lab;
     }
 }
 
@@ -253,7 +325,9 @@ void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, 
     radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
     const unsigned g = grid_for(n, 256, 256 * 16);
     KTimer kt(c, "k1.assign");
-    if (k <= KD1_LDS)
+    if (k <= KD1_LDS && !getenv("ST_KD1_WALK"))
+        hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+    else if (k <= KD1_LDS)
         hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
     else
         hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);

@@ -199,3 +199,20 @@ def test_nd_assign_full_palette_argmin(ctx, n, k, dup):
         got = dist.gather(1, lab[s:e, None]).squeeze(1)
         bad += int((got != mn).sum().item())
     assert bad == 0, f'{bad} labels miss the exact f64 minimum'
+
+
+@pytest.mark.parametrize('levels', [7, 50, 300])
+def test_cluster1d_ties_and_duplicates_vs_oracle(ctx, levels):
+    """1-D k-means on integer-valued columns: many points lie exactly midway between two
+    centroids (equal rounded distances), empty clusters are re-seeded onto existing values
+    (duplicate centroids), so the assign must fall back to the KdTree walk's tie-break."""
+    rng = np.random.default_rng(levels)
+    n = 40_000
+    cols = [rng.integers(-levels, levels, n).astype(np.float32) for _ in range(3)]
+    cols[1] *= np.float32(0.5)
+    draws = oracle.mulberry32(levels, 1 << 15)
+    cent, labels, used = ctx.cluster1d(cols, 5, draws)
+    rc, ocent, olabels, oused = oracle.cluster1d(cols, 5, draws)
+    assert rc == 0 and used == oused
+    assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
+    assert np.array_equal(labels, olabels)
