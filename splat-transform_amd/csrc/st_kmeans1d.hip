@@ -313,6 +313,286 @@ __global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ v
     cen[cl] = (float)(s / (double)(s1 - s0));
 }
 
+// ---- chunked update: every cluster's members split into SC_CH-member chunks ----------
+// One workgroup per chunk instead of one per cluster: the clusters of a 1-D codebook are
+// few (256) and uneven (the one straddling 0 can hold 1.5% of 30M points), so a
+// per-cluster workgroup leaves the chip idle behind the largest cluster.
+constexpr uint32_t SC_CH = 4096;  // members per chunk
+constexpr int SC_T = 256;         // threads per chunk (16 members each)
+constexpr int SC_PER = SC_CH / SC_T;
+
+struct Chunk {
+    uint32_t cl, begin, end, pad;
+};
+
+__global__ __launch_bounds__(256) void k_chunk_counts(const uint32_t *__restrict__ start, int k,
+                                                      uint32_t *__restrict__ cnt) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x)
+        cnt[cl] = (start[cl + 1] - start[cl] + SC_CH - 1) / SC_CH;
+}
+
+__global__ __launch_bounds__(256) void k_chunk_list(const uint32_t *__restrict__ start, int k,
+                                                    const uint32_t *__restrict__ first, Chunk *__restrict__ chunks) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
+        const uint32_t s0 = start[cl], s1 = start[cl + 1];
+        uint32_t o = first[cl];
+        for (uint32_t b = s0; b < s1; b += SC_CH) chunks[o++] = Chunk{(uint32_t)cl, b, min(s1, b + SC_CH), 0u};
+    }
+}
+
+// per-cluster accumulators of the certificate pass
+struct SumAcc {
+    double sum, sabs;
+    int emin;
+    int pad;
+};
+
+__global__ __launch_bounds__(256) void k_sumacc_init(SumAcc *acc, int k) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x)
+        acc[cl] = SumAcc{0.0, 0.0, 1 << 20, 0};
+}
+
+// chunk partials of sum, sum|x|, min ulp exponent.  Under the certificate every partial sum
+// is exact, so the block reduction and the atomic order are immaterial; otherwise the sum
+// is discarded (the replay below recomputes it).
+__global__ __launch_bounds__(SC_T) void k_sum1d_chunks(const uint32_t *__restrict__ vals,
+                                                      const Chunk *__restrict__ chunks,
+                                                      const uint32_t *__restrict__ nchunks, SumAcc *acc) {
+    if (blockIdx.x >= *nchunks) return;
+    const Chunk ch = chunks[blockIdx.x];
+    double sum = 0, sabs = 0;
+    int emin = 1 << 20;
+    for (uint32_t j = ch.begin + threadIdx.x; j < ch.end; j += SC_T) {
+        const float x = __builtin_bit_cast(float, vals[j]);
+        sum += (double)x;
+        sabs += (double)__builtin_fabsf(x);
+        if (x != 0.0f) emin = min(emin, ulp_exp(x));
+    }
+    __shared__ double rs[SC_T / 64], ra[SC_T / 64];
+    __shared__ int re[SC_T / 64];
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        sabs += __shfl_xor(sabs, o, 64);
+        emin = min(emin, __shfl_xor(emin, o, 64));
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+        rs[w] = sum;
+        ra[w] = sabs;
+        re[w] = emin;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    sum = rs[0];
+    sabs = ra[0];
+    emin = re[0];
+    for (int i = 1; i < SC_T / 64; ++i) {
+        sum += rs[i];
+        sabs += ra[i];
+        emin = min(emin, re[i]);
+    }
+    atomicAdd(&acc[ch.cl].sum, sum);
+    atomicAdd(&acc[ch.cl].sabs, sabs);
+    atomicMin(&acc[ch.cl].emin, emin);
+}
+
+__global__ __launch_bounds__(256) void k_sum1d_final(const SumAcc *__restrict__ acc, const uint32_t *__restrict__ start,
+                                                     int k, float *__restrict__ cen, uint32_t *__restrict__ seq_flag,
+                                                     int32_t *__restrict__ emin_c, double *__restrict__ sabs_c) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
+        const uint32_t cnt = start[cl + 1] - start[cl];
+        if (cnt == 0) {  // empty: re-seeded separately
+            seq_flag[cl] = 0;
+            continue;
+        }
+        const SumAcc a = acc[cl];
+        const bool exact = sum_is_exact(a.sabs, a.emin);
+        seq_flag[cl] = exact ? 0u : 1u;
+        emin_c[cl] = a.emin;
+        sabs_c[cl] = a.sabs;
+        if (exact) cen[cl] = (float)(a.sum / (double)cnt);
+    }
+}
+
+// ---- chunked replay of the flagged clusters (the algorithm of st_replay.h) -----------
+__device__ inline __int128 shfl_up_i128(__int128 v, int o) {
+    const uint64_t lo = __shfl_up((uint64_t)v, o, 64), hi = __shfl_up((uint64_t)(v >> 64), o, 64);
+    return (__int128)(((unsigned __int128)hi << 64) | lo);
+}
+// exclusive scan of one int128 per thread over an SC_T block
+__device__ inline __int128 sc_exscan_i128(__int128 v, __int128 *total) {
+    __shared__ __int128 ws[SC_T / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __int128 incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const __int128 u = shfl_up_i128(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    __int128 off = 0, tot = 0;
+    for (int i = 0; i < SC_T / 64; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+__device__ inline uint32_t sc_exscan_u32(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t ws[SC_T / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < SC_T / 64; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+__device__ inline __int128 rp_margin(double sabs, int e_lo) {
+    int e_top;
+    __builtin_frexp(sabs, &e_top);
+    return ((__int128)1) << max(e_top - 33 - e_lo, 0);
+}
+
+// A: exact chunk sums in units of 2^e_lo
+__global__ __launch_bounds__(SC_T) void k_rp_sums(const uint32_t *__restrict__ vals, const Chunk *__restrict__ chunks,
+                                                 const uint32_t *__restrict__ nchunks,
+                                                 const uint32_t *__restrict__ seq_flag,
+                                                 const int32_t *__restrict__ emin_c, __int128 *__restrict__ csum) {
+    if (blockIdx.x >= *nchunks) return;
+    const Chunk ch = chunks[blockIdx.x];
+    if (seq_flag[ch.cl] != 1u) return;
+    const int e_lo = emin_c[ch.cl];
+    __int128 local = 0;
+    for (uint32_t j = ch.begin + threadIdx.x; j < ch.end; j += SC_T) local += f32_units(vals[j], e_lo);
+    __int128 tot;
+    sc_exscan_i128(local, &tot);
+    if (threadIdx.x == 0) csum[blockIdx.x] = tot;
+}
+
+// B / D: one thread per flagged cluster walks its chunks in order (exclusive prefixes)
+__global__ __launch_bounds__(256) void k_rp_prefix(const uint32_t *__restrict__ first, int k,
+                                                   uint32_t *__restrict__ seq_flag, const double *__restrict__ sabs_c,
+                                                   const int32_t *__restrict__ emin_c, __int128 *__restrict__ csum,
+                                                   __int128 *__restrict__ total) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
+        if (seq_flag[cl] != 1u) continue;
+        if (!(sabs_c[cl] * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin_c[cl] + 118))) {  // int128 range
+            seq_flag[cl] = 2u;
+            continue;
+        }
+        __int128 run = 0;
+        for (uint32_t c = first[cl]; c < first[cl + 1]; ++c) {
+            const __int128 v = csum[c];
+            csum[c] = run;  // in place: exclusive prefix of the chunk
+            run += v;
+        }
+        total[cl] = run;
+    }
+}
+__global__ __launch_bounds__(256) void k_rp_cprefix(const uint32_t *__restrict__ first, int k,
+                                                    uint32_t *__restrict__ seq_flag, const uint32_t *__restrict__ ccnt,
+                                                    uint32_t *__restrict__ cof, uint32_t *__restrict__ ctot) {
+    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
+        if (seq_flag[cl] != 1u) continue;
+        uint32_t run = 0;
+        for (uint32_t c = first[cl]; c < first[cl + 1]; ++c) {
+            cof[c] = run;
+            run += ccnt[c];
+        }
+        ctot[cl] = run;
+        if (run > (uint32_t)CAND_MAX) seq_flag[cl] = 2u;  // the sequential chain
+    }
+}
+
+// C (WRITE = false): candidates per chunk; E (WRITE = true): write them in member order
+template <bool WRITE>
+__global__ __launch_bounds__(SC_T) void k_rp_cands(const uint32_t *__restrict__ vals, const Chunk *__restrict__ chunks,
+                                                  const uint32_t *__restrict__ nchunks,
+                                                  const uint32_t *__restrict__ seq_flag,
+                                                  const int32_t *__restrict__ emin_c,
+                                                  const double *__restrict__ sabs_c,
+                                                  const __int128 *__restrict__ coff, uint32_t *__restrict__ ccnt,
+                                                  __int128 *__restrict__ cand_all) {
+    if (blockIdx.x >= *nchunks) return;
+    const Chunk ch = chunks[blockIdx.x];
+    if (seq_flag[ch.cl] != 1u) return;
+    const int e_lo = emin_c[ch.cl];
+    const __int128 margin = rp_margin(sabs_c[ch.cl], e_lo);
+    // this thread's contiguous slice of the chunk
+    const uint32_t a = min(ch.end, ch.begin + threadIdx.x * SC_PER), b = min(ch.end, a + SC_PER);
+    __int128 local = 0;
+    for (uint32_t j = a; j < b; ++j) local += f32_units(vals[j], e_lo);
+    __int128 tot;
+    const __int128 off = coff[blockIdx.x] + sc_exscan_i128(local, &tot);
+    uint32_t mine = 0;
+    __int128 P = off;
+    for (uint32_t j = a; j < b; ++j) {
+        const uint32_t xb = vals[j];
+        const __int128 Pn = P + f32_units(xb, e_lo);
+        mine += replay_candidate(P, Pn, xb, e_lo, margin) ? 1u : 0u;
+        P = Pn;
+    }
+    uint32_t ctot;
+    const uint32_t cof = sc_exscan_u32(mine, &ctot);
+    if (!WRITE) {
+        if (threadIdx.x == 0) ccnt[blockIdx.x] = ctot;
+        return;
+    }
+    uint32_t o = ccnt[blockIdx.x] + cof;
+    __int128 *cand = cand_all + (uint64_t)ch.cl * CAND_MAX;
+    P = off;
+    for (uint32_t j = a; j < b; ++j) {
+        const uint32_t xb = vals[j];
+        const __int128 Pn = P + f32_units(xb, e_lo);
+        if (replay_candidate(P, Pn, xb, e_lo, margin)) cand[o++] = Pn;
+        P = Pn;
+    }
+}
+
+// F: one lane per flagged cluster replays its candidates
+__global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ start, const uint32_t *__restrict__ ctot_c,
+                                                  int k, uint32_t *__restrict__ seq_flag,
+                                                  const int32_t *__restrict__ emin_c, const double *__restrict__ sabs_c,
+                                                  const __int128 *__restrict__ total, const __int128 *__restrict__ cand_all,
+                                                  float *__restrict__ cen) {
+    const int cl = blockIdx.x * 64 + threadIdx.x;
+    if (cl >= k || seq_flag[cl] != 1u) return;
+    const int e_lo = emin_c[cl];
+    const __int128 margin = rp_margin(sabs_c[cl], e_lo);
+    const uint32_t ctot = ctot_c[cl];
+    const __int128 *cand = cand_all + (uint64_t)cl * CAND_MAX;
+    __int128 sv = 0, Pprev = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < ctot; ++i) {
+        const __int128 Pc = cand[i];
+        const __int128 V = sv + (Pc - Pprev);
+        sv = f64_representable(V) ? V : f64_units(f64_round(V, e_lo), e_lo);
+        Pprev = Pc;
+        const __int128 dev = sv - Pc;
+        ok = ok && (dev < 0 ? -dev : dev) < margin;
+    }
+    const __int128 fin = sv + (total[cl] - Pprev);
+    if (!ok || !f64_representable(fin)) {
+        seq_flag[cl] = 2u;
+        return;
+    }
+    cen[cl] = (float)(f64_round(fin, e_lo) / (double)(start[cl + 1] - start[cl]));
+    seq_flag[cl] = 0u;
+}
+
 }  // namespace
 
 // one exact 1-D assign: KdTree build == stable sort of the centroid values
@@ -343,6 +623,18 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     auto *emin_c = wsT<int32_t>(c, "k1.emin", (size_t)k);
     auto *sabs_c = wsT<double>(c, "k1.sabs", (size_t)k);
     auto *cand_buf = wsT<__int128>(c, "k1.cands", (size_t)k * CAND_MAX);
+    // chunked update (ST_K1_BLOCK=1 selects the one-workgroup-per-cluster kernels)
+    const bool chunked = !getenv("ST_K1_BLOCK");
+    const uint64_t maxch = n / SC_CH + (uint64_t)k + 1;
+    auto *ch_cnt = wsT<uint32_t>(c, "k1.chcnt", (size_t)k);
+    auto *ch_first = wsT<uint32_t>(c, "k1.chfirst", (size_t)k + 1);
+    auto *chunks = wsT<Chunk>(c, "k1.chunks", maxch);
+    auto *acc = wsT<SumAcc>(c, "k1.acc", (size_t)k);
+    auto *rp_csum = wsT<__int128>(c, "k1.rpcsum", maxch);
+    auto *rp_ccnt = wsT<uint32_t>(c, "k1.rpccnt", maxch);
+    auto *rp_cof = wsT<uint32_t>(c, "k1.rpcof", maxch);
+    auto *rp_ctot = wsT<uint32_t>(c, "k1.rpctot", (size_t)k);
+    auto *rp_total = wsT<__int128>(c, "k1.rptotal", (size_t)k);
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
     for (int it = 0; it < iters; ++it) {
@@ -356,18 +648,48 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         bounds_from_sorted(c, keys, n, k, start);
         {
             KTimer kt(c, "k1.sum");
-            hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen, seq_flag, emin_c,
-                               sabs_c);
-            ST_LAUNCH_CHECK();
+            if (chunked) {
+                const unsigned gk = grid_for((uint64_t)k, 256, 1024);
+                hipLaunchKernelGGL(k_chunk_counts, dim3(gk), dim3(256), 0, c->stream, start, k, ch_cnt);
+                scan_u32(c, ch_cnt, ch_first, (uint64_t)k, ch_first + k);
+                hipLaunchKernelGGL(k_chunk_list, dim3(gk), dim3(256), 0, c->stream, start, k, ch_first, chunks);
+                hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, k);
+                hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k,
+                                   acc);
+                hipLaunchKernelGGL(k_sum1d_final, dim3(gk), dim3(256), 0, c->stream, acc, start, k, cen, seq_flag,
+                                   emin_c, sabs_c);
+                ST_LAUNCH_CHECK();
+            } else {
+                hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen, seq_flag, emin_c,
+                                   sabs_c);
+                ST_LAUNCH_CHECK();
+            }
             std::vector<uint32_t> f1;
             if (getenv("ST_DEBUG")) {
                 ST_HIP(hipStreamSynchronize(c->stream));
                 f1.resize(k);
                 ST_HIP(hipMemcpy(f1.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost));
             }
-            hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals, start, seq_flag, emin_c, sabs_c,
-                               cen, cand_buf);
-            ST_LAUNCH_CHECK();
+            if (chunked) {
+                const unsigned gk = grid_for((uint64_t)k, 256, 1024);
+                hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k,
+                                   seq_flag, emin_c, rp_csum);
+                hipLaunchKernelGGL(k_rp_prefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, sabs_c,
+                                   emin_c, rp_csum, rp_total);
+                hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks,
+                                   ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_ccnt, cand_buf);
+                hipLaunchKernelGGL(k_rp_cprefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, rp_ccnt,
+                                   rp_cof, rp_ctot);
+                hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks,
+                                   ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_cof, cand_buf);
+                hipLaunchKernelGGL(k_rp_finish, dim3((k + 63) / 64), dim3(64), 0, c->stream, start, rp_ctot, k,
+                                   seq_flag, emin_c, sabs_c, rp_total, cand_buf, cen);
+                ST_LAUNCH_CHECK();
+            } else {
+                hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals, start, seq_flag, emin_c,
+                                   sabs_c, cen, cand_buf);
+                ST_LAUNCH_CHECK();
+            }
             if (getenv("ST_DEBUG")) {
                 ST_HIP(hipStreamSynchronize(c->stream));
                 std::vector<uint32_t> f2(k);
