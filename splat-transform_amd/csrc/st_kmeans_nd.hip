@@ -340,6 +340,10 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
 
     // ctiles is a multiple of CT_STAGE (the tail is padded with never-winning rows)
     const uint32_t nstages = ctiles / CT_STAGE;
+    // MODE 1 splits the centroid stages over gridDim.y workgroups (few ambiguous points:
+    // each split sweeps part of the palette, the candidate lists are filled atomically)
+    const uint32_t sg_begin = MODE == 1 ? (uint32_t)((uint64_t)blockIdx.y * nstages / gridDim.y) : 0u;
+    const uint32_t sg_end = MODE == 1 ? (uint32_t)((uint64_t)(blockIdx.y + 1) * nstages / gridDim.y) : nstages;
     // centroid stages move global -> LDS by DMA (global_load_lds_dwordx4: no VGPR staging,
     // one wave-instruction fills 1 KiB at a wave-uniform base + 16 B per lane)
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(w) * 64;
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                                                  (__attribute__((address_space(3))) void *)&lds[buf][wbase + q * WG],
                                                  16, 0, 0);
     };
-    stage_in(0, 0);
+    stage_in(0, sg_begin);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // one score buffer per point tile: slot t of a centroid tile writes buf[t] while the
@@ -365,10 +369,10 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
 #pragma unroll
         for (int r = 0; r < 16; ++r) buf[t][r] = __builtin_inff();  // no-op slots before the first
     uint32_t tile_prev = 0;  // centroid tile of the previous ct iteration
-    for (uint32_t sg = 0; sg < nstages; ++sg) {
-        const int cur = sg & 1;
+    for (uint32_t sg = sg_begin; sg < sg_end; ++sg) {
+        const int cur = (sg - sg_begin) & 1;
         // the other buffer was last read in stage sg - 1, which ended with a barrier
-        if (sg + 1 < nstages) stage_in(cur ^ 1, sg + 1);
+        if (sg + 1 < sg_end) stage_in(cur ^ 1, sg + 1);
         // A fragments ping-pong between two register sets: tile ct + 1 is read from LDS while
         // tile ct's MFMAs run (the read at the stage's last tile re-reads it, unused)
         f16x8 a0[KS], a1[KS];
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             tile_step(ct, a0, a1);
             tile_step(ct + 1, a1, a0);
         }
-        if (sg + 1 < nstages) {
+        if (sg + 1 < sg_end) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
@@ -852,7 +856,10 @@ struct Sweep {
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
                         uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
         const uint32_t per_block = NW * PT;
-        const dim3 grid((atiles + per_block - 1) / per_block);
+        const uint32_t blocks = (atiles + per_block - 1) / per_block;
+        // enough workgroups to cover the chip twice over
+        const uint32_t split = std::max(1u, std::min(ctiles / CT_STAGE, (2048u + blocks - 1) / blocks));
+        const dim3 grid(blocks, split);
         KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const uint32_t *)nullptr, bnd, (uint32_t *)nullptr, thr_slot,
