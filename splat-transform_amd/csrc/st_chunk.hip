@@ -130,8 +130,31 @@ __global__ __launch_bounds__(256) void k_rows_aos(const TransposeArgs a) {
     for (uint64_t e = t; e < nrows * a.rl / 4; e += 256) dst[e] = s4[e];
 }
 
+// SH bytes (write-compressed-ply.ts:83-87) in the input's row order: a value depends on its
+// own splat only, so it is computed while the columns stream in (coalesced), then gathered
+// with the row as SHB contiguous bytes (3C bytes, padded to 16-byte rows)
+constexpr int SHB = 48;  // byte row stride of the SH rows (3C <= 45)
+__device__ inline uint8_t sh_byte(float v) {
+    const double nv = (double)v / 8 + 0.5;
+    return js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+}
+__global__ __launch_bounds__(256) void k_sh_rows(const TransposeArgs a, int nsh, uint8_t *__restrict__ shrows) {
+    __shared__ uint32_t stage[256 * SHB / 4];
+    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t t = threadIdx.x;
+    uint8_t *st8 = reinterpret_cast<uint8_t *>(stage);
+    const bool real = r0 + t < a.n;
+    for (int k = 0; k < SHB; ++k) st8[t * SHB + k] = (k < nsh && real) ? sh_byte(a.src[14 + k][r0 + t]) : 0u;
+    __syncthreads();
+    const uint64_t nrows = (a.n - r0 < 256) ? (a.n - r0) : 256;
+    uint4 *dst = reinterpret_cast<uint4 *>(shrows + r0 * SHB);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
+    for (uint64_t e = t; e < nrows * SHB / 16; e += 256) dst[e] = s4[e];
+}
+
 struct ChunkArgs {
-    const float *rows;  // AoS rows: x y z scale_0..2 f_dc_0..2 opacity rot_0..3, then the SH
+    const float *rows;  // AoS rows of RL = 16 floats: x y z scale_0..2 f_dc_0..2 opacity rot_0..3
+    const uint8_t *shrows;  // SH bytes, SHB per row (k_sh_rows)
     int rl, nsh;
     uint64_t n;
     const uint32_t *order;
@@ -163,10 +186,17 @@ __global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
     if (a.nsh) {
         uint8_t *stage = reinterpret_cast<uint8_t *>(sh_stage);
         if (real) {
-            for (int k = 0; k < a.nsh; ++k) {
-                const double nv = (double)a.rows[(uint64_t)row * a.rl + 14 + k] / 8 + 0.5;
-                stage[j * a.nsh + k] = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.shrows + (uint64_t)row * SHB);
+            uint32_t w[SHB / 4];
+#pragma unroll
+            for (int q = 0; q < SHB / 16; ++q) {
+                const uint4 v = src[q];
+                w[4 * q] = v.x;
+                w[4 * q + 1] = v.y;
+                w[4 * q + 2] = v.z;
+                w[4 * q + 3] = v.w;
             }
+            for (int k = 0; k < a.nsh; ++k) stage[j * a.nsh + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
         }
         __syncthreads();
         uint8_t *o = a.sh_out + base * (uint64_t)a.nsh;
@@ -227,12 +257,14 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
         snprintf(nm, sizeof nm, "f_rest_%d", i);
         ta.src[14 + i] = col_or_null(t, nm);
     }
-    ta.ncol = 14 + nsh;
-    ta.rl = (ta.ncol + 3) & ~3;
+    ta.ncol = 14;
+    ta.rl = 16;
     ta.n = n;
     ta.rows = wsT<float>(c, "chunk.rows", n * (uint64_t)ta.rl);
+    uint8_t *shrows = nsh ? wsT<uint8_t>(c, "chunk.shrows", n * (uint64_t)SHB) : nullptr;
     ChunkArgs a{};
     a.rows = ta.rows;
+    a.shrows = shrows;
     a.rl = ta.rl;
     a.nsh = nsh;
     a.n = n;
@@ -243,6 +275,7 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     const uint64_t nchunks = (n + 255) / 256;
     KTimer kt(c, "chunk.pack");
     hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, c->stream, ta);
+    if (nsh) hipLaunchKernelGGL(k_sh_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, ta, nsh, shrows);
     hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();
 }
