@@ -16,8 +16,8 @@ end-to-end rate.
 N > 1 is launched by torch.distributed.run: one process per GPU, each rank holds
 a shard of S splats of one N*S-splat table (weak scaling) and the job writes the
 SOG of the whole table: k-means exchanges the centroid sums over RCCL every
-iteration (exact, splat_dist.py), Morton all-gathers x/y/z, textures reduce to
-rank 0.
+iteration (exact, splat_dist.py), Morton all-gathers x/y/z, rank 0 gathers the
+texels.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
 (the MFMA assign sweep, measured with HIP events on its own stream) and the
@@ -126,10 +126,10 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
+    torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
     if world > 1:
         dist.init_process_group(args.backend, init_method='env://')
-    local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
-    torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
     # one real stream for the library and the torch glue (st_ctx_set_stream(NULL) would select the
@@ -153,7 +153,7 @@ def main():
             return ctx.dev_sog(cols, args.iters, draws, tex)
     else:
         # rows sharded in rank order; kmeans/cluster1d exchange centroid sums over RCCL, Morton
-        # all-gathers x/y/z, textures reduce to rank 0 (splat_dist.py)
+        # all-gathers x/y/z, rank 0 gathers every rank's texels (splat_dist.py)
         import splat_dist
         ops = splat_dist.HipOps(ctx, dev)
         comm = splat_dist.Comm()

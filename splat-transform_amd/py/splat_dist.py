@@ -16,8 +16,9 @@ the single-device results on that global table, bit for bit:
   (init rows, empty-cluster re-seeds in ascending cluster order); the owner of a
   drawn row supplies its values.
 * Morton order (ordering.ts:4-110) is a global sort: x/y/z are all-gathered and
-  every rank orders the whole table (one exchange of 12 B/splat), then writes the
-  texels of its own rows at their global positions; textures are summed to rank 0.
+  every rank orders the whole table (one exchange of 12 B/splat).  Each rank writes
+  the texels of its own rows in row order; rank 0 gathers them (4 B per splat and
+  texture) and places them at their global Morton positions.
 
 `HipOps` is the product backend (the C-ABI step API on device tensors).  Any object
 with the same methods can stand in (tests/dist_oracle_ops.py checks the exchange
@@ -65,6 +66,13 @@ class Comm:
         if x is not t:
             t.copy_(x)
         return t
+
+    def gather(self, t, dst=0):
+        """list of every rank's tensor (equal shapes) on rank dst, None elsewhere"""
+        x = self._io(t)
+        out = [torch.empty_like(x) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(x, out, dst=dst, group=self.group)
+        return None if out is None else [o.to(t.device) for o in out]
 
     def allgather(self, t):
         """list of every rank's tensor (shapes may differ in dim 0)"""
@@ -326,8 +334,9 @@ def write_sog(ops, comm, cols, iters, draws):
     del xyz
     pos_all = torch.empty(N, dtype=torch.int32, device=dev)
     pos_all[idx.long()] = torch.arange(N, dtype=torch.int32, device=dev)
-    pos = pos_all[shard.off:shard.off + shard.n].contiguous()
-    del pos_all, idx
+    del idx
+    if comm.rank != 0:
+        pos_all = None  # rank 0 places every rank's texels
     lo, hi = ops.minmax([cols['x'], cols['y'], cols['z']])
     t = torch.tensor(list(lo) + [-v for v in hi], dtype=torch.float64)
     comm.allreduce(t, dist.ReduceOp.MIN)
@@ -341,9 +350,12 @@ def write_sog(ops, comm, cols, iters, draws):
     cursor += u
     meta['scales_codebook'] = scb.cpu().numpy()
     meta['sh0_codebook'] = ccb.cpu().numpy()
-    tex = {k: torch.zeros(W * H * 4, dtype=torch.uint8, device=dev)
-           for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0')}
+    # texels of this rank's rows in local row order (4 B per row and texture); rank 0
+    # gathers them and places them at their global Morton positions
+    keys = ('means_l', 'means_u', 'quats', 'scales', 'sh0') + (('shN_labels',) if C else ())
+    loc = {k: torch.zeros(shard.n * 4, dtype=torch.uint8, device=dev) for k in keys}
     shn_lab = None
+    shn_cent = None
     if C:
         D = 3 * C
         cen, shn_lab, u = kmeans(ops, comm, shard, [cols[f'f_rest_{i}'] for i in range(D)], pal, iters,
@@ -352,18 +364,41 @@ def write_sog(ops, comm, cols, iters, draws):
         ncb, ncl, u = ops.cluster1d_local([cen[i].contiguous() for i in range(D)], iters, draws[cursor:])
         cursor += u
         meta['shn_codebook'] = ncb.cpu().numpy()
-        tex['shN_labels'] = torch.zeros(W * H * 4, dtype=torch.uint8, device=dev)
-        tex['shN_centroids'] = torch.zeros(cw * ch * 4, dtype=torch.uint8, device=dev)
         if comm.rank == 0:
-            ops.shn_centroids(ncl, C, pal, tex['shN_centroids'])
-    m = ops.scatter(cols, pos, lo, hi, slab, clab, shn_lab, tex)
-    for key in tex:
-        comm.reduce_sum(tex[key], 0)
+            shn_cent = torch.zeros(cw * ch * 4, dtype=torch.uint8, device=dev)
+            ops.shn_centroids(ncl, C, pal, shn_cent)
+    rows = torch.arange(shard.n, dtype=torch.int32, device=dev)
+    m = ops.scatter(cols, rows, lo, hi, slab, clab, shn_lab, loc)
+    tex = gather_texels(comm, shard, loc, pos_all, W * H)
     if comm.rank != 0:
         return None, None, cursor
+    if shn_cent is not None:
+        tex['shN_centroids'] = shn_cent
     meta.update(width=W, height=H, count=N, means_min=list(m.means_min), means_max=list(m.means_max),
                 sh_bands={0: 0, 3: 1, 8: 2, 15: 3}[C], palette_size=pal, shn_width=cw, shn_height=ch)
     return tex, meta, cursor
+
+
+def gather_texels(comm, shard, loc, pos_all, size):
+    """The textures of the global table on rank 0 (None elsewhere): every rank holds the RGBA
+    texels of its own rows in local row order (`loc`, 4 B per row); rank 0 gathers them (one
+    point-to-point transfer per rank, N x 4 B per texture in total, instead of a sum-reduce of
+    whole textures) and places global row r at pos_all[r], its position in the Morton order.
+    Texels past the table stay zero, as in the single-device writer."""
+    m = max(shard.counts)
+    out = {}
+    for key, t in loc.items():
+        v = t.view(torch.int32)
+        pad = torch.zeros(m, dtype=torch.int32, device=v.device)
+        pad[:v.numel()] = v
+        parts = comm.gather(pad, 0)
+        if parts is None:
+            continue
+        full = torch.cat([p[:c] for p, c in zip(parts, shard.counts)])
+        tex = torch.zeros(size, dtype=torch.int32, device=v.device)
+        tex[pos_all.long()] = full
+        out[key] = tex.view(torch.uint8)
+    return out if comm.rank == 0 else None
 
 
 def _sh_coeffs(cols):

@@ -85,3 +85,49 @@ def test_distributed_kmeans_matches_single_process():
     assert rc == 0 and res['used1'] == used1
     assert np.array_equal(res['cb'].view(np.uint32), cb.view(np.uint32))
     assert np.array_equal(res['lab8'], lab8)
+
+
+def _texel_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import splat_dist
+    counts = [5, 9, 0][:world]  # uneven shards, one empty
+    N, size = sum(counts), 20
+    g = torch.Generator().manual_seed(3)
+    pos_all = torch.randperm(N, generator=g).to(torch.int32)  # a global Morton order
+    rows = torch.arange(N, dtype=torch.int32)
+    comm = splat_dist.Comm()
+    shard = splat_dist.Shard(comm, counts[rank])
+    off = sum(counts[:rank])
+    # texel of global row r: its index + 1 (non-zero), 4 bytes
+    loc = {'a': (rows[off:off + counts[rank]] + 1).view(torch.uint8).clone(),
+           'b': (rows[off:off + counts[rank]] * 7 + 3).view(torch.uint8).clone()}
+    tex = splat_dist.gather_texels(comm, shard, loc, pos_all if rank == 0 else None, size)
+    if rank == 0:
+        out.put({k: v.view(torch.int32).numpy().copy() for k, v in tex.items()})
+    else:
+        assert tex is None
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gather_texels_places_rows_at_morton_positions(world):
+    """rank 0 assembles each texture from the ranks' row-ordered texels: global row r lands
+    at pos_all[r], the rest of the W*H texture stays zero (splat_dist.gather_texels)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_texel_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    counts = [5, 9, 0][:world]
+    N = sum(counts)
+    pos_all = torch.randperm(N, generator=torch.Generator().manual_seed(3)).numpy()
+    for key, f in (('a', lambda r: r + 1), ('b', lambda r: r * 7 + 3)):
+        want = np.zeros(20, np.int32)
+        want[pos_all] = f(np.arange(N))
+        assert np.array_equal(res[key], want)
