@@ -35,7 +35,7 @@ def lib():
         L.st_o_log.argtypes = [c_d]
         for f in ('st_o_quat_from_euler', 'st_o_mat4_trs', 'st_o_mat3_from_quat', 'st_o_rotate_sh',
                   'st_o_transform', 'st_o_filter_finite', 'st_o_morton_order', 'st_o_pack_compressed',
-                  'st_o_kmeans', 'st_o_cluster1d', 'st_o_sog'):
+                  'st_o_kmeans', 'st_o_cluster1d', 'st_o_sog', 'st_o_kmeans_assign_mt'):
             getattr(L, f).restype = c_i
         L.st_o_filter_finite.restype = c_u64
         L.st_o_quat_from_euler.argtypes = [c_d, c_d, c_d, vp]
@@ -145,13 +145,17 @@ def kmeans(col_list, k, iters, draws):
     return rc, cent.reshape(d, kk), labels, used.value
 
 
-def kmeans_assign(col_list, centroids):
-    """centroids: (d, k) float32"""
+def kmeans_assign(col_list, centroids, threads=1):
+    """centroids: (d, k) float32; threads > 1 splits the points over OpenMP threads"""
     d, n = len(col_list), len(col_list[0])
     cen = np.ascontiguousarray(centroids, np.float32)
     labels = np.zeros(n, np.uint32)
-    rc = lib().st_o_kmeans_assign(_ptrs(col_list), ctypes.c_int(d), ctypes.c_uint64(n), _p(cen),
-                                  ctypes.c_int(cen.shape[1]), _p(labels))
+    if threads > 1:
+        rc = lib().st_o_kmeans_assign_mt(_ptrs(col_list), ctypes.c_int(d), ctypes.c_uint64(n), _p(cen),
+                                         ctypes.c_int(cen.shape[1]), _p(labels), ctypes.c_int(threads))
+    else:
+        rc = lib().st_o_kmeans_assign(_ptrs(col_list), ctypes.c_int(d), ctypes.c_uint64(n), _p(cen),
+                                      ctypes.c_int(cen.shape[1]), _p(labels))
     return rc, labels
 
 

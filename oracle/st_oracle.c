@@ -826,6 +826,41 @@ int st_o_kmeans_assign(const float *const *cols, int d, uint64_t n, const float 
     return rc;
 }
 
+/* The same assign with the point loop split over `threads` OpenMP threads (one tree, built
+ * once; each search reads it only).  Used to time the reference algorithm on every host core
+ * for the bench's CPU baseline; the labels are those of st_o_kmeans_assign. */
+int st_o_kmeans_assign_mt(const float *const *cols, int d, uint64_t n, const float *centroids, int k,
+                          uint32_t *labels, int threads)
+{
+    const float **ccols = (const float **)malloc(sizeof(float *) * d);
+    for (int c = 0; c < d; ++c) ccols[c] = centroids + (uint64_t)c * k;
+    kdtree t;
+    t.cols = ccols;
+    t.d = d;
+    t.nodes = (kdnode *)malloc(sizeof(kdnode) * k);
+    t.tmp = (uint32_t *)malloc(sizeof(uint32_t) * k);
+    t.nnodes = 0;
+    uint32_t *kidx = (uint32_t *)malloc(sizeof(uint32_t) * k);
+    for (int i = 0; i < k; ++i) kidx[i] = (uint32_t)i;
+    const int root = kd_build(&t, kidx, (uint64_t)k, 0);
+    int rc = 0;
+#pragma omp parallel num_threads(threads) reduction(|: rc)
+    {
+        float *point = (float *)malloc(sizeof(float) * d);
+#pragma omp for schedule(dynamic, 16)
+        for (uint64_t i = 0; i < n; ++i) {
+            for (int c = 0; c < d; ++c) point[c] = cols[c][i];
+            kdsearch s = {&t, point, INFINITY, -1};
+            kd_recurse(&s, root, 0);
+            if (s.mini < 0) rc = -1;
+            else labels[i] = (uint32_t)s.mini;
+        }
+        free(point);
+    }
+    free(ccols); free(t.nodes); free(t.tmp); free(kidx);
+    return rc;
+}
+
 /* cluster1d (write-sog.ts:56-99) */
 int st_o_cluster1d(const float *const *cols, int ncols, uint64_t n, int iters,
                    const double *draws, uint64_t ndraws, uint64_t *used,

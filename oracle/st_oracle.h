@@ -62,6 +62,8 @@ int st_o_kmeans(const float *const *cols, int d, uint64_t n, int k, int iters,
  * centroids (d columns of k) + findNearest for every point.  Used to time
  * the CPU baseline of the assign step. */
 int st_o_kmeans_assign(const float *const *cols, int d, uint64_t n, const float *centroids, int k, uint32_t *labels);
+int st_o_kmeans_assign_mt(const float *const *cols, int d, uint64_t n, const float *centroids, int k,
+                          uint32_t *labels, int threads);
 
 /* cluster1d (write-sog.ts:56-99): centroids[256] sorted ascending, labels u8 (ncols x n). */
 int st_o_cluster1d(const float *const *cols, int ncols, uint64_t n, int iters,
