@@ -62,7 +62,9 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
 void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n);  // workspace: kn.pfrag/kn.pnorm/kn.aos
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
                km::State *dstate);
-void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels);
+// returns true when it also wrote the update's (label, value bits) pairs into keys/vals
+bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,
+              uint32_t *keys = nullptr, uint32_t *vals = nullptr);
 void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n);
 
 // KdTree tie-break for exact-distance ties (st_kdtree.hip)

@@ -131,7 +131,8 @@ constexpr int KD1_CELLS = 1024;
 __global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict__ pts, uint64_t n,
                                                          const float *__restrict__ cen,
                                                          const uint32_t *__restrict__ order, int k,
-                                                         uint32_t *__restrict__ labels) {
+                                                         uint32_t *__restrict__ labels, uint32_t *__restrict__ keys,
+                                                         uint32_t *__restrict__ vals) {
     __shared__ float sv[KD1_LDS];
     __shared__ uint32_t si[KD1_LDS];
     __shared__ uint16_t cc[KD1_LDS];
@@ -184,6 +185,10 @@ __global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict
         if (!tie) lab = si[dl < dr ? L : R];
         else lab = kd1_walk(p, k, val, idx);
         labels[i] = lab;
+        if (keys) {  // the member-sort pairs of the update (label, value bits)
+            keys[i] = lab;
+            vals[i] = __builtin_bit_cast(uint32_t, pf);
+        }
     }
 }
 
@@ -597,7 +602,8 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
 
 // one exact 1-D assign: KdTree build == stable sort of the centroid values
 // (kd-tree.ts:73-99), then the walk simulation
-void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels) {
+bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels, uint32_t *keys,
+              uint32_t *vals) {
     auto *ckeys = wsT<uint32_t>(c, "k1.ckeys", (size_t)k);
     auto *corder = wsT<uint32_t>(c, "k1.corder", (size_t)k);
     hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
@@ -605,13 +611,17 @@ void assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, 
     radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
     const unsigned g = grid_for(n, 256, 256 * 16);
     KTimer kt(c, "k1.assign");
-    if (k <= KD1_LDS && !getenv("ST_KD1_WALK"))
-        hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
-    else if (k <= KD1_LDS)
+    if (k <= KD1_LDS && !getenv("ST_KD1_WALK")) {
+        hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels, keys,
+                           vals);
+        ST_LAUNCH_CHECK();
+        return keys != nullptr;
+    } else if (k <= KD1_LDS)
         hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
     else
         hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
     ST_LAUNCH_CHECK();
+    return false;
 }
 
 void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
@@ -638,14 +648,18 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
     for (int it = 0; it < iters; ++it) {
-        assign1d(c, pts, n, k, cen, labels);
+        const bool paired = assign1d(c, pts, n, k, cen, labels, keys, vals);
         mark(c, "k1.assign");
         // update
-        hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,
-                           vals);
-        ST_LAUNCH_CHECK();
-        radix_sort_u32(c, keys, vals, n, 0, kbits, "k1.msort");
-        bounds_from_sorted(c, keys, n, k, start);
+        if (!paired) {
+            hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,
+                               vals);
+            ST_LAUNCH_CHECK();
+        }
+        uint32_t *skeys = keys, *svals = vals;  // where the sort leaves its result (no copy back)
+        radix_sort_u32_inplace_or_swap(c, keys, vals, n, 0, kbits, "k1.msort", &skeys, &svals);
+        bounds_from_sorted(c, skeys, n, k, start);
+        const uint32_t *vals_s = svals;
         {
             KTimer kt(c, "k1.sum");
             if (chunked) {
@@ -654,13 +668,13 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                 scan_u32(c, ch_cnt, ch_first, (uint64_t)k, ch_first + k);
                 hipLaunchKernelGGL(k_chunk_list, dim3(gk), dim3(256), 0, c->stream, start, k, ch_first, chunks);
                 hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, k);
-                hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k,
+                hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
                                    acc);
                 hipLaunchKernelGGL(k_sum1d_final, dim3(gk), dim3(256), 0, c->stream, acc, start, k, cen, seq_flag,
                                    emin_c, sabs_c);
                 ST_LAUNCH_CHECK();
             } else {
-                hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals, start, k, cen, seq_flag, emin_c,
+                hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals_s, start, k, cen, seq_flag, emin_c,
                                    sabs_c);
                 ST_LAUNCH_CHECK();
             }
@@ -672,21 +686,21 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             }
             if (chunked) {
                 const unsigned gk = grid_for((uint64_t)k, 256, 1024);
-                hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k,
+                hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
                                    seq_flag, emin_c, rp_csum);
                 hipLaunchKernelGGL(k_rp_prefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, sabs_c,
                                    emin_c, rp_csum, rp_total);
-                hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks,
+                hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks,
                                    ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_ccnt, cand_buf);
                 hipLaunchKernelGGL(k_rp_cprefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, rp_ccnt,
                                    rp_cof, rp_ctot);
-                hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks,
+                hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks,
                                    ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_cof, cand_buf);
                 hipLaunchKernelGGL(k_rp_finish, dim3((k + 63) / 64), dim3(64), 0, c->stream, start, rp_ctot, k,
                                    seq_flag, emin_c, sabs_c, rp_total, cand_buf, cen);
                 ST_LAUNCH_CHECK();
             } else {
-                hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals, start, seq_flag, emin_c,
+                hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals_s, start, seq_flag, emin_c,
                                    sabs_c, cen, cand_buf);
                 ST_LAUNCH_CHECK();
             }
@@ -701,7 +715,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                 }
                 fprintf(stderr, "[st k1] n=%llu uncertified=%d sequential-fallback=%d\n", (unsigned long long)n, a, b);
             }
-            hipLaunchKernelGGL(k_sum1d_seq, dim3(k), dim3(64), 0, c->stream, vals, start, seq_flag, cen);
+            hipLaunchKernelGGL(k_sum1d_seq, dim3(k), dim3(64), 0, c->stream, vals_s, start, seq_flag, cen);
             ST_LAUNCH_CHECK();
         }
         reseed_empty(c, dcols, 1, n, k, start, ddraws, ndraws, dstate, cen);

@@ -108,6 +108,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K *__restrict__ ke
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
+// One tile of RS_TILE elements: wave-level ranks by ballot (stable), then the tile is
+// reordered by digit in LDS so each digit's run leaves as consecutive addresses
+// (coalesced stores) at its global offset.
 template <typename K>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                            uint64_t n, int shift, int bits,
@@ -116,13 +119,18 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
     __shared__ uint32_t wcount[RS_WAVES][256];
     __shared__ uint32_t wbase[RS_WAVES][256];
     __shared__ uint32_t goff[256];
+    __shared__ uint32_t dstart[256];  // first local position of each digit
+    __shared__ uint32_t wtot[RS_WAVES];
+    __shared__ K sk[RS_TILE];
+    __shared__ uint32_t sv[RS_TILE];
     for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wcount[0][0])[i] = 0;
     goff[threadIdx.x] = offs[(uint64_t)threadIdx.x * nblocks + blockIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t mask = (1u << bits) - 1u;
-    const uint64_t wbase_e = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WAVE_SPAN;
+    const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t wbase_e = tbase + (uint64_t)w * RS_WAVE_SPAN;
     K k[RS_ROWS];
     uint32_t v[RS_ROWS];
     uint32_t off[RS_ROWS];
@@ -133,6 +141,11 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
         const bool valid = e < n;
         k[r] = valid ? keys[e] : (K)0;
         v[r] = valid ? vals[e] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_ROWS; ++r) {
+        const uint64_t e = wbase_e + (uint64_t)r * 64 + lane;
+        const bool valid = e < n;
         const uint32_t d = (uint32_t)(k[r] >> shift) & mask;
         dg[r] = d;
         uint64_t peers = __ballot(valid);
@@ -150,6 +163,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
     }
     __syncthreads();
     {
+        // per digit: offsets of the waves, and the digit's total for the tile
         const int d = threadIdx.x;
         uint32_t s = 0;
 #pragma unroll
@@ -157,22 +171,45 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
             wbase[i][d] = s;
             s += wcount[i][d];
         }
+        // exclusive scan of the digit totals across the block (256 threads)
+        uint32_t incl = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wtot[w] = incl;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int i = 0; i < w; ++i) woff += wtot[i];
+        dstart[d] = woff + incl - s;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ROWS; ++r) {
         const uint64_t e = wbase_e + (uint64_t)r * 64 + lane;
         if (e < n) {
-            const uint32_t pos = goff[dg[r]] + wbase[w][dg[r]] + off[r];
-            okeys[pos] = k[r];
-            ovals[pos] = v[r];
+            const uint32_t lp = dstart[dg[r]] + wbase[w][dg[r]] + off[r];
+            sk[lp] = k[r];
+            sv[lp] = v[r];
         }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : (uint64_t)RS_TILE);
+    for (uint32_t i = threadIdx.x; i < cnt; i += RS_THREADS) {
+        const K kk = sk[i];
+        const uint32_t d = (uint32_t)(kk >> shift) & mask;
+        const uint32_t pos = goff[d] + (i - dstart[d]);
+        okeys[pos] = kk;
+        ovals[pos] = sv[i];
     }
 }
 
 template <typename K>
 void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
-                     const std::string &tag) {
+                     const std::string &tag, K **out_keys = nullptr, uint32_t **out_vals = nullptr) {
+    if (out_keys) *out_keys = keys;
+    if (out_vals) *out_vals = vals;
     if (n <= 1 || end_bit <= begin_bit) return;
     ST_REQUIRE(n < (1ull << 32), ST_ERR_ARG, "radix sort: n must be < 2^32");
     const uint32_t nblocks = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
@@ -194,6 +231,11 @@ void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_b
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
+    }
+    if (out_keys) {  // the caller takes the result where the last pass left it
+        *out_keys = ka;
+        *out_vals = va;
+        return;
     }
     if (passes & 1) {
         ST_HIP(hipMemcpyAsync(keys, ka, n * sizeof(K), hipMemcpyDeviceToDevice, c->stream));
@@ -228,6 +270,11 @@ void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t
 
 void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
     radix_sort_impl<uint32_t>(c, keys, vals, n, b0, b1, tag);
+}
+
+void radix_sort_u32_inplace_or_swap(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1,
+                                    const std::string &tag, uint32_t **out_keys, uint32_t **out_vals) {
+    radix_sort_impl<uint32_t>(c, keys, vals, n, b0, b1, tag, out_keys, out_vals);
 }
 
 void radix_sort_u64(st_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
