@@ -528,6 +528,35 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
                                   const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
                                   uint32_t *__restrict__ ties, State *st);
 
+// all-reduce over a 16-lane DPP row (every lane of the row active): quad_perm xor 1, xor 2,
+// then row_ror 4 and 8 -- DPP moves folded into the VALU op, no LDS round trips
+template <int CTRL>
+__device__ inline uint32_t dpp_u(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ inline float dpp_f(float x) {
+    return __builtin_bit_cast(float, dpp_u<CTRL>(__builtin_bit_cast(uint32_t, x)));
+}
+__device__ inline float row16_min(float v) {
+    v = fminf(v, dpp_f<0xB1>(v));
+    v = fminf(v, dpp_f<0x4E>(v));
+    v = fminf(v, dpp_f<0x124>(v));
+    return fminf(v, dpp_f<0x128>(v));
+}
+__device__ inline uint32_t row16_umin(uint32_t v) {
+    v = min(v, dpp_u<0xB1>(v));
+    v = min(v, dpp_u<0x4E>(v));
+    v = min(v, dpp_u<0x124>(v));
+    return min(v, dpp_u<0x128>(v));
+}
+__device__ inline uint32_t row16_sum(uint32_t v) {
+    v += dpp_u<0xB1>(v);
+    v += dpp_u<0x4E>(v);
+    v += dpp_u<0x124>(v);
+    return v + dpp_u<0x128>(v);
+}
+
 template <int G>
 __device__ inline void fix_group(const float *__restrict__ aos, int d, const float2 *__restrict__ cfix,
                                  const float *__restrict__ caos, int k, uint64_t p, int r, uint32_t code,
@@ -572,16 +601,28 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
     const float lo = valid ? s - (s * rel + ab) : __builtin_inff();
     const float hi = valid ? s + (s * rel + ab) : __builtin_inff();
     float mh = hi;
+    if (G == 16) {
+        mh = row16_min(mh);
+    } else {
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
+        for (int o = G / 2; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
+    }
     bool cand = valid && lo <= mh;  // NaN/inf screens fall through to the exact path
     uint32_t ncand = cand ? 1u : 0u;
+    if (G == 16) {
+        ncand = row16_sum(ncand);
+    } else {
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
+        for (int o = G / 2; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
+    }
     if (ncand == 1) {
         uint32_t w = cand ? c : 0xffffffffu;
+        if (G == 16) {
+            w = row16_umin(w);
+        } else {
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
+            for (int o = G / 2; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
+        }
         if (r == 0) labels[p] = w;
         return;
     }
@@ -720,10 +761,10 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
     const uint32_t cb = 16 + rr < cnt ? labels[pb] : 0u;
     auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
     auto code_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? ca : cb, gl + (i & 15), 64); };
-    auto slice = [&](uint32_t pt) {
-        return rr < LD / 4 ? reinterpret_cast<const float4 *>(aos + (uint64_t)pt * LD)[rr]
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
+    // every lane loads (lanes past LD / 4 repeat a slice nobody broadcasts): no branch around
+    // the load, so the wait before the scoring covers only the older loads
+    const int sq = rr % (LD / 4);
+    auto slice = [&](uint32_t pt) { return reinterpret_cast<const float4 *>(aos + (uint64_t)pt * LD)[sq]; };
     float4 row[LD / 4];
     uint32_t have = 0xffffffffu, c = 0;
     bool valid = false;
@@ -740,7 +781,14 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
 #pragma unroll
             for (int q = 0; q < LD / 4; ++q) row[q] = src[q];
         }
-        const float4 nxt = slice(pn);
+        // the next point's slice is loaded by hand so the compiler cannot sink the load below
+        // the scoring (it would wait for it at the top of the next iteration); the wait
+        // before `cur = nxt` covers it
+        float4 nxt;
+        {
+            const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn * LD) + sq;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt) : "v"(src) : "memory");
+        }
         float s0 = 0.f, s1 = 0.f;  // two chains: the screen bound holds for any summation order
         static_for<LD / 4>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
@@ -754,6 +802,7 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
             s1 = __builtin_fmaf(v, v, s1);
         });
         fix_decide<16>(s0 + s1, valid, c, d, caos, aos + (uint64_t)p * LD, p, rr, labels, ties, st);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cur = nxt;
         p = pn;
     }
