@@ -603,6 +603,9 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
     float mh = hi;
     if (G == 16) {
         mh = row16_min(mh);
+    } else if (G == 32) {
+        mh = row16_min(mh);
+        mh = fminf(mh, __shfl_xor(mh, 16, 64));
     } else {
 #pragma unroll
         for (int o = G / 2; o > 0; o >>= 1) mh = fminf(mh, __shfl_xor(mh, o, 64));
@@ -611,6 +614,9 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
     uint32_t ncand = cand ? 1u : 0u;
     if (G == 16) {
         ncand = row16_sum(ncand);
+    } else if (G == 32) {
+        ncand = row16_sum(ncand);
+        ncand += __shfl_xor(ncand, 16, 64);
     } else {
 #pragma unroll
         for (int o = G / 2; o > 0; o >>= 1) ncand += __shfl_xor(ncand, o, 64);
@@ -619,6 +625,9 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
         uint32_t w = cand ? c : 0xffffffffu;
         if (G == 16) {
             w = row16_umin(w);
+        } else if (G == 32) {
+            w = row16_umin(w);
+            w = min(w, __shfl_xor(w, 16, 64));
         } else {
 #pragma unroll
             for (int o = G / 2; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
@@ -806,6 +815,42 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
         cur = nxt;
         p = pn;
     }
+}
+
+// pair points with the point row broadcast by DPP: lanes 0-15 score the rows of the first
+// tile-half, lanes 16-31 the second (two DPP rows); each lane loads one float4 slice of the
+// point, rows come from the coalesced cfix layout
+template <int LD>
+__global__ __launch_bounds__(256) void k_fixpair_b(const float *__restrict__ aos, int d,
+                                                   const float2 *__restrict__ cfix, const float *__restrict__ caos,
+                                                   int k, const uint32_t *__restrict__ pair_pts,
+                                                   const uint2 *__restrict__ pair_codes, uint32_t npairs,
+                                                   uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                   State *st) {
+    const uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 5;
+    if (i >= npairs) return;  // uniform per 32-lane group
+    const int r = threadIdx.x & 31, rr = r & 15;
+    const uint2 cc = pair_codes[i];
+    const uint32_t p = pair_pts[i];
+    const uint32_t code = r < 16 ? cc.x : cc.y;
+    const uint32_t c = code_row(code, rr);
+    const bool valid = c < (uint32_t)k;
+    const float4 pv = reinterpret_cast<const float4 *>(aos + (uint64_t)p * LD)[rr % (LD / 4)];
+    const float2 *crow = cfix + (uint64_t)(code >> 1) * 2 * (LD / 2) * 16 + (uint64_t)(code & 1) * (LD / 2) * 16 + rr;
+    float s0 = 0.f, s1 = 0.f;
+    static_for<LD / 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const float2 c0 = crow[(2 * q) * 16], c1 = crow[(2 * q + 1) * 16];
+        float v = row_bcast<q>(pv.x) - c0.x;
+        s0 = __builtin_fmaf(v, v, s0);
+        v = row_bcast<q>(pv.y) - c0.y;
+        s1 = __builtin_fmaf(v, v, s1);
+        v = row_bcast<q>(pv.z) - c1.x;
+        s0 = __builtin_fmaf(v, v, s0);
+        v = row_bcast<q>(pv.w) - c1.y;
+        s1 = __builtin_fmaf(v, v, s1);
+    });
+    fix_decide<32>(valid ? s0 + s1 : 0.f, valid, c, d, caos, aos + (uint64_t)p * LD, p, r, labels, ties, st);
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)
@@ -1042,8 +1087,19 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     const uint32_t npair = h->pairs;
     if (npair) {
         KTimer kt(c, "kn.fixpair");
-        hipLaunchKernelGGL(k_fixpair, dim3((npair * 32 + 255) / 256), dim3(256), 0, c->stream, aos, d, cfix, caos, k,
-                           pair_pts, pair_codes, npair, labels, ties, dstate);
+        const dim3 g((npair * 32 + 255) / 256);
+        if (ld == 48)
+            hipLaunchKernelGGL(k_fixpair_b<48>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, ties, dstate);
+        else if (ld == 24)
+            hipLaunchKernelGGL(k_fixpair_b<24>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, ties, dstate);
+        else if (ld == 12)
+            hipLaunchKernelGGL(k_fixpair_b<12>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, ties, dstate);
+        else
+            hipLaunchKernelGGL(k_fixpair, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts, pair_codes,
+                               npair, labels, ties, dstate);
         ST_LAUNCH_CHECK();
     }
     mark(c, "kn.assign");
