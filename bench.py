@@ -48,6 +48,7 @@ def parse():
                     'rehearse several ranks on one GPU)')
     ap.add_argument('--cpu-assign-sample', type=int, default=1000)
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
+    ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     return ap.parse_args()
 
 
@@ -130,6 +131,69 @@ def cpu_baseline(args):
                    f'{args.cpu_assign_sample} points ({ta * 1e3:.2f} ms/point/iter) x {args.iters} iters + SH0 '
                    f'writeSog pipeline timed on {n} splats ({tb * 1e6:.2f} us/splat); extrapolated per splat'),
     }, all_cores
+
+
+PLY_ORDER = (['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] +
+             ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3'])
+
+
+def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
+    """The CLI's work for `splat-transform in.ply out.sog` on this table: the step's table is
+    written once as a binary little-endian 3DGS PLY (62 float properties, 248 B per splat,
+    normals 0; untimed), then each timed rep reads the file into device columns
+    (st_dev_ply_read: page cache -> pinned chunks -> HBM -> k_ply_cols), runs the same
+    writeSog step, builds the .sog archive (WebP x7 + CRC + ZIP) and writes it to a file.
+    The archive must equal the in-memory step's byte for byte."""
+    import tempfile
+
+    import numpy as np
+    import torch
+    n = cols['x'].shape[0]
+    d = tempfile.mkdtemp(prefix='st_e2e_', dir=os.environ.get('TMPDIR', '/tmp'))
+    src, dst = os.path.join(d, 'in.ply'), os.path.join(d, 'out.sog')
+    try:
+        head = ('ply\nformat binary_little_endian 1.0\n' + f'element vertex {n}\n' +
+                ''.join(f'property float {k}\n' for k in PLY_ORDER) + 'end_header\n').encode()
+        zero = torch.zeros(n, dtype=torch.float32, device=cols['x'].device)
+        with open(src, 'wb') as f:
+            f.write(head)
+            step = 1 << 22
+            for a in range(0, n, step):
+                b = min(n, a + step)
+                rows = torch.stack([(cols[k][a:b] if k in cols else zero[a:b]) for k in PLY_ORDER], 1)
+                f.write(rows.cpu().numpy().tobytes())
+        del zero
+        file_bytes = os.path.getsize(src)
+        times, same = [], True
+        for r in range(reps + 1):  # rep 0 warms the file cache and the ingest buffers
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, els = ctx.read_ply_dev(src)
+            vc = dict(els)['vertex']
+            table = {k: v for k, v in vc.items() if not k.startswith('n')}
+            meta, _ = ctx.dev_sog(table, iters, draws, tex)
+            addr, size = ctx.dev_sog_bundle_view(meta, n, tex, 0, 0)
+            with open(dst, 'wb') as f:
+                f.write((ctypes_char_array(size)).from_address(addr))
+            t1 = time.perf_counter()
+            if r:
+                times.append(t1 - t0)
+            del els, vc, table
+            same = same and (open(dst, 'rb').read() == ref_archive)
+        ms = sorted(times)[len(times) // 2] * 1e3
+        return {'what': 'PLY file (page cache) -> device columns -> writeSog step -> .sog archive -> file, rank 0',
+                'ply_bytes': file_bytes, 'sog_bytes': size, 'ms': ms, 'Msplats_per_s': n / ms / 1e3,
+                'reps': reps, 'archive_equals_in_memory_step': same}
+    finally:
+        for f in (src, dst):
+            if os.path.exists(f):
+                os.remove(f)
+        os.rmdir(d)
+
+
+def ctypes_char_array(size):
+    import ctypes
+    return ctypes.c_char * size
 
 
 def main():
@@ -229,7 +293,8 @@ def main():
     else:
         import splat_dist
         bmeta, btex, bcount = splat_dist.meta_struct(last['meta']), last['tex'], n * world
-    ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)  # warm: workspace + pinned archive
+    addr0, size0 = ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)  # warm: workspace + pinned archive
+    ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0)) if world == 1 else None
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     torch.cuda.synchronize()
@@ -248,6 +313,9 @@ def main():
     D = 45
     flops_per_launch = 2.0 * n * pal * D  # nearest-centroid dot products, one assign pass
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = end_to_end(ctx, cols, args.iters, draws, tex, ref_archive)
     cpu, cpu_all = (None, None) if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
@@ -298,6 +366,7 @@ def main():
             'end_to_end_ms_per_step': elapsed / args.steps * 1e3 + container_ms,
             'end_to_end_Msplats_per_s': (n * world) / (elapsed / args.steps + container_ms / 1e3) / 1e6,
         },
+        'end_to_end_file': e2e,
         'stages_ms': stages,
         'kernels': kstats,
         'draws_used_per_step': used,
