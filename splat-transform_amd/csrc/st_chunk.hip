@@ -113,18 +113,23 @@ struct TransposeArgs {
     float *rows;
 };
 
-// 64 rows per block through LDS: coalesced column reads, coalesced row writes
+// RA_ROWS rows per block through LDS: coalesced column reads (all of a thread's loads issued
+// before the first LDS store), coalesced row writes
+constexpr int RA_ROWS = 256;
 __global__ __launch_bounds__(256) void k_rows_aos(const TransposeArgs a) {
-    __shared__ float tile[64 * 64];
-    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    __shared__ float tile[RA_ROWS * 16];  // rl <= 16
+    const uint64_t r0 = (uint64_t)blockIdx.x * RA_ROWS;
     const int t = threadIdx.x;
-    for (int e = t; e < 64 * a.rl; e += 256) {
-        const int col = e / 64, r = e % 64;
-        const uint64_t row = r0 + r;
-        tile[r * a.rl + col] = (col < a.ncol && row < a.n) ? a.src[col][row] : 0.0f;
-    }
+    const uint64_t row = r0 + t;
+    const uint64_t rsafe = row < a.n ? row : a.n - 1;  // every load in bounds, no branch around it
+    float v[16];
+#pragma unroll
+    for (int col = 0; col < 16; ++col) v[col] = (col < a.ncol) ? a.src[col][rsafe] : 0.0f;
+#pragma unroll
+    for (int col = 0; col < 16; ++col)
+        if (col < a.rl) tile[t * a.rl + col] = (col < a.ncol && row < a.n) ? v[col] : 0.0f;
     __syncthreads();
-    const uint64_t nrows = (a.n - r0 < 64) ? (a.n - r0) : 64;
+    const uint64_t nrows = (a.n - r0 < RA_ROWS) ? (a.n - r0) : RA_ROWS;
     float4 *dst = reinterpret_cast<float4 *>(a.rows + r0 * a.rl);
     const float4 *s4 = reinterpret_cast<const float4 *>(tile);
     for (uint64_t e = t; e < nrows * a.rl / 4; e += 256) dst[e] = s4[e];
@@ -144,7 +149,15 @@ __global__ __launch_bounds__(256) void k_sh_rows(const TransposeArgs a, int nsh,
     const uint32_t t = threadIdx.x;
     uint8_t *st8 = reinterpret_cast<uint8_t *>(stage);
     const bool real = r0 + t < a.n;
-    for (int k = 0; k < SHB; ++k) st8[t * SHB + k] = (k < nsh && real) ? sh_byte(a.src[14 + k][r0 + t]) : 0u;
+    const uint64_t rsafe = real ? r0 + t : a.n - 1;  // loads stay in bounds without a branch
+    // batches of 12 columns: the loads of a batch are in flight together
+    for (int k0 = 0; k0 < SHB; k0 += 12) {
+        float v[12];
+#pragma unroll
+        for (int u = 0; u < 12; ++u) v[u] = a.src[14 + min(k0 + u, nsh - 1)][rsafe];
+#pragma unroll
+        for (int u = 0; u < 12; ++u) st8[t * SHB + k0 + u] = (k0 + u < nsh && real) ? sh_byte(v[u]) : 0u;
+    }
     __syncthreads();
     const uint64_t nrows = (a.n - r0 < 256) ? (a.n - r0) : 256;
     uint4 *dst = reinterpret_cast<uint4 *>(shrows + r0 * SHB);
@@ -274,7 +287,7 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     a.sh_out = sh;
     const uint64_t nchunks = (n + 255) / 256;
     KTimer kt(c, "chunk.pack");
-    hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, c->stream, ta);
+    hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + RA_ROWS - 1) / RA_ROWS)), dim3(256), 0, c->stream, ta);
     if (nsh) hipLaunchKernelGGL(k_sh_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, ta, nsh, shrows);
     hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();

@@ -122,6 +122,83 @@ __global__ __launch_bounds__(256) void k_gather_cols(float *const *src, float *c
     }
 }
 
+// ---- wide streaming forms: 4 consecutive rows per thread, column pointers in kernel
+// arguments, 8 columns' loads in flight before any test (the loops above wait on every
+// column's load in turn)
+constexpr int WIDE_COLS = 64;
+struct ColPtrs {
+    const float *p[WIDE_COLS];
+};
+
+__device__ inline uint32_t nonfinite_bit(float x) {
+    return ((__builtin_bit_cast(uint32_t, x) & 0x7f800000u) == 0x7f800000u) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_finite_flags4(const ColPtrs cp, int ncol, uint64_t n,
+                                                       uint32_t *__restrict__ flags) {
+    const uint64_t nq = n / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+        uint32_t bad = 0;  // bit r: row 4q + r holds a non-finite value
+        int c = 0;
+        for (; c + 8 <= ncol; c += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4 *>(cp.p[c + u])[q];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                bad |= nonfinite_bit(v[u].x) | (nonfinite_bit(v[u].y) << 1) | (nonfinite_bit(v[u].z) << 2) |
+                       (nonfinite_bit(v[u].w) << 3);
+        }
+        for (; c < ncol; ++c) {
+            const float4 v = reinterpret_cast<const float4 *>(cp.p[c])[q];
+            bad |= nonfinite_bit(v.x) | (nonfinite_bit(v.y) << 1) | (nonfinite_bit(v.z) << 2) | (nonfinite_bit(v.w) << 3);
+        }
+        reinterpret_cast<uint4 *>(flags)[q] =
+            make_uint4((bad & 1u) ^ 1u, ((bad >> 1) & 1u) ^ 1u, ((bad >> 2) & 1u) ^ 1u, ((bad >> 3) & 1u) ^ 1u);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n % 4) {  // the last n % 4 rows
+        const uint64_t i = nq * 4 + threadIdx.x;
+        uint32_t bad = 0;
+        for (int c = 0; c < ncol; ++c) bad |= nonfinite_bit(cp.p[c][i]);
+        flags[i] = bad ^ 1u;
+    }
+}
+
+// permuteRows with 4 destination rows per thread: 4 x 8 gathered loads in flight, float4
+// stores (dst columns and idx 16-byte aligned)
+__global__ __launch_bounds__(256) void k_gather_cols4(const ColPtrs src, const ColPtrs dst, int ncol,
+                                                      const uint32_t *__restrict__ idx, uint64_t m) {
+    const uint64_t mq = m / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < mq; q += stride) {
+        const uint4 ii = reinterpret_cast<const uint4 *>(idx)[q];
+        int c = 0;
+        for (; c + 8 <= ncol; c += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float *sp = src.p[c + u];
+                v[u] = make_float4(sp[ii.x], sp[ii.y], sp[ii.z], sp[ii.w]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) reinterpret_cast<float4 *>(const_cast<float *>(dst.p[c + u]))[q] = v[u];
+        }
+        for (; c < ncol; ++c) {
+            const float *sp = src.p[c];
+            reinterpret_cast<float4 *>(const_cast<float *>(dst.p[c]))[q] =
+                make_float4(sp[ii.x], sp[ii.y], sp[ii.z], sp[ii.w]);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < m % 4) {
+        const uint64_t j = mq * 4 + threadIdx.x;
+        const uint32_t sj = idx[j];
+        for (int c = 0; c < ncol; ++c) const_cast<float *>(dst.p[c])[j] = src.p[c][sj];
+    }
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
 }  // namespace
 
 void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p) {
@@ -176,9 +253,20 @@ uint64_t filter_finite_dev(st_ctx *c, const st_table *t, uint32_t *out_idx) {
     if (n == 0) return 0;
     auto *flags = wsT<uint32_t>(c, "filter.flags", n);
     auto *pos = wsT<uint32_t>(c, "filter.pos", n + 1);
-    float *const *dcols = upload_ptrs(c, "filter.cols", t->cols, t->ncol);
-    hipLaunchKernelGGL(k_finite_flags, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, dcols, t->ncol, n,
-                       flags);
+    bool wide = t->ncol <= WIDE_COLS;
+    ColPtrs cp{};
+    for (int i = 0; wide && i < t->ncol; ++i) {
+        cp.p[i] = t->cols[i];
+        wide = aligned16(t->cols[i]);
+    }
+    if (wide) {
+        hipLaunchKernelGGL(k_finite_flags4, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, c->stream, cp,
+                           t->ncol, n, flags);
+    } else {
+        float *const *dcols = upload_ptrs(c, "filter.cols", t->cols, t->ncol);
+        hipLaunchKernelGGL(k_finite_flags, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, dcols, t->ncol, n,
+                           flags);
+    }
     ST_LAUNCH_CHECK();
     scan_u32(c, flags, pos, n, pos + n);
     hipLaunchKernelGGL(k_compact, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, flags, pos, n, out_idx);
@@ -191,9 +279,22 @@ uint64_t filter_finite_dev(st_ctx *c, const st_table *t, uint32_t *out_idx) {
 
 void permute_rows_dev(st_ctx *c, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst) {
     if (m == 0 || src->ncol == 0) return;
-    float *const *s = upload_ptrs(c, "permute.src", src->cols, src->ncol);
-    float *const *d = upload_ptrs(c, "permute.dst", dst->cols, dst->ncol);
-    hipLaunchKernelGGL(k_gather_cols, dim3(grid_for(m, 256, 8192)), dim3(256), 0, c->stream, s, d, src->ncol, idx, m);
+    bool wide = src->ncol <= WIDE_COLS && aligned16(idx);
+    ColPtrs sp{}, dp{};
+    for (int i = 0; wide && i < src->ncol; ++i) {
+        sp.p[i] = src->cols[i];
+        dp.p[i] = dst->cols[i];
+        wide = aligned16(dst->cols[i]);
+    }
+    if (wide) {
+        hipLaunchKernelGGL(k_gather_cols4, dim3(grid_for((m + 3) / 4, 256, 8192)), dim3(256), 0, c->stream, sp, dp,
+                           src->ncol, idx, m);
+    } else {
+        float *const *s = upload_ptrs(c, "permute.src", src->cols, src->ncol);
+        float *const *d = upload_ptrs(c, "permute.dst", dst->cols, dst->ncol);
+        hipLaunchKernelGGL(k_gather_cols, dim3(grid_for(m, 256, 8192)), dim3(256), 0, c->stream, s, d, src->ncol, idx,
+                           m);
+    }
     ST_LAUNCH_CHECK();
 }
 
