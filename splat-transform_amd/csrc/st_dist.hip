@@ -228,19 +228,9 @@ __global__ __launch_bounds__(256) void k_average(int d, int k, const uint32_t *_
 
 // ---------------------------------------------------------------------------
 void minmax_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, double *lo, double *hi) {
-    auto **dcols = wsT<const float *>(c, "ds.mmcols", (size_t)ncols);
-    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * ncols, hipMemcpyHostToDevice, c->stream));
     auto *mm = wsT<uint32_t>(c, "ds.mm", 2 * (size_t)ncols);
     std::vector<uint32_t> init(2 * ncols);
-    for (int a = 0; a < ncols; ++a) {
-        init[2 * a] = 0xffffffffu;
-        init[2 * a + 1] = 0;
-    }
-    ST_HIP(hipMemcpyAsync(mm, init.data(), init.size() * 4, hipMemcpyHostToDevice, c->stream));
-    if (n) {
-        hipLaunchKernelGGL(k_minmax_cols, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, dcols, ncols, n, mm);
-        ST_LAUNCH_CHECK();
-    }
+    minmax_keys_dev(c, cols, ncols, n, mm);
     ST_HIP(hipMemcpyAsync(init.data(), mm, init.size() * 4, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     for (int a = 0; a < ncols; ++a) {
@@ -253,7 +243,7 @@ void dist_prepare(st_ctx *c, const float *const *cols, int d, uint64_t n) {
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans: n must be < 2^31 per device");
     auto **dcols = wsT<const float *>(c, "ds.cols", (size_t)d);
     ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
-    check_finite(c, dcols, d, n);
+    check_finite(c, cols, dcols, d, n);
     if (d > 1) nd_prepare(c, dcols, d, n);
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 
 #include <cstdint>
 #include <map>
@@ -75,6 +76,9 @@ struct StageTimer {
 
 struct st_ctx {
     int device = 0;
+    // max |x| over the k-means point set, found by check_finite in the same pass as the
+    // finiteness test (negative: not known, nd_prepare computes it)
+    float km_absmax = -1.0f;
     // the N-D k-means point set prepared by nd_prepare (fp16 scale and shape)
     float kn_sigma = 1.0f;
     uint64_t kn_n = 0;
@@ -153,6 +157,10 @@ void radix_sort_u64(st_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t n, int b
                     const std::string &tag);
 
 // iota
+// min and max of each column as order-preserving u32 keys (NaN ignored; an all-NaN or empty
+// column gives min 0xffffffff, max 0): out[2a] = min, out[2a + 1] = max.  cols: host array of
+// device pointers, ncols <= 64
+void minmax_keys_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, uint32_t *out);
 void iota_u32(st_ctx *c, uint32_t *out, uint64_t n);
 
 // column lookups on an st_table

@@ -65,7 +65,9 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
 // returns true when it also wrote the update's (label, value bits) pairs into keys/vals
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,
               uint32_t *keys = nullptr, uint32_t *vals = nullptr);
-void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n);
+// throws ST_ERR_NONFINITE on a non-finite value; also leaves max |x| in c->km_absmax
+// (cols: host array of the device columns, dcols: the same array on the device)
+void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n);
 
 // KdTree tie-break for exact-distance ties (st_kdtree.hip)
 void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,

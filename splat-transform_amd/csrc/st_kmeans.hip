@@ -39,6 +39,65 @@ __global__ __launch_bounds__(256) void k_nonfinite(const float *const *cols, int
     if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
+// the same test and max |x| in one pass: 4 rows per thread (float4), 8 columns' loads in
+// flight, one atomic per workgroup
+struct ScanCols {
+    const float *p[64];
+};
+__global__ __launch_bounds__(256) void k_scan_cols(const ScanCols cp, int d, uint64_t n, uint32_t *flag,
+                                                   uint32_t *amax_bits) {
+    const uint64_t nq = n / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t bad = 0;
+    float m = 0.f;
+    auto take = [&](float v) {
+        bad |= js::isfinitef_(v) ? 0u : 1u;
+        m = __builtin_fmaxf(m, __builtin_fabsf(v));
+    };
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+        int c = 0;
+        for (; c + 8 <= d; c += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4 *>(cp.p[c + u])[q];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                take(v[u].x);
+                take(v[u].y);
+                take(v[u].z);
+                take(v[u].w);
+            }
+        }
+        for (; c < d; ++c) {
+            const float4 v = reinterpret_cast<const float4 *>(cp.p[c])[q];
+            take(v.x);
+            take(v.y);
+            take(v.z);
+            take(v.w);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n % 4)
+        for (int c = 0; c < d; ++c) take(cp.p[c][nq * 4 + threadIdx.x]);
+    __shared__ uint32_t sb[4];
+    __shared__ float sm[4];
+    for (int o = 32; o > 0; o >>= 1) {
+        bad |= __shfl_xor(bad, o, 64);
+        m = __builtin_fmaxf(m, __shfl_xor(m, o, 64));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sb[w] = bad;
+        sm[w] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        bad = sb[0] | sb[1] | sb[2] | sb[3];
+        m = __builtin_fmaxf(__builtin_fmaxf(sm[0], sm[1]), __builtin_fmaxf(sm[2], sm[3]));
+        if (bad) atomicOr(flag, 1u);
+        atomicMax(amax_bits, __builtin_bit_cast(uint32_t, m));  // non-negative floats order as their bits
+    }
+}
+
 // initializeCentroids1D (k-means.ts:23-39)
 __global__ __launch_bounds__(256) void k_minmax1d(const float *v, uint64_t n, uint32_t *mm) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -117,16 +176,27 @@ __global__ void k_advance_cursor(State *st, const uint32_t *total_empty) { st->c
 using namespace km;
 
 // ---------------------------------------------------------------------------
-void check_finite(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
-    auto *flag = wsT<uint32_t>(c, "km.nf", 1);
-    ST_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_nonfinite, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c->stream, dcols, d, n, flag);
+void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n) {
+    auto *flag = wsT<uint32_t>(c, "km.nf", 2);  // [0] non-finite seen, [1] max |x| bits
+    ST_HIP(hipMemsetAsync(flag, 0, 8, c->stream));
+    bool wide = d <= 64;
+    ScanCols sc{};
+    for (int j = 0; wide && j < d; ++j) {
+        sc.p[j] = cols[j];
+        wide = ((uintptr_t)cols[j] & 15u) == 0;
+    }
+    if (wide)
+        hipLaunchKernelGGL(k_scan_cols, dim3(grid_for((n + 3) / 4, 256, 1024)), dim3(256), 0, c->stream, sc, d, n,
+                           flag, flag + 1);
+    else
+        hipLaunchKernelGGL(k_nonfinite, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c->stream, dcols, d, n, flag);
     ST_LAUNCH_CHECK();
     auto *h = static_cast<uint32_t *>(pinned(c, 16));
-    ST_HIP(hipMemcpyAsync(h, flag, 4, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipMemcpyAsync(h, flag, 8, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     ST_REQUIRE(h[0] == 0, ST_ERR_NONFINITE,
                "kmeans: non-finite point (the reference's KdTree returns index -1 and k-means.ts:131 throws)");
+    c->km_absmax = wide ? __builtin_bit_cast(float, h[1]) : -1.0f;
 }
 
 // reseed + cursor bookkeeping shared by both update paths
@@ -170,7 +240,7 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     }
     auto **dcols = wsT<const float *>(c, "km.cols", (size_t)d);
     ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
-    check_finite(c, dcols, d, n);
+    check_finite(c, cols, dcols, d, n);
     mark(c, "km.check");
 
     // Math.random stream: uploaded once, consumed on device in reference order
@@ -179,9 +249,7 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     uint64_t init_used = 0;
     if (d == 1) {
         auto *mm = wsT<uint32_t>(c, "km.mm", 2);
-        const uint32_t init_mm[2] = {0xffffffffu, 0u};
-        ST_HIP(hipMemcpyAsync(mm, init_mm, 8, hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(k_minmax1d, dim3(grid_for(n, 256, 1024)), dim3(256), 0, c->stream, cols[0], n, mm);
+        minmax_keys_dev(c, cols, 1, n, mm);  // finite input (checked above): keys of min and max
         hipLaunchKernelGGL(k_init1d, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, mm, cen, k);
         ST_LAUNCH_CHECK();
     } else {

@@ -998,14 +998,18 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits
-    // scale: max|x| * sigma in [1, 2)
+    // scale: max|x| * sigma in [1, 2); check_finite found max|x| in its pass over the points
     ST_HIP(hipMemsetAsync(scal, 0, 16, c->stream));
-    hipLaunchKernelGGL(k_absmax, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, dcols, d, n, scal);
-    ST_LAUNCH_CHECK();
-    uint32_t amax_bits = 0;
-    ST_HIP(hipMemcpyAsync(&amax_bits, scal, 4, hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
-    const float amax = __builtin_bit_cast(float, amax_bits);
+    float amax = c->km_absmax;
+    c->km_absmax = -1.0f;
+    if (amax < 0.0f) {
+        hipLaunchKernelGGL(k_absmax, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, dcols, d, n, scal);
+        ST_LAUNCH_CHECK();
+        uint32_t amax_bits = 0;
+        ST_HIP(hipMemcpyAsync(&amax_bits, scal, 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        amax = __builtin_bit_cast(float, amax_bits);
+    }
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
     hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(256), 0,

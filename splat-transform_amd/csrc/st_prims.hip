@@ -205,6 +205,94 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
     }
 }
 
+// ---- min/max of columns as order-preserving keys (NaN skipped), two stages ----------
+// Stage 1: gridDim.y = column, each workgroup reduces a contiguous slice (float4 loads
+// when the column is 16-byte aligned, 4 quads in flight per thread) to one partial;
+// stage 2: one workgroup per column.  No same-address atomics (a few thousand workgroups
+// hammering six words cost more than the reads).
+constexpr int MM_BLOCKS = 512;
+__device__ inline uint32_t mm_key(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline void mm_take(float v, uint32_t &lo, uint32_t &hi) {
+    if (v == v) {
+        const uint32_t k = mm_key(v);
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+}
+__device__ inline void mm_block(uint32_t &lo, uint32_t &hi) {
+    __shared__ uint32_t slo[4], shi[4];
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t0 = __shfl_xor(lo, o, 64), t1 = __shfl_xor(hi, o, 64);
+        lo = t0 < lo ? t0 : lo;
+        hi = t1 > hi ? t1 : hi;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        slo[w] = lo;
+        shi[w] = hi;
+    }
+    __syncthreads();
+    lo = min(min(slo[0], slo[1]), min(slo[2], slo[3]));
+    hi = max(max(shi[0], shi[1]), max(shi[2], shi[3]));
+}
+struct MMCols {
+    const float *p[64];
+};
+__global__ __launch_bounds__(256) void k_mm_partial(const MMCols cols, uint64_t n, uint32_t *__restrict__ part) {
+    const float *v = cols.p[blockIdx.y];
+    const uint64_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~(uint64_t)3;  // slices keep 16-B alignment
+    const uint64_t a = min(n, (uint64_t)blockIdx.x * per), b = min(n, a + per);
+    uint32_t lo = 0xffffffffu, hi = 0;
+    if ((((uintptr_t)(v + a)) & 15u) == 0) {
+        const uint64_t nq = (b - a) / 4;
+        const float4 *v4 = reinterpret_cast<const float4 *>(v + a);
+        uint64_t q = threadIdx.x;
+        for (; q + 3 * 256 < nq; q += 4 * 256) {
+            float4 t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = v4[q + u * 256];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                mm_take(t[u].x, lo, hi);
+                mm_take(t[u].y, lo, hi);
+                mm_take(t[u].z, lo, hi);
+                mm_take(t[u].w, lo, hi);
+            }
+        }
+        for (; q < nq; q += 256) {
+            const float4 t = v4[q];
+            mm_take(t.x, lo, hi);
+            mm_take(t.y, lo, hi);
+            mm_take(t.z, lo, hi);
+            mm_take(t.w, lo, hi);
+        }
+        for (uint64_t i = a + nq * 4 + threadIdx.x; i < b; i += 256) mm_take(v[i], lo, hi);
+    } else {
+        for (uint64_t i = a + threadIdx.x; i < b; i += 256) mm_take(v[i], lo, hi);
+    }
+    mm_block(lo, hi);
+    if (threadIdx.x == 0) {
+        part[(uint64_t)blockIdx.y * 2 * gridDim.x + blockIdx.x] = lo;
+        part[(uint64_t)blockIdx.y * 2 * gridDim.x + gridDim.x + blockIdx.x] = hi;
+    }
+}
+__global__ __launch_bounds__(256) void k_mm_final(const uint32_t *__restrict__ part, int nb, uint32_t *__restrict__ out) {
+    const uint32_t *p = part + (uint64_t)blockIdx.x * 2 * nb;
+    uint32_t lo = 0xffffffffu, hi = 0;
+    for (int i = threadIdx.x; i < nb; i += 256) {
+        lo = min(lo, p[i]);
+        hi = max(hi, p[nb + i]);
+    }
+    mm_block(lo, hi);
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = lo;
+        out[2 * blockIdx.x + 1] = hi;
+    }
+}
+
 template <typename K>
 void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
                      const std::string &tag, K **out_keys = nullptr, uint32_t **out_vals = nullptr) {
@@ -279,6 +367,17 @@ void radix_sort_u32_inplace_or_swap(st_ctx *c, uint32_t *keys, uint32_t *vals, u
 
 void radix_sort_u64(st_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
     radix_sort_impl<uint64_t>(c, keys, vals, n, b0, b1, tag);
+}
+
+void minmax_keys_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, uint32_t *out) {
+    ST_REQUIRE(ncols >= 1 && ncols <= 64, ST_ERR_ARG, "minmax: 1..64 columns");
+    MMCols mc{};
+    for (int i = 0; i < ncols; ++i) mc.p[i] = cols[i];
+    const unsigned nb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(MM_BLOCKS, (n + 4095) / 4096));
+    auto *part = wsT<uint32_t>(c, "mm.part", (size_t)ncols * 2 * nb);
+    hipLaunchKernelGGL(k_mm_partial, dim3(nb, ncols), dim3(256), 0, c->stream, mc, n, part);
+    hipLaunchKernelGGL(k_mm_final, dim3(ncols), dim3(256), 0, c->stream, part, (int)nb, out);
+    ST_LAUNCH_CHECK();
 }
 
 void iota_u32(st_ctx *c, uint32_t *out, uint64_t n) {

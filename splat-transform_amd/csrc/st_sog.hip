@@ -78,6 +78,12 @@ struct MeansArgs {
     double mn[3], mx[3];
 };
 
+// pos[idx[i]] = i: the texel of each row under the Morton order idx
+__global__ __launch_bounds__(256) void k_invert(const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ pos) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        pos[idx[i]] = (uint32_t)i;
+}
+
 // Texture kernels run in two forms: gather (texel i <- row idx[i], the single-device
 // writeSog) or scatter (local row i -> texel pos[i], one shard of a multi-GPU writeSog)
 __device__ inline void tex_slot(const uint32_t *idx, const uint32_t *pos, uint64_t i, uint32_t &row, uint64_t &o) {
@@ -303,32 +309,34 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     auto *idx = wsT<uint32_t>(c, "sog.idx", n);
     iota_u32(c, idx, n);
     morton_order_dev(c, m[0], m[1], m[2], idx, n);
+    // the texture kernels run in scatter form: row r (read in input order, coalesced) writes
+    // texel pos[r], one 4-byte store, instead of gathering 3-4 values per texel at random
+    auto *pos = wsT<uint32_t>(c, "sog.pos", n);
+    hipLaunchKernelGGL(k_invert, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, idx, n, pos);
+    ST_LAUNCH_CHECK();
     mark(c, "sog.morton");
     const unsigned g = grid_for(n, 256, 8192);
 
     // means (write-sog.ts:161-187)
     auto *mm = wsT<uint32_t>(c, "sog.mm", 6);
-    const uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0};
-    ST_HIP(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_minmax3, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, m[0], m[1], m[2], n, mm);
-    ST_LAUNCH_CHECK();
+    minmax_keys_dev(c, m, 3, n, mm);  // [min, max] keys of x, y, z (NaN skipped)
     uint32_t hmm[6];
     ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     MeansArgs ma{};
     for (int a = 0; a < 3; ++a) {
         ma.c[a] = m[a];
-        const double lo = hmm[a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[a]);
-        const double hi = hmm[3 + a] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[3 + a]);
+        const double lo = hmm[2 * a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[2 * a]);
+        const double hi = hmm[2 * a + 1] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[2 * a + 1]);
         ma.mn[a] = js::log_transform(lo);
         ma.mx[a] = js::log_transform(hi);
         meta->means_min[a] = ma.mn[a];
         meta->means_max[a] = ma.mx[a];
     }
-    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, idx, (const uint32_t *)nullptr, n,
+    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
                        (uint32_t *)out->means_l, (uint32_t *)out->means_u);
-    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13], idx,
-                       (const uint32_t *)nullptr, n, (uint32_t *)out->quats);
+    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13],
+                       (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
     ST_LAUNCH_CHECK();
     mark(c, "sog.means_quats");
 
@@ -339,14 +347,14 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
     hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
-                       (const float *)nullptr, idx, (const uint32_t *)nullptr, n, (uint32_t *)out->scales);
+                       (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
     ST_LAUNCH_CHECK();
     mark(c, "sog.scales");
     // colour + opacity (write-sog.ts:253-268)
     cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9], idx,
-                       (const uint32_t *)nullptr, n, (uint32_t *)out->sh0);
+    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9],
+                       (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
 
@@ -376,8 +384,8 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
         ST_HIP(hipMemsetAsync(out->shn_labels, 0, texels * 4, c->stream));
         hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
                            cl, C, pal, (uint32_t *)out->shn_centroids);
-        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, idx,
-                           (const uint32_t *)nullptr, n, (uint32_t *)out->shn_labels);
+        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, (const uint32_t *)nullptr,
+                           pos, n, (uint32_t *)out->shn_labels);
         ST_LAUNCH_CHECK();
         mark(c, "sog.shn");
     }
