@@ -1,0 +1,158 @@
+"""Edge cases of the HIP path against the pinned CPU restatement (oracle/): degenerate and
+non-finite inputs, ragged sizes around the 256-splat chunk and the 1,024-row tile, and
+the whole writeSog pipeline for every SH band.  Integer / byte / index outputs bit-exact,
+floats bit-exact (NaN as NaN)."""
+import numpy as np
+import pytest
+
+import oracle
+import splat_hip as sh
+from test_oracle_golden import same_bits
+
+pytestmark = pytest.mark.gpu
+
+MEMBERS = ['x', 'y', 'z', 'scale_0', 'scale_1', 'scale_2', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity',
+           'rot_0', 'rot_1', 'rot_2', 'rot_3']
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    import torch  # noqa: F401  (torch's HIP runtime first: see splat_hip.Context)
+    return sh.Context(0)
+
+
+def _table(n, C, seed, spice=False):
+    rng = np.random.default_rng(seed)
+    cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in MEMBERS}
+    for i in range(3):
+        cols[f'scale_{i}'] = (rng.random(n) * 5 - 7).astype(np.float32)
+    for i in range(3 * C):
+        cols[f'f_rest_{i}'] = (rng.normal(0, 0.1, n)).astype(np.float32)
+    if spice and n:
+        # +-Inf / NaN members, scales past the +-20 clamp, zero and negative-dominant quaternions,
+        # SH bytes past both saturation ends, -0
+        k = max(1, n // 50)
+        idx = rng.choice(n, size=min(n, 6 * k), replace=False)
+        a, b, c_, d, e, f = np.array_split(idx, 6)
+        cols['x'][a] = np.inf
+        cols['y'][b] = -np.inf
+        cols['z'][c_] = np.nan
+        cols['scale_0'][d] = 100.0
+        cols['scale_1'][d] = -100.0
+        for i in range(4):
+            cols[f'rot_{i}'][e] = 0.0
+        cols['rot_2'][f] = -5.0
+        cols['opacity'][a] = np.nan
+        cols['f_dc_1'][b] = -0.0
+        if C:
+            cols['f_rest_0'][c_] = 50.0
+            cols['f_rest_1'][d] = -50.0
+            cols['f_rest_2'][e] = np.nan
+    return cols
+
+
+@pytest.mark.parametrize('n', [0, 1, 2, 3, 255, 256, 257, 1023, 1025])
+def test_morton_ragged_vs_oracle(ctx, n):
+    rng = np.random.default_rng(n)
+    x, y, z = (rng.normal(0, 5, n).astype(np.float32) for _ in range(3))
+    same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
+
+
+@pytest.mark.parametrize('case', ['all_equal', 'nan_coords', 'inf_extent', 'one_axis_flat', 'big_equal_run',
+                                  'neg_zero'])
+def test_morton_degenerate_vs_oracle(ctx, case):
+    """ordering.ts:53-65: zero-length extents, non-finite extents (ordering skipped), NaN
+    coordinates (key 0), equal-key runs longer than 256 (recursion with their own extents)."""
+    rng = np.random.default_rng(7)
+    n = 5000
+    x, y, z = (rng.normal(0, 5, n).astype(np.float32) for _ in range(3))
+    if case == 'all_equal':
+        x[:], y[:], z[:] = 1.5, -2.0, 3.25
+    elif case == 'nan_coords':
+        x[rng.random(n) < 0.1] = np.nan
+        z[rng.random(n) < 0.05] = np.nan
+    elif case == 'inf_extent':
+        y[17] = np.inf
+    elif case == 'one_axis_flat':
+        z[:] = 4.0
+    elif case == 'big_equal_run':
+        m = rng.random(n) < 0.4
+        for a in (x, y, z):
+            a[m] = 0.5
+        x[m] += (rng.integers(0, 3, m.sum()) * 1e-6).astype(np.float32)
+    elif case == 'neg_zero':
+        x[::2] = -0.0
+        x[1::2] = 0.0
+    same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
+
+
+@pytest.mark.parametrize('n,C', [(1, 0), (255, 3), (256, 15), (257, 8), (1000, 15), (4097, 3)])
+def test_pack_compressed_edges_vs_oracle(ctx, n, C):
+    """compressed-chunk.ts:44-180: NaN-propagating chunk min/max, the +-20 scale clamp, zero
+    quaternions, the padded last chunk (write-compressed-ply.ts:90-93), SH byte saturation."""
+    cols = _table(n, C, 100 + n, spice=True)
+    order = np.random.default_rng(n).permutation(n).astype(np.uint32)
+    got = ctx.pack_compressed(cols, order, 3 * C)
+    want = oracle.pack_compressed(cols, order, 3 * C)
+    for g, w in zip(got, want):
+        same_bits(np.asarray(g).view(np.uint8), np.asarray(w).view(np.uint8))
+
+
+@pytest.mark.parametrize('kind', ['none', 'all', 'sparse', 'last_row', 'inf_only'])
+def test_filter_finite_edges_vs_oracle(ctx, kind):
+    n = 3001
+    cols = _table(n, 3, 5)
+    names = list(cols)
+    rng = np.random.default_rng(9)
+    if kind == 'all':
+        for r in range(n):
+            cols[names[r % len(names)]][r] = np.nan
+    elif kind == 'sparse':
+        for r in rng.choice(n, 40, replace=False):
+            cols[names[rng.integers(len(names))]][r] = np.nan if r % 2 else -np.inf
+    elif kind == 'last_row':
+        cols['rot_3'][n - 1] = np.inf
+    elif kind == 'inf_only':
+        cols['x'][::7] = np.inf
+    got = ctx.filter_finite(cols)
+    want = oracle.filter_finite([cols[k] for k in names])
+    same_bits(np.asarray(got, np.uint32), np.asarray(want, np.uint32))
+
+
+@pytest.mark.parametrize('action', [('scale', 0.0), ('scale', 1e30), ('translate', (1e38, -1e38, 0.0)),
+                                    ('rotate', (90, 0, 180)), ('rotate', (0.0, 0.0, 0.0))])
+def test_transform_extremes_vs_oracle(ctx, action):
+    """transform.ts:12-65 with a zero / huge scale (log(0) = -inf, overflow), huge
+    translations and exact-angle rotations over NaN / Inf / -0 inputs."""
+    kind, value = action
+    cols = _table(2000, 15, 11, spice=True)
+    ref = {k: v.copy() for k, v in cols.items()}
+    if kind == 'scale':
+        op = oracle.transform_params(s=float(value))
+    elif kind == 'translate':
+        op = oracle.transform_params(t=value)
+    else:
+        op = oracle.transform_params(euler=value)
+    oracle.transform(ref, op, 15)
+    ctx.transform(cols, sh.action_params(kind, value))
+    for k in cols:
+        same_bits(cols[k], ref[k])
+
+
+@pytest.mark.parametrize('C', [0, 3, 8, 15])
+def test_sog_all_bands_vs_oracle(ctx, C):
+    """writeSog (write-sog.ts:110-370) end to end for every SH band: textures, meta and the
+    Math.random draws consumed (paletteSize 4,096 at n = 5,000)."""
+    n = 5000
+    cols = _table(n, C, 40 + C)
+    draws = oracle.mulberry32(C + 1, 1 << 15)
+    tex, meta, used = ctx.sog(cols, 3, draws)
+    rc, otex, ometa, oused = oracle.sog(cols, C, 3, draws)
+    assert rc == 0 and used == oused
+    assert set(tex) == set(otex)
+    for k in tex:
+        same_bits(tex[k], otex[k])
+    for f in ('width', 'height', 'sh_bands', 'palette_size', 'shn_width', 'shn_height'):
+        assert getattr(meta, f) == getattr(ometa, f), f
+    for f in ('means_min', 'means_max', 'scales_codebook', 'sh0_codebook', 'shn_codebook'):
+        same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
