@@ -72,22 +72,24 @@ __global__ void k_ext_init(uint32_t *ext, uint32_t nseg) {
 
 // segmented NaN-ignoring min/max via ordered-int atomics; block-level pre-reduction
 // when the whole block lies in one segment (the level-0 case).
+// single (level 0): one segment, P = identity, S = 0 -- neither is read, and each block
+// leaves its six extents in part[block] (no same-address atomics; k_ext_final reduces)
 __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const float *__restrict__ y,
                                              const float *__restrict__ z, const uint32_t *__restrict__ idx,
                                              const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
-                                             uint64_t total, uint32_t *ext) {
+                                             uint64_t total, int single, uint32_t *ext, uint32_t *part) {
     __shared__ uint32_t red[6][4];
     const uint64_t base = (uint64_t)blockIdx.x * 4096;
     if (base >= total) return;
     const uint64_t last = (base + 4096 < total ? base + 4096 : total) - 1;
-    const bool one_seg = S[base] == S[last];
+    const bool one_seg = single || S[base] == S[last];
     const float *cols[3] = {x, y, z};
     uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
     for (int r = 0; r < 16; ++r) {
         const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
         if (j > last) break;
-        const uint32_t row = idx[P[j]];
-        const uint32_t s = S[j];
+        const uint32_t row = single ? idx[j] : idx[P[j]];
+        const uint32_t s = single ? 0u : S[j];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             const float v = cols[a][row];
@@ -123,9 +125,41 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
         const int q = threadIdx.x;
         uint32_t v = red[q][0];
         for (int i = 1; i < 4; ++i) v = q < 3 ? (red[q][i] < v ? red[q][i] : v) : (red[q][i] > v ? red[q][i] : v);
+        if (single) {
+            part[(uint64_t)blockIdx.x * 6 + q] = v;
+            return;
+        }
         const uint32_t s = S[base];
         if (q < 3) atomicMin(&ext[s * 6 + q], v);
         else atomicMax(&ext[s * 6 + q], v);
+    }
+}
+
+// level 0: the six extents from the per-block partials
+__global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ part, uint32_t nb, uint32_t *ext) {
+    __shared__ uint32_t red[6][4];
+    uint32_t v[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    for (uint32_t b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const uint32_t t = part[(uint64_t)b * 6 + q];
+            v[q] = q < 3 ? (t < v[q] ? t : v[q]) : (t > v[q] ? t : v[q]);
+        }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t t = __shfl_xor(v[q], o, 64);
+            v[q] = q < 3 ? (t < v[q] ? t : v[q]) : (t > v[q] ? t : v[q]);
+        }
+        if (lane == 0) red[q][w] = v[q];
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int q = threadIdx.x;
+        uint32_t r = red[q][0];
+        for (int i = 1; i < 4; ++i) r = q < 3 ? (red[q][i] < r ? red[q][i] : r) : (red[q][i] > r ? red[q][i] : r);
+        ext[q] = r;
     }
 }
 
@@ -191,48 +225,49 @@ __global__ __launch_bounds__(256) void k_scatter_back(const uint32_t *__restrict
         idx[single ? (uint32_t)j : P[j]] = vals[j];
 }
 
-// run starts: flag[j] = 1 if j starts a run of equal keys
-template <typename K>
-__global__ __launch_bounds__(256) void k_run_flags(const K *__restrict__ keys, uint64_t total,
-                                                   uint32_t *__restrict__ flag) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride)
-        flag[j] = (j == 0 || keys[j] != keys[j - 1]) ? 1u : 0u;
-}
 
-__global__ __launch_bounds__(256) void k_run_starts(const uint32_t *__restrict__ flag,
-                                                    const uint32_t *__restrict__ rid, uint64_t total,
-                                                    uint32_t *__restrict__ run_start) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride)
-        if (flag[j]) run_start[rid[j]] = (uint32_t)j;
-}
 
-// big runs of sortable segments -> flag; run_start[nruns] == total sentinel
-template <typename K>
-__global__ __launch_bounds__(256) void k_big_runs(const uint32_t *__restrict__ run_start, uint32_t nruns,
-                                                  const K *__restrict__ keys, const SegInfo *__restrict__ info,
-                                                  uint32_t *__restrict__ big) {
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += gridDim.x * blockDim.x) {
-        const uint32_t len = run_start[r + 1] - run_start[r];
-        const uint32_t s = (uint32_t)(keys[run_start[r]] >> 30);
-        big[r] = (len > 256 && info[s].ok) ? 1u : 0u;
-    }
-}
 
-__global__ __launch_bounds__(256) void k_emit_segs(const uint32_t *__restrict__ run_start, uint32_t nruns,
-                                                   const uint32_t *__restrict__ big, const uint32_t *__restrict__ bpos,
-                                                   const uint32_t *__restrict__ P, int single,
-                                                   uint32_t *__restrict__ nstart, uint32_t *__restrict__ nlen) {
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += gridDim.x * blockDim.x) {
-        if (!big[r]) continue;
-        const uint32_t j = run_start[r];
-        nstart[bpos[r]] = single ? j : P[j];
-        nlen[bpos[r]] = run_start[r + 1] - j;
-    }
-}
 
 __global__ void k_set_sentinel(uint32_t *a, uint32_t i, uint32_t v) { a[i] = v; }
+
+// Runs of equal keys longer than 256 (ordering.ts:90-104) without listing every run: j
+// starts such a run iff it starts a run and keys[j + 256] == keys[j] (the keys are sorted).
+// Their order in the next level's segment list is immaterial: a segment's rows go back to
+// their own positions.  Few runs qualify, so they are appended with an atomic.
+template <typename K>
+__global__ __launch_bounds__(256) void k_big_starts(const K *__restrict__ keys, uint64_t total,
+                                                    const SegInfo *__restrict__ info, uint32_t *__restrict__ starts,
+                                                    uint32_t *__restrict__ count) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j + 256 < total; j += stride) {
+        const K k = keys[j];
+        if (keys[j + 256] == k && (j == 0 || keys[j - 1] != k) && info[(uint32_t)(k >> 30)].ok)
+            starts[atomicAdd(count, 1u)] = (uint32_t)j;
+    }
+}
+
+// end of each big run by binary search (first position past j whose key differs), then the
+// next level's segment (start position in idx, length)
+template <typename K>
+__global__ __launch_bounds__(256) void k_big_segs(const K *__restrict__ keys, uint64_t total,
+                                                  const uint32_t *__restrict__ starts, const uint32_t *__restrict__ count,
+                                                  const uint32_t *__restrict__ P, int single,
+                                                  uint32_t *__restrict__ nstart, uint32_t *__restrict__ nlen) {
+    const uint32_t nb = *count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+        const uint32_t j = starts[i];
+        const K k = keys[j];
+        uint64_t lo = (uint64_t)j + 257, hi = total;  // keys[j + 256] == k
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (keys[mid] == k) lo = mid + 1;
+            else hi = mid;
+        }
+        nstart[i] = single ? j : P[j];
+        nlen[i] = (uint32_t)(lo - j);
+    }
+}
 
 }  // namespace
 
@@ -256,9 +291,9 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
     uint64_t total = n;
     auto *P = wsT<uint32_t>(c, "mo.P", n);
     auto *S = wsT<uint32_t>(c, "mo.S", n);
-    auto *flag = wsT<uint32_t>(c, "mo.flag", n + 1);
-    auto *rid = wsT<uint32_t>(c, "mo.rid", n + 1);
     auto *vals = wsT<uint32_t>(c, "mo.vals", n);
+    auto *bigpos = wsT<uint32_t>(c, "mo.bigpos", n / 257 + 2);  // starts of runs longer than 256
+    auto *bigcnt = wsT<uint32_t>(c, "mo.bigcnt", 1);
     for (int level = 0; nseg > 0; ++level) {
         const bool single = (level == 0);
         if (!single) {
@@ -269,16 +304,19 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_expand, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, seg_start, seg_off,
                                nseg, total, P, S);
             ST_LAUNCH_CHECK();
-        } else {
-            // level 0: P = identity, S = 0 (only k_ext reads them)
-            iota_u32(c, P, n);
-            ST_HIP(hipMemsetAsync(S, 0, n * sizeof(uint32_t), c->stream));
-        }
+        }  // level 0: P = identity, S = 0, never materialised
         auto *ext = wsT<uint32_t>(c, "mo.ext", (size_t)nseg * 6);
         auto *info = static_cast<SegInfo *>(ws(c, "mo.info", sizeof(SegInfo) * (size_t)nseg));
-        hipLaunchKernelGGL(k_ext_init, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
-        hipLaunchKernelGGL(k_ext, dim3((unsigned)((total + 4095) / 4096)), dim3(256), 0, c->stream, x, y, z, idx, P, S,
-                           total, ext);
+        const unsigned eb = (unsigned)((total + 4095) / 4096);
+        if (single) {
+            auto *part = wsT<uint32_t>(c, "mo.extpart", (size_t)eb * 6);
+            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, 1, ext, part);
+            hipLaunchKernelGGL(k_ext_final, dim3(1), dim3(256), 0, c->stream, part, eb, ext);
+        } else {
+            hipLaunchKernelGGL(k_ext_init, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
+            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, 0, ext,
+                               (uint32_t *)nullptr);
+        }
         ST_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx, seg_start,
                            ext, nseg, info);
@@ -286,33 +324,21 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         int seg_bits = 0;
         while ((1u << seg_bits) < nseg) ++seg_bits;
         const unsigned g = grid_for(total, 256, 8192);
-        uint32_t nruns;
         if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
             hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
                                (int)single, keys, vals);
             ST_LAUNCH_CHECK();
-            radix_sort_u32(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs32");
-            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, (int)single, idx);
-            hipLaunchKernelGGL(k_run_flags<uint32_t>, dim3(g), dim3(256), 0, c->stream, keys, total, flag);
+            uint32_t *skeys = keys, *svals = vals;
+            radix_sort_u32_inplace_or_swap(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs32", &skeys, &svals);
+            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, svals, total, (int)single, idx);
+            ST_HIP(hipMemsetAsync(bigcnt, 0, 4, c->stream));
+            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, skeys, total, info, bigpos,
+                               bigcnt);
+            hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
+                               c->stream, skeys, total, bigpos, bigcnt, P, (int)single, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
-            scan_u32(c, flag, rid, total, rid + total);
-            ST_HIP(hipMemcpyAsync(h, rid + total, 4, hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipStreamSynchronize(c->stream));
-            nruns = h[0];
-            auto *run_start = wsT<uint32_t>(c, "mo.run_start", (size_t)nruns + 1);
-            hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, c->stream, flag, rid, total, run_start);
-            hipLaunchKernelGGL(k_set_sentinel, dim3(1), dim3(1), 0, c->stream, run_start, nruns, (uint32_t)total);
-            auto *big = wsT<uint32_t>(c, "mo.big", (size_t)nruns + 1);
-            hipLaunchKernelGGL(k_big_runs<uint32_t>, dim3(grid_for(nruns, 256, 8192)), dim3(256), 0, c->stream,
-                               run_start, nruns, keys, info, big);
-            ST_LAUNCH_CHECK();
-            auto *bpos = wsT<uint32_t>(c, "mo.bpos", (size_t)nruns + 1);
-            scan_u32(c, big, bpos, nruns, bpos + nruns);
-            hipLaunchKernelGGL(k_emit_segs, dim3(grid_for(nruns, 256, 8192)), dim3(256), 0, c->stream, run_start,
-                               nruns, big, bpos, P, (int)single, nseg_start, nseg_len);
-            ST_LAUNCH_CHECK();
-            ST_HIP(hipMemcpyAsync(h, bpos + nruns, 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else {
             auto *keys = wsT<uint64_t>(c, "mo.k64", total + 1);
             hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
@@ -320,25 +346,13 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_LAUNCH_CHECK();
             radix_sort_u64(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs64");
             hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, (int)single, idx);
-            hipLaunchKernelGGL(k_run_flags<uint64_t>, dim3(g), dim3(256), 0, c->stream, keys, total, flag);
+            ST_HIP(hipMemsetAsync(bigcnt, 0, 4, c->stream));
+            hipLaunchKernelGGL(k_big_starts<uint64_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
+                               bigcnt);
+            hipLaunchKernelGGL(k_big_segs<uint64_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
+                               c->stream, keys, total, bigpos, bigcnt, P, (int)single, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
-            scan_u32(c, flag, rid, total, rid + total);
-            ST_HIP(hipMemcpyAsync(h, rid + total, 4, hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipStreamSynchronize(c->stream));
-            nruns = h[0];
-            auto *run_start = wsT<uint32_t>(c, "mo.run_start", (size_t)nruns + 1);
-            hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, c->stream, flag, rid, total, run_start);
-            hipLaunchKernelGGL(k_set_sentinel, dim3(1), dim3(1), 0, c->stream, run_start, nruns, (uint32_t)total);
-            auto *big = wsT<uint32_t>(c, "mo.big", (size_t)nruns + 1);
-            hipLaunchKernelGGL(k_big_runs<uint64_t>, dim3(grid_for(nruns, 256, 8192)), dim3(256), 0, c->stream,
-                               run_start, nruns, keys, info, big);
-            ST_LAUNCH_CHECK();
-            auto *bpos = wsT<uint32_t>(c, "mo.bpos", (size_t)nruns + 1);
-            scan_u32(c, big, bpos, nruns, bpos + nruns);
-            hipLaunchKernelGGL(k_emit_segs, dim3(grid_for(nruns, 256, 8192)), dim3(256), 0, c->stream, run_start,
-                               nruns, big, bpos, P, (int)single, nseg_start, nseg_len);
-            ST_LAUNCH_CHECK();
-            ST_HIP(hipMemcpyAsync(h, bpos + nruns, 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         }
         ST_HIP(hipStreamSynchronize(c->stream));
         nseg = h[0];
