@@ -186,28 +186,36 @@ __global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
     const bool real = j < num;
     const uint32_t row = a.order[base + (real ? j : num - 1)];
     const float4 *r4 = reinterpret_cast<const float4 *>(a.rows + (uint64_t)row * a.rl);
+    // both gathered rows are requested before anything waits on them (the padded lanes
+    // read the chunk's last row, always in bounds)
+    float4 mv[4];
+    uint4 sv[SHB / 16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mv[q] = r4[q];
+    if (a.nsh) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.shrows + (uint64_t)row * SHB);
+#pragma unroll
+        for (int q = 0; q < SHB / 16; ++q) sv[q] = src[q];
+    }
     float d[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const float4 v = r4[q];
-        d[4 * q] = v.x;
-        d[4 * q + 1] = v.y;
-        d[4 * q + 2] = v.z;
-        d[4 * q + 3] = v.w;
+        d[4 * q] = mv[q].x;
+        d[4 * q + 1] = mv[q].y;
+        d[4 * q + 2] = mv[q].z;
+        d[4 * q + 3] = mv[q].w;
     }
     // 8-bit SH (write-compressed-ply.ts:83-87), staged in LDS for coalesced stores
     if (a.nsh) {
         uint8_t *stage = reinterpret_cast<uint8_t *>(sh_stage);
         if (real) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(a.shrows + (uint64_t)row * SHB);
             uint32_t w[SHB / 4];
 #pragma unroll
             for (int q = 0; q < SHB / 16; ++q) {
-                const uint4 v = src[q];
-                w[4 * q] = v.x;
-                w[4 * q + 1] = v.y;
-                w[4 * q + 2] = v.z;
-                w[4 * q + 3] = v.w;
+                w[4 * q] = sv[q].x;
+                w[4 * q + 1] = sv[q].y;
+                w[4 * q + 2] = sv[q].z;
+                w[4 * q + 3] = sv[q].w;
             }
             for (int k = 0; k < a.nsh; ++k) stage[j * a.nsh + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
         }

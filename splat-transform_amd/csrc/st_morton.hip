@@ -85,14 +85,27 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
     const bool one_seg = single || S[base] == S[last];
     const float *cols[3] = {x, y, z};
     uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    // all 16 rows' indices, then all their coordinates, in flight before the first test
+    uint32_t rows_[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
+        const uint64_t jj = j > last ? last : j;
+        rows_[r] = single ? idx[jj] : idx[P[jj]];
+    }
+    float vals_[16][3];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) vals_[r][a] = cols[a][rows_[r]];
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
         if (j > last) break;
-        const uint32_t row = single ? idx[j] : idx[P[j]];
         const uint32_t s = single ? 0u : S[j];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float v = cols[a][row];
+            const float v = vals_[r][a];
             if (v == v) {
                 const uint32_t k = fkey(v);
                 if (one_seg) {
