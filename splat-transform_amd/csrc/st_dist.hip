@@ -29,30 +29,6 @@ namespace {
 
 using namespace km;
 
-// NaN-ignoring per-column min/max as ordered keys
-__global__ __launch_bounds__(256) void k_minmax_cols(const float *const *cols, int ncols, uint64_t n, uint32_t *mm) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (int a = 0; a < ncols; ++a) {
-        uint32_t lo = 0xffffffffu, hi = 0;
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-            const float v = cols[a][i];
-            if (v == v) {
-                const uint32_t k = fkey_(v);
-                lo = k < lo ? k : lo;
-                hi = k > hi ? k : hi;
-            }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t t0 = __shfl_xor(lo, o, 64), t1 = __shfl_xor(hi, o, 64);
-            lo = t0 < lo ? t0 : lo;
-            hi = t1 > hi ? t1 : hi;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&mm[2 * a], lo);
-            atomicMax(&mm[2 * a + 1], hi);
-        }
-    }
-}
 
 // sort key of point i: (segment, label)
 __global__ __launch_bounds__(256) void k_seg_keys(const uint32_t *labels, uint64_t n, uint64_t seg_len, int k,

@@ -98,24 +98,7 @@ __global__ __launch_bounds__(256) void k_scan_cols(const ScanCols cp, int d, uin
     }
 }
 
-// initializeCentroids1D (k-means.ts:23-39)
-__global__ __launch_bounds__(256) void k_minmax1d(const float *v, uint64_t n, uint32_t *mm) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    float lo = __builtin_inff(), hi = -__builtin_inff();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        lo = fminf(lo, v[i]);
-        hi = fmaxf(hi, v[i]);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, o, 64));
-        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(&mm[0], fkey_(lo));
-        atomicMax(&mm[1], fkey_(hi));
-    }
-}
-
+// initializeCentroids1D (k-means.ts:23-39): linspace over [min, max] (keys from minmax_keys_dev)
 __global__ void k_init1d(const uint32_t *mm, float *cen, int k) {
     const double m = fkey_inv_(mm[0]), M = fkey_inv_(mm[1]);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x)

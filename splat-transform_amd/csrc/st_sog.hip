@@ -43,35 +43,6 @@ __global__ __launch_bounds__(256) void k_remap_labels(const uint32_t *lab, const
         out[i] = (uint8_t)inv[lab[i]];
 }
 
-// NaN-ignoring min/max (write-sog.ts:15-31: `if (value < min)` skips NaN)
-__global__ __launch_bounds__(256) void k_minmax3(const float *x, const float *y, const float *z, uint64_t n,
-                                                 uint32_t *mm) {
-    const float *c[3] = {x, y, z};
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0, 0, 0};
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = c[a][i];
-            if (v == v) {
-                const uint32_t k = fkey_(v);
-                lo[a] = k < lo[a] ? k : lo[a];
-                hi[a] = k > hi[a] ? k : hi[a];
-            }
-        }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t t0 = __shfl_xor(lo[a], o, 64), t1 = __shfl_xor(hi[a], o, 64);
-            lo[a] = t0 < lo[a] ? t0 : lo[a];
-            hi[a] = t1 > hi[a] ? t1 : hi[a];
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&mm[a], lo[a]);
-            atomicMax(&mm[3 + a], hi[a]);
-        }
-    }
-}
 
 struct MeansArgs {
     const float *c[3];
