@@ -244,7 +244,10 @@ class Context:
         # live in one process, torch's must initialise first (the other order leaves torch
         # without a device).  Device tensors are still shared through plain pointers.
         if 'torch' in sys.modules:
-            sys.modules['torch'].cuda.init()
+            try:
+                sys.modules['torch'].cuda.init()
+            except RuntimeError:
+                pass  # no device: st_ctx_create reports it
         self.h = ctypes.c_void_p()
         check(lib().st_ctx_create(ctypes.c_int32(device), ctypes.byref(self.h)))
 
