@@ -169,8 +169,11 @@ __global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict
     auto val = [&](uint32_t pos) -> float { return sv[pos]; };
     auto idx = [&](uint32_t pos) -> uint32_t { return si[pos]; };
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const float pf = pts[i];
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float pnext = i < n ? pts[i] : 0.f;  // the next point's value is in flight while this one is placed
+    for (; i < n; i += stride) {
+        const float pf = pnext;
+        if (i + stride < n) pnext = pts[i + stride];
         const double p = pf;
         const int g = cell(pf);
         int u = (int)first[g];
@@ -573,22 +576,34 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
                                                   const int32_t *__restrict__ emin_c, const double *__restrict__ sabs_c,
                                                   const __int128 *__restrict__ total, const __int128 *__restrict__ cand_all,
                                                   float *__restrict__ cen) {
-    const int cl = blockIdx.x * 64 + threadIdx.x;
-    if (cl >= k || seq_flag[cl] != 1u) return;
+    // one workgroup per cluster: the wave stages the candidates in LDS 256 at a time, lane 0
+    // replays them (the chain is sequential; its loads need not be)
+    const int cl = blockIdx.x;
+    if (cl >= k || seq_flag[cl] != 1u) return;  // uniform per workgroup
+    __shared__ __int128 buf[256];
     const int e_lo = emin_c[cl];
     const __int128 margin = rp_margin(sabs_c[cl], e_lo);
     const uint32_t ctot = ctot_c[cl];
     const __int128 *cand = cand_all + (uint64_t)cl * CAND_MAX;
     __int128 sv = 0, Pprev = 0;
     bool ok = true;
-    for (uint32_t i = 0; i < ctot; ++i) {
-        const __int128 Pc = cand[i];
-        const __int128 V = sv + (Pc - Pprev);
-        sv = f64_representable(V) ? V : f64_units(f64_round(V, e_lo), e_lo);
-        Pprev = Pc;
-        const __int128 dev = sv - Pc;
-        ok = ok && (dev < 0 ? -dev : dev) < margin;
+    for (uint32_t b = 0; b < ctot; b += 256) {
+        const uint32_t m = min(256u, ctot - b);
+        for (uint32_t i = threadIdx.x; i < m; i += 64) buf[i] = cand[b + i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t i = 0; i < m; ++i) {
+                const __int128 Pc = buf[i];
+                const __int128 V = sv + (Pc - Pprev);
+                sv = f64_representable(V) ? V : f64_units(f64_round(V, e_lo), e_lo);
+                Pprev = Pc;
+                const __int128 dev = sv - Pc;
+                ok = ok && (dev < 0 ? -dev : dev) < margin;
+            }
+        }
+        __syncthreads();
     }
+    if (threadIdx.x != 0) return;
     const __int128 fin = sv + (total[cl] - Pprev);
     if (!ok || !f64_representable(fin)) {
         seq_flag[cl] = 2u;
@@ -696,7 +711,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                                    rp_cof, rp_ctot);
                 hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks,
                                    ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_cof, cand_buf);
-                hipLaunchKernelGGL(k_rp_finish, dim3((k + 63) / 64), dim3(64), 0, c->stream, start, rp_ctot, k,
+                hipLaunchKernelGGL(k_rp_finish, dim3(k), dim3(64), 0, c->stream, start, rp_ctot, k,
                                    seq_flag, emin_c, sabs_c, rp_total, cand_buf, cen);
                 ST_LAUNCH_CHECK();
             } else {
