@@ -283,12 +283,16 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
     for _ in range(iters):
         ops.assign(P.pts, k, cen, labels)
         sums, sabs, emin, counts = ops.partials(P.pts, P.nseg, k, labels)
-        S, A = sums.sum(0), sabs.sum(0)
-        E, C = emin.min(0).values.contiguous(), counts.sum(0, dtype=torch.int32)
-        comm.allreduce(S)
-        comm.allreduce(A)
+        # one SUM allreduce for the f64 sums, sum|x| and the counts (exact in f64 below 2^53),
+        # one MIN allreduce for the ulp exponents
+        SAC = torch.cat([sums.sum(0).reshape(-1), sabs.sum(0).reshape(-1),
+                         counts.sum(0, dtype=torch.float64).reshape(-1)])
+        E = emin.min(0).values.contiguous()
+        comm.allreduce(SAC)
         comm.allreduce(E, dist.ReduceOp.MIN)
-        comm.allreduce(C)
+        S = SAC[:d * k].reshape(d, k)
+        A = SAC[d * k:2 * d * k].reshape(d, k)
+        C = SAC[2 * d * k:].to(torch.int32)
         pending = ops.finish(d, k, S, A, E, C, cen)
         if pending.numel():
             running = ops.zeros((pending.numel(),), torch.float64)
