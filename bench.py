@@ -49,6 +49,7 @@ def parse():
     ap.add_argument('--cpu-assign-sample', type=int, default=1000)
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
+    ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')
     return ap.parse_args()
 
 
@@ -316,6 +317,13 @@ def main():
     e2e = None
     if world == 1 and not args.no_e2e:
         e2e = end_to_end(ctx, cols, args.iters, draws, tex, ref_archive)
+    paths = None
+    if world == 1 and not args.no_paths:
+        # BASELINE config 3 (-r 0,45,0, filterNaN, Morton, chunk pack -> .compressed.ply) on its own
+        # 10M SH-3 table: each HBM-bound stage priced by its algorithmic bytes (tools/bench_paths.py)
+        sys.path.insert(0, os.path.join(ROOT, 'tools'))
+        import bench_paths
+        paths = bench_paths.measure(ctx, stream, dev, n=10_000_000, reps=5)
     cpu, cpu_all = (None, None) if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
@@ -367,6 +375,7 @@ def main():
             'end_to_end_Msplats_per_s': (n * world) / (elapsed / args.steps + container_ms / 1e3) / 1e6,
         },
         'end_to_end_file': e2e,
+        'paths_config3': paths,
         'stages_ms': stages,
         'kernels': kstats,
         'draws_used_per_step': used,

@@ -31,6 +31,15 @@ def main(n=10_000_000, reps=5):
     torch.cuda.set_stream(stream)
     ctx = sh.Context(0)
     ctx.set_stream(stream.cuda_stream)
+    out = measure(ctx, stream, dev, n, reps)
+    os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+    with open(os.path.join(ROOT, 'gpurun_out', 'paths.json'), 'w') as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+def measure(ctx, stream, dev, n=10_000_000, reps=5):
+    """the stage table and the whole config-3 pipeline; ctx runs on `stream`"""
     g = torch.Generator(device=dev)
     g.manual_seed(1003)
     names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
@@ -97,10 +106,7 @@ def main(n=10_000_000, reps=5):
         ctx.dev_pack_compressed(pack_cols, order, chunk, vertex, shb)
     ms = timed(pipeline)
     out['config3'] = {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'kept': m}
-    os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
-    with open(os.path.join(ROOT, 'gpurun_out', 'paths.json'), 'w') as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == '__main__':
