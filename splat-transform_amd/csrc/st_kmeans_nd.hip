@@ -124,7 +124,17 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
     const uint64_t p0 = (uint64_t)blockIdx.x * PF_PTS;
     const int j = threadIdx.x;
     const bool valid = p0 + j < n;
-    for (int k = 0; k < d; ++k) x[k * PF_LDS_LD + j] = valid ? cols[k][p0 + j] : 0.0f;
+    const uint64_t pj = valid ? p0 + j : n - 1;  // loads stay in bounds without a branch
+    // batches of 8 columns: the loads of a batch are in flight together
+    int k0 = 0;
+    for (; k0 + 8 <= d; k0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = cols[k0 + u][pj];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[(k0 + u) * PF_LDS_LD + j] = valid ? v[u] : 0.0f;
+    }
+    for (; k0 < d; ++k0) x[k0 * PF_LDS_LD + j] = valid ? cols[k0][pj] : 0.0f;
     __syncthreads();
     if (valid) {
         double nn = 0;
