@@ -89,6 +89,26 @@ __device__ inline float wbound(const Bound &B, float pn, float cm) {
     return (2.0f * e + 2.0f * B.rel * s * s) * 1.0001f;
 }
 
+// the same window with the best row's error bounded by its own tile-half's largest norm cb
+// (<= cm): the rows that can beat it are bounded by cm, the best row itself by cb
+__device__ inline float wbound2(const Bound &B, float pn, float cb, float cm) {
+    const float e1 = B.a * pn * cb + B.b * cb * cb + B.ec * (pn + cb) + B.ep;
+    const float e2 = B.a * pn * cm + B.b * cm * cm + B.ec * (pn + cm) + B.ep;
+    const float s = pn + cm;
+    return (e1 + e2 + 2.0f * B.rel * s * s) * 1.0001f;
+}
+
+// largest norm (rounded up) among the 16 rows of each tile-half
+__global__ __launch_bounds__(256) void k_half_max(const float *__restrict__ cnorm, uint32_t nhalves,
+                                                  float *__restrict__ chalf) {
+    for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nhalves; h += gridDim.x * blockDim.x) {
+        float m = 0.f;
+        for (int rr = 0; rr < 16; ++rr)
+            m = fmaxf(m, cnorm[(h >> 1) * 32 + 4 * (h & 1) + (rr & 3) + 8 * (rr >> 2)]);
+        chalf[h] = m;
+    }
+}
+
 // does v_mfma_f32_32x32x16_f16 keep fp16 denormal inputs?
 __global__ void k_probe_denorm(float *out) {
     const int lane = threadIdx.x;
@@ -190,7 +210,7 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
 // one thread per centroid row; rows >= k can never win
 __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
                                                         float sigma, uint4 *cfrag, uint32_t *cmax_bits, float *caos,
-                                                        float2 *cfix) {
+                                                        float2 *cfix, float *cnorm) {
     const uint32_t total = ctiles * 32;
     const int ld = aos_ld(d);
     float mymax = 0.f;
@@ -219,8 +239,11 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
             n2 = h_bits((float)r1);
             const double r2 = r1 - (double)h_val(n2);
             n3 = h_bits((float)r2);
-            mymax = fmaxf(mymax, (float)(__builtin_sqrt(nn) * (1.0 + 1e-6)));
+            const float nr = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+            mymax = fmaxf(mymax, nr);
+            cnorm[r] = nr;
         } else {
+            cnorm[r] = 0.0f;  // padding row: never the best
             n1 = h_bits(60000.0f);  // padding: score ~6e4 >> any real score (< 200)
             n2 = n3 = 0;
         }
@@ -263,6 +286,7 @@ template <int KS, int MODE>
 __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
                                                const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
+                                               const float *__restrict__ chalf,
                                                const Bound bnd, uint32_t *__restrict__ labels,
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
@@ -443,7 +467,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
         bool is_amb = false, is_pair = false;
         if (h == 0 && p < npts) {
-            const float W = wbound(bnd, pnorm[p], cm);
+            const float W = wbound2(bnd, pnorm[p], chalf[code1], cm);
             if (nm2 > nm1 + W) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
             } else if (nm3 > nm1 + W) {
@@ -947,13 +971,13 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
 template <int KS>
 struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
-                     const float *pnorm, const uint32_t *cmax, const Bound &bnd, uint32_t *labels, float *thr,
-                     uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
+                     const float *pnorm, const uint32_t *cmax, const float *chalf, const Bound &bnd,
+                     uint32_t *labels, float *thr, uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
         const uint32_t per_block = NW * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(WG), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
-                           cmax, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
+                           cmax, chalf, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
                            pair_codes);
         ST_LAUNCH_CHECK();
     }
@@ -966,7 +990,8 @@ struct Sweep {
         const dim3 grid(blocks, split);
         KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
-                           (const float *)nullptr, (const uint32_t *)nullptr, bnd, (uint32_t *)nullptr, thr_slot,
+                           (const float *)nullptr, (const uint32_t *)nullptr, (const float *)nullptr, bnd,
+                           (uint32_t *)nullptr, thr_slot,
                            (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
                            (uint2 *)nullptr);
         ST_LAUNCH_CHECK();
@@ -1054,14 +1079,18 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     ST_HIP(hipMemsetAsync(scal + 1, 0, 4, c->stream));
     auto *caos = wsT<float>(c, "kn.caos", (size_t)k * aos_ld(d));
     auto *cfix = wsT<float2>(c, "kn.cfix", (size_t)ctiles * 32 * (aos_ld(d) / 2));
+    auto *cnorm = wsT<float>(c, "kn.cnorm", (size_t)ctiles * 32);
+    auto *chalf = wsT<float>(c, "kn.chalf", (size_t)ctiles * 2);
     hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
-                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix);
+                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix, cnorm);
+    hipLaunchKernelGGL(k_half_max, dim3(grid_for((uint64_t)ctiles * 2, 256, 1024)), dim3(256), 0, c->stream, cnorm,
+                       ctiles * 2, chalf);
     ST_LAUNCH_CHECK();
     auto *pair_pts = wsT<uint32_t>(c, "kn.pairpts", n);
     auto *pair_codes = wsT<uint2>(c, "kn.paircodes", n);
     ST_HIP(hipMemsetAsync(&dstate->amb, 0, 16, c->stream));  // amb + ties + overflow + pairs
-    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, bnd, labels,
-                                        thr, amb, dstate, pair_pts, pair_codes)));
+    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, chalf, bnd,
+                                        labels, thr, amb, dstate, pair_pts, pair_codes)));
     const uint32_t ncodes = ctiles * 2;
     const int ld = aos_ld(d);
     if (ncodes <= (uint32_t)FB_MAX_CODES && (ld == 48 || ld == 24 || ld == 12) && !getenv("ST_FIXROW_L2")) {
