@@ -51,6 +51,7 @@ __device__ inline void static_for(F &&f) {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int PT = 4;          // point tiles per wave
 constexpr int NW = 4;          // waves per workgroup (they share the LDS centroid stages)
@@ -832,19 +833,18 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
             const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn * LD) + sq;
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt) : "v"(src) : "memory");
         }
-        float s0 = 0.f, s1 = 0.f;  // two chains: the screen bound holds for any summation order
+        // differences by DPP-broadcast subtracts (v_sub_f32_dpp), squares accumulated in pairs
+        // (v_pk_fma_f32): four chains, the screen bound holds for any summation order
+        f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
         static_for<LD / 4>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            float v = row_bcast<q>(cur.x) - row[q].x;
-            s0 = __builtin_fmaf(v, v, s0);
-            v = row_bcast<q>(cur.y) - row[q].y;
-            s1 = __builtin_fmaf(v, v, s1);
-            v = row_bcast<q>(cur.z) - row[q].z;
-            s0 = __builtin_fmaf(v, v, s0);
-            v = row_bcast<q>(cur.w) - row[q].w;
-            s1 = __builtin_fmaf(v, v, s1);
+            const f32x2 t01 = {row_bcast<q>(cur.x) - row[q].x, row_bcast<q>(cur.y) - row[q].y};
+            const f32x2 t23 = {row_bcast<q>(cur.z) - row[q].z, row_bcast<q>(cur.w) - row[q].w};
+            a01 = __builtin_elementwise_fma(t01, t01, a01);
+            a23 = __builtin_elementwise_fma(t23, t23, a23);
         });
-        fix_decide<16>(s0 + s1, valid, c, d, caos, aos + (uint64_t)p * LD, p, rr, labels, ties, st);
+        fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos, aos + (uint64_t)p * LD, p, rr, labels,
+                       ties, st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cur = nxt;
         p = pn;
@@ -871,20 +871,17 @@ __global__ __launch_bounds__(256) void k_fixpair_b(const float *__restrict__ aos
     const bool valid = c < (uint32_t)k;
     const float4 pv = reinterpret_cast<const float4 *>(aos + (uint64_t)p * LD)[rr % (LD / 4)];
     const float2 *crow = cfix + (uint64_t)(code >> 1) * 2 * (LD / 2) * 16 + (uint64_t)(code & 1) * (LD / 2) * 16 + rr;
-    float s0 = 0.f, s1 = 0.f;
+    f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};  // DPP subtracts, packed FMAs (as k_fixrow_b)
     static_for<LD / 4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         const float2 c0 = crow[(2 * q) * 16], c1 = crow[(2 * q + 1) * 16];
-        float v = row_bcast<q>(pv.x) - c0.x;
-        s0 = __builtin_fmaf(v, v, s0);
-        v = row_bcast<q>(pv.y) - c0.y;
-        s1 = __builtin_fmaf(v, v, s1);
-        v = row_bcast<q>(pv.z) - c1.x;
-        s0 = __builtin_fmaf(v, v, s0);
-        v = row_bcast<q>(pv.w) - c1.y;
-        s1 = __builtin_fmaf(v, v, s1);
+        const f32x2 t01 = {row_bcast<q>(pv.x) - c0.x, row_bcast<q>(pv.y) - c0.y};
+        const f32x2 t23 = {row_bcast<q>(pv.z) - c1.x, row_bcast<q>(pv.w) - c1.y};
+        a01 = __builtin_elementwise_fma(t01, t01, a01);
+        a23 = __builtin_elementwise_fma(t23, t23, a23);
     });
-    fix_decide<32>(valid ? s0 + s1 : 0.f, valid, c, d, caos, aos + (uint64_t)p * LD, p, r, labels, ties, st);
+    const float s = (a01.x + a01.y) + (a23.x + a23.y);
+    fix_decide<32>(valid ? s : 0.f, valid, c, d, caos, aos + (uint64_t)p * LD, p, r, labels, ties, st);
 }
 
 // one wave per ambiguous point: exact distances over its candidates (or all K on overflow)

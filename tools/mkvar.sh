@@ -8,7 +8,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 B=$R/splat-transform_amd/build
 mkdir -p $R/tools/var
 flags="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result"
-[ "$base" = st_kmeans_nd ] && flags="$flags -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans"
+[ "$base" = st_kmeans_nd ] && flags="$flags -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $flags $EXTRA -I$R/splat-transform_amd/csrc -I$R/include -c $src -o /tmp/var_$name.o
 objs=$(ls $B/*.o | grep -v "/${base}.hip.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/tools/var/$name.so $objs /tmp/var_$name.o
