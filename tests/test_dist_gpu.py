@@ -1,4 +1,4 @@
-"""Multi-process writeSog on the GPU: two ranks (one shard each) on cuda:0 over gloo,
+"""Multi-process writeSog on the GPU: two or four ranks (uneven shards) on cuda:0 over gloo,
 product step API (splat_dist.HipOps), must reproduce the single-device st_dev_sog of
 the whole table bit for bit.  (On an 8-GPU node the same code runs one rank per GPU
 over RCCL; bench.py --gpus N.)"""
@@ -46,7 +46,7 @@ def _rank(rank, world, port, n, seed, iters, q):
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     full = _table(n, seed)
-    cuts = [0, n * 3 // 7, n]
+    cuts = {2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
     lo, hi = cuts[rank], cuts[rank + 1]
     cols = {k: torch.from_numpy(v[lo:hi].copy()).to(dev) for k, v in full.items()}
     draws = np.random.default_rng(seed + 1).random(1 << 20)
@@ -64,7 +64,8 @@ def _rank(rank, world, port, n, seed, iters, q):
 
 
 @pytest.mark.gpu
-def test_two_rank_write_sog_matches_single_device():
+@pytest.mark.parametrize('world', [2, 4])
+def test_multi_rank_write_sog_matches_single_device(world):
     import torch.multiprocessing as mp
     import splat_hip as sh
     n, seed, iters = 24000, 5, 3
@@ -74,7 +75,7 @@ def test_two_rank_write_sog_matches_single_device():
     s.close()
     mctx = mp.get_context('spawn')
     q = mctx.Queue()
-    procs = [mctx.Process(target=_rank, args=(r, 2, port, n, seed, iters, q)) for r in range(2)]
+    procs = [mctx.Process(target=_rank, args=(r, world, port, n, seed, iters, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=600)
