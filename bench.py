@@ -50,6 +50,8 @@ def parse():
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')
+    ap.add_argument('--dist', action='store_true', help='N = 1 through the sharded N > 1 code path (splat_dist over '
+                    'a one-rank process group) instead of st_dev_sog: its per-rank cost')
     return ap.parse_args()
 
 
@@ -210,8 +212,11 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
     torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
-    if world > 1:
-        dist.init_process_group(args.backend, init_method='env://')
+    sharded = world > 1 or args.dist
+    if sharded:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29533')
+        dist.init_process_group(args.backend, init_method='env://', rank=rank, world_size=world)
     dev = torch.device('cuda', local)
 
     # one real stream for the library and the torch glue (st_ctx_set_stream(NULL) would select the
@@ -226,7 +231,7 @@ def main():
     # one stream for the whole job, identical on every rank
     draws = np.random.default_rng(42).random(2 * 65536 * (args.iters + 2))
     W, H, pal, cw, ch = sh.sog_geometry(n * world, 15)
-    if world == 1:
+    if not sharded:
         u8 = dict(device=dev, dtype=torch.uint8)
         tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
         tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
@@ -277,7 +282,7 @@ def main():
 
     # one more step with per-stage event marks (outside the timed region; single device only)
     stages = None
-    if world == 1:
+    if not sharded:
         os.environ['ST_TIMING'] = '1'
         step()
         torch.cuda.synchronize()
@@ -285,17 +290,17 @@ def main():
         os.environ.pop('ST_TIMING', None)
 
     if rank != 0:
-        if world > 1:
+        if sharded:
             dist.destroy_process_group()
         return
     # the .sog container of this step's textures on rank 0 (outside the headline's timed region)
-    if world == 1:
+    if not sharded:
         bmeta, btex, bcount = meta, tex, n
     else:
         import splat_dist
         bmeta, btex, bcount = splat_dist.meta_struct(last['meta']), last['tex'], n * world
     addr0, size0 = ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)  # warm: workspace + pinned archive
-    ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0)) if world == 1 else None
+    ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0)) if not sharded else None
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     torch.cuda.synchronize()
@@ -315,10 +320,10 @@ def main():
     flops_per_launch = 2.0 * n * pal * D  # nearest-centroid dot products, one assign pass
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
     e2e = None
-    if world == 1 and not args.no_e2e:
+    if not sharded and not args.no_e2e:
         e2e = end_to_end(ctx, cols, args.iters, draws, tex, ref_archive)
     paths = None
-    if world == 1 and not args.no_paths:
+    if not sharded and not args.no_paths:
         # BASELINE config 3 (-r 0,45,0, filterNaN, Morton, chunk pack -> .compressed.ply) on its own
         # 10M SH-3 table: each HBM-bound stage priced by its algorithmic bytes (tools/bench_paths.py)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
@@ -348,7 +353,7 @@ def main():
         'config': {'workload': f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters, '
                                f'paletteSize {pal}',
                    'splats_per_gpu': n, 'splats_total': n * world, 'sh_bands': 3, 'palette_size': pal,
-                   'iterations': args.iters, 'parallelism': f'rowshard{world}' if world > 1 else 'single'},
+                   'iterations': args.iters, 'parallelism': f'rowshard{world}' if sharded else 'single'},
         'roofline': {
             'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-3 tile minima per splat)',
             'bound': 'mfma',
@@ -381,7 +386,7 @@ def main():
         'draws_used_per_step': used,
     }
     print(json.dumps(out))
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 

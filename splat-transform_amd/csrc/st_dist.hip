@@ -22,7 +22,6 @@
 
 #include "st_jsmath.h"
 #include "st_kmeans.h"
-#include "st_replay.h"
 
 namespace st {
 namespace {
@@ -58,52 +57,26 @@ __global__ __launch_bounds__(256) void k_partials_nd(const float *__restrict__ a
     const int ld = aos_ld(d);
     double sum = 0, sa = 0;
     int em = 1 << 20;
-    for (uint32_t j = s0; j < s1; ++j) {
-        const float v = aos[(uint64_t)members[j] * ld + lane];
+    auto add = [&](float v) {
         sum += (double)v;
         sa += (double)__builtin_fabsf(v);
         if (v != 0.0f) em = min(em, ulp_exp(v));
+    };
+    uint32_t j = s0;
+    // 16 member rows in flight per wave (the adds stay in ascending point order), as k_sumnd
+    constexpr int U = 16;
+    for (; j + U <= s1; j += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+        for (int u = 0; u < U; ++u) add(v[u]);
     }
+    for (; j < s1; ++j) add(aos[(uint64_t)members[j] * ld + lane]);
     const uint64_t o = ((uint64_t)seg * d + lane) * k + cl;
     sums[o] = sum;
     sabs[o] = sa;
     emin[o] = em;
-}
-
-// 1-D partials: one block per (segment, cluster) over the label-sorted value bits
-__global__ __launch_bounds__(256) void k_partials_1d(const uint32_t *__restrict__ vals,
-                                                     const uint32_t *__restrict__ start, int k, int nseg,
-                                                     double *__restrict__ sums, double *__restrict__ sabs,
-                                                     int32_t *__restrict__ emin, uint32_t *__restrict__ counts) {
-    const uint32_t sc = blockIdx.x;
-    const uint32_t s0 = start[sc], s1 = start[sc + 1];
-    __shared__ double red_s[4], red_a[4];
-    __shared__ int red_e[4];
-    double sum = 0, sa = 0;
-    int em = 1 << 20;
-    for (uint32_t j = s0 + threadIdx.x; j < s1; j += blockDim.x) {
-        const float x = __builtin_bit_cast(float, vals[j]);
-        sum += (double)x;
-        sa += (double)__builtin_fabsf(x);
-        if (x != 0.0f) em = min(em, ulp_exp(x));
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int o = 32; o > 0; o >>= 1) {
-        sum += __shfl_xor(sum, o, 64);
-        sa += __shfl_xor(sa, o, 64);
-        em = min(em, __shfl_xor(em, o, 64));
-    }
-    if (lane == 0) {
-        red_s[w] = sum;
-        red_a[w] = sa;
-        red_e[w] = em;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    sums[sc] = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);  // only used when certified (exact)
-    sabs[sc] = (red_a[0] + red_a[1]) + (red_a[2] + red_a[3]);
-    emin[sc] = min(min(red_e[0], red_e[1]), min(red_e[2], red_e[3]));
-    counts[sc] = s1 - s0;
 }
 
 // continue the sequential sums of the pending (cluster, dim) pairs over this rank's
@@ -119,28 +92,18 @@ __global__ __launch_bounds__(64) void k_seqsum_nd(const float *__restrict__ aos,
     const uint32_t sc = (uint32_t)seg * k + cl;
     const int ld = aos_ld(d);
     double s = running[p];
-    for (uint32_t j = start[sc]; j < start[sc + 1]; ++j) s += (double)aos[(uint64_t)members[j] * ld + dim];
+    uint32_t j = start[sc];
+    const uint32_t e = start[sc + 1];
+    constexpr int U = 8;  // loads in flight ahead of the ordered add chain
+    for (; j + U <= e; j += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + dim];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += (double)v[u];
+    }
+    for (; j < e; ++j) s += (double)aos[(uint64_t)members[j] * ld + dim];
     running[p] = s;
-}
-
-// 1-D: the exact replay (st_replay.h) of each pending cluster's sum over this segment,
-// starting from its running value; one RT-thread block per pair.  Pairs the replay
-// cannot take are flagged for k_seqsum_1d.
-__global__ __launch_bounds__(RT) void k_seqsum_1d_replay(const uint32_t *__restrict__ vals,
-                                                         const uint32_t *__restrict__ start, int k, int seg,
-                                                         const uint32_t *__restrict__ pairs,
-                                                         double *__restrict__ running,
-                                                         const int32_t *__restrict__ emin,
-                                                         const double *__restrict__ sabs, __int128 *__restrict__ cand_all,
-                                                         uint32_t *__restrict__ flag) {
-    const uint32_t p = blockIdx.x, cl = pairs[p];
-    const uint32_t sc = (uint32_t)seg * k + cl;
-    double out = 0;
-    const bool ok = replay_sum(vals, start[sc], start[sc + 1], emin[cl], sabs[cl], running[p],
-                               cand_all + (uint64_t)p * CAND_MAX, &out);
-    if (threadIdx.x != 0) return;
-    flag[p] = ok ? 0u : 1u;
-    if (ok) running[p] = out;
 }
 
 // 1-D fallback: one wave per flagged pending cluster, lane 0 walks the contiguous values
@@ -251,8 +214,7 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
     radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
     bounds_from_sorted(c, keys, n, (int)nk, start);
     if (d == 1) {
-        hipLaunchKernelGGL(k_partials_1d, dim3((unsigned)nk), dim3(256), 0, c->stream, payload, start, k, nseg, sums,
-                           sabs, emin, counts);
+        partials1d(c, payload, n, start, (int)nk, sums, sabs, emin, counts);
     } else {
         ST_REQUIRE(c->kn_n == n && c->kn_d == d, ST_ERR_ARG, "kmeans partials: point set not prepared");
         auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
@@ -275,11 +237,8 @@ void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32
     auto *payload = wsT<uint32_t>(c, "ds.payload", n);
     auto *start = wsT<uint32_t>(c, "ds.start", nk + 1);
     if (d == 1) {
-        auto *cand = wsT<__int128>(c, "ds.cands", (size_t)npairs * CAND_MAX);
         auto *flag = wsT<uint32_t>(c, "ds.sflag", npairs);
-        hipLaunchKernelGGL(k_seqsum_1d_replay, dim3(npairs), dim3(RT), 0, c->stream, payload, start, k, seg, pairs,
-                           running, emin, sabs, cand, flag);
-        ST_LAUNCH_CHECK();
+        seqsum1d(c, payload, n, start + (uint64_t)seg * k, k, pairs, npairs, running, emin, sabs, flag);
         hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, flag,
                            running);
     } else {

@@ -65,6 +65,14 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
 // returns true when it also wrote the update's (label, value bits) pairs into keys/vals
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,
               uint32_t *keys = nullptr, uint32_t *vals = nullptr);
+// the multi-GPU update's 1-D pieces (st_kmeans1d.hip's chunked kernels): per-(segment,
+// cluster) partials of the label-sorted value bits (nk = nseg * k ranges of start), and the
+// exact replay of the pending clusters' sums over one segment (start: that segment's k + 1
+// bounds) from their running values; pflag[p] = 1 where the sequential chain must finish
+void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int nk, double *sums, double *sabs,
+                int32_t *emin, uint32_t *counts);
+void seqsum1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int k, const uint32_t *pairs,
+              uint32_t npairs, double *running, const int32_t *emin, const double *sabs, uint32_t *pflag);
 // throws ST_ERR_NONFINITE on a non-finite value; also leaves max |x| in c->km_absmax
 // (cols: host array of the device columns, dcols: the same array on the device)
 void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n);

@@ -468,6 +468,14 @@ __device__ inline uint32_t sc_exscan_u32(uint32_t v, uint32_t *total) {
     *total = tot;
     return off + incl - v;
 }
+// |running start| + sum|x| bounds every prefix of a cluster's chain; base (nullable) holds
+// each cluster's running start (the multi-GPU segment chain), zero in the one-device loop
+__device__ inline double rp_bound(const double *__restrict__ sabs_c, const double *__restrict__ base, int cl) {
+    return sabs_c[cl] + (base ? __builtin_fabs(base[cl]) : 0.0);
+}
+__device__ inline __int128 rp_base(const double *__restrict__ base, int cl, int e_lo) {
+    return base ? f64_units(base[cl], e_lo) : (__int128)0;
+}
 __device__ inline __int128 rp_margin(double sabs, int e_lo) {
     int e_top;
     __builtin_frexp(sabs, &e_top);
@@ -494,10 +502,10 @@ __global__ __launch_bounds__(SC_T) void k_rp_sums(const uint32_t *__restrict__ v
 __global__ __launch_bounds__(256) void k_rp_prefix(const uint32_t *__restrict__ first, int k,
                                                    uint32_t *__restrict__ seq_flag, const double *__restrict__ sabs_c,
                                                    const int32_t *__restrict__ emin_c, __int128 *__restrict__ csum,
-                                                   __int128 *__restrict__ total) {
+                                                   __int128 *__restrict__ total, const double *__restrict__ base) {
     for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
         if (seq_flag[cl] != 1u) continue;
-        if (!(sabs_c[cl] * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin_c[cl] + 118))) {  // int128 range
+        if (!(rp_bound(sabs_c, base, cl) * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin_c[cl] + 118))) {  // int128 range
             seq_flag[cl] = 2u;
             continue;
         }
@@ -512,7 +520,8 @@ __global__ __launch_bounds__(256) void k_rp_prefix(const uint32_t *__restrict__ 
 }
 __global__ __launch_bounds__(256) void k_rp_cprefix(const uint32_t *__restrict__ first, int k,
                                                     uint32_t *__restrict__ seq_flag, const uint32_t *__restrict__ ccnt,
-                                                    uint32_t *__restrict__ cof, uint32_t *__restrict__ ctot) {
+                                                    uint32_t *__restrict__ cof, uint32_t *__restrict__ ctot,
+                                                    uint32_t cap) {
     for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
         if (seq_flag[cl] != 1u) continue;
         uint32_t run = 0;
@@ -521,7 +530,7 @@ __global__ __launch_bounds__(256) void k_rp_cprefix(const uint32_t *__restrict__
             run += ccnt[c];
         }
         ctot[cl] = run;
-        if (run > (uint32_t)CAND_MAX) seq_flag[cl] = 2u;  // the sequential chain
+        if (run > cap) seq_flag[cl] = 2u;  // the sequential chain
     }
 }
 
@@ -533,18 +542,18 @@ __global__ __launch_bounds__(SC_T) void k_rp_cands(const uint32_t *__restrict__ 
                                                   const int32_t *__restrict__ emin_c,
                                                   const double *__restrict__ sabs_c,
                                                   const __int128 *__restrict__ coff, uint32_t *__restrict__ ccnt,
-                                                  __int128 *__restrict__ cand_all) {
+                                                  __int128 *__restrict__ cand_all, const double *__restrict__ base) {
     if (blockIdx.x >= *nchunks) return;
     const Chunk ch = chunks[blockIdx.x];
     if (seq_flag[ch.cl] != 1u) return;
     const int e_lo = emin_c[ch.cl];
-    const __int128 margin = rp_margin(sabs_c[ch.cl], e_lo);
+    const __int128 margin = rp_margin(rp_bound(sabs_c, base, ch.cl), e_lo);
     // this thread's contiguous slice of the chunk
     const uint32_t a = min(ch.end, ch.begin + threadIdx.x * SC_PER), b = min(ch.end, a + SC_PER);
     __int128 local = 0;
     for (uint32_t j = a; j < b; ++j) local += f32_units(vals[j], e_lo);
     __int128 tot;
-    const __int128 off = coff[blockIdx.x] + sc_exscan_i128(local, &tot);
+    const __int128 off = rp_base(base, ch.cl, e_lo) + coff[blockIdx.x] + sc_exscan_i128(local, &tot);
     uint32_t mine = 0;
     __int128 P = off;
     for (uint32_t j = a; j < b; ++j) {
@@ -570,22 +579,25 @@ __global__ __launch_bounds__(SC_T) void k_rp_cands(const uint32_t *__restrict__ 
     }
 }
 
-// F: one lane per flagged cluster replays its candidates
+// F: one lane per flagged cluster replays its candidates; the centroid (cen) or, with a
+// running start (base), the f64 sum itself (sum_out)
 __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ start, const uint32_t *__restrict__ ctot_c,
                                                   int k, uint32_t *__restrict__ seq_flag,
                                                   const int32_t *__restrict__ emin_c, const double *__restrict__ sabs_c,
                                                   const __int128 *__restrict__ total, const __int128 *__restrict__ cand_all,
-                                                  float *__restrict__ cen) {
+                                                  float *__restrict__ cen, const double *__restrict__ base,
+                                                  double *__restrict__ sum_out) {
     // one workgroup per cluster: the wave stages the candidates in LDS 256 at a time, lane 0
     // replays them (the chain is sequential; its loads need not be)
     const int cl = blockIdx.x;
     if (cl >= k || seq_flag[cl] != 1u) return;  // uniform per workgroup
     __shared__ __int128 buf[256];
     const int e_lo = emin_c[cl];
-    const __int128 margin = rp_margin(sabs_c[cl], e_lo);
+    const __int128 margin = rp_margin(rp_bound(sabs_c, base, cl), e_lo);
     const uint32_t ctot = ctot_c[cl];
     const __int128 *cand = cand_all + (uint64_t)cl * CAND_MAX;
-    __int128 sv = 0, Pprev = 0;
+    const __int128 b0 = rp_base(base, cl, e_lo);
+    __int128 sv = b0, Pprev = b0;
     bool ok = true;
     for (uint32_t b = 0; b < ctot; b += 256) {
         const uint32_t m = min(256u, ctot - b);
@@ -604,13 +616,89 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
         __syncthreads();
     }
     if (threadIdx.x != 0) return;
-    const __int128 fin = sv + (total[cl] - Pprev);
+    const __int128 fin = sv + (b0 + total[cl] - Pprev);
     if (!ok || !f64_representable(fin)) {
         seq_flag[cl] = 2u;
         return;
     }
-    cen[cl] = (float)(f64_round(fin, e_lo) / (double)(start[cl + 1] - start[cl]));
+    if (sum_out)
+        sum_out[cl] = f64_round(fin, e_lo);
+    else
+        cen[cl] = (float)(f64_round(fin, e_lo) / (double)(start[cl + 1] - start[cl]));
     seq_flag[cl] = 0u;
+}
+
+// candidates one replay takes (CAND_MAX); ST_REPLAY_CAP lowers it so that tests can drive
+// the sequential chain with small inputs
+uint32_t replay_cap() {
+    static const uint32_t cap = [] {
+        const char *e = getenv("ST_REPLAY_CAP");
+        return e ? std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 10), (uint32_t)CAND_MAX) : (uint32_t)CAND_MAX;
+    }();
+    return cap;
+}
+
+// stages A-F of the chunked replay for the clusters flagged 1 (left 0 when replayed, 2 when
+// the sequential chain must take them)
+void chunked_replay(st_ctx *c, const uint32_t *vals, const uint32_t *start, int k, uint64_t maxch, const Chunk *chunks,
+                    const uint32_t *ch_first, uint32_t *seq_flag, const int32_t *emin_c, const double *sabs_c,
+                    __int128 *csum, __int128 *total, uint32_t *ccnt, uint32_t *cof, uint32_t *ctot, __int128 *cands,
+                    float *cen, const double *base, double *sum_out) {
+    const unsigned gk = grid_for((uint64_t)k, 256, 1024);
+    hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag, emin_c,
+                       csum);
+    hipLaunchKernelGGL(k_rp_prefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, sabs_c, emin_c, csum,
+                       total, base);
+    hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
+                       emin_c, sabs_c, csum, ccnt, cands, base);
+    hipLaunchKernelGGL(k_rp_cprefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, ccnt, cof, ctot,
+                       replay_cap());
+    hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
+                       emin_c, sabs_c, csum, cof, cands, base);
+    hipLaunchKernelGGL(k_rp_finish, dim3(k), dim3(64), 0, c->stream, start, ctot, k, seq_flag, emin_c, sabs_c, total,
+                       cands, cen, base, sum_out);
+    ST_LAUNCH_CHECK();
+}
+
+// the chunk list of every cluster's member range (k clusters, start[k + 1])
+void chunk_list(st_ctx *c, const uint32_t *start, int k, uint32_t *ch_cnt, uint32_t *ch_first, Chunk *chunks) {
+    const unsigned gk = grid_for((uint64_t)k, 256, 1024);
+    hipLaunchKernelGGL(k_chunk_counts, dim3(gk), dim3(256), 0, c->stream, start, k, ch_cnt);
+    scan_u32(c, ch_cnt, ch_first, (uint64_t)k, ch_first + k);
+    hipLaunchKernelGGL(k_chunk_list, dim3(gk), dim3(256), 0, c->stream, start, k, ch_first, chunks);
+    ST_LAUNCH_CHECK();
+}
+
+// ---- the multi-GPU update's 1-D pieces (st_dist.hip) --------------------------------
+__global__ __launch_bounds__(256) void k_partials_out(const SumAcc *__restrict__ acc, const uint32_t *__restrict__ start,
+                                                      int nk, double *__restrict__ sums, double *__restrict__ sabs,
+                                                      int32_t *__restrict__ emin, uint32_t *__restrict__ counts) {
+    for (int sc = blockIdx.x * blockDim.x + threadIdx.x; sc < nk; sc += gridDim.x * blockDim.x) {
+        const SumAcc a = acc[sc];
+        sums[sc] = a.sum;  // only used when certified (then exact in any order)
+        sabs[sc] = a.sabs;
+        emin[sc] = a.emin;
+        counts[sc] = start[sc + 1] - start[sc];
+    }
+}
+
+// pending pairs (clusters) -> per-cluster flag 1 and running start
+__global__ __launch_bounds__(256) void k_pend_in(const uint32_t *__restrict__ pairs, uint32_t npairs,
+                                                 const double *__restrict__ running, uint32_t *__restrict__ flag_cl,
+                                                 double *__restrict__ base_cl) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x) {
+        flag_cl[pairs[p]] = 1u;
+        base_cl[pairs[p]] = running[p];
+    }
+}
+__global__ __launch_bounds__(256) void k_pend_out(const uint32_t *__restrict__ pairs, uint32_t npairs,
+                                                  const uint32_t *__restrict__ flag_cl, const double *__restrict__ sum_cl,
+                                                  double *__restrict__ running, uint32_t *__restrict__ pflag) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x) {
+        const uint32_t f = flag_cl[pairs[p]];
+        if (f == 0u) running[p] = sum_cl[pairs[p]];
+        pflag[p] = f == 2u ? 1u : 0u;
+    }
 }
 
 }  // namespace
@@ -679,9 +767,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             KTimer kt(c, "k1.sum");
             if (chunked) {
                 const unsigned gk = grid_for((uint64_t)k, 256, 1024);
-                hipLaunchKernelGGL(k_chunk_counts, dim3(gk), dim3(256), 0, c->stream, start, k, ch_cnt);
-                scan_u32(c, ch_cnt, ch_first, (uint64_t)k, ch_first + k);
-                hipLaunchKernelGGL(k_chunk_list, dim3(gk), dim3(256), 0, c->stream, start, k, ch_first, chunks);
+                chunk_list(c, start, k, ch_cnt, ch_first, chunks);
                 hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, k);
                 hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
                                    acc);
@@ -700,20 +786,8 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                 ST_HIP(hipMemcpy(f1.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost));
             }
             if (chunked) {
-                const unsigned gk = grid_for((uint64_t)k, 256, 1024);
-                hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
-                                   seq_flag, emin_c, rp_csum);
-                hipLaunchKernelGGL(k_rp_prefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, sabs_c,
-                                   emin_c, rp_csum, rp_total);
-                hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks,
-                                   ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_ccnt, cand_buf);
-                hipLaunchKernelGGL(k_rp_cprefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, rp_ccnt,
-                                   rp_cof, rp_ctot);
-                hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks,
-                                   ch_first + k, seq_flag, emin_c, sabs_c, rp_csum, rp_cof, cand_buf);
-                hipLaunchKernelGGL(k_rp_finish, dim3(k), dim3(64), 0, c->stream, start, rp_ctot, k,
-                                   seq_flag, emin_c, sabs_c, rp_total, cand_buf, cen);
-                ST_LAUNCH_CHECK();
+                chunked_replay(c, vals_s, start, k, maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum,
+                               rp_total, rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr);
             } else {
                 hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals_s, start, seq_flag, emin_c,
                                    sabs_c, cen, cand_buf);
@@ -735,6 +809,55 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         }
         reseed_empty(c, dcols, 1, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "k1.update");
+    }
+}
+
+void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int nk, double *sums, double *sabs,
+                int32_t *emin, uint32_t *counts) {
+    const uint64_t maxch = n / SC_CH + (uint64_t)nk + 1;
+    auto *ch_cnt = wsT<uint32_t>(c, "d1.chcnt", (size_t)nk);
+    auto *ch_first = wsT<uint32_t>(c, "d1.chfirst", (size_t)nk + 1);
+    auto *chunks = wsT<Chunk>(c, "d1.chunks", maxch);
+    auto *acc = wsT<SumAcc>(c, "d1.acc", (size_t)nk);
+    chunk_list(c, start, nk, ch_cnt, ch_first, chunks);
+    const unsigned gk = grid_for((uint64_t)nk, 256, 1024);
+    hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, nk);
+    hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + nk, acc);
+    hipLaunchKernelGGL(k_partials_out, dim3(gk), dim3(256), 0, c->stream, acc, start, nk, sums, sabs, emin, counts);
+    ST_LAUNCH_CHECK();
+}
+
+void seqsum1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int k, const uint32_t *pairs,
+              uint32_t npairs, double *running, const int32_t *emin, const double *sabs, uint32_t *pflag) {
+    const uint64_t maxch = n / SC_CH + (uint64_t)k + 1;
+    auto *ch_cnt = wsT<uint32_t>(c, "d1.chcnt", (size_t)k);
+    auto *ch_first = wsT<uint32_t>(c, "d1.chfirst", (size_t)k + 1);
+    auto *chunks = wsT<Chunk>(c, "d1.chunks", maxch);
+    auto *flag_cl = wsT<uint32_t>(c, "d1.flag", (size_t)k);
+    auto *base_cl = wsT<double>(c, "d1.base", (size_t)k);
+    auto *sum_cl = wsT<double>(c, "d1.sum", (size_t)k);
+    auto *csum = wsT<__int128>(c, "d1.csum", maxch);
+    auto *ccnt = wsT<uint32_t>(c, "d1.ccnt", maxch);
+    auto *cof = wsT<uint32_t>(c, "d1.cof", maxch);
+    auto *ctot = wsT<uint32_t>(c, "d1.ctot", (size_t)k);
+    auto *total = wsT<__int128>(c, "d1.total", (size_t)k);
+    auto *cands = wsT<__int128>(c, "d1.cands", (size_t)k * CAND_MAX);
+    ST_HIP(hipMemsetAsync(flag_cl, 0, sizeof(uint32_t) * k, c->stream));
+    const unsigned gp = grid_for(npairs, 256, 1024);
+    hipLaunchKernelGGL(k_pend_in, dim3(gp), dim3(256), 0, c->stream, pairs, npairs, running, flag_cl, base_cl);
+    ST_LAUNCH_CHECK();
+    chunk_list(c, start, k, ch_cnt, ch_first, chunks);
+    chunked_replay(c, vals, start, k, maxch, chunks, ch_first, flag_cl, emin, sabs, csum, total, ccnt, cof, ctot, cands,
+                   nullptr, base_cl, sum_cl);
+    hipLaunchKernelGGL(k_pend_out, dim3(gp), dim3(256), 0, c->stream, pairs, npairs, flag_cl, sum_cl, running, pflag);
+    ST_LAUNCH_CHECK();
+    if (getenv("ST_DEBUG")) {
+        std::vector<uint32_t> f(npairs);
+        ST_HIP(hipMemcpyAsync(f.data(), pflag, 4ull * npairs, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        uint32_t seq = 0;
+        for (uint32_t v : f) seq += v;
+        fprintf(stderr, "[st d1] pending=%u replayed=%u sequential=%u\n", npairs, npairs - seq, seq);
     }
 }
 

@@ -1,4 +1,5 @@
 """Multi-process writeSog on the GPU: two or four ranks (uneven shards) on cuda:0 over gloo,
+and the RCCL code path at world size 1;
 product step API (splat_dist.HipOps), must reproduce the single-device st_dev_sog of
 the whole table bit for bit.  (On an 8-GPU node the same code runs one rank per GPU
 over RCCL; bench.py --gpus N.)"""
@@ -37,16 +38,16 @@ def _table(n, seed):
     return cols
 
 
-def _rank(rank, world, port, n, seed, iters, q):
+def _rank(rank, world, backend, port, n, seed, iters, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)  # before the process group: RCCL binds the rank to this device
+    dist.init_process_group(backend, rank=rank, world_size=world)
     import splat_hip as sh
     import splat_dist
-    dev = torch.device('cuda', 0)
-    torch.cuda.set_device(dev)
     full = _table(n, seed)
-    cuts = {2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
+    cuts = {1: [0, n], 2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
     lo, hi = cuts[rank], cuts[rank + 1]
     cols = {k: torch.from_numpy(v[lo:hi].copy()).to(dev) for k, v in full.items()}
     draws = np.random.default_rng(seed + 1).random(1 << 20)
@@ -63,9 +64,108 @@ def _rank(rank, world, port, n, seed, iters, q):
     ctx.close()
 
 
+def _adversarial_1d(n, seed):
+    """three columns whose cluster sums defeat the order-free certificate: values over 15
+    decades (tiny members under large sums: replay candidates, and past CAND_MAX the
+    sequential chain), zeros and -0"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(3):
+        u = rng.random(n)
+        v = rng.normal(0, 1, n)
+        v = np.where(u < 0.3, v * 1e-9, v)
+        v = np.where((u >= 0.7) & (u < 0.9), v * 1e3, v)
+        v = np.where(u >= 0.9, np.sign(v) * rng.uniform(1e5, 1e6, n), v)
+        v[rng.random(n) < 0.01] = 0.0
+        v[rng.random(n) < 0.01] = -0.0
+        out.append(v.astype(np.float32))
+    return out
+
+
+def _c1d_rank(rank, world, port, n, seed, iters, q, cap):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    if cap is not None:
+        os.environ['ST_REPLAY_CAP'] = str(cap)
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import splat_hip as sh
+    import splat_dist
+    full = _adversarial_1d(n, seed)
+    cuts = [0] + [n * (r + 1) * (r + 2) // (world * (world + 1)) for r in range(world)]  # uneven shards
+    lo, hi = cuts[rank], cuts[rank + 1]
+    cols = [torch.from_numpy(c[lo:hi].copy()).to(dev) for c in full]
+    draws = np.random.default_rng(seed + 1).random(1 << 16)
+    ctx = sh.Context(0)
+    ops = splat_dist.HipOps(ctx, dev)
+    comm = splat_dist.Comm()
+    shard = splat_dist.Shard(comm, hi - lo)
+    cb, lab8, used = splat_dist.cluster1d(ops, comm, shard, cols, iters, draws)
+    torch.cuda.synchronize()
+    q.put(dict(rank=rank, cb=cb.cpu().numpy(), lab=lab8.cpu().numpy().reshape(3, hi - lo), used=used, lo=lo, hi=hi))
+    dist.destroy_process_group()
+    ctx.close()
+
+
+def _single_c1d(q, n, seed, iters, cap):
+    if cap is not None:
+        os.environ['ST_REPLAY_CAP'] = str(cap)
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    full = _adversarial_1d(n, seed)
+    cols = [torch.from_numpy(c).to(dev) for c in full]
+    cb = torch.empty(256, dtype=torch.float32, device=dev)
+    lab = torch.empty(3 * n, dtype=torch.uint8, device=dev)
+    draws = np.random.default_rng(seed + 1).random(1 << 16)
+    ctx = sh.Context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    used = ctx.dev_cluster1d(cols, iters, draws, cb, lab)
+    torch.cuda.synchronize()
+    q.put(dict(cb=cb.cpu().numpy(), lab=lab.cpu().numpy().reshape(3, n), used=used))
+    ctx.close()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('world', [2, 4])
-def test_multi_rank_write_sog_matches_single_device(world):
+@pytest.mark.parametrize('world,cap', [(1, None), (3, None), (3, 0)])
+def test_dist_cluster1d_adversarial_matches_single_device(world, cap):
+    """cluster1d over sharded columns (segments = rank x column) where 1-D cluster sums are
+    uncertified: the chunked replay from each segment's running start must give the
+    single-device codebook and labels bit for bit.  cap = 0 (ST_REPLAY_CAP) sends every
+    uncertified sum down the sequential chain instead, on both sides.  The single-device
+    reference result is computed in its own process under the same cap."""
+    import torch.multiprocessing as mp
+    n, seed, iters = 90000, 11, 4
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    mctx = mp.get_context('spawn')
+    q = mctx.Queue()
+    procs = [mctx.Process(target=_c1d_rank, args=(r, world, port, n, seed, iters, q, cap)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in range(world)), key=lambda r: r['rank'])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    p = mctx.Process(target=_single_c1d, args=(q, n, seed, iters, cap))
+    p.start()
+    one = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for r in res:
+        assert r['used'] == one['used']
+        assert np.array_equal(r['cb'].view(np.uint32), one['cb'].view(np.uint32))
+        assert np.array_equal(r['lab'], one['lab'][:, r['lo']:r['hi']])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('backend,world', [('gloo', 2), ('gloo', 4), ('nccl', 1)])
+def test_multi_rank_write_sog_matches_single_device(backend, world):
+    """gloo: 2 and 4 ranks sharing cuda:0.  nccl: RCCL refuses two ranks on one GPU, so the
+    RCCL leg runs the same sharded code path at world size 1 (device-tensor collectives,
+    every dtype / reduce op the 8-GPU job issues)."""
     import torch.multiprocessing as mp
     import splat_hip as sh
     n, seed, iters = 24000, 5, 3
@@ -75,7 +175,7 @@ def test_multi_rank_write_sog_matches_single_device(world):
     s.close()
     mctx = mp.get_context('spawn')
     q = mctx.Queue()
-    procs = [mctx.Process(target=_rank, args=(r, world, port, n, seed, iters, q)) for r in range(world)]
+    procs = [mctx.Process(target=_rank, args=(r, world, backend, port, n, seed, iters, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=600)
