@@ -385,10 +385,19 @@ def main():
         'kernels': kstats,
         'draws_used_per_step': used,
     }
-    print(json.dumps(out))
+    _RESULT.write(json.dumps(out) + '\n')
+    _RESULT.flush()
     if sharded:
         dist.destroy_process_group()
 
 
+# stdout carries exactly the one JSON line: whatever the libraries print there (RCCL's
+# version banner, for one) goes to stderr instead
+_RESULT = sys.stdout
+
 if __name__ == '__main__':
+    sys.stdout.flush()
+    _RESULT = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
     main()

@@ -177,8 +177,9 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
 void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
                          uint8_t *sh);
 // returns draws consumed
+// (host_init: initializeCentroids by the host's loop instead of on the device)
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
-                    uint64_t ndraws, float *centroids, uint32_t *labels);
+                    uint64_t ndraws, float *centroids, uint32_t *labels, bool host_init = false);
 uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, int iters, const double *draws,
                        uint64_t ndraws, float *centroids256, uint8_t *labels);
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,

@@ -6,7 +6,7 @@
 namespace st {
 namespace km {
 
-enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u };
+enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u, ERR_INIT_WINDOW = 8u };
 
 // device-resident k-means state (one per call)
 struct State {

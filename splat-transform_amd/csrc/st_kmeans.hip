@@ -114,6 +114,42 @@ __global__ __launch_bounds__(256) void k_gather_init(const float *const *cols, i
     }
 }
 
+// initializeCentroids (k-means.ts:8-20) on the device: row floor(draw * n) of draw i is
+// taken iff no earlier draw chose it, until k rows are taken.  first[row] = the earliest
+// draw choosing it (first[] preset to ~0); draw i is a taking iff first[row_i] == i, and
+// its rank among the takings (an exclusive scan) is its centroid slot.
+__device__ inline uint32_t init_row(const double *draws, uint32_t i, uint64_t n) {  // ~0: outside the table
+    const double f = __builtin_floor(draws[i] * (double)n);
+    return (f >= 0.0 && f < (double)n) ? (uint32_t)f : 0xffffffffu;
+}
+__global__ __launch_bounds__(256) void k_init_first(const double *__restrict__ draws, uint32_t m, uint64_t n,
+                                                    uint32_t *__restrict__ first, State *st) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t r = init_row(draws, i, n);
+        if (r < n)
+            atomicMin(&first[r], i);
+        else
+            atomicOr(&st->err, ERR_INIT_WINDOW);  // a draw outside [0, 1): the host loop reports it
+    }
+}
+__global__ __launch_bounds__(256) void k_init_flags(const double *__restrict__ draws, uint32_t m, uint64_t n,
+                                                    const uint32_t *__restrict__ first, uint32_t *__restrict__ flags) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t r = init_row(draws, i, n);
+        flags[i] = (r < n && first[r] == i) ? 1u : 0u;
+    }
+}
+__global__ __launch_bounds__(256) void k_init_select(const double *__restrict__ draws, uint32_t m, uint64_t n, int k,
+                                                     const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
+                                                     uint32_t *__restrict__ rows, State *st) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        if (!flags[i] || pos[i] >= (uint32_t)k) continue;
+        rows[pos[i]] = init_row(draws, i, n);
+        if (pos[i] == (uint32_t)k - 1) st->cursor = (uint64_t)i + 1;  // draws consumed
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && pos[m] < (uint32_t)k) st->err |= ERR_INIT_WINDOW;
+}
+
 // ---------------------------------------------------------------------------
 // update: cluster boundaries in the label-sorted member list
 __global__ __launch_bounds__(256) void k_bounds(const uint32_t *__restrict__ sorted_labels, uint64_t n, int k,
@@ -212,7 +248,7 @@ void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t 
 }
 
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
-                    uint64_t ndraws, float *cen, uint32_t *labels) {
+                    uint64_t ndraws, float *cen, uint32_t *labels, bool host_init) {
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans: n must be < 2^31 per device");
     if (n < (uint64_t)k) {  // k-means.ts:139-144
         for (int j = 0; j < d; ++j)
@@ -230,11 +266,17 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     auto *dstate = static_cast<State *>(ws(c, "km.state", sizeof(State)));
     State hs{};
     uint64_t init_used = 0;
+    uint32_t dev_init_m = 0;  // > 0: initializeCentroids runs on the device over this many draws
     if (d == 1) {
         auto *mm = wsT<uint32_t>(c, "km.mm", 2);
         minmax_keys_dev(c, cols, 1, n, mm);  // finite input (checked above): keys of min and max
         hipLaunchKernelGGL(k_init1d, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, mm, cen, k);
         ST_LAUNCH_CHECK();
+    } else if (!host_init && !getenv("ST_KM_HOST_INIT") && n >= 4 * (uint64_t)k && ndraws > 0) {
+        // initializeCentroids on the device over a window of the draws (k-means.ts:8-20): with
+        // n >= 4k the k-th distinct row comes after ~n ln(n / (n - k)) <= 1.151 k draws; a
+        // window too short sets ERR_INIT_WINDOW and the call reruns with the host's loop
+        dev_init_m = (uint32_t)std::min<uint64_t>(ndraws, (uint64_t)k + k / 4 + 4096);
     } else {
         // initializeCentroids (k-means.ts:8-20): k distinct rows by rejection on the
         // host-owned Math.random stream; the rows are then gathered on the device.
@@ -246,6 +288,7 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
             do {
                 ST_REQUIRE(cur < ndraws, ST_ERR_DRAWS, "kmeans: Math.random draws exhausted during initialisation");
                 cand = (uint64_t)std::floor(draws[cur++] * (double)n);
+                ST_REQUIRE(cand < n, ST_ERR_ARG, "kmeans: Math.random draws must lie in [0, 1)");
             } while (chosen[cand]);
             chosen[cand] = 1;
             rows[i] = (uint32_t)cand;
@@ -260,10 +303,28 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     hs.cursor = init_used;
     ST_HIP(hipMemcpyAsync(dstate, &hs, sizeof(State), hipMemcpyHostToDevice, c->stream));
     // re-seeds consume at most k draws per iteration: upload only that window of the stream
-    const uint64_t window = std::min<uint64_t>(ndraws, init_used + (uint64_t)k * (uint64_t)iters);
+    const uint64_t window = std::min<uint64_t>(ndraws, std::max<uint64_t>(init_used, dev_init_m) +
+                                                           (uint64_t)k * (uint64_t)iters);
     auto *ddraws = wsT<double>(c, "km.draws", window ? window : 1);
     if (window) ST_HIP(hipMemcpyAsync(ddraws, draws, window * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    const uint64_t ndraws_all = ndraws;
     ndraws = window;
+    if (dev_init_m) {
+        const uint32_t m = dev_init_m;
+        auto *first = wsT<uint32_t>(c, "km.ifirst", n);
+        auto *flags = wsT<uint32_t>(c, "km.iflags", m);
+        auto *pos = wsT<uint32_t>(c, "km.ipos", (size_t)m + 1);
+        auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
+        ST_HIP(hipMemsetAsync(first, 0xff, n * sizeof(uint32_t), c->stream));
+        const unsigned g = grid_for(m, 256, 1024);
+        hipLaunchKernelGGL(k_init_first, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, dstate);
+        hipLaunchKernelGGL(k_init_flags, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, flags);
+        scan_u32(c, flags, pos, m, pos + m);
+        hipLaunchKernelGGL(k_init_select, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, k, flags, pos, drows, dstate);
+        hipLaunchKernelGGL(k_gather_init, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, drows, k,
+                           cen);
+        ST_LAUNCH_CHECK();
+    }
     mark(c, "km.init");
 
     if (d == 1)
@@ -273,6 +334,8 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
 
     ST_HIP(hipMemcpyAsync(&hs, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
+    if (hs.err & ERR_INIT_WINDOW)  // the device window held fewer than k distinct rows
+        return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, true);
     ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
     ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");
     return hs.cursor;

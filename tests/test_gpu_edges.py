@@ -156,3 +156,35 @@ def test_sog_all_bands_vs_oracle(ctx, C):
         assert getattr(meta, f) == getattr(ometa, f), f
     for f in ('means_min', 'means_max', 'scales_codebook', 'sh0_codebook', 'shn_codebook'):
         same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
+
+
+@pytest.mark.parametrize('case', ['n_eq_4k', 'repeats', 'host_env'])
+def test_kmeans_device_init_vs_oracle(ctx, case, monkeypatch):
+    """initializeCentroids (k-means.ts:8-20) on the device (n >= 4k): first occurrences of
+    floor(draw * n) in draw order over a window of the draws.  'repeats' fills the window
+    with a few rows so it holds fewer than k distinct ones (the call reruns with the host's
+    loop); 'host_env' forces the host loop (ST_KM_HOST_INIT)."""
+    k, d, iters = 1024, 9, 2
+    n = 4 * k if case == 'n_eq_4k' else 20_000
+    rng = np.random.default_rng(3)
+    cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
+    draws = oracle.mulberry32(99, 8 * k * (iters + 2))
+    if case == 'repeats':
+        draws[:k + k // 4 + 4000] = (rng.integers(0, 7, k + k // 4 + 4000) + 0.5) / n
+    if case == 'host_env':
+        monkeypatch.setenv('ST_KM_HOST_INIT', '1')
+    cent, labels, used = ctx.kmeans(cols, k, iters, draws)
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, iters, draws)
+    assert rc == 0 and used == oused
+    same_bits(labels, olabels)
+    same_bits(cent, ocent)
+
+
+def test_kmeans_draw_outside_unit_interval_fails(ctx):
+    k, n = 256, 4096
+    rng = np.random.default_rng(4)
+    cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
+    draws = rng.random(4 * k * 4)
+    draws[10] = 1.0
+    with pytest.raises(sh.StError):
+        ctx.kmeans(cols, k, 2, draws)
