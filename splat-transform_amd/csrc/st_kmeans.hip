@@ -316,6 +316,8 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
         auto *pos = wsT<uint32_t>(c, "km.ipos", (size_t)m + 1);
         auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
         ST_HIP(hipMemsetAsync(first, 0xff, n * sizeof(uint32_t), c->stream));
+        // rows a short window leaves unset stay 0: the discarded run still reads inside the table
+        ST_HIP(hipMemsetAsync(drows, 0, (size_t)k * sizeof(uint32_t), c->stream));
         const unsigned g = grid_for(m, 256, 1024);
         hipLaunchKernelGGL(k_init_first, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, dstate);
         hipLaunchKernelGGL(k_init_flags, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, flags);
