@@ -293,6 +293,48 @@ __global__ __launch_bounds__(256) void k_mm_final(const uint32_t *__restrict__ p
     }
 }
 
+// stable sort of at most SS_MAX pairs in one workgroup: every element's rank is the count
+// of smaller keys plus equal keys before it (the LDS reads of key j are broadcasts).  Short
+// sorts -- the 256 centroids of every 1-D k-means iteration -- were 4 passes x 3 launches
+constexpr uint32_t SS_MAX = 2048;
+constexpr int SS_T = 1024;
+template <typename K>
+__global__ __launch_bounds__(SS_T) void k_small_sort(K *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t n,
+                                                     int shift, int bits) {
+    __shared__ K sk[SS_MAX];
+    __shared__ uint32_t sv[SS_MAX];
+    for (uint32_t i = threadIdx.x; i < n; i += SS_T) {
+        sk[i] = keys[i];
+        sv[i] = vals[i];
+    }
+    __syncthreads();
+    const K mask = bits >= (int)(8 * sizeof(K)) ? ~(K)0 : (((K)1 << bits) - 1);
+    K mine[SS_MAX / SS_T];
+    uint32_t rank[SS_MAX / SS_T];
+#pragma unroll
+    for (int u = 0; u < (int)(SS_MAX / SS_T); ++u) {
+        const uint32_t e = threadIdx.x + u * SS_T;
+        mine[u] = e < n ? (sk[e] >> shift) & mask : (K)0;
+        rank[u] = 0;
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        const K kj = (sk[j] >> shift) & mask;
+#pragma unroll
+        for (int u = 0; u < (int)(SS_MAX / SS_T); ++u) {
+            const uint32_t e = threadIdx.x + u * SS_T;
+            rank[u] += (kj < mine[u] || (kj == mine[u] && j < e)) ? 1u : 0u;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < (int)(SS_MAX / SS_T); ++u) {
+        const uint32_t e = threadIdx.x + u * SS_T;
+        if (e < n) {
+            keys[rank[u]] = sk[e];
+            vals[rank[u]] = sv[e];
+        }
+    }
+}
+
 template <typename K>
 void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
                      const std::string &tag, K **out_keys = nullptr, uint32_t **out_vals = nullptr) {
@@ -300,6 +342,12 @@ void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_b
     if (out_vals) *out_vals = vals;
     if (n <= 1 || end_bit <= begin_bit) return;
     ST_REQUIRE(n < (1ull << 32), ST_ERR_ARG, "radix sort: n must be < 2^32");
+    if (n <= SS_MAX) {  // in place, one launch
+        hipLaunchKernelGGL(k_small_sort<K>, dim3(1), dim3(SS_T), 0, c->stream, keys, vals, (uint32_t)n, begin_bit,
+                           end_bit - begin_bit);
+        ST_LAUNCH_CHECK();
+        return;
+    }
     const uint32_t nblocks = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     K *k2 = wsT<K>(c, tag + ".k2", n);
     uint32_t *v2 = wsT<uint32_t>(c, tag + ".v2", n);
