@@ -337,6 +337,16 @@ def main():
     if os.path.exists(tfile) and n == 10_000_000:
         traffic = json.load(open(tfile))['hbm_bytes_per_launch']
         tsrc = os.path.relpath(tfile, ROOT)
+    # the engine clock the chip holds under the sweep (PMC GRBM_GUI_ACTIVE, tools/pmc.sh + pmc_util.py):
+    # beside `frac` (against the 2.4 GHz headline peak), the fraction of the peak at that clock
+    clock = None
+    ufile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_util.json')
+    if os.path.exists(ufile) and achieved:
+        u = json.load(open(ufile))
+        clock = {'engine_clock_GHz': u['engine_clock_GHz'], 'mfma_busy_frac': u['mfma_busy_frac'],
+                 'peak_at_clock': u['dense_fp16_peak_at_this_clock_TFLOPs'],
+                 'frac_at_clock': achieved / u['dense_fp16_peak_at_this_clock_TFLOPs'],
+                 'source': os.path.relpath(ufile, ROOT)}
     out = {
         'metric': 'Msplats/sec PLY->SOG (SH-3, 10 k-means iters)',
         'value': value,
@@ -367,6 +377,7 @@ def main():
             'algorithmic_flops_per_launch': flops_per_launch,
             'avg_launch_ms': avg_sweep_s * 1e3,
             'launches': sweep_launches,
+            'clock': clock,
         },
         'cpu_baseline': cpu,
         'cpu_baseline_all_cores': cpu_all,
