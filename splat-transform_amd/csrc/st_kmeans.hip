@@ -190,6 +190,54 @@ __global__ __launch_bounds__(256) void k_reseed(const float *const *cols, int d,
 
 __global__ void k_advance_cursor(State *st, const uint32_t *total_empty) { st->cursor += *total_empty; }
 
+// the three steps above in one workgroup for k <= RS1_MAX (the 1-D codebooks, k = 256):
+// empty flags, their exclusive scan in LDS, the re-seeds, the cursor
+constexpr int RS1_T = 1024, RS1_MAX = 4096;
+__global__ __launch_bounds__(RS1_T) void k_reseed_small(const float *const *cols, int d, uint64_t n, int k,
+                                                        const uint32_t *__restrict__ start,
+                                                        const double *__restrict__ draws, uint64_t ndraws, State *st,
+                                                        float *__restrict__ cen) {
+    constexpr int PER = RS1_MAX / RS1_T;
+    __shared__ uint32_t wsum[RS1_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t f[PER], mine = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {  // thread t owns clusters t*PER .. t*PER+PER-1 (ascending)
+        const int c = t * PER + u;
+        f[u] = (c < k && start[c + 1] == start[c]) ? 1u : 0u;
+        mine += f[u];
+    }
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (int i = 0; i < RS1_T / 64; ++i) {
+        if (i < w) off += wsum[i];
+        total += wsum[i];
+    }
+    const uint64_t cursor = st->cursor;
+    uint32_t rank = off + incl - mine;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        if (!f[u]) continue;
+        const int c = t * PER + u;
+        const uint64_t di = cursor + rank++;
+        if (di >= ndraws) {
+            atomicOr(&st->err, ERR_DRAWS);
+            continue;
+        }
+        const uint64_t row = (uint64_t)__builtin_floor(draws[di] * (double)n);
+        for (int j = 0; j < d; ++j) cen[(uint64_t)j * k + c] = cols[j][row];
+    }
+    __syncthreads();  // every thread has read st->cursor
+    if (t == 0) st->cursor = cursor + total;
+}
+
 }  // namespace km
 
 using namespace km;
@@ -221,6 +269,12 @@ void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols
 // reseed + cursor bookkeeping shared by both update paths
 void reseed_empty(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *start,
                   const double *ddraws, uint64_t ndraws, State *dstate, float *cen) {
+    if (k <= RS1_MAX) {
+        hipLaunchKernelGGL(k_reseed_small, dim3(1), dim3(RS1_T), 0, c->stream, dcols, d, n, k, start, ddraws, ndraws,
+                           dstate, cen);
+        ST_LAUNCH_CHECK();
+        return;
+    }
     auto *flags = wsT<uint32_t>(c, "km.eflags", (size_t)k + 1);
     auto *rank = wsT<uint32_t>(c, "km.erank", (size_t)k + 1);
     hipLaunchKernelGGL(k_empty_flags, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, start, k, flags);
