@@ -660,12 +660,62 @@ void chunked_replay(st_ctx *c, const uint32_t *vals, const uint32_t *start, int 
     ST_LAUNCH_CHECK();
 }
 
-// the chunk list of every cluster's member range (k clusters, start[k + 1])
-void chunk_list(st_ctx *c, const uint32_t *start, int k, uint32_t *ch_cnt, uint32_t *ch_first, Chunk *chunks) {
+// counts, their exclusive scan, the chunk list and (acc != null) the accumulators in one
+// workgroup for k <= CL_MAX (the 1-D codebooks): one launch instead of four
+constexpr int CL_T = 1024, CL_MAX = 4096;
+__global__ __launch_bounds__(CL_T) void k_chunk_list_small(const uint32_t *__restrict__ start, int k,
+                                                           uint32_t *__restrict__ first, Chunk *__restrict__ chunks,
+                                                           SumAcc *acc) {
+    constexpr int PER = CL_MAX / CL_T;
+    __shared__ uint32_t wsum[CL_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t cnt[PER], mine = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {  // thread t owns clusters t*PER .. t*PER+PER-1
+        const int cl = t * PER + u;
+        cnt[u] = cl < k ? (start[cl + 1] - start[cl] + SC_CH - 1) / SC_CH : 0u;
+        mine += cnt[u];
+        if (acc && cl < k) acc[cl] = SumAcc{0.0, 0.0, 1 << 20, 0};
+    }
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (int i = 0; i < CL_T / 64; ++i) {
+        if (i < w) off += wsum[i];
+        total += wsum[i];
+    }
+    uint32_t o = off + incl - mine;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int cl = t * PER + u;
+        if (cl >= k) break;
+        first[cl] = o;
+        const uint32_t s0 = start[cl], s1 = start[cl + 1];
+        for (uint32_t b = s0; b < s1; b += SC_CH) chunks[o++] = Chunk{(uint32_t)cl, b, min(s1, b + SC_CH), 0u};
+    }
+    if (t == 0) first[k] = total;
+}
+
+// the chunk list of every cluster's member range (k clusters, start[k + 1]); acc (nullable):
+// the per-cluster accumulators to reset
+void chunk_list(st_ctx *c, const uint32_t *start, int k, uint32_t *ch_cnt, uint32_t *ch_first, Chunk *chunks,
+                SumAcc *acc = nullptr) {
+    if (k <= CL_MAX) {
+        hipLaunchKernelGGL(k_chunk_list_small, dim3(1), dim3(CL_T), 0, c->stream, start, k, ch_first, chunks, acc);
+        ST_LAUNCH_CHECK();
+        return;
+    }
     const unsigned gk = grid_for((uint64_t)k, 256, 1024);
     hipLaunchKernelGGL(k_chunk_counts, dim3(gk), dim3(256), 0, c->stream, start, k, ch_cnt);
     scan_u32(c, ch_cnt, ch_first, (uint64_t)k, ch_first + k);
     hipLaunchKernelGGL(k_chunk_list, dim3(gk), dim3(256), 0, c->stream, start, k, ch_first, chunks);
+    if (acc) hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, k);
     ST_LAUNCH_CHECK();
 }
 
@@ -767,8 +817,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             KTimer kt(c, "k1.sum");
             if (chunked) {
                 const unsigned gk = grid_for((uint64_t)k, 256, 1024);
-                chunk_list(c, start, k, ch_cnt, ch_first, chunks);
-                hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, k);
+                chunk_list(c, start, k, ch_cnt, ch_first, chunks, acc);
                 hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
                                    acc);
                 hipLaunchKernelGGL(k_sum1d_final, dim3(gk), dim3(256), 0, c->stream, acc, start, k, cen, seq_flag,
@@ -819,9 +868,8 @@ void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *sta
     auto *ch_first = wsT<uint32_t>(c, "d1.chfirst", (size_t)nk + 1);
     auto *chunks = wsT<Chunk>(c, "d1.chunks", maxch);
     auto *acc = wsT<SumAcc>(c, "d1.acc", (size_t)nk);
-    chunk_list(c, start, nk, ch_cnt, ch_first, chunks);
+    chunk_list(c, start, nk, ch_cnt, ch_first, chunks, acc);
     const unsigned gk = grid_for((uint64_t)nk, 256, 1024);
-    hipLaunchKernelGGL(k_sumacc_init, dim3(gk), dim3(256), 0, c->stream, acc, nk);
     hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + nk, acc);
     hipLaunchKernelGGL(k_partials_out, dim3(gk), dim3(256), 0, c->stream, acc, start, nk, sums, sabs, emin, counts);
     ST_LAUNCH_CHECK();
