@@ -205,6 +205,16 @@ int st_dev_sog(st_ctx *ctx, const st_table *table, int32_t iters, const double *
 int st_dev_minmax(st_ctx *ctx, const float *const *cols, int32_t ncols, uint64_t n, double *lo, double *hi);
 /* validates (ST_ERR_NONFINITE) and prepares the local point set for assign/partials */
 int st_dev_kmeans_prepare(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n);
+/* initializeCentroids (k-means.ts:8-20) over the global table of n rows, identical on every rank:
+ * rows (device, k entries) = the first k distinct floor(draw * n) in draw order; *used = draws
+ * consumed (replaces splat_dist's host selection; the owners then supply the rows) */
+int st_dev_kmeans_init_rows(st_ctx *ctx, const double *draws, uint64_t ndraws, uint64_t n, int32_t k,
+                            uint32_t *rows, uint64_t *used);
+/* out[c * k + i] (device) = cols[c][rows[i] - offset] for the rows this rank holds
+ * (offset <= rows[i] < offset + n_local), bit pattern 0 elsewhere: an integer SUM of the bit
+ * patterns over the ranks assembles the global rows exactly (-0 and NaN payloads included) */
+int st_dev_gather_rows(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n_local, uint64_t offset,
+                       const uint32_t *rows, int32_t k, float *out);
 /* exact nearest centroid (KdTree.findNearest semantics) of each local point */
 int st_dev_kmeans_assign(st_ctx *ctx, const float *const *cols, int32_t d, uint64_t n, int32_t k,
                          const float *centroids, uint32_t *labels);

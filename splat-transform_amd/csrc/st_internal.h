@@ -177,6 +177,13 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
 void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
                          uint8_t *sh);
 // returns draws consumed
+// initializeCentroids over a table of n rows: rows (device) = the k distinct floor(draw * n) in
+// draw order, *used = draws consumed (device window with the host loop as fallback)
+void kmeans_init_rows(st_ctx *c, const double *draws, uint64_t ndraws, uint64_t n, int k, uint32_t *rows,
+                      uint64_t *used);
+// out[c * k + i] = cols[c][rows[i] - offset] where offset <= rows[i] < offset + n_local, bits 0 elsewhere
+void gather_owned_rows(st_ctx *c, const float *const *cols, int d, uint64_t n_local, uint64_t offset,
+                       const uint32_t *rows, int k, float *out);
 // (host_init: initializeCentroids by the host's loop instead of on the device)
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
                     uint64_t ndraws, float *centroids, uint32_t *labels, bool host_init = false);

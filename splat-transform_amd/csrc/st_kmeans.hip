@@ -150,6 +150,18 @@ __global__ __launch_bounds__(256) void k_init_select(const double *__restrict__ 
     if (blockIdx.x == 0 && threadIdx.x == 0 && pos[m] < (uint32_t)k) st->err |= ERR_INIT_WINDOW;
 }
 
+// out[c][i] = the local row rows[i] - offset of column c where this rank holds it, bit
+// pattern 0 elsewhere (an integer SUM over the ranks then assembles every row exactly)
+__global__ __launch_bounds__(256) void k_gather_owned(const float *const *cols, int d, uint64_t n_local,
+                                                      uint64_t offset, const uint32_t *__restrict__ rows, int k,
+                                                      float *__restrict__ out) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) {
+        const uint64_t r = rows[i];
+        const bool mine = r >= offset && r - offset < n_local;
+        for (int c = 0; c < d; ++c) out[(uint64_t)c * k + i] = mine ? cols[c][r - offset] : 0.0f;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // update: cluster boundaries in the label-sorted member list
 __global__ __launch_bounds__(256) void k_bounds(const uint32_t *__restrict__ sorted_labels, uint64_t n, int k,
@@ -301,6 +313,80 @@ void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t 
     bounds_from_sorted(c, sorted_labels, n, k, start);
 }
 
+// initializeCentroids (k-means.ts:8-20) on the host: k distinct rows by rejection on the
+// Math.random stream; returns the draws consumed
+static uint64_t init_rows_host(const double *draws, uint64_t ndraws, uint64_t n, int k, std::vector<uint32_t> &rows) {
+    rows.resize(k);
+    std::vector<uint8_t> chosen(n, 0);
+    uint64_t cur = 0;
+    for (int i = 0; i < k; ++i) {
+        uint64_t cand;
+        do {
+            ST_REQUIRE(cur < ndraws, ST_ERR_DRAWS, "kmeans: Math.random draws exhausted during initialisation");
+            cand = (uint64_t)std::floor(draws[cur++] * (double)n);
+            ST_REQUIRE(cand < n, ST_ERR_ARG, "kmeans: Math.random draws must lie in [0, 1)");
+        } while (chosen[cand]);
+        chosen[cand] = 1;
+        rows[i] = (uint32_t)cand;
+    }
+    return cur;
+}
+
+// the same on the device over the first m draws of ddraws (already uploaded): rows (k, device),
+// the draws consumed in st->cursor, or ERR_INIT_WINDOW in st->err when the window holds fewer
+// than k distinct rows (or a draw outside [0, 1)); unset rows stay 0
+static void init_rows_dev(st_ctx *c, const double *ddraws, uint32_t m, uint64_t n, int k, uint32_t *drows,
+                          State *dstate) {
+    auto *first = wsT<uint32_t>(c, "km.ifirst", n);
+    auto *flags = wsT<uint32_t>(c, "km.iflags", m);
+    auto *pos = wsT<uint32_t>(c, "km.ipos", (size_t)m + 1);
+    ST_HIP(hipMemsetAsync(first, 0xff, n * sizeof(uint32_t), c->stream));
+    ST_HIP(hipMemsetAsync(drows, 0, (size_t)k * sizeof(uint32_t), c->stream));
+    const unsigned g = grid_for(m, 256, 1024);
+    hipLaunchKernelGGL(k_init_first, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, dstate);
+    hipLaunchKernelGGL(k_init_flags, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, flags);
+    scan_u32(c, flags, pos, m, pos + m);
+    hipLaunchKernelGGL(k_init_select, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, k, flags, pos, drows, dstate);
+    ST_LAUNCH_CHECK();
+}
+// draws the device init looks at: with n >= 4k the k-th distinct row comes after about
+// n ln(n / (n - k)) <= 1.151 k draws
+static uint64_t init_window(uint64_t ndraws, int k) { return std::min<uint64_t>(ndraws, (uint64_t)k + k / 4 + 4096); }
+
+void kmeans_init_rows(st_ctx *c, const double *draws, uint64_t ndraws, uint64_t n, int k, uint32_t *rows,
+                      uint64_t *used) {
+    ST_REQUIRE(n < (1ull << 31) && k > 0 && (uint64_t)k <= n, ST_ERR_ARG, "kmeans init: need 0 < k <= n < 2^31");
+    if (n >= 4 * (uint64_t)k && ndraws > 0 && !getenv("ST_KM_HOST_INIT")) {
+        const uint32_t m = (uint32_t)init_window(ndraws, k);
+        auto *ddraws = wsT<double>(c, "km.idraws", m);
+        auto *dstate = static_cast<State *>(ws(c, "km.istate", sizeof(State)));
+        State hs{};
+        ST_HIP(hipMemcpyAsync(dstate, &hs, sizeof(State), hipMemcpyHostToDevice, c->stream));
+        ST_HIP(hipMemcpyAsync(ddraws, draws, m * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        init_rows_dev(c, ddraws, m, n, k, rows, dstate);
+        ST_HIP(hipMemcpyAsync(&hs, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        if (!(hs.err & ERR_INIT_WINDOW)) {
+            *used = hs.cursor;
+            return;
+        }
+    }
+    std::vector<uint32_t> hrows;
+    *used = init_rows_host(draws, ndraws, n, k, hrows);
+    ST_HIP(hipMemcpyAsync(rows, hrows.data(), sizeof(uint32_t) * k, hipMemcpyHostToDevice, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));  // hrows is released on return
+}
+
+void gather_owned_rows(st_ctx *c, const float *const *cols, int d, uint64_t n_local, uint64_t offset,
+                       const uint32_t *rows, int k, float *out) {
+    ST_REQUIRE(d > 0 && d <= 4096 && k > 0, ST_ERR_ARG, "gather rows: bad shape");
+    auto **dcols = wsT<const float *>(c, "km.gcols", (size_t)d);
+    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_gather_owned, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, n_local,
+                       offset, rows, k, out);
+    ST_LAUNCH_CHECK();
+}
+
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
                     uint64_t ndraws, float *cen, uint32_t *labels, bool host_init) {
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans: n must be < 2^31 per device");
@@ -327,27 +413,13 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
         hipLaunchKernelGGL(k_init1d, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, mm, cen, k);
         ST_LAUNCH_CHECK();
     } else if (!host_init && !getenv("ST_KM_HOST_INIT") && n >= 4 * (uint64_t)k && ndraws > 0) {
-        // initializeCentroids on the device over a window of the draws (k-means.ts:8-20): with
-        // n >= 4k the k-th distinct row comes after ~n ln(n / (n - k)) <= 1.151 k draws; a
-        // window too short sets ERR_INIT_WINDOW and the call reruns with the host's loop
-        dev_init_m = (uint32_t)std::min<uint64_t>(ndraws, (uint64_t)k + k / 4 + 4096);
+        // initializeCentroids on the device over a window of the draws (init_rows_dev); a window
+        // too short sets ERR_INIT_WINDOW and the call reruns with the host's loop
+        dev_init_m = (uint32_t)init_window(ndraws, k);
     } else {
-        // initializeCentroids (k-means.ts:8-20): k distinct rows by rejection on the
-        // host-owned Math.random stream; the rows are then gathered on the device.
-        std::vector<uint32_t> rows(k);
-        std::vector<uint8_t> chosen(n, 0);
-        uint64_t cur = 0;
-        for (int i = 0; i < k; ++i) {
-            uint64_t cand;
-            do {
-                ST_REQUIRE(cur < ndraws, ST_ERR_DRAWS, "kmeans: Math.random draws exhausted during initialisation");
-                cand = (uint64_t)std::floor(draws[cur++] * (double)n);
-                ST_REQUIRE(cand < n, ST_ERR_ARG, "kmeans: Math.random draws must lie in [0, 1)");
-            } while (chosen[cand]);
-            chosen[cand] = 1;
-            rows[i] = (uint32_t)cand;
-        }
-        init_used = cur;
+        // initializeCentroids by the host's loop; the rows are then gathered on the device
+        std::vector<uint32_t> rows;
+        init_used = init_rows_host(draws, ndraws, n, k, rows);
         auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
         ST_HIP(hipMemcpyAsync(drows, rows.data(), sizeof(uint32_t) * k, hipMemcpyHostToDevice, c->stream));
         hipLaunchKernelGGL(k_gather_init, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, drows, k,
@@ -364,19 +436,9 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     const uint64_t ndraws_all = ndraws;
     ndraws = window;
     if (dev_init_m) {
-        const uint32_t m = dev_init_m;
-        auto *first = wsT<uint32_t>(c, "km.ifirst", n);
-        auto *flags = wsT<uint32_t>(c, "km.iflags", m);
-        auto *pos = wsT<uint32_t>(c, "km.ipos", (size_t)m + 1);
-        auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
-        ST_HIP(hipMemsetAsync(first, 0xff, n * sizeof(uint32_t), c->stream));
         // rows a short window leaves unset stay 0: the discarded run still reads inside the table
-        ST_HIP(hipMemsetAsync(drows, 0, (size_t)k * sizeof(uint32_t), c->stream));
-        const unsigned g = grid_for(m, 256, 1024);
-        hipLaunchKernelGGL(k_init_first, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, dstate);
-        hipLaunchKernelGGL(k_init_flags, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, first, flags);
-        scan_u32(c, flags, pos, m, pos + m);
-        hipLaunchKernelGGL(k_init_select, dim3(g), dim3(256), 0, c->stream, ddraws, m, n, k, flags, pos, drows, dstate);
+        auto *drows = wsT<uint32_t>(c, "km.initrows", (size_t)k);
+        init_rows_dev(c, ddraws, dev_init_m, n, k, drows, dstate);
         hipLaunchKernelGGL(k_gather_init, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, drows, k,
                            cen);
         ST_LAUNCH_CHECK();

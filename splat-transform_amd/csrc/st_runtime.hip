@@ -419,6 +419,24 @@ int st_dev_kmeans_assign(st_ctx *c, const float *const *cols, int32_t d, uint64_
     });
 }
 
+int st_dev_kmeans_init_rows(st_ctx *c, const double *draws, uint64_t ndraws, uint64_t n, int32_t k, uint32_t *rows,
+                            uint64_t *used) {
+    return guarded([&] {
+        ST_ARG(c && (draws || ndraws == 0) && k > 0 && rows && used, "bad argument");
+        use_device(c);
+        kmeans_init_rows(c, draws, ndraws, n, k, rows, used);
+    });
+}
+
+int st_dev_gather_rows(st_ctx *c, const float *const *cols, int32_t d, uint64_t n_local, uint64_t offset,
+                       const uint32_t *rows, int32_t k, float *out) {
+    return guarded([&] {
+        ST_ARG(c && cols && d > 0 && k > 0 && rows && out, "bad argument");
+        use_device(c);
+        gather_owned_rows(c, cols, d, n_local, offset, rows, k, out);
+    });
+}
+
 int st_dev_kmeans_partials(st_ctx *c, const float *const *cols, int32_t d, uint64_t n, int32_t nseg, int32_t k,
                            const uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
     return guarded([&] {

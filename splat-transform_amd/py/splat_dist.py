@@ -132,6 +132,16 @@ class HipOps:
     def minmax(self, cols):
         return self.ctx.dev_minmax(cols)
 
+    def init_rows(self, draws, n, k):
+        rows = self.empty((k,), torch.int32)
+        used = self.ctx.dev_kmeans_init_rows(draws, n, k, rows)
+        return rows, used
+
+    def gather_rows(self, pts, offset, rows):
+        out = self.empty((len(pts), rows.shape[0]), torch.float32)
+        self.ctx.dev_gather_rows(pts, offset, rows, out)
+        return out
+
     def prepare(self, pts):
         self.ctx.dev_kmeans_prepare(pts)
 
@@ -241,22 +251,6 @@ def _gather_rows(ops, comm, P, rows):
     return out[:, :m]
 
 
-def _distinct_rows(draws, cursor, k, N):
-    """initializeCentroids (k-means.ts:8-20): rows floor(draw * N), rejecting repeats, until k
-    distinct -- vectorised: the first k distinct values in draw order"""
-    m = 2 * k + 64
-    while True:
-        chunk = draws[cursor:cursor + m]
-        g = np.floor(np.asarray(chunk, dtype=np.float64) * N).astype(np.int64)
-        _, first = np.unique(g, return_index=True)
-        first.sort()
-        if first.size >= k:
-            return g[first[:k]], cursor + int(first[k - 1]) + 1
-        if cursor + m >= len(draws):
-            raise sh.StError(sh.ST_ERR_DRAWS, 'kmeans: Math.random draws exhausted during initialisation')
-        m *= 2
-
-
 def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
     """kmeans over the global table (k-means.ts:137-201, --no-gpu results).
 
@@ -277,8 +271,12 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
         cen_np = (m + (M - m) * i / (k - 1)).astype(np.float32)  # initializeCentroids1D (k-means.ts:23-39)
         cen = torch.from_numpy(cen_np).to(P.pts[0].device).reshape(1, k)
     else:
-        rows, cursor = _distinct_rows(draws, cursor, k, P.N)
-        cen = _gather_rows(ops, comm, P, rows).contiguous()
+        # initializeCentroids: the same k global rows on every rank (st_dev_kmeans_init_rows); each
+        # rank supplies the rows it holds, the others' bit patterns are 0, an integer SUM assembles them
+        rows, used = ops.init_rows(draws[cursor:], P.N, k)
+        cursor += used
+        cen = ops.gather_rows(P.pts, shard.off, rows).contiguous()
+        comm.allreduce(cen.view(torch.int32))
     labels = ops.empty((n,), torch.int32)
     for _ in range(iters):
         ops.assign(P.pts, k, cen, labels)

@@ -87,7 +87,8 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
-    'st_dev_minmax', 'st_dev_kmeans_prepare', 'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
+    'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
+    'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
@@ -556,6 +557,21 @@ class Context:
         check(lib().st_dev_kmeans_seqsum(self.h, ctypes.c_int32(d), ctypes.c_int32(k), ctypes.c_int32(seg),
                                          _ptr(pairs), ctypes.c_uint32(len(pairs)), _ptr(running), _ptr(emin),
                                          _ptr(sabs)))
+
+    def dev_kmeans_init_rows(self, draws, n, k, rows):
+        """initializeCentroids over n global rows: rows (device uint32/int32, k) filled; returns draws used"""
+        used = ctypes.c_uint64(0)
+        draws = np.ascontiguousarray(draws, dtype=np.float64)
+        check(lib().st_dev_kmeans_init_rows(self.h, _vp(draws), ctypes.c_uint64(len(draws)), ctypes.c_uint64(n),
+                                            ctypes.c_int32(k), _ptr(rows), ctypes.byref(used)))
+        return used.value
+
+    def dev_gather_rows(self, col_list, offset, rows, out):
+        """out (device f32, d*k) = the rows this rank holds, bit pattern 0 elsewhere"""
+        d, k = len(col_list), len(rows)
+        ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in col_list])
+        check(lib().st_dev_gather_rows(self.h, ptrs, ctypes.c_int32(d), ctypes.c_uint64(len(col_list[0])),
+                                       ctypes.c_uint64(offset), _ptr(rows), ctypes.c_int32(k), _ptr(out)))
 
     def dev_kmeans_finish(self, d, k, sums, sabs, emin, counts, centroids, pending):
         np_ = ctypes.c_uint32(0)

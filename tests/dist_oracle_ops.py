@@ -36,6 +36,28 @@ class OracleOps:
             hi.append(float(a.max()) if a.size else float('-inf'))
         return lo, hi
 
+    def init_rows(self, draws, n, k):
+        """initializeCentroids (k-means.ts:8-20): the reference's rejection loop over the global n"""
+        rows, chosen, cur = [], set(), 0
+        while len(rows) < k:
+            if cur >= len(draws):
+                raise sh.StError(sh.ST_ERR_DRAWS, 'kmeans: Math.random draws exhausted during initialisation')
+            r = int(np.floor(draws[cur] * n))
+            cur += 1
+            if r not in chosen:
+                chosen.add(r)
+                rows.append(r)
+        return torch.tensor(rows, dtype=torch.int64), cur
+
+    def gather_rows(self, pts, offset, rows):
+        n = pts[0].shape[0]
+        out = torch.zeros((len(pts), rows.shape[0]), dtype=torch.float32)
+        for i, r in enumerate(rows.tolist()):
+            if offset <= r < offset + n:
+                for j, p in enumerate(pts):
+                    out[j, i] = p[r - offset]
+        return out
+
     def prepare(self, pts):
         if not all(np.isfinite(p.numpy()).all() for p in pts):
             raise sh.StError(sh.ST_ERR_NONFINITE, 'kmeans: non-finite point')
