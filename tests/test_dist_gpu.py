@@ -20,7 +20,7 @@ NAMES = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in 
     ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
 
 
-def _table(n, seed):
+def _table(n, seed, C=15):
     rng = np.random.default_rng(seed)
     cols = {}
     cube = rng.random(n) < 0.05
@@ -28,7 +28,7 @@ def _table(n, seed):
         cols[a] = np.where(cube, off + rng.random(n) * 1e-3, rng.normal(0, 10, n)).astype(np.float32)
     for i in range(3):
         cols[f'f_dc_{i}'] = rng.normal(0, 1, n).astype(np.float32)
-    for i in range(45):
+    for i in range(3 * C):
         cols[f'f_rest_{i}'] = (rng.normal(0, 0.1, n)).astype(np.float32)
     cols['opacity'] = rng.normal(0, 2, n).astype(np.float32)
     for i in range(3):
@@ -38,7 +38,7 @@ def _table(n, seed):
     return cols
 
 
-def _rank(rank, world, backend, port, n, seed, iters, q):
+def _rank(rank, world, backend, port, n, seed, iters, q, C=15):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dev = torch.device('cuda', 0)
@@ -46,8 +46,8 @@ def _rank(rank, world, backend, port, n, seed, iters, q):
     dist.init_process_group(backend, rank=rank, world_size=world)
     import splat_hip as sh
     import splat_dist
-    full = _table(n, seed)
-    cuts = {1: [0, n], 2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
+    full = _table(n, seed, C)
+    cuts = {1: [0, n], 3: [0, n // 5, n * 3 // 5, n], 2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
     lo, hi = cuts[rank], cuts[rank + 1]
     cols = {k: torch.from_numpy(v[lo:hi].copy()).to(dev) for k, v in full.items()}
     draws = np.random.default_rng(seed + 1).random(1 << 20)
@@ -62,6 +62,25 @@ def _rank(rank, world, backend, port, n, seed, iters, q):
         q.put(dict(tex={k: v.cpu().numpy() for k, v in tex.items()}, meta=meta, used=used, zip=z))
     dist.destroy_process_group()
     ctx.close()
+
+
+def _collect(q, procs, count, timeout=600):
+    """count results from the rank processes; fails at once when a rank dies (the others would
+    wait in a collective until gloo's timeout)"""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < count:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > timeout:
+                for p in procs:
+                    if p.is_alive():
+                        p.kill()
+                raise AssertionError(f'rank process failed (exit codes {[p.exitcode for p in procs]})')
+    return out
 
 
 def _adversarial_1d(n, seed):
@@ -145,13 +164,13 @@ def test_dist_cluster1d_adversarial_matches_single_device(world, cap):
     procs = [mctx.Process(target=_c1d_rank, args=(r, world, port, n, seed, iters, q, cap)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=600) for _ in range(world)), key=lambda r: r['rank'])
+    res = sorted(_collect(q, procs, world), key=lambda r: r['rank'])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     p = mctx.Process(target=_single_c1d, args=(q, n, seed, iters, cap))
     p.start()
-    one = q.get(timeout=600)
+    one = _collect(q, [p], 1)[0]
     p.join(timeout=120)
     assert p.exitcode == 0
     for r in res:
@@ -161,11 +180,13 @@ def test_dist_cluster1d_adversarial_matches_single_device(world, cap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('backend,world', [('gloo', 2), ('gloo', 4), ('nccl', 1)])
-def test_multi_rank_write_sog_matches_single_device(backend, world):
-    """gloo: 2 and 4 ranks sharing cuda:0.  nccl: RCCL refuses two ranks on one GPU, so the
+@pytest.mark.parametrize('backend,world,C', [('gloo', 2, 15), ('gloo', 4, 15), ('nccl', 1, 15), ('gloo', 2, 0),
+                                             ('gloo', 3, 3), ('gloo', 2, 8)])
+def test_multi_rank_write_sog_matches_single_device(backend, world, C):
+    """gloo: 2 to 4 ranks sharing cuda:0.  nccl: RCCL refuses two ranks on one GPU, so the
     RCCL leg runs the same sharded code path at world size 1 (device-tensor collectives,
-    every dtype / reduce op the 8-GPU job issues)."""
+    every dtype / reduce op the 8-GPU job issues).  C: SH coefficients per channel (bands
+    3, 0, 1, 2; write-sog.ts:296)."""
     import torch.multiprocessing as mp
     import splat_hip as sh
     n, seed, iters = 24000, 5, 3
@@ -175,21 +196,23 @@ def test_multi_rank_write_sog_matches_single_device(backend, world):
     s.close()
     mctx = mp.get_context('spawn')
     q = mctx.Queue()
-    procs = [mctx.Process(target=_rank, args=(r, world, backend, port, n, seed, iters, q)) for r in range(world)]
+    procs = [mctx.Process(target=_rank, args=(r, world, backend, port, n, seed, iters, q, C)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=600)
+    res = _collect(q, procs, 1)[0]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
 
     dev = torch.device('cuda', 0)
-    full = _table(n, seed)
+    full = _table(n, seed, C)
     cols = {k: torch.from_numpy(v).to(dev) for k, v in full.items()}
-    W, H, pal, cw, ch = sh.sog_geometry(n, 15)
+    W, H, pal, cw, ch = sh.sog_geometry(n, C)
     u8 = dict(device=dev, dtype=torch.uint8)
-    tex = {k: torch.zeros(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
-    tex['shN_centroids'] = torch.zeros(cw * ch * 4, **u8)
+    keys = ('means_l', 'means_u', 'quats', 'scales', 'sh0') + (('shN_labels',) if C else ())
+    tex = {k: torch.zeros(W * H * 4, **u8) for k in keys}
+    if C:
+        tex['shN_centroids'] = torch.zeros(cw * ch * 4, **u8)
     draws = np.random.default_rng(seed + 1).random(1 << 20)
     ctx = sh.Context(0)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -200,7 +223,8 @@ def test_multi_rank_write_sog_matches_single_device(backend, world):
         assert np.array_equal(res['tex'][k], v.cpu().numpy()), k
     m = res['meta']
     assert list(m['means_min']) == list(meta.means_min) and list(m['means_max']) == list(meta.means_max)
-    for k in ('scales_codebook', 'sh0_codebook', 'shn_codebook'):
+    assert set(res['tex']) == set(tex)
+    for k in ('scales_codebook', 'sh0_codebook') + (('shn_codebook',) if C else ()):
         assert np.array_equal(np.asarray(m[k]).view(np.uint32), np.array(getattr(meta, k), np.float32).view(np.uint32)), k
     # identical .sog archive
     assert ctx.dev_sog_bundle(meta, n, tex, 0x6a2b, 0x58b1) == res['zip']
