@@ -216,3 +216,59 @@ def test_cluster1d_ties_and_duplicates_vs_oracle(ctx, levels):
     assert rc == 0 and used == oused
     assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
     assert np.array_equal(labels, olabels)
+
+
+def test_kmeans_bench_size_first_assign_and_update(ctx):
+    """The bench's SH k-means at full size (10M x 45, K = 65,536; SURVEY 8d data): one
+    iteration, checked through size-independent properties.  The init rows are the first K
+    distinct floor(draw * n) (k-means.ts:8-20); every sampled label must reach the exact f64
+    minimum over those K centroids (kd-tree.ts:26-35 order), and sampled centroids must equal
+    the sequential f64 mean of their members (calcAverage, k-means.ts:41-63)."""
+    import torch
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1002)
+    n, d, k = 10_000_000, 45, 65536
+    cols = [torch.randn(n, generator=g, device=dev) * 0.1 for _ in range(d)]
+    draws = np.random.default_rng(42).random(4 * k)
+    cen = torch.empty(d * k, device=dev)
+    labels = torch.empty(n, dtype=torch.int32, device=dev)
+    used = ctx.dev_kmeans(cols, k, 1, draws, cen, labels)
+    torch.cuda.synchronize()
+    # the init rows, as the reference draws them
+    rows, seen, cur = [], set(), 0
+    while len(rows) < k:
+        r = int(np.floor(draws[cur] * n))
+        cur += 1
+        if r not in seen:
+            seen.add(r)
+            rows.append(r)
+    assert used >= cur  # the init consumed exactly cur draws; re-seeds may add more
+    ridx = torch.tensor(rows, device=dev)
+    c0 = torch.stack([c[ridx] for c in cols]).double()  # (d, k) init centroids
+    sample = torch.randint(0, n, (4096,), generator=g, device=dev)
+    lab = labels[sample].long()
+    bad = 0
+    for s in range(0, sample.numel(), 512):
+        idx = sample[s:s + 512]
+        dist = torch.zeros(idx.numel(), k, dtype=torch.float64, device=dev)
+        for j in range(d):
+            v = c0[j][None, :] - cols[j][idx].double()[:, None]
+            dist += v * v
+        got = dist.gather(1, lab[s:s + 512, None]).squeeze(1)
+        bad += int((got != dist.min(1).values).sum().item())
+    assert bad == 0, f'{bad} of 4096 sampled labels miss the exact f64 minimum'
+    # the update: sequential f64 means of a few clusters' members (ascending point order)
+    lab_all = labels.long()
+    cen = cen.view(d, k)
+    for cl in torch.randint(0, k, (6,), generator=g, device=dev).tolist():
+        members = torch.nonzero(lab_all == cl).flatten()
+        if members.numel() == 0:
+            continue  # re-seeded
+        vals = torch.stack([c[members] for c in cols]).cpu().numpy().astype(np.float64)
+        for j in range(d):
+            acc = 0.0
+            for v in vals[j]:
+                acc += float(v)
+            want = np.float32(acc / members.numel())
+            assert np.float32(cen[j, cl].item()).view(np.uint32) == want.view(np.uint32), (cl, j)
