@@ -233,7 +233,9 @@ def test_kmeans_bench_size_first_assign_and_update(ctx):
     draws = np.random.default_rng(42).random(4 * k)
     cen = torch.empty(d * k, device=dev)
     labels = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # the context runs on its own stream
     used = ctx.dev_kmeans(cols, k, 1, draws, cen, labels)
+    ctx.synchronize()
     torch.cuda.synchronize()
     # the init rows, as the reference draws them
     rows, seen, cur = [], set(), 0
