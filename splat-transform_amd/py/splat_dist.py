@@ -74,6 +74,18 @@ class Comm:
         dist.gather(x, out, dst=dst, group=self.group)
         return None if out is None else [o.to(t.device) for o in out]
 
+    def gather_async(self, t, dst=0):
+        """gather() issued without waiting: returns wait() -> the list on rank dst, None elsewhere.
+        `t` must stay untouched until wait() returns."""
+        x = self._io(t)
+        out = [torch.empty_like(x) for _ in range(self.world)] if self.rank == dst else None
+        work = dist.gather(x, out, dst=dst, group=self.group, async_op=True)
+
+        def wait():
+            work.wait()
+            return None if out is None else [o.to(t.device) for o in out]
+        return wait
+
     def allgather(self, t):
         """list of every rank's tensor (shapes may differ in dim 0)"""
         x = self._io(t)
@@ -353,10 +365,13 @@ def write_sog(ops, comm, cols, iters, draws):
     meta['scales_codebook'] = scb.cpu().numpy()
     meta['sh0_codebook'] = ccb.cpu().numpy()
     # texels of this rank's rows in local row order (4 B per row and texture); rank 0
-    # gathers them and places them at their global Morton positions
-    keys = ('means_l', 'means_u', 'quats', 'scales', 'sh0') + (('shN_labels',) if C else ())
-    loc = {k: torch.zeros(shard.n * 4, dtype=torch.uint8, device=dev) for k in keys}
-    shn_lab = None
+    # gathers them and places them at their global Morton positions.  The five textures
+    # that do not wait for the SH k-means go out now, their gathers overlapping it.
+    rows = torch.arange(shard.n, dtype=torch.int32, device=dev)
+    early = ('means_l', 'means_u', 'quats', 'scales', 'sh0')
+    loc = {k: torch.zeros(shard.n * 4, dtype=torch.uint8, device=dev) for k in early}
+    m = ops.scatter(cols, rows, lo, hi, slab, clab, None, loc)
+    pending = gather_texels_start(comm, shard, loc)
     shn_cent = None
     if C:
         D = 3 * C
@@ -369,9 +384,10 @@ def write_sog(ops, comm, cols, iters, draws):
         if comm.rank == 0:
             shn_cent = torch.zeros(cw * ch * 4, dtype=torch.uint8, device=dev)
             ops.shn_centroids(ncl, C, pal, shn_cent)
-    rows = torch.arange(shard.n, dtype=torch.int32, device=dev)
-    m = ops.scatter(cols, rows, lo, hi, slab, clab, shn_lab, loc)
-    tex = gather_texels(comm, shard, loc, pos_all, W * H)
+        late = {'shN_labels': torch.zeros(shard.n * 4, dtype=torch.uint8, device=dev)}
+        ops.scatter(cols, rows, lo, hi, None, None, shn_lab, late)
+        pending.update(gather_texels_start(comm, shard, late))
+    tex = gather_texels_finish(comm, shard, pending, pos_all, W * H)
     if comm.rank != 0:
         return None, None, cursor
     if shn_cent is not None:
@@ -387,17 +403,30 @@ def gather_texels(comm, shard, loc, pos_all, size):
     point-to-point transfer per rank, N x 4 B per texture in total, instead of a sum-reduce of
     whole textures) and places global row r at pos_all[r], its position in the Morton order.
     Texels past the table stay zero, as in the single-device writer."""
+    return gather_texels_finish(comm, shard, gather_texels_start(comm, shard, loc), pos_all, size)
+
+
+def gather_texels_start(comm, shard, loc):
+    """issue the (asynchronous) gathers of gather_texels; returns the pending transfers"""
     m = max(shard.counts)
-    out = {}
+    pending = {}
     for key, t in loc.items():
         v = t.view(torch.int32)
         pad = torch.zeros(m, dtype=torch.int32, device=v.device)
         pad[:v.numel()] = v
-        parts = comm.gather(pad, 0)
+        pending[key] = comm.gather_async(pad, 0)
+    return pending
+
+
+def gather_texels_finish(comm, shard, pending, pos_all, size):
+    """wait for the gathers and place the rows on rank 0 (see gather_texels)"""
+    out = {}
+    for key, wait in pending.items():
+        parts = wait()
         if parts is None:
             continue
         full = torch.cat([p[:c] for p, c in zip(parts, shard.counts)])
-        tex = torch.zeros(size, dtype=torch.int32, device=v.device)
+        tex = torch.zeros(size, dtype=torch.int32, device=full.device)
         tex[pos_all.long()] = full
         out[key] = tex.view(torch.uint8)
     return out if comm.rank == 0 else None
