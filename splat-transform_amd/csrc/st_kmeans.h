@@ -63,8 +63,9 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n);  // wo
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
                km::State *dstate);
 // returns true when it also wrote the update's (label, value bits) pairs into keys/vals
+// (need_labels = false with keys: the labels are not written, only the pairs)
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,
-              uint32_t *keys = nullptr, uint32_t *vals = nullptr);
+              uint32_t *keys = nullptr, uint32_t *vals = nullptr, bool need_labels = true);
 // the multi-GPU update's 1-D pieces (st_kmeans1d.hip's chunked kernels): per-(segment,
 // cluster) partials of the label-sorted value bits (nk = nseg * k ranges of start), and the
 // exact replay of the pending clusters' sums over one segment (start: that segment's k + 1

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict
         uint32_t lab;
         if (!tie) lab = si[dl < dr ? L : R];
         else lab = kd1_walk(p, k, val, idx);
-        labels[i] = lab;
+        if (labels) labels[i] = lab;  // only the last iteration's labels are the result
         if (keys) {  // the member-sort pairs of the update (label, value bits)
             keys[i] = lab;
             vals[i] = __builtin_bit_cast(uint32_t, pf);
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(256) void k_pend_out(const uint32_t *__restrict__ p
 // one exact 1-D assign: KdTree build == stable sort of the centroid values
 // (kd-tree.ts:73-99), then the walk simulation
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels, uint32_t *keys,
-              uint32_t *vals) {
+              uint32_t *vals, bool need_labels) {
     auto *ckeys = wsT<uint32_t>(c, "k1.ckeys", (size_t)k);
     auto *corder = wsT<uint32_t>(c, "k1.corder", (size_t)k);
     hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
@@ -765,8 +765,8 @@ bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, 
     const unsigned g = grid_for(n, 256, 256 * 16);
     KTimer kt(c, "k1.assign");
     if (k <= KD1_LDS && !getenv("ST_KD1_WALK")) {
-        hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels, keys,
-                           vals);
+        hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
+                           (keys && !need_labels) ? (uint32_t *)nullptr : labels, keys, vals);
         ST_LAUNCH_CHECK();
         return keys != nullptr;
     } else if (k <= KD1_LDS)
@@ -801,7 +801,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
     for (int it = 0; it < iters; ++it) {
-        const bool paired = assign1d(c, pts, n, k, cen, labels, keys, vals);
+        const bool paired = assign1d(c, pts, n, k, cen, labels, keys, vals, it == iters - 1);
         mark(c, "k1.assign");
         // update
         if (!paired) {
