@@ -60,23 +60,9 @@ class Comm:
             t.copy_(x)
         return t
 
-    def reduce_sum(self, t, dst=0):
-        x = self._io(t)
-        dist.reduce(x, dst=dst, op=dist.ReduceOp.SUM, group=self.group)
-        if x is not t:
-            t.copy_(x)
-        return t
-
-    def gather(self, t, dst=0):
-        """list of every rank's tensor (equal shapes) on rank dst, None elsewhere"""
-        x = self._io(t)
-        out = [torch.empty_like(x) for _ in range(self.world)] if self.rank == dst else None
-        dist.gather(x, out, dst=dst, group=self.group)
-        return None if out is None else [o.to(t.device) for o in out]
-
     def gather_async(self, t, dst=0):
-        """gather() issued without waiting: returns wait() -> the list on rank dst, None elsewhere.
-        `t` must stay untouched until wait() returns."""
+        """every rank's tensor (equal shapes) gathered on rank dst, issued without waiting: returns
+        wait() -> the list on rank dst, None elsewhere.  `t` must stay untouched until wait() returns."""
         x = self._io(t)
         out = [torch.empty_like(x) for _ in range(self.world)] if self.rank == dst else None
         work = dist.gather(x, out, dst=dst, group=self.group, async_op=True)
