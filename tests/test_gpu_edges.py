@@ -188,3 +188,46 @@ def test_kmeans_draw_outside_unit_interval_fails(ctx):
     draws[10] = 1.0
     with pytest.raises(sh.StError):
         ctx.kmeans(cols, k, 2, draws)
+
+
+@pytest.mark.parametrize('case', ['device', 'short_window', 'small_n'])
+def test_step_api_init_rows_and_gather(ctx, case):
+    """st_dev_kmeans_init_rows (the sharded k-means init): the reference's rejection loop
+    (k-means.ts:8-20) over the global n -- on the device when n >= 4k, by the host when the
+    draw window is short or n < 4k -- and st_dev_gather_rows' owned-row assembly."""
+    import torch
+    dev = torch.device('cuda', 0)
+    k = 4096
+    n = 3 * k if case == 'small_n' else 100_000
+    rng = np.random.default_rng(21)
+    draws = rng.random(8 * k)
+    if case == 'short_window':
+        draws[:k + k // 4 + 5000] = (rng.integers(0, 9, k + k // 4 + 5000) + 0.5) / n
+    want, seen, cur = [], set(), 0
+    while len(want) < k:
+        r = int(np.floor(draws[cur] * n))
+        cur += 1
+        if r not in seen:
+            seen.add(r)
+            want.append(r)
+    rows = torch.empty(k, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    used = ctx.dev_kmeans_init_rows(draws, n, k, rows)
+    ctx.synchronize()
+    assert used == cur
+    assert rows.cpu().numpy().tolist() == want
+    # owned-row gather: two shards of the table, assembled by an integer sum of the bit patterns
+    d = 5
+    cols = [torch.from_numpy(rng.normal(0, 1, n).astype(np.float32)).to(dev) for _ in range(d)]
+    cols[0][int(want[0])] = -0.0
+    cut = n // 3
+    parts = []
+    for lo, hi in ((0, cut), (cut, n)):
+        out = torch.empty((d, k), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        ctx.dev_gather_rows([c[lo:hi].contiguous() for c in cols], lo, rows, out)
+        ctx.synchronize()
+        parts.append(out.view(torch.int32))
+    got = (parts[0] + parts[1]).view(torch.float32).cpu().numpy()
+    ref = np.stack([c.cpu().numpy()[want] for c in cols])
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
