@@ -39,9 +39,10 @@ __global__ __launch_bounds__(256) void k_seg_keys(const uint32_t *labels, uint64
     }
 }
 
-// N-D partials: one wave per (segment, cluster), lane = dimension; the reference's
-// sequential f64 sum over the members in ascending point order, sum|x| and the
-// smallest ulp exponent.  Layout [seg][dim][k].
+// N-D partials: one wave per (segment, cluster), lane = dimension; f64 sum, sum|x| and the
+// smallest ulp exponent of the members.  The sum is used only where the certificate holds
+// (every partial sum exact, in any order), so it is kept in 4 interleaved accumulators:
+// a quarter of the dependent f64 add chain.  Layout [seg][dim][k].
 __global__ __launch_bounds__(256) void k_partials_nd(const float *__restrict__ aos, int d,
                                                      const uint32_t *__restrict__ members,
                                                      const uint32_t *__restrict__ start, int k, int nseg,
@@ -55,27 +56,26 @@ __global__ __launch_bounds__(256) void k_partials_nd(const float *__restrict__ a
     if (lane == 0) counts[sc] = s1 - s0;
     if (lane >= d) return;
     const int ld = aos_ld(d);
-    double sum = 0, sa = 0;
+    double sum[4] = {0, 0, 0, 0}, sa[4] = {0, 0, 0, 0};
     int em = 1 << 20;
-    auto add = [&](float v) {
-        sum += (double)v;
-        sa += (double)__builtin_fabsf(v);
+    auto add = [&](float v, int a) {
+        sum[a] += (double)v;
+        sa[a] += (double)__builtin_fabsf(v);
         if (v != 0.0f) em = min(em, ulp_exp(v));
     };
     uint32_t j = s0;
-    // 16 member rows in flight per wave (the adds stay in ascending point order), as k_sumnd
-    constexpr int U = 16;
+    constexpr int U = 16;  // member rows in flight per wave
     for (; j + U <= s1; j += U) {
         float v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
 #pragma unroll
-        for (int u = 0; u < U; ++u) add(v[u]);
+        for (int u = 0; u < U; ++u) add(v[u], u & 3);
     }
-    for (; j < s1; ++j) add(aos[(uint64_t)members[j] * ld + lane]);
+    for (; j < s1; ++j) add(aos[(uint64_t)members[j] * ld + lane], 0);
     const uint64_t o = ((uint64_t)seg * d + lane) * k + cl;
-    sums[o] = sum;
-    sabs[o] = sa;
+    sums[o] = (sum[0] + sum[1]) + (sum[2] + sum[3]);
+    sabs[o] = (sa[0] + sa[1]) + (sa[2] + sa[3]);
     emin[o] = em;
 }
 
