@@ -30,12 +30,19 @@ using namespace km;
 
 
 // sort key of point i: (segment, label)
-__global__ __launch_bounds__(256) void k_seg_keys(const uint32_t *labels, uint64_t n, uint64_t seg_len, int k,
+// (n < 2^31: 32-bit index arithmetic; the segment of i advances by a compare, not a division)
+__global__ __launch_bounds__(256) void k_seg_keys(const uint32_t *labels, uint32_t n, uint32_t seg_len, int k,
                                                   const float *vals, uint32_t *keys, uint32_t *payload) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        keys[i] = (uint32_t)(i / seg_len) * (uint32_t)k + labels[i];
-        payload[i] = vals ? __builtin_bit_cast(uint32_t, vals[i]) : (uint32_t)i;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t seg = i / seg_len, next = (seg + 1) * seg_len;
+    for (; i < n; i += stride) {
+        while (i >= next) {
+            ++seg;
+            next += seg_len;
+        }
+        keys[i] = seg * (uint32_t)k + labels[i];
+        payload[i] = vals ? __builtin_bit_cast(uint32_t, vals[i]) : i;
     }
 }
 
@@ -208,7 +215,9 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
     auto *start = wsT<uint32_t>(c, "ds.start", nk + 1);
     int bits = 1;
     while ((1ull << bits) < nk) ++bits;
-    hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, n, n / nseg, k,
+    ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans partials: n must be < 2^31 per device");
+    hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                       (uint32_t)(n / nseg), k,
                        d == 1 ? cols[0] : (const float *)nullptr, keys, payload);
     ST_LAUNCH_CHECK();
     radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
