@@ -194,6 +194,78 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
         os.rmdir(d)
 
 
+def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
+    """Re-run the step with the library's k-means snapshot on (outside the timed region) and
+    check its output against the reference's definitions (k-means.ts:137-201, kd-tree.ts:22-70):
+      * the textures equal those of the last timed step (the verified step IS the timed one);
+      * sampled SH labels are exact f64 argmins (sequential sum of (c - p)^2 over the 45 dims,
+        kd-tree.ts:26-33) over the centroids the last assign used; an exact tie (KdTree order
+        decides) is counted, not checked;
+      * sampled centroids are the f32-rounded sequential f64 means of their members in
+        ascending point order (calcAverage, k-means.ts:41-63);
+      * every shN_labels texel holds the label of the row at its Morton position."""
+    import numpy as np
+    import torch
+    dev = cols['x'].device
+    before = {k: v.clone() for k, v in tex.items()}
+    ctx.set_verify(True)
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_verify(False)
+    same = all(torch.equal(before[k], tex[k]) for k in tex)
+    del before
+    prev, cen, lab = ctx.verify_snapshot(dev)
+    d, k = prev.shape
+    n = lab.shape[0]
+    sh = torch.stack([cols[f'f_rest_{i}'] for i in range(d)])  # [d, n] f32
+    g = torch.Generator(device='cpu')
+    g.manual_seed(seed)
+    pts = torch.randint(0, n, (n_labels,), generator=g).to(dev)
+    lab64 = lab.long()
+    pd_all = sh[:, pts].double()
+    cd = prev.double()
+    bad_labels, ties = 0, 0
+    for s in range(0, n_labels, 256):
+        e = min(n_labels, s + 256)
+        dist = torch.zeros(e - s, k, dtype=torch.float64, device=dev)
+        for j in range(d):
+            v = cd[j][None, :] - pd_all[j, s:e][:, None]
+            dist += v * v
+        mn = dist.min(1).values
+        got = dist.gather(1, lab64[pts[s:e], None]).squeeze(1)
+        nmin = (dist == mn[:, None]).sum(1)
+        bad_labels += int((got != mn).sum().item())
+        ties += int((nmin > 1).sum().item())
+    # centroids: sequential f64 mean of the members (numpy cumsum is a left-to-right chain)
+    counts = torch.bincount(lab64, minlength=k)
+    nonempty = torch.nonzero(counts > 0).squeeze(1)
+    pick = nonempty[torch.randperm(nonempty.numel(), generator=g)[:n_clusters - 1].to(dev)]
+    pick = torch.cat([pick, torch.argmax(counts)[None]])
+    bad_cen = 0
+    cen_h = cen.cpu().numpy()
+    for c in pick.tolist():
+        members = torch.nonzero(lab64 == c).squeeze(1)
+        vals = sh[:, members].double().cpu().numpy()
+        mean = (np.cumsum(vals, axis=1)[:, -1] / members.numel()).astype(np.float32)
+        bad_cen += int((mean.view(np.uint32) != cen_h[:, c].view(np.uint32)).sum())
+    # texels: shN_labels[i] = label of the row at Morton position i (write-sog.ts:338-348)
+    order = torch.arange(n, dtype=torch.int32, device=dev)  # generateIndices (write-sog.ts:42-49)
+    ctx.dev_morton_order(cols['x'], cols['y'], cols['z'], order)
+    ctx.synchronize()
+    t = tex['shN_labels'].view(-1, 4)[:n].long()
+    tl = t[:, 0] | (t[:, 1] << 8)
+    bad_texels = int((tl != (lab64[order.long()] & 0xffff)).sum().item())
+    ok = same and bad_labels == 0 and bad_cen == 0 and bad_texels == 0
+    return {'ok': ok, 'textures_equal_timed_step': same, 'labels_checked': n_labels, 'labels_wrong': bad_labels,
+            'label_exact_ties_unchecked': ties, 'clusters_checked': len(pick), 'centroid_values_wrong': bad_cen,
+            'empty_clusters': int((counts == 0).sum().item()), 'texel_labels_checked': n,
+            'texel_labels_wrong': bad_texels,
+            'how': 'snapshot of the SH palette k-means (st_ctx_set_verify) on a re-run of the step; f64 argmin '
+                   'over the last assign\'s centroids, sequential f64 member means, Morton texel placement'}
+
+
 def ctypes_char_array(size):
     import ctypes
     return ctypes.c_char * size
@@ -288,6 +360,11 @@ def main():
         torch.cuda.synchronize()
         stages = json.loads(ctx.timings())
         os.environ.pop('ST_TIMING', None)
+
+    # the last timed step's output checked against the reference's definitions (single device)
+    verification = None
+    if not sharded:
+        verification = verify_step(ctx, cols, tex, step)
 
     if rank != 0:
         if sharded:
@@ -395,11 +472,15 @@ def main():
         'stages_ms': stages,
         'kernels': kstats,
         'draws_used_per_step': used,
+        'verified': verification['ok'] if verification else None,
+        'verification': verification,
     }
     _RESULT.write(json.dumps(out) + '\n')
     _RESULT.flush()
     if sharded:
         dist.destroy_process_group()
+    if verification and not verification['ok']:
+        sys.exit(1)
 
 
 # stdout carries exactly the one JSON line: whatever the libraries print there (RCCL's

@@ -155,6 +155,15 @@ const char *st_ctx_last_timings(st_ctx *ctx);
 int st_ctx_set_profiling(st_ctx *ctx, int32_t enable);
 int st_ctx_reset_kernel_stats(st_ctx *ctx);
 int st_ctx_kernel_stats(st_ctx *ctx, const char *name, double *total_ms, uint64_t *launches);
+/* Output verification (bench.py, tests): when enabled, every N-D k-means (d > 1) keeps a
+ * device copy of the centroids its LAST assign used, its final centroids and its labels
+ * (k-means.ts:164-192: the returned labels come from the last assign, the centroids from the
+ * update after it).  st_ctx_verify_snapshot writes d, k, n and, where the pointers are not
+ * NULL, copies them into caller DEVICE buffers on the context stream: centroids [d][k]
+ * float32, labels uint32[n].  Costs three device copies per k-means call while enabled. */
+int st_ctx_set_verify(st_ctx *ctx, int32_t enable);
+int st_ctx_verify_snapshot(st_ctx *ctx, float *prev_centroids, float *centroids, uint32_t *labels,
+                           int32_t *d, int32_t *k, uint64_t *n);
 
 /* ---- host constants ------------------------------------------------------ */
 int st_quat_from_euler(double ex_deg, double ey_deg, double ez_deg, double q_xyzw[4]);

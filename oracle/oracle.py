@@ -61,6 +61,11 @@ def mulberry32(seed, n):
     return (t ^ (t >> np.uint32(14))).astype(np.float64) / 4294967296.0
 
 
+def set_threads(threads):
+    """OpenMP threads for the k-means assign loop (labels are those of the sequential loop)."""
+    lib().st_o_set_threads(ctypes.c_int(threads))
+
+
 def exp(x):
     return lib().st_o_exp(float(x))
 

@@ -712,6 +712,10 @@ static void kd_recurse(kdsearch *s, int node, int depth)
 
 typedef struct { const double *draws; uint64_t n, used; } rng;
 
+/* threads for st_o_kmeans's assign loop (1 = the reference's sequential loop) */
+static int o_threads = 1;
+void st_o_set_threads(int threads) { o_threads = threads > 1 ? threads : 1; }
+
 static int rng_next(rng *r, double *out)
 {
     if (r->used >= r->n) return -2;
@@ -768,12 +772,30 @@ int st_o_kmeans(const float *const *cols, int d, uint64_t n, int k, int iters,
         for (int i = 0; i < k; ++i) kidx[i] = (uint32_t)i;
         t.nnodes = 0;
         const int root = kd_build(&t, kidx, (uint64_t)k, 0);
-        for (uint64_t i = 0; i < n; ++i) {
-            for (int c = 0; c < d; ++c) point[c] = cols[c][i];
-            kdsearch s = {&t, point, INFINITY, -1};
-            kd_recurse(&s, root, 0);
-            if (s.mini < 0) { rc = -1; break; } /* reference crashes (labels[i] = -1) */
-            labels[i] = (uint32_t)s.mini;
+        if (o_threads > 1) {
+            /* the point loop over OpenMP threads: each search only reads the tree, so the
+             * labels are those of the sequential loop (fixture generation at N = 100k) */
+#pragma omp parallel num_threads(o_threads) reduction(|: rc)
+            {
+                float *pt = (float *)malloc(sizeof(float) * d);
+#pragma omp for schedule(dynamic, 16)
+                for (uint64_t i = 0; i < n; ++i) {
+                    for (int c = 0; c < d; ++c) pt[c] = cols[c][i];
+                    kdsearch s = {&t, pt, INFINITY, -1};
+                    kd_recurse(&s, root, 0);
+                    if (s.mini < 0) rc = -1;
+                    else labels[i] = (uint32_t)s.mini;
+                }
+                free(pt);
+            }
+        } else {
+            for (uint64_t i = 0; i < n; ++i) {
+                for (int c = 0; c < d; ++c) point[c] = cols[c][i];
+                kdsearch s = {&t, point, INFINITY, -1};
+                kd_recurse(&s, root, 0);
+                if (s.mini < 0) { rc = -1; break; } /* reference crashes (labels[i] = -1) */
+                labels[i] = (uint32_t)s.mini;
+            }
         }
         if (rc) break;
         /* groupLabels + calcAverage: f64 running sum in ascending point order */

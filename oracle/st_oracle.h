@@ -54,6 +54,8 @@ void st_o_pack_compressed(uint64_t n, const float *const m14[14], const float *c
  * cols: d columns of n points.  draws: the Math.random stream.  centroids:
  * d columns of k (or n when n < k).  Returns 0, or -1 on a reference crash
  * condition (non-finite distance), -2 draws exhausted. */
+/* OpenMP threads for st_o_kmeans's assign (labels unchanged; default 1) */
+void st_o_set_threads(int threads);
 int st_o_kmeans(const float *const *cols, int d, uint64_t n, int k, int iters,
                 const double *draws, uint64_t ndraws, uint64_t *used,
                 float *centroids, uint32_t *labels);

@@ -109,6 +109,10 @@ struct st_ctx {
     };
     std::vector<KEv> kevents;
     std::vector<hipEvent_t> event_pool;
+    // st_ctx_set_verify: snapshot of the last N-D k-means (prev / final centroids, labels)
+    bool verify = false;
+    int vf_d = 0, vf_k = 0;
+    uint64_t vf_n = 0;
 };
 
 namespace st {

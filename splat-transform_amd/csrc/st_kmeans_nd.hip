@@ -1189,7 +1189,10 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     auto *members = wsT<uint32_t>(c, "kn.members", n);
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
     nd_prepare(c, dcols, d, n);
+    const size_t cbytes = (size_t)k * d * sizeof(float);
     for (int it = 0; it < iters; ++it) {
+        if (c->verify && it == iters - 1)
+            ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         nd_assign(c, dcols, d, n, k, cen, labels, dstate);
         // update
         member_sort(c, labels, n, k, sorted_labels, members, start);
@@ -1200,6 +1203,13 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         }
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "kn.update");
+    }
+    if (c->verify && iters > 0) {
+        ST_HIP(hipMemcpyAsync(ws(c, "verify.cen", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
+        ST_HIP(hipMemcpyAsync(ws(c, "verify.labels", n * 4), labels, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        c->vf_d = d;
+        c->vf_k = k;
+        c->vf_n = n;
     }
 }
 

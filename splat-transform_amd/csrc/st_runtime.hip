@@ -296,6 +296,33 @@ int st_ctx_kernel_stats(st_ctx *c, const char *name, double *total_ms, uint64_t 
     });
 }
 
+int st_ctx_set_verify(st_ctx *c, int32_t enable) {
+    return guarded([&] {
+        ST_ARG(c, "ctx is NULL");
+        c->verify = enable != 0;
+    });
+}
+
+int st_ctx_verify_snapshot(st_ctx *c, float *prev, float *cen, uint32_t *labels, int32_t *d, int32_t *k,
+                           uint64_t *n) {
+    return guarded([&] {
+        ST_ARG(c && d && k && n, "NULL argument");
+        ST_REQUIRE(c->vf_k > 0, ST_ERR_ARG, "no k-means snapshot (st_ctx_set_verify before the call)");
+        use_device(c);
+        const size_t cbytes = (size_t)c->vf_k * c->vf_d * sizeof(float);
+        const struct {
+            void *dst;
+            const char *slot;
+            size_t bytes;
+        } parts[3] = {{prev, "verify.prev", cbytes}, {cen, "verify.cen", cbytes}, {labels, "verify.labels", c->vf_n * 4}};
+        for (auto &p : parts)
+            if (p.dst) ST_HIP(hipMemcpyAsync(p.dst, ws(c, p.slot, p.bytes), p.bytes, hipMemcpyDeviceToDevice, c->stream));
+        *d = c->vf_d;
+        *k = c->vf_k;
+        *n = c->vf_n;
+    });
+}
+
 // ---- device entry points --------------------------------------------------
 int st_dev_transform(st_ctx *c, const st_table *t, const st_transform_params *p) {
     return guarded([&] {

@@ -83,7 +83,7 @@ class PlyHeader(ctypes.Structure):
 EXPORTS = [
     'st_abi_version', 'st_last_error', 'st_device_count', 'st_ctx_create', 'st_ctx_destroy', 'st_ctx_set_stream',
     'st_ctx_synchronize', 'st_ctx_last_timings', 'st_ctx_set_profiling', 'st_ctx_reset_kernel_stats',
-    'st_ctx_kernel_stats', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
+    'st_ctx_kernel_stats', 'st_ctx_set_verify', 'st_ctx_verify_snapshot', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
@@ -284,6 +284,24 @@ class Context:
         cnt = ctypes.c_uint64(0)
         check(lib().st_ctx_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
         return ms.value, cnt.value
+
+    def set_verify(self, on=True):
+        check(lib().st_ctx_set_verify(self.h, ctypes.c_int32(1 if on else 0)))
+
+    def verify_snapshot(self, device='cuda'):
+        """(prev_centroids [d, k], centroids [d, k], labels [n]) torch tensors of the last N-D
+        k-means run while verification was on (st_ctx_verify_snapshot)"""
+        import torch
+        d, k, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_uint64()
+        check(lib().st_ctx_verify_snapshot(self.h, None, None, None, ctypes.byref(d), ctypes.byref(k),
+                                           ctypes.byref(n)))
+        prev = torch.empty((d.value, k.value), dtype=torch.float32, device=device)
+        cen = torch.empty_like(prev)
+        lab = torch.empty(n.value, dtype=torch.int32, device=device)
+        check(lib().st_ctx_verify_snapshot(self.h, _ptr(prev), _ptr(cen), _ptr(lab), ctypes.byref(d),
+                                           ctypes.byref(k), ctypes.byref(n)))
+        self.synchronize()
+        return prev, cen, lab
 
     # ---- host-memory seams ----------------------------------------------------
     def transform(self, cols, params):

@@ -28,7 +28,24 @@ const { generateOrdering } = require(path.join(REF, 'ordering.js'));
 const { processDataTable } = require(path.join(REF, 'process.js'));
 const { RotateSH } = require(path.join(REF, 'utils/rotate-sh.js'));
 const { sigmoid } = require(path.join(REF, 'utils/math.js'));
-const { kmeans } = require(path.join(REF, 'utils/k-means.js'));
+// every kmeans() call writeSog makes can be recorded (sog65k): the k-means module's export is
+// wrapped BEFORE write-sog.js binds it; the wrapper calls the reference function unchanged
+const kmeansModule = require(path.join(REF, 'utils/k-means.js'));
+const kmeansCalls = [];
+let recordKmeans = false;
+{
+    const origKmeans = kmeansModule.kmeans;
+    kmeansModule.kmeans = async (points, k, iters, device) => {
+        const drawsBefore = drawCount;
+        const res = await origKmeans(points, k, iters, device);
+        if (recordKmeans) {
+            kmeansCalls.push({ n: points.numRows, d: points.numColumns, k, iters, drawsBefore, drawsAfter: drawCount,
+                centroids: res.centroids.columns.map(c => Float32Array.from(c.data)), labels: Uint32Array.from(res.labels) });
+        }
+        return res;
+    };
+}
+const { kmeans } = kmeansModule;
 const { writeCompressedPly } = require(path.join(REF, 'writers/write-compressed-ply.js'));
 const { writeSog, cluster1d } = require(path.join(REF, 'writers/write-sog.js'));
 const { combine } = require(path.join(REF, 'index.js'));
@@ -137,6 +154,34 @@ const makeSplats = (n, shCoeffs, seed, opts = {}) => {
     }
     return { names, cols };
 };
+
+// transcendental-free splats (sog65k): every value is made of mulberry32 draws with + - * only,
+// so numpy reproduces the table bit for bit (tests/golden_io.py: bell_splats).  228 draws per row:
+// cube flag, 4 per x/y/z, f_dc, f_rest, opacity, rot (Irwin-Hall sum of 4 draws), 1 per scale.
+const makeBellSplats = (n, shCoeffs, seed, cubeFrac) => {
+    const u = mulberry32(seed);
+    const bell = (sigma) => ((((u() + u()) + u()) + u()) - 2) * sigma;
+    const names = gsColumnNames(shCoeffs);
+    const cols = {};
+    names.forEach((nm) => { cols[nm] = new Float32Array(n); });
+    const off = [1, -2, 3];
+    for (let i = 0; i < n; ++i) {
+        const cube = u() < cubeFrac;
+        ['x', 'y', 'z'].forEach((a, j) => {
+            const v = bell(17.32);
+            cols[a][i] = cube ? off[j] + (v + 34.64) * 1e-5 : v;
+        });
+        for (let c = 0; c < 3; ++c) cols[`f_dc_${c}`][i] = bell(1.732);
+        for (let c = 0; c < shCoeffs * 3; ++c) cols[`f_rest_${c}`][i] = bell(0.1732);
+        cols.opacity[i] = bell(3.464);
+        for (let c = 0; c < 3; ++c) cols[`scale_${c}`][i] = -7 + 5 * u();
+        for (let c = 0; c < 4; ++c) cols[`rot_${c}`][i] = bell(1.732);
+    }
+    return { names, cols };
+};
+
+const sha256 = (arr) => require('crypto').createHash('sha256')
+    .update(Buffer.from(arr.buffer, arr.byteOffset, arr.byteLength)).digest('hex');
 
 const toTable = (names, cols) => new DataTable(names.map(nm => new Column(nm, cols[nm].slice())));
 
@@ -497,6 +542,52 @@ cases.ply_io = async () => {
         fx.meta[`${name}_columns`] = out.columns.map(c => c.name);
         for (const c of out.columns) fx.add(`${name}_dec_${c.name}`, c.data);
     }
+    fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
+    fx.save();
+};
+
+// writeSog at paletteSize 65,536 (write-sog.ts:296-359; k-means.ts:137-201): N = 100,000 SH-3
+// splats, 2 iterations, through the reference's own --no-gpu path (~10 min on one core).  The
+// table is reproducible from its seed (makeBellSplats), so the fixture holds sha256 digests of
+// the input columns, of the seven RGBA textures and of every kmeans() call's centroids and
+// labels, plus meta and the draw counts -- no bulk data.
+cases.sog65k = async () => {
+    const fx = new Fixture('sog65k');
+    const n = Number(process.env.ST_SOG65K_N || 100000), shc = 15, iters = 2, seed = 651, dseed = 652;
+    const { names, cols } = makeBellSplats(n, shc, seed, 0.05);
+    const table = toTable(names, cols);
+    const dir = fs.mkdtempSync('/tmp/st_sog65k_');
+    const metaPath = path.join(dir, 'meta.json');
+    const fh = await fs.promises.open(metaPath, 'w');
+    seedRandom(dseed);
+    kmeansCalls.length = 0;
+    recordKmeans = true;
+    const t0 = Date.now();
+    try {
+        await quiet(() => writeSog(fh, table, metaPath, iters, 'cpu'));
+    } finally {
+        recordKmeans = false;
+    }
+    await fh.close();
+    const meta = JSON.parse(fs.readFileSync(metaPath, 'utf8'));
+    const files = ['means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels'];
+    const tex = {};
+    files.forEach((f) => {
+        const t = readRGBA(path.join(dir, `${f}.webp`));
+        tex[f] = { w: t.w, h: t.h, sha256: sha256(t.data) };
+    });
+    fx.meta = {
+        generator: 'makeBellSplats', n, sh_coeffs: shc, iters, seed, draw_seed: dseed, cube_frac: 0.05,
+        draws: drawCount, seconds: (Date.now() - t0) / 1000, meta,
+        input_sha256: Object.fromEntries(names.map(nm => [nm, sha256(cols[nm])])),
+        textures: tex,
+        kmeans_calls: kmeansCalls.map(c => ({ n: c.n, d: c.d, k: c.k, iters: c.iters, draws_before: c.drawsBefore,
+            draws_after: c.drawsAfter, centroids_sha256: sha256(Buffer.concat(c.centroids.map(a => Buffer.from(a.buffer)))),
+            labels_sha256: sha256(c.labels) }))
+    };
+    // the SH palette's labels themselves (400 KB): a mismatch can then be located
+    const shCall = kmeansCalls.find(c => c.d === shc * 3);
+    fx.add('sh_labels', shCall.labels);
     fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
     fx.save();
 };
