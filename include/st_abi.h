@@ -10,8 +10,10 @@
  *                                           new RotateSH(mat3)                  transform.ts:13-15,
  *                                                                               rotate-sh.ts:49-149
  *   st_filter_finite / st_dev_filter_finite filter(dt, isFinite-all) indices    process.ts:47-61,84-95
- *   st_dev_permute_rows                     DataTable.permuteRows               data-table.ts:135-149
- *   st_dev_concat_rows                      combine() column copy               index.ts:158-210
+ *   st_filter_nan                           filterNaN: filter + permuteRows     process.ts:84-95
+ *   st_dev_permute_rows[_t]                 DataTable.permuteRows               data-table.ts:135-149
+ *   st_combine_layout / st_dev_combine      combine()                           index.ts:158-210
+ *   st_dev_concat_rows                      combine() of float32 tables         index.ts:158-210
  *   st_morton_order / st_dev_morton_order   generateOrdering(dataTable, idx)    ordering.ts:4-110
  *   st_pack_compressed / st_dev_...         writeCompressedPly chunk loop +
  *                                           CompressedChunk.pack                write-compressed-ply.ts:56-109,
@@ -132,6 +134,18 @@ typedef struct {
     st_ply_element elements[ST_PLY_MAX_ELEMENTS];
 } st_ply_header;
 
+/* Typed SoA table: the reference's eight column types (data-table.ts:1-27) as st_ply_type
+ * codes (ST_PLY_CHAR = Int8Array ... ST_PLY_FLOAT = Float32Array, ST_PLY_DOUBLE =
+ * Float64Array).  Used where the reference handles every type: filterNaN, permuteRows,
+ * combine.  Column data must be aligned to its element size. */
+typedef struct {
+    uint64_t n;
+    int32_t ncol;
+    const char *const *names;
+    const int32_t *types;       /* st_ply_type per column */
+    void *const *cols;
+} st_ttable;
+
 typedef struct {
     uint8_t *means_l, *means_u, *quats, *scales, *sh0; /* width*height*4 each */
     uint8_t *shn_centroids;                           /* shn_width*shn_height*4 (NULL if sh_bands==0) */
@@ -175,6 +189,10 @@ int st_sog_geometry(uint64_t n, int32_t sh_coeffs, int32_t *width, int32_t *heig
 /* ---- host-memory entry points ---------------------------------------------- */
 int st_transform(st_ctx *ctx, const st_table *table, const st_transform_params *p);
 int st_filter_finite(st_ctx *ctx, const st_table *table, uint32_t *out_idx, uint64_t *out_n);
+/* filterNaN on host columns in one call (process.ts:84-95 -> filter -> permuteRows): the table
+ * is uploaded once, the surviving rows are compacted on the device and the first *out_m rows of
+ * each dst column (host, src's types, capacity n rows) receive them */
+int st_filter_nan(st_ctx *ctx, const st_ttable *src, const st_ttable *dst, uint64_t *out_m);
 int st_morton_order(st_ctx *ctx, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
 int st_pack_compressed(st_ctx *ctx, const st_table *table, const uint32_t *order,
                        float *chunk, uint32_t *vertex, uint8_t *sh);
@@ -190,6 +208,20 @@ int st_dev_transform(st_ctx *ctx, const st_table *table, const st_transform_para
 int st_dev_filter_finite(st_ctx *ctx, const st_table *table, uint32_t *out_idx, uint64_t *out_n);
 int st_dev_permute_rows(st_ctx *ctx, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst);
 int st_dev_concat_rows(st_ctx *ctx, const st_table *const *srcs, int32_t nsrc, const st_table *dst);
+/* typed forms (every column type, as the reference):
+ *   filterNaN's indices: float32 and float64 columns are tested with isFinite, integer
+ *     columns are always finite (process.ts:84-95)
+ *   permuteRows: dst[c][j] = src[c][idx[j]], dst columns of src's types (data-table.ts:135-149)
+ *   combine: st_combine_layout lists the result columns -- (table, column) of each, the
+ *     first table's columns then every later column without a (name, type) match
+ *     (index.ts:164-178); st_dev_combine fills a dst of that layout with sum(n) rows: zeros,
+ *     then each source column at its table's row offset in its first (name, type) match */
+int st_dev_filter_finite_t(st_ctx *ctx, const st_ttable *table, uint32_t *out_idx, uint64_t *out_n);
+int st_dev_permute_rows_t(st_ctx *ctx, const st_ttable *src, const uint32_t *idx, uint64_t m, const st_ttable *dst);
+/* host only (no device); col_table / col_index may be NULL to query the count */
+int st_combine_layout(const st_ttable *const *srcs, int32_t nsrc, int32_t *col_table, int32_t *col_index,
+                      int32_t *ncol);
+int st_dev_combine(st_ctx *ctx, const st_ttable *const *srcs, int32_t nsrc, const st_ttable *dst);
 int st_dev_morton_order(st_ctx *ctx, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
 int st_dev_pack_compressed(st_ctx *ctx, const st_table *table, const uint32_t *order,
                            float *chunk, uint32_t *vertex, uint8_t *sh);

@@ -224,3 +224,39 @@ def decompress_ply(chunk, vertex, sh):
                               ctypes.c_int(len(sv)), _ptrs([out[k] for k in names]))
     return out
 
+
+
+# ---- whole-table row operations on typed columns (numpy restatement) -----------------
+def combine(tables):
+    """combine (index.ts:158-210): tables are lists of (name, array).  Result columns: the first
+    table's, then each later column whose (name, dtype) is not yet present; rows appended in
+    table order; each source column lands in the FIRST result column of its (name, dtype);
+    the rest stays zero."""
+    if len(tables) == 1:
+        return list(tables[0])
+    cols = list(tables[0])
+    for t in tables[1:]:
+        for name, a in t:
+            if not any(n == name and b.dtype == a.dtype for n, b in cols):
+                cols.append((name, a))
+    total = sum(len(t[0][1]) for t in tables)
+    out = [(name, np.zeros(total, a.dtype)) for name, a in cols]
+    off = 0
+    for t in tables:
+        for name, a in t:
+            tgt = next(b for n, b in out if n == name and b.dtype == a.dtype)
+            tgt[off:off + len(a)] = a
+        off += len(t[0][1])
+    return out
+
+
+def filter_nan(cols):
+    """filterNaN (process.ts:84-95 -> filter :47-61 -> permuteRows data-table.ts:135-149): keep a row
+    iff isFinite holds for every column value (always for integer columns)"""
+    n = len(cols[0][1])
+    keep = np.ones(n, bool)
+    for _, a in cols:
+        if a.dtype.kind == 'f':
+            keep &= np.isfinite(a)
+    idx = np.nonzero(keep)[0].astype(np.uint32)
+    return [(name, a[idx]) for name, a in cols], idx

@@ -115,6 +115,36 @@ int st_filter_finite(st_ctx *c, const st_table *t, uint32_t *out_idx, uint64_t *
     });
 }
 
+int st_filter_nan(st_ctx *c, const st_ttable *src, const st_ttable *dst, uint64_t *out_m) {
+    return guarded_h([&] {
+        ST_ARGH(c && src && dst && out_m, "NULL argument");
+        ST_ARGH(src->ncol == dst->ncol && dst->n >= src->n, "filter_nan: dst needs src's columns and n rows");
+        use_device(c);
+        const uint64_t n = src->n;
+        std::vector<void *> dcols(src->ncol), ocols(src->ncol);
+        for (int i = 0; i < src->ncol; ++i) {
+            const int sz = type_size(src->types[i]);
+            ST_ARGH(sz > 0 && dst->types[i] == src->types[i], "filter_nan: bad or mismatched column type");
+            dcols[i] = ws(c, "h.fn" + std::to_string(i), n * sz + 16);
+            if (n) ST_HIP(hipMemcpyAsync(dcols[i], src->cols[i], n * sz, hipMemcpyHostToDevice, c->stream));
+        }
+        st_ttable d = *src;
+        d.cols = dcols.data();
+        auto *didx = wsT<uint32_t>(c, "h.fnidx", n);
+        const uint64_t m = filter_finite_tdev(c, &d, didx);
+        for (int i = 0; i < src->ncol; ++i) ocols[i] = ws(c, "h.fno" + std::to_string(i), m * type_size(src->types[i]) + 16);
+        st_ttable o = d;
+        o.n = m;
+        o.cols = ocols.data();
+        permute_rows_tdev(c, &d, didx, m, &o);
+        for (int i = 0; i < src->ncol; ++i)
+            if (m) ST_HIP(hipMemcpyAsync(dst->cols[i], ocols[i], m * type_size(src->types[i]), hipMemcpyDeviceToHost,
+                                         c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        *out_m = m;
+    });
+}
+
 int st_morton_order(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *idx, uint64_t n) {
     return guarded_h([&] {
         ST_ARGH(c && ((x && y && z && idx) || n == 0), "NULL argument");

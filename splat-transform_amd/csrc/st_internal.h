@@ -177,6 +177,12 @@ void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p);
 uint64_t filter_finite_dev(st_ctx *c, const st_table *t, uint32_t *out_idx);
 void permute_rows_dev(st_ctx *c, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst);
 void concat_rows_dev(st_ctx *c, const st_table *const *srcs, int nsrc, const st_table *dst);
+// typed tables (st_table.hip)
+int type_size(int32_t st_ply_type);  // 0 for an unknown code
+uint64_t filter_finite_tdev(st_ctx *c, const st_ttable *t, uint32_t *out_idx);
+void permute_rows_tdev(st_ctx *c, const st_ttable *src, const uint32_t *idx, uint64_t m, const st_ttable *dst);
+int combine_layout(const st_ttable *const *srcs, int nsrc, int32_t *col_table, int32_t *col_index);
+void combine_tdev(st_ctx *c, const st_ttable *const *srcs, int nsrc, const st_ttable *dst);
 void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
 void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
                          uint8_t *sh);

@@ -29,19 +29,7 @@
 namespace st {
 namespace {
 
-int type_size(int t) {
-    switch (t) {
-        case ST_PLY_CHAR:
-        case ST_PLY_UCHAR: return 1;
-        case ST_PLY_SHORT:
-        case ST_PLY_USHORT: return 2;
-        case ST_PLY_INT:
-        case ST_PLY_UINT:
-        case ST_PLY_FLOAT: return 4;
-        case ST_PLY_DOUBLE: return 8;
-        default: return 0;
-    }
-}
+// type_size: st_table.hip (st_internal.h)
 
 int type_of(const std::string &s) {
     static const char *names[] = {"char", "uchar", "short", "ushort", "int", "uint", "float", "double"};

@@ -363,6 +363,61 @@ int st_dev_concat_rows(st_ctx *c, const st_table *const *srcs, int32_t nsrc, con
     });
 }
 
+static void check_ttable(const st_ttable *t) {
+    ST_ARG(t != nullptr, "table is NULL");
+    ST_ARG(t->ncol >= 0 && (t->ncol == 0 || (t->names && t->types && t->cols)), "table: bad column arrays");
+    for (int i = 0; i < t->ncol; ++i) {
+        ST_ARG(t->names[i] && (t->cols[i] || t->n == 0), "table: NULL column");
+        ST_ARG(type_size(t->types[i]) > 0, std::string("table: column ") + t->names[i] + " has an unknown type");
+        ST_ARG(((uintptr_t)t->cols[i] % type_size(t->types[i])) == 0,
+               std::string("table: column ") + t->names[i] + " is not aligned to its element size");
+    }
+}
+
+int st_dev_filter_finite_t(st_ctx *c, const st_ttable *t, uint32_t *out_idx, uint64_t *out_n) {
+    return guarded([&] {
+        ST_ARG(c && out_n && (out_idx || (t && t->n == 0)), "NULL argument");
+        check_ttable(t);
+        use_device(c);
+        *out_n = filter_finite_tdev(c, t, out_idx);
+    });
+}
+
+int st_dev_permute_rows_t(st_ctx *c, const st_ttable *src, const uint32_t *idx, uint64_t m, const st_ttable *dst) {
+    return guarded([&] {
+        ST_ARG(c && (idx || m == 0), "NULL argument");
+        check_ttable(src);
+        check_ttable(dst);
+        ST_ARG(dst->ncol == src->ncol && dst->n == m, "permute_rows: dst must have src's columns and m rows");
+        for (int i = 0; i < src->ncol; ++i)
+            ST_ARG(src->types[i] == dst->types[i], "permute_rows: dst column types differ from src");
+        use_device(c);
+        permute_rows_tdev(c, src, idx, m, dst);
+    });
+}
+
+int st_combine_layout(const st_ttable *const *srcs, int32_t nsrc, int32_t *col_table, int32_t *col_index,
+                      int32_t *ncol) {
+    return guarded([&] {
+        ST_ARG(srcs && nsrc > 0 && ncol, "NULL argument");
+        for (int i = 0; i < nsrc; ++i) {
+            ST_ARG(srcs[i] && srcs[i]->ncol >= 0 && (srcs[i]->ncol == 0 || (srcs[i]->names && srcs[i]->types)),
+                   "combine_layout: bad table");
+        }
+        *ncol = combine_layout(srcs, nsrc, col_table, col_index);
+    });
+}
+
+int st_dev_combine(st_ctx *c, const st_ttable *const *srcs, int32_t nsrc, const st_ttable *dst) {
+    return guarded([&] {
+        ST_ARG(c && srcs && nsrc > 0, "NULL argument");
+        for (int i = 0; i < nsrc; ++i) check_ttable(srcs[i]);
+        check_ttable(dst);
+        use_device(c);
+        combine_tdev(c, srcs, nsrc, dst);
+    });
+}
+
 int st_dev_morton_order(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *idx, uint64_t n) {
     return guarded([&] {
         ST_ARG(c && ((x && y && z && idx) || n == 0), "NULL argument");

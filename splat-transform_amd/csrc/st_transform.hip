@@ -1,5 +1,5 @@
-// st_transform.hip -- per-splat TRS + SH-band rotation, filterNaN compaction,
-// row gather and row concatenation on SoA float32 columns.
+// st_transform.hip -- per-splat TRS + SH-band rotation on SoA float32 columns
+// (filterNaN / permuteRows / combine: st_table.hip).
 //
 // transform(): transform.ts:12-65.  One thread per splat, f64 arithmetic in the
 // reference's order (no FMA contraction), f32 stores:
@@ -94,111 +94,6 @@ void launch_transform(st_ctx *c, const TransformArgs &a, bool pos, bool rot, boo
 #undef ST_T
 }
 
-// ---------------------------------------------------------------------------
-// filterNaN: keep row iff every column value is finite (process.ts:84-95)
-__global__ __launch_bounds__(256) void k_finite_flags(float *const *cols, int ncol, uint64_t n, uint32_t *flags) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t ok = 1;
-        for (int c = 0; c < ncol; ++c) ok &= js::isfinitef_(cols[c][i]) ? 1u : 0u;
-        flags[i] = ok;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_compact(const uint32_t *flags, const uint32_t *pos, uint64_t n,
-                                                 uint32_t *out) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        if (flags[i]) out[pos[i]] = (uint32_t)i;
-}
-
-// permuteRows (data-table.ts:135-149): dst[c][j] = src[c][idx[j]]
-__global__ __launch_bounds__(256) void k_gather_cols(float *const *src, float *const *dst, int ncol,
-                                                     const uint32_t *__restrict__ idx, uint64_t m) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
-        const uint32_t s = idx[j];
-        for (int c = 0; c < ncol; ++c) dst[c][j] = src[c][s];
-    }
-}
-
-// ---- wide streaming forms: 4 consecutive rows per thread, column pointers in kernel
-// arguments, 8 columns' loads in flight before any test (the loops above wait on every
-// column's load in turn)
-constexpr int WIDE_COLS = 64;
-struct ColPtrs {
-    const float *p[WIDE_COLS];
-};
-
-__device__ inline uint32_t nonfinite_bit(float x) {
-    return ((__builtin_bit_cast(uint32_t, x) & 0x7f800000u) == 0x7f800000u) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(256) void k_finite_flags4(const ColPtrs cp, int ncol, uint64_t n,
-                                                       uint32_t *__restrict__ flags) {
-    const uint64_t nq = n / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
-        uint32_t bad = 0;  // bit r: row 4q + r holds a non-finite value
-        int c = 0;
-        for (; c + 8 <= ncol; c += 8) {
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4 *>(cp.p[c + u])[q];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                bad |= nonfinite_bit(v[u].x) | (nonfinite_bit(v[u].y) << 1) | (nonfinite_bit(v[u].z) << 2) |
-                       (nonfinite_bit(v[u].w) << 3);
-        }
-        for (; c < ncol; ++c) {
-            const float4 v = reinterpret_cast<const float4 *>(cp.p[c])[q];
-            bad |= nonfinite_bit(v.x) | (nonfinite_bit(v.y) << 1) | (nonfinite_bit(v.z) << 2) | (nonfinite_bit(v.w) << 3);
-        }
-        reinterpret_cast<uint4 *>(flags)[q] =
-            make_uint4((bad & 1u) ^ 1u, ((bad >> 1) & 1u) ^ 1u, ((bad >> 2) & 1u) ^ 1u, ((bad >> 3) & 1u) ^ 1u);
-    }
-    if (blockIdx.x == 0 && threadIdx.x < n % 4) {  // the last n % 4 rows
-        const uint64_t i = nq * 4 + threadIdx.x;
-        uint32_t bad = 0;
-        for (int c = 0; c < ncol; ++c) bad |= nonfinite_bit(cp.p[c][i]);
-        flags[i] = bad ^ 1u;
-    }
-}
-
-// permuteRows with 4 destination rows per thread: 4 x 8 gathered loads in flight, float4
-// stores (dst columns and idx 16-byte aligned)
-__global__ __launch_bounds__(256) void k_gather_cols4(const ColPtrs src, const ColPtrs dst, int ncol,
-                                                      const uint32_t *__restrict__ idx, uint64_t m) {
-    const uint64_t mq = m / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < mq; q += stride) {
-        const uint4 ii = reinterpret_cast<const uint4 *>(idx)[q];
-        int c = 0;
-        for (; c + 8 <= ncol; c += 8) {
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const float *sp = src.p[c + u];
-                v[u] = make_float4(sp[ii.x], sp[ii.y], sp[ii.z], sp[ii.w]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) reinterpret_cast<float4 *>(const_cast<float *>(dst.p[c + u]))[q] = v[u];
-        }
-        for (; c < ncol; ++c) {
-            const float *sp = src.p[c];
-            reinterpret_cast<float4 *>(const_cast<float *>(dst.p[c]))[q] =
-                make_float4(sp[ii.x], sp[ii.y], sp[ii.z], sp[ii.w]);
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x < m % 4) {
-        const uint64_t j = mq * 4 + threadIdx.x;
-        const uint32_t sj = idx[j];
-        for (int c = 0; c < ncol; ++c) const_cast<float *>(dst.p[c])[j] = src.p[c][sj];
-    }
-}
-
-bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
-
 }  // namespace
 
 void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p) {
@@ -240,85 +135,6 @@ void transform_dev(st_ctx *c, const st_table *t, const st_transform_params *p) {
         default: launch_transform<15>(c, a, pos, rot, scl); break;
     }
     ST_LAUNCH_CHECK();
-}
-
-static float *const *upload_ptrs(st_ctx *c, const std::string &slot, float *const *ptrs, int n) {
-    auto **d = wsT<float *>(c, slot, (size_t)(n > 0 ? n : 1));
-    if (n > 0) ST_HIP(hipMemcpyAsync(d, ptrs, sizeof(float *) * n, hipMemcpyHostToDevice, c->stream));
-    return d;
-}
-
-uint64_t filter_finite_dev(st_ctx *c, const st_table *t, uint32_t *out_idx) {
-    const uint64_t n = t->n;
-    if (n == 0) return 0;
-    auto *flags = wsT<uint32_t>(c, "filter.flags", n);
-    auto *pos = wsT<uint32_t>(c, "filter.pos", n + 1);
-    bool wide = t->ncol <= WIDE_COLS;
-    ColPtrs cp{};
-    for (int i = 0; wide && i < t->ncol; ++i) {
-        cp.p[i] = t->cols[i];
-        wide = aligned16(t->cols[i]);
-    }
-    if (wide) {
-        hipLaunchKernelGGL(k_finite_flags4, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, c->stream, cp,
-                           t->ncol, n, flags);
-    } else {
-        float *const *dcols = upload_ptrs(c, "filter.cols", t->cols, t->ncol);
-        hipLaunchKernelGGL(k_finite_flags, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, dcols, t->ncol, n,
-                           flags);
-    }
-    ST_LAUNCH_CHECK();
-    scan_u32(c, flags, pos, n, pos + n);
-    hipLaunchKernelGGL(k_compact, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, flags, pos, n, out_idx);
-    ST_LAUNCH_CHECK();
-    auto *h = static_cast<uint32_t *>(pinned(c, 16));
-    ST_HIP(hipMemcpyAsync(h, pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
-    return h[0];
-}
-
-void permute_rows_dev(st_ctx *c, const st_table *src, const uint32_t *idx, uint64_t m, const st_table *dst) {
-    if (m == 0 || src->ncol == 0) return;
-    bool wide = src->ncol <= WIDE_COLS && aligned16(idx);
-    ColPtrs sp{}, dp{};
-    for (int i = 0; wide && i < src->ncol; ++i) {
-        sp.p[i] = src->cols[i];
-        dp.p[i] = dst->cols[i];
-        wide = aligned16(dst->cols[i]);
-    }
-    if (wide) {
-        hipLaunchKernelGGL(k_gather_cols4, dim3(grid_for((m + 3) / 4, 256, 8192)), dim3(256), 0, c->stream, sp, dp,
-                           src->ncol, idx, m);
-    } else {
-        float *const *s = upload_ptrs(c, "permute.src", src->cols, src->ncol);
-        float *const *d = upload_ptrs(c, "permute.dst", dst->cols, dst->ncol);
-        hipLaunchKernelGGL(k_gather_cols, dim3(grid_for(m, 256, 8192)), dim3(256), 0, c->stream, s, d, src->ncol, idx,
-                           m);
-    }
-    ST_LAUNCH_CHECK();
-}
-
-// combine() (index.ts:158-210): dst columns are the union by name (f32 only);
-// rows are appended in source order, absent columns zero-filled.
-void concat_rows_dev(st_ctx *c, const st_table *const *srcs, int nsrc, const st_table *dst) {
-    uint64_t total = 0;
-    for (int i = 0; i < nsrc; ++i) total += srcs[i]->n;
-    ST_REQUIRE(total == dst->n, ST_ERR_ARG, "concat_rows: dst rows != sum of src rows");
-    for (int col = 0; col < dst->ncol; ++col) {
-        uint64_t off = 0;
-        for (int i = 0; i < nsrc; ++i) {
-            const uint64_t n = srcs[i]->n;
-            float *s = col_or_null(srcs[i], dst->names[col]);
-            if (n) {
-                if (s)
-                    ST_HIP(hipMemcpyAsync(dst->cols[col] + off, s, n * sizeof(float), hipMemcpyDeviceToDevice,
-                                          c->stream));
-                else
-                    ST_HIP(hipMemsetAsync(dst->cols[col] + off, 0, n * sizeof(float), c->stream));
-            }
-            off += n;
-        }
-    }
 }
 
 }  // namespace st

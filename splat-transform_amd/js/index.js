@@ -9,7 +9,8 @@
 //
 //   transform(dataTable, t, r, s)           transform.ts:12-65
 //   generateOrdering(dataTable, indices)    ordering.ts:4-110
-//   filterNaN(dataTable)                    process.ts:84-95 (+ filter :47-61)
+//   filterNaN(dataTable)                    process.ts:84-95 (+ filter :47-61, permuteRows)
+//   combine(dataTables)                     index.ts:158-210
 //   packCompressed(dataTable)               write-compressed-ply.ts:56-109 (the chunk loop)
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
 //   cluster1d(dataTable, iterations)        write-sog.ts:56-99
@@ -111,8 +112,25 @@ const shCoeffsOf = (dataTable) => {
 };
 
 // ---- the path ------------------------------------------------------------------------
-// t: {x, y, z} (Vec3), r: {x, y, z, w} (Quat), s: number -- mutates the columns in place
+// the columns transform.ts:16-20 reads and writes (position, rotation, scale, SH by the band rule)
+const transformColumns = (dataTable) => {
+    const groups = [['x', 'y', 'z'], ['rot_0', 'rot_1', 'rot_2', 'rot_3'], ['scale_0', 'scale_1', 'scale_2']];
+    const names = [];
+    groups.forEach((g) => { if (g.every(n => dataTable.hasColumn(n))) names.push(...g); });
+    for (let i = 0; i < 3 * shCoeffsOf(dataTable); ++i) names.push(`f_rest_${i}`);
+    return names;
+};
+
+// t: {x, y, z} (Vec3), r: {x, y, z, w} (Quat), s: number -- mutates the columns in place.
+// The device path computes in f64 and stores float32 (the PLY 3DGS layout); a transformed column
+// of another type throws instead of being skipped.
 const transform = (dataTable, t, r, s) => {
+    for (const name of transformColumns(dataTable)) {
+        const c = dataTable.getColumnByName(name);
+        if (!(c.data instanceof Float32Array)) {
+            throw new Error(`splat-hip: transform supports float32 columns only ('${name}' is ${c.data.constructor.name})`);
+        }
+    }
     const { cols, names } = f32Columns(dataTable);
     addon.transform(cols, names, [t.x, t.y, t.z], [r.x, r.y, r.z, r.w], s);
 };
@@ -129,15 +147,34 @@ const generateOrdering = (dataTable, indices) => {
     return addon.mortonOrder(x, y, z, indices);
 };
 
-// rows whose every column is finite, in order (filterNaN)
+// rows whose every column value isFinite, in order (filterNaN): every column type, the
+// compaction and the row gather on the device, each column keeping its type
 const filterNaN = (dataTable) => {
-    const { cols } = f32Columns(dataTable);
-    const keep = addon.filterFinite(cols);
-    return new DataTable(dataTable.columns.map((c) => {
-        const out = new c.data.constructor(keep.length);
-        for (let i = 0; i < keep.length; ++i) out[i] = c.data[keep[i]];
-        return new Column(c.name, out);
-    }));
+    const out = addon.filterNaN(dataTable.columns.map(c => c.data));
+    return new DataTable(dataTable.columns.map((c, i) => new Column(c.name, out[i])));
+};
+
+const PLY_TYPE = { Int8Array: 1, Uint8Array: 2, Int16Array: 3, Uint16Array: 4, Int32Array: 5, Uint32Array: 6,
+    Float32Array: 7, Float64Array: 8 };
+
+// index.ts:158-210: columns united by (name, dataType), rows appended, absent columns zero
+const combine = (dataTables) => {
+    if (dataTables.length === 1) return dataTables[0];
+    const layout = addon.combineLayout(dataTables.map(t => ({
+        names: t.columns.map(c => c.name), types: t.columns.map(c => PLY_TYPE[c.data.constructor.name] || 0)
+    })));
+    const total = dataTables.reduce((sum, t) => sum + t.numRows, 0);
+    const result = layout.map(([t, j]) => {
+        const c = dataTables[t].columns[j];
+        return new Column(c.name, new c.data.constructor(total));
+    });
+    const target = (c) => result.find(r => r.name === c.name && r.data.constructor === c.data.constructor);
+    let offset = 0;
+    for (const t of dataTables) {
+        for (const c of t.columns) target(c).data.set(c.data, offset);
+        offset += t.numRows;
+    }
+    return new DataTable(result);
 };
 
 // the chunk / vertex / sh arrays writeCompressedPly writes after its header
@@ -266,6 +303,7 @@ module.exports = {
     quatFromEuler,
     generateOrdering,
     filterNaN,
+    combine,
     packCompressed,
     kmeans,
     cluster1d,

@@ -247,6 +247,155 @@ fail:
     return NULL;
 }
 
+/* TypedArray element type -> st_ply_type (0: not one of the reference's eight) */
+static int ply_type_of(napi_typedarray_type t, size_t *esize) {
+    switch (t) {
+        case napi_int8_array: *esize = 1; return ST_PLY_CHAR;
+        case napi_uint8_array: *esize = 1; return ST_PLY_UCHAR;
+        case napi_int16_array: *esize = 2; return ST_PLY_SHORT;
+        case napi_uint16_array: *esize = 2; return ST_PLY_USHORT;
+        case napi_int32_array: *esize = 4; return ST_PLY_INT;
+        case napi_uint32_array: *esize = 4; return ST_PLY_UINT;
+        case napi_float32_array: *esize = 4; return ST_PLY_FLOAT;
+        case napi_float64_array: *esize = 8; return ST_PLY_DOUBLE;
+        default: *esize = 0; return 0;
+    }
+}
+
+/* filterNaN(columns: TypedArray[]) -> TypedArray[] of the rows whose every value isFinite
+ * (process.ts:84-95 -> filter -> permuteRows): one upload, compaction on the device, each
+ * result column of its source's type (st_filter_nan) */
+static napi_value js_filter_nan(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out = NULL;
+    uint32_t m = 0;
+    uint64_t n = 0, kept = 0;
+    st_ctx *ctx;
+    void **src = NULL, **dst = NULL;
+    int32_t *types = NULL;
+    napi_typedarray_type *nt = NULL;
+    size_t *es = NULL;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    NAPI_OK(napi_get_array_length(env, argv[0], &m));
+    src = (void **)calloc(m + 1, sizeof(void *));
+    dst = (void **)calloc(m + 1, sizeof(void *));
+    types = (int32_t *)calloc(m + 1, sizeof(int32_t));
+    nt = (napi_typedarray_type *)calloc(m + 1, sizeof(napi_typedarray_type));
+    es = (size_t *)calloc(m + 1, sizeof(size_t));
+    for (uint32_t i = 0; i < m; ++i) {
+        napi_value e, ab;
+        bool is_ta = false;
+        size_t len = 0, off = 0;
+        NAPI_OK(napi_get_element(env, argv[0], i, &e));
+        if (napi_is_typedarray(env, e, &is_ta) != napi_ok || !is_ta ||
+            napi_get_typedarray_info(env, e, &nt[i], &len, &src[i], &ab, &off) != napi_ok ||
+            !(types[i] = ply_type_of(nt[i], &es[i]))) {
+            napi_throw_type_error(env, NULL, "splat-hip: filterNaN expects the reference's TypedArray columns");
+            goto fail;
+        }
+        if (i == 0) n = len;
+        else if (len != n) {
+            napi_throw_range_error(env, NULL, "splat-hip: columns differ in length");
+            goto fail;
+        }
+    }
+    for (uint32_t i = 0; i < m; ++i) dst[i] = malloc(n * es[i] + 8);
+    {
+        st_ttable ts = {n, (int32_t)m, NULL, types, src};
+        st_ttable td = {n, (int32_t)m, NULL, types, dst};
+        const char **noname = (const char **)calloc(m + 1, sizeof(char *));
+        for (uint32_t i = 0; i < m; ++i) noname[i] = "";
+        ts.names = td.names = noname;
+        int rc = get_ctx(env, &ctx) ? st_filter_nan(ctx, &ts, &td, &kept) : 1;
+        free(noname);
+        if (rc != ST_OK) {
+            if (rc != 1) throw_st(env, rc);
+            goto fail;
+        }
+    }
+    NAPI_OK(napi_create_array_with_length(env, m, &out));
+    for (uint32_t i = 0; i < m; ++i) {
+        void *buf;
+        napi_value ta = new_typed(env, nt[i], kept, es[i], &buf);
+        if (!ta) goto fail;
+        memcpy(buf, dst[i], kept * es[i]);
+        NAPI_OK(napi_set_element(env, out, i, ta));
+    }
+    for (uint32_t i = 0; i < m; ++i) free(dst[i]);
+    free(src); free(dst); free(types); free(nt); free(es);
+    return out;
+fail:
+    if (dst)
+        for (uint32_t i = 0; i < m; ++i) free(dst[i]);
+    free(src); free(dst); free(types); free(nt); free(es);
+    return NULL;
+}
+
+/* combineLayout(tables: [{names: string[], types: number[]}]) -> [[table, column], ...]:
+ * combine()'s result columns (index.ts:164-178, st_combine_layout) */
+static napi_value js_combine_layout(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out = NULL;
+    uint32_t nt = 0;
+    st_ttable *tabs = NULL;
+    const st_ttable **ptrs = NULL;
+    char ***names = NULL;
+    int32_t **types = NULL;
+    uint32_t *ncols = NULL;
+    int32_t *ct = NULL, *ci = NULL, nout = 0;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    NAPI_OK(napi_get_array_length(env, argv[0], &nt));
+    tabs = (st_ttable *)calloc(nt + 1, sizeof(st_ttable));
+    ptrs = (const st_ttable **)calloc(nt + 1, sizeof(st_ttable *));
+    names = (char ***)calloc(nt + 1, sizeof(char **));
+    types = (int32_t **)calloc(nt + 1, sizeof(int32_t *));
+    ncols = (uint32_t *)calloc(nt + 1, sizeof(uint32_t));
+    for (uint32_t t = 0; t < nt; ++t) {
+        napi_value tab, nv, tv, e;
+        NAPI_OK(napi_get_element(env, argv[0], t, &tab));
+        NAPI_OK(napi_get_named_property(env, tab, "names", &nv));
+        NAPI_OK(napi_get_named_property(env, tab, "types", &tv));
+        NAPI_OK(napi_get_array_length(env, nv, &ncols[t]));
+        names[t] = str_list(env, nv, ncols[t]);
+        types[t] = (int32_t *)calloc(ncols[t] + 1, sizeof(int32_t));
+        for (uint32_t j = 0; j < ncols[t]; ++j) {
+            NAPI_OK(napi_get_element(env, tv, j, &e));
+            types[t][j] = (int32_t)num(env, e);
+        }
+        tabs[t].ncol = (int32_t)ncols[t];
+        tabs[t].names = (const char *const *)names[t];
+        tabs[t].types = types[t];
+        ptrs[t] = &tabs[t];
+    }
+    {
+        int rc = st_combine_layout(ptrs, (int32_t)nt, NULL, NULL, &nout);
+        if (rc == ST_OK) {
+            ct = (int32_t *)calloc(nout + 1, sizeof(int32_t));
+            ci = (int32_t *)calloc(nout + 1, sizeof(int32_t));
+            rc = st_combine_layout(ptrs, (int32_t)nt, ct, ci, &nout);
+        }
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+    }
+    NAPI_OK(napi_create_array_with_length(env, nout, &out));
+    for (int32_t i = 0; i < nout; ++i) {
+        napi_value pair;
+        NAPI_OK(napi_create_array_with_length(env, 2, &pair));
+        NAPI_OK(napi_set_element(env, pair, 0, make_num(env, ct[i])));
+        NAPI_OK(napi_set_element(env, pair, 1, make_num(env, ci[i])));
+        NAPI_OK(napi_set_element(env, out, i, pair));
+    }
+fail:
+    for (uint32_t t = 0; t < nt; ++t) {
+        free_strs(names ? names[t] : NULL, ncols ? ncols[t] : 0);
+        if (types) free(types[t]);
+    }
+    free(tabs); free(ptrs); free(names); free(types); free(ncols); free(ct); free(ci);
+    return out;
+}
+
 /* mortonOrder(x, y, z, indices): reorders `indices` in place, returns it */
 static napi_value js_morton(napi_env env, napi_callback_info info) {
     size_t argc = 4, nx = 0, ny = 0, nz = 0, ni = 0;
@@ -713,6 +862,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"quatFromEuler", js_quat_from_euler},
                {"transform", js_transform},
                {"filterFinite", js_filter_finite},
+               {"filterNaN", js_filter_nan},
+               {"combineLayout", js_combine_layout},
                {"mortonOrder", js_morton},
                {"packCompressed", js_pack_compressed},
                {"kmeans", js_kmeans},

@@ -33,6 +33,11 @@ class Table(ctypes.Structure):
                 ('names', ctypes.POINTER(ctypes.c_char_p)), ('cols', ctypes.POINTER(ctypes.c_void_p))]
 
 
+class TTable(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_uint64), ('ncol', ctypes.c_int32), ('names', ctypes.POINTER(ctypes.c_char_p)),
+                ('types', ctypes.POINTER(ctypes.c_int32)), ('cols', ctypes.POINTER(ctypes.c_void_p))]
+
+
 class TransformParams(ctypes.Structure):
     _fields_ = [('m4', ctypes.c_float * 16), ('r', ctypes.c_double * 4), ('s', ctypes.c_double),
                 ('sh1', ctypes.c_double * 9), ('sh2', ctypes.c_double * 25), ('sh3', ctypes.c_double * 49)]
@@ -87,6 +92,7 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
+    'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
     'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
@@ -153,6 +159,48 @@ def make_table(cols):
               ctypes.cast(c_cols, ctypes.POINTER(ctypes.c_void_p)))
     t._keep = (c_names, c_cols, cols)
     return t
+
+
+_NP_TO_PLY = {np.dtype(v[1]): k for k, v in PLY_TYPES.items()}
+
+
+def ply_type_of(a):
+    """st_ply_type code of a numpy array or torch tensor's element type"""
+    if hasattr(a, 'data_ptr'):
+        import torch
+        tmap = {torch.int8: 1, torch.uint8: 2, torch.int16: 3, torch.uint16: 4, torch.int32: 5, torch.uint32: 6,
+                torch.float32: 7, torch.float64: 8}
+        return tmap[a.dtype]
+    return _NP_TO_PLY[np.dtype(a.dtype)]
+
+
+def make_ttable(cols, n=None):
+    """st_ttable over a list of (name, array) or a dict (numpy host or torch device, any of the eight
+    types); keeps refs alive"""
+    items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+    names = [k for k, _ in items]
+    if n is None:
+        n = len(items[0][1]) if items else 0
+    c_names = (ctypes.c_char_p * len(items))(*[k.encode() for k in names])
+    c_types = (ctypes.c_int32 * len(items))(*[ply_type_of(a) for _, a in items])
+    c_cols = (ctypes.c_void_p * len(items))(*[_ptr(a).value for _, a in items])
+    t = TTable(n, len(items), ctypes.cast(c_names, ctypes.POINTER(ctypes.c_char_p)),
+               ctypes.cast(c_types, ctypes.POINTER(ctypes.c_int32)), ctypes.cast(c_cols, ctypes.POINTER(ctypes.c_void_p)))
+    t._keep = (c_names, c_types, c_cols, items)
+    return t
+
+
+def combine_layout(tables):
+    """combine()'s result columns (index.ts:164-178): [(table index, column index)]; tables are lists
+    of (name, array)"""
+    tts = [make_ttable(t) for t in tables]
+    arr = (ctypes.POINTER(TTable) * len(tts))(*[ctypes.pointer(t) for t in tts])
+    ncol = ctypes.c_int32()
+    check(lib().st_combine_layout(arr, ctypes.c_int32(len(tts)), None, None, ctypes.byref(ncol)))
+    ct = (ctypes.c_int32 * max(ncol.value, 1))()
+    ci = (ctypes.c_int32 * max(ncol.value, 1))()
+    check(lib().st_combine_layout(arr, ctypes.c_int32(len(tts)), ct, ci, ctypes.byref(ncol)))
+    return [(ct[i], ci[i]) for i in range(ncol.value)]
 
 
 def quat_from_euler(ex, ey, ez):
@@ -510,6 +558,32 @@ class Context:
         m = ctypes.c_uint64(0)
         check(lib().st_dev_filter_finite(self.h, ctypes.byref(t), _ptr(out_idx), ctypes.byref(m)))
         return m.value
+
+    def filter_nan(self, cols):
+        """filterNaN on host columns (list of (name, numpy array), any type) -> the surviving rows"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        out = [(k, np.empty_like(a)) for k, a in items]
+        ts, td = make_ttable(items), make_ttable(out)
+        m = ctypes.c_uint64()
+        check(lib().st_filter_nan(self.h, ctypes.byref(ts), ctypes.byref(td), ctypes.byref(m)))
+        return [(k, a[:m.value].copy()) for k, a in out]
+
+    def dev_filter_finite_t(self, cols, out_idx):
+        t = make_ttable(cols)
+        m = ctypes.c_uint64()
+        check(lib().st_dev_filter_finite_t(self.h, ctypes.byref(t), _ptr(out_idx), ctypes.byref(m)))
+        return m.value
+
+    def dev_permute_rows_t(self, src, idx, m, dst):
+        ts, td = make_ttable(src), make_ttable(dst, m)
+        check(lib().st_dev_permute_rows_t(self.h, ctypes.byref(ts), _ptr(idx), ctypes.c_uint64(m), ctypes.byref(td)))
+
+    def dev_combine(self, tables, dst):
+        """tables: lists of (name, device tensor); dst: list of (name, tensor) in combine_layout order"""
+        tts = [make_ttable(t) for t in tables]
+        arr = (ctypes.POINTER(TTable) * len(tts))(*[ctypes.pointer(t) for t in tts])
+        td = make_ttable(dst)
+        check(lib().st_dev_combine(self.h, arr, ctypes.c_int32(len(tts)), ctypes.byref(td)))
 
     def dev_permute_rows(self, src, idx, m, dst):
         ts, td = make_table(src), make_table(dst)

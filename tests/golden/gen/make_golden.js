@@ -615,6 +615,51 @@ cases.filter_combine = () => {
     const merged = combine([a, b, c]);
     fx.meta.cmb_out_types = merged.columns.map(col => col.dataType);
     addTable(fx, 'cmb_out_', merged);
+    // by position too: the result holds two 'tag' columns (uint8 and float32)
+    merged.columns.forEach((col, j) => fx.add(`cmb_out_i${j}`, col.data));
+
+    // every column type (data-table.ts:1-27): filterNaN tests float64 columns as well, integer
+    // columns are always finite; permuteRows keeps each column's type
+    const tg = new Gen(79);
+    const nt = 333;
+    const ctors = { int8: Int8Array, uint8: Uint8Array, int16: Int16Array, uint16: Uint16Array,
+        int32: Int32Array, uint32: Uint32Array, float32: Float32Array, float64: Float64Array };
+    const typedCols = Object.keys(ctors).map((t) => {
+        const a = new ctors[t](nt);
+        for (let i = 0; i < nt; ++i) a[i] = (t.startsWith('float') ? tg.normal(0, 100) : Math.floor(tg.u() * 1e10) - 5e9);
+        return new Column(`c_${t}`, a);
+    });
+    const f32 = typedCols[6].data, f64 = typedCols[7].data;
+    [3, 50, 51, 200].forEach((r, i) => { f64[r] = [NaN, Infinity, -Infinity, NaN][i]; });
+    [7, 50, 332].forEach((r, i) => { f32[r] = [Infinity, NaN, -Infinity][i]; });
+    f64[9] = 1e308 * 10;  // +Infinity from arithmetic
+    f64[10] = 5e-324; f64[11] = -0;
+    const typed = new DataTable(typedCols);
+    fx.meta.typed_types = typed.columns.map(col => col.dataType);
+    addTable(fx, 'typed_in_', typed);
+    const typedOut = processDataTable(typed, [{ kind: 'filterNaN' }]);
+    fx.meta.typed_out_types = typedOut.columns.map(col => col.dataType);
+    addTable(fx, 'typed_out_', typedOut);
+
+    // combine over four tables: mixed types per name, a duplicate column in the first table,
+    // an empty table, columns absent from some tables
+    const mk = (name, ctor, vals) => new Column(name, ctor.from(vals));
+    const t0 = new DataTable([mk('x', Float32Array, [1, 2]), mk('id', Uint32Array, [10, 11]), mk('x', Float32Array, [5, 6]),
+        mk('w', Float64Array, [0.1, 0.2])]);
+    const t1 = new DataTable([mk('id', Int32Array, [-1, -2, -3]), mk('x', Float32Array, [7, 8, 9]), mk('q', Int16Array, [300, -300, 1])]);
+    const t2 = new DataTable([mk('x', Float32Array, []), mk('w', Float32Array, [])]);
+    const t3 = new DataTable([mk('q', Int16Array, [4]), mk('w', Float64Array, [NaN]), mk('id', Uint32Array, [4000000000]),
+        mk('b', Int8Array, [-7])]);
+    const c4 = [t0, t1, t2, t3];
+    c4.forEach((t, i) => {
+        fx.meta[`c4_${i}_types`] = t.columns.map(col => col.dataType);
+        fx.meta[`c4_${i}_names`] = t.columns.map(col => col.name);
+        t.columns.forEach((col, j) => fx.add(`c4_${i}_i${j}`, col.data));
+    });
+    const m4 = combine(c4);
+    fx.meta.c4_out_types = m4.columns.map(col => col.dataType);
+    fx.meta.c4_out_names = m4.columns.map(col => col.name);
+    m4.columns.forEach((col, j) => fx.add(`c4_out_i${j}`, col.data));
     fx.save();
 };
 

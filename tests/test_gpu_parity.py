@@ -274,3 +274,50 @@ def test_kmeans_bench_size_first_assign_and_update(ctx):
                 acc += float(v)
             want = np.float32(acc / members.numel())
             assert np.float32(cen[j, cl].item()).view(np.uint32) == want.view(np.uint32), (cl, j)
+
+
+def test_config3_chain_vs_oracle(ctx):
+    """BASELINE config 3 as one device chain (-r 0,45,0 -> filterNaN -> permuteRows ->
+    generateOrdering -> writeCompressedPly's chunk pack), inputs resident in HBM, 1M SH-3 splats
+    with 0.1% of rows holding NaN/Inf; every output array bit-exact against the oracle chain
+    (process.ts:64-145, data-table.ts:135-149, ordering.ts:4-110, write-compressed-ply.ts:56-109)"""
+    import torch
+    n = 1_000_000
+    rng = np.random.default_rng(1003)
+    names = ['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+        ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
+    cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in names}
+    cols['x'] *= 10
+    cube = rng.random(n) < 0.05  # equal-key Morton runs > 256 (SURVEY 8d)
+    cols['x'][cube] = 1 + rng.random(cube.sum()).astype(np.float32) * 1e-3
+    bad = rng.choice(n, n // 1000, replace=False)
+    for j, r in enumerate(bad):
+        cols[names[j % len(names)]][r] = [np.nan, np.inf, -np.inf][j % 3]
+    ref = {k: v.copy() for k, v in cols.items()}
+    d = {k: torch.from_numpy(v).cuda() for k, v in cols.items()}
+    # device chain
+    ctx.dev_transform(d, sh.action_params('rotate', (0, 45, 0)))
+    idx = torch.empty(n, dtype=torch.int32, device='cuda')
+    m = ctx.dev_filter_finite(d, idx)
+    kept = {k: torch.empty(m, device='cuda') for k in names}
+    ctx.dev_permute_rows(d, idx, m, kept)
+    order = torch.arange(m, dtype=torch.int32, device='cuda')
+    ctx.dev_morton_order(kept['x'], kept['y'], kept['z'], order)
+    chunk = torch.empty((m + 255) // 256 * 18, device='cuda')
+    vertex = torch.empty(m * 4, dtype=torch.int32, device='cuda')
+    shb = torch.empty(m * 45, dtype=torch.uint8, device='cuda')
+    ctx.dev_pack_compressed({k: v for k, v in kept.items() if not k.startswith('n')}, order, chunk, vertex, shb)
+    ctx.synchronize()
+    # oracle chain
+    oracle.transform(ref, oracle.transform_params(euler=(0, 45, 0)), 15)
+    oidx = oracle.filter_finite([ref[k] for k in names])
+    assert m == len(oidx)
+    same_bits(idx[:m].cpu().numpy().view(np.uint32), oidx)
+    oref = {k: v[oidx] for k, v in ref.items()}
+    for k in names:
+        same_bits(kept[k].cpu().numpy(), oref[k])
+    oorder = oracle.morton_order(oref['x'], oref['y'], oref['z'])
+    same_bits(order.cpu().numpy().view(np.uint32), oorder)
+    want = oracle.pack_compressed(oref, oorder, 45)
+    for got, w in zip((chunk, vertex, shb), want):
+        same_bits(got.cpu().numpy().view(w.dtype), w)

@@ -38,7 +38,7 @@ def test_addon_exports(addon_built):
     assert r.returncode == 0, r.stderr
     keys, ver = r.stdout.strip().rsplit(' ', 1)
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
-                                       'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
+                                       'filterNaN', 'combineLayout', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly'])
     assert ver == '1'
 
@@ -60,6 +60,34 @@ def test_no_cpu_fallback(addon_built):
              " catch (e) { console.log('THREW ' + e.message) }")
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith('THREW splat-hip:'), r.stdout
+
+
+def _table_ops(what):
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'table_ops.js'), what], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout)
+
+
+def test_js_combine_matches_reference(addon_built):
+    """combine() (index.ts:158-210) through the addon's st_combine_layout: union by (name, type),
+    duplicates of the first table kept, zero fill (host-only, no device)"""
+    out = _table_ops('combine')
+    assert out['names'] == ['x', 'id', 'x', 'w', 'id', 'q', 'w', 'b']
+    assert all(out['same']) and all(out['same3']), out
+
+
+def test_js_transform_rejects_non_f32(addon_built):
+    out = _table_ops('transform_f64')
+    assert out['threw'] and "'x' is Float64Array" in out['message'], out
+
+
+@pytest.mark.gpu
+def test_js_filter_nan_every_type_matches_reference(addon_built):
+    """filterNaN through the addon (st_filter_nan): float64 columns tested, integer columns kept,
+    each column's type preserved; the splat table too"""
+    out = _table_ops('filter')
+    assert all(out['same']) and all(out['same2']), out
 
 
 @pytest.mark.gpu
