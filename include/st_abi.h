@@ -22,6 +22,9 @@
  *                                                                               kd-tree.ts:9-100
  *   st_cluster1d / st_dev_cluster1d         cluster1d(dataTable, iters)         write-sog.ts:56-99
  *   st_sog / st_dev_sog                     writeSog texture + meta generation  write-sog.ts:110-370
+ *   st_set_devices / st_group_sog /         writeSog with the rows sharded over
+ *   st_dev_sog_sharded                      GPUs (RCCL; device choice of        write-sog.ts:241-243,313
+ *                                           the reference's clusterer)
  *   st_dev_kmeans_* (step API)              one k-means iteration split at the
  *                                           centroid-sum exchange (multi-GPU)   k-means.ts:164-192
  *   st_dev_cluster1d_codebook               cluster1d's sorted codebook + byte
@@ -283,6 +286,43 @@ int st_dev_sog_scatter(st_ctx *ctx, const st_table *local, const uint32_t *pos, 
                        st_sog_meta *meta, const st_sog_textures *out);
 int st_dev_sog_shn_centroids(st_ctx *ctx, const uint8_t *codebook_labels, int32_t sh_coeffs, int32_t palette,
                              uint8_t *out);
+
+/* ---- multi-GPU writeSog, native (SURVEY 8b st_set_devices, 8e) ----------------
+ * The reference picks one device for its clusterer (write-sog.ts:241-243, :313); here the
+ * splat rows are sharded across GPUs and the library runs the whole writeSog: k-means
+ * centroid sums all-reduced over RCCL every iteration (exact: DESIGN.md (e)), rank 0 orders
+ * the global table (Morton) and gathers the texels.  Results equal st_sog on the global table.
+ * Rows of the global table = the input tables concatenated in order (combine(), index.ts:
+ * 158-210: float32 columns by name, absent columns zero, band from the union of names). */
+typedef struct st_comm st_comm;
+typedef struct st_group st_group;
+/* process-wide: st_sog / st_sog_bundle shard their rows over GPUs 0..ngpu-1 (one host thread
+ * and stream per GPU, RCCL communicators from ncclCommInitAll); 1 (default) = one device */
+int st_set_devices(int32_t ngpu);
+int st_get_devices(int32_t *ngpu);
+/* one process per GPU: rank 0 creates the id, the launcher distributes it, every rank joins */
+int st_comm_unique_id(uint8_t id[128]);
+int st_comm_init_rank(st_ctx *ctx, int32_t world, int32_t rank, const uint8_t id[128], st_comm **out);
+void st_comm_destroy(st_comm *comm);
+/* one rank's part of a sharded writeSog: `locals` are this rank's tables (device columns; its
+ * files or file parts, in global order); every rank calls it with the same iters and draws.
+ * meta / out (device textures) are written on rank 0 only. */
+int st_dev_sog_sharded(st_ctx *ctx, st_comm *comm, const st_table *const *locals, int32_t nlocal, int32_t iters,
+                       const double *draws, uint64_t ndraws, uint64_t *used, st_sog_meta *meta,
+                       const st_sog_textures *out);
+/* a set of ranks in this process: devices[r] is rank r's GPU (repeats allowed with
+ * host_staged != 0: the exchange then goes through host memory -- several ranks on one GPU) */
+int st_group_create(const int32_t *devices, int32_t n, int32_t host_staged, st_group **out);
+void st_group_destroy(st_group *g);
+/* writeSog of the concatenation of host tables; rank r takes global rows [splits[r], splits[r+1])
+ * (splits: n + 1 ascending bounds from 0 to the row count; NULL = an even split); textures to
+ * host memory (as st_sog) or the .sog archive (as st_sog_bundle) */
+int st_group_sog(st_group *g, const st_table *const *tables, int32_t ntables, const uint64_t *splits, int32_t iters,
+                 const double *draws, uint64_t ndraws, uint64_t *used, st_sog_meta *meta,
+                 const st_sog_textures *out);
+int st_group_sog_bundle(st_group *g, const st_table *const *tables, int32_t ntables, const uint64_t *splits,
+                        int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time,
+                        uint16_t dos_date, uint8_t **out, uint64_t *out_size);
 
 /* ---- WebP lossless, CRC-32, the .sog container ---------------
  * WebP: a valid lossless VP8L stream (predictor transform + canonical prefix

@@ -109,6 +109,8 @@ struct st_ctx {
     };
     std::vector<KEv> kevents;
     std::vector<hipEvent_t> event_pool;
+    // side context on the same device (multi-GPU writeSog: rank 0's Morton order runs there)
+    st_ctx *aux = nullptr;
     // st_ctx_set_verify: snapshot of the last N-D k-means (prev / final centroids, labels)
     bool verify = false;
     int vf_d = 0, vf_k = 0;
@@ -225,5 +227,8 @@ uint32_t dist_finish(st_ctx *c, int d, int k, const double *sums, const double *
                      const uint32_t *counts, float *cen, uint32_t *pending);
 void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npairs, const double *running,
                   const uint32_t *counts, float *cen);
+
+// multi-GPU writeSog (st_multi.hip): the st_set_devices group (nullptr: one device)
+st_group *default_group();
 
 }  // namespace st

@@ -224,6 +224,7 @@ int st_ctx_create(int32_t device, st_ctx **out) {
 
 void st_ctx_destroy(st_ctx *c) {
     if (!c) return;
+    st_ctx_destroy(c->aux);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->ws.release();

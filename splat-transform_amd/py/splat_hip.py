@@ -92,6 +92,8 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
+    'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_destroy',
+    'st_dev_sog_sharded', 'st_group_create', 'st_group_destroy', 'st_group_sog', 'st_group_sog_bundle',
     'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
     'st_dev_kmeans_assign', 'st_dev_kmeans_partials',
@@ -120,12 +122,14 @@ def lib():
         L.st_last_error.restype = ctypes.c_char_p
         L.st_ctx_last_timings.restype = ctypes.c_char_p
         L.st_ctx_destroy.restype = None
+        L.st_comm_destroy.restype = None
+        L.st_group_destroy.restype = None
         L.st_free.restype = None
         L.st_webp_max_size.restype = ctypes.c_uint64
         L.st_ply_row_bytes.restype = ctypes.c_uint64
         for name in EXPORTS:
             if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy', 'st_free', 'st_webp_max_size',
-                            'st_ply_row_bytes'):
+                            'st_ply_row_bytes', 'st_comm_destroy', 'st_group_destroy'):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -201,6 +205,121 @@ def combine_layout(tables):
     ci = (ctypes.c_int32 * max(ncol.value, 1))()
     check(lib().st_combine_layout(arr, ctypes.c_int32(len(tts)), ct, ci, ctypes.byref(ncol)))
     return [(ct[i], ci[i]) for i in range(ncol.value)]
+
+
+def set_devices(n):
+    """st_set_devices: st_sog / st_sog_bundle shard their rows over GPUs 0..n-1 (RCCL)"""
+    check(lib().st_set_devices(ctypes.c_int32(n)))
+
+
+def get_devices():
+    n = ctypes.c_int32()
+    check(lib().st_get_devices(ctypes.byref(n)))
+    return n.value
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (rank 0 creates it; the launcher hands it to every rank)"""
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().st_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def _tables_arg(tables):
+    ts = [make_table(t) for t in tables]
+    arr = (ctypes.POINTER(Table) * len(ts))(*[ctypes.pointer(t) for t in ts])
+    return ts, arr
+
+
+def _sog_out(N, C, host=True, device=None):
+    W, H, pal, cw, ch = sog_geometry(N, C)
+    names = ['means_l', 'means_u', 'quats', 'scales', 'sh0'] + (['shN_labels'] if C else [])
+    if host:
+        tex = {k: np.zeros(W * H * 4, np.uint8) for k in names}
+        if C:
+            tex['shN_centroids'] = np.zeros(cw * ch * 4, np.uint8)
+    else:
+        import torch
+        tex = {k: torch.empty(W * H * 4, dtype=torch.uint8, device=device) for k in names}
+        if C:
+            tex['shN_centroids'] = torch.empty(cw * ch * 4, dtype=torch.uint8, device=device)
+    out = SogTextures(*[(_ptr(tex[k]).value if k in tex else None) for k in
+                        ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+    return tex, out, (W, H, cw, ch)
+
+
+def _union_coeffs(tables):
+    names = set()
+    for t in tables:
+        names.update(t.keys())
+    miss = next((i for i in range(45) if f'f_rest_{i}' not in names), -1)
+    return [0, 3, 8, 15][{9: 1, 24: 2, -1: 3}.get(miss, 0)]
+
+
+class Group:
+    """st_group: several ranks in this process (one context + host thread each).  host_staged: the
+    exchange goes through host memory, so ranks may share a GPU (the multi-rank tests)"""
+
+    def __init__(self, devices, host_staged=False):
+        self.h = ctypes.c_void_p()
+        arr = (ctypes.c_int32 * len(devices))(*devices)
+        check(lib().st_group_create(arr, ctypes.c_int32(len(devices)), ctypes.c_int32(1 if host_staged else 0),
+                                    ctypes.byref(self.h)))
+        self.world = len(devices)
+
+    def close(self):
+        if self.h:
+            lib().st_group_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sog(self, tables, iters, draws, splits=None):
+        """writeSog of the concatenated host tables (dicts name -> float32 array)"""
+        N = sum(len(next(iter(t.values()))) for t in tables)
+        C = _union_coeffs(tables)
+        tex, out, (W, H, cw, ch) = _sog_out(N, C)
+        ts, arr = _tables_arg(tables)
+        sp = (ctypes.c_uint64 * (self.world + 1))(*splits) if splits is not None else None
+        meta = SogMeta()
+        used = ctypes.c_uint64()
+        check(lib().st_group_sog(self.h, arr, ctypes.c_int32(len(ts)), sp, ctypes.c_int32(iters), _vp(draws),
+                                 ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                                 ctypes.byref(out)))
+        res = {k: v.reshape(H, W, 4) for k, v in tex.items() if k != 'shN_centroids'}
+        if C:
+            res['shN_centroids'] = tex['shN_centroids'].reshape(ch, cw, 4)
+        return res, meta, used.value
+
+    def sog_bundle(self, tables, iters, draws, dos_time, dos_date, splits=None):
+        ts, arr = _tables_arg(tables)
+        sp = (ctypes.c_uint64 * (self.world + 1))(*splits) if splits is not None else None
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        used = ctypes.c_uint64()
+        check(lib().st_group_sog_bundle(self.h, arr, ctypes.c_int32(len(ts)), sp, ctypes.c_int32(iters),
+                                        _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                                        ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
+                                        ctypes.byref(size)))
+        return _take(out, size), used.value
+
+
+class Comm:
+    """st_comm: this process's rank of a one-process-per-GPU RCCL job"""
+
+    def __init__(self, ctx, world, rank, uid):
+        self.h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().st_comm_init_rank(ctx.h, ctypes.c_int32(world), ctypes.c_int32(rank), buf, ctypes.byref(self.h)))
+        self.world, self.rank = world, rank
+
+    def close(self):
+        if self.h:
+            lib().st_comm_destroy(self.h)
+            self.h = ctypes.c_void_p()
 
 
 def quat_from_euler(ex, ey, ez):
@@ -606,6 +725,22 @@ class Context:
                                      ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)),
                                      ctypes.byref(used), _ptr(centroids), _ptr(labels)))
         return used.value
+
+    def dev_sog_sharded(self, comm, locals_, iters, draws, tex=None):
+        """this rank's part of a sharded writeSog; locals_: list of dicts name -> device column (this
+        rank's tables in global order); tex (rank 0): dict of device outputs as dev_sog's"""
+        ts, arr = _tables_arg(locals_)
+        meta = SogMeta()
+        used = ctypes.c_uint64()
+        out = None
+        if tex is not None:
+            out = SogTextures(*[(_ptr(tex[k]).value if k in tex else None) for k in
+                                ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        check(lib().st_dev_sog_sharded(self.h, comm.h, arr, ctypes.c_int32(len(ts)), ctypes.c_int32(iters),
+                                       _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
+                                       ctypes.byref(meta) if tex is not None else None,
+                                       ctypes.byref(out) if out is not None else None))
+        return meta, used.value
 
     def dev_sog(self, cols, iters, draws, tex):
         """tex: dict of device uint8 tensors (see sog_geometry for sizes)"""

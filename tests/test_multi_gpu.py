@@ -1,0 +1,143 @@
+"""Native multi-GPU writeSog (st_multi.hip: st_group_* / st_comm_* / st_dev_sog_sharded /
+st_set_devices) against the single-device writeSog of the global table, bit for bit.
+
+On the one-GPU test box several ranks share cuda:0 through the host-staged exchange (the same
+orchestration code as RCCL, a different transport); the RCCL transport runs at world size 1
+(in-process ncclCommInitAll, and the one-process-per-GPU ncclCommInitRank form).  Config 5's
+combine of several inputs (index.ts:158-210) is covered by tables with different schemas."""
+import numpy as np
+import pytest
+
+import oracle
+import splat_hip as sh
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+    ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
+
+
+def _table(n, seed, C=15, adversarial=False):
+    rng = np.random.default_rng(seed)
+    cols = {}
+    cube = rng.random(n) < 0.05
+    for a, off in zip('xyz', (1.0, -2.0, 3.0)):
+        cols[a] = np.where(cube, off + rng.random(n) * 1e-3, rng.normal(0, 10, n)).astype(np.float32)
+    for i in range(3):
+        cols[f'f_dc_{i}'] = rng.normal(0, 1, n).astype(np.float32)
+    for i in range(3 * C):
+        cols[f'f_rest_{i}'] = rng.normal(0, 0.1, n).astype(np.float32)
+    cols['opacity'] = rng.normal(0, 2, n).astype(np.float32)
+    for i in range(3):
+        v = rng.random(n) * 5 - 7
+        if adversarial:  # cluster sums that fail the order-free certificate (values over 15 decades)
+            u = rng.random(n)
+            v = np.where(u < 0.3, v * 1e-9, np.where(u > 0.9, v * 1e5, v))
+        cols[f'scale_{i}'] = v.astype(np.float32)
+    for i in range(4):
+        cols[f'rot_{i}'] = rng.normal(0, 1, n).astype(np.float32)
+    return cols
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    import torch  # noqa: F401
+    c = sh.Context(0)
+    yield c
+    c.close()
+
+
+def _same(got, want):
+    tex, meta, used = got
+    wtex, wmeta, wused = want
+    assert used == wused
+    assert sorted(tex) == sorted(wtex)
+    for k in wtex:
+        assert np.array_equal(tex[k], wtex[k]), k
+    for f in ('width', 'height', 'sh_bands', 'palette_size', 'shn_width', 'shn_height'):
+        assert getattr(meta, f) == getattr(wmeta, f), f
+    assert list(meta.means_min) == list(wmeta.means_min) and list(meta.means_max) == list(wmeta.means_max)
+    for f in ('scales_codebook', 'sh0_codebook', 'shn_codebook'):
+        assert np.array_equal(np.array(getattr(meta, f), np.float32).view(np.uint32),
+                              np.array(getattr(wmeta, f), np.float32).view(np.uint32)), f
+
+
+@pytest.mark.parametrize('world,splits,adv', [(2, None, False), (3, 'empty0', False), (4, 'ragged', True)])
+def test_group_host_staged_equals_single_device(ctx, world, splits, adv):
+    n = 30_011
+    cols = _table(n, 40 + world, adversarial=adv)
+    draws = np.random.default_rng(7).random(1 << 18)
+    want = ctx.sog(cols, 2, draws)
+    sp = None
+    if splits == 'empty0':
+        sp = [0, 0, n // 2, n]
+    elif splits == 'ragged':
+        sp = [0, 7, 9000, 9001, n]
+    g = sh.Group([0] * world, host_staged=True)
+    try:
+        _same(g.sog([cols], 2, draws, sp), want)
+    finally:
+        g.close()
+
+
+def test_group_combine_inputs_equals_single_device_on_combined(ctx):
+    """config 5 in small: three input tables (SH-3, SH-3, SH-0) concatenated by combine() --
+    the SH-0 table's f_rest rows are zero -- sharded over 3 ranks that cut across table bounds"""
+    tabs = [_table(9_000, 1), _table(12_345, 2), _table(7_000, 3, C=0)]
+    draws = np.random.default_rng(9).random(1 << 18)
+    combined = oracle.combine([list(t.items()) for t in tabs])
+    want = ctx.sog(dict(combined), 2, draws)
+    g = sh.Group([0, 0, 0], host_staged=True)
+    try:
+        _same(g.sog(tabs, 2, draws), want)
+        _same(g.sog(tabs, 2, draws, [0, 15_000, 15_001, 28_345]), want)
+    finally:
+        g.close()
+
+
+def test_group_rccl_world1_and_bundle(ctx):
+    cols = _table(20_000, 5)
+    draws = np.random.default_rng(11).random(1 << 18)
+    want = ctx.sog(cols, 2, draws)
+    g = sh.Group([0], host_staged=False)
+    try:
+        _same(g.sog([cols], 2, draws), want)
+        z, used = g.sog_bundle([cols], 2, draws, 0x6a2b, 0x58b1)
+        zw, usedw = ctx.sog_bundle(cols, 2, draws, 0x6a2b, 0x58b1)
+        assert used == usedw and z == zw
+    finally:
+        g.close()
+
+
+def test_comm_rank_world1_dev_sog_sharded(ctx):
+    """the one-process-per-GPU form (ncclCommInitRank) at world size 1: st_dev_sog_sharded of two
+    local tables == st_dev_sog of their concatenation"""
+    import torch
+    a, b = _table(11_000, 6), _table(6_000, 7)
+    full = {k: np.concatenate([a[k], b[k]]) for k in a}
+    draws = np.random.default_rng(13).random(1 << 18)
+    dev = lambda t: {k: torch.from_numpy(v).cuda() for k, v in t.items()}  # noqa: E731
+    W, H, pal, cw, ch = sh.sog_geometry(17_000, 15)
+    mk = lambda: {**{k: torch.zeros(W * H * 4, dtype=torch.uint8, device='cuda') for k in  # noqa: E731
+                     ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')},
+                  'shN_centroids': torch.zeros(cw * ch * 4, dtype=torch.uint8, device='cuda')}
+    t1, t2 = mk(), mk()
+    m1, u1 = ctx.dev_sog(dev(full), 2, draws, t1)
+    comm = sh.Comm(ctx, 1, 0, sh.comm_unique_id())
+    try:
+        m2, u2 = ctx.dev_sog_sharded(comm, [dev(a), dev(b)], 2, draws, t2)
+    finally:
+        comm.close()
+    torch.cuda.synchronize()
+    assert u1 == u2
+    for k in t1:
+        assert torch.equal(t1[k], t2[k]), k
+    assert list(m1.means_min) == list(m2.means_min)
+
+
+def test_set_devices(ctx):
+    assert sh.get_devices() == 1
+    sh.set_devices(1)
+    with pytest.raises(sh.StError):
+        sh.set_devices(sh.device_count() + 1)
+    assert sh.get_devices() == 1
