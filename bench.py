@@ -1,27 +1,30 @@
 #!/usr/bin/env python3
 """bench.py -- Msplats/s PLY->SOG (SH-3, 10 k-means iters) on MI355X.
 
-One step = the whole SOG device pipeline of write-sog.ts:110-370 over one
-synthetic SH-3 splat table already resident in HBM: Morton order, means /
-quats textures, cluster1d(scales), cluster1d(f_dc) + opacity, the SH palette
-k-means (K = 65,536, 10 iterations), the codebook cluster1d and the shN
-textures (the headline is the device pipeline).  The .sog
-container stage -- WebP lossless encode of the seven textures, CRC-32 and the
-ZIP layout (st_dev_sog_bundle_view, archive in pinned host memory) -- is timed
-right after on the same textures and reported in "container" with the
-end-to-end rate.
+One step = the whole SOG device pipeline of write-sog.ts:110-370 over a synthetic SH-3 splat
+table already resident in HBM: Morton order, means / quats textures, cluster1d(scales),
+cluster1d(f_dc) + opacity, the SH palette k-means (K = 65,536, 10 iterations), the codebook
+cluster1d and the shN textures (the headline is the device pipeline).  The .sog
+container stage -- WebP lossless encode of the seven textures, CRC-32 and the ZIP layout
+(st_dev_sog_bundle_view, archive in pinned host memory) -- is timed right after on the same
+textures and reported in "container" with the end-to-end rate.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S] [--total-splats T] [--merge F]
 
-N > 1 is launched by torch.distributed.run: one process per GPU, each rank holds
-a shard of S splats of one N*S-splat table (weak scaling) and the job writes the
-SOG of the whole table: k-means exchanges the centroid sums over RCCL every
-iteration (exact, splat_dist.py), Morton all-gathers x/y/z, rank 0 gathers the
-texels.
+Workloads (BASELINE.json configs):
+  N = 1 (default)       10M splats on one GPU, st_dev_sog (the metric's 1-GPU point)
+  N > 1 (default)       config 4: one 50M-splat table split N ways (strong scaling), each rank
+                        runs st_dev_sog_sharded (the library's RCCL exchange, st_multi.hip); a
+                        second record times 10M splats per GPU (weak scaling)
+  --merge F             config 5: F input tables of 10M splats (--file-splats) concatenated
+                        (combine, index.ts:158-210) + Morton + SOG, the rows split over the ranks
+  --total-splats T      one T-splat table split over the ranks
+N > 1 is launched by torch.distributed.run (one process per GPU); torch.distributed carries
+only the RCCL unique id, the barriers and the max-over-ranks timing.
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
-(the MFMA assign sweep, measured with HIP events on its own stream) and the
-CPU-oracle baseline timed on a bounded sample.
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (the MFMA assign
+sweep, measured with HIP events on its own stream), the CPU-oracle baseline timed on a
+bounded sample, and the verification of the last step's output.
 """
 import argparse
 import json
@@ -41,17 +44,25 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--splats', type=int, default=10_000_000, help='splats per GPU')
+    ap.add_argument('--splats', type=int, default=None, help='splats per GPU (weak scaling; default 10M at N = 1)')
+    ap.add_argument('--total-splats', type=int, default=None,
+                    help='one table of this many splats split over the ranks (default 50M at N > 1: config 4)')
+    ap.add_argument('--merge', type=int, default=0, help='config 5: this many input tables concatenated')
+    ap.add_argument('--file-splats', type=int, default=10_000_000, help='rows per --merge input')
+    ap.add_argument('--no-weak', action='store_true', help='N > 1: skip the 10M-per-GPU weak-scaling record')
     ap.add_argument('--iters', type=int, default=10, help='k-means iterations (reference default 10)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo to '
-                    'rehearse several ranks on one GPU)')
+    ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo with '
+                    '--dist-python rehearses several ranks on one GPU)')
     ap.add_argument('--cpu-assign-sample', type=int, default=1000)
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')
-    ap.add_argument('--dist', action='store_true', help='N = 1 through the sharded N > 1 code path (splat_dist over '
-                    'a one-rank process group) instead of st_dev_sog: its per-rank cost')
+    ap.add_argument('--no-verify', action='store_true', help='skip the output verification of the last step')
+    ap.add_argument('--dist', action='store_true', help='N = 1 through the sharded code path (st_dev_sog_sharded '
+                    'over a one-rank RCCL communicator) instead of st_dev_sog: its per-rank cost')
+    ap.add_argument('--dist-python', action='store_true', help='the sharded path through splat_dist.py '
+                    '(torch.distributed collectives around the step API) instead of the library')
     return ap.parse_args()
 
 
@@ -194,6 +205,66 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
         os.rmdir(d)
 
 
+def check_labels(sh, prev, lab, n_labels, g):
+    """sampled points: is the label the exact f64 argmin over `prev` (kd-tree.ts:26-33 order)?
+    returns (wrong labels, exact ties -- the KdTree order decides those, not checked)"""
+    import torch
+    dev = sh.device
+    d, k = prev.shape
+    n = lab.shape[0]
+    if n == 0:
+        return 0, 0
+    pts = torch.randint(0, n, (n_labels,), generator=g).to(dev)
+    lab64 = lab.long()
+    pd_all = sh[:, pts].double()
+    cd = prev.double()
+    bad, ties = 0, 0
+    for s in range(0, n_labels, 256):
+        e = min(n_labels, s + 256)
+        dist = torch.zeros(e - s, k, dtype=torch.float64, device=dev)
+        for j in range(d):
+            v = cd[j][None, :] - pd_all[j, s:e][:, None]
+            dist += v * v
+        mn = dist.min(1).values
+        got = dist.gather(1, lab64[pts[s:e], None]).squeeze(1)
+        bad += int((got != mn).sum().item())
+        ties += int(((dist == mn[:, None]).sum(1) > 1).sum().item())
+    return bad, ties
+
+
+def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7):
+    """the sharded step's output (every rank): the library's k-means snapshot on a re-run; this
+    rank's sampled labels are exact f64 argmins over the last assign's centroids, every rank holds
+    the same final centroids, and rank 0's textures equal the last timed step's"""
+    import torch
+    import torch.distributed as dist
+    before = {k: v.clone() for k, v in tex.items()} if tex else None
+    ctx.set_verify(True)
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_verify(False)
+    same = all(torch.equal(before[k], tex[k]) for k in tex) if tex else True
+    prev, cen, lab = ctx.verify_snapshot(local_sh.device)
+    g = torch.Generator(device='cpu')
+    g.manual_seed(seed + dist.get_rank())
+    bad, ties = check_labels(local_sh, prev, lab, n_labels, g)
+    ref = cen.clone()
+    dist.broadcast(ref, 0)
+    same_cen = bool(torch.equal(ref, cen))
+    t = torch.tensor([bad, ties, 0 if same else 1, 0 if same_cen else 1], dtype=torch.float64,
+                     device=local_sh.device)
+    dist.all_reduce(t)
+    same_cen = int(t[3].item()) == 0
+    ok = int(t[0].item()) == 0 and int(t[2].item()) == 0 and same_cen
+    return {'ok': ok, 'labels_checked': n_labels * dist.get_world_size(), 'labels_wrong': int(t[0].item()),
+            'label_exact_ties_unchecked': int(t[1].item()), 'textures_equal_timed_step': int(t[2].item()) == 0,
+            'centroids_identical_on_every_rank': same_cen,
+            'how': 'snapshot of the sharded SH palette k-means (st_ctx_set_verify) on a re-run of the step; '
+                   'each rank checks sampled labels as exact f64 argmins over the last assign\'s centroids'}
+
+
 def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
     """Re-run the step with the library's k-means snapshot on (outside the timed region) and
     check its output against the reference's definitions (k-means.ts:137-201, kd-tree.ts:22-70):
@@ -222,22 +293,8 @@ def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
     sh = torch.stack([cols[f'f_rest_{i}'] for i in range(d)])  # [d, n] f32
     g = torch.Generator(device='cpu')
     g.manual_seed(seed)
-    pts = torch.randint(0, n, (n_labels,), generator=g).to(dev)
+    bad_labels, ties = check_labels(sh, prev, lab, n_labels, g)
     lab64 = lab.long()
-    pd_all = sh[:, pts].double()
-    cd = prev.double()
-    bad_labels, ties = 0, 0
-    for s in range(0, n_labels, 256):
-        e = min(n_labels, s + 256)
-        dist = torch.zeros(e - s, k, dtype=torch.float64, device=dev)
-        for j in range(d):
-            v = cd[j][None, :] - pd_all[j, s:e][:, None]
-            dist += v * v
-        mn = dist.min(1).values
-        got = dist.gather(1, lab64[pts[s:e], None]).squeeze(1)
-        nmin = (dist == mn[:, None]).sum(1)
-        bad_labels += int((got != mn).sum().item())
-        ties += int((nmin > 1).sum().item())
     # centroids: sequential f64 mean of the members (numpy cumsum is a left-to-right chain)
     counts = torch.bincount(lab64, minlength=k)
     nonempty = torch.nonzero(counts > 0).squeeze(1)
@@ -271,6 +328,32 @@ def ctypes_char_array(size):
     return ctypes.c_char * size
 
 
+def rank_tables(args, world, rank, dev):
+    """this rank's input tables (device columns) and the workload's description"""
+    if args.merge:
+        F, S = args.merge, args.file_splats
+        total = F * S
+        lo, hi = total * rank // world, total * (rank + 1) // world
+        tabs = []
+        for f in range(F):
+            a, b = max(lo, f * S), min(hi, (f + 1) * S)
+            if b > a or (f == F - 1 and not tabs):
+                full = synth_table(S, 5001 + f, dev)  # SURVEY 8d: merge inputs use seeds 5001..
+                tabs.append({k: v[a - f * S:max(a, b) - f * S].contiguous() for k, v in full.items()})
+                del full
+        return tabs, total, (f'config 5: merge {F} x {S // 1_000_000}M-splat inputs (combine) + Morton -> writeSog '
+                             f'SH3, {args.iters} k-means iters, {total} splats over {world} GPU(s)'), 'strong'
+    if args.total_splats:
+        T = args.total_splats
+        lo, hi = T * rank // world, T * (rank + 1) // world
+        return [synth_table(hi - lo, 1002 + rank, dev)], T, (
+            f'config 4: writeSog SH3 of one {T // 1_000_000}M-splat table split {world} way(s), {args.iters} '
+            f'k-means iters'), 'strong'
+    n = args.splats
+    return [synth_table(n, 1002 + rank, dev)], n * world, (
+        f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters'), 'weak'
+
+
 def main():
     args = parse()
     import numpy as np
@@ -284,7 +367,14 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
     torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
-    sharded = world > 1 or args.dist
+    if args.splats is None and args.total_splats is None and not args.merge:
+        if world == 1:
+            args.splats = 10_000_000
+        else:
+            args.total_splats = 50_000_000  # BASELINE config 4
+    if args.splats is None:
+        args.splats = 10_000_000
+    sharded = world > 1 or args.dist or args.dist_python or bool(args.merge) or bool(args.total_splats)
     if sharded:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29533')
@@ -297,53 +387,75 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = sh.Context(local)
     ctx.set_stream(stream.cuda_stream)
-    n = args.splats
-    cols = synth_table(n, 1002 + rank, dev)
     # the host's Math.random stream (any uniform [0,1) doubles; the reference uses Math.random):
     # one stream for the whole job, identical on every rank
     draws = np.random.default_rng(42).random(2 * 65536 * (args.iters + 2))
-    W, H, pal, cw, ch = sh.sog_geometry(n * world, 15)
-    if not sharded:
-        u8 = dict(device=dev, dtype=torch.uint8)
-        tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
-        tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
+    comm = None
+    if sharded and not args.dist_python:
+        # the library's own RCCL communicator (st_comm_init_rank); torch.distributed hands out the id
+        uid = [sh.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = sh.Comm(ctx, world, rank, uid[0])
 
-        def step():
-            return ctx.dev_sog(cols, args.iters, draws, tex)
-    else:
-        # rows sharded in rank order; kmeans/cluster1d exchange centroid sums over RCCL, Morton
-        # all-gathers x/y/z, rank 0 gathers every rank's texels (splat_dist.py)
-        import splat_dist
-        ops = splat_dist.HipOps(ctx, dev)
-        comm = splat_dist.Comm()
-
+    def make_step(tabs, total):
+        """the step closure over this rank's tables and rank 0's device outputs"""
+        W, H, pal, cw, ch = sh.sog_geometry(total, 15)
+        tex = None
+        if rank == 0:
+            u8 = dict(device=dev, dtype=torch.uint8)
+            tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0',
+                                                            'shN_labels')}
+            tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
         last = {}
+        if not sharded:
+            def step():
+                return ctx.dev_sog(tabs[0], args.iters, draws, tex)
+        elif not args.dist_python:
+            def step():
+                return ctx.dev_sog_sharded(comm, tabs, args.iters, draws, tex)
+        else:
+            import splat_dist
+            ops = splat_dist.HipOps(ctx, dev)
+            pcomm = splat_dist.Comm()
+            cols = tabs[0] if len(tabs) == 1 else {k: torch.cat([t[k] for t in tabs]) for k in tabs[0]}
 
-        def step():
-            t_, m_, used = splat_dist.write_sog(ops, comm, cols, args.iters, draws)
-            last.update(tex=t_, meta=m_)
-            return None, used
+            def step():
+                t_, m_, used = splat_dist.write_sog(ops, pcomm, cols, args.iters, draws)
+                last.update(tex=t_, meta=m_)
+                if rank == 0:
+                    for k in tex:
+                        tex[k].copy_(t_[k])
+                return (splat_dist.meta_struct(m_) if rank == 0 else None), used
+        return step, tex, pal
+
+    def timed(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        if sharded:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            meta, used = step()
+        torch.cuda.synchronize()
+        if sharded:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if sharded:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, meta, used
+
+    tabs, total, workload, scaling = rank_tables(args, world, rank, dev)
+    step, tex, pal = make_step(tabs, total)
     torch.cuda.synchronize()
-
     for _ in range(args.warmup):
         step()
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     os.environ.pop('ST_TIMING', None)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        meta, used = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed, meta, used = timed(step, args.steps, 0)
     sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
     kstats = {}
     for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum',
@@ -351,6 +463,7 @@ def main():
         ms, cnt = ctx.kernel_stats(name)
         kstats[name] = {'avg_ms': ms / max(cnt, 1), 'launches': cnt}
     ctx.set_profiling(False)
+    n_local = sum(t['x'].shape[0] for t in tabs)
 
     # one more step with per-stage event marks (outside the timed region; single device only)
     stages = None
@@ -361,44 +474,60 @@ def main():
         stages = json.loads(ctx.timings())
         os.environ.pop('ST_TIMING', None)
 
-    # the last timed step's output checked against the reference's definitions (single device)
+    # the last timed step's output checked against the reference's definitions
     verification = None
-    if not sharded:
-        verification = verify_step(ctx, cols, tex, step)
+    if not args.no_verify:
+        if not sharded:
+            verification = verify_step(ctx, tabs[0], tex, step)
+        elif not args.dist_python:
+            local_sh = torch.stack([torch.cat([t[f'f_rest_{i}'] for t in tabs]) for i in range(45)])
+            verification = verify_sharded(ctx, local_sh, tex, step)
+            del local_sh
+
+    # N > 1: the weak-scaling record (10M splats per GPU) beside the strong one
+    weak = None
+    if world > 1 and not args.no_weak and not args.merge and not args.dist_python:
+        del step, tabs
+        torch.cuda.empty_cache()
+        wt = [synth_table(10_000_000, 1002 + rank, dev)]
+        wstep, _, _ = make_step(wt, 10_000_000 * world)
+        wel, _, _ = timed(wstep, args.steps, args.warmup)
+        weak = {'workload': f'writeSog SH3 10M splats per GPU ({10_000_000 * world} total), {args.iters} iters',
+                'value': 10_000_000 * world * args.steps / wel / 1e6, 'unit': 'Msplats/s',
+                'ms_per_step': wel / args.steps * 1e3, 'scaling': 'weak'}
+        del wt, wstep
 
     if rank != 0:
+        if comm:
+            comm.close()
         if sharded:
             dist.destroy_process_group()
+        if verification and not verification['ok']:
+            sys.exit(1)
         return
     # the .sog container of this step's textures on rank 0 (outside the headline's timed region)
-    if not sharded:
-        bmeta, btex, bcount = meta, tex, n
-    else:
-        import splat_dist
-        bmeta, btex, bcount = splat_dist.meta_struct(last['meta']), last['tex'], n * world
-    addr0, size0 = ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)  # warm: workspace + pinned archive
-    ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0)) if not sharded else None
+    addr0, size0 = ctx.dev_sog_bundle_view(meta, total, tex, 0, 0)  # warm: workspace + pinned archive
+    ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0))
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        _, archive_bytes = ctx.dev_sog_bundle_view(bmeta, bcount, btex, 0, 0)
+        _, archive_bytes = ctx.dev_sog_bundle_view(meta, total, tex, 0, 0)
     container_ms = (time.perf_counter() - t0) / args.steps * 1e3
     ckern = {}
     for name in ('webp.predict', 'webp.hist', 'webp.bits', 'webp.emit', 'crc32'):
         ms, cnt = ctx.kernel_stats(name)
         ckern[name] = ms / args.steps
     ctx.set_profiling(False)
-    total_splats = n * world * args.steps
-    value = total_splats / elapsed / 1e6
+    value = total * args.steps / elapsed / 1e6
     avg_sweep_s = (sweep_ms / max(sweep_launches, 1)) / 1e3
     D = 45
-    flops_per_launch = 2.0 * n * pal * D  # nearest-centroid dot products, one assign pass
+    flops_per_launch = 2.0 * n_local * pal * D  # nearest-centroid dot products, one assign pass (this rank)
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
     e2e = None
     if not sharded and not args.no_e2e:
-        e2e = end_to_end(ctx, cols, args.iters, draws, tex, ref_archive)
+        e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive)
     paths = None
     if not sharded and not args.no_paths:
         # BASELINE config 3 (-r 0,45,0, filterNaN, Morton, chunk pack -> .compressed.ply) on its own
@@ -410,14 +539,18 @@ def main():
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
     traffic, tsrc = None, None
-    tfile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_traffic.json')
-    if os.path.exists(tfile) and n == 10_000_000:
+    tfile = os.path.join(ROOT, 'profiles', 'r02', 'pmc_sweep_traffic.json')
+    if not os.path.exists(tfile):
+        tfile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_traffic.json')
+    if os.path.exists(tfile) and n_local == 10_000_000:
         traffic = json.load(open(tfile))['hbm_bytes_per_launch']
         tsrc = os.path.relpath(tfile, ROOT)
     # the engine clock the chip holds under the sweep (PMC GRBM_GUI_ACTIVE, tools/pmc.sh + pmc_util.py):
     # beside `frac` (against the 2.4 GHz headline peak), the fraction of the peak at that clock
     clock = None
-    ufile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_util.json')
+    ufile = os.path.join(ROOT, 'profiles', 'r02', 'pmc_sweep_util.json')
+    if not os.path.exists(ufile):
+        ufile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_util.json')
     if os.path.exists(ufile) and achieved:
         u = json.load(open(ufile))
         clock = {'engine_clock_GHz': u['engine_clock_GHz'], 'mfma_busy_frac': u['mfma_busy_frac'],
@@ -433,14 +566,14 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': elapsed / args.steps * 1e3,
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': scaling,
         'vs_baseline': None,
         'dtype': 'f64+f32 (bit-exact JS semantics); fp16 MFMA (f32 accumulate) for the assign prefilter',
-        'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seed 1002+rank), resident in HBM',
-        'config': {'workload': f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters, '
-                               f'paletteSize {pal}',
-                   'splats_per_gpu': n, 'splats_total': n * world, 'sh_bands': 3, 'palette_size': pal,
-                   'iterations': args.iters, 'parallelism': f'rowshard{world}' if sharded else 'single'},
+        'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seeds 1002+rank / 5001+file), resident in HBM',
+        'config': {'workload': workload, 'splats_total': total, 'splats_rank0': n_local, 'sh_bands': 3,
+                   'palette_size': pal, 'iterations': args.iters,
+                   'parallelism': (f'rowshard{world}' + ('-pytorch' if args.dist_python else '-native'))
+                   if sharded else 'single'},
         'roofline': {
             'kernel': 'k_sweep<KS=3> (v_mfma_f32_32x32x16_f16 nearest-centroid score |c|^2-2p.c, top-3 tile minima per splat)',
             'bound': 'mfma',
@@ -465,18 +598,21 @@ def main():
             'archive_bytes': archive_bytes,
             'kernel_ms': ckern,
             'end_to_end_ms_per_step': elapsed / args.steps * 1e3 + container_ms,
-            'end_to_end_Msplats_per_s': (n * world) / (elapsed / args.steps + container_ms / 1e3) / 1e6,
+            'end_to_end_Msplats_per_s': total / (elapsed / args.steps + container_ms / 1e3) / 1e6,
         },
         'end_to_end_file': e2e,
         'paths_config3': paths,
         'stages_ms': stages,
         'kernels': kstats,
         'draws_used_per_step': used,
+        'weak_10M_per_gpu': weak,
         'verified': verification['ok'] if verification else None,
         'verification': verification,
     }
     _RESULT.write(json.dumps(out) + '\n')
     _RESULT.flush()
+    if comm:
+        comm.close()
     if sharded:
         dist.destroy_process_group()
     if verification and not verification['ok']:

@@ -400,7 +400,10 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     auto *pending = wsT<uint32_t>(c, t + ".pend", dk);
     auto *running = wsT<double>(c, t + ".run", dk);
     std::vector<uint32_t> hC(k);
+    const size_t cbytes = 4 * dk;
     for (int it = 0; it < iters; ++it) {
+        if (c->verify && d > 1 && it == iters - 1)  // st_ctx_set_verify: the last assign's centroids
+            ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         if (P.n) {
             dist_assign(c, P.pts.data(), d, P.n, k, cen, labels);
             dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
@@ -440,6 +443,15 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
             cls.push_back((uint32_t)i);
         }
         supply_rows(c, co, P, rows, cls, k, cen);
+    }
+    if (c->verify && d > 1 && iters > 0) {  // final centroids (replicated) and this rank's labels
+        ST_HIP(hipMemcpyAsync(ws(c, "verify.cen", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
+        if (P.n)
+            ST_HIP(hipMemcpyAsync(ws(c, "verify.labels", P.n * 4), labels, P.n * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        c->vf_d = d;
+        c->vf_k = k;
+        c->vf_n = P.n;
     }
     return cursor;
 }
