@@ -295,7 +295,14 @@ const decompressPly = (ply) => {
     return new DataTable(out.map((d, i) => new Column(names[i], d)));
 };
 
+// the GPUs writeSog shards its rows over (st_set_devices; the reference's device choice is
+// write-sog.ts:241-243): 1 (default) = one device
+const setDevices = (n) => addon.setDevices(n);
+const getDevices = () => addon.getDevices();
+
 module.exports = {
+    setDevices,
+    getDevices,
     Column,
     DataTable,
     addon,

@@ -247,6 +247,27 @@ fail:
     return NULL;
 }
 
+/* setDevices(n): writeSog (sog / sogBundle) shards its rows over GPUs 0..n-1 (st_set_devices) */
+static napi_value js_set_devices(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    {
+        const int rc = st_set_devices((int32_t)num(env, argv[0]));
+        if (rc != ST_OK) return throw_st(env, rc);
+    }
+    return NULL;
+fail:
+    return NULL;
+}
+
+static napi_value js_get_devices(napi_env env, napi_callback_info info) {
+    int32_t n = 1;
+    (void)info;
+    st_get_devices(&n);
+    return make_num(env, n);
+}
+
 /* TypedArray element type -> st_ply_type (0: not one of the reference's eight) */
 static int ply_type_of(napi_typedarray_type t, size_t *esize) {
     switch (t) {
@@ -863,6 +884,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"transform", js_transform},
                {"filterFinite", js_filter_finite},
                {"filterNaN", js_filter_nan},
+               {"setDevices", js_set_devices},
+               {"getDevices", js_get_devices},
                {"combineLayout", js_combine_layout},
                {"mortonOrder", js_morton},
                {"packCompressed", js_pack_compressed},

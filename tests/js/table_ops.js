@@ -50,5 +50,15 @@ if (what === 'combine') {
         out.threw = true;
         out.message = e.message;
     }
+} else if (what === 'devices') {
+    out.before = host.getDevices();
+    host.setDevices(1);
+    out.after = host.getDevices();
+    try {
+        host.setDevices(1000);
+        out.threw = false;
+    } catch (e) {
+        out.threw = /status -1\)/.test(e.message);
+    }
 }
 console.log(JSON.stringify(out));

@@ -38,7 +38,7 @@ def test_addon_exports(addon_built):
     assert r.returncode == 0, r.stderr
     keys, ver = r.stdout.strip().rsplit(' ', 1)
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
-                                       'filterNaN', 'combineLayout', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
+                                       'filterNaN', 'combineLayout', 'setDevices', 'getDevices', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly'])
     assert ver == '1'
 
@@ -88,6 +88,13 @@ def test_js_filter_nan_every_type_matches_reference(addon_built):
     each column's type preserved; the splat table too"""
     out = _table_ops('filter')
     assert all(out['same']) and all(out['same2']), out
+
+
+@pytest.mark.gpu
+def test_js_set_devices(addon_built):
+    """setDevices (st_set_devices): the GPU count writeSog shards over"""
+    out = _table_ops('devices')
+    assert out == {'before': 1, 'after': 1, 'threw': True}, out
 
 
 @pytest.mark.gpu
