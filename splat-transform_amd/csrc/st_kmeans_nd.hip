@@ -313,17 +313,18 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
     // being folded into v_min plus two NaN canonicalisations
     float ninf;
     asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(ninf));
-    // per point tile: top-3 of the tile minima seen by this lane-half and the tiles of the
-    // best two
+    // per point tile: top-3 of the keyed tile minima seen by this lane-half (key = the tile
+    // minimum with the tile index in its low kbits mantissa bits)
     float m1[PT], m2[PT], m3[PT], th[PT];
-    uint32_t t1[PT], t2[PT];
+    const uint32_t kbits = ctiles > 1 ? 32u - (uint32_t)__builtin_clz(ctiles - 1) : 0u;
+    const uint32_t kmask = (1u << kbits) - 1u;
+    uint32_t kmask_v;  // in a VGPR: v_bfi_b32 takes one scalar operand (the tile index)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kmask_v) : "s"(kmask));
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         m1[t] = __builtin_inff();
         m2[t] = __builtin_inff();
         m3[t] = __builtin_inff();
-        t1[t] = 0;
-        t2[t] = 0;
         th[t] = -__builtin_inff();
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -344,20 +345,14 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
         for (int r = (q == 0 ? 1 : r0); r < r1; ++r) mn = fminf(mn, sc[r]);
         if (q == KS - 1) {
             if (MODE == 0) {
-                // selects on scalar temporaries (a select between two array elements is
-                // lowered through scratch memory)
-                // a tile minimum >= m3 leaves the top-3 unchanged; late in the sweep most
-                // wave-wide slots have none below it, so the update is skipped
-                if (__builtin_expect(__ballot(mn < m3[t]) != 0, 0)) {
-                    const bool lt1 = mn < m1[t], lt2 = mn < m2[t];
-                    const uint32_t o1 = t1[t], o2 = t2[t];
-                    const uint32_t n2 = lt2 ? ctile : o2;
-                    t2[t] = lt1 ? o1 : n2;
-                    t1[t] = lt1 ? ctile : o1;
-                    m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], mn);
-                    m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], mn);
-                    m1[t] = fminf(m1[t], mn);
-                }
+                // branch-free top-3: the tile index rides in the key's low kbits bits (v_bfi;
+                // |key - mn| < 2^kbits ulp, added to the decision window), two v_med3 + one v_min
+                uint32_t kb;
+                asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(kb) : "v"(kmask_v), "s"(ctile), "v"(mn));
+                const float key = __builtin_bit_cast(float, kb);
+                m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], key);
+                m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], key);
+                m1[t] = fminf(m1[t], key);
             } else if (mn <= th[t]) {
                 // candidates are rare (a handful of the K centroids per point)
                 const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
@@ -402,7 +397,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
 #pragma unroll
     for (int t = 0; t < PT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) buf[t][r] = __builtin_inff();  // no-op slots before the first
+        for (int r = 0; r < 16; ++r) buf[t][r] = 0x1p+120f;  // slots before the first: finite keys, never kept
     uint32_t tile_prev = 0;  // centroid tile of the previous ct iteration
     for (uint32_t sg = sg_begin; sg < sg_end; ++sg) {
         const int cur = (sg - sg_begin) & 1;
@@ -458,7 +453,8 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
         // (tile, lane-half) of the best two
         const float a1 = m1[t], a2 = m2[t], a3 = m3[t];
         const float b1 = __shfl_xor(a1, 32, 64), b2 = __shfl_xor(a2, 32, 64), b3 = __shfl_xor(a3, 32, 64);
-        const uint32_t ca1 = t1[t] * 2u + (uint32_t)h, ca2 = t2[t] * 2u + (uint32_t)h;
+        const uint32_t ca1 = (__builtin_bit_cast(uint32_t, a1) & kmask) * 2u + (uint32_t)h;
+        const uint32_t ca2 = (__builtin_bit_cast(uint32_t, a2) & kmask) * 2u + (uint32_t)h;
         const uint32_t cb1 = __shfl_xor(ca1, 32, 64), cb2 = __shfl_xor(ca2, 32, 64);
         const float nm1 = fminf(a1, b1);
         const float nm2 = fminf(fmaxf(a1, b1), fminf(a2, b2));
@@ -468,16 +464,20 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
         const uint32_t p = (tile0 + t) * 32 + (lane & 31);
         bool is_amb = false, is_pair = false;
         if (h == 0 && p < npts) {
+            // keys differ from the tile minima by < 2^kbits ulp <= |key| 2^(kbits - 23) (+ one
+            // denormal ulp); 2^-20 |key| on top covers the f32 roundings of the window sums
+            const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
+            const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float W = wbound2(bnd, pnorm[p], chalf[code1], cm);
-            if (nm2 > nm1 + W) {
+            if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
-            } else if (nm3 > nm1 + W) {
+            } else if (nm3 > nm1 + W + e1 + (__builtin_fabsf(nm3) * kr + ka)) {
                 is_pair = true;  // every candidate lies in the two best tile-halves
                 labels[p] = 0xfffffffeu;
             } else {
                 is_amb = true;
                 labels[p] = 0xffffffffu;
-                thr[p] = nm1 + W;
+                thr[p] = nm1 + e1 + W;
             }
         }
         const uint64_t pmask = __ballot(is_pair);
