@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'build', 'libst_oracle.so')
+LIB_PATH = os.environ.get('ST_ORACLE_LIB') or os.path.join(HERE, 'build', 'libst_oracle.so')
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags='C')
 _lib = None

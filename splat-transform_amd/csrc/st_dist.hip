@@ -35,6 +35,7 @@ __global__ __launch_bounds__(256) void k_seg_keys(const uint32_t *labels, uint32
                                                   const float *vals, uint32_t *keys, uint32_t *payload) {
     const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;  // also an empty shard (seg_len = 0)
     uint32_t seg = i / seg_len, next = (seg + 1) * seg_len;
     for (; i < n; i += stride) {
         while (i >= next) {

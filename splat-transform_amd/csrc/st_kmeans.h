@@ -6,7 +6,7 @@
 namespace st {
 namespace km {
 
-enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u, ERR_INIT_WINDOW = 8u };
+enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u, ERR_INIT_WINDOW = 8u, ERR_DRAW_RANGE = 16u };
 
 // device-resident k-means state (one per call)
 struct State {

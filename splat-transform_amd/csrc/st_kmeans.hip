@@ -195,7 +195,12 @@ __global__ __launch_bounds__(256) void k_reseed(const float *const *cols, int d,
             atomicOr(&st->err, ERR_DRAWS);
             continue;
         }
-        const uint64_t row = (uint64_t)__builtin_floor(draws[di] * (double)n);
+        const double dr = draws[di];
+        if (!(dr >= 0.0 && dr < 1.0)) {  // a Math.random draw outside [0, 1): no row to read
+            atomicOr(&st->err, ERR_DRAW_RANGE);
+            continue;
+        }
+        const uint64_t row = (uint64_t)__builtin_floor(dr * (double)n);
         for (int j = 0; j < d; ++j) cen[(uint64_t)j * k + c] = cols[j][row];
     }
 }
@@ -243,7 +248,12 @@ __global__ __launch_bounds__(RS1_T) void k_reseed_small(const float *const *cols
             atomicOr(&st->err, ERR_DRAWS);
             continue;
         }
-        const uint64_t row = (uint64_t)__builtin_floor(draws[di] * (double)n);
+        const double dr = draws[di];
+        if (!(dr >= 0.0 && dr < 1.0)) {
+            atomicOr(&st->err, ERR_DRAW_RANGE);
+            continue;
+        }
+        const uint64_t row = (uint64_t)__builtin_floor(dr * (double)n);
         for (int j = 0; j < d; ++j) cen[(uint64_t)j * k + c] = cols[j][row];
     }
     __syncthreads();  // every thread has read st->cursor
@@ -455,6 +465,7 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     if (hs.err & ERR_INIT_WINDOW)  // the device window held fewer than k distinct rows
         return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, true);
     ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
+    ST_REQUIRE(!(hs.err & ERR_DRAW_RANGE), ST_ERR_ARG, "kmeans: a re-seed draw outside [0, 1)");
     ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");
     return hs.cursor;
 }

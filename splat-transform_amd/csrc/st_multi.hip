@@ -439,7 +439,9 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
         for (int i = 0; i < k; ++i) {
             if (hC[i]) continue;
             ST_REQUIRE(cursor < ndraws, ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
-            rows.push_back((uint64_t)std::floor(draws[cursor++] * (double)P.N));
+            const double dr = draws[cursor++];
+            ST_REQUIRE(dr >= 0.0 && dr < 1.0, ST_ERR_ARG, "kmeans: a re-seed draw outside [0, 1)");
+            rows.push_back((uint64_t)std::floor(dr * (double)P.N));
             cls.push_back((uint32_t)i);
         }
         supply_rows(c, co, P, rows, cls, k, cen);

@@ -113,11 +113,12 @@ class HipOps:
         self.device = device
         # library kernels and the torch glue between them share one stream.  It must be a
         # real stream: st_ctx_set_stream(NULL) selects the context's own stream, so torch's
-        # legacy default stream (handle 0) would not order against the library.
+        # legacy default stream (handle 0) would not order against the library.  The entry
+        # points below run their torch glue on it (`_on_stream`); the caller's current stream
+        # is left as it was.
         cur = torch.cuda.current_stream(device)
         if cur.cuda_stream == 0:
             cur = torch.cuda.Stream(device)
-            torch.cuda.set_stream(cur)
         self.stream = cur
         ctx.set_stream(cur.cuda_stream)
 
@@ -229,6 +230,24 @@ class _Points:
         return r, g - offs[r]
 
 
+def _on_stream(f):
+    """run an entry point's torch glue on the library's stream (ops.stream), then restore the
+    caller's current stream"""
+    import functools
+
+    @functools.wraps(f)
+    def wrap(ops, *a, **kw):
+        if getattr(ops, 'stream', None) is None:  # a host backend (the tests' CPU stand-in)
+            return f(ops, *a, **kw)
+        caller = torch.cuda.current_stream(ops.device)
+        ops.stream.wait_stream(caller)  # the inputs were produced on the caller's stream
+        with torch.cuda.stream(ops.stream):
+            out = f(ops, *a, **kw)
+        caller.wait_stream(ops.stream)  # and the outputs are read there
+        return out
+    return wrap
+
+
 def _gather_rows(ops, comm, P, rows):
     """values (d, len(rows)) of global points `rows`, supplied by their owners"""
     m = len(rows)
@@ -249,6 +268,7 @@ def _gather_rows(ops, comm, P, rows):
     return out[:, :m]
 
 
+@_on_stream
 def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
     """kmeans over the global table (k-means.ts:137-201, --no-gpu results).
 
@@ -303,6 +323,8 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
             for _ in empty:
                 if cursor >= len(draws):
                     raise sh.StError(sh.ST_ERR_DRAWS, 'kmeans: Math.random draws exhausted while re-seeding')
+                if not 0.0 <= draws[cursor] < 1.0:  # the row would fall outside the table
+                    raise sh.StError(sh.ST_ERR_ARG, 'kmeans: a re-seed draw outside [0, 1)')
                 rows.append(math.floor(draws[cursor] * P.N))
                 cursor += 1
             vals = _gather_rows(ops, comm, P, rows)
@@ -310,6 +332,7 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
     return cen, labels, cursor
 
 
+@_on_stream
 def cluster1d(ops, comm, shard, cols, iters, draws):
     """cluster1d (write-sog.ts:56-99) over the global table: codebook (256) + byte labels
     of the local rows, one column block per input column"""
@@ -319,6 +342,7 @@ def cluster1d(ops, comm, shard, cols, iters, draws):
 
 
 # ---- writeSog ------------------------------------------------------------------------------
+@_on_stream
 def write_sog(ops, comm, cols, iters, draws):
     """writeSog's textures + meta (write-sog.ts:110-370) for the global table.
     cols: dict name -> local device column.  Returns (textures, meta) on rank 0 (None elsewhere)
@@ -441,6 +465,7 @@ def meta_struct(meta):
     return m
 
 
+@_on_stream
 def write_sog_bundle(ops, comm, cols, iters, draws, dos_time, dos_date):
     """writeSog to a .sog archive (write-sog.ts:110-370 + zip-writer.ts) for the global table:
     the textures of write_sog, then WebP + CRC + ZIP on rank 0's device.  Returns the archive
