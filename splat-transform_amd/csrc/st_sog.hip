@@ -216,7 +216,8 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
     const float *m[8];
     for (int i = 0; i < 8; ++i) {
         m[i] = col_or_null(t, members[i]);
-        ST_REQUIRE(m[i], ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
+        // an empty shard's columns may be NULL (no rows to read): only the meta is computed
+        ST_REQUIRE(m[i] || n == 0, ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
     }
     MeansArgs ma{};
     for (int a = 0; a < 3; ++a) {

@@ -128,7 +128,11 @@ class HipOps:
     def zeros(self, shape, dtype):
         return torch.zeros(shape, dtype=dtype, device=self.device)
 
+    # an empty shard (a rank with no rows) skips the library calls over its rows: their
+    # contributions are the identities of the collectives that follow
     def minmax(self, cols):
+        if cols[0].numel() == 0:
+            return [math.inf] * len(cols), [-math.inf] * len(cols)
         return self.ctx.dev_minmax(cols)
 
     def init_rows(self, draws, n, k):
@@ -142,10 +146,13 @@ class HipOps:
         return out
 
     def prepare(self, pts):
-        self.ctx.dev_kmeans_prepare(pts)
+        self.rows = pts[0].numel()
+        if self.rows:
+            self.ctx.dev_kmeans_prepare(pts)
 
     def assign(self, pts, k, cen, labels):
-        self.ctx.dev_kmeans_assign(pts, k, cen, labels)
+        if pts[0].numel():
+            self.ctx.dev_kmeans_assign(pts, k, cen, labels)
 
     def partials(self, pts, nseg, k, labels):
         d = len(pts)
@@ -153,11 +160,14 @@ class HipOps:
         sabs = self.empty((nseg, d, k), torch.float64)
         emin = self.empty((nseg, d, k), torch.int32)
         counts = self.empty((nseg, k), torch.int32)
+        if pts[0].numel() == 0:  # st_dist.hip k_partials: sums 0, ulp exponent 2^20 for no members
+            return sums.zero_(), sabs.zero_(), emin.fill_(1 << 20), counts.zero_()
         self.ctx.dev_kmeans_partials(pts, nseg, k, labels, sums, sabs, emin, counts)
         return sums, sabs, emin, counts
 
     def seqsum(self, d, k, seg, pairs, running, emin, sabs):
-        self.ctx.dev_kmeans_seqsum(d, k, seg, pairs, running, emin, sabs)
+        if self.rows:  # an empty shard adds nothing to the running sums
+            self.ctx.dev_kmeans_seqsum(d, k, seg, pairs, running, emin, sabs)
 
     def finish(self, d, k, sums, sabs, emin, counts, cen):
         pending = self.empty((d * k,), torch.int32)

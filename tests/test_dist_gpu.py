@@ -38,7 +38,7 @@ def _table(n, seed, C=15):
     return cols
 
 
-def _rank(rank, world, backend, port, n, seed, iters, q, C=15):
+def _rank(rank, world, backend, port, n, seed, iters, q, C=15, empty=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dev = torch.device('cuda', 0)
@@ -48,6 +48,8 @@ def _rank(rank, world, backend, port, n, seed, iters, q, C=15):
     import splat_dist
     full = _table(n, seed, C)
     cuts = {1: [0, n], 3: [0, n // 5, n * 3 // 5, n], 2: [0, n * 3 // 7, n], 4: [0, n // 7, n * 3 // 7, n * 6 // 7, n]}[world]  # uneven shards
+    if empty:  # rank 0 holds no rows
+        cuts = [0, 0] + cuts[2:]
     lo, hi = cuts[rank], cuts[rank + 1]
     cols = {k: torch.from_numpy(v[lo:hi].copy()).to(dev) for k, v in full.items()}
     draws = np.random.default_rng(seed + 1).random(1 << 20)
@@ -180,13 +182,15 @@ def test_dist_cluster1d_adversarial_matches_single_device(world, cap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('backend,world,C', [('gloo', 2, 15), ('gloo', 4, 15), ('nccl', 1, 15), ('gloo', 2, 0),
-                                             ('gloo', 3, 3), ('gloo', 2, 8)])
-def test_multi_rank_write_sog_matches_single_device(backend, world, C):
+@pytest.mark.parametrize('backend,world,C,empty', [('gloo', 2, 15, False), ('gloo', 4, 15, False),
+                                                   ('nccl', 1, 15, False), ('gloo', 2, 0, False),
+                                                   ('gloo', 3, 3, False), ('gloo', 2, 8, False),
+                                                   ('gloo', 3, 15, True)])
+def test_multi_rank_write_sog_matches_single_device(backend, world, C, empty):
     """gloo: 2 to 4 ranks sharing cuda:0.  nccl: RCCL refuses two ranks on one GPU, so the
     RCCL leg runs the same sharded code path at world size 1 (device-tensor collectives,
     every dtype / reduce op the 8-GPU job issues).  C: SH coefficients per channel (bands
-    3, 0, 1, 2; write-sog.ts:296)."""
+    3, 0, 1, 2; write-sog.ts:296).  empty: rank 0 holds no rows."""
     import torch.multiprocessing as mp
     import splat_hip as sh
     n, seed, iters = 24000, 5, 3
@@ -196,7 +200,8 @@ def test_multi_rank_write_sog_matches_single_device(backend, world, C):
     s.close()
     mctx = mp.get_context('spawn')
     q = mctx.Queue()
-    procs = [mctx.Process(target=_rank, args=(r, world, backend, port, n, seed, iters, q, C)) for r in range(world)]
+    procs = [mctx.Process(target=_rank, args=(r, world, backend, port, n, seed, iters, q, C, empty))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = _collect(q, procs, 1)[0]
