@@ -41,6 +41,10 @@
  *   st_ply_read / st_dev_ply_read           readPly element rows -> columns     read-ply.ts:139-188
  *   st_dev_ply_transpose                    (the same, rows already in HBM)     read-ply.ts:165-182
  *   st_decompress_ply / st_dev_...          decompressPly                       readers/decompress-ply.ts:82-232
+ *   st_process                              processDataTable(dataTable, actions) process.ts:64-145
+ *   st_compressed_ply / st_dev_...          processDataTable + writeCompressedPly
+ *                                           (CLI: in.ply [actions] out.compressed.ply) index.ts:463-496,
+ *                                                                               write-compressed-ply.ts:31-115
  *
  * Conventions
  *  - Columns are SoA float32 arrays of n rows (the reference's Float32Array
@@ -235,6 +239,42 @@ int st_dev_cluster1d(st_ctx *ctx, const float *const *cols, int32_t ncols, uint6
                      const double *draws, uint64_t ndraws, uint64_t *used, float *centroids256, uint8_t *labels);
 int st_dev_sog(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                uint64_t *used, st_sog_meta *meta, const st_sog_textures *out);
+
+/* ---- processDataTable + writeCompressedPly in one upload (BASELINE config 3) -----
+ * The reference's action list (process.ts:64-145) applied to a typed table in order:
+ *   ST_ACTION_TRANSFORM     one transform() pass (translate / rotate / scale, process.ts:72-83),
+ *                           params from st_transform_params_make; the transformed columns
+ *                           (x y z rot_* scale_* f_rest_*) must be float32 (ST_ERR_UNSUPPORTED)
+ *   ST_ACTION_FILTER_NAN    filterNaN (process.ts:84-95)
+ *   ST_ACTION_FILTER_VALUE  filterByValue (process.ts:97-109): row[column] <compare> value;
+ *                           compare outside ST_CMP_LT..ST_CMP_NEQ keeps every row (:108)
+ *   ST_ACTION_FILTER_BANDS  filterBands (process.ts:110-134): f_rest columns renamed / dropped
+ *                           (the input band is read from the ORIGINAL table, as :111 does)
+ *   ST_ACTION_PARAM         no-op (:135-138)
+ * st_process: the processed table's columns are matched by (name, type) into dst (host, capacity
+ * src->n rows); *out_m = its rows.  st_compressed_ply: the processed table goes on through
+ * writeCompressedPly's ordering and chunk loop (write-compressed-ply.ts:31-115): chunk
+ * ceil(m/256)*18 f32, vertex m*4 u32, sh m*3C u8 (host, sized for src->n rows and src's band);
+ * *out_m = m, *out_sh_coeffs = C.  st_dev_compressed_ply: the same over device columns
+ * (transformed in place, like the reference's table) into device outputs. */
+enum st_action_kind {
+    ST_ACTION_TRANSFORM = 1, ST_ACTION_FILTER_NAN, ST_ACTION_FILTER_VALUE, ST_ACTION_FILTER_BANDS, ST_ACTION_PARAM
+};
+enum st_compare { ST_CMP_LT = 0, ST_CMP_LTE, ST_CMP_GT, ST_CMP_GTE, ST_CMP_EQ, ST_CMP_NEQ };
+typedef struct {
+    int32_t kind;                    /* st_action_kind */
+    int32_t compare;                 /* ST_ACTION_FILTER_VALUE: st_compare */
+    const char *column;              /* ST_ACTION_FILTER_VALUE */
+    double value;                    /* ST_ACTION_FILTER_VALUE */
+    int32_t bands;                   /* ST_ACTION_FILTER_BANDS: output bands 0..3 */
+    st_transform_params transform;   /* ST_ACTION_TRANSFORM */
+} st_action;
+int st_process(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions, const st_ttable *dst,
+               uint64_t *out_m);
+int st_compressed_ply(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions, float *chunk,
+                      uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs);
+int st_dev_compressed_ply(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions,
+                          float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs);
 
 /* ---- multi-GPU building blocks -----------------------------------
  * One process per GPU; rows are sharded in contiguous ranges in rank order; the

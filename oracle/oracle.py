@@ -260,3 +260,62 @@ def filter_nan(cols):
             keep &= np.isfinite(a)
     idx = np.nonzero(keep)[0].astype(np.uint32)
     return [(name, a[idx]) for name, a in cols], idx
+
+
+def _band_coeffs(names):
+    """{ '9': 1, '24': 2, '-1': 3 }[index of the first missing f_rest_i] ?? 0, as coefficients"""
+    first_missing = next((i for i in range(45) if f'f_rest_{i}' not in names), -1)
+    return {9: 3, 24: 8, -1: 15}.get(first_missing, 0)
+
+
+def process(cols, actions):
+    """processDataTable (process.ts:64-145) over a list of (name, array): actions are dicts with
+    'kind' translate / rotate (Euler degrees) / scale / filterNaN / filterByValue (columnName,
+    comparator, value) / filterBands (value) / param.  transform() runs in the C restatement on
+    the float32 columns; the filters are numpy predicates + the permuteRows gather; filterBands
+    renames / drops f_rest columns against the ORIGINAL table's band (process.ts:111)."""
+    cols = [(k, np.array(a, copy=True)) for k, a in cols]
+    in_coeffs = _band_coeffs([k for k, _ in cols])
+    for act in actions:
+        kind = act['kind']
+        if kind in ('translate', 'rotate', 'scale'):
+            v = act['value']
+            p = (transform_params(t=v) if kind == 'translate' else
+                 transform_params(euler=v) if kind == 'rotate' else transform_params(s=float(v)))
+            f32 = {k: a for k, a in cols if a.dtype == np.float32}
+            if f32:
+                transform(f32, p, _band_coeffs(list(f32)))
+        elif kind == 'filterNaN':
+            cols, _ = filter_nan(cols)
+        elif kind == 'filterByValue':
+            n = len(cols[0][1]) if cols else 0
+            col = next((a for k, a in cols if k == act['columnName']), None)
+            x = np.full(n, np.nan) if col is None else col.astype(np.float64)
+            v = float(act['value'])
+            with np.errstate(invalid='ignore'):
+                keep = {'lt': lambda: x < v, 'lte': lambda: x <= v, 'gt': lambda: x > v, 'gte': lambda: x >= v,
+                        'eq': lambda: x == v, 'neq': lambda: ~(x == v)}.get(act['comparator'],
+                                                                          lambda: np.ones(n, bool))()
+            idx = np.nonzero(keep)[0]
+            cols = [(k, a[idx]) for k, a in cols]
+        elif kind == 'filterBands':
+            out_coeffs = [0, 3, 8, 15][act['value']]
+            if out_coeffs < in_coeffs:
+                mp = {}
+                for i in range(in_coeffs):
+                    for j in range(3):
+                        mp[f'f_rest_{i + j * in_coeffs}'] = f'f_rest_{i + j * out_coeffs}' if i < out_coeffs else None
+                cols = [(mp.get(k, k), a) for k, a in cols if k not in mp or mp[k] is not None]
+        elif kind != 'param':
+            raise ValueError(kind)
+    return cols
+
+
+def compressed_ply(cols, actions):
+    """processDataTable then writeCompressedPly's arrays (write-compressed-ply.ts:31-115):
+    (processed table, chunk, vertex, sh)"""
+    out = process(cols, actions)
+    d = dict(out)
+    nsh = 3 * _band_coeffs([k for k, _ in out])
+    order = morton_order(d['x'], d['y'], d['z'])
+    return (out,) + tuple(pack_compressed(d, order, nsh))

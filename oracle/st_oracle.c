@@ -32,17 +32,27 @@ static inline uint32_t js_to_uint32(double v) { return (uint32_t)js_to_int32(v);
 
 static inline uint8_t js_to_uint8(double v) { return (uint8_t)(js_to_uint32(v) & 0xff); }
 
-/* Math.min / Math.max: NaN-propagating, -0 < +0 */
+/* Math.min / Math.max: NaN-propagating, -0 < +0.  A NaN result is V8's NaN on x86-64, the
+ * default NaN with the sign bit set (0xfff8000000000000; 0xffc00000 once stored to a
+ * Float32Array: tests/golden/process_chain, make_golden.js) */
+static inline double js_nan(void)
+{
+    const uint64_t bits = 0xfff8000000000000ull;
+    double v;
+    memcpy(&v, &bits, sizeof v);
+    return v;
+}
+
 static inline double js_min(double a, double b)
 {
-    if (isnan(a) || isnan(b)) return NAN;
+    if (isnan(a) || isnan(b)) return js_nan();
     if (a == 0 && b == 0) return signbit(a) ? a : b;
     return a < b ? a : b;
 }
 
 static inline double js_max(double a, double b)
 {
-    if (isnan(a) || isnan(b)) return NAN;
+    if (isnan(a) || isnan(b)) return js_nan();
     if (a == 0 && b == 0) return signbit(a) ? b : a;
     return a > b ? a : b;
 }

@@ -1,0 +1,258 @@
+// st_chain.hip -- processDataTable (process.ts:64-145) over a table resident in HBM, and the
+// CLI's `in.ply [actions] out.compressed.ply` (index.ts:463-496 -> writeCompressedPly,
+// write-compressed-ply.ts:31-115) as one call: the table crosses PCIe once in each direction
+// (columns up, packed chunk / vertex / sh bytes down) instead of once per action.
+//
+// The chain holds the current table as (name, type, device pointer) columns.  A transform
+// updates float32 columns in place; a filter gathers the survivors into the other of two
+// workspace generations (ping-pong), so a long action list needs at most two copies of the
+// table beside the input.
+#include <cstring>
+
+#include "st_internal.h"
+
+namespace st {
+namespace {
+
+struct ChainCol {
+    std::string name;
+    int32_t type;
+    void *ptr;
+};
+
+struct Chain {
+    st_ctx *c;
+    uint64_t n = 0;
+    std::vector<ChainCol> cols;
+    int gen = 0;  // workspace generation the next filter writes
+
+    // views over the current columns (rebuilt on demand; pointers stay valid until the next change)
+    std::vector<const char *> names;
+    std::vector<int32_t> types;
+    std::vector<void *> ptrs;
+    std::vector<float *> fptrs;
+    std::vector<const char *> fnames;
+    st_ttable tt{};
+    st_table ft{};
+
+    const st_ttable *typed() {
+        names.clear(), types.clear(), ptrs.clear();
+        for (auto &k : cols) names.push_back(k.name.c_str()), types.push_back(k.type), ptrs.push_back(k.ptr);
+        tt = st_ttable{n, (int32_t)cols.size(), names.data(), types.data(), ptrs.data()};
+        return &tt;
+    }
+    // the float32 columns as an st_table (the transform / pack kernels read columns by name)
+    const st_table *f32() {
+        fnames.clear(), fptrs.clear();
+        for (auto &k : cols)
+            if (k.type == ST_PLY_FLOAT) fnames.push_back(k.name.c_str()), fptrs.push_back(static_cast<float *>(k.ptr));
+        ft = st_table{n, (int32_t)fptrs.size(), fnames.data(), fptrs.data()};
+        return &ft;
+    }
+    bool has(const std::string &nm) const {
+        for (auto &k : cols)
+            if (k.name == nm) return true;
+        return false;
+    }
+    // the kernels read these by name from the float32 columns: a same-named column of another
+    // type would be silently skipped (the reference reads any type through getRow)
+    void require_f32(const std::string &nm, const char *what) const {
+        for (auto &k : cols)
+            if (k.name == nm && k.type != ST_PLY_FLOAT)
+                throw Error(ST_ERR_UNSUPPORTED, std::string(what) + ": column " + nm + " is not float32");
+    }
+
+    void gather(const uint32_t *idx, uint64_t m) {
+        const st_ttable *src = typed();
+        std::vector<void *> dst(cols.size());
+        for (size_t i = 0; i < cols.size(); ++i)
+            dst[i] = ws(c, "chain.g" + std::to_string(gen) + "." + std::to_string(i), m * type_size(cols[i].type) + 16);
+        st_ttable d = *src;
+        d.n = m;
+        d.cols = dst.data();
+        permute_rows_tdev(c, src, idx, m, &d);
+        for (size_t i = 0; i < cols.size(); ++i) cols[i].ptr = dst[i];
+        n = m;
+        gen ^= 1;
+    }
+};
+
+int band_coeffs(const std::vector<ChainCol> &cols) {
+    // { '9': 1, '24': 2, '-1': 3 }[shNames.findIndex(v => !dataTable.hasColumn(v))] ?? 0
+    int first_missing = -1;
+    for (int i = 0; i < 45 && first_missing < 0; ++i) {
+        const std::string nm = "f_rest_" + std::to_string(i);
+        bool hit = false;
+        for (auto &k : cols) hit = hit || k.name == nm;
+        if (!hit) first_missing = i;
+    }
+    return first_missing == 9 ? 3 : first_missing == 24 ? 8 : first_missing == -1 ? 15 : 0;
+}
+
+void run_actions(Chain &ch, const st_action *actions, int nactions) {
+    static const char *tcols[] = {"x", "y", "z", "rot_0", "rot_1", "rot_2", "rot_3", "scale_0", "scale_1", "scale_2"};
+    const int in_coeffs = band_coeffs(ch.cols);  // filterBands reads the ORIGINAL table (process.ts:111)
+    for (int a = 0; a < nactions; ++a) {
+        const st_action &act = actions[a];
+        switch (act.kind) {
+            case ST_ACTION_TRANSFORM: {
+                for (auto *nm : tcols) ch.require_f32(nm, "transform");
+                for (int i = 0; i < 45; ++i) ch.require_f32("f_rest_" + std::to_string(i), "transform");
+                transform_dev(ch.c, ch.f32(), &act.transform);
+                break;
+            }
+            case ST_ACTION_FILTER_NAN:
+            case ST_ACTION_FILTER_VALUE: {
+                if (ch.n == 0) break;
+                auto *idx = wsT<uint32_t>(ch.c, "chain.idx", ch.n);
+                const uint64_t m = act.kind == ST_ACTION_FILTER_NAN
+                                       ? filter_finite_tdev(ch.c, ch.typed(), idx)
+                                       : filter_value_tdev(ch.c, ch.typed(), act.column, act.compare, act.value, idx);
+                if (m != ch.n) ch.gather(idx, m);  // all rows kept: permuteRows by the identity
+                break;
+            }
+            case ST_ACTION_FILTER_BANDS: {
+                ST_REQUIRE(act.bands >= 0 && act.bands <= 3, ST_ERR_ARG, "filterBands: bands must be 0..3");
+                static const int coeffs[4] = {0, 3, 8, 15};
+                const int out_coeffs = coeffs[act.bands];
+                if (out_coeffs >= in_coeffs) break;  // outputBands < inputBands only (:115)
+                std::vector<ChainCol> next;
+                for (auto &k : ch.cols) {
+                    int hit = -1, to = -1;
+                    for (int i = 0; i < in_coeffs && hit < 0; ++i)
+                        for (int j = 0; j < 3 && hit < 0; ++j)
+                            if (k.name == "f_rest_" + std::to_string(i + j * in_coeffs)) {
+                                hit = 1;
+                                if (i < out_coeffs) to = i + j * out_coeffs;
+                            }
+                    if (hit < 0) next.push_back(k);
+                    else if (to >= 0) next.push_back(ChainCol{"f_rest_" + std::to_string(to), k.type, k.ptr});
+                }
+                ch.cols.swap(next);
+                break;
+            }
+            case ST_ACTION_PARAM:
+                break;
+            default:
+                throw Error(ST_ERR_ARG, "process: unknown action kind " + std::to_string(act.kind));
+        }
+    }
+}
+
+// writeCompressedPly's device part on the processed table: Morton order of the identity
+// (write-compressed-ply.ts:59-64), then the chunk loop
+void compressed_tail(Chain &ch, float *chunk, uint32_t *vertex, uint8_t *sh, int32_t *out_coeffs) {
+    static const char *pcols[] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
+                                  "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    for (auto *nm : pcols) ch.require_f32(nm, "writeCompressedPly");
+    const int C = band_coeffs(ch.cols);
+    for (int i = 0; i < 3 * C; ++i) ch.require_f32("f_rest_" + std::to_string(i), "writeCompressedPly");
+    *out_coeffs = C;
+    if (ch.n == 0) return;
+    const st_table *t = ch.f32();
+    auto *order = wsT<uint32_t>(ch.c, "chain.order", ch.n);
+    iota_u32(ch.c, order, ch.n);
+    morton_order_dev(ch.c, col_or_null(t, "x"), col_or_null(t, "y"), col_or_null(t, "z"), order, ch.n);
+    pack_compressed_dev(ch.c, t, order, chunk, vertex, sh);
+}
+
+void check_src(const st_ttable *src) {
+    ST_REQUIRE(src->ncol >= 0 && (src->ncol == 0 || (src->names && src->types && src->cols)), ST_ERR_ARG,
+               "process: bad table");
+    for (int i = 0; i < src->ncol; ++i) {
+        ST_REQUIRE(type_size(src->types[i]) > 0, ST_ERR_ARG, "process: bad column type");
+        ST_REQUIRE(src->n == 0 || src->cols[i], ST_ERR_ARG, "process: NULL column");
+    }
+}
+
+// upload the host table once
+void upload_chain(st_ctx *c, const st_ttable *src, Chain &ch) {
+    ch.n = src->n;
+    for (int i = 0; i < src->ncol; ++i) {
+        const int sz = type_size(src->types[i]);
+        void *d = ws(c, "chain.in." + std::to_string(i), src->n * sz + 16);
+        if (src->n) ST_HIP(hipMemcpyAsync(d, src->cols[i], src->n * sz, hipMemcpyHostToDevice, c->stream));
+        ch.cols.push_back(ChainCol{src->names[i], src->types[i], d});
+    }
+}
+
+}  // namespace
+}  // namespace st
+
+using namespace st;
+
+extern "C" {
+
+int st_process(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions, const st_ttable *dst,
+               uint64_t *out_m) {
+    return guard([&] {
+        ST_REQUIRE(c && src && dst && out_m && (actions || nactions == 0), ST_ERR_ARG, "NULL argument");
+        check_src(src);
+        use_device(c);
+        Chain ch{c};
+        upload_chain(c, src, ch);
+        run_actions(ch, actions, nactions);
+        std::vector<int> from(dst->ncol, -1);
+        for (int j = 0; j < dst->ncol; ++j) {
+            for (size_t i = 0; i < ch.cols.size() && from[j] < 0; ++i)
+                if (ch.cols[i].name == dst->names[j] && ch.cols[i].type == dst->types[j]) from[j] = (int)i;
+            ST_REQUIRE(from[j] >= 0, ST_ERR_ARG, std::string("process: result has no column ") + dst->names[j]);
+        }
+        for (int j = 0; j < dst->ncol; ++j)
+            if (ch.n)
+                ST_HIP(hipMemcpyAsync(dst->cols[j], ch.cols[from[j]].ptr, ch.n * type_size(dst->types[j]),
+                                      hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        *out_m = ch.n;
+    });
+}
+
+int st_compressed_ply(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions, float *chunk,
+                      uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs) {
+    return guard([&] {
+        ST_REQUIRE(c && src && out_m && out_sh_coeffs && (actions || nactions == 0), ST_ERR_ARG, "NULL argument");
+        check_src(src);
+        use_device(c);
+        Chain ch{c};
+        upload_chain(c, src, ch);
+        run_actions(ch, actions, nactions);
+        const uint64_t m = ch.n, nch = (m + 255) / 256;
+        ST_REQUIRE(m == 0 || (chunk && vertex), ST_ERR_ARG, "compressed_ply: NULL output");
+        auto *dchunk = wsT<float>(c, "chain.chunk", nch * 18);
+        auto *dvert = wsT<uint32_t>(c, "chain.vert", m * 4);
+        const int Cmax = band_coeffs(ch.cols);
+        auto *dsh = wsT<uint8_t>(c, "chain.sh", m * 3 * (uint64_t)Cmax + 1);
+        int32_t C = 0;
+        compressed_tail(ch, dchunk, dvert, dsh, &C);
+        ST_REQUIRE(C == 0 || m == 0 || sh, ST_ERR_ARG, "compressed_ply: sh output is NULL");
+        if (m) {
+            ST_HIP(hipMemcpyAsync(chunk, dchunk, nch * 18 * 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(vertex, dvert, m * 16, hipMemcpyDeviceToHost, c->stream));
+            if (C) ST_HIP(hipMemcpyAsync(sh, dsh, m * 3 * (uint64_t)C, hipMemcpyDeviceToHost, c->stream));
+        }
+        ST_HIP(hipStreamSynchronize(c->stream));
+        *out_m = m;
+        *out_sh_coeffs = C;
+    });
+}
+
+int st_dev_compressed_ply(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions,
+                          float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs) {
+    return guard([&] {
+        ST_REQUIRE(c && src && out_m && out_sh_coeffs && (actions || nactions == 0), ST_ERR_ARG, "NULL argument");
+        check_src(src);
+        use_device(c);
+        Chain ch{c};
+        ch.n = src->n;
+        for (int i = 0; i < src->ncol; ++i) ch.cols.push_back(ChainCol{src->names[i], src->types[i], src->cols[i]});
+        run_actions(ch, actions, nactions);
+        ST_REQUIRE(ch.n == 0 || (chunk && vertex), ST_ERR_ARG, "compressed_ply: NULL output");
+        int32_t C = 0;
+        if (band_coeffs(ch.cols) && ch.n) ST_REQUIRE(sh, ST_ERR_ARG, "compressed_ply: sh output is NULL");
+        compressed_tail(ch, chunk, vertex, sh, &C);
+        *out_m = ch.n;
+        *out_sh_coeffs = C;
+    });
+}
+
+}  // extern "C"

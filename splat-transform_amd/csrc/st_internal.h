@@ -182,6 +182,10 @@ void concat_rows_dev(st_ctx *c, const st_table *const *srcs, int nsrc, const st_
 // typed tables (st_table.hip)
 int type_size(int32_t st_ply_type);  // 0 for an unknown code
 uint64_t filter_finite_tdev(st_ctx *c, const st_ttable *t, uint32_t *out_idx);
+// stable compaction: out_idx = the rows with flags[i] != 0, ascending; returns their count (syncs)
+uint64_t compact_flags_dev(st_ctx *c, const uint32_t *flags, uint64_t n, uint32_t *out_idx);
+uint64_t filter_value_tdev(st_ctx *c, const st_ttable *t, const char *column, int32_t cmp, double value,
+                           uint32_t *out_idx);
 void permute_rows_tdev(st_ctx *c, const st_ttable *src, const uint32_t *idx, uint64_t m, const st_ttable *dst);
 int combine_layout(const st_ttable *const *srcs, int nsrc, int32_t *col_table, int32_t *col_index);
 void combine_tdev(st_ctx *c, const st_ttable *const *srcs, int nsrc, const st_ttable *dst);

@@ -41,13 +41,16 @@ __host__ __device__ inline int32_t to_int32(double v) {
 __host__ __device__ inline uint32_t to_uint32(double v) { return (uint32_t)to_int32(v); }
 __host__ __device__ inline uint8_t to_uint8(double v) { return (uint8_t)(to_uint32(v) & 0xffu); }
 
+// Math.min / Math.max with a NaN operand return V8's NaN: the x86-64 default NaN, sign bit set
+// (0xffc00000 once stored to a Float32Array; reference fixture process_chain)
+__host__ __device__ inline double nan_() { return mkd(0xfff80000u, 0u); }
 __host__ __device__ inline double min_(double a, double b) {
-    if (isnan_(a) || isnan_(b)) return __builtin_nan("");
+    if (isnan_(a) || isnan_(b)) return nan_();
     if (a == 0 && b == 0) return signbit_(a) ? a : b;
     return a < b ? a : b;
 }
 __host__ __device__ inline double max_(double a, double b) {
-    if (isnan_(a) || isnan_(b)) return __builtin_nan("");
+    if (isnan_(a) || isnan_(b)) return nan_();
     if (a == 0 && b == 0) return signbit_(a) ? b : a;
     return a > b ? a : b;
 }

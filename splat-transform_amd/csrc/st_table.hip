@@ -45,6 +45,26 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t *flags, const ui
         if (flags[i]) out[pos[i]] = (uint32_t)i;
 }
 
+// filterByValue's predicate on one column (process.ts:99-106), in f64 like the JS comparison
+template <typename T>
+__global__ __launch_bounds__(256) void k_cmp_flags(const T *__restrict__ col, uint64_t n, int cmp, double v,
+                                                   uint32_t *flags) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double x = (double)col[i];
+        bool keep;
+        switch (cmp) {
+            case ST_CMP_LT: keep = x < v; break;
+            case ST_CMP_LTE: keep = x <= v; break;
+            case ST_CMP_GT: keep = x > v; break;
+            case ST_CMP_GTE: keep = x >= v; break;
+            case ST_CMP_EQ: keep = x == v; break;
+            default: keep = !(x == v); break;  // ST_CMP_NEQ: !== (true when either is NaN)
+        }
+        flags[i] = keep ? 1u : 0u;
+    }
+}
+
 // permuteRows (data-table.ts:135-149): dst[c][j] = src[c][idx[j]]
 __global__ __launch_bounds__(256) void k_gather_cols(float *const *src, float *const *dst, int ncol,
                                                      const uint32_t *__restrict__ idx, uint64_t m) {
@@ -194,7 +214,6 @@ uint64_t filter_finite_tdev(st_ctx *c, const st_ttable *t, uint32_t *out_idx) {
     const uint64_t n = t->n;
     if (n == 0) return 0;
     auto *flags = wsT<uint32_t>(c, "filter.flags", n);
-    auto *pos = wsT<uint32_t>(c, "filter.pos", n + 1);
     std::vector<float *> f32;
     std::vector<double *> f64;
     for (int i = 0; i < t->ncol; ++i) {
@@ -208,6 +227,12 @@ uint64_t filter_finite_tdev(st_ctx *c, const st_ttable *t, uint32_t *out_idx) {
                            n, flags);
         ST_LAUNCH_CHECK();
     }
+    return compact_flags_dev(c, flags, n, out_idx);
+}
+
+uint64_t compact_flags_dev(st_ctx *c, const uint32_t *flags, uint64_t n, uint32_t *out_idx) {
+    if (n == 0) return 0;
+    auto *pos = wsT<uint32_t>(c, "filter.pos", n + 1);
     scan_u32(c, flags, pos, n, pos + n);
     hipLaunchKernelGGL(k_compact, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, flags, pos, n, out_idx);
     ST_LAUNCH_CHECK();
@@ -215,6 +240,40 @@ uint64_t filter_finite_tdev(st_ctx *c, const st_ttable *t, uint32_t *out_idx) {
     ST_HIP(hipMemcpyAsync(h, pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     return h[0];
+}
+
+// filterByValue (process.ts:97-109): row[columnName] <cmp> value on the column's value as a JS
+// number (every column type converts to f64 exactly).  NaN compares false except !==; a
+// missing column reads undefined (NaN); an unknown comparator keeps every row (:108)
+uint64_t filter_value_tdev(st_ctx *c, const st_ttable *t, const char *column, int32_t cmp, double value,
+                           uint32_t *out_idx) {
+    const uint64_t n = t->n;
+    if (n == 0) return 0;
+    auto *flags = wsT<uint32_t>(c, "filter.flags", n);
+    int col = -1;
+    for (int i = 0; i < t->ncol && col < 0; ++i)
+        if (column && std::strcmp(t->names[i], column) == 0) col = i;
+    const unsigned g = grid_for(n, 256, 8192);
+    if (cmp < ST_CMP_LT || cmp > ST_CMP_NEQ) {
+        ST_HIP(hipMemsetD32Async(flags, 1, n, c->stream));
+    } else if (col < 0) {
+        ST_HIP(hipMemsetD32Async(flags, cmp == ST_CMP_NEQ ? 1 : 0, n, c->stream));
+    } else {
+        void *p = t->cols[col];
+        switch (t->types[col]) {
+            case ST_PLY_CHAR: hipLaunchKernelGGL(k_cmp_flags<int8_t>, dim3(g), dim3(256), 0, c->stream, (const int8_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_UCHAR: hipLaunchKernelGGL(k_cmp_flags<uint8_t>, dim3(g), dim3(256), 0, c->stream, (const uint8_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_SHORT: hipLaunchKernelGGL(k_cmp_flags<int16_t>, dim3(g), dim3(256), 0, c->stream, (const int16_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_USHORT: hipLaunchKernelGGL(k_cmp_flags<uint16_t>, dim3(g), dim3(256), 0, c->stream, (const uint16_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_INT: hipLaunchKernelGGL(k_cmp_flags<int32_t>, dim3(g), dim3(256), 0, c->stream, (const int32_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_UINT: hipLaunchKernelGGL(k_cmp_flags<uint32_t>, dim3(g), dim3(256), 0, c->stream, (const uint32_t *)p, n, cmp, value, flags); break;
+            case ST_PLY_FLOAT: hipLaunchKernelGGL(k_cmp_flags<float>, dim3(g), dim3(256), 0, c->stream, (const float *)p, n, cmp, value, flags); break;
+            case ST_PLY_DOUBLE: hipLaunchKernelGGL(k_cmp_flags<double>, dim3(g), dim3(256), 0, c->stream, (const double *)p, n, cmp, value, flags); break;
+            default: throw Error(ST_ERR_ARG, "filterByValue: bad column type");
+        }
+        ST_LAUNCH_CHECK();
+    }
+    return compact_flags_dev(c, flags, n, out_idx);
 }
 
 template <typename T>

@@ -12,6 +12,9 @@
 //   filterNaN(dataTable)                    process.ts:84-95 (+ filter :47-61, permuteRows)
 //   combine(dataTables)                     index.ts:158-210
 //   packCompressed(dataTable)               write-compressed-ply.ts:56-109 (the chunk loop)
+//   processDataTable(dataTable, actions)    process.ts:64-145 (one upload for the whole list)
+//   writeCompressedPly(fh, dataTable[, actions])  write-compressed-ply.ts:31-115 (actions first,
+//                                           same device call: the CLI's config-3 path)
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
 //   cluster1d(dataTable, iterations)        write-sog.ts:56-99
 //   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
@@ -187,6 +190,91 @@ const packCompressed = (dataTable) => {
     return addon.packCompressed(cols, names, order, 3 * shCoeffsOf(dataTable));
 };
 
+// ---- processDataTable / writeCompressedPly (process.ts:64-145, write-compressed-ply.ts:31-115) ----
+// ProcessAction objects as the reference's CLI builds them (process.ts:6-42): Vec3 values for
+// translate / rotate, a number for scale, {columnName, comparator, value} for filterByValue.
+// Normalised for the addon: k = st_action_kind, transform params as t / r / s.
+const ACTION = { transform: 1, filterNaN: 2, filterByValue: 3, filterBands: 4, param: 5 };
+const COMPARE = { lt: 0, lte: 1, gt: 2, gte: 3, eq: 4, neq: 5 };
+const normaliseActions = actions => actions.map((a) => {
+    switch (a.kind) {
+        case 'translate':
+            return { k: ACTION.transform, t: [a.value.x, a.value.y, a.value.z], r: [0, 0, 0, 1], s: 1 };
+        case 'rotate': {
+            const q = addon.quatFromEuler(a.value.x, a.value.y, a.value.z);
+            return { k: ACTION.transform, t: [0, 0, 0], r: q, s: 1 };
+        }
+        case 'scale':
+            return { k: ACTION.transform, t: [0, 0, 0], r: [0, 0, 0, 1], s: a.value };
+        case 'filterNaN':
+            return { k: ACTION.filterNaN };
+        case 'filterByValue':
+            return { k: ACTION.filterByValue, column: String(a.columnName),
+                compare: Object.prototype.hasOwnProperty.call(COMPARE, a.comparator) ? COMPARE[a.comparator] : -1,
+                value: Number(a.value) };
+        case 'filterBands':
+            return { k: ACTION.filterBands, bands: a.value };
+        case 'param':
+            return { k: ACTION.param };
+        default:
+            return { k: 0 };  // unknown kinds: the reference's switch ignores them
+    }
+}).filter(a => a.k !== 0);
+
+// the columns processDataTable leaves: filterBands renames / drops f_rest columns against the
+// ORIGINAL table's band (process.ts:110-134); [name, index of the source column]
+const processSchema = (dataTable, actions) => {
+    const inCoeffs = shCoeffsOf(dataTable);
+    let cols = dataTable.columns.map((c, i) => [c.name, i]);
+    for (const a of actions) {
+        if (a.kind !== 'filterBands') continue;
+        const outCoeffs = [0, 3, 8, 15][a.value];
+        if (!(outCoeffs < inCoeffs)) continue;
+        const map = {};
+        for (let i = 0; i < inCoeffs; ++i) {
+            for (let j = 0; j < 3; ++j) map[`f_rest_${i + j * inCoeffs}`] = i < outCoeffs ? `f_rest_${i + j * outCoeffs}` : null;
+        }
+        cols = cols.map(([n, i]) => (Object.prototype.hasOwnProperty.call(map, n) ? [map[n], i] : [n, i]))
+            .filter(([n]) => n !== null);
+    }
+    return cols;
+};
+
+// processDataTable(dataTable, processActions) -> DataTable: the whole action list on the device
+// with one upload and one download (transform passes, filters and the row gathers in HBM)
+const processDataTable = (dataTable, processActions) => {
+    const schema = processSchema(dataTable, processActions);
+    const out = addon.process(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+        normaliseActions(processActions), schema.map(s => s[0]), schema.map(s => s[1]));
+    return new DataTable(schema.map((s, j) => new Column(s[0], out[j])));
+};
+
+const CHUNK_PROPS_OUT = ['min_x', 'min_y', 'min_z', 'max_x', 'max_y', 'max_z', 'min_scale_x', 'min_scale_y',
+    'min_scale_z', 'max_scale_x', 'max_scale_y', 'max_scale_z', 'min_r', 'min_g', 'min_b', 'max_r', 'max_g', 'max_b'];
+const VERTEX_PROPS_OUT = ['packed_position', 'packed_rotation', 'packed_scale', 'packed_color'];
+
+// write-compressed-ply.ts:31-115: header + chunk + vertex + sh writes.  With processActions the
+// actions run first in the same device call (the CLI's `in.ply [actions] out.compressed.ply`:
+// the table crosses PCIe once each way).  version: the package version of the header comment.
+const writeCompressedPly = async (fileHandle, dataTable, processActions, version) => {
+    const res = addon.compressedPly(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+        normaliseActions(processActions || []));
+    const numSplats = res.numRows;
+    const numChunks = Math.ceil(numSplats / 256);
+    const outputSHCoeffs = res.shCoeffs;
+    const shHeader = outputSHCoeffs ? [`element sh ${numSplats}`].concat(
+        new Array(outputSHCoeffs * 3).fill('').map((_, i) => `property uchar f_rest_${i}`)) : [];
+    const headerText = [].concat(
+        'ply', 'format binary_little_endian 1.0', `comment Generated by splat-transform ${version || '0.10.1'}`,
+        `element chunk ${numChunks}`, CHUNK_PROPS_OUT.map(p => `property float ${p}`),
+        `element vertex ${numSplats}`, VERTEX_PROPS_OUT.map(p => `property uint ${p}`),
+        shHeader, 'end_header\n').join('\n');
+    await fileHandle.write(Buffer.from(headerText, 'utf8'));
+    await fileHandle.write(new Uint8Array(res.chunk.buffer));
+    await fileHandle.write(new Uint8Array(res.vertex.buffer));
+    await fileHandle.write(res.sh);
+};
+
 const kmeans = (points, k, iterations) => {
     const cols = points.columns.map(c => c.data);
     const n = points.numRows;
@@ -312,6 +400,8 @@ module.exports = {
     filterNaN,
     combine,
     packCompressed,
+    processDataTable,
+    writeCompressedPly,
     kmeans,
     cluster1d,
     sogTextures,

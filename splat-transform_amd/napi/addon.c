@@ -30,6 +30,11 @@
  *        [{name, columns: [{name, data}]}]}
  *   decompressPly(chunk[18], vertex[4], sh[]) decompressPly (readers/decompress-ply.ts:82-232)
  *        -> Float32Array[14 + sh.length]
+ *   compressedPly(cols, names, actions)       processDataTable + writeCompressedPly's arrays, one
+ *        -> {numRows, shCoeffs, chunk,        upload (process.ts:64-145, write-compressed-ply.ts:
+ *            vertex, sh}                      31-115)
+ *   process(cols, names, actions, outNames,   processDataTable, one upload (process.ts:64-145)
+ *           outSrc) -> TypedArray[]
  */
 #include <node_api.h>
 #include <stdio.h>
@@ -349,6 +354,212 @@ fail:
     if (dst)
         for (uint32_t i = 0; i < m; ++i) free(dst[i]);
     free(src); free(dst); free(types); free(nt); free(es);
+    return NULL;
+}
+
+/* ---- processDataTable chain (st_process / st_compressed_ply) ----------------------------
+ * columns: TypedArray[] of the reference's eight types, names: string[], actions: the host's
+ * normalised list [{k, t[3], r[4], s, column, compare, value, bands}] (js/index.js) */
+typedef struct {
+    uint32_t m;
+    uint64_t n;
+    void **cols;
+    int32_t *types;
+    napi_typedarray_type *nt;
+    size_t *es;
+    char **names;
+    uint32_t na;
+    st_action *acts;
+    char **acols;
+} chain_args;
+
+static void chain_free(chain_args *a) {
+    free(a->cols); free(a->types); free(a->nt); free(a->es);
+    free_strs(a->names, a->m);
+    free_strs(a->acols, a->na);
+    free(a->acts);
+}
+
+static double prop_num(napi_env env, napi_value obj, const char *k) {
+    napi_value v;
+    if (napi_get_named_property(env, obj, k, &v) != napi_ok) return 0;
+    return num(env, v);
+}
+
+static int chain_parse(napi_env env, napi_value cols, napi_value names, napi_value actions, chain_args *a) {
+    memset(a, 0, sizeof *a);
+    if (napi_get_array_length(env, cols, &a->m) != napi_ok || napi_get_array_length(env, actions, &a->na) != napi_ok) {
+        napi_throw_type_error(env, NULL, "splat-hip: expected column and action arrays");
+        return 0;
+    }
+    a->cols = (void **)calloc(a->m + 1, sizeof(void *));
+    a->types = (int32_t *)calloc(a->m + 1, sizeof(int32_t));
+    a->nt = (napi_typedarray_type *)calloc(a->m + 1, sizeof(napi_typedarray_type));
+    a->es = (size_t *)calloc(a->m + 1, sizeof(size_t));
+    for (uint32_t i = 0; i < a->m; ++i) {
+        napi_value e, ab;
+        bool is_ta = false;
+        size_t len = 0, off = 0;
+        napi_get_element(env, cols, i, &e);
+        if (napi_is_typedarray(env, e, &is_ta) != napi_ok || !is_ta ||
+            napi_get_typedarray_info(env, e, &a->nt[i], &len, &a->cols[i], &ab, &off) != napi_ok ||
+            !(a->types[i] = ply_type_of(a->nt[i], &a->es[i]))) {
+            napi_throw_type_error(env, NULL, "splat-hip: expected the reference's TypedArray columns");
+            return 0;
+        }
+        if (i == 0) a->n = len;
+        else if (len != a->n) {
+            napi_throw_range_error(env, NULL, "splat-hip: columns differ in length");
+            return 0;
+        }
+    }
+    a->names = str_list(env, names, a->m);
+    a->acts = (st_action *)calloc(a->na + 1, sizeof(st_action));
+    a->acols = (char **)calloc(a->na + 1, sizeof(char *));
+    for (uint32_t i = 0; i < a->na; ++i) {
+        napi_value o, v;
+        st_action *x = &a->acts[i];
+        napi_get_element(env, actions, i, &o);
+        x->kind = (int32_t)prop_num(env, o, "k");
+        x->compare = (int32_t)prop_num(env, o, "compare");
+        x->value = prop_num(env, o, "value");
+        x->bands = (int32_t)prop_num(env, o, "bands");
+        if (x->kind == ST_ACTION_FILTER_VALUE && napi_get_named_property(env, o, "column", &v) == napi_ok) {
+            size_t len = 0;
+            napi_get_value_string_utf8(env, v, NULL, 0, &len);
+            a->acols[i] = (char *)malloc(len + 1);
+            napi_get_value_string_utf8(env, v, a->acols[i], len + 1, &len);
+            x->column = a->acols[i];
+        }
+        if (x->kind == ST_ACTION_TRANSFORM) {
+            double t[3], r[4];
+            napi_value tv, rv, e;
+            napi_get_named_property(env, o, "t", &tv);
+            napi_get_named_property(env, o, "r", &rv);
+            for (uint32_t j = 0; j < 3; ++j) napi_get_element(env, tv, j, &e), t[j] = num(env, e);
+            for (uint32_t j = 0; j < 4; ++j) napi_get_element(env, rv, j, &e), r[j] = num(env, e);
+            int rc = st_transform_params_make(t, r, prop_num(env, o, "s"), &x->transform);
+            if (rc != ST_OK) {
+                throw_st(env, rc);
+                return 0;
+            }
+        }
+    }
+    return 1;
+}
+
+/* compressedPly(columns, names, actions) -> {numRows, shCoeffs, chunk, vertex, sh}:
+ * processDataTable then writeCompressedPly's arrays in one upload (st_compressed_ply) */
+static napi_value js_compressed_ply(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out = NULL;
+    chain_args a;
+    st_ctx *ctx;
+    float *chunk = NULL;
+    uint32_t *vertex = NULL;
+    uint8_t *sh = NULL;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
+    if (!get_ctx(env, &ctx)) goto fail;
+    chunk = (float *)malloc(((a.n + 255) / 256 * 18 + 1) * 4);
+    vertex = (uint32_t *)malloc((a.n * 4 + 1) * 4);
+    sh = (uint8_t *)malloc(a.n * 45 + 1);
+    {
+        st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+        uint64_t m = 0;
+        int32_t C = 0;
+        void *p;
+        napi_value tch, tvx, tsh;
+        int rc = st_compressed_ply(ctx, &ts, a.acts, (int32_t)a.na, chunk, vertex, sh, &m, &C);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        const uint64_t nch = (m + 255) / 256;
+        if (!(tch = new_typed(env, napi_float32_array, nch * 18, 4, &p))) goto fail;
+        memcpy(p, chunk, nch * 18 * 4);
+        if (!(tvx = new_typed(env, napi_uint32_array, m * 4, 4, &p))) goto fail;
+        memcpy(p, vertex, m * 16);
+        if (!(tsh = new_typed(env, napi_uint8_array, m * 3 * (uint64_t)C, 1, &p))) goto fail;
+        memcpy(p, sh, m * 3 * (uint64_t)C);
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "numRows", make_num(env, (double)m));
+        set_named(env, out, "shCoeffs", make_num(env, C));
+        set_named(env, out, "chunk", tch);
+        set_named(env, out, "vertex", tvx);
+        set_named(env, out, "sh", tsh);
+    }
+    free(chunk); free(vertex); free(sh);
+    chain_free(&a);
+    return out;
+fail:
+    free(chunk); free(vertex); free(sh);
+    chain_free(&a);
+    return NULL;
+}
+
+/* process(columns, names, actions, outNames, outSrc) -> TypedArray[]: processDataTable in one
+ * upload (st_process); result column j is named outNames[j] and has the type of source column
+ * outSrc[j] (the host computes filterBands' renaming) */
+static napi_value js_process(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5], out = NULL;
+    chain_args a;
+    st_ctx *ctx;
+    uint32_t mo = 0;
+    char **onames = NULL;
+    void **dst = NULL;
+    int32_t *otypes = NULL;
+    uint32_t *osrc = NULL;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
+    if (napi_get_array_length(env, argv[3], &mo) != napi_ok) goto fail;
+    onames = str_list(env, argv[3], mo);
+    dst = (void **)calloc(mo + 1, sizeof(void *));
+    otypes = (int32_t *)calloc(mo + 1, sizeof(int32_t));
+    osrc = (uint32_t *)calloc(mo + 1, sizeof(uint32_t));
+    for (uint32_t j = 0; j < mo; ++j) {
+        napi_value e;
+        napi_get_element(env, argv[4], j, &e);
+        osrc[j] = (uint32_t)num(env, e);
+        if (osrc[j] >= a.m) {
+            napi_throw_range_error(env, NULL, "splat-hip: bad result column source");
+            goto fail;
+        }
+        otypes[j] = a.types[osrc[j]];
+        dst[j] = malloc(a.n * a.es[osrc[j]] + 8);
+    }
+    if (!get_ctx(env, &ctx)) goto fail;
+    {
+        st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+        st_ttable td = {a.n, (int32_t)mo, (const char *const *)onames, otypes, dst};
+        uint64_t m = 0;
+        int rc = st_process(ctx, &ts, a.acts, (int32_t)a.na, &td, &m);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        if (napi_create_array_with_length(env, mo, &out) != napi_ok) goto fail;
+        for (uint32_t j = 0; j < mo; ++j) {
+            void *buf;
+            const size_t es = a.es[osrc[j]];
+            napi_value ta = new_typed(env, a.nt[osrc[j]], m, es, &buf);
+            if (!ta) goto fail;
+            memcpy(buf, dst[j], m * es);
+            napi_set_element(env, out, j, ta);
+        }
+    }
+    for (uint32_t j = 0; j < mo; ++j) free(dst[j]);
+    free(dst); free(otypes); free(osrc);
+    free_strs(onames, mo);
+    chain_free(&a);
+    return out;
+fail:
+    if (dst)
+        for (uint32_t j = 0; j < mo; ++j) free(dst[j]);
+    free(dst); free(otypes); free(osrc);
+    free_strs(onames, mo);
+    chain_free(&a);
     return NULL;
 }
 
@@ -895,7 +1106,9 @@ static napi_value init(napi_env env, napi_value exports) {
                {"webpLossless", js_webp_lossless},
                {"sogBundle", js_sog_bundle},
                {"readPly", js_read_ply},
-               {"decompressPly", js_decompress_ply}};
+               {"decompressPly", js_decompress_ply},
+               {"compressedPly", js_compressed_ply},
+               {"process", js_process}};
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;
         if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok) return NULL;

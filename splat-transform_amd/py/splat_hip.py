@@ -56,6 +56,15 @@ class SogTextures(ctypes.Structure):
                 ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shn_centroids', 'shn_labels')]
 
 
+class Action(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('compare', ctypes.c_int32), ('column', ctypes.c_char_p),
+                ('value', ctypes.c_double), ('bands', ctypes.c_int32), ('transform', TransformParams)]
+
+
+ACTION_TRANSFORM, ACTION_FILTER_NAN, ACTION_FILTER_VALUE, ACTION_FILTER_BANDS, ACTION_PARAM = 1, 2, 3, 4, 5
+COMPARE = {'lt': 0, 'lte': 1, 'gt': 2, 'gte': 3, 'eq': 4, 'neq': 5}
+
+
 PLY_TYPES = {1: ('char', np.int8), 2: ('uchar', np.uint8), 3: ('short', np.int16), 4: ('ushort', np.uint16),
              5: ('int', np.int32), 6: ('uint', np.uint32), 7: ('float', np.float32), 8: ('double', np.float64)}
 
@@ -103,6 +112,7 @@ EXPORTS = [
     'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
+    'st_process', 'st_compressed_ply', 'st_dev_compressed_ply',
 ]
 
 
@@ -344,6 +354,54 @@ def action_params(kind, value):
     if kind == 'scale':
         return transform_params(s=float(value))
     raise ValueError(kind)
+
+
+def make_actions(actions):
+    """processDataTable's ProcessAction list (process.ts:6-42) as st_action[]: dicts with 'kind' in
+    translate / rotate / scale (value as in action_params), filterNaN, filterByValue (columnName,
+    comparator, value), filterBands (value), param"""
+    arr = (Action * max(1, len(actions)))()
+    keep = []
+    for a, act in zip(arr, actions):
+        k = act['kind']
+        if k in ('translate', 'rotate', 'scale'):
+            a.kind, a.transform = ACTION_TRANSFORM, action_params(k, act['value'])
+        elif k == 'filterNaN':
+            a.kind = ACTION_FILTER_NAN
+        elif k == 'filterByValue':
+            col = act['columnName'].encode()
+            keep.append(col)
+            a.kind, a.column, a.value = ACTION_FILTER_VALUE, col, float(act['value'])
+            a.compare = COMPARE.get(act['comparator'], -1)
+        elif k == 'filterBands':
+            a.kind, a.bands = ACTION_FILTER_BANDS, int(act['value'])
+        elif k == 'param':
+            a.kind = ACTION_PARAM
+        else:
+            raise ValueError(k)
+    arr._keep = keep
+    return arr
+
+
+def process_schema(items, actions):
+    """the (name, dtype) columns processDataTable leaves (filterBands renames / drops f_rest
+    columns against the ORIGINAL table's band, process.ts:110-134)"""
+    names = [k for k, _ in items]
+    first_missing = next((i for i in range(45) if f'f_rest_{i}' not in names), -1)
+    in_coeffs = {9: 3, 24: 8, -1: 15}.get(first_missing, 0)
+    cols = [(k, np.dtype(a.dtype)) for k, a in items]
+    for act in actions:
+        if act['kind'] != 'filterBands':
+            continue
+        out_coeffs = [0, 3, 8, 15][act['value']]
+        if out_coeffs >= in_coeffs:
+            continue
+        mp = {}
+        for i in range(in_coeffs):
+            for j in range(3):
+                mp[f'f_rest_{i + j * in_coeffs}'] = f'f_rest_{i + j * out_coeffs}' if i < out_coeffs else None
+        cols = [(mp[k], t) if k in mp else (k, t) for k, t in cols if k not in mp or mp[k] is not None]
+    return cols
 
 
 def sog_geometry(n, sh_coeffs):
@@ -686,6 +744,43 @@ class Context:
         m = ctypes.c_uint64()
         check(lib().st_filter_nan(self.h, ctypes.byref(ts), ctypes.byref(td), ctypes.byref(m)))
         return [(k, a[:m.value].copy()) for k, a in out]
+
+    def process(self, cols, actions):
+        """processDataTable (process.ts:64-145) on host columns (list of (name, numpy array) or a
+        dict) in one upload -> the processed table as a list of (name, array)"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        n = len(items[0][1]) if items else 0
+        out = [(k, np.empty(n, t)) for k, t in process_schema(items, actions)]
+        ts, td = make_ttable(items), make_ttable(out, n)
+        acts = make_actions(actions)
+        m = ctypes.c_uint64()
+        check(lib().st_process(self.h, ctypes.byref(ts), acts, ctypes.c_int32(len(actions)), ctypes.byref(td),
+                               ctypes.byref(m)))
+        return [(k, a[:m.value].copy()) for k, a in out]
+
+    def compressed_ply(self, cols, actions):
+        """processDataTable then writeCompressedPly's device part, one upload: (m, chunk, vertex, sh)"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        n = len(items[0][1]) if items else 0
+        chunk = np.zeros(max(1, (n + 255) // 256 * 18), np.float32)
+        vertex = np.zeros(max(1, n * 4), np.uint32)
+        sh = np.zeros(max(1, n * 45), np.uint8)
+        ts = make_ttable(items, n)
+        acts = make_actions(actions)
+        m, C = ctypes.c_uint64(), ctypes.c_int32()
+        check(lib().st_compressed_ply(self.h, ctypes.byref(ts), acts, ctypes.c_int32(len(actions)), _vp(chunk),
+                                      _vp(vertex), _vp(sh), ctypes.byref(m), ctypes.byref(C)))
+        m, C = m.value, C.value
+        return m, chunk[:(m + 255) // 256 * 18], vertex[:m * 4], sh[:m * 3 * C]
+
+    def dev_compressed_ply(self, cols, actions, chunk, vertex, sh):
+        """the same over device columns (list of (name, tensor)) into device outputs sized for n rows"""
+        ts = make_ttable(cols)
+        acts = make_actions(actions)
+        m, C = ctypes.c_uint64(), ctypes.c_int32()
+        check(lib().st_dev_compressed_ply(self.h, ctypes.byref(ts), acts, ctypes.c_int32(len(actions)), _ptr(chunk),
+                                          _ptr(vertex), _ptr(sh), ctypes.byref(m), ctypes.byref(C)))
+        return m.value, C.value
 
     def dev_filter_finite_t(self, cols, out_idx):
         t = make_ttable(cols)

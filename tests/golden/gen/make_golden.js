@@ -663,6 +663,86 @@ cases.filter_combine = () => {
     fx.save();
 };
 
+// processDataTable over every action kind (process.ts:64-145) followed by writeCompressedPly
+// (write-compressed-ply.ts:31-115): the CLI's `in.ply [actions] out.compressed.ply`
+// (index.ts:463-496).  Per case: the input table, the processed table (names, types, data) and
+// the four file writes of the compressed PLY (or the error either step threw).
+cases.process_chain = async () => {
+    const fx = new Fixture('process_chain');
+    const V = (x, y, z) => new pc.Vec3(x, y, z);
+    const specs = [];
+    {   // BASELINE config 3: -r 0,45,0 --filterNaN
+        const { names, cols } = makeSplats(3000, 15, 901, { cubeFrac: 0.1 });
+        const g = new Gen(902);
+        for (let i = 0; i < 30; ++i) cols[names[g.int(names.length)]][g.int(3000)] = [NaN, Infinity, -Infinity][i % 3];
+        specs.push(['config3', names, cols, [{ kind: 'rotate', value: V(0, 45, 0) }, { kind: 'filterNaN' }]]);
+    }
+    {   // filterByValue / scale / filterBands(1) with NaN in the filtered column
+        const { names, cols } = makeSplats(2500, 15, 903, { cubeFrac: 0.05 });
+        cols.opacity[3] = NaN; cols.opacity[4] = 0.5; cols.opacity[5] = -0;
+        specs.push(['value_bands1', names, cols, [{ kind: 'filterByValue', columnName: 'opacity', comparator: 'gt', value: 0.5 },
+            { kind: 'scale', value: 2 }, { kind: 'filterBands', value: 1 }]]);
+    }
+    {   // filterBands(2), lte, translate, filterNaN, then a param (no-op)
+        const { names, cols } = makeSplats(2000, 15, 904);
+        cols.x[7] = 0; cols.x[8] = -0; cols.y[9] = NaN;
+        specs.push(['bands2_lte', names, cols, [{ kind: 'filterBands', value: 2 },
+            { kind: 'filterByValue', columnName: 'x', comparator: 'lte', value: 0 },
+            { kind: 'translate', value: V(1, 2, 3) }, { kind: 'filterNaN' }, { kind: 'param', name: 'a', value: 'b' }]]);
+    }
+    {   // eq / neq on exact values, a missing column (neq keeps all, eq keeps none is a separate case),
+        // an unknown comparator (keeps all), gte / lt
+        const { names, cols } = makeSplats(1500, 3, 905, { cubeFrac: 0.2 });
+        for (let i = 0; i < 1500; i += 7) cols.scale_0[i] = -4;
+        cols.scale_0[11] = NaN;
+        specs.push(['eq_neq', names, cols, [{ kind: 'filterByValue', columnName: 'scale_0', comparator: 'neq', value: -4 },
+            { kind: 'filterByValue', columnName: 'nope', comparator: 'neq', value: 1 },
+            { kind: 'filterByValue', columnName: 'z', comparator: 'bogus', value: 1 },
+            { kind: 'filterByValue', columnName: 'y', comparator: 'gte', value: -5 },
+            { kind: 'filterByValue', columnName: 'rot_0', comparator: 'lt', value: 1.25 },
+            { kind: 'rotate', value: V(-30.5, 170, 45.25) }]]);
+    }
+    {   // eq keeps the exact matches only; SH1 -> bands 0
+        const { names, cols } = makeSplats(1200, 3, 906);
+        for (let i = 0; i < 1200; i += 5) cols.f_dc_1[i] = 0.25;
+        specs.push(['eq_bands0', names, cols, [{ kind: 'filterByValue', columnName: 'f_dc_1', comparator: 'eq', value: 0.25 },
+            { kind: 'filterBands', value: 0 }, { kind: 'rotate', value: V(90, 0, 0) }]]);
+    }
+    {   // every row filtered out
+        const { names, cols } = makeSplats(700, 8, 907);
+        specs.push(['empty', names, cols, [{ kind: 'filterByValue', columnName: 'x', comparator: 'gt', value: 1e30 }]]);
+    }
+    {   // SH0 table, filterBands above its band (no-op), two filters in a row
+        const { names, cols } = makeSplats(900, 0, 908);
+        cols.opacity[1] = Infinity;
+        specs.push(['sh0_two_filters', names, cols, [{ kind: 'filterBands', value: 3 }, { kind: 'filterNaN' },
+            { kind: 'filterByValue', columnName: 'opacity', comparator: 'lt', value: 2 }, { kind: 'scale', value: 0.5 }]]);
+    }
+    fx.meta.cases = specs.map(s => s[0]);
+    const actionsMeta = (acts) => acts.map(a => (a.value && a.value.x !== undefined)
+        ? Object.assign({}, a, { value: [a.value.x, a.value.y, a.value.z] }) : a);
+    for (const [name, names, cols, acts] of specs) {
+        const table = toTable(names, cols);
+        fx.meta[`${name}_actions`] = actionsMeta(acts);
+        addTable(fx, `${name}_in_`, table);
+        const out = processDataTable(table, acts);
+        fx.meta[`${name}_out_types`] = out.columns.map(c => c.dataType);
+        addTable(fx, `${name}_out_`, out);
+        const { writes, handle } = captureHandle();
+        try {
+            await quiet(() => writeCompressedPly(handle, out));
+            const u8 = (b) => new Uint8Array(b.buffer.slice(b.byteOffset, b.byteOffset + b.length));
+            fx.add(`${name}_header`, u8(writes[0]));
+            fx.add(`${name}_chunk`, new Float32Array(u8(writes[1]).buffer));
+            fx.add(`${name}_vertex`, new Uint32Array(u8(writes[2]).buffer));
+            fx.add(`${name}_sh`, u8(writes[3]));
+        } catch (e) {
+            fx.meta[`${name}_write_error`] = String(e);
+        }
+    }
+    fx.save();
+};
+
 (async () => {
     for (const name of Object.keys(cases)) {
         if (only.length && only.indexOf(name) < 0) continue;

@@ -1,0 +1,46 @@
+'use strict';
+// Node host: processDataTable and writeCompressedPly (with the actions in the same device call)
+// on the reference's own vectors (tests/golden/process_chain.*).  Prints one JSON object:
+// per case, whether the processed table and the four compressed-PLY writes match byte for byte.
+const fs = require('fs');
+const path = require('path');
+
+const host = require(path.join(__dirname, '..', '..', 'splat-transform_amd', 'js'));
+const GOLDEN = path.join(__dirname, '..', 'golden');
+
+const CTOR = { f4: Float32Array, f8: Float64Array, u4: Uint32Array, i4: Int32Array, u1: Uint8Array, i1: Int8Array,
+    u2: Uint16Array, i2: Int16Array };
+const man = JSON.parse(fs.readFileSync(path.join(GOLDEN, 'process_chain.json'), 'utf8'));
+const blob = fs.readFileSync(path.join(GOLDEN, 'process_chain.bin'));
+const arr = (k) => {
+    const a = man.arrays[k];
+    const ctor = CTOR[a.dtype];
+    const copy = Buffer.from(blob.subarray(a.offset, a.offset + a.nbytes));
+    return new ctor(copy.buffer, copy.byteOffset, a.nbytes / ctor.BYTES_PER_ELEMENT);
+};
+const bytes = a => Buffer.from(a.buffer, a.byteOffset, a.byteLength);
+const sameBytes = (a, b) => a.constructor === b.constructor && a.length === b.length && bytes(a).equals(bytes(b));
+// the fixture stores Vec3 action values as [x, y, z]
+const actionsOf = c => man.meta[`${c}_actions`].map(a => (Array.isArray(a.value)
+    ? Object.assign({}, a, { value: { x: a.value[0], y: a.value[1], z: a.value[2] } }) : a));
+const tableOf = c => new host.DataTable(man.meta[`${c}_in_columns`].map(n => new host.Column(n, arr(`${c}_in_${n}`))));
+
+(async () => {
+    const out = {};
+    for (const c of man.meta.cases) {
+        const r = {};
+        const res = host.processDataTable(tableOf(c), actionsOf(c));
+        r.names = JSON.stringify(res.columns.map(col => col.name)) === JSON.stringify(man.meta[`${c}_out_columns`]);
+        r.table = res.columns.every(col => sameBytes(col.data, arr(`${c}_out_${col.name}`)));
+        const writes = [];
+        const fh = { write: async (d) => { writes.push(Buffer.from(d.buffer, d.byteOffset, d.byteLength)); } };
+        await host.writeCompressedPly(fh, tableOf(c), actionsOf(c));
+        r.writes = writes.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => writes[i].equals(bytes(arr(`${c}_${k}`))));
+        // the reference's split: processDataTable, then writeCompressedPly of its result
+        const w2 = [];
+        await host.writeCompressedPly({ write: async (d) => { w2.push(Buffer.from(d.buffer, d.byteOffset, d.byteLength)); } }, res);
+        r.writes2 = w2.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => w2[i].equals(bytes(arr(`${c}_${k}`))));
+        out[c] = r;
+    }
+    console.log(JSON.stringify(out));
+})().catch((e) => { console.error(e); process.exit(1); });

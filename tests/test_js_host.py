@@ -39,7 +39,8 @@ def test_addon_exports(addon_built):
     keys, ver = r.stdout.strip().rsplit(' ', 1)
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
                                        'filterNaN', 'combineLayout', 'setDevices', 'getDevices', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
-                                       'webpLossless', 'sogBundle', 'readPly', 'decompressPly'])
+                                       'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
+                                       'process'])
     assert ver == '1'
 
 
@@ -88,6 +89,19 @@ def test_js_filter_nan_every_type_matches_reference(addon_built):
     each column's type preserved; the splat table too"""
     out = _table_ops('filter')
     assert all(out['same']) and all(out['same2']), out
+
+
+@pytest.mark.gpu
+def test_js_process_and_compressed_ply_match_reference(addon_built):
+    """processDataTable (process.ts:64-145) and writeCompressedPly (write-compressed-ply.ts:31-115),
+    alone and with the action list in the same device call, against the reference's writes:
+    every action kind, header text included"""
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'process_chain.js')], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout)
+    bad = {c: v for c, v in out.items() if not all(v.values())}
+    assert not bad, bad
 
 
 @pytest.mark.gpu

@@ -1,0 +1,154 @@
+"""processDataTable (process.ts:64-145) and the CLI's `in.ply [actions] out.compressed.ply`
+(index.ts:463-496 -> writeCompressedPly, write-compressed-ply.ts:31-115) as one call
+(st_process / st_compressed_ply / st_dev_compressed_ply), against the reference's own vectors
+(tests/golden/process_chain.*: make_golden.js process_chain -- every action kind, NaN/-0 edges,
+an unknown comparator, a missing column, an empty result) and, at 1M splats, the oracle chain.
+Compressed-PLY outputs are compared as file bytes (NaN bit patterns included)."""
+import numpy as np
+import pytest
+
+import oracle
+import splat_hip as sh
+from golden_io import Golden
+
+TYPES = {'int8': np.int8, 'uint8': np.uint8, 'int16': np.int16, 'uint16': np.uint16, 'int32': np.int32,
+         'uint32': np.uint32, 'float32': np.float32, 'float64': np.float64}
+
+
+def _bytes_equal(a, b, what):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    assert a.dtype == b.dtype and a.shape == b.shape, (what, a.dtype, b.dtype, a.shape, b.shape)
+    bad = np.nonzero(a.view(np.uint8) != b.view(np.uint8))[0]
+    assert bad.size == 0, f'{what}: {bad.size} bytes differ, first at byte {bad[:4]}'
+
+
+def _case(g, c):
+    src = [(k, g[f'{c}_in_{k}']) for k in g.meta[f'{c}_in_columns']]
+    want = [(k, g[f'{c}_out_{k}']) for k in g.meta[f'{c}_out_columns']]
+    return src, g.meta[f'{c}_actions'], want
+
+
+G = Golden('process_chain')
+CASES = G.meta['cases']
+
+
+# ---- CPU: the oracle and the host-side schema logic against the reference --------------
+@pytest.mark.parametrize('case', CASES)
+def test_oracle_chain_matches_reference(case):
+    src, acts, want = _case(G, case)
+    out, chunk, vertex, shb = oracle.compressed_ply(src, acts)
+    assert [k for k, _ in out] == [k for k, _ in want]
+    assert [str(a.dtype) for _, a in out] == [str(np.dtype(TYPES[t])) for t in G.meta[f'{case}_out_types']]
+    for (k, a), (_, b) in zip(out, want):
+        _bytes_equal(a, b, k)
+    for nm, a in (('chunk', chunk), ('vertex', vertex), ('sh', shb)):
+        _bytes_equal(a, G[f'{case}_{nm}'], nm)
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_process_schema_matches_reference(case):
+    src, acts, want = _case(G, case)
+    assert [k for k, _ in sh.process_schema(src, acts)] == [k for k, _ in want]
+
+
+# ---- GPU: the one-call chain --------------------------------------------------------------
+@pytest.fixture(scope='module')
+def ctx():
+    import torch  # noqa: F401
+    c = sh.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES)
+def test_compressed_ply_matches_reference(ctx, case):
+    src, acts, want = _case(G, case)
+    m, chunk, vertex, shb = ctx.compressed_ply(src, acts)
+    assert m == len(want[0][1])
+    for nm, a in (('chunk', chunk), ('vertex', vertex), ('sh', shb)):
+        _bytes_equal(a, G[f'{case}_{nm}'], nm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES)
+def test_process_matches_reference(ctx, case):
+    src, acts, want = _case(G, case)
+    out = ctx.process(src, acts)
+    assert [k for k, _ in out] == [k for k, _ in want]
+    for (k, a), (_, b) in zip(out, want):
+        _bytes_equal(a, b, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['config3', 'bands2_lte', 'empty'])
+def test_dev_compressed_ply_matches_reference(ctx, case):
+    import torch
+    src, acts, want = _case(G, case)
+    n = len(src[0][1])
+    d = [(k, torch.from_numpy(np.ascontiguousarray(a)).cuda()) for k, a in src]
+    chunk = torch.full(((n + 255) // 256 * 18 + 1,), 7.0, device='cuda')
+    vertex = torch.zeros(n * 4 + 1, dtype=torch.int32, device='cuda')
+    shb = torch.zeros(n * 45 + 1, dtype=torch.uint8, device='cuda')
+    m, C = ctx.dev_compressed_ply(d, acts, chunk, vertex, shb)
+    ctx.synchronize()
+    assert m == len(want[0][1])
+    _bytes_equal(chunk[:(m + 255) // 256 * 18].cpu().numpy(), G[f'{case}_chunk'], 'chunk')
+    _bytes_equal(vertex[:m * 4].cpu().numpy().view(np.uint32), G[f'{case}_vertex'], 'vertex')
+    _bytes_equal(shb[:m * 3 * C].cpu().numpy(), G[f'{case}_sh'], 'sh')
+
+
+@pytest.mark.gpu
+def test_compressed_ply_config3_1m_vs_oracle(ctx):
+    """BASELINE config 3's chain at 1M SH-3 splats, one call: -r 0,45,0 --filterNaN then the
+    Morton order and chunk pack, 0.1% of rows non-finite, 5% in a 1e-3 cube (Morton runs > 256)"""
+    n = 1_000_000
+    rng = np.random.default_rng(2003)
+    names = ['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+        ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
+    cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in names}
+    cols['x'] *= 10
+    cube = rng.random(n) < 0.05
+    cols['x'][cube] = 1 + rng.random(cube.sum()).astype(np.float32) * 1e-3
+    bad = rng.choice(n, n // 1000, replace=False)
+    for j, r in enumerate(bad):
+        cols[names[j % len(names)]][r] = [np.nan, np.inf, -np.inf][j % 3]
+    acts = [{'kind': 'rotate', 'value': [0, 45, 0]}, {'kind': 'filterNaN'}]
+    src = list(cols.items())
+    m, chunk, vertex, shb = ctx.compressed_ply(src, acts)
+    out, ochunk, overtex, osh = oracle.compressed_ply(src, acts)
+    assert m == len(out[0][1])
+    _bytes_equal(chunk, ochunk, 'chunk')
+    _bytes_equal(vertex, overtex, 'vertex')
+    _bytes_equal(shb, osh, 'sh')
+
+
+@pytest.mark.gpu
+def test_process_typed_filter_by_value_vs_oracle(ctx):
+    """filterByValue on integer and float64 columns (compared as JS numbers), then filterNaN,
+    over the reference's all-types table"""
+    g = Golden('filter_combine')
+    src = list(g.table('typed_in_').items())
+    for acts in ([{'kind': 'filterByValue', 'columnName': 'c_uint8', 'comparator': 'gt', 'value': 100}],
+                 [{'kind': 'filterByValue', 'columnName': 'c_int32', 'comparator': 'lte', 'value': -1.5e9},
+                  {'kind': 'filterNaN'}],
+                 [{'kind': 'filterByValue', 'columnName': 'c_float64', 'comparator': 'neq', 'value': 0},
+                  {'kind': 'filterByValue', 'columnName': 'c_int16', 'comparator': 'gte', 'value': 0}],
+                 [{'kind': 'filterByValue', 'columnName': 'c_uint32', 'comparator': 'eq', 'value': 0}]):
+        out = ctx.process(src, acts)
+        want = oracle.process(src, acts)
+        assert [k for k, _ in out] == [k for k, _ in want]
+        for (k, a), (_, b) in zip(out, want):
+            _bytes_equal(a, b, k)
+
+
+@pytest.mark.gpu
+def test_chain_errors(ctx):
+    src, acts, _ = _case(G, 'config3')
+    typed = [(k, a.astype(np.float64) if k == 'rot_1' else a) for k, a in src]
+    with pytest.raises(sh.StError) as e:
+        ctx.compressed_ply(typed, acts)
+    assert e.value.code == -6  # ST_ERR_UNSUPPORTED: transform reads float32 columns
+    with pytest.raises(sh.StError) as e:
+        ctx.compressed_ply(src, [{'kind': 'filterBands', 'value': 4}])
+    assert e.value.code == sh.ST_ERR_ARG
