@@ -286,7 +286,13 @@ def kmeans(ops, comm, shard, cols, k, iters, draws, concat=False):
     of the columns.  Returns (centroids (d, k) float32, local labels, draws used)."""
     P = _Points(shard, cols, concat)
     if P.N < k:
-        raise NotImplementedError('distributed kmeans with fewer points than clusters')
+        # k-means.ts:139-144: the points themselves are the centroids, point i is labelled i
+        cen = _gather_rows(ops, comm, P, np.arange(P.N))
+        r = comm.rank
+        cnt, off = shard.counts[r], shard.offsets[r]
+        j = np.arange(P.n, dtype=np.int64)
+        g = (j // max(cnt, 1)) * shard.N + off + j % max(cnt, 1) if concat else off + j
+        return cen, torch.from_numpy(g.astype(np.int32)).to(P.pts[0].device), 0
     d, n = P.d, P.n
     ops.prepare(P.pts)
     cursor = 0

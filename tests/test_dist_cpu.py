@@ -55,9 +55,13 @@ def _worker(rank, world, port, seed, out):
     labs = comm.allgather(lab)
     cb, lab8, used1 = splat_dist.cluster1d(ops, comm, shard, cols[:3], 3, draws)
     lab8s = comm.allgather(lab8.reshape(3, -1).t().contiguous())
+    # fewer points than clusters (k-means.ts:139-144): the points are the centroids
+    cen2, lab2, used2 = splat_dist.kmeans(ops, comm, shard, cols, n + 80, 2, draws)
+    lab2s = comm.allgather(lab2)
     if rank == 0:
         out.put(dict(cen=cen.numpy().copy(), lab=torch.cat(labs).numpy().copy(), used=used,
-                     cb=cb.numpy().copy(), lab8=torch.cat(lab8s).t().numpy().copy(), used1=used1))
+                     cb=cb.numpy().copy(), lab8=torch.cat(lab8s).t().numpy().copy(), used1=used1,
+                     cen2=cen2.numpy().copy(), lab2=torch.cat(lab2s).numpy().copy(), used2=used2))
     dist.destroy_process_group()
 
 
@@ -85,6 +89,10 @@ def test_distributed_kmeans_matches_single_process():
     assert rc == 0 and res['used1'] == used1
     assert np.array_equal(res['cb'].view(np.uint32), cb.view(np.uint32))
     assert np.array_equal(res['lab8'], lab8)
+    rc, cen2, lab2, used2 = oracle.kmeans([x[j] for j in range(x.shape[0])], x.shape[1] + 80, 2, draws)
+    assert rc == 0 and res['used2'] == used2 == 0
+    assert np.array_equal(res['lab2'], lab2) and np.array_equal(lab2, np.arange(x.shape[1]))
+    assert np.array_equal(res['cen2'].view(np.uint32), cen2.view(np.uint32))
 
 
 def _texel_worker(rank, world, port, out):
