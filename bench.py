@@ -54,7 +54,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo with '
                     '--dist-python rehearses several ranks on one GPU)')
-    ap.add_argument('--cpu-assign-sample', type=int, default=1000)
+    ap.add_argument('--cpu-assign-sample', type=int, default=3000)
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')

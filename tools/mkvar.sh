@@ -11,5 +11,5 @@ flags="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result"
 [ "$base" = st_kmeans_nd ] && flags="$flags -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans -fno-slp-vectorize"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $flags $EXTRA -I$R/splat-transform_amd/csrc -I$R/include -c $src -o /tmp/var_$name.o
 objs=$(ls $B/*.o | grep -v "/${base}.hip.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/tools/var/$name.so $objs /tmp/var_$name.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -pthread -o $R/tools/var/$name.so $objs /tmp/var_$name.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built tools/var/$name.so
