@@ -106,6 +106,28 @@ def measure(ctx, stream, dev, n=10_000_000, reps=5):
         ctx.dev_pack_compressed(pack_cols, order, chunk, vertex, shb)
     ms = timed(pipeline)
     out['config3'] = {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'kept': m}
+
+    # the same chain as ONE library call (st_dev_compressed_ply: processDataTable's actions, then
+    # writeCompressedPly's ordering + chunk loop), and its host form (st_compressed_ply: the table
+    # uploaded from pageable host arrays, the packed arrays downloaded -- the Node CLI's path,
+    # PCIe-inclusive)
+    acts = [{'kind': 'rotate', 'value': (0, 45, 0)}, {'kind': 'filterNaN'}]
+    items = list(cols.items())
+    dchunk = torch.empty((n + 255) // 256 * 18, device=dev)
+    dvertex = torch.empty(n * 4, dtype=torch.int32, device=dev)
+    dsh = torch.empty(n * 45, dtype=torch.uint8, device=dev)
+    ms1 = timed(lambda: ctx.dev_compressed_ply(items, acts, dchunk, dvertex, dsh))
+    out['config3_one_call'] = {'ms': ms1, 'Msplats_per_s': n / (ms1 / 1e3) / 1e6,
+                               'what': 'st_dev_compressed_ply (rotate 0,45,0 + filterNaN + Morton + chunk pack)'}
+    host = [(k, v.cpu().numpy()) for k, v in items]
+    ctx.compressed_ply(host, acts)  # warm (workspace)
+    t0 = time.perf_counter()
+    for _ in range(2):
+        ctx.compressed_ply(host, acts)
+    ms2 = (time.perf_counter() - t0) / 2 * 1e3
+    out['config3_host_one_call'] = {'ms': ms2, 'Msplats_per_s': n / (ms2 / 1e3) / 1e6,
+                                    'what': 'st_compressed_ply from pageable host columns (62 x 4 B/splat up, '
+                                            '16 + 45 B/splat + chunks down): the PCIe-inclusive rate of the Node path'}
     return out
 
 
