@@ -195,6 +195,180 @@ __global__ __launch_bounds__(256) void k_kd1_assign_fast(const float *__restrict
     }
 }
 
+// ---- fused iteration for k <= 256 (cluster1d's codebooks) ------------------------------
+// The member sort only has to lay each cluster's values out in ascending point order: the
+// label is an 8-bit digit, so one counting-sort pass does it, and the cluster starts are
+// the scanned digit counts.  Assign + tile histogram in one kernel (byte labels out), the
+// scan of the (digit, tile) counts, then a scatter that moves 4-byte values only: 14 bytes
+// per point against 36 for assign -> (label, value) pairs -> radix pass -> bounds.
+constexpr int F1_T = 256, F1_ROWS = 16, F1_TILE = F1_T * F1_ROWS, F1_WAVES = F1_T / 64;
+
+// k_kd1_assign_fast's bracket assign over one 4,096-point tile per workgroup; lab8 = labels
+// as bytes, labels (if non-null) the u32 result, hist[d * ntiles + tile] = count of digit d
+__global__ __launch_bounds__(F1_T) void k_kd1_assign_hist(const float *__restrict__ pts, uint64_t n,
+                                                         const float *__restrict__ cen,
+                                                         const uint32_t *__restrict__ order, int k,
+                                                         uint32_t *__restrict__ labels, uint8_t *__restrict__ lab8,
+                                                         uint32_t *__restrict__ hist, uint32_t ntiles) {
+    __shared__ float sv[256];
+    __shared__ uint32_t si[256];
+    __shared__ uint16_t cc[256];
+    __shared__ uint32_t first[KD1_CELLS + 1];
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+        const uint32_t o = order[i];
+        si[i] = o;
+        sv[i] = cen[o];
+    }
+    const uint64_t base = (uint64_t)blockIdx.x * F1_TILE;
+    float pv[F1_ROWS];  // the tile's points in flight while the tables are built
+#pragma unroll
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t i = base + (uint64_t)r * F1_T + threadIdx.x;
+        pv[r] = i < n ? pts[i] : 0.f;
+    }
+    __syncthreads();
+    const float lo = sv[0], hi = sv[k - 1];
+    const float span = hi - lo;
+    const float inv = (span > 0.f && span < __builtin_inff()) ? (float)KD1_CELLS / span : 0.f;
+    auto cell = [&](float x) -> int {
+        const float t = (x - lo) * inv;
+        return (int)__builtin_fminf(__builtin_fmaxf(t, 0.f), (float)(KD1_CELLS - 1));
+    };
+    for (int i = threadIdx.x; i < k; i += blockDim.x) cc[i] = (uint16_t)cell(sv[i]);
+    __syncthreads();
+    for (int g = threadIdx.x; g <= KD1_CELLS; g += blockDim.x) {
+        int a = 0, b = k;
+        while (a < b) {
+            const int m = (a + b) >> 1;
+            if ((int)cc[m] < g) a = m + 1;
+            else b = m;
+        }
+        first[g] = (uint32_t)a;
+    }
+    __syncthreads();
+    auto dist = [&](int pos, double p) {
+        const double v = (double)sv[pos] - p;
+        return 0.0 + v * v;
+    };
+    auto val = [&](uint32_t pos) -> float { return sv[pos]; };
+    auto idx = [&](uint32_t pos) -> uint32_t { return si[pos]; };
+#pragma unroll
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t i = base + (uint64_t)r * F1_T + threadIdx.x;
+        if (i >= n) break;
+        const float pf = pv[r];
+        const double p = pf;
+        const int g = cell(pf);
+        int u = (int)first[g];
+        const int ue = (int)first[g + 1];
+        while (u < ue && sv[u] <= pf) ++u;
+        const int L = u - 1, R = u;
+        const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
+        const double dr = R < k ? dist(R, p) : __builtin_inf();
+        const double m = __builtin_fmin(dl, dr);
+        const bool tie = dl == dr || (L >= 1 && dist(L - 1, p) == m) || (R + 1 < k && dist(R + 1, p) == m);
+        const uint32_t lab = !tie ? si[dl < dr ? L : R] : kd1_walk(p, k, val, idx);
+        lab8[i] = (uint8_t)lab;
+        if (labels) labels[i] = lab;
+        atomicAdd(&h[lab], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// stable counting-sort pass on the byte labels moving the value bits only: each wave ranks its
+// 1,024 points with ballots over the `bits` label bits, the tile is reordered by label in LDS
+// and each label's run is stored contiguously at its scanned offset
+__global__ __launch_bounds__(F1_T) void k_lab_scatter(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
+                                                      uint64_t n, int bits, const uint32_t *__restrict__ offs,
+                                                      uint32_t ntiles, uint32_t *__restrict__ ovals) {
+    __shared__ uint32_t wcount[F1_WAVES][256];
+    __shared__ uint32_t wbase[F1_WAVES][256];
+    __shared__ uint32_t goff[256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t wtot[F1_WAVES];
+    __shared__ uint32_t sval[F1_TILE];
+    __shared__ uint8_t sdig[F1_TILE];
+    for (int i = threadIdx.x; i < F1_WAVES * 256; i += F1_T) (&wcount[0][0])[i] = 0;
+    goff[threadIdx.x] = offs[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t tbase = (uint64_t)blockIdx.x * F1_TILE;
+    const uint64_t wb = tbase + (uint64_t)w * 64 * F1_ROWS;
+    uint32_t v[F1_ROWS], off[F1_ROWS], dg[F1_ROWS];
+#pragma unroll
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t e = wb + (uint64_t)r * 64 + lane;
+        const bool valid = e < n;
+        dg[r] = valid ? lab8[e] : 0u;
+        v[r] = valid ? __builtin_bit_cast(uint32_t, pts[e]) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t e = wb + (uint64_t)r * 64 + lane;
+        const bool valid = e < n;
+        const uint32_t d = dg[r];
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t before = valid ? wcount[w][d] : 0u;
+        off[r] = before + rank;
+        if (valid && (peers & lt) == 0) wcount[w][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < F1_WAVES; ++i) {
+            wbase[i][d] = s;
+            s += wcount[i][d];
+        }
+        uint32_t incl = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wtot[w] = incl;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int i = 0; i < w; ++i) woff += wtot[i];
+        dstart[d] = woff + incl - s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t e = wb + (uint64_t)r * 64 + lane;
+        if (e < n) {
+            const uint32_t lp = dstart[dg[r]] + wbase[w][dg[r]] + off[r];
+            sval[lp] = v[r];
+            sdig[lp] = (uint8_t)dg[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((n - tbase) < (uint64_t)F1_TILE ? (n - tbase) : (uint64_t)F1_TILE);
+    for (uint32_t i = threadIdx.x; i < cnt; i += F1_T) {
+        const uint32_t d = sdig[i];
+        ovals[goff[d] + (i - dstart[d])] = sval[i];
+    }
+}
+
+// cluster starts from the scanned (digit, tile) counts: start[c] = offs[c * ntiles], start[k] = n
+__global__ void k_f1_starts(const uint32_t *__restrict__ offs, uint32_t ntiles, int k, uint64_t n,
+                            uint32_t *__restrict__ start) {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c <= k; c += gridDim.x * blockDim.x)
+        start[c] = c < k ? offs[(uint64_t)c * ntiles] : (uint32_t)n;
+}
+
 // pairs for the member sort: key = label, val = value bits (ascending point order kept)
 __global__ __launch_bounds__(256) void k_pairs1d(const float *pts, const uint32_t *labels, uint64_t n,
                                                  uint32_t *keys, uint32_t *vals) {
@@ -800,19 +974,48 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     auto *rp_total = wsT<__int128>(c, "k1.rptotal", (size_t)k);
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
+    // the fused iteration (k <= 256, no ST_KD1_WALK / ST_K1_PAIRS): byte labels + tile counts,
+    // scan, value-only scatter
+    const bool fused = k <= 256 && n > 0 && n < (1ull << 32) && !getenv("ST_KD1_WALK") && !getenv("ST_K1_PAIRS");
+    const uint32_t ntiles = (uint32_t)((n + F1_TILE - 1) / F1_TILE);
+    uint8_t *lab8 = fused ? wsT<uint8_t>(c, "k1.lab8", n) : nullptr;
+    uint32_t *fhist = fused ? wsT<uint32_t>(c, "k1.fhist", (size_t)256 * ntiles) : nullptr;
     for (int it = 0; it < iters; ++it) {
-        const bool paired = assign1d(c, pts, n, k, cen, labels, keys, vals, it == iters - 1);
-        mark(c, "k1.assign");
-        // update
-        if (!paired) {
-            hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n, keys,
-                               vals);
+        const uint32_t *vals_s = nullptr;
+        if (fused) {
+            auto *ckeys = wsT<uint32_t>(c, "k1.ckeys", (size_t)k);
+            auto *corder = wsT<uint32_t>(c, "k1.corder", (size_t)k);
+            hipLaunchKernelGGL(k_sortkeys, dim3(grid_for(k, 256, 256)), dim3(256), 0, c->stream, cen, k, ckeys, corder);
             ST_LAUNCH_CHECK();
+            radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
+            {
+                KTimer kt(c, "k1.assign");
+                hipLaunchKernelGGL(k_kd1_assign_hist, dim3(ntiles), dim3(F1_T), 0, c->stream, pts, n, cen, corder, k,
+                                   it == iters - 1 ? labels : (uint32_t *)nullptr, lab8, fhist, ntiles);
+                ST_LAUNCH_CHECK();
+            }
+            mark(c, "k1.assign");
+            scan_u32(c, fhist, fhist, (uint64_t)256 * ntiles, nullptr);
+            hipLaunchKernelGGL(k_lab_scatter, dim3(ntiles), dim3(F1_T), 0, c->stream, lab8, pts, n, kbits, fhist,
+                               ntiles, vals);
+            hipLaunchKernelGGL(k_f1_starts, dim3(grid_for((uint64_t)k + 1, 256, 256)), dim3(256), 0, c->stream,
+                               fhist, ntiles, k, n, start);
+            ST_LAUNCH_CHECK();
+            vals_s = vals;
+        } else {
+            const bool paired = assign1d(c, pts, n, k, cen, labels, keys, vals, it == iters - 1);
+            mark(c, "k1.assign");
+            // update
+            if (!paired) {
+                hipLaunchKernelGGL(k_pairs1d, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, pts, labels, n,
+                                   keys, vals);
+                ST_LAUNCH_CHECK();
+            }
+            uint32_t *skeys = keys, *svals = vals;  // where the sort leaves its result (no copy back)
+            radix_sort_u32_inplace_or_swap(c, keys, vals, n, 0, kbits, "k1.msort", &skeys, &svals);
+            bounds_from_sorted(c, skeys, n, k, start);
+            vals_s = svals;
         }
-        uint32_t *skeys = keys, *svals = vals;  // where the sort leaves its result (no copy back)
-        radix_sort_u32_inplace_or_swap(c, keys, vals, n, 0, kbits, "k1.msort", &skeys, &svals);
-        bounds_from_sorted(c, skeys, n, k, start);
-        const uint32_t *vals_s = svals;
         {
             KTimer kt(c, "k1.sum");
             if (chunked) {
