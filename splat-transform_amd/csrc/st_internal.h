@@ -234,5 +234,6 @@ void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npair
 
 // multi-GPU writeSog (st_multi.hip): the st_set_devices group (nullptr: one device)
 st_group *default_group();
+int apply_env_devices();  // ST_NUM_GPUS on first use; ST_OK or the error (st_last_error set)
 
 }  // namespace st

@@ -758,6 +758,7 @@ namespace {
 std::mutex g_group_mu;
 st_group *g_group = nullptr;  // st_set_devices
 int g_ndev = 1;
+std::atomic<bool> g_env_done{false};  // ST_NUM_GPUS applied (or overridden by st_set_devices)
 
 template <typename F>
 int guarded_m(F &&f) {
@@ -998,6 +999,7 @@ int st_group_sog_bundle(st_group *g, const st_table *const *tables, int32_t ntab
 }
 
 int st_set_devices(int32_t ngpu) {
+    g_env_done.store(true);  // an explicit choice overrides ST_NUM_GPUS
     return guarded_m([&] {
         int avail = 0;
         ST_HIP(hipGetDeviceCount(&avail));
@@ -1017,6 +1019,7 @@ int st_set_devices(int32_t ngpu) {
 
 int st_get_devices(int32_t *ngpu) {
     if (!ngpu) return ST_ERR_ARG;
+    if (int rc = st::apply_env_devices()) return rc;
     *ngpu = g_ndev;
     return ST_OK;
 }
@@ -1024,6 +1027,29 @@ int st_get_devices(int32_t *ngpu) {
 }  // extern "C"
 
 namespace st {
+// ST_NUM_GPUS=<n> (the host's device-count switch): st_set_devices(n) before the first
+// writeSog of the process unless the host chose explicitly; a bad value fails that call
+int apply_env_devices() {
+    static std::mutex mu;
+    static int rc = ST_OK;
+    static std::string msg;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!g_env_done.exchange(true)) {
+        const char *e = getenv("ST_NUM_GPUS");
+        if (e && *e) {
+            char *end = nullptr;
+            const long n = strtol(e, &end, 10);
+            if (*end || n < 1 || n > 1024) {
+                rc = ST_ERR_ARG;
+                msg = std::string("ST_NUM_GPUS: not a device count: ") + e;
+            } else if ((rc = st_set_devices((int32_t)n)) != ST_OK) {
+                msg = std::string("ST_NUM_GPUS: ") + st_last_error();
+            }
+        }
+    }
+    if (rc != ST_OK) set_last_error(msg);
+    return rc;
+}
 // the process-wide group of st_set_devices (nullptr: one device)
 st_group *default_group() { return g_group; }
 uint64_t default_group_sog(const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,

@@ -78,3 +78,25 @@ def test_context_without_gpu_fails_loudly(L):
         pytest.skip('GPU present')
     with pytest.raises(sh.StError):
         sh.Context(0)
+
+
+def _get_devices_with_env(value):
+    """st_get_devices in a fresh process with ST_NUM_GPUS set (the switch applies once per process)"""
+    import subprocess
+    import sys
+    code = ('import ctypes, sys; sys.path.insert(0, %r); import splat_hip as sh; L = sh.lib(); '
+            'n = ctypes.c_int32(); rc = L.st_get_devices(ctypes.byref(n)); '
+            'print(rc, n.value, L.st_last_error().decode())' % os.path.join(ROOT, 'splat-transform_amd', 'py'))
+    env = dict(os.environ, ST_NUM_GPUS=value)
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rc, n, msg = r.stdout.strip().split(' ', 2) + [''] * (3 - len(r.stdout.strip().split(' ', 2)))
+    return int(rc), int(n), msg
+
+
+def test_st_num_gpus_rejects_a_bad_value():
+    """ST_NUM_GPUS: a value that is not a device count fails loudly, before any device call"""
+    rc, n, msg = _get_devices_with_env('two')
+    assert rc == sh.ST_ERR_ARG and n == 0 and 'ST_NUM_GPUS' in msg
+    rc, _, msg = _get_devices_with_env('0')
+    assert rc == sh.ST_ERR_ARG and 'ST_NUM_GPUS' in msg

@@ -141,3 +141,19 @@ def test_set_devices(ctx):
     with pytest.raises(sh.StError):
         sh.set_devices(sh.device_count() + 1)
     assert sh.get_devices() == 1
+
+
+def test_st_num_gpus_env():
+    """ST_NUM_GPUS=<n> selects the writeSog device count on first use (st_set_devices); more GPUs
+    than the box has fails loudly"""
+    import os
+    import subprocess
+    import sys
+    py = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'splat-transform_amd', 'py')
+    code = ('import ctypes, sys; sys.path.insert(0, %r); import splat_hip as sh; L = sh.lib(); '
+            'n = ctypes.c_int32(); rc = L.st_get_devices(ctypes.byref(n)); print(rc, n.value)' % py)
+    for value, want in (('1', '0 1'), (str(sh.device_count() + 1), '-1 0')):
+        r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, ST_NUM_GPUS=value))
+        assert r.returncode == 0, r.stderr
+        assert r.stdout.strip() == want, (value, r.stdout)
