@@ -42,6 +42,8 @@
  *   st_dev_ply_transpose                    (the same, rows already in HBM)     read-ply.ts:165-182
  *   st_decompress_ply / st_dev_...          decompressPly                       readers/decompress-ply.ts:82-232
  *   st_process                              processDataTable(dataTable, actions) process.ts:64-145
+ *   st_ply_compressed_ply / st_ply_sog_bundle  readPly + processDataTable + writer, resident
+ *                                           (the CLI's one-input path)           index.ts:463-496
  *   st_compressed_ply / st_dev_...          processDataTable + writeCompressedPly
  *                                           (CLI: in.ply [actions] out.compressed.ply) index.ts:463-496,
  *                                                                               write-compressed-ply.ts:31-115
@@ -275,6 +277,19 @@ int st_compressed_ply(st_ctx *ctx, const st_ttable *src, const st_action *action
                       uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs);
 int st_dev_compressed_ply(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions,
                           float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m, int32_t *out_sh_coeffs);
+/* The same straight from the PLY file (`in.ply [actions] out.compressed.ply` / `in.ply [actions]
+ * out.sog`, index.ts:463-496): the element's rows stream page cache -> pinned -> HBM
+ * (st_dev_ply_read, read-ply.ts:139-188) and stay resident through the actions and the writer;
+ * only the outputs cross back.  element < 0 selects the element named "vertex".
+ * st_ply_compressed_ply: outputs sized for the element's row count and band.
+ * st_ply_sog_bundle: st_sog_bundle of the processed table (malloc'd archive, st_free); with
+ * st_set_devices(n > 1) the processed columns are sharded over the group from the host. */
+int st_ply_compressed_ply(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
+                          int32_t nactions, float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m,
+                          int32_t *out_sh_coeffs);
+int st_ply_sog_bundle(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
+                      int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                      uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size);
 
 /* ---- multi-GPU building blocks -----------------------------------
  * One process per GPU; rows are sharded in contiguous ranges in rank order; the

@@ -7,9 +7,11 @@
 // updates float32 columns in place; a filter gathers the survivors into the other of two
 // workspace generations (ping-pong), so a long action list needs at most two copies of the
 // table beside the input.
+#include <cstdlib>
 #include <cstring>
 
 #include "st_internal.h"
+#include "st_webp.h"
 
 namespace st {
 namespace {
@@ -176,6 +178,32 @@ void upload_chain(st_ctx *c, const st_ttable *src, Chain &ch) {
     }
 }
 
+// the element's rows straight from the file into HBM columns (page cache -> pinned -> HBM,
+// st_dev_ply_read); element < 0 selects the one named "vertex" (read-ply.ts's splat element)
+void ply_chain(st_ctx *c, int fd, const st_ply_header *h, int element, Chain &ch) {
+    if (element < 0)
+        for (int e = 0; e < h->nelements && element < 0; ++e)
+            if (std::strcmp(h->elements[e].name, "vertex") == 0) element = e;
+    ST_REQUIRE(element >= 0 && element < h->nelements, ST_ERR_ARG, "ply: no such element");
+    const st_ply_element &el = h->elements[element];
+    std::vector<void *> cols(el.nprops);
+    for (int p = 0; p < el.nprops; ++p) {
+        cols[p] = ws(c, "chain.in." + std::to_string(p), el.count * type_size(el.props[p].type) + 16);
+        ch.cols.push_back(ChainCol{el.props[p].name, el.props[p].type, cols[p]});
+    }
+    ch.n = el.count;
+    ply_read_dev(c, fd, *h, element, cols.data());
+}
+
+// the processed table as writeSog reads it: float32 columns by name (write-sog.ts:110-370)
+const st_table *sog_view(Chain &ch) {
+    static const char *scols[] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0", "f_dc_1", "f_dc_2",
+                                  "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    for (auto *nm : scols) ch.require_f32(nm, "writeSog");
+    for (int i = 0; i < 45; ++i) ch.require_f32("f_rest_" + std::to_string(i), "writeSog");
+    return ch.f32();
+}
+
 }  // namespace
 }  // namespace st
 
@@ -253,6 +281,95 @@ int st_dev_compressed_ply(st_ctx *c, const st_ttable *src, const st_action *acti
         *out_m = ch.n;
         *out_sh_coeffs = C;
     });
+}
+
+int st_ply_compressed_ply(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
+                          int32_t nactions, float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m,
+                          int32_t *out_sh_coeffs) {
+    return guard([&] {
+        ST_REQUIRE(c && h && fd >= 0 && out_m && out_sh_coeffs && (actions || nactions == 0), ST_ERR_ARG,
+                   "NULL argument");
+        use_device(c);
+        Chain ch{c};
+        ply_chain(c, fd, h, element, ch);
+        run_actions(ch, actions, nactions);
+        const uint64_t m = ch.n, nch = (m + 255) / 256;
+        ST_REQUIRE(m == 0 || (chunk && vertex), ST_ERR_ARG, "compressed_ply: NULL output");
+        auto *dchunk = wsT<float>(c, "chain.chunk", nch * 18);
+        auto *dvert = wsT<uint32_t>(c, "chain.vert", m * 4);
+        auto *dsh = wsT<uint8_t>(c, "chain.sh", m * 3 * (uint64_t)band_coeffs(ch.cols) + 1);
+        int32_t C = 0;
+        compressed_tail(ch, dchunk, dvert, dsh, &C);
+        ST_REQUIRE(C == 0 || m == 0 || sh, ST_ERR_ARG, "compressed_ply: sh output is NULL");
+        if (m) {
+            ST_HIP(hipMemcpyAsync(chunk, dchunk, nch * 18 * 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(vertex, dvert, m * 16, hipMemcpyDeviceToHost, c->stream));
+            if (C) ST_HIP(hipMemcpyAsync(sh, dsh, m * 3 * (uint64_t)C, hipMemcpyDeviceToHost, c->stream));
+        }
+        ST_HIP(hipStreamSynchronize(c->stream));
+        *out_m = m;
+        *out_sh_coeffs = C;
+    });
+}
+
+int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
+                      int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                      uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
+    if (int rc = apply_env_devices()) return rc;
+    std::vector<std::vector<float>> host;  // multi-GPU: the processed columns, sharded from the host
+    std::vector<float *> hcols;
+    std::vector<std::string> hnames;
+    std::vector<const char *> hcn;
+    st_table ht{};
+    int rc = guard([&] {
+        ST_REQUIRE(c && h && fd >= 0 && out && out_size && (actions || nactions == 0), ST_ERR_ARG, "NULL argument");
+        use_device(c);
+        Chain ch{c};
+        ply_chain(c, fd, h, element, ch);
+        run_actions(ch, actions, nactions);
+        const st_table *t = sog_view(ch);
+        if (default_group()) {
+            for (int i = 0; i < t->ncol; ++i) {
+                host.emplace_back(t->n);
+                hnames.push_back(t->names[i]);
+                if (t->n)
+                    ST_HIP(hipMemcpyAsync(host.back().data(), t->cols[i], t->n * 4, hipMemcpyDeviceToHost, c->stream));
+            }
+            ST_HIP(hipStreamSynchronize(c->stream));
+            for (size_t i = 0; i < host.size(); ++i) hcols.push_back(host[i].data()), hcn.push_back(hnames[i].c_str());
+            ht = st_table{t->n, t->ncol, hcn.data(), hcols.data()};
+            return;
+        }
+        const int C = sh_coeffs_of(t);
+        int32_t W, H, pal, cw, chh;
+        ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
+        const uint64_t tex = (uint64_t)W * H * 4;
+        st_sog_textures dt{};
+        dt.means_l = wsT<uint8_t>(c, "h.s.ml", tex);
+        dt.means_u = wsT<uint8_t>(c, "h.s.mu", tex);
+        dt.quats = wsT<uint8_t>(c, "h.s.q", tex);
+        dt.scales = wsT<uint8_t>(c, "h.s.sc", tex);
+        dt.sh0 = wsT<uint8_t>(c, "h.s.sh0", tex);
+        if (C) {
+            dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
+            dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
+        }
+        st_sog_meta meta{};
+        const uint64_t u = sog_dev(c, t, iters, draws, ndraws, &meta, &dt);
+        const uint8_t *view;
+        uint64_t nb;
+        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, &view, &nb);
+        uint8_t *buf = (uint8_t *)std::malloc(nb);
+        ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
+        std::memcpy(buf, view, nb);
+        *out = buf;
+        *out_size = nb;
+        if (used) *used = u;
+    });
+    if (rc != ST_OK || !ht.ncol) return rc;
+    const st_table *tp = &ht;
+    return st_group_sog_bundle(default_group(), &tp, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out,
+                               out_size);
 }
 
 }  // extern "C"

@@ -112,7 +112,7 @@ EXPORTS = [
     'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
-    'st_process', 'st_compressed_ply', 'st_dev_compressed_ply',
+    'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
 ]
 
 
@@ -781,6 +781,47 @@ class Context:
         check(lib().st_dev_compressed_ply(self.h, ctypes.byref(ts), acts, ctypes.c_int32(len(actions)), _ptr(chunk),
                                           _ptr(vertex), _ptr(sh), ctypes.byref(m), ctypes.byref(C)))
         return m.value, C.value
+
+    def ply_compressed_ply(self, path, actions, element=-1):
+        """readPly + processDataTable + writeCompressedPly's arrays from the file, resident in HBM
+        (st_ply_compressed_ply): (m, chunk, vertex, sh)"""
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = PlyHeader()
+            check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+            ei = element if element >= 0 else [e[0] for e in h.layout()].index('vertex')
+            n = h.layout()[ei][1]
+            chunk = np.zeros(max(1, (n + 255) // 256 * 18), np.float32)
+            vertex = np.zeros(max(1, n * 4), np.uint32)
+            sh = np.zeros(max(1, n * 45), np.uint8)
+            acts = make_actions(actions)
+            m, C = ctypes.c_uint64(), ctypes.c_int32()
+            check(lib().st_ply_compressed_ply(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(element),
+                                              acts, ctypes.c_int32(len(actions)), _vp(chunk), _vp(vertex), _vp(sh),
+                                              ctypes.byref(m), ctypes.byref(C)))
+        finally:
+            os.close(fd)
+        m, C = m.value, C.value
+        return m, chunk[:(m + 255) // 256 * 18], vertex[:m * 4], sh[:m * 3 * C]
+
+    def ply_sog_bundle(self, path, actions, iters, draws, dos_time, dos_date, element=-1):
+        """readPly + processDataTable + writeSog to .sog bytes from the file (st_ply_sog_bundle):
+        (archive bytes, draws used)"""
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = PlyHeader()
+            check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+            acts = make_actions(actions)
+            draws = np.ascontiguousarray(draws, np.float64)
+            used, size = ctypes.c_uint64(), ctypes.c_uint64()
+            out = ctypes.c_void_p()
+            check(lib().st_ply_sog_bundle(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(element), acts,
+                                          ctypes.c_int32(len(actions)), ctypes.c_int32(iters), _vp(draws),
+                                          ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.c_uint16(dos_time),
+                                          ctypes.c_uint16(dos_date), ctypes.byref(out), ctypes.byref(size)))
+        finally:
+            os.close(fd)
+        return _take(out, size), used.value
 
     def dev_filter_finite_t(self, cols, out_idx):
         t = make_ttable(cols)

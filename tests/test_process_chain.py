@@ -152,3 +152,45 @@ def test_chain_errors(ctx):
     with pytest.raises(sh.StError) as e:
         ctx.compressed_ply(src, [{'kind': 'filterBands', 'value': 4}])
     assert e.value.code == sh.ST_ERR_ARG
+
+
+# ---- GPU: the same chain straight from the PLY file (st_ply_compressed_ply / st_ply_sog_bundle) --
+def _write_ply(path, items):
+    """binary little-endian PLY of one 'vertex' element (float32 / uchar / double columns as given)"""
+    code = {np.dtype(np.float32): 'float', np.dtype(np.float64): 'double', np.dtype(np.uint8): 'uchar',
+            np.dtype(np.int32): 'int'}
+    n = len(items[0][1])
+    rows = np.zeros(n, np.dtype([(k, a.dtype.newbyteorder('<')) for k, a in items]))
+    for k, a in items:
+        rows[k] = a
+    head = 'ply\nformat binary_little_endian 1.0\ncomment test\n' + f'element vertex {n}\n' + ''.join(
+        f'property {code[np.dtype(a.dtype)]} {k}\n' for k, a in items) + 'end_header\n'
+    with open(path, 'wb') as f:
+        f.write(head.encode() + rows.tobytes())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES)
+def test_ply_compressed_ply_matches_reference(ctx, case, tmp_path):
+    src, acts, want = _case(G, case)
+    p = str(tmp_path / 'in.ply')
+    _write_ply(p, src)
+    m, chunk, vertex, shb = ctx.ply_compressed_ply(p, acts)
+    assert m == len(want[0][1])
+    for nm, a in (('chunk', chunk), ('vertex', vertex), ('sh', shb)):
+        _bytes_equal(a, G[f'{case}_{nm}'], nm)
+
+
+@pytest.mark.gpu
+def test_ply_sog_bundle_equals_host_one_call(ctx, tmp_path):
+    """in.ply -r 0,45,0 --filterNaN out.sog from the file, resident: the archive equals writeSog's
+    bundle of the processed table computed through the host entry points"""
+    src, acts, _ = _case(G, 'config3')
+    p = str(tmp_path / 'in.ply')
+    _write_ply(p, src)
+    draws = oracle.mulberry32(5, 200_000)
+    got, used = ctx.ply_sog_bundle(p, acts, 3, draws, 0x6000, 0x5a21)
+    proc = dict(ctx.process(src, acts))
+    want, used2 = ctx.sog_bundle({k: v for k, v in proc.items() if k not in ('nx', 'ny', 'nz')}, 3, draws, 0x6000,
+                                 0x5a21)
+    assert used == used2 and got == want
