@@ -15,6 +15,8 @@
 //   processDataTable(dataTable, actions)    process.ts:64-145 (one upload for the whole list)
 //   writeCompressedPly(fh, dataTable[, actions])  write-compressed-ply.ts:31-115 (actions first,
 //                                           same device call: the CLI's config-3 path)
+//   compressPlyFile(inFh, outFh, actions)   readPly + processDataTable + writeCompressedPly, the rows
+//   sogFromPlyFile(inFh, actions, iters)    resident in HBM (the CLI's one-input paths, index.ts:463-496)
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
 //   cluster1d(dataTable, iterations)        write-sog.ts:56-99
 //   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
@@ -259,20 +261,42 @@ const VERTEX_PROPS_OUT = ['packed_position', 'packed_rotation', 'packed_scale', 
 const writeCompressedPly = async (fileHandle, dataTable, processActions, version) => {
     const res = addon.compressedPly(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
         normaliseActions(processActions || []));
-    const numSplats = res.numRows;
-    const numChunks = Math.ceil(numSplats / 256);
-    const outputSHCoeffs = res.shCoeffs;
-    const shHeader = outputSHCoeffs ? [`element sh ${numSplats}`].concat(
-        new Array(outputSHCoeffs * 3).fill('').map((_, i) => `property uchar f_rest_${i}`)) : [];
-    const headerText = [].concat(
-        'ply', 'format binary_little_endian 1.0', `comment Generated by splat-transform ${version || '0.10.1'}`,
-        `element chunk ${numChunks}`, CHUNK_PROPS_OUT.map(p => `property float ${p}`),
-        `element vertex ${numSplats}`, VERTEX_PROPS_OUT.map(p => `property uint ${p}`),
-        shHeader, 'end_header\n').join('\n');
-    await fileHandle.write(Buffer.from(headerText, 'utf8'));
+    await fileHandle.write(Buffer.from(compressedPlyHeader(res.numRows, res.shCoeffs, version), 'utf8'));
     await fileHandle.write(new Uint8Array(res.chunk.buffer));
     await fileHandle.write(new Uint8Array(res.vertex.buffer));
     await fileHandle.write(res.sh);
+};
+
+// the CLI's one-input paths straight from the file (index.ts:463-496): readPly + processDataTable +
+// the writer in one device call, the rows resident in HBM (read page cache -> pinned -> HBM); only
+// the outputs cross back.  inHandle / outHandle: fs.promises FileHandles.
+const compressedPlyHeader = (numSplats, outputSHCoeffs, version) => {
+    const shHeader = outputSHCoeffs ? [`element sh ${numSplats}`].concat(
+        new Array(outputSHCoeffs * 3).fill('').map((_, i) => `property uchar f_rest_${i}`)) : [];
+    return [].concat(
+        'ply', 'format binary_little_endian 1.0', `comment Generated by splat-transform ${version || '0.10.1'}`,
+        `element chunk ${Math.ceil(numSplats / 256)}`, CHUNK_PROPS_OUT.map(p => `property float ${p}`),
+        `element vertex ${numSplats}`, VERTEX_PROPS_OUT.map(p => `property uint ${p}`),
+        shHeader, 'end_header\n').join('\n');
+};
+
+const compressPlyFile = async (inHandle, outHandle, processActions, version) => {
+    const res = addon.compressedPlyFromFile(inHandle.fd, normaliseActions(processActions || []));
+    await outHandle.write(Buffer.from(compressedPlyHeader(res.numRows, res.shCoeffs, version), 'utf8'));
+    await outHandle.write(new Uint8Array(res.chunk.buffer));
+    await outHandle.write(new Uint8Array(res.vertex.buffer));
+    await outHandle.write(res.sh);
+};
+
+const sogFromPlyFile = (inHandle, processActions, iterations) => {
+    const k = 65536;
+    const date = new Date();
+    const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
+    const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
+    const acts = normaliseActions(processActions || []);
+    const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
+        draws => addon.sogBundleFromFile(inHandle.fd, acts, iterations, draws, dosTime, dosDate));
+    return Promise.resolve(res.archive);
 };
 
 const kmeans = (points, k, iterations) => {
@@ -402,6 +426,8 @@ module.exports = {
     packCompressed,
     processDataTable,
     writeCompressedPly,
+    compressPlyFile,
+    sogFromPlyFile,
     kmeans,
     cluster1d,
     sogTextures,

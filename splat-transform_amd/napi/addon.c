@@ -35,6 +35,12 @@
  *            vertex, sh}                      31-115)
  *   process(cols, names, actions, outNames,   processDataTable, one upload (process.ts:64-145)
  *           outSrc) -> TypedArray[]
+ *   compressedPlyFromFile(fd, actions)        readPly + processDataTable + writeCompressedPly's
+ *        -> {numRows, shCoeffs, chunk,        arrays, the rows resident in HBM (index.ts:463-496)
+ *            vertex, sh}
+ *   sogBundleFromFile(fd, actions, iters,     readPly + processDataTable + writeSog -> .sog bytes,
+ *        draws, dosTime, dosDate)             resident
+ *        -> {archive, used}
  */
 #include <node_api.h>
 #include <stdio.h>
@@ -386,6 +392,8 @@ static double prop_num(napi_env env, napi_value obj, const char *k) {
     return num(env, v);
 }
 
+static int parse_actions(napi_env env, napi_value actions, chain_args *a);
+
 static int chain_parse(napi_env env, napi_value cols, napi_value names, napi_value actions, chain_args *a) {
     memset(a, 0, sizeof *a);
     if (napi_get_array_length(env, cols, &a->m) != napi_ok || napi_get_array_length(env, actions, &a->na) != napi_ok) {
@@ -414,6 +422,11 @@ static int chain_parse(napi_env env, napi_value cols, napi_value names, napi_val
         }
     }
     a->names = str_list(env, names, a->m);
+    return parse_actions(env, actions, a);
+}
+
+/* the normalised action list into a->acts (a->na set by the caller) */
+static int parse_actions(napi_env env, napi_value actions, chain_args *a) {
     a->acts = (st_action *)calloc(a->na + 1, sizeof(st_action));
     a->acols = (char **)calloc(a->na + 1, sizeof(char *));
     for (uint32_t i = 0; i < a->na; ++i) {
@@ -494,6 +507,114 @@ static napi_value js_compressed_ply(napi_env env, napi_callback_info info) {
     return out;
 fail:
     free(chunk); free(vertex); free(sh);
+    chain_free(&a);
+    return NULL;
+}
+
+/* compressedPlyFromFile(fd, actions) -> {numRows, shCoeffs, chunk, vertex, sh}: readPly +
+ * processDataTable + writeCompressedPly's arrays, the rows resident in HBM (st_ply_compressed_ply) */
+static napi_value js_compressed_ply_file(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out = NULL;
+    chain_args a;
+    st_ctx *ctx;
+    st_ply_header *h = NULL;
+    float *chunk = NULL;
+    uint32_t *vertex = NULL;
+    uint8_t *sh = NULL;
+    memset(&a, 0, sizeof a);
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (napi_get_array_length(env, argv[1], &a.na) != napi_ok || !parse_actions(env, argv[1], &a)) goto fail;
+    if (!get_ctx(env, &ctx)) goto fail;
+    h = (st_ply_header *)calloc(1, sizeof *h);
+    {
+        const int32_t fd = (int32_t)num(env, argv[0]);
+        int rc = st_ply_read_header(fd, h), el = -1;
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        for (int e = 0; e < h->nelements && el < 0; ++e)
+            if (strcmp(h->elements[e].name, "vertex") == 0) el = e;
+        if (el < 0) {
+            napi_throw_error(env, NULL, "splat-hip: no vertex element");
+            goto fail;
+        }
+        const uint64_t n = h->elements[el].count;
+        chunk = (float *)malloc(((n + 255) / 256 * 18 + 1) * 4);
+        vertex = (uint32_t *)malloc((n * 4 + 1) * 4);
+        sh = (uint8_t *)malloc(n * 45 + 1);
+        uint64_t m = 0;
+        int32_t C = 0;
+        void *p;
+        napi_value tch, tvx, tsh;
+        rc = st_ply_compressed_ply(ctx, fd, h, el, a.acts, (int32_t)a.na, chunk, vertex, sh, &m, &C);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        const uint64_t nch = (m + 255) / 256;
+        if (!(tch = new_typed(env, napi_float32_array, nch * 18, 4, &p))) goto fail;
+        memcpy(p, chunk, nch * 18 * 4);
+        if (!(tvx = new_typed(env, napi_uint32_array, m * 4, 4, &p))) goto fail;
+        memcpy(p, vertex, m * 16);
+        if (!(tsh = new_typed(env, napi_uint8_array, m * 3 * (uint64_t)C, 1, &p))) goto fail;
+        memcpy(p, sh, m * 3 * (uint64_t)C);
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "numRows", make_num(env, (double)m));
+        set_named(env, out, "shCoeffs", make_num(env, C));
+        set_named(env, out, "chunk", tch);
+        set_named(env, out, "vertex", tvx);
+        set_named(env, out, "sh", tsh);
+    }
+    free(chunk); free(vertex); free(sh); free(h);
+    chain_free(&a);
+    return out;
+fail:
+    free(chunk); free(vertex); free(sh); free(h);
+    chain_free(&a);
+    return NULL;
+}
+
+/* sogBundleFromFile(fd, actions, iters, draws: Float64Array, dosTime, dosDate) -> {archive, used}:
+ * readPly + processDataTable + writeSog to .sog bytes, resident (st_ply_sog_bundle) */
+static napi_value js_sog_bundle_file(napi_env env, napi_callback_info info) {
+    size_t argc = 6, nd = 0;
+    napi_value argv[6], out = NULL, buf;
+    chain_args a;
+    st_ctx *ctx;
+    st_ply_header *h = NULL;
+    uint8_t *arch = NULL;
+    uint64_t size = 0, used = 0;
+    memset(&a, 0, sizeof a);
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (napi_get_array_length(env, argv[1], &a.na) != napi_ok || !parse_actions(env, argv[1], &a)) goto fail;
+    {
+        double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);
+        if (!draws || !get_ctx(env, &ctx)) goto fail;
+        h = (st_ply_header *)calloc(1, sizeof *h);
+        const int32_t fd = (int32_t)num(env, argv[0]);
+        int rc = st_ply_read_header(fd, h);
+        if (rc == ST_OK)
+            rc = st_ply_sog_bundle(ctx, fd, h, -1, a.acts, (int32_t)a.na, (int32_t)num(env, argv[2]), draws, nd, &used,
+                                   (uint16_t)num(env, argv[4]), (uint16_t)num(env, argv[5]), &arch, &size);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        void *p;
+        if (napi_create_buffer_copy(env, size, arch, &p, &buf) != napi_ok) goto fail;
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "archive", buf);
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    st_free(arch);
+    free(h);
+    chain_free(&a);
+    return out;
+fail:
+    st_free(arch);
+    free(h);
     chain_free(&a);
     return NULL;
 }
@@ -1108,6 +1229,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"readPly", js_read_ply},
                {"decompressPly", js_decompress_ply},
                {"compressedPly", js_compressed_ply},
+               {"compressedPlyFromFile", js_compressed_ply_file},
+               {"sogBundleFromFile", js_sog_bundle_file},
                {"process", js_process}};
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;

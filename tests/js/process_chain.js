@@ -40,6 +40,24 @@ const tableOf = c => new host.DataTable(man.meta[`${c}_in_columns`].map(n => new
         const w2 = [];
         await host.writeCompressedPly({ write: async (d) => { w2.push(Buffer.from(d.buffer, d.byteOffset, d.byteLength)); } }, res);
         r.writes2 = w2.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => w2[i].equals(bytes(arr(`${c}_${k}`))));
+        // the same from a PLY file of the input table (readPly + actions + writer in one call)
+        const dir = fs.mkdtempSync(path.join(require('os').tmpdir(), 'st_chain_'));
+        const names = man.meta[`${c}_in_columns`];
+        const n = arr(`${c}_in_${names[0]}`).length;
+        const header = Buffer.from(['ply', 'format binary_little_endian 1.0', `element vertex ${n}`]
+            .concat(names.map(nm => `property float ${nm}`), 'end_header\n').join('\n'), 'utf8');
+        const rows = Buffer.alloc(n * 4 * names.length);
+        const cols = names.map(nm => arr(`${c}_in_${nm}`));
+        for (let i = 0; i < n; ++i) for (let j = 0; j < names.length; ++j) rows.writeFloatLE(cols[j][i], (i * names.length + j) * 4);
+        fs.writeFileSync(path.join(dir, 'in.ply'), Buffer.concat([header, rows]));
+        const inH = await fs.promises.open(path.join(dir, 'in.ply'), 'r');
+        const w3 = [];
+        await host.compressPlyFile(inH, { write: async (d) => { w3.push(Buffer.from(d.buffer, d.byteOffset, d.byteLength)); } },
+            actionsOf(c));
+        await inH.close();
+        fs.unlinkSync(path.join(dir, 'in.ply'));
+        fs.rmdirSync(dir);
+        r.file = w3.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => w3[i].equals(bytes(arr(`${c}_${k}`))));
         out[c] = r;
     }
     console.log(JSON.stringify(out));

@@ -40,7 +40,7 @@ def test_addon_exports(addon_built):
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
                                        'filterNaN', 'combineLayout', 'setDevices', 'getDevices', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
-                                       'process'])
+                                       'process', 'compressedPlyFromFile', 'sogBundleFromFile'])
     assert ver == '1'
 
 
