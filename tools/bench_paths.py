@@ -120,7 +120,7 @@ def measure(ctx, stream, dev, n=10_000_000, reps=5):
     out['config3_one_call'] = {'ms': ms1, 'Msplats_per_s': n / (ms1 / 1e3) / 1e6,
                                'what': 'st_dev_compressed_ply (rotate 0,45,0 + filterNaN + Morton + chunk pack)'}
     host = [(k, v.cpu().numpy()) for k, v in items]
-    ctx.compressed_ply(host, acts)  # warm (workspace)
+    ref = ctx.compressed_ply(host, acts)  # warm (workspace)
     t0 = time.perf_counter()
     for _ in range(2):
         ctx.compressed_ply(host, acts)
@@ -128,7 +128,54 @@ def measure(ctx, stream, dev, n=10_000_000, reps=5):
     out['config3_host_one_call'] = {'ms': ms2, 'Msplats_per_s': n / (ms2 / 1e3) / 1e6,
                                     'what': 'st_compressed_ply from pageable host columns (62 x 4 B/splat up, '
                                             '16 + 45 B/splat + chunks down): the PCIe-inclusive rate of the Node path'}
+    out['config3_file'] = file_path(ctx, host, acts, ref)
     return out
+
+
+def file_path(ctx, host, acts, ref, reps=2):
+    """the CLI's `in.ply -r 0,45,0 --filterNaN out.compressed.ply` from the file in one resident
+    call (st_ply_compressed_ply: page cache -> pinned -> HBM, the chain, the packed arrays back),
+    plus writing the output file; the table written once as a binary PLY (untimed)"""
+    import tempfile
+
+    import numpy as np
+    n = len(host[0][1])
+    d = tempfile.mkdtemp(prefix='st_c3_', dir=os.environ.get('TMPDIR', '/tmp'))
+    src, dst = os.path.join(d, 'in.ply'), os.path.join(d, 'out.compressed.ply')
+    try:
+        head = ('ply\nformat binary_little_endian 1.0\n' + f'element vertex {n}\n' +
+                ''.join(f'property float {k}\n' for k, _ in host) + 'end_header\n').encode()
+        with open(src, 'wb') as f:
+            f.write(head)
+            step = 1 << 22
+            for a in range(0, n, step):
+                f.write(np.stack([v[a:a + step] for _, v in host], 1).tobytes())
+        times, calls, same = [], [], True
+        for r in range(reps + 1):  # rep 0 warms the page cache and the buffers
+            t0 = time.perf_counter()
+            m, chunk, vertex, shb = ctx.ply_compressed_ply(src, acts)
+            tc = time.perf_counter() - t0
+            with open(dst, 'wb') as f:
+                f.write(b'ply header\n')  # the header text is the host's (a few hundred bytes)
+                f.write(chunk.tobytes())
+                f.write(vertex.tobytes())
+                f.write(shb.tobytes())
+            if r:
+                times.append(time.perf_counter() - t0)
+                calls.append(tc)
+            same = same and m == ref[0] and all(np.array_equal(a.view(np.uint8), b.view(np.uint8))
+                                                for a, b in zip((chunk, vertex, shb), ref[1:]))
+        ms = sorted(times)[len(times) // 2] * 1e3
+        mc = sorted(calls)[len(calls) // 2] * 1e3
+        return {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'call_ms': mc, 'call_Msplats_per_s': n / mc / 1e3,
+                'ply_bytes': os.path.getsize(src),
+                'equals_host_one_call': same,
+                'what': 'st_ply_compressed_ply from a PLY file in the page cache + the output file written'}
+    finally:
+        for f in (src, dst):
+            if os.path.exists(f):
+                os.remove(f)
+        os.rmdir(d)
 
 
 if __name__ == '__main__':
