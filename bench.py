@@ -328,6 +328,39 @@ def ctypes_char_array(size):
     return ctypes.c_char * size
 
 
+def sog_stage_table(stages, n, iters, K=65536, D=45):
+    """writeSog's top-level stages (the stage-marked step) priced by their algorithmic work
+    (SURVEY 8d): HBM bytes per splat for the memory-bound ones, dot-product flops for the SH
+    palette k-means (whose sweep is MFMA-bound; its HBM bytes are listed too)"""
+    if not stages:
+        return None
+    cb = K * D  # values of the codebook cluster1d (the palette's centroid coordinates)
+    spec = {
+        'sog.morton': ('hbm', 92 * n, 'generateOrdering: extents 12 + keys 16 + 4 LSD passes on 8-B pairs 64 B/splat'),
+        'sog.means_quats': ('hbm', 40 * n, 'x, y, z, rot_0..3 read (28 B) + means_l/u, quats texels (12 B) per splat'),
+        'sog.scales': ('hbm', 15 * iters * n + 7 * n, 'cluster1d over 3 columns: 5 B per value-iteration '
+                       '(4 B read + 1 B label) x 3 values + the scales texels'),
+        'sog.sh0': ('hbm', 15 * iters * n + 11 * n, 'cluster1d of f_dc as sog.scales + opacity read + sh0 texels'),
+        'sog.shkmeans': ('mfma', 2.0 * n * K * D * iters, 'SH palette k-means: 2 n K D flop per iteration '
+                         '(the sweep); 184 B/splat/iter of HBM besides'),
+        'sog.shn': ('hbm', 5 * iters * cb + 8 * n, 'codebook cluster1d over K x D values + shN labels texels'),
+    }
+    out = {}
+    for k, (bound, work, what) in spec.items():
+        ms = stages.get(k)
+        if ms is None or ms <= 0:
+            continue
+        if bound == 'hbm':
+            gbs = work / (ms / 1e3) / 1e9
+            out[k] = {'ms': ms, 'bound': 'hbm', 'alg_bytes': work, 'achieved_GBps': gbs,
+                      'frac_hbm': gbs / (HBM_TBPS * 1e3), 'work': what}
+        else:
+            tf = work / (ms / 1e3) / 1e12
+            out[k] = {'ms': ms, 'bound': 'mfma', 'alg_flops': work, 'achieved_TFLOPs': tf,
+                      'frac_peak': tf / MFMA_F16_DENSE_TFLOPS, 'work': what}
+    return out
+
+
 def rank_tables(args, world, rank, dev):
     """this rank's input tables (device columns) and the workload's description"""
     if args.merge:
@@ -603,6 +636,7 @@ def main():
         'end_to_end_file': e2e,
         'paths_config3': paths,
         'stages_ms': stages,
+        'sog_stages': sog_stage_table(stages, n_local, args.iters),
         'kernels': kstats,
         'draws_used_per_step': used,
         'weak_10M_per_gpu': weak,

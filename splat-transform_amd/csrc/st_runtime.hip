@@ -114,13 +114,24 @@ static void end_timing(st_ctx *c) {
     if (!c->timing) return;
     mark(c, "end");
     ST_HIP(hipEventSynchronize(c->marks.back().ev));
+    // per name: the sum of its intervals (the time since the previous mark, over every time the
+    // stage ran: a k-means iteration marks each pass); "sog.*" names mark writeSog's top-level
+    // stages and take the interval since the previous "sog.*" mark, nested marks included
+    std::vector<std::string> order;
+    std::map<std::string, double> tot;
+    size_t top = 0;
+    for (size_t i = 1; i < c->marks.size(); ++i) {
+        const std::string &nm = c->marks[i].name;
+        const bool is_top = nm.compare(0, 4, "sog.") == 0;
+        float ms = 0;
+        ST_HIP(hipEventElapsedTime(&ms, c->marks[is_top ? top : i - 1].ev, c->marks[i].ev));
+        if (!tot.count(nm)) order.push_back(nm);
+        tot[nm] += ms;
+        if (is_top) top = i;
+    }
     std::ostringstream os;
     os << "{";
-    for (size_t i = 1; i < c->marks.size(); ++i) {
-        float ms = 0;
-        ST_HIP(hipEventElapsedTime(&ms, c->marks[i - 1].ev, c->marks[i].ev));
-        os << (i > 1 ? ", " : "") << "\"" << c->marks[i].name << "\": " << ms;
-    }
+    for (size_t i = 0; i < order.size(); ++i) os << (i ? ", " : "") << "\"" << order[i] << "\": " << tot[order[i]];
     os << "}";
     c->last_timings = os.str();
     if (getenv("ST_TIMING_PRINT")) fprintf(stderr, "[st timing] %s\n", c->last_timings.c_str());
