@@ -378,6 +378,16 @@ int st_group_sog(st_group *g, const st_table *const *tables, int32_t ntables, co
 int st_group_sog_bundle(st_group *g, const st_table *const *tables, int32_t ntables, const uint64_t *splits,
                         int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time,
                         uint16_t dos_date, uint8_t **out, uint64_t *out_size);
+/* the same with each input table's processDataTable actions (process.ts:64-145: the CLI's
+ * `a.ply [actions] b.ply [actions] out.sog`) applied on the GPUs to each rank's part of that
+ * input before writeSog: transform and the filters are row-local (the filtered
+ * parts concatenate to the filtered input; the shard offsets come from the all-gathered survivor
+ * counts); nactions[t] == 0 leaves table t as it is.  With one input its list may also carry the
+ * output's actions (combine of one table is the table, index.ts:158-160). */
+int st_group_sog_bundle_process(st_group *g, const st_table *const *tables, int32_t ntables, const uint64_t *splits,
+                                const st_action *const *actions, const int32_t *nactions, int32_t iters,
+                                const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time,
+                                uint16_t dos_date, uint8_t **out, uint64_t *out_size);
 
 /* ---- WebP lossless, CRC-32, the .sog container ---------------
  * WebP: a valid lossless VP8L stream (predictor transform + canonical prefix

@@ -26,7 +26,8 @@ struct Chain {
     st_ctx *c;
     uint64_t n = 0;
     std::vector<ChainCol> cols;
-    int gen = 0;  // workspace generation the next filter writes
+    int gen = 0;                  // workspace generation the next filter writes
+    std::string tag = "chain";    // workspace slot prefix (several chains alive at once)
 
     // views over the current columns (rebuilt on demand; pointers stay valid until the next change)
     std::vector<const char *> names;
@@ -68,7 +69,7 @@ struct Chain {
         const st_ttable *src = typed();
         std::vector<void *> dst(cols.size());
         for (size_t i = 0; i < cols.size(); ++i)
-            dst[i] = ws(c, "chain.g" + std::to_string(gen) + "." + std::to_string(i), m * type_size(cols[i].type) + 16);
+            dst[i] = ws(c, tag + ".g" + std::to_string(gen) + "." + std::to_string(i), m * type_size(cols[i].type) + 16);
         st_ttable d = *src;
         d.n = m;
         d.cols = dst.data();
@@ -106,7 +107,7 @@ void run_actions(Chain &ch, const st_action *actions, int nactions) {
             case ST_ACTION_FILTER_NAN:
             case ST_ACTION_FILTER_VALUE: {
                 if (ch.n == 0) break;
-                auto *idx = wsT<uint32_t>(ch.c, "chain.idx", ch.n);
+                auto *idx = wsT<uint32_t>(ch.c, ch.tag + ".idx", ch.n);
                 const uint64_t m = act.kind == ST_ACTION_FILTER_NAN
                                        ? filter_finite_tdev(ch.c, ch.typed(), idx)
                                        : filter_value_tdev(ch.c, ch.typed(), act.column, act.compare, act.value, idx);
@@ -205,6 +206,24 @@ const st_table *sog_view(Chain &ch) {
 }
 
 }  // namespace
+
+// processDataTable on a device float32 table (transforms in place, filters into workspace slots
+// under `tag`): the processed table's columns in `out`
+void chain_apply_f32(st_ctx *c, const st_table *in, const st_action *actions, int nactions, const std::string &tag,
+                     ProcessedF32 &out) {
+    Chain ch{c};
+    ch.tag = tag;
+    ch.n = in->n;
+    for (int i = 0; i < in->ncol; ++i) ch.cols.push_back(ChainCol{in->names[i], ST_PLY_FLOAT, in->cols[i]});
+    run_actions(ch, actions, nactions);
+    out.names.clear();
+    out.cn.clear();
+    out.cols.clear();
+    for (auto &k : ch.cols) out.names.push_back(k.name), out.cols.push_back(static_cast<float *>(k.ptr));
+    for (auto &nm : out.names) out.cn.push_back(nm.c_str());
+    out.t = st_table{ch.n, (int32_t)out.cols.size(), out.cn.data(), out.cols.data()};
+}
+
 }  // namespace st
 
 using namespace st;

@@ -232,6 +232,16 @@ uint32_t dist_finish(st_ctx *c, int d, int k, const double *sums, const double *
 void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npairs, const double *running,
                   const uint32_t *counts, float *cen);
 
+// processDataTable on a device float32 table (st_chain.hip)
+struct ProcessedF32 {
+    std::vector<std::string> names;
+    std::vector<const char *> cn;
+    std::vector<float *> cols;
+    st_table t{};
+};
+void chain_apply_f32(st_ctx *c, const st_table *in, const st_action *actions, int nactions, const std::string &tag,
+                     ProcessedF32 &out);
+
 // multi-GPU writeSog (st_multi.hip): the st_set_devices group (nullptr: one device)
 st_group *default_group();
 int apply_env_devices();  // ST_NUM_GPUS on first use; ST_OK or the error (st_last_error set)

@@ -552,12 +552,13 @@ LocalTable combine_local(st_ctx *c, Coll &co, const st_table *const *tabs, int n
 // writeSog's textures + meta (write-sog.ts:110-370) of the global table, on rank 0's device
 // (`out`/`meta` are read on rank 0 only).  Returns the draws consumed.
 uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab, int iters, const double *draws,
-                     uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out) {
+                     uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out, uint64_t *n_global = nullptr) {
     use_device(c);
     LocalTable L = combine_local(c, co, tabs, ntab);
     const st_table *t = &L.t;
     const Shard sh = make_shard(c, co, t->n);
     const uint64_t N = sh.N;
+    if (n_global) *n_global = N;
     ST_REQUIRE(N > 0, ST_ERR_ARG, "sog: empty table");
     ST_REQUIRE(N < (1ull << 31), ST_ERR_ARG, "sog: the table must have < 2^31 rows");
     const int C = L.C;
@@ -840,7 +841,9 @@ RankSlice upload_slice(st_ctx *c, const st_table *const *tabs, int ntab, uint64_
 // the group form of writeSog from host tables; textures on rank 0's device (dev_out) and,
 // if host_out, copied there
 static uint64_t group_sog(st_group *g, const st_table *const *tabs, int ntab, const uint64_t *splits, int iters,
-                          const double *draws, uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *dev_out) {
+                          const double *draws, uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *dev_out,
+                          const st_action *const *actions = nullptr, const int32_t *nactions = nullptr,
+                          uint64_t *n_out = nullptr) {
     uint64_t N = 0;
     for (int t = 0; t < ntab; ++t) N += tabs[t]->n;
     const int world = (int)g->ctx.size();
@@ -853,7 +856,18 @@ static uint64_t group_sog(st_group *g, const st_table *const *tabs, int ntab, co
         st_ctx *c = g->ctx[r];
         const uint64_t lo = splits ? splits[r] : N * r / world, hi = splits ? splits[r + 1] : N * (r + 1) / world;
         RankSlice s = upload_slice(c, tabs, ntab, lo, hi);
-        used[r] = sog_sharded(c, *g->coll[r], s.ptrs.data(), ntab, iters, draws, ndraws, meta, dev_out);
+        // each input's processDataTable actions on this rank's part of it: every action is row-local
+        // (transform) or order-preserving row selection (filters) or a renaming (filterBands against
+        // the input's own band, the same on every rank), so the parts concatenate to the processed input
+        std::vector<ProcessedF32> pr(actions ? ntab : 0);
+        for (int t = 0; t < ntab && actions; ++t) {
+            if (!nactions[t]) continue;
+            chain_apply_f32(c, s.ptrs[t], actions[t], nactions[t], "gp" + std::to_string(t), pr[t]);
+            s.ptrs[t] = &pr[t].t;
+        }
+        uint64_t nr = 0;
+        used[r] = sog_sharded(c, *g->coll[r], s.ptrs.data(), ntab, iters, draws, ndraws, meta, dev_out, &nr);
+        if (r == 0 && n_out) *n_out = nr;
     });
     for (int r = 1; r < world; ++r)
         ST_REQUIRE(used[r] == used[0], ST_ERR_INTERNAL, "multi-GPU: ranks consumed different draw counts");
@@ -984,6 +998,36 @@ int st_group_sog_bundle(st_group *g, const st_table *const *tables, int32_t ntab
         GroupTex dt = group_tex(g->ctx[0], N, union_coeffs(tables, ntables));
         st_sog_meta meta{};
         const uint64_t u = group_sog(g, tables, ntables, splits, iters, draws, ndraws, &meta, &dt.t);
+        st_ctx *c = g->ctx[0];
+        use_device(c);
+        const uint8_t *view;
+        uint64_t nb;
+        sog_bundle_dev(c, meta, N, dt.t, dos_time, dos_date, &view, &nb);
+        uint8_t *buf = (uint8_t *)std::malloc(nb);
+        ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
+        std::memcpy(buf, view, nb);
+        *out = buf;
+        *out_size = nb;
+        if (used) *used = u;
+    });
+}
+
+int st_group_sog_bundle_process(st_group *g, const st_table *const *tables, int32_t ntables, const uint64_t *splits,
+                                const st_action *const *actions, const int32_t *nactions, int32_t iters,
+                                const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time,
+                                uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
+    return guarded_m([&] {
+        ST_REQUIRE(g && tables && ntables >= 1 && out && out_size && actions && nactions, ST_ERR_ARG, "NULL argument");
+        for (int t = 0; t < ntables; ++t) ST_REQUIRE(nactions[t] == 0 || actions[t], ST_ERR_ARG, "NULL action list");
+        uint64_t N0 = 0;
+        for (int t = 0; t < ntables; ++t) N0 += tables[t]->n;
+        // textures for the unprocessed row count and band: filters only shrink the table and
+        // filterBands only lowers the band, so these hold the processed table's
+        GroupTex dt = group_tex(g->ctx[0], N0, 15);
+        st_sog_meta meta{};
+        uint64_t N = 0;
+        const uint64_t u = group_sog(g, tables, ntables, splits, iters, draws, ndraws, &meta, &dt.t, actions, nactions,
+                                     &N);
         st_ctx *c = g->ctx[0];
         use_device(c);
         const uint8_t *view;

@@ -113,6 +113,7 @@ EXPORTS = [
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
+    'st_group_sog_bundle_process',
 ]
 
 
@@ -314,6 +315,23 @@ class Group:
                                         _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used),
                                         ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
                                         ctypes.byref(size)))
+        return _take(out, size), used.value
+
+
+    def sog_bundle_process(self, tables, actions, iters, draws, dos_time, dos_date, splits=None):
+        """writeSog -> .sog bytes of the combine of `tables` after each table's processDataTable
+        `actions` (one list per table) ran on the ranks' parts (st_group_sog_bundle_process)"""
+        ts, arr = _tables_arg(tables)
+        acts = [make_actions(a) for a in actions]
+        aptr = (ctypes.POINTER(Action) * len(ts))(*[ctypes.cast(a, ctypes.POINTER(Action)) for a in acts])
+        nact = (ctypes.c_int32 * len(ts))(*[len(a) for a in actions])
+        sp = (ctypes.c_uint64 * (self.world + 1))(*splits) if splits is not None else None
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        used = ctypes.c_uint64()
+        check(lib().st_group_sog_bundle_process(self.h, arr, ctypes.c_int32(len(ts)), sp, aptr, nact,
+                                                ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)),
+                                                ctypes.byref(used), ctypes.c_uint16(dos_time),
+                                                ctypes.c_uint16(dos_date), ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size), used.value
 
 

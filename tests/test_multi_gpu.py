@@ -157,3 +157,29 @@ def test_st_num_gpus_env():
                            env=dict(os.environ, ST_NUM_GPUS=value))
         assert r.returncode == 0, r.stderr
         assert r.stdout.strip() == want, (value, r.stdout)
+
+
+@pytest.mark.parametrize('world,splits', [(2, None), (3, [0, 5_000, 5_001, 23_345])])
+def test_group_bundle_with_input_actions_equals_single_device(ctx, world, splits):
+    """`a.ply -r 0,45,0 --filterNaN b.ply -s 2 --filterByValue opacity,gt,0 --filterBands 1 out.sog` on
+    `world` ranks: each input's actions run on the ranks' parts of it (transform / filters sharded,
+    SURVEY 8e row 1), then combine + writeSog; the .sog bytes equal processDataTable per input ->
+    combine -> writeSog on one device"""
+    a, b = _table(11_000, 21), _table(12_345, 22)
+    for k, r in (('x', 3), ('f_rest_7', 4_000), ('opacity', 10_999)):
+        a[k][r] = np.nan
+    b['opacity'][5] = np.nan  # filterByValue opacity > 0 drops it (NaN compares false)
+    acts = [[{'kind': 'rotate', 'value': (0, 45, 0)}, {'kind': 'filterNaN'}],
+            [{'kind': 'scale', 'value': 2.0}, {'kind': 'filterByValue', 'columnName': 'opacity', 'comparator': 'gt',
+                                               'value': 0.0}, {'kind': 'filterBands', 'value': 1}]]
+    draws = np.random.default_rng(13).random(1 << 18)
+    pa = ctx.process(list(a.items()), acts[0])
+    pb = ctx.process(list(b.items()), acts[1])
+    combined = dict(oracle.combine([pa, pb]))
+    want, wused = ctx.sog_bundle(combined, 2, draws, 0x6000, 0x5a21)
+    g = sh.Group([0] * world, host_staged=True)
+    try:
+        got, used = g.sog_bundle_process([a, b], acts, 2, draws, 0x6000, 0x5a21, splits)
+    finally:
+        g.close()
+    assert used == wused and got == want
