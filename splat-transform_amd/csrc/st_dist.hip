@@ -217,12 +217,16 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
     int bits = 1;
     while ((1ull << bits) < nk) ++bits;
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans partials: n must be < 2^31 per device");
-    hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
-                       (uint32_t)(n / nseg), k,
-                       d == 1 ? cols[0] : (const float *)nullptr, keys, payload);
-    ST_LAUNCH_CHECK();
-    radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
-    bounds_from_sorted(c, keys, n, (int)nk, start);
+    if (d == 1 && k <= 256) {
+        // stable by label inside each (contiguous) segment: one value-only counting pass per segment
+        seg_label_sort1d(c, cols[0], labels, n, nseg, k, payload, start);
+    } else {
+        hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                           (uint32_t)(n / nseg), k, d == 1 ? cols[0] : (const float *)nullptr, keys, payload);
+        ST_LAUNCH_CHECK();
+        radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
+        bounds_from_sorted(c, keys, n, (int)nk, start);
+    }
     if (d == 1) {
         partials1d(c, payload, n, start, (int)nk, sums, sabs, emin, counts);
     } else {

@@ -70,6 +70,8 @@ bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, 
 // cluster) partials of the label-sorted value bits (nk = nseg * k ranges of start), and the
 // exact replay of the pending clusters' sums over one segment (start: that segment's k + 1
 // bounds) from their running values; pflag[p] = 1 where the sequential chain must finish
+void seg_label_sort1d(st_ctx *c, const float *pts, const uint32_t *labels, uint64_t n, int nseg, int k,
+                      uint32_t *vals, uint32_t *start);
 void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int nk, double *sums, double *sabs,
                 int32_t *emin, uint32_t *counts);
 void seqsum1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int k, const uint32_t *pairs,

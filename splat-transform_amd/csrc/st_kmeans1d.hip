@@ -281,7 +281,8 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_hist(const float *__restric
 // stable counting-sort pass on the byte labels moving the value bits only: each wave ranks its
 // 1,024 points with ballots over the `bits` label bits, the tile is reordered by label in LDS
 // and each label's run is stored contiguously at its scanned offset
-__global__ __launch_bounds__(F1_T) void k_lab_scatter(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
+template <typename L>
+__global__ __launch_bounds__(F1_T) void k_lab_scatter(const L *__restrict__ lab8, const float *__restrict__ pts,
                                                       uint64_t n, int bits, const uint32_t *__restrict__ offs,
                                                       uint32_t ntiles, uint32_t *__restrict__ ovals) {
     __shared__ uint32_t wcount[F1_WAVES][256];
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(F1_T) void k_lab_scatter(const uint8_t *__restrict_
     for (int r = 0; r < F1_ROWS; ++r) {
         const uint64_t e = wb + (uint64_t)r * 64 + lane;
         const bool valid = e < n;
-        dg[r] = valid ? lab8[e] : 0u;
+        dg[r] = valid ? (uint32_t)lab8[e] : 0u;
         v[r] = valid ? __builtin_bit_cast(uint32_t, pts[e]) : 0u;
     }
 #pragma unroll
@@ -362,11 +363,28 @@ __global__ __launch_bounds__(F1_T) void k_lab_scatter(const uint8_t *__restrict_
     }
 }
 
-// cluster starts from the scanned (digit, tile) counts: start[c] = offs[c * ntiles], start[k] = n
+// cluster starts from the scanned (digit, tile) counts: start[c] = base + offs[c * ntiles],
+// start[k] = base + n
 __global__ void k_f1_starts(const uint32_t *__restrict__ offs, uint32_t ntiles, int k, uint64_t n,
-                            uint32_t *__restrict__ start) {
+                            uint32_t *__restrict__ start, uint32_t base = 0) {
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c <= k; c += gridDim.x * blockDim.x)
-        start[c] = c < k ? offs[(uint64_t)c * ntiles] : (uint32_t)n;
+        start[c] = base + (c < k ? offs[(uint64_t)c * ntiles] : (uint32_t)n);
+}
+
+// tile histogram of given u32 labels (< 256): hist[d * ntiles + tile]
+__global__ __launch_bounds__(F1_T) void k_lab_hist(const uint32_t *__restrict__ labels, uint64_t n,
+                                                   uint32_t *__restrict__ hist, uint32_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * F1_TILE;
+#pragma unroll 4
+    for (int r = 0; r < F1_ROWS; ++r) {
+        const uint64_t i = base + (uint64_t)r * F1_T + threadIdx.x;
+        if (i < n) atomicAdd(&h[labels[i] & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
 // pairs for the member sort: key = label, val = value bits (ascending point order kept)
@@ -996,8 +1014,8 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             }
             mark(c, "k1.assign");
             scan_u32(c, fhist, fhist, (uint64_t)256 * ntiles, nullptr);
-            hipLaunchKernelGGL(k_lab_scatter, dim3(ntiles), dim3(F1_T), 0, c->stream, lab8, pts, n, kbits, fhist,
-                               ntiles, vals);
+            hipLaunchKernelGGL(k_lab_scatter<uint8_t>, dim3(ntiles), dim3(F1_T), 0, c->stream, lab8, pts, n, kbits,
+                               fhist, ntiles, vals);
             hipLaunchKernelGGL(k_f1_starts, dim3(grid_for((uint64_t)k + 1, 256, 256)), dim3(256), 0, c->stream,
                                fhist, ntiles, k, n, start);
             ST_LAUNCH_CHECK();
@@ -1061,6 +1079,32 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         }
         reseed_empty(c, dcols, 1, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "k1.update");
+    }
+}
+
+// the sharded 1-D member order: a stable sort by (segment, label) is a stable sort by label inside
+// each segment (segments are contiguous point ranges), done as one counting-sort pass per segment
+// that moves value bits only; start[s * k + c] = first position of (s, c), start[nseg * k] = n
+void seg_label_sort1d(st_ctx *c, const float *pts, const uint32_t *labels, uint64_t n, int nseg, int k,
+                      uint32_t *vals, uint32_t *start) {
+    const uint64_t ns = n / (uint64_t)nseg;
+    int kbits = 1;
+    while ((1 << kbits) < k) ++kbits;
+    const uint32_t ntiles = (uint32_t)((ns + F1_TILE - 1) / F1_TILE);
+    auto *hist = wsT<uint32_t>(c, "k1.shist", (size_t)256 * (ntiles ? ntiles : 1));
+    for (int sg = 0; sg < nseg; ++sg) {
+        const uint64_t o = (uint64_t)sg * ns;
+        if (ns) {
+            hipLaunchKernelGGL(k_lab_hist, dim3(ntiles), dim3(F1_T), 0, c->stream, labels + o, ns, hist, ntiles);
+            scan_u32(c, hist, hist, (uint64_t)256 * ntiles, nullptr);
+            hipLaunchKernelGGL(k_lab_scatter<uint32_t>, dim3(ntiles), dim3(F1_T), 0, c->stream, labels + o, pts + o, ns,
+                               kbits, hist, ntiles, vals + o);
+            hipLaunchKernelGGL(k_f1_starts, dim3(grid_for((uint64_t)k + 1, 256, 256)), dim3(256), 0, c->stream, hist,
+                               ntiles, k, ns, start + (uint64_t)sg * k, (uint32_t)o);
+        } else {
+            ST_HIP(hipMemsetD32Async(start + (uint64_t)sg * k, (uint32_t)o, (size_t)k + 1, c->stream));
+        }
+        ST_LAUNCH_CHECK();
     }
 }
 
