@@ -60,11 +60,11 @@ def test_morton_ragged_vs_oracle(ctx, n):
 
 @pytest.mark.parametrize('case', ['all_equal', 'nan_coords', 'inf_extent', 'one_axis_flat', 'big_equal_run',
                                   'neg_zero'])
-def test_morton_degenerate_vs_oracle(ctx, case):
+@pytest.mark.parametrize('n', [5000, 70001])
+def test_morton_degenerate_vs_oracle(ctx, case, n):
     """ordering.ts:53-65: zero-length extents, non-finite extents (ordering skipped), NaN
     coordinates (key 0), equal-key runs longer than 256 (recursion with their own extents)."""
     rng = np.random.default_rng(7)
-    n = 5000
     x, y, z = (rng.normal(0, 5, n).astype(np.float32) for _ in range(3))
     if case == 'all_equal':
         x[:], y[:], z[:] = 1.5, -2.0, 3.25
@@ -83,6 +83,21 @@ def test_morton_degenerate_vs_oracle(ctx, case):
     elif case == 'neg_zero':
         x[::2] = -0.0
         x[1::2] = 0.0
+    same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
+
+
+@pytest.mark.parametrize('n', [65535, 65536, 65537, 4096 * 25 + 1, 4096 * 37, 1_500_007])
+def test_morton_onesweep_sizes_vs_oracle(ctx, n):
+    """Level-0 sorts of whole and ragged 4,096-key tiles, and a caller-supplied permutation of
+    the indices (the values carried through the passes are idx[j]: ordering.ts:4-20 sorts the
+    indices it is given)."""
+    rng = np.random.default_rng(n)
+    x, y, z = (rng.normal(0, 10, n).astype(np.float32) for _ in range(3))
+    m = rng.random(n) < 0.05
+    for a in (x, y, z):
+        a[m] = (2 + rng.random(m.sum()) * 1e-3).astype(np.float32)
+    perm = rng.permutation(n).astype(np.uint32)
+    same_bits(ctx.morton_order(x, y, z, perm), oracle.morton_order(x, y, z, perm))
     same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
 
 
