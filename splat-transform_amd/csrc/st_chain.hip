@@ -171,12 +171,14 @@ void check_src(const st_ttable *src) {
 // upload the host table once
 void upload_chain(st_ctx *c, const st_ttable *src, Chain &ch) {
     ch.n = src->n;
+    std::vector<HostXfer> up;
     for (int i = 0; i < src->ncol; ++i) {
         const int sz = type_size(src->types[i]);
         void *d = ws(c, "chain.in." + std::to_string(i), src->n * sz + 16);
-        if (src->n) ST_HIP(hipMemcpyAsync(d, src->cols[i], src->n * sz, hipMemcpyHostToDevice, c->stream));
+        up.push_back(HostXfer{src->cols[i], d, src->n * sz});
         ch.cols.push_back(ChainCol{src->names[i], src->types[i], d});
     }
+    staged_h2d(c, up);
 }
 
 // the element's rows straight from the file into HBM columns (page cache -> pinned -> HBM,
@@ -245,11 +247,10 @@ int st_process(st_ctx *c, const st_ttable *src, const st_action *actions, int32_
                 if (ch.cols[i].name == dst->names[j] && ch.cols[i].type == dst->types[j]) from[j] = (int)i;
             ST_REQUIRE(from[j] >= 0, ST_ERR_ARG, std::string("process: result has no column ") + dst->names[j]);
         }
+        std::vector<HostXfer> down;
         for (int j = 0; j < dst->ncol; ++j)
-            if (ch.n)
-                ST_HIP(hipMemcpyAsync(dst->cols[j], ch.cols[from[j]].ptr, ch.n * type_size(dst->types[j]),
-                                      hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+            down.push_back(HostXfer{dst->cols[j], ch.cols[from[j]].ptr, ch.n * type_size(dst->types[j])});
+        staged_d2h(c, down);
         *out_m = ch.n;
     });
 }
@@ -272,12 +273,13 @@ int st_compressed_ply(st_ctx *c, const st_ttable *src, const st_action *actions,
         int32_t C = 0;
         compressed_tail(ch, dchunk, dvert, dsh, &C);
         ST_REQUIRE(C == 0 || m == 0 || sh, ST_ERR_ARG, "compressed_ply: sh output is NULL");
+        std::vector<HostXfer> down;
         if (m) {
-            ST_HIP(hipMemcpyAsync(chunk, dchunk, nch * 18 * 4, hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipMemcpyAsync(vertex, dvert, m * 16, hipMemcpyDeviceToHost, c->stream));
-            if (C) ST_HIP(hipMemcpyAsync(sh, dsh, m * 3 * (uint64_t)C, hipMemcpyDeviceToHost, c->stream));
+            down.push_back(HostXfer{chunk, dchunk, nch * 18 * 4});
+            down.push_back(HostXfer{vertex, dvert, m * 16});
+            if (C) down.push_back(HostXfer{sh, dsh, m * 3 * (uint64_t)C});
         }
-        ST_HIP(hipStreamSynchronize(c->stream));
+        staged_d2h(c, down);
         *out_m = m;
         *out_sh_coeffs = C;
     });
@@ -320,12 +322,13 @@ int st_ply_compressed_ply(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t
         int32_t C = 0;
         compressed_tail(ch, dchunk, dvert, dsh, &C);
         ST_REQUIRE(C == 0 || m == 0 || sh, ST_ERR_ARG, "compressed_ply: sh output is NULL");
+        std::vector<HostXfer> down;
         if (m) {
-            ST_HIP(hipMemcpyAsync(chunk, dchunk, nch * 18 * 4, hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipMemcpyAsync(vertex, dvert, m * 16, hipMemcpyDeviceToHost, c->stream));
-            if (C) ST_HIP(hipMemcpyAsync(sh, dsh, m * 3 * (uint64_t)C, hipMemcpyDeviceToHost, c->stream));
+            down.push_back(HostXfer{chunk, dchunk, nch * 18 * 4});
+            down.push_back(HostXfer{vertex, dvert, m * 16});
+            if (C) down.push_back(HostXfer{sh, dsh, m * 3 * (uint64_t)C});
         }
-        ST_HIP(hipStreamSynchronize(c->stream));
+        staged_d2h(c, down);
         *out_m = m;
         *out_sh_coeffs = C;
     });
@@ -348,13 +351,13 @@ int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t ele
         run_actions(ch, actions, nactions);
         const st_table *t = sog_view(ch);
         if (default_group()) {
+            std::vector<HostXfer> down;
             for (int i = 0; i < t->ncol; ++i) {
                 host.emplace_back(t->n);
                 hnames.push_back(t->names[i]);
-                if (t->n)
-                    ST_HIP(hipMemcpyAsync(host.back().data(), t->cols[i], t->n * 4, hipMemcpyDeviceToHost, c->stream));
+                down.push_back(HostXfer{host.back().data(), t->cols[i], t->n * 4});
             }
-            ST_HIP(hipStreamSynchronize(c->stream));
+            staged_d2h(c, down);
             for (size_t i = 0; i < host.size(); ++i) hcols.push_back(host[i].data()), hcn.push_back(hnames[i].c_str());
             ht = st_table{t->n, t->ncol, hcn.data(), hcols.data()};
             return;

@@ -18,6 +18,28 @@ struct DevTable {
     st_table t{};
 };
 
+// host <-> device transfers of one call, moved together through the staged copies
+struct Batch {
+    st_ctx *c;
+    std::vector<HostXfer> v;
+    template <typename T>
+    void add(const T *host, T *dev, size_t count) {
+        v.push_back(HostXfer{const_cast<T *>(host), dev, count * sizeof(T)});
+    }
+    template <typename T>
+    void add_d2h(T *host, const T *dev, size_t count) {
+        v.push_back(HostXfer{host, const_cast<T *>(dev), count * sizeof(T)});
+    }
+    void h2d() {
+        staged_h2d(c, v);
+        v.clear();
+    }
+    void d2h() {
+        staged_d2h(c, v);
+        v.clear();
+    }
+};
+
 // upload the named subset (or all columns when `want` is empty) of a host table
 DevTable upload(st_ctx *c, const st_table *h, const std::vector<std::string> &want, const std::string &tag) {
     DevTable d;
@@ -29,12 +51,14 @@ DevTable upload(st_ctx *c, const st_table *h, const std::vector<std::string> &wa
         }
         d.names.push_back(h->names[i]);
     }
+    Batch up{c};
     for (size_t i = 0; i < d.names.size(); ++i) {
         const int src = find_col(h, d.names[i].c_str());
         float *p = wsT<float>(c, tag + std::to_string(i), h->n);
-        if (h->n) ST_HIP(hipMemcpyAsync(p, h->cols[src], h->n * 4, hipMemcpyHostToDevice, c->stream));
+        up.add(h->cols[src], p, h->n);
         d.cols.push_back(p);
     }
+    up.h2d();
     for (auto &s : d.names) d.cnames.push_back(s.c_str());
     d.t.n = h->n;
     d.t.ncol = (int32_t)d.names.size();
@@ -44,11 +68,12 @@ DevTable upload(st_ctx *c, const st_table *h, const std::vector<std::string> &wa
 }
 
 void download(st_ctx *c, const DevTable &d, const st_table *h) {
+    Batch down{c};
     for (size_t i = 0; i < d.names.size(); ++i) {
         const int dst = find_col(h, d.names[i].c_str());
-        if (h->n) ST_HIP(hipMemcpyAsync(h->cols[dst], d.cols[i], h->n * 4, hipMemcpyDeviceToHost, c->stream));
+        down.add_d2h(h->cols[dst], d.cols[i], h->n);
     }
-    ST_HIP(hipStreamSynchronize(c->stream));
+    down.d2h();
 }
 
 std::vector<std::string> transform_columns() {
@@ -57,16 +82,12 @@ std::vector<std::string> transform_columns() {
     return v;
 }
 
+// a workspace slot that receives `count` host elements with the batch's next h2d()
 template <typename T>
-T *to_dev(st_ctx *c, const std::string &slot, const T *h, size_t count) {
-    T *d = wsT<T>(c, slot, count);
-    if (count) ST_HIP(hipMemcpyAsync(d, h, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+T *to_dev(Batch &b, const std::string &slot, const T *h, size_t count) {
+    T *d = wsT<T>(b.c, slot, count);
+    b.add(h, d, count);
     return d;
-}
-
-template <typename T>
-void to_host(st_ctx *c, T *h, const T *d, size_t count) {
-    if (count) ST_HIP(hipMemcpyAsync(h, d, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
 }
 
 }  // namespace
@@ -109,8 +130,9 @@ int st_filter_finite(st_ctx *c, const st_table *t, uint32_t *out_idx, uint64_t *
         DevTable d = upload(c, t, {}, "h.f");
         auto *didx = wsT<uint32_t>(c, "h.fidx", t->n);
         const uint64_t m = filter_finite_dev(c, &d.t, didx);
-        to_host(c, out_idx, didx, m);
-        ST_HIP(hipStreamSynchronize(c->stream));
+        Batch b{c};
+        b.add_d2h(out_idx, didx, m);
+        b.d2h();
         *out_n = m;
     });
 }
@@ -122,12 +144,14 @@ int st_filter_nan(st_ctx *c, const st_ttable *src, const st_ttable *dst, uint64_
         use_device(c);
         const uint64_t n = src->n;
         std::vector<void *> dcols(src->ncol), ocols(src->ncol);
+        Batch b{c};
         for (int i = 0; i < src->ncol; ++i) {
             const int sz = type_size(src->types[i]);
             ST_ARGH(sz > 0 && dst->types[i] == src->types[i], "filter_nan: bad or mismatched column type");
             dcols[i] = ws(c, "h.fn" + std::to_string(i), n * sz + 16);
-            if (n) ST_HIP(hipMemcpyAsync(dcols[i], src->cols[i], n * sz, hipMemcpyHostToDevice, c->stream));
+            b.add(static_cast<const char *>(src->cols[i]), static_cast<char *>(dcols[i]), n * sz);
         }
+        b.h2d();
         st_ttable d = *src;
         d.cols = dcols.data();
         auto *didx = wsT<uint32_t>(c, "h.fnidx", n);
@@ -138,9 +162,9 @@ int st_filter_nan(st_ctx *c, const st_ttable *src, const st_ttable *dst, uint64_
         o.cols = ocols.data();
         permute_rows_tdev(c, &d, didx, m, &o);
         for (int i = 0; i < src->ncol; ++i)
-            if (m) ST_HIP(hipMemcpyAsync(dst->cols[i], ocols[i], m * type_size(src->types[i]), hipMemcpyDeviceToHost,
-                                         c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+            b.add_d2h(static_cast<char *>(dst->cols[i]), static_cast<const char *>(ocols[i]),
+                      m * type_size(src->types[i]));
+        b.d2h();
         *out_m = m;
     });
 }
@@ -150,11 +174,13 @@ int st_morton_order(st_ctx *c, const float *x, const float *y, const float *z, u
         ST_ARGH(c && ((x && y && z && idx) || n == 0), "NULL argument");
         if (n == 0) return;
         use_device(c);
-        float *dx = to_dev(c, "h.mx", x, n), *dy = to_dev(c, "h.my", y, n), *dz = to_dev(c, "h.mz", z, n);
-        uint32_t *di = to_dev(c, "h.mi", idx, n);
+        Batch b{c};
+        float *dx = to_dev(b, "h.mx", x, n), *dy = to_dev(b, "h.my", y, n), *dz = to_dev(b, "h.mz", z, n);
+        uint32_t *di = to_dev(b, "h.mi", idx, n);
+        b.h2d();
         morton_order_dev(c, dx, dy, dz, di, n);
-        to_host(c, idx, di, n);
-        ST_HIP(hipStreamSynchronize(c->stream));
+        b.add_d2h(idx, di, n);
+        b.d2h();
     });
 }
 
@@ -167,15 +193,17 @@ int st_pack_compressed(st_ctx *c, const st_table *t, const uint32_t *order, floa
         DevTable d = upload(c, t, {}, "h.c");
         const uint64_t n = t->n, nch = (n + 255) / 256;
         const int nsh = 3 * sh_coeffs_of(t);
-        uint32_t *dord = to_dev(c, "h.cord", order, n);
+        Batch b{c};
+        uint32_t *dord = to_dev(b, "h.cord", order, n);
+        b.h2d();
         auto *dchunk = wsT<float>(c, "h.cchunk", nch * 18);
         auto *dvert = wsT<uint32_t>(c, "h.cvert", n * 4);
         auto *dsh = wsT<uint8_t>(c, "h.csh", n * (uint64_t)nsh + 1);
         pack_compressed_dev(c, &d.t, dord, dchunk, dvert, dsh);
-        to_host(c, chunk, dchunk, nch * 18);
-        to_host(c, vertex, dvert, n * 4);
-        if (nsh) to_host(c, sh, dsh, n * (uint64_t)nsh);
-        ST_HIP(hipStreamSynchronize(c->stream));
+        b.add_d2h(chunk, dchunk, nch * 18);
+        b.add_d2h(vertex, dvert, n * 4);
+        if (nsh) b.add_d2h(sh, dsh, n * (uint64_t)nsh);
+        b.d2h();
     });
 }
 
@@ -185,14 +213,16 @@ int st_kmeans(st_ctx *c, const float *const *cols, int32_t d, uint64_t n, int32_
         ST_ARGH(c && cols && d > 0 && k > 0 && centroids && labels, "bad argument");
         use_device(c);
         std::vector<const float *> dc(d);
-        for (int j = 0; j < d; ++j) dc[j] = to_dev(c, "h.k" + std::to_string(j), cols[j], n);
+        Batch b{c};
+        for (int j = 0; j < d; ++j) dc[j] = to_dev(b, "h.k" + std::to_string(j), cols[j], n);
+        b.h2d();
         const uint64_t kk = n < (uint64_t)k ? n : (uint64_t)k;
         auto *dcen = wsT<float>(c, "h.kcen", (size_t)d * (k > (int)kk ? k : kk));
         auto *dlab = wsT<uint32_t>(c, "h.klab", n);
         const uint64_t u = kmeans_dev(c, dc.data(), d, n, k, iters, draws, ndraws, dcen, dlab);
-        to_host(c, centroids, dcen, (size_t)d * kk);
-        to_host(c, labels, dlab, n);
-        ST_HIP(hipStreamSynchronize(c->stream));
+        b.add_d2h(centroids, dcen, (size_t)d * kk);
+        b.add_d2h(labels, dlab, n);
+        b.d2h();
         if (used) *used = u;
     });
 }
@@ -203,13 +233,15 @@ int st_cluster1d(st_ctx *c, const float *const *cols, int32_t ncols, uint64_t n,
         ST_ARGH(c && cols && ncols > 0 && centroids256 && labels, "bad argument");
         use_device(c);
         std::vector<const float *> dc(ncols);
-        for (int j = 0; j < ncols; ++j) dc[j] = to_dev(c, "h.1d" + std::to_string(j), cols[j], n);
+        Batch b{c};
+        for (int j = 0; j < ncols; ++j) dc[j] = to_dev(b, "h.1d" + std::to_string(j), cols[j], n);
+        b.h2d();
         auto *dcen = wsT<float>(c, "h.1dcen", 256);
         auto *dlab = wsT<uint8_t>(c, "h.1dlab", n * (uint64_t)ncols);
         const uint64_t u = cluster1d_dev(c, dc.data(), ncols, n, iters, draws, ndraws, dcen, dlab);
-        to_host(c, centroids256, dcen, 256);
-        to_host(c, labels, dlab, n * (uint64_t)ncols);
-        ST_HIP(hipStreamSynchronize(c->stream));
+        b.add_d2h(centroids256, dcen, 256);
+        b.add_d2h(labels, dlab, n * (uint64_t)ncols);
+        b.d2h();
         if (used) *used = u;
     });
 }
@@ -237,17 +269,18 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
             dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
         }
         const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, meta, &dt);
-        to_host(c, out->means_l, dt.means_l, tex);
-        to_host(c, out->means_u, dt.means_u, tex);
-        to_host(c, out->quats, dt.quats, tex);
-        to_host(c, out->scales, dt.scales, tex);
-        to_host(c, out->sh0, dt.sh0, tex);
+        Batch b{c};
+        b.add_d2h(out->means_l, dt.means_l, tex);
+        b.add_d2h(out->means_u, dt.means_u, tex);
+        b.add_d2h(out->quats, dt.quats, tex);
+        b.add_d2h(out->scales, dt.scales, tex);
+        b.add_d2h(out->sh0, dt.sh0, tex);
         if (C) {
             ST_ARGH(out->shn_labels && out->shn_centroids, "sog: shN outputs are NULL");
-            to_host(c, out->shn_labels, dt.shn_labels, tex);
-            to_host(c, out->shn_centroids, dt.shn_centroids, (uint64_t)cw * chh * 4);
+            b.add_d2h(out->shn_labels, dt.shn_labels, tex);
+            b.add_d2h(out->shn_centroids, dt.shn_centroids, (uint64_t)cw * chh * 4);
         }
-        ST_HIP(hipStreamSynchronize(c->stream));
+        b.d2h();
         if (used) *used = u;
     });
 }

@@ -98,6 +98,11 @@ struct st_ctx {
     // pinned host chunks of the PLY reader
     void *io = nullptr;
     size_t io_bytes = 0;
+    // staged host <-> device copies of pageable buffers (staged_h2d / staged_d2h): pinned
+    // slots, their events and the host threads that fill / drain them
+    void *xfer = nullptr;
+    hipEvent_t xfer_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    void *xfer_pool = nullptr;
     std::vector<st::StageTimer> marks;
     bool timing = false;
     std::string last_timings = "{}";
@@ -127,6 +132,17 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
 void *archive_buf(st_ctx *c, size_t bytes);  // host pinned archive buffer (reused, grow-only)
 void *io_buf(st_ctx *c, size_t bytes);       // host pinned file-chunk buffer (reused, grow-only)
+// copies between pageable host buffers and HBM for the one-call host forms: the bytes move
+// through pinned slots that several host threads fill (drain) while the DMA engine moves the
+// previous slot, instead of the runtime's single-threaded pageable staging.  Stream-ordered on
+// c->stream; both return when every byte has arrived (the host buffers may be reused).
+struct HostXfer {
+    void *host;
+    void *dev;
+    size_t bytes;
+};
+void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs);
+void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs);
 void use_device(st_ctx *c);
 void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
 

@@ -435,11 +435,10 @@ int st_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, 
         for (int p = 0; p < el.nprops; ++p)
             dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * type_size(el.props[p].type) + 8);
         ply_read_dev(c, fd, *h, element, dcols.data());
+        std::vector<HostXfer> down;
         for (int p = 0; p < el.nprops; ++p)
-            if (el.count)
-                ST_HIP(hipMemcpyAsync(host_cols[p], dcols[p], el.count * type_size(el.props[p].type),
-                                      hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+            down.push_back(HostXfer{host_cols[p], dcols[p], el.count * type_size(el.props[p].type)});
+        staged_d2h(c, down);
     });
 }
 
@@ -464,26 +463,28 @@ int st_decompress_ply(st_ctx *c, uint64_t n, const float *const *chunk, const ui
         std::vector<const uint32_t *> dvert(4);
         std::vector<const uint8_t *> dsh(nsh);
         std::vector<float *> dout(14 + nsh);
+        std::vector<HostXfer> up;
         for (int k = 0; k < 18; ++k) {
             float *d = wsT<float>(c, "dph.ch" + std::to_string(k), nch);
-            if (nch) ST_HIP(hipMemcpyAsync(d, chunk[k], nch * 4, hipMemcpyHostToDevice, c->stream));
+            up.push_back(HostXfer{const_cast<float *>(chunk[k]), d, nch * 4});
             dchunk[k] = d;
         }
         for (int k = 0; k < 4; ++k) {
             uint32_t *d = wsT<uint32_t>(c, "dph.v" + std::to_string(k), n);
-            if (n) ST_HIP(hipMemcpyAsync(d, vertex[k], n * 4, hipMemcpyHostToDevice, c->stream));
+            up.push_back(HostXfer{const_cast<uint32_t *>(vertex[k]), d, n * 4});
             dvert[k] = d;
         }
         for (int k = 0; k < nsh; ++k) {
             uint8_t *d = wsT<uint8_t>(c, "dph.s" + std::to_string(k), n);
-            if (n) ST_HIP(hipMemcpyAsync(d, sh[k], n, hipMemcpyHostToDevice, c->stream));
+            up.push_back(HostXfer{const_cast<uint8_t *>(sh[k]), d, n});
             dsh[k] = d;
         }
+        staged_h2d(c, up);
         for (int k = 0; k < 14 + nsh; ++k) dout[k] = wsT<float>(c, "dph.o" + std::to_string(k), n);
         decompress_ply_dev(c, n, dchunk.data(), dvert.data(), dsh.data(), nsh, dout.data());
-        for (int k = 0; k < 14 + nsh; ++k)
-            if (n) ST_HIP(hipMemcpyAsync(out[k], dout[k], n * 4, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+        std::vector<HostXfer> down;
+        for (int k = 0; k < 14 + nsh; ++k) down.push_back(HostXfer{out[k], dout[k], n * 4});
+        staged_d2h(c, down);
     });
 }
 

@@ -317,7 +317,22 @@ __global__ __launch_bounds__(SS_T) void k_small_sort(K *__restrict__ keys, uint3
         mine[u] = e < n ? (sk[e] >> shift) & mask : (K)0;
         rank[u] = 0;
     }
-    for (uint32_t j = 0; j < n; ++j) {
+    // eight broadcast LDS reads in flight per step: the loop was bound by one read's latency
+    constexpr uint32_t SU = 8;
+    uint32_t j = 0;
+    for (; j + SU <= n; j += SU) {
+        K kj[SU];
+#pragma unroll
+        for (uint32_t q = 0; q < SU; ++q) kj[q] = (sk[j + q] >> shift) & mask;
+#pragma unroll
+        for (uint32_t q = 0; q < SU; ++q)
+#pragma unroll
+            for (int u = 0; u < (int)(SS_MAX / SS_T); ++u) {
+                const uint32_t e = threadIdx.x + u * SS_T;
+                rank[u] += (kj[q] < mine[u] || (kj[q] == mine[u] && j + q < e)) ? 1u : 0u;
+            }
+    }
+    for (; j < n; ++j) {
         const K kj = (sk[j] >> shift) & mask;
 #pragma unroll
         for (int u = 0; u < (int)(SS_MAX / SS_T); ++u) {

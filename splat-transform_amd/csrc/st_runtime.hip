@@ -1,8 +1,13 @@
 // st_runtime.hip -- context, workspace, error plumbing, table helpers.
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <sstream>
+#include <thread>
 
 #include "st_internal.h"
 
@@ -70,6 +75,162 @@ void *io_buf(st_ctx *c, size_t bytes) {
 }
 
 void use_device(st_ctx *c) { ST_HIP(hipSetDevice(c->device)); }
+
+// ---- staged pageable copies ----------------------------------------------------------
+namespace {
+constexpr int XF_SLOTS = 4;                 // pinned slots (st_ctx::xfer_ev)
+// bytes per slot and host threads copying one slot (ST_XFER_CHUNK_MB / ST_XFER_THREADS: experiments)
+const size_t XF_CHUNK = (getenv("ST_XFER_CHUNK_MB") ? std::strtoull(getenv("ST_XFER_CHUNK_MB"), nullptr, 10) : 16ull) << 20;
+const int XF_THREADS = getenv("ST_XFER_THREADS") ? std::atoi(getenv("ST_XFER_THREADS")) : 8;
+constexpr size_t XF_DIRECT = 1ull << 20;     // smaller copies go through the runtime as they are
+
+// host threads that run one job at a time, each thread taking its share
+struct CopyPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int left = 0;
+    bool stop = false;
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i)
+            th.emplace_back([this, i] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> j;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        go.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        j = job;
+                    }
+                    j(i);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--left == 0) done.notify_all();
+                }
+            });
+    }
+    void run(std::function<void(int)> f) {
+        std::unique_lock<std::mutex> lk(mu);
+        job = std::move(f);
+        left = (int)th.size();
+        ++gen;
+        go.notify_all();
+        done.wait(lk, [&] { return left == 0; });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto &t : th) t.join();
+    }
+};
+
+struct Piece {
+    char *host, *dev;
+    size_t bytes;
+};
+
+void xfer_setup(st_ctx *c) {
+    ST_REQUIRE(XF_CHUNK > 0 && XF_THREADS > 0, ST_ERR_ARG, "ST_XFER_CHUNK_MB / ST_XFER_THREADS must be positive");
+    if (!c->xfer) ST_HIP(hipHostMalloc(&c->xfer, XF_SLOTS * XF_CHUNK, hipHostMallocDefault));
+    for (auto &e : c->xfer_ev)
+        if (!e) ST_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->xfer_pool) c->xfer_pool = new CopyPool(XF_THREADS);
+}
+
+// host-side copy of one piece: split over the pool when it is large
+void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes) {
+    if (bytes < (2ull << 20)) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    static_cast<CopyPool *>(c->xfer_pool)->run([=](int t) {
+        const size_t a0 = bytes * t / XF_THREADS, a1 = bytes * (t + 1) / XF_THREADS;
+        std::memcpy(dst + a0, src + a0, a1 - a0);
+    });
+}
+
+// the staged transfers cut into slot-sized pieces; small ones are issued directly
+std::vector<Piece> pieces_of(st_ctx *c, const std::vector<HostXfer> &xs, bool h2d) {
+    std::vector<Piece> ps;
+    for (const auto &x : xs) {
+        if (!x.bytes) continue;
+        if (x.bytes < XF_DIRECT) {
+            if (h2d) ST_HIP(hipMemcpyAsync(x.dev, x.host, x.bytes, hipMemcpyHostToDevice, c->stream));
+            else ST_HIP(hipMemcpyAsync(x.host, x.dev, x.bytes, hipMemcpyDeviceToHost, c->stream));
+            continue;
+        }
+        for (size_t o = 0; o < x.bytes; o += XF_CHUNK)
+            ps.push_back(Piece{static_cast<char *>(x.host) + o, static_cast<char *>(x.dev) + o,
+                               std::min(XF_CHUNK, x.bytes - o)});
+    }
+    return ps;
+}
+}  // namespace
+
+// ST_XFER_PRINT=1: bytes and rate of every staged copy on stderr
+struct XferLog {
+    const char *what;
+    const std::vector<HostXfer> &xs;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~XferLog() {
+        if (!getenv("ST_XFER_PRINT")) return;
+        size_t b = 0;
+        for (auto &x : xs) b += x.bytes;
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[st xfer] %s %.1f MB in %.2f ms = %.1f GB/s\n", what, b / 1e6, s * 1e3, b / s / 1e9);
+    }
+};
+
+void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs) {
+    XferLog log{"h2d", xs};
+    std::vector<Piece> ps = pieces_of(c, xs, true);
+    if (!ps.empty()) {
+        xfer_setup(c);
+        bool pending[XF_SLOTS] = {false, false, false, false};
+        for (size_t k = 0; k < ps.size(); ++k) {
+            const int b = (int)(k % XF_SLOTS);
+            char *slot = static_cast<char *>(c->xfer) + b * XF_CHUNK;
+            if (pending[b]) ST_HIP(hipEventSynchronize(c->xfer_ev[b]));  // the slot's last DMA is done
+            host_copy(c, slot, ps[k].host, ps[k].bytes);
+            ST_HIP(hipMemcpyAsync(ps[k].dev, slot, ps[k].bytes, hipMemcpyHostToDevice, c->stream));
+            ST_HIP(hipEventRecord(c->xfer_ev[b], c->stream));
+            pending[b] = true;
+        }
+    }
+    ST_HIP(hipStreamSynchronize(c->stream));
+}
+
+void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs) {
+    XferLog log{"d2h", xs};
+    std::vector<Piece> ps = pieces_of(c, xs, false);
+    if (!ps.empty()) {
+        xfer_setup(c);
+        long held[XF_SLOTS] = {-1, -1, -1, -1};  // the piece whose bytes wait in each slot
+        auto drain = [&](int b) {
+            if (held[b] < 0) return;
+            ST_HIP(hipEventSynchronize(c->xfer_ev[b]));
+            const Piece &p = ps[(size_t)held[b]];
+            host_copy(c, p.host, static_cast<char *>(c->xfer) + b * XF_CHUNK, p.bytes);
+            held[b] = -1;
+        };
+        for (size_t k = 0; k < ps.size(); ++k) {
+            const int b = (int)(k % XF_SLOTS);
+            drain(b);
+            ST_HIP(hipMemcpyAsync(static_cast<char *>(c->xfer) + b * XF_CHUNK, ps[k].dev, ps[k].bytes,
+                                  hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipEventRecord(c->xfer_ev[b], c->stream));
+            held[b] = (long)k;
+        }
+        for (size_t k = ps.size() > XF_SLOTS ? ps.size() - XF_SLOTS : 0; k < ps.size(); ++k) drain((int)(k % XF_SLOTS));
+    }
+    ST_HIP(hipStreamSynchronize(c->stream));
+}
 
 void mark(st_ctx *c, const char *name) {
     if (!c->timing) return;
@@ -242,6 +403,10 @@ void st_ctx_destroy(st_ctx *c) {
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->archive) (void)hipHostFree(c->archive);
     if (c->io) (void)hipHostFree(c->io);
+    if (c->xfer) (void)hipHostFree(c->xfer);
+    for (auto e : c->xfer_ev)
+        if (e) (void)hipEventDestroy(e);
+    delete static_cast<CopyPool *>(c->xfer_pool);
     for (auto &m : c->marks) (void)hipEventDestroy(m.ev);
     for (auto &k : c->kevents) {
         (void)hipEventDestroy(k.a);
