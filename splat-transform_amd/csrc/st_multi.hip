@@ -820,12 +820,13 @@ RankSlice upload_slice(st_ctx *c, const st_table *const *tabs, int ntab, uint64_
     s.cols.resize(ntab);
     s.tabs.resize(ntab);
     uint64_t off = 0;
+    std::vector<HostXfer> up;  // each rank's host thread stages its own slice (staged_h2d)
     for (int t = 0; t < ntab; ++t) {
         const uint64_t a = std::max(lo, off), b = std::min(hi, off + tabs[t]->n);
         const uint64_t m = b > a ? b - a : 0;
         for (int j = 0; j < tabs[t]->ncol; ++j) {
             float *d = wsT<float>(c, "gs.t" + std::to_string(t) + "." + std::to_string(j), m + 1);
-            if (m) ST_HIP(hipMemcpyAsync(d, tabs[t]->cols[j] + (a - off), 4 * m, hipMemcpyHostToDevice, c->stream));
+            up.push_back(HostXfer{const_cast<float *>(tabs[t]->cols[j] + (a - off)), d, 4 * m});
             s.cols[t].push_back(d);
         }
         s.tabs[t] = *tabs[t];
@@ -833,6 +834,7 @@ RankSlice upload_slice(st_ctx *c, const st_table *const *tabs, int ntab, uint64_
         s.tabs[t].cols = s.cols[t].data();
         off += tabs[t]->n;
     }
+    staged_h2d(c, up);
     for (auto &t : s.tabs) s.ptrs.push_back(&t);
     return s;
 }
@@ -974,16 +976,17 @@ int st_group_sog(st_group *g, const st_table *const *tables, int32_t ntables, co
         const uint64_t tex = (uint64_t)meta->width * meta->height * 4;
         uint8_t *dst[6] = {out->means_l, out->means_u, out->quats, out->scales, out->sh0, out->shn_labels};
         uint8_t *src[6] = {dt.t.means_l, dt.t.means_u, dt.t.quats, dt.t.scales, dt.t.sh0, dt.t.shn_labels};
+        std::vector<HostXfer> down;
         for (int i = 0; i < (C ? 6 : 5); ++i) {
             ST_REQUIRE(dst[i], ST_ERR_ARG, "sog: texture output is NULL");
-            ST_HIP(hipMemcpyAsync(dst[i], src[i], tex, hipMemcpyDeviceToHost, c->stream));
+            down.push_back(HostXfer{dst[i], src[i], tex});
         }
         if (C) {
             ST_REQUIRE(out->shn_centroids, ST_ERR_ARG, "sog: shN outputs are NULL");
-            ST_HIP(hipMemcpyAsync(out->shn_centroids, dt.t.shn_centroids,
-                                  (size_t)meta->shn_width * meta->shn_height * 4, hipMemcpyDeviceToHost, c->stream));
+            down.push_back(HostXfer{out->shn_centroids, dt.t.shn_centroids,
+                                    (size_t)meta->shn_width * meta->shn_height * 4});
         }
-        ST_HIP(hipStreamSynchronize(c->stream));
+        staged_d2h(c, down);
         if (used) *used = u;
     });
 }

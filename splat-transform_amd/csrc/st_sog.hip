@@ -8,6 +8,8 @@
 // Uint8Arrays).  WebP encoding / ZIP packaging stay on the host (out of the
 // device pipeline).
 #include <cmath>
+#include <exception>
+#include <thread>
 
 #include "st_jsmath.h"
 #include "st_kmeans.h"
@@ -277,6 +279,41 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     for (uint8_t *p : {out->means_l, out->means_u, out->quats, out->scales, out->sh0})
         ST_HIP(hipMemsetAsync(p, 0, texels * 4, c->stream));
 
+    // cluster1d of the colours (write-sog.ts:253-268) runs on a side context from its own host
+    // thread while this one orders, packs means / quats and clusters the scales.  Its draws
+    // start where the scales' k-means stops taking them (re-seeds of empty clusters only), so
+    // it starts at the scales' cursor 0 and is kept only if the scales took no draw; otherwise
+    // it reruns here at the right cursor (bit-identical either way)
+    if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    st_ctx *aux = c->aux;
+    auto *lab_c = wsT<uint8_t>(aux, "sog.lab_c", n * 3);
+    auto *cb_c = wsT<float>(aux, "sog.cb_c", 256);
+    uint64_t used_c = 0;
+    std::exception_ptr err_c;
+    {
+        // the colour columns are the caller's: whatever the caller queued on c->stream first
+        hipEvent_t ev;
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, c->stream));
+        ST_HIP(hipStreamWaitEvent(aux->stream, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+    }
+    std::thread colours([&] {
+        try {
+            use_device(aux);
+            used_c = cluster1d_dev(aux, m + 6, 3, n, iters, draws, ndraws, cb_c, lab_c);
+            ST_HIP(hipStreamSynchronize(aux->stream));
+        } catch (...) {
+            err_c = std::current_exception();
+        }
+    });
+    struct Joiner {
+        std::thread &th;
+        ~Joiner() {
+            if (th.joinable()) th.join();
+        }
+    } joiner{colours};
+
     // Morton order (write-sog.ts:42-49)
     auto *idx = wsT<uint32_t>(c, "sog.idx", n);
     iota_u32(c, idx, n);
@@ -323,9 +360,19 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     ST_LAUNCH_CHECK();
     mark(c, "sog.scales");
     // colour + opacity (write-sog.ts:253-268)
-    cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
-    ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n, m[9],
+    colours.join();
+    const uint8_t *clab = lab_c;
+    const float *ccb = cb_c;
+    if (cursor == 0) {
+        if (err_c) std::rethrow_exception(err_c);
+        cursor += used_c;
+    } else {  // the scales took draws: the colours' k-means starts after them
+        cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
+        clab = lab;
+        ccb = cb;
+    }
+    ST_HIP(hipMemcpyAsync(meta->sh0_codebook, ccb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n, m[9],
                        (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
