@@ -173,6 +173,33 @@ def test_sog_all_bands_vs_oracle(ctx, C):
         same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
 
 
+@pytest.mark.parametrize('who', ['scales', 'colours', 'both', 'neither'])
+def test_sog_reseeding_cluster1d_vs_oracle(ctx, who):
+    """The colours' cluster1d runs beside the scales' on a side context from draw 0 and is kept
+    only when the scales' k-means took no draw (re-seeds of empty clusters, k-means.ts:174-178);
+    otherwise it reruns after them.  Columns with a far outlier leave most linspace centroids
+    (k-means.ts:23-39) without members, so that cluster1d consumes draws."""
+    n, C = 5000, 3
+    cols = _table(n, C, 77)
+    rng = np.random.default_rng(5)
+    outlier = {'scales': ['scale_0', 'scale_1', 'scale_2'], 'colours': ['f_dc_0', 'f_dc_1', 'f_dc_2'],
+               'both': ['scale_0', 'f_dc_2'], 'neither': []}[who]
+    for k in outlier:
+        cols[k] = (rng.integers(0, 4, n) * 0.25 - 5).astype(np.float32)
+        cols[k][17] = 40.0
+    draws = oracle.mulberry32(123, 1 << 15)
+    s_cols = [cols[f'scale_{i}'] for i in range(3)]
+    _, _, _, s_used = oracle.cluster1d(s_cols, 3, draws)
+    assert (s_used > 0) == (who in ('scales', 'both'))
+    tex, meta, used = ctx.sog(cols, 3, draws)
+    rc, otex, ometa, oused = oracle.sog(cols, C, 3, draws)
+    assert rc == 0 and used == oused
+    for k in tex:
+        same_bits(tex[k], otex[k])
+    for f in ('scales_codebook', 'sh0_codebook', 'shn_codebook'):
+        same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
+
+
 @pytest.mark.parametrize('case', ['n_eq_4k', 'repeats', 'host_env'])
 def test_kmeans_device_init_vs_oracle(ctx, case, monkeypatch):
     """initializeCentroids (k-means.ts:8-20) on the device (n >= 4k): first occurrences of
