@@ -746,7 +746,7 @@ __global__ __launch_bounds__(256) void k_code_hist(const uint32_t *__restrict__ 
 // cursor = exclusive scan of the histogram; each round ranks its points per code in LDS,
 // reserves one range per code with a global atomic, and writes the point indices
 __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict__ labels, uint32_t n, uint32_t ncodes,
-                                                      uint32_t *__restrict__ cursor, uint32_t *__restrict__ grouped) {
+                                                      uint32_t *__restrict__ cursor, uint2 *__restrict__ grouped) {
     __shared__ uint32_t h[FB_MAX_CODES];
     constexpr int PER = FB_TILE / 256;
     for (uint32_t base = blockIdx.x * FB_TILE; base < n; base += gridDim.x * FB_TILE) {
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PER; ++j)
-            if (code[j] < ncodes) grouped[h[code[j]] + rank[j]] = base + j * 256 + threadIdx.x;
+            if (code[j] < ncodes) grouped[h[code[j]] + rank[j]] = make_uint2(base + j * 256 + threadIdx.x, code[j]);
         __syncthreads();
     }
 }
@@ -786,7 +786,7 @@ __device__ inline float row_bcast(float x) {
 // this one is scored.  (c - p)^2 is taken as (p - c)^2: the same rounded square.
 template <int LD>
 __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos, int d, const float *__restrict__ caos,
-                                                  int k, const uint32_t *__restrict__ grouped,
+                                                  int k, const uint2 *__restrict__ grouped,
                                                   const uint32_t *__restrict__ ndecided,
                                                   uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
                                                   State *st) {
@@ -799,10 +799,10 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
     const int cnt = (int)min(nd - j0, (uint32_t)FB_RUN);
     const int rr = threadIdx.x & 15;
     const int gl = (threadIdx.x & 63) & ~15;  // first lane of this group in the wave
-    const uint32_t pa = rr < cnt ? grouped[j0 + rr] : 0u;
-    const uint32_t pb = 16 + rr < cnt ? grouped[j0 + 16 + rr] : 0u;
-    const uint32_t ca = rr < cnt ? labels[pa] : 0u;
-    const uint32_t cb = 16 + rr < cnt ? labels[pb] : 0u;
+    // (point, tile-half code) pairs: the codes come with the points, not from labels[] at random
+    const uint2 ga = rr < cnt ? grouped[j0 + rr] : make_uint2(0u, 0u);
+    const uint2 gb = 16 + rr < cnt ? grouped[j0 + 16 + rr] : make_uint2(0u, 0u);
+    const uint32_t pa = ga.x, pb = gb.x, ca = ga.y, cb = gb.y;
     auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
     auto code_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? ca : cb, gl + (i & 15), 64); };
     // every lane loads (lanes past LD / 4 repeat a slice nobody broadcasts): no branch around
@@ -1096,7 +1096,7 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
         auto *hist = wsT<uint32_t>(c, "kn.fbhist", ncodes);
         auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
         auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
-        auto *grouped = wsT<uint32_t>(c, "kn.fbpts", n);
+        auto *grouped = wsT<uint2>(c, "kn.fbpts2", n);
         ST_HIP(hipMemsetAsync(hist, 0, ncodes * sizeof(uint32_t), c->stream));
         hipLaunchKernelGGL(k_code_hist, dim3(grid_for(n, 256 * 64, 512)), dim3(256), 0, c->stream, labels,
                            (uint32_t)n, ncodes, hist);

@@ -1,7 +1,7 @@
 #!/bin/bash
+# k-means parity tests (single device + sharded) and the N-D k-means micro-bench at the bench shape
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -k "kmeans or assign or sog or cluster1d or ties" > gpurun_out/kn_tests.log 2>&1 || { tail -40 gpurun_out/kn_tests.log; exit 1; }
-tail -15 gpurun_out/kn_tests.log
-timeout -k 10 300 python tools/kn_bench.py --n 10000000 --iters 3 > gpurun_out/kn_bench.log 2>&1 || { tail -20 gpurun_out/kn_bench.log; exit 1; }
-cat gpurun_out/kn_bench.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edges.py tests/test_sog65k.py tests/test_dist_gpu.py -x -q --timeout 300 --timeout-method thread -k "kmeans or assign or sog or ties or partials or dist or step" > gpurun_out/kn_tests.log 2>&1 || { tail -30 gpurun_out/kn_tests.log; exit 1; }
+tail -2 gpurun_out/kn_tests.log
+timeout -k 10 300 python3 tools/kn_bench.py --n 10000000 --iters 2 2>&1 | grep -v amdgpu.ids
