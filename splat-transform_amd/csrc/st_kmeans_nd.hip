@@ -952,8 +952,8 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
-    // 16 member rows in flight per wave (the adds stay in ascending point order)
-    constexpr int U = 16;
+    // 32 member rows in flight per wave (the adds stay in ascending point order)
+    constexpr int U = 32;
     for (; j + U <= s1; j += U) {
         float v[U];
 #pragma unroll
