@@ -65,8 +65,11 @@ __host__ __device__ inline int kp_of(int d) { return ((d + 3) + 15) / 16 * 16; }
 __device__ inline uint16_t h_bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 __device__ inline float h_val(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 
+// |score_mfma - score| <= E(p, c) = r (|p| |dc| + |dp| |c~|) + a |p~| |c~| + b |c~|^2 + ec (|p~| + |c~|) + ep
+// with dp = p - p~, dc = c - c~ the fp16 rounding residuals (p.c - p~.c~ = p.dc + dp.c~, x2 for
+// the -2 factor), a / b the f32 accumulation, ec / ep the fp16 underflow; delta = rel (|p| + |c|)^2
 struct Bound {
-    float a, b, ec, ep, rel;  // E = a|p|cm + b cm^2 + ec (|p| + cm) + ep; delta = rel (|p| + cm)^2
+    float r, a, b, ec, ep, rel;
 };
 
 // error-bound constants for a given dimension and fp16-denormal behaviour
@@ -75,8 +78,9 @@ Bound make_bound(int d, bool denorm) {
     const double e_abs = denorm ? std::ldexp(1.0, -25) : std::ldexp(1.0, -14);
     const double gam = (d + 3 + 3) * std::ldexp(1.0, -23);  // f32 accumulation, truncation-safe
     Bound B{};
-    // rounding of p and c (x2 for the -2 factor) + accumulation, 5% slack
-    B.a = (float)((2 * 2 * u * (1 + u) + 2.01 * gam) * 1.05);
+    // rounding residuals of p and c (x2 for the -2 factor), accumulation; 5% slack
+    B.r = (float)(2 * 1.05);
+    B.a = (float)(2.01 * gam * (1 + u) * (1 + u) * 1.05);
     B.b = (float)((1.01 * gam + std::ldexp(1.0, -22)) * 1.05);
     B.ec = (float)(2 * std::sqrt((double)d) * e_abs * (1 + u) * 1.05);
     B.ep = (float)((2 * d * e_abs * e_abs + 3 * e_abs) * 1.05 + 1e-30);
@@ -84,29 +88,39 @@ Bound make_bound(int d, bool denorm) {
     return B;
 }
 
-__device__ inline float wbound(const Bound &B, float pn, float cm) {
-    const float e = B.a * pn * cm + B.b * cm * cm + B.ec * (pn + cm) + B.ep;
-    const float s = pn + cm;
-    return (2.0f * e + 2.0f * B.rel * s * s) * 1.0001f;
+// E for point norm pn, residual norm dp and centroid norm cn, residual norm dc (all rounded up;
+// |p~| <= pn + dp, |c~| <= cn + dc)
+__device__ inline float err_bound(const Bound &B, float pn, float dp, float cn, float dc) {
+    const float pt = pn + dp, ct = cn + dc;
+    return B.r * (pn * dc + dp * ct) + B.a * pt * ct + B.b * ct * ct + B.ec * (pt + ct) + B.ep;
 }
 
-// the same window with the best row's error bounded by its own tile-half's largest norm cb
-// (<= cm): the rows that can beat it are bounded by cm, the best row itself by cb
-__device__ inline float wbound2(const Bound &B, float pn, float cb, float cm) {
-    const float e1 = B.a * pn * cb + B.b * cb * cb + B.ec * (pn + cb) + B.ep;
-    const float e2 = B.a * pn * cm + B.b * cm * cm + B.ec * (pn + cm) + B.ep;
+// the decision window: the best row's error bounded by its own tile-half's largest norm cb and
+// residual dcb, the rows that can beat it by the palette's cm / dcm
+__device__ inline float wbound2(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float dcm) {
     const float s = pn + cm;
-    return (e1 + e2 + 2.0f * B.rel * s * s) * 1.0001f;
+    return (err_bound(B, pn, dp, cb, dcb) + err_bound(B, pn, dp, cm, dcm) + 2.0f * B.rel * s * s) * 1.0001f;
 }
 
-// largest norm (rounded up) among the 16 rows of each tile-half
-__global__ __launch_bounds__(256) void k_half_max(const float *__restrict__ cnorm, uint32_t nhalves,
-                                                  float *__restrict__ chalf) {
+// the window between two given tile-halves (largest norms ca, cb and residuals dca, dcb)
+__device__ inline float wbound_pair(const Bound &B, float pn, float dp, float ca, float dca, float cb, float dcb) {
+    const float s = pn + fmaxf(ca, cb);
+    return (err_bound(B, pn, dp, ca, dca) + err_bound(B, pn, dp, cb, dcb) + 2.0f * B.rel * s * s) * 1.0001f;
+}
+
+// largest norm and largest rounding-residual norm (rounded up) among the 16 rows of each tile-half
+__global__ __launch_bounds__(256) void k_half_max(const float *__restrict__ cnorm, const float *__restrict__ cdn,
+                                                  uint32_t nhalves, float *__restrict__ chalf,
+                                                  float *__restrict__ chalf_d) {
     for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nhalves; h += gridDim.x * blockDim.x) {
-        float m = 0.f;
-        for (int rr = 0; rr < 16; ++rr)
-            m = fmaxf(m, cnorm[(h >> 1) * 32 + 4 * (h & 1) + (rr & 3) + 8 * (rr >> 2)]);
+        float m = 0.f, md = 0.f;
+        for (int rr = 0; rr < 16; ++rr) {
+            const uint32_t r = (h >> 1) * 32 + 4 * (h & 1) + (rr & 3) + 8 * (rr >> 2);
+            m = fmaxf(m, cnorm[r]);
+            md = fmaxf(md, cdn[r]);
+        }
         chalf[h] = m;
+        chalf_d[h] = md;
     }
 }
 
@@ -140,7 +154,8 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
 constexpr int PF_PTS = 256;            // points per workgroup (8 tiles)
 constexpr int PF_LDS_LD = PF_PTS + 1;  // LDS column stride: row-wise reads hit distinct banks
 __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
-                                                     int ks, float sigma, uint4 *pfrag, float *pnorm, float *aos) {
+                                                     int ks, float sigma, uint4 *pfrag, float *pnorm, float *pdn,
+                                                     float *aos) {
     __shared__ float x[61 * PF_LDS_LD];  // d <= 61
     const uint64_t p0 = (uint64_t)blockIdx.x * PF_PTS;
     const int j = threadIdx.x;
@@ -158,12 +173,16 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
     for (; k0 < d; ++k0) x[k0 * PF_LDS_LD + j] = valid ? cols[k0][pj] : 0.0f;
     __syncthreads();
     if (valid) {
-        double nn = 0;
+        // |sigma p| and the norm of its fp16 rounding residual p - p~ (exact in f64), rounded up
+        double nn = 0, dd = 0;
         for (int k = 0; k < d; ++k) {
-            const double v = (double)(x[k * PF_LDS_LD + j] * sigma);
+            const float f = x[k * PF_LDS_LD + j] * sigma;
+            const double v = (double)f, r = v - (double)h_val(h_bits(f));
             nn += v * v;
+            dd += r * r;
         }
         pnorm[p0 + j] = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+        pdn[p0 + j] = (float)(__builtin_sqrt(dd) * (1.0 + 1e-6));
     }
     // AoS rows: one float4 per thread-step over the workgroup's contiguous row block
     const int ld = aos_ld(d), q4 = ld / 4;
@@ -211,10 +230,10 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
 // one thread per centroid row; rows >= k can never win
 __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
                                                         float sigma, uint4 *cfrag, uint32_t *cmax_bits, float *caos,
-                                                        float2 *cfix, float *cnorm) {
+                                                        float2 *cfix, float *cnorm, float *cdn) {
     const uint32_t total = ctiles * 32;
     const int ld = aos_ld(d);
-    float mymax = 0.f;
+    float mymax = 0.f, mydmax = 0.f;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < total; r += gridDim.x * blockDim.x) {
         const bool valid = r < (uint32_t)k;
         if (valid) {
@@ -228,10 +247,12 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
                 cfix[(((uint64_t)(r >> 5) * 2 + hh) * (ld / 2) + q) * 16 + r16] = make_float2(a, b);
             }
         }
-        double nn = 0;
+        double nn = 0, dd = 0;
         for (int c = 0; c < d; ++c) {
-            const double x = valid ? (double)(cen[(uint64_t)c * k + r] * sigma) : 0.0;
+            const float f = valid ? cen[(uint64_t)c * k + r] * sigma : 0.0f;
+            const double x = (double)f, e = x - (double)h_val(h_bits(f));
             nn += x * x;
+            dd += e * e;
         }
         uint16_t n1, n2, n3;
         if (valid) {
@@ -241,10 +262,14 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
             const double r2 = r1 - (double)h_val(n2);
             n3 = h_bits((float)r2);
             const float nr = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+            const float dr = (float)(__builtin_sqrt(dd) * (1.0 + 1e-6));
             mymax = fmaxf(mymax, nr);
+            mydmax = fmaxf(mydmax, dr);
             cnorm[r] = nr;
+            cdn[r] = dr;
         } else {
             cnorm[r] = 0.0f;  // padding row: never the best
+            cdn[r] = 0.0f;
             n1 = h_bits(60000.0f);  // padding: score ~6e4 >> any real score (< 200)
             n2 = n3 = 0;
         }
@@ -270,8 +295,14 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
                 cfrag[((uint64_t)t * ks + s) * 64 + h * 32 + row] = v;
             }
     }
-    for (int o = 32; o > 0; o >>= 1) mymax = fmaxf(mymax, __shfl_xor(mymax, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(cmax_bits, __builtin_bit_cast(uint32_t, mymax));
+    for (int o = 32; o > 0; o >>= 1) {
+        mymax = fmaxf(mymax, __shfl_xor(mymax, o, 64));
+        mydmax = fmaxf(mydmax, __shfl_xor(mydmax, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(cmax_bits, __builtin_bit_cast(uint32_t, mymax));  // non-negative floats: bit order
+        atomicMax(cmax_bits + 1, __builtin_bit_cast(uint32_t, mydmax));
+    }
 }
 
 // ---- the MFMA sweep -------------------------------------------------------------
@@ -286,8 +317,9 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
 template <int KS, int MODE>
 __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
-                                               const float *__restrict__ pnorm, const uint32_t *__restrict__ cmax_bits,
-                                               const float *__restrict__ chalf,
+                                               const float *__restrict__ pnorm, const float *__restrict__ pdn,
+                                               const uint32_t *__restrict__ cmax_bits, const float *__restrict__ chalf,
+                                               const float *__restrict__ chalf_d,
                                                const Bound bnd, uint32_t *__restrict__ labels,
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
@@ -446,7 +478,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
     });
     if (MODE == 1) return;
 
-    const float cm = __builtin_bit_cast(float, *cmax_bits);
+    const float cm = __builtin_bit_cast(float, cmax_bits[0]), dcm = __builtin_bit_cast(float, cmax_bits[1]);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         // merge the two lane-halves' top-3 (sorted) into the point's top-3; codes =
@@ -468,12 +500,21 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             // denormal ulp); 2^-20 |key| on top covers the f32 roundings of the window sums
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
-            const float W = wbound2(bnd, pnorm[p], chalf[code1], cm);
+            const float pn = pnorm[p], dp = pdn[p];
+            const float W = wbound2(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, dcm);
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
             } else if (nm3 > nm1 + W + e1 + (__builtin_fabsf(nm3) * kr + ka)) {
-                is_pair = true;  // every candidate lies in the two best tile-halves
-                labels[p] = 0xfffffffeu;
+                // every candidate lies in the two best tile-halves.  Only the second one competes
+                // with the first, so its own largest norm bounds its rows' error instead of the
+                // palette's (chalf[code2] <= cm): often that already decides the point
+                const float W2 = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], chalf[code2], chalf_d[code2]);
+                if (nm2 > nm1 + W2 + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
+                    labels[p] = code1;
+                } else {
+                    is_pair = true;
+                    labels[p] = 0xfffffffeu;
+                }
             } else {
                 is_amb = true;
                 labels[p] = 0xffffffffu;
@@ -968,13 +1009,14 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
 template <int KS>
 struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
-                     const float *pnorm, const uint32_t *cmax, const float *chalf, const Bound &bnd,
+                     const float *pnorm, const float *pdn, const uint32_t *cmax, const float *chalf,
+                     const float *chalf_d, const Bound &bnd,
                      uint32_t *labels, float *thr, uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
         const uint32_t per_block = NW * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(WG), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
-                           cmax, chalf, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
+                           pdn, cmax, chalf, chalf_d, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
                            pair_codes);
         ST_LAUNCH_CHECK();
     }
@@ -987,7 +1029,8 @@ struct Sweep {
         const dim3 grid(blocks, split);
         KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
-                           (const float *)nullptr, (const uint32_t *)nullptr, (const float *)nullptr, bnd,
+                           (const float *)nullptr, (const float *)nullptr, (const uint32_t *)nullptr,
+                           (const float *)nullptr, (const float *)nullptr, bnd,
                            (uint32_t *)nullptr, thr_slot,
                            (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
                            (uint2 *)nullptr);
@@ -1028,8 +1071,9 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     const uint32_t ntiles = (uint32_t)((n + 31) / 32);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
+    auto *pdn = wsT<float>(c, "kn.pdn", n);
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
-    auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits
+    auto *scal = wsT<uint32_t>(c, "kn.scal", 4);  // [0]=absmax bits [1]=cmax bits [2]=max residual norm bits
     // scale: max|x| * sigma in [1, 2); check_finite found max|x| in its pass over the points
     ST_HIP(hipMemsetAsync(scal, 0, 16, c->stream));
     float amax = c->km_absmax;
@@ -1045,7 +1089,7 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
     hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(256), 0,
-                       c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, aos);
+                       c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, pdn, aos);
     ST_LAUNCH_CHECK();
     c->kn_sigma = sigma;
     c->kn_n = n;
@@ -1063,6 +1107,7 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     const uint32_t ctiles = (uint32_t)(((k + 31) / 32 + CT_STAGE - 1) / CT_STAGE * CT_STAGE);
     auto *pfrag = wsT<uint4>(c, "kn.pfrag", (size_t)ntiles * ks * 64);
     auto *pnorm = wsT<float>(c, "kn.pnorm", n);
+    auto *pdn = wsT<float>(c, "kn.pdn", n);
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     auto *scal = wsT<uint32_t>(c, "kn.scal", 4);
     auto *cfrag = wsT<uint4>(c, "kn.cfrag", (size_t)ctiles * ks * 64);
@@ -1073,20 +1118,23 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     const Bound bnd = make_bound(d, probe_denorm(c));
     const float sigma = c->kn_sigma;
 
-    ST_HIP(hipMemsetAsync(scal + 1, 0, 4, c->stream));
+    ST_HIP(hipMemsetAsync(scal + 1, 0, 8, c->stream));
     auto *caos = wsT<float>(c, "kn.caos", (size_t)k * aos_ld(d));
     auto *cfix = wsT<float2>(c, "kn.cfix", (size_t)ctiles * 32 * (aos_ld(d) / 2));
     auto *cnorm = wsT<float>(c, "kn.cnorm", (size_t)ctiles * 32);
     auto *chalf = wsT<float>(c, "kn.chalf", (size_t)ctiles * 2);
+    auto *cdn = wsT<float>(c, "kn.cdn", (size_t)ctiles * 32);
+    auto *chalf_d = wsT<float>(c, "kn.chalfd", (size_t)ctiles * 2);
     hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
-                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix, cnorm);
+                       cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix, cnorm, cdn);
     hipLaunchKernelGGL(k_half_max, dim3(grid_for((uint64_t)ctiles * 2, 256, 1024)), dim3(256), 0, c->stream, cnorm,
-                       ctiles * 2, chalf);
+                       cdn, ctiles * 2, chalf, chalf_d);
     ST_LAUNCH_CHECK();
     auto *pair_pts = wsT<uint32_t>(c, "kn.pairpts", n);
     auto *pair_codes = wsT<uint2>(c, "kn.paircodes", n);
     ST_HIP(hipMemsetAsync(&dstate->amb, 0, 16, c->stream));  // amb + ties + overflow + pairs
-    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, scal + 1, chalf, bnd,
+    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
+                                        chalf_d, bnd,
                                         labels, thr, amb, dstate, pair_pts, pair_codes)));
     const uint32_t ncodes = ctiles * 2;
     const int ld = aos_ld(d);
@@ -1173,10 +1221,14 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
                     (unsigned long long)hist[3], (unsigned long long)hist[4], (unsigned long long)hist[5]);
         }
     }
+    if (npair && !namb) {  // the tie count read before k_fixpair_b: its exact ties count too
+        ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+    }
     if (getenv("ST_DEBUG"))
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
                 (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
-    // exact ties from k_fixrow and k_exact: the KdTree walk decides
+    // exact ties from k_fixrow, k_fixpair and k_exact: the KdTree walk decides
     if (h->ties) kd_resolve_ties(c, dcols, d, n, k, cen, ties, h->ties, labels);
     mark(c, "kn.exact");
 }

@@ -273,3 +273,32 @@ def test_step_api_init_rows_and_gather(ctx, case):
     got = (parts[0] + parts[1]).view(torch.float32).cpu().numpy()
     ref = np.stack([c.cpu().numpy()[want] for c in cols])
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize('swap', [False, True])
+def test_assign_pair_ties_without_ambiguous_points(ctx, swap):
+    """Exact ties found by the pair fix-up (two tile-halves) when no point is ambiguous: the
+    KdTree walk (kd-tree.ts:39-68) must still decide them.  Points at (3,0,0) are exactly 1 from
+    centroids (2,0,0) and (3,1,0), which sit in different halves of tile 0; every other centroid is
+    far away, so no point needs the collect sweep."""
+    import torch
+    dev = torch.device('cuda', 0)
+    k, n = 64, 3000
+    cen = np.zeros((3, k), np.float32)
+    for i in range(k):
+        cen[:, i] = (40 + i, 40, 40)
+    a, b = (28, 1) if swap else (1, 28)  # rows 1 and 28 of tile 0: lane-halves 0 and 1
+    cen[:, a] = (2, 0, 0)
+    cen[:, b] = (3, 1, 0)
+    pts = np.zeros((3, n), np.float32)
+    pts[:, : n // 2] = np.array([[3], [0], [0]], np.float32)
+    pts[:, n // 2:] = np.array([[2], [0], [0]], np.float32)
+    cols = [np.ascontiguousarray(pts[j]) for j in range(3)]
+    _, want = oracle.kmeans_assign(cols, cen)
+    tcols = [torch.from_numpy(c).to(dev) for c in cols]
+    tcen = torch.from_numpy(cen.reshape(-1).copy()).to(dev)
+    lab = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.dev_kmeans_prepare(tcols)
+    ctx.dev_kmeans_assign(tcols, k, tcen, lab)
+    ctx.synchronize()
+    same_bits(lab.cpu().numpy().astype(np.uint32), want)
