@@ -53,6 +53,8 @@ struct Coll {
     // root: recv[r] (at offset displ[r]) = rank r's send of bytes[r]; recv ignored elsewhere
     virtual void gatherv(const void *send, size_t mybytes, void *recv, const std::vector<size_t> &bytes,
                          const std::vector<size_t> &displ, int root, hipStream_t s) = 0;
+    // rank `to` receives rank `from`'s buf (every rank makes the call; the others pass through)
+    virtual void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) = 0;
     virtual void abort() {}
 };
 
@@ -97,6 +99,11 @@ struct RcclColl : Coll {
             ST_NCCL(ncclSend(send, mybytes, ncclUint8, root, comm, s));
         }
         ST_NCCL(ncclGroupEnd());
+    }
+    void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
+        if (world == 1 || from == to || !bytes || (rank != from && rank != to)) return;
+        if (rank == from) ST_NCCL(ncclSend(buf, bytes, ncclUint8, to, comm, s));
+        else ST_NCCL(ncclRecv(buf, bytes, ncclUint8, from, comm, s));
     }
     void abort() override {
         if (comm) ncclCommAbort(comm);
@@ -199,6 +206,15 @@ struct HostColl : Coll {
                 if (bytes[r])
                     ST_HIP(hipMemcpyAsync(static_cast<char *>(recv) + displ[r], hub->slot[r].data(), bytes[r],
                                           hipMemcpyHostToDevice, s));
+            ST_HIP(hipStreamSynchronize(s));
+        }
+        hub->barrier();
+    }
+    void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
+        if (rank == from) put(buf, bytes, s);
+        hub->barrier();
+        if (rank == to && from != to && bytes) {
+            ST_HIP(hipMemcpyAsync(buf, hub->slot[from].data(), bytes, hipMemcpyHostToDevice, s));
             ST_HIP(hipStreamSynchronize(s));
         }
         hub->barrier();
@@ -423,12 +439,17 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
         const uint32_t np = dist_finish(c, d, k, sac, sac + dk, E, C, cen, pending);
         if (np) {
             // the sequential f64 chain of each pending (cluster, dim): segments in global order
+            // the sequential f64 chain of each pending (cluster, dim): segments in global order, the
+            // running values handed from owner to owner (point to point), then to every rank
             ST_HIP(hipMemsetAsync(running, 0, 8 * (size_t)np, c->stream));
+            int prev = -1;
             for (int seg = 0; seg < P.nseg; ++seg)
                 for (int r = 0; r < co.world; ++r) {
+                    if (prev >= 0) co.sendrecv(running, 8 * (size_t)np, prev, r, c->stream);
                     if (r == co.rank && P.n) dist_seqsum(c, d, k, seg, pending, np, running, E, sac + dk);
-                    co.broadcast(running, 8 * (size_t)np, r, c->stream);
+                    prev = r;
                 }
+            co.broadcast(running, 8 * (size_t)np, prev, c->stream);
             dist_average(c, d, k, pending, np, running, C, cen);
         }
         // re-seed the empty clusters (k-means.ts:174-178): ascending clusters, one draw each
