@@ -92,6 +92,8 @@ struct st_ctx {
     // pinned host staging for small readbacks
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
+    // named pinned host buffers (pinned_slot): readbacks queued ahead of the sync that waits for them
+    std::map<std::string, std::pair<void *, size_t>> pinned_slots;
     // pinned host buffer of the last .sog archive (st_dev_sog_bundle*)
     void *archive = nullptr;
     size_t archive_bytes = 0;
@@ -130,6 +132,7 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
     return static_cast<T *>(c->ws.get(slot, count * sizeof(T) + 16));
 }
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
+void *pinned_slot(st_ctx *c, const std::string &name, size_t bytes);  // named, grow-only
 void *archive_buf(st_ctx *c, size_t bytes);  // host pinned archive buffer (reused, grow-only)
 void *io_buf(st_ctx *c, size_t bytes);       // host pinned file-chunk buffer (reused, grow-only)
 // copies between pageable host buffers and HBM for the one-call host forms: the bytes move

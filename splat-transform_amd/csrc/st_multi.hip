@@ -415,7 +415,8 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     auto *counts = wsT<uint32_t>(c, t + ".counts", (size_t)P.nseg * k);
     auto *pending = wsT<uint32_t>(c, t + ".pend", dk);
     auto *running = wsT<double>(c, t + ".run", dk);
-    std::vector<uint32_t> hC(k);
+    // the counts come back with dist_finish's readback (one stream sync per iteration)
+    auto *hC = static_cast<uint32_t *>(pinned_slot(c, t + ".hC", 4 * (size_t)k));
     const size_t cbytes = 4 * dk;
     for (int it = 0; it < iters; ++it) {
         if (c->verify && d > 1 && it == iters - 1)  // st_ctx_set_verify: the last assign's centroids
@@ -436,6 +437,7 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
         co.allreduce(E, dk, Dt::I32, Op::Min, c->stream);
         hipLaunchKernelGGL(k_counts_u32, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, sac + 2 * dk, k, C);
         ST_LAUNCH_CHECK();
+        ST_HIP(hipMemcpyAsync(hC, C, 4 * (size_t)k, hipMemcpyDeviceToHost, c->stream));
         const uint32_t np = dist_finish(c, d, k, sac, sac + dk, E, C, cen, pending);
         if (np) {
             // the sequential f64 chain of each pending (cluster, dim): segments in global order
@@ -452,9 +454,8 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
             co.broadcast(running, 8 * (size_t)np, prev, c->stream);
             dist_average(c, d, k, pending, np, running, C, cen);
         }
-        // re-seed the empty clusters (k-means.ts:174-178): ascending clusters, one draw each
-        ST_HIP(hipMemcpyAsync(hC.data(), C, 4 * (size_t)k, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+        // re-seed the empty clusters (k-means.ts:174-178): ascending clusters, one draw each (hC
+        // arrived with dist_finish's sync)
         std::vector<uint64_t> rows;
         std::vector<uint32_t> cls;
         for (int i = 0; i < k; ++i) {

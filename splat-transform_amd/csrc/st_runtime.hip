@@ -51,6 +51,18 @@ void *pinned(st_ctx *c, size_t bytes) {
     return c->pinned;
 }
 
+void *pinned_slot(st_ctx *c, const std::string &name, size_t bytes) {
+    auto &b = c->pinned_slots[name];
+    if (b.second < bytes) {
+        if (b.first) ST_HIP(hipHostFree(b.first));
+        b.first = nullptr;
+        b.second = 0;
+        ST_HIP(hipHostMalloc(&b.first, bytes, hipHostMallocDefault));
+        b.second = bytes;
+    }
+    return b.first;
+}
+
 void *archive_buf(st_ctx *c, size_t bytes) {
     if (c->archive_bytes < bytes) {
         if (c->archive) ST_HIP(hipHostFree(c->archive));
@@ -404,6 +416,8 @@ void st_ctx_destroy(st_ctx *c) {
     if (c->archive) (void)hipHostFree(c->archive);
     if (c->io) (void)hipHostFree(c->io);
     if (c->xfer) (void)hipHostFree(c->xfer);
+    for (auto &kv : c->pinned_slots)
+        if (kv.second.first) (void)hipHostFree(kv.second.first);
     for (auto e : c->xfer_ev)
         if (e) (void)hipEventDestroy(e);
     delete static_cast<CopyPool *>(c->xfer_pool);
