@@ -174,6 +174,9 @@ void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t
 // stable LSD radix sort of (key, value) pairs on bits [begin_bit, end_bit)
 void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
                     const std::string &tag);
+// the same from read-only keys with the identity permutation as values, into out_keys / out_vals
+void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int begin_bit, int end_bit,
+                         uint32_t *out_keys, uint32_t *out_vals, const std::string &tag);
 // as radix_sort_u32, but the result stays in whichever buffer pair the last pass wrote
 // (the caller's or the workspace's): *out_keys / *out_vals point at it
 void radix_sort_u32_inplace_or_swap(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1,

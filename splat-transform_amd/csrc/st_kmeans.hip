@@ -315,11 +315,9 @@ void bounds_from_sorted(st_ctx *c, const uint32_t *sorted_labels, uint64_t n, in
 
 void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t *sorted_labels, uint32_t *members,
                  uint32_t *start) {
-    ST_HIP(hipMemcpyAsync(sorted_labels, labels, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
-    iota_u32(c, members, n);
     int bits = 1;
     while ((1ull << bits) < (uint64_t)k) ++bits;
-    radix_sort_u32(c, sorted_labels, members, n, 0, bits, "km.ms");
+    radix_sort_u32_iota(c, labels, n, 0, bits, sorted_labels, members, "km.ms");
     bounds_from_sorted(c, sorted_labels, n, k, start);
 }
 

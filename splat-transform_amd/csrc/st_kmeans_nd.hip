@@ -323,7 +323,8 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                                                const Bound bnd, uint32_t *__restrict__ labels,
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
-                                               uint32_t *__restrict__ pair_pts, uint2 *__restrict__ pair_codes) {
+                                               uint32_t *__restrict__ pair_pts, uint2 *__restrict__ pair_codes,
+                                               uint32_t *__restrict__ code_hist) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
     constexpr int PER_THREAD = (STAGE_U4 + WG - 1) / WG;
     static_assert(STAGE_U4 % 64 == 0, "a stage is whole wave-instructions");
@@ -504,6 +505,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float W = wbound2(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, dcm);
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
+                if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
             } else if (nm3 > nm1 + W + e1 + (__builtin_fabsf(nm3) * kr + ka)) {
                 // every candidate lies in the two best tile-halves.  Only the second one competes
                 // with the first, so its own largest norm bounds its rows' error instead of the
@@ -511,6 +513,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                 const float W2 = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], chalf[code2], chalf_d[code2]);
                 if (nm2 > nm1 + W2 + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                     labels[p] = code1;
+                    if (code_hist) atomicAdd(&code_hist[code1], 1u);
                 } else {
                     is_pair = true;
                     labels[p] = 0xfffffffeu;
@@ -762,27 +765,13 @@ __global__ __launch_bounds__(256) void k_fixpair(const float *__restrict__ aos, 
 
 // ---- decided points grouped by tile-half ------------------------------------------
 // At K = 65,536 there are 4,096 tile-halves and ~2,000 decided points per half.  A
-// counting sort groups the points by their half (k_code_hist, scan, k_code_scatter; the
+// counting sort groups the points by their half (counts from the sweep, scan, k_code_scatter; the
 // order inside a group is immaterial), then k_fixrow_b keeps each lane's centroid row in
 // VGPRs across a run of points of one half: centroid rows are read once per run instead of
 // 3 KiB per point from L2.
 constexpr int FB_MAX_CODES = 8192;  // LDS histogram limit (2 x 4,096 tiles = K <= 131,072)
 constexpr int FB_TILE = 4096;        // points per k_code_scatter round (16 per thread)
 constexpr int FB_RUN = 32;           // consecutive grouped points per 16-lane group
-
-__global__ __launch_bounds__(256) void k_code_hist(const uint32_t *__restrict__ labels, uint32_t n, uint32_t ncodes,
-                                                   uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[FB_MAX_CODES];
-    for (uint32_t i = threadIdx.x; i < ncodes; i += 256) h[i] = 0;
-    __syncthreads();
-    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
-        const uint32_t code = labels[p];
-        if (code < ncodes) atomicAdd(&h[code], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ncodes; i += 256)
-        if (h[i]) atomicAdd(&hist[i], h[i]);
-}
 
 // cursor = exclusive scan of the histogram; each round ranks its points per code in LDS,
 // reserves one range per code with a global atomic, and writes the point indices
@@ -1011,13 +1000,14 @@ struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
                      const float *pnorm, const float *pdn, const uint32_t *cmax, const float *chalf,
                      const float *chalf_d, const Bound &bnd,
-                     uint32_t *labels, float *thr, uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes) {
+                     uint32_t *labels, float *thr, uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes,
+                     uint32_t *code_hist) {
         const uint32_t per_block = NW * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(WG), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
                            pdn, cmax, chalf, chalf_d, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
-                           pair_codes);
+                           pair_codes, code_hist);
         ST_LAUNCH_CHECK();
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
@@ -1033,7 +1023,7 @@ struct Sweep {
                            (const float *)nullptr, (const float *)nullptr, bnd,
                            (uint32_t *)nullptr, thr_slot,
                            (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
-                           (uint2 *)nullptr);
+                           (uint2 *)nullptr, (uint32_t *)nullptr);
         ST_LAUNCH_CHECK();
     }
 };
@@ -1133,22 +1123,22 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
     auto *pair_pts = wsT<uint32_t>(c, "kn.pairpts", n);
     auto *pair_codes = wsT<uint2>(c, "kn.paircodes", n);
     ST_HIP(hipMemsetAsync(&dstate->amb, 0, 16, c->stream));  // amb + ties + overflow + pairs
-    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
-                                        chalf_d, bnd,
-                                        labels, thr, amb, dstate, pair_pts, pair_codes)));
     const uint32_t ncodes = ctiles * 2;
     const int ld = aos_ld(d);
-    if (ncodes <= (uint32_t)FB_MAX_CODES && (ld == 48 || ld == 24 || ld == 12) && !getenv("ST_FIXROW_L2")) {
+    // decided points grouped by tile-half for k_fixrow_b: the sweep counts them per code
+    const bool grouped_fix =
+        ncodes <= (uint32_t)FB_MAX_CODES && (ld == 48 || ld == 24 || ld == 12) && !getenv("ST_FIXROW_L2");
+    auto *hist = grouped_fix ? wsT<uint32_t>(c, "kn.fbhist", ncodes) : nullptr;
+    if (hist) ST_HIP(hipMemsetAsync(hist, 0, ncodes * sizeof(uint32_t), c->stream));
+    ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
+                                        chalf_d, bnd,
+                                        labels, thr, amb, dstate, pair_pts, pair_codes, hist)));
+    if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
         KTimer kt(c, "kn.fixrow");
-        auto *hist = wsT<uint32_t>(c, "kn.fbhist", ncodes);
         auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
         auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
         auto *grouped = wsT<uint2>(c, "kn.fbpts2", n);
-        ST_HIP(hipMemsetAsync(hist, 0, ncodes * sizeof(uint32_t), c->stream));
-        hipLaunchKernelGGL(k_code_hist, dim3(grid_for(n, 256 * 64, 512)), dim3(256), 0, c->stream, labels,
-                           (uint32_t)n, ncodes, hist);
-        ST_LAUNCH_CHECK();
         scan_u32(c, hist, cursor, ncodes, ndec);
         hipLaunchKernelGGL(k_code_scatter, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream, labels,
                            (uint32_t)n, ncodes, cursor, grouped);

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K *__restrict__
         const uint64_t e = wbase_e + (uint64_t)r * 64 + lane;
         const bool valid = e < n;
         k[r] = valid ? keys[e] : (K)0;
-        v[r] = valid ? vals[e] : 0u;
+        v[r] = valid ? (vals ? vals[e] : (uint32_t)e) : 0u;  // no vals: the identity permutation
     }
 #pragma unroll
     for (int r = 0; r < RS_ROWS; ++r) {
@@ -417,6 +417,43 @@ void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t
                        nullptr, 0);
     ST_LAUNCH_CHECK();
     if (d_total) ST_HIP(hipMemcpyAsync(d_total, partial + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+}
+
+// stable sort of in_keys (left unchanged) with the identity permutation as values: the first pass
+// reads in_keys and takes value e for element e, the passes alternate so the last writes out_*
+void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int b0, int b1, uint32_t *out_keys,
+                         uint32_t *out_vals, const std::string &tag) {
+    if (n == 0) return;
+    const int passes = (b1 - b0 + 7) / 8;
+    if (n <= SS_MAX || passes == 0) {
+        ST_HIP(hipMemcpyAsync(out_keys, in_keys, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        iota_u32(c, out_vals, n);
+        radix_sort_impl<uint32_t>(c, out_keys, out_vals, n, b0, b1, tag);
+        return;
+    }
+    ST_REQUIRE(n < (1ull << 32), ST_ERR_ARG, "radix sort: n must be < 2^32");
+    const uint32_t nblocks = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint32_t *k2 = wsT<uint32_t>(c, tag + ".k2", n);
+    uint32_t *v2 = wsT<uint32_t>(c, tag + ".v2", n);
+    uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", (uint64_t)256 * nblocks);
+    // an even number of passes starts into the scratch pair, an odd one into out_*
+    uint32_t *dk = (passes & 1) ? out_keys : k2, *dv = (passes & 1) ? out_vals : v2;
+    const uint32_t *ka = in_keys, *va = nullptr;
+    for (int shift = b0, p = 0; shift < b1; shift += 8, ++p) {
+        const int bits = (b1 - shift) < 8 ? (b1 - shift) : 8;
+        hipLaunchKernelGGL(k_rs_hist<uint32_t>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, n, shift, bits, hist,
+                           nblocks);
+        ST_LAUNCH_CHECK();
+        scan_u32(c, hist, hist, (uint64_t)256 * nblocks, nullptr);
+        hipLaunchKernelGGL(k_rs_scatter<uint32_t>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, va, n, shift,
+                           bits, hist, nblocks, dk, dv);
+        ST_LAUNCH_CHECK();
+        ka = dk;
+        va = dv;
+        const bool to_out = dk == out_keys;
+        dk = to_out ? k2 : out_keys;
+        dv = to_out ? v2 : out_vals;
+    }
 }
 
 void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {
