@@ -194,3 +194,26 @@ def test_ply_sog_bundle_equals_host_one_call(ctx, tmp_path):
     want, used2 = ctx.sog_bundle({k: v for k, v in proc.items() if k not in ('nx', 'ny', 'nz')}, 3, draws, 0x6000,
                                  0x5a21)
     assert used == used2 and got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('n', [262_145, 4_194_305 + 7])
+def test_process_staged_copies_vs_oracle(ctx, n):
+    """The one-call host forms move columns of 1 MiB and more through the pinned slots that host
+    threads fill and drain (staged_h2d / staged_d2h; smaller ones go straight through the
+    runtime): a typed table whose columns fall on both sides of that line and across several
+    16 MiB slots, through processDataTable (filterByValue, filterNaN, a transform) and back."""
+    rng = np.random.default_rng(n)
+    src = [('x', rng.normal(0, 5, n).astype(np.float32)), ('y', rng.normal(0, 5, n).astype(np.float32)),
+           ('z', rng.normal(0, 5, n).astype(np.float32)),
+           ('c_f64', rng.normal(0, 1, n)), ('c_u8', rng.integers(0, 256, n).astype(np.uint8)),
+           ('c_i16', rng.integers(-30000, 30000, n).astype(np.int16))]
+    src[3][1][rng.random(n) < 0.01] = np.nan
+    acts = [{'kind': 'filterByValue', 'columnName': 'c_u8', 'comparator': 'gte', 'value': 3},
+            {'kind': 'filterNaN'},
+            {'kind': 'translate', 'value': (1.0, -2.0, 0.5)}]
+    out = ctx.process(src, acts)
+    want = oracle.process(src, acts)
+    assert [k for k, _ in out] == [k for k, _ in want]
+    for (k, a), (_, b) in zip(out, want):
+        _bytes_equal(a, b, k)
