@@ -113,6 +113,22 @@ def test_pack_compressed_edges_vs_oracle(ctx, n, C):
         same_bits(np.asarray(g).view(np.uint8), np.asarray(w).view(np.uint8))
 
 
+@pytest.mark.parametrize('n,C,kind', [(70_001, 15, 'perm'), (70_001, 15, 'repeats'), (1000, 8, 'repeats'),
+                                      (300_000, 3, 'perm')])
+def test_pack_compressed_orders_vs_oracle(ctx, n, C, kind):
+    """Chunk packing over a permutation and over an index list that repeats rows (the
+    reference's chunk loop, write-compressed-ply.ts:56-109, accepts any list of row indices)."""
+    cols = _table(n, C, 300 + n + C, spice=True)
+    rng = np.random.default_rng(n + C)
+    order = rng.permutation(n).astype(np.uint32)
+    if kind == 'repeats':
+        order[rng.integers(0, n, max(1, n // 100))] = order[0]
+    got = ctx.pack_compressed(cols, order, 3 * C)
+    want = oracle.pack_compressed(cols, order, 3 * C)
+    for g, w in zip(got, want):
+        same_bits(np.asarray(g).view(np.uint8), np.asarray(w).view(np.uint8))
+
+
 @pytest.mark.parametrize('kind', ['none', 'all', 'sparse', 'last_row', 'inf_only'])
 def test_filter_finite_edges_vs_oracle(ctx, kind):
     n = 3001
