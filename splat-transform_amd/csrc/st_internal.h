@@ -30,7 +30,14 @@ void set_last_error(const std::string &msg);
             throw ::st::Error(ST_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
-#define ST_LAUNCH_CHECK() ST_HIP(hipGetLastError())
+// ST_SYNC_CHECK=1 (read when a context is created): every launch check also synchronizes the
+// device, so a kernel's fault is reported at the launch that caused it (debugging)
+extern bool g_sync_check;
+#define ST_LAUNCH_CHECK()                                       \
+    do {                                                        \
+        ST_HIP(hipGetLastError());                              \
+        if (::st::g_sync_check) ST_HIP(hipDeviceSynchronize()); \
+    } while (0)
 
 #define ST_REQUIRE(cond, code, msg)                  \
     do {                                             \

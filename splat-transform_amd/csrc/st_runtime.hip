@@ -14,6 +14,7 @@
 namespace st {
 
 static thread_local std::string g_last_error;
+bool g_sync_check = false;
 
 void set_last_error(const std::string &msg) { g_last_error = msg; }
 
@@ -392,6 +393,7 @@ int st_ctx_create(int32_t device, st_ctx **out) {
         int n = 0;
         ST_HIP(hipGetDeviceCount(&n));
         ST_REQUIRE(n > 0, ST_ERR_HIP, "no HIP device visible (the MI355X product path has no CPU fallback)");
+        g_sync_check = getenv("ST_SYNC_CHECK") != nullptr;
         ST_ARG(device >= 0 && device < n, "device index out of range");
         hipDeviceProp_t prop;
         ST_HIP(hipGetDeviceProperties(&prop, device));

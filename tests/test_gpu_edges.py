@@ -318,3 +318,21 @@ def test_assign_pair_ties_without_ambiguous_points(ctx, swap):
     ctx.dev_kmeans_assign(tcols, k, tcen, lab)
     ctx.synchronize()
     same_bits(lab.cpu().numpy().astype(np.uint32), want)
+
+
+def test_sync_check_mode_vs_oracle(monkeypatch):
+    """ST_SYNC_CHECK=1 (read when a context is created) synchronizes the device after every
+    launch check, so a fault is reported at the launch that caused it; results are unchanged."""
+    n, C = 5000, 3
+    cols = _table(n, C, 61)
+    draws = oracle.mulberry32(5, 1 << 15)
+    monkeypatch.setenv('ST_SYNC_CHECK', '1')
+    c1 = sh.Context(0)
+    tex, meta, used = c1.sog(cols, 2, draws)
+    monkeypatch.delenv('ST_SYNC_CHECK')
+    c1.close()
+    sh.Context(0).close()  # a context created without it turns the checks off again
+    rc, otex, ometa, oused = oracle.sog(cols, C, 2, draws)
+    assert rc == 0 and used == oused
+    for k in tex:
+        same_bits(tex[k], otex[k])
