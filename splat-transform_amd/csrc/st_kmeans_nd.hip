@@ -149,11 +149,12 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
 
 // point B fragments: pfrag[t][s][lane] = 8 fp16 of B[k = 16s + 8h + j][p = 32t + (lane&31)];
 // also |sigma p| (rounded up) and the AoS f32 copy (row stride aos_ld(d), zero padded).
-// One workgroup per 256 points: the d column slices land in LDS (coalesced reads), then
-// the AoS rows and the 8 point tiles' fragments leave as contiguous runs (coalesced writes).
-constexpr int PF_PTS = 256;            // points per workgroup (8 tiles)
+// One workgroup per PF_PTS points: the d column slices land in LDS (coalesced reads), then
+// the AoS rows and the point tiles' fragments leave as contiguous runs (coalesced writes).
+constexpr int PF_PTS = 128;            // points (= threads) per workgroup (4 tiles): 31.5 KiB of LDS,
+                                       // five workgroups per CU
 constexpr int PF_LDS_LD = PF_PTS + 1;  // LDS column stride: row-wise reads hit distinct banks
-__global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
+__global__ __launch_bounds__(PF_PTS) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
                                                      int ks, float sigma, uint4 *pfrag, float *pnorm, float *pdn,
                                                      float *aos) {
     __shared__ float x[61 * PF_LDS_LD];  // d <= 61
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
     const int ld = aos_ld(d), q4 = ld / 4;
     const uint32_t rows = (uint32_t)min((uint64_t)PF_PTS, n - min(n, p0));
     float4 *dst = reinterpret_cast<float4 *>(aos + p0 * ld);
-    for (uint32_t f = j; f < rows * q4; f += 256) {
+    for (uint32_t f = j; f < rows * q4; f += PF_PTS) {
         const uint32_t r = f / q4, c = (f % q4) * 4;
         float4 v;
         v.x = c + 0 < (uint32_t)d ? x[(c + 0) * PF_LDS_LD + r] : 0.0f;
@@ -197,10 +198,10 @@ __global__ __launch_bounds__(256) void k_point_frags(const float *const *cols, i
         v.w = c + 3 < (uint32_t)d ? x[(c + 3) * PF_LDS_LD + r] : 0.0f;
         dst[f] = v;
     }
-    // fragments of the 8 tiles (contiguous: tile-major, then k-step, then lane)
+    // fragments of the workgroup's tiles (contiguous: tile-major, then k-step, then lane)
     const uint32_t t0 = blockIdx.x * (PF_PTS / 32);
     const uint32_t tiles = min((uint32_t)(PF_PTS / 32), ntiles - t0);
-    for (uint32_t f = j; f < tiles * ks * 64; f += 256) {
+    for (uint32_t f = j; f < tiles * ks * 64; f += PF_PTS) {
         const uint32_t t = f / (ks * 64), rem = f % (ks * 64);
         const int st = (int)(rem / 64), h = (int)((rem % 64) / 32), l = (int)(rem % 32);
         const uint32_t r = t * 32 + l;
@@ -1078,7 +1079,7 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     }
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
-    hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(256), 0,
+    hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(PF_PTS), 0,
                        c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, pdn, aos);
     ST_LAUNCH_CHECK();
     c->kn_sigma = sigma;
