@@ -184,6 +184,15 @@ void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b
 // the same from read-only keys with the identity permutation as values, into out_keys / out_vals
 void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int begin_bit, int end_bit,
                          uint32_t *out_keys, uint32_t *out_vals, const std::string &tag);
+// the general form: in_vals null = the identity permutation; out_vals may alias in_vals when the
+// pass count is even (the first pass writes the scratch pair).  hist0, when not null, holds the
+// first digit's per-tile counts in the sort's layout (count of digit d in tile t at
+// d * radix_tiles(n) + t, tiles of RADIX_TILE elements), produced by the caller's key kernel;
+// it is scanned in place and reused as the histogram buffer of the later passes
+constexpr int RADIX_TILE = 4096;
+inline uint32_t radix_tiles(uint64_t n) { return (uint32_t)((n + RADIX_TILE - 1) / RADIX_TILE); }
+void radix_sort_u32_from(st_ctx *c, const uint32_t *in_keys, const uint32_t *in_vals, uint64_t n, int begin_bit,
+                         int end_bit, uint32_t *out_keys, uint32_t *out_vals, uint32_t *hist0, const std::string &tag);
 // as radix_sort_u32, but the result stays in whichever buffer pair the last pass wrote
 // (the caller's or the workspace's): *out_keys / *out_vals point at it
 void radix_sort_u32_inplace_or_swap(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1,

@@ -177,11 +177,13 @@ __global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ 
 }
 
 // ordering.ts:32-65 per segment
+// (level 0: seg_start null, the one segment starts at 0); also zeroes the level's big-run count
 __global__ void k_seg_info(const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ z,
                            const uint32_t *__restrict__ idx, const uint32_t *__restrict__ seg_start,
-                           const uint32_t *__restrict__ ext, uint32_t nseg, SegInfo *info) {
+                           const uint32_t *__restrict__ ext, uint32_t nseg, SegInfo *info, uint32_t *bigcnt) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *bigcnt = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
-        const uint32_t first = idx[seg_start[s]];
+        const uint32_t first = idx[seg_start ? seg_start[s] : 0u];
         const float f[3] = {x[first], y[first], z[first]};
         SegInfo si{};
         bool valid = true, all_zero = true;
@@ -229,6 +231,45 @@ __global__ __launch_bounds__(256) void k_keys(const float *__restrict__ x, const
         keys[j] = ((K)s << 30) | (K)m;
         vals[j] = row;
     }
+}
+
+// level 0: one segment, P = identity -- keys only (the sort takes idx itself as its values) and
+// the first radix digit's count per sort tile (RADIX_TILE keys per workgroup), so the sort
+// skips its first histogram pass
+__global__ __launch_bounds__(256) void k_keys0(const float *__restrict__ x, const float *__restrict__ y,
+                                               const float *__restrict__ z, const uint32_t *__restrict__ idx,
+                                               const SegInfo *__restrict__ info, uint64_t n,
+                                               uint32_t *__restrict__ keys, uint32_t *__restrict__ hist,
+                                               uint32_t ntiles) {
+    constexpr int ROWS = RADIX_TILE / 256;
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const SegInfo si = info[0];
+    const uint64_t base = (uint64_t)blockIdx.x * RADIX_TILE;
+    uint32_t rows_[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
+        rows_[r] = j < n ? idx[j] : 0u;
+    }
+#pragma unroll 4
+    for (int r = 0; r < ROWS; ++r) {
+        const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
+        if (j >= n) break;
+        const uint32_t row = rows_[r];
+        uint32_t m = 0;
+        if (si.ok) {
+            const uint32_t ix = axis_q(x[row], si.mn[0], si.mul[0]);
+            const uint32_t iy = axis_q(y[row], si.mn[1], si.mul[1]);
+            const uint32_t iz = axis_q(z[row], si.mn[2], si.mul[2]);
+            m = (part1by2(iz) << 2) + (part1by2(iy) << 1) + part1by2(ix);
+        }
+        keys[j] = m;
+        atomicAdd(&h[m & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void k_scatter_back(const uint32_t *__restrict__ P, const uint32_t *__restrict__ vals,
@@ -288,19 +329,13 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
     if (n == 0) return;
     ST_REQUIRE(n < (1ull << 32) - 1, ST_ERR_ARG, "morton: n must be < 2^32-1");
     auto *h = static_cast<uint32_t *>(pinned(c, 64));
-    // active segment list
+    // active segment list (level 0's single segment is implicit)
     auto *seg_start = wsT<uint32_t>(c, "mo.seg_start", n / 257 + 2);
     auto *seg_len = wsT<uint32_t>(c, "mo.seg_len", n / 257 + 2);
     auto *nseg_start = wsT<uint32_t>(c, "mo.nseg_start", n / 257 + 2);
     auto *nseg_len = wsT<uint32_t>(c, "mo.nseg_len", n / 257 + 2);
     auto *seg_off = wsT<uint32_t>(c, "mo.seg_off", n / 257 + 3);
     uint32_t nseg = 1;
-    {
-        uint32_t one[2] = {0u, (uint32_t)n};
-        ST_HIP(hipMemcpyAsync(seg_start, &one[0], 4, hipMemcpyHostToDevice, c->stream));
-        ST_HIP(hipMemcpyAsync(seg_len, &one[1], 4, hipMemcpyHostToDevice, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-    }
     uint64_t total = n;
     auto *P = wsT<uint32_t>(c, "mo.P", n);
     auto *S = wsT<uint32_t>(c, "mo.S", n);
@@ -331,13 +366,28 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
                                (uint32_t *)nullptr);
         }
         ST_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx, seg_start,
-                           ext, nseg, info);
+        hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
+                           single ? nullptr : seg_start, ext, nseg, info, bigcnt);
         ST_LAUNCH_CHECK();
         int seg_bits = 0;
         while ((1u << seg_bits) < nseg) ++seg_bits;
         const unsigned g = grid_for(total, 256, 8192);
-        if (seg_bits + 30 <= 32) {
+        if (single) {
+            // keys + first digit counts, then the sort reads idx as its values and its last
+            // (fourth) pass writes the ordered rows straight back into idx
+            const uint32_t nt = radix_tiles(n);
+            auto *keys = wsT<uint32_t>(c, "mo.k32", n + 1);
+            auto *hist = wsT<uint32_t>(c, "mo.hist0", (size_t)256 * nt);
+            hipLaunchKernelGGL(k_keys0, dim3(nt), dim3(256), 0, c->stream, x, y, z, idx, info, n, keys, hist, nt);
+            ST_LAUNCH_CHECK();
+            radix_sort_u32_from(c, keys, idx, n, 0, 30, keys, idx, hist, "mo.rs32");
+            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
+                               bigcnt);
+            hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
+                               c->stream, keys, total, bigpos, bigcnt, P, 1, nseg_start, nseg_len);
+            ST_LAUNCH_CHECK();
+            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
+        } else if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
             hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
                                (int)single, keys, vals);
@@ -345,7 +395,6 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             uint32_t *skeys = keys, *svals = vals;
             radix_sort_u32_inplace_or_swap(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs32", &skeys, &svals);
             hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, svals, total, (int)single, idx);
-            ST_HIP(hipMemsetAsync(bigcnt, 0, 4, c->stream));
             hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, skeys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
@@ -359,7 +408,6 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_LAUNCH_CHECK();
             radix_sort_u64(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs64");
             hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, (int)single, idx);
-            ST_HIP(hipMemsetAsync(bigcnt, 0, 4, c->stream));
             hipLaunchKernelGGL(k_big_starts<uint64_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint64_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,

@@ -89,6 +89,7 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ROWS = 16;
 constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_TILE = RS_THREADS * RS_ROWS;  // 4096
+static_assert(RS_TILE == RADIX_TILE, "st_internal.h's tile size");
 constexpr int RS_WAVE_SPAN = 64 * RS_ROWS;     // 1024
 
 template <typename K>
@@ -419,15 +420,20 @@ void scan_u32(st_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t
     if (d_total) ST_HIP(hipMemcpyAsync(d_total, partial + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
 }
 
-// stable sort of in_keys (left unchanged) with the identity permutation as values: the first pass
-// reads in_keys and takes value e for element e, the passes alternate so the last writes out_*
-void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int b0, int b1, uint32_t *out_keys,
-                         uint32_t *out_vals, const std::string &tag) {
+// stable sort of in_keys (left unchanged) with in_vals (null: the identity permutation) as
+// values: the first pass reads the inputs, the passes alternate so the last writes out_*
+void radix_sort_u32_from(st_ctx *c, const uint32_t *in_keys, const uint32_t *in_vals, uint64_t n, int b0, int b1,
+                         uint32_t *out_keys, uint32_t *out_vals, uint32_t *hist0, const std::string &tag) {
     if (n == 0) return;
     const int passes = (b1 - b0 + 7) / 8;
+    ST_REQUIRE(!(((in_vals && in_vals == out_vals) || in_keys == out_keys) && (passes & 1)), ST_ERR_INTERNAL,
+               "radix sort: in-place outputs need an even pass count");
     if (n <= SS_MAX || passes == 0) {
-        ST_HIP(hipMemcpyAsync(out_keys, in_keys, n * 4, hipMemcpyDeviceToDevice, c->stream));
-        iota_u32(c, out_vals, n);
+        if (out_keys != in_keys)
+            ST_HIP(hipMemcpyAsync(out_keys, in_keys, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (!in_vals) iota_u32(c, out_vals, n);
+        else if (out_vals != in_vals)
+            ST_HIP(hipMemcpyAsync(out_vals, in_vals, n * 4, hipMemcpyDeviceToDevice, c->stream));
         radix_sort_impl<uint32_t>(c, out_keys, out_vals, n, b0, b1, tag);
         return;
     }
@@ -435,15 +441,17 @@ void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int b0,
     const uint32_t nblocks = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     uint32_t *k2 = wsT<uint32_t>(c, tag + ".k2", n);
     uint32_t *v2 = wsT<uint32_t>(c, tag + ".v2", n);
-    uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", (uint64_t)256 * nblocks);
+    uint32_t *hist = hist0 ? hist0 : wsT<uint32_t>(c, tag + ".hist", (uint64_t)256 * nblocks);
     // an even number of passes starts into the scratch pair, an odd one into out_*
     uint32_t *dk = (passes & 1) ? out_keys : k2, *dv = (passes & 1) ? out_vals : v2;
-    const uint32_t *ka = in_keys, *va = nullptr;
+    const uint32_t *ka = in_keys, *va = in_vals;
     for (int shift = b0, p = 0; shift < b1; shift += 8, ++p) {
         const int bits = (b1 - shift) < 8 ? (b1 - shift) : 8;
-        hipLaunchKernelGGL(k_rs_hist<uint32_t>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, n, shift, bits, hist,
-                           nblocks);
-        ST_LAUNCH_CHECK();
+        if (p > 0 || !hist0) {
+            hipLaunchKernelGGL(k_rs_hist<uint32_t>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, n, shift, bits,
+                               hist, nblocks);
+            ST_LAUNCH_CHECK();
+        }
         scan_u32(c, hist, hist, (uint64_t)256 * nblocks, nullptr);
         hipLaunchKernelGGL(k_rs_scatter<uint32_t>, dim3(nblocks), dim3(RS_THREADS), 0, c->stream, ka, va, n, shift,
                            bits, hist, nblocks, dk, dv);
@@ -454,6 +462,11 @@ void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int b0,
         dk = to_out ? k2 : out_keys;
         dv = to_out ? v2 : out_vals;
     }
+}
+
+void radix_sort_u32_iota(st_ctx *c, const uint32_t *in_keys, uint64_t n, int b0, int b1, uint32_t *out_keys,
+                         uint32_t *out_vals, const std::string &tag) {
+    radix_sort_u32_from(c, in_keys, nullptr, n, b0, b1, out_keys, out_vals, nullptr, tag);
 }
 
 void radix_sort_u32(st_ctx *c, uint32_t *keys, uint32_t *vals, uint64_t n, int b0, int b1, const std::string &tag) {

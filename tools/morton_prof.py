@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Morton ordering (generateOrdering) of 10M Gaussian device columns, repeated: run under
+rocprofv3 --kernel-trace --stats for the per-kernel split of one config-3 Morton stage."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
+import torch
+
+import splat_hip as sh
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+dev = torch.device('cuda', 0)
+stream = torch.cuda.Stream(dev)
+torch.cuda.set_stream(stream)
+ctx = sh.Context(0)
+ctx.set_stream(stream.cuda_stream)
+g = torch.Generator(device=dev)
+g.manual_seed(7)
+x, y, z = (torch.randn(n, generator=g, device=dev) for _ in range(3))
+order = torch.empty(n, dtype=torch.int32, device=dev)
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+best = 1e9
+for r in range(12):
+    order.copy_(torch.arange(n, dtype=torch.int32, device=dev))
+    ev[0].record(stream)
+    ctx.dev_morton_order(x, y, z, order)
+    ev[1].record(stream)
+    stream.synchronize()
+    if r >= 2:
+        best = min(best, ev[0].elapsed_time(ev[1]))
+print(f'morton n={n}: {best * 1e3:.1f} us per call (best of 10)')
