@@ -92,21 +92,43 @@ constexpr int RS_TILE = RS_THREADS * RS_ROWS;  // 4096
 static_assert(RS_TILE == RADIX_TILE, "st_internal.h's tile size");
 constexpr int RS_WAVE_SPAN = 64 * RS_ROWS;     // 1024
 
+// per-tile digit counts: one LDS histogram per wave (less same-bin contention), 32-bit keys
+// read as four 16-byte quads per thread on whole aligned tiles
 template <typename K>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K *__restrict__ keys, uint64_t n, int shift, int bits,
                                                         uint32_t *__restrict__ hist, uint32_t nblocks) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+    __shared__ uint32_t h[RS_WAVES][256];
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
     const uint32_t mask = (1u << bits) - 1u;
+    uint32_t *hw = h[threadIdx.x >> 6];
+    bool quads = false;
+    if constexpr (sizeof(K) == 4) quads = base + RS_TILE <= n && (((uintptr_t)(keys + base)) & 15u) == 0;
+    if (quads) {
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+        uint4 q[RS_ROWS / 4];
+#pragma unroll
+        for (int r = 0; r < RS_ROWS / 4; ++r) q[r] = k4[r * RS_THREADS + threadIdx.x];
+#pragma unroll
+        for (int r = 0; r < RS_ROWS / 4; ++r) {
+            atomicAdd(&hw[(q[r].x >> shift) & mask], 1u);
+            atomicAdd(&hw[(q[r].y >> shift) & mask], 1u);
+            atomicAdd(&hw[(q[r].z >> shift) & mask], 1u);
+            atomicAdd(&hw[(q[r].w >> shift) & mask], 1u);
+        }
+    } else {
 #pragma unroll 4
-    for (int r = 0; r < RS_ROWS; ++r) {
-        const uint64_t e = base + (uint64_t)r * RS_THREADS + threadIdx.x;
-        if (e < n) atomicAdd(&h[(uint32_t)(keys[e] >> shift) & mask], 1u);
+        for (int r = 0; r < RS_ROWS; ++r) {
+            const uint64_t e = base + (uint64_t)r * RS_THREADS + threadIdx.x;
+            if (e < n) atomicAdd(&hw[(uint32_t)(keys[e] >> shift) & mask], 1u);
+        }
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < RS_WAVES; ++i) t += h[i][threadIdx.x];
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = t;
 }
 
 // One tile of RS_TILE elements: wave-level ranks by ballot (stable), then the tile is
