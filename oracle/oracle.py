@@ -116,7 +116,7 @@ def filter_finite(col_list):
 def morton_order(x, y, z, indices=None):
     n = len(x)
     idx = np.arange(n, dtype=np.uint32) if indices is None else np.ascontiguousarray(indices, np.uint32).copy()
-    lib().st_o_morton_order(_p(x), _p(y), _p(z), _p(idx), ctypes.c_uint64(n))
+    lib().st_o_morton_order(_p(x), _p(y), _p(z), _p(idx), ctypes.c_uint64(len(idx)))
     return idx
 
 

@@ -86,7 +86,7 @@ def test_morton_degenerate_vs_oracle(ctx, case, n):
     same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
 
 
-@pytest.mark.parametrize('n', [65535, 65536, 65537, 4096 * 25 + 1, 4096 * 37, 1_500_007])
+@pytest.mark.parametrize('n', [2048, 2049, 4095, 65535, 65536, 65537, 4096 * 25 + 1, 4096 * 37, 1_500_007])
 def test_morton_onesweep_sizes_vs_oracle(ctx, n):
     """Level-0 sorts of whole and ragged 4,096-key tiles, and a caller-supplied permutation of
     the indices (the values carried through the passes are idx[j]: ordering.ts:4-20 sorts the
@@ -99,6 +99,24 @@ def test_morton_onesweep_sizes_vs_oracle(ctx, n):
     perm = rng.permutation(n).astype(np.uint32)
     same_bits(ctx.morton_order(x, y, z, perm), oracle.morton_order(x, y, z, perm))
     same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
+
+
+@pytest.mark.parametrize('n,m', [(3000, 2000), (100_000, 70_001), (50_000, 200_003)])
+def test_morton_index_subsets_vs_oracle(ctx, n, m):
+    """generateOrdering over an index list that is not a permutation (a subset with repeated
+    rows, shorter or longer than the table): extents, keys and the stable order all follow
+    the given indices (ordering.ts:4-20); level 0 sorts idx in place as its own values."""
+    import torch
+    dev = torch.device('cuda', 0)
+    rng = np.random.default_rng(m)
+    x, y, z = (rng.normal(0, 3, n).astype(np.float32) for _ in range(3))
+    x[rng.random(n) < 0.01] = np.nan
+    idx = rng.integers(0, n, m).astype(np.uint32)
+    tx, ty, tz = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    tidx = torch.from_numpy(idx.view(np.int32).copy()).to(dev)
+    ctx.dev_morton_order(tx, ty, tz, tidx)
+    ctx.synchronize()
+    same_bits(tidx.cpu().numpy().view(np.uint32), oracle.morton_order(x, y, z, idx))
 
 
 @pytest.mark.parametrize('n,C', [(1, 0), (255, 3), (256, 15), (257, 8), (1000, 15), (4097, 3)])
