@@ -70,19 +70,15 @@ __global__ void k_ext_init(uint32_t *ext, uint32_t nseg) {
     }
 }
 
-// segmented NaN-ignoring min/max via ordered-int atomics; block-level pre-reduction
-// when the whole block lies in one segment (the level-0 case).
-// single (level 0): one segment, P = identity, S = 0 -- neither is read, and each block
-// leaves its six extents in part[block] (no same-address atomics; k_ext_final reduces)
+// level 0 (one segment, P = identity, S = 0 -- neither is read): each block leaves its six
+// extents (NaN-ignoring min / max as ordered ints) in part[block]; k_ext_final reduces them
 __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const float *__restrict__ y,
                                              const float *__restrict__ z, const uint32_t *__restrict__ idx,
-                                             const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
-                                             uint64_t total, int single, uint32_t *ext, uint32_t *part) {
+                                             uint64_t total, uint32_t *part) {
     __shared__ uint32_t red[6][4];
     const uint64_t base = (uint64_t)blockIdx.x * 4096;
     if (base >= total) return;
     const uint64_t last = (base + 4096 < total ? base + 4096 : total) - 1;
-    const bool one_seg = single || S[base] == S[last];
     const float *cols[3] = {x, y, z};
     uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
     // all 16 rows' indices, then all their coordinates, in flight before the first test
@@ -90,8 +86,7 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
-        const uint64_t jj = j > last ? last : j;
-        rows_[r] = single ? idx[jj] : idx[P[jj]];
+        rows_[r] = idx[j > last ? last : j];
     }
     float vals_[16][3];
 #pragma unroll
@@ -102,23 +97,16 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
     for (int r = 0; r < 16; ++r) {
         const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
         if (j > last) break;
-        const uint32_t s = single ? 0u : S[j];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             const float v = vals_[r][a];
             if (v == v) {
                 const uint32_t k = fkey(v);
-                if (one_seg) {
-                    mn[a] = k < mn[a] ? k : mn[a];
-                    mx[a] = k > mx[a] ? k : mx[a];
-                } else {
-                    atomicMin(&ext[s * 6 + a], k);
-                    atomicMax(&ext[s * 6 + 3 + a], k);
-                }
+                mn[a] = k < mn[a] ? k : mn[a];
+                mx[a] = k > mx[a] ? k : mx[a];
             }
         }
     }
-    if (!one_seg) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -138,13 +126,122 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
         const int q = threadIdx.x;
         uint32_t v = red[q][0];
         for (int i = 1; i < 4; ++i) v = q < 3 ? (red[q][i] < v ? red[q][i] : v) : (red[q][i] > v ? red[q][i] : v);
-        if (single) {
-            part[(uint64_t)blockIdx.x * 6 + q] = v;
-            return;
+        part[(uint64_t)blockIdx.x * 6 + q] = v;
+    }
+}
+
+// deeper levels: the segments are runs of > 256 elements, contiguous in P order, so the 4,096
+// elements of a block touch at most 17 of them and a wave's 1,024 consecutive elements at most
+// 5.  Lanes keep min / max for the wave's current segment while whole 64-element rows stay in
+// it; on a change the wave reduces them by shuffles into the block's LDS slot of that segment
+// (rows that straddle a boundary go to the slots lane by lane); the block then merges its
+// slots into the global extents with one atomic per (segment, value).  (Per-element global
+// atomics on a handful of addresses took 2.5 ms at 10M on a lattice input.)
+constexpr int EXT_SLOTS = 4096 / 257 + 2;
+__global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, const float *__restrict__ y,
+                                                 const float *__restrict__ z, const uint32_t *__restrict__ idx,
+                                                 const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
+                                                 uint64_t total, uint32_t *ext) {
+    __shared__ uint32_t slot[EXT_SLOTS * 6];
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    if (base >= total) return;
+    const uint64_t last = (base + 4096 < total ? base + 4096 : total) - 1;
+    const uint32_t s0 = S[base], s1 = S[last];
+    for (int i = threadIdx.x; i < EXT_SLOTS * 6; i += 256) slot[i] = (i % 6) < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const float *cols[3] = {x, y, z};
+    const int lane = threadIdx.x & 63;
+    const uint64_t wb = base + (uint64_t)(threadIdx.x >> 6) * 1024;
+    uint32_t seg_[16], rows_[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint64_t j = wb + (uint64_t)r * 64 + lane;
+        const uint64_t jj = j > last ? last : j;
+        seg_[r] = j > last ? 0xffffffffu : S[jj];
+        rows_[r] = idx[P[jj]];
+    }
+    float vals_[16][3];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) vals_[r][a] = cols[a][rows_[r]];
+    auto take = [&](uint32_t s, const float *v) {  // one lane into its segment's slot
+        const uint32_t q = s - s0;
+        uint32_t *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)s * 6];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+            if (v[a] == v[a]) {
+                atomicMin(&dst[a], fkey(v[a]));
+                atomicMax(&dst[3 + a], fkey(v[a]));
+            }
+    };
+    uint32_t cur = 0xffffffffu;  // wave-uniform
+    uint32_t mn[3], mx[3];
+    auto reset = [&] {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = 0xffffffffu;
+            mx[a] = 0u;
         }
-        const uint32_t s = S[base];
-        if (q < 3) atomicMin(&ext[s * 6 + q], v);
-        else atomicMax(&ext[s * 6 + q], v);
+    };
+    auto flush = [&] {
+        if (cur == 0xffffffffu) return;
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint32_t t0 = __shfl_xor(mn[a], o, 64), t1 = __shfl_xor(mx[a], o, 64);
+                mn[a] = t0 < mn[a] ? t0 : mn[a];
+                mx[a] = t1 > mx[a] ? t1 : mx[a];
+            }
+        if (lane == 0) {
+            const uint32_t q = cur - s0;
+            uint32_t *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)cur * 6];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (mn[a] != 0xffffffffu) atomicMin(&dst[a], mn[a]);
+                if (mx[a] != 0u) atomicMax(&dst[3 + a], mx[a]);
+            }
+        }
+        cur = 0xffffffffu;
+    };
+    reset();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t s = seg_[r];
+        const uint32_t sf = __builtin_amdgcn_readfirstlane(s);
+        if (__ballot(s != sf) == 0ull) {  // the whole row lies in one segment (or past the end)
+            if (sf == 0xffffffffu) continue;
+            if (sf != cur) {
+                flush();
+                reset();
+                cur = sf;
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float v = vals_[r][a];
+                if (v == v) {
+                    const uint32_t k = fkey(v);
+                    mn[a] = k < mn[a] ? k : mn[a];
+                    mx[a] = k > mx[a] ? k : mx[a];
+                }
+            }
+        } else {
+            flush();
+            reset();
+            if (s != 0xffffffffu) take(s, vals_[r]);
+        }
+    }
+    flush();
+    __syncthreads();
+    const uint32_t used = (s1 - s0 + 1) * 6;
+    for (uint32_t i = threadIdx.x; i < used && i < (uint32_t)EXT_SLOTS * 6; i += 256) {
+        const uint32_t v = slot[i], q = i / 6, a = i % 6;
+        if (a < 3) {
+            if (v != 0xffffffffu) atomicMin(&ext[(uint64_t)(s0 + q) * 6 + a], v);
+        } else if (v != 0u) {
+            atomicMax(&ext[(uint64_t)(s0 + q) * 6 + a], v);
+        }
     }
 }
 
@@ -174,6 +271,31 @@ __global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ 
         for (int i = 1; i < 4; ++i) r = q < 3 ? (red[q][i] < r ? red[q][i] : r) : (red[q][i] > r ? red[q][i] : r);
         ext[q] = r;
     }
+}
+
+// segments that sort (info.ok): flags and member counts for the two scans below
+__global__ void k_seg_flags(const SegInfo *__restrict__ info, const uint32_t *__restrict__ seg_len, uint32_t nseg,
+                            uint32_t *__restrict__ flag, uint32_t *__restrict__ mlen) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
+        const uint32_t ok = info[s].ok;
+        flag[s] = ok;
+        mlen[s] = ok ? seg_len[s] : 0u;
+    }
+}
+
+// the sorting segments only (ordering.ts:53-61 returns before sorting the others): their
+// starts, element offsets and infos, in order
+__global__ void k_seg_compact(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                              const uint32_t *__restrict__ seg_start, const uint32_t *__restrict__ moff,
+                              const SegInfo *__restrict__ info, uint32_t nseg, uint32_t *__restrict__ cstart,
+                              uint32_t *__restrict__ coff, SegInfo *__restrict__ cinfo) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)
+        if (flag[s]) {
+            const uint32_t q = pos[s];
+            cstart[q] = seg_start[s];
+            coff[q] = moff[s];
+            cinfo[q] = info[s];
+        }
 }
 
 // ordering.ts:32-65 per segment
@@ -358,17 +480,47 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         const unsigned eb = (unsigned)((total + 4095) / 4096);
         if (single) {
             auto *part = wsT<uint32_t>(c, "mo.extpart", (size_t)eb * 6);
-            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, 1, ext, part);
+            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, total, part);
             hipLaunchKernelGGL(k_ext_final, dim3(1), dim3(256), 0, c->stream, part, eb, ext);
         } else {
             hipLaunchKernelGGL(k_ext_init, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
-            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, 0, ext,
-                               (uint32_t *)nullptr);
+            hipLaunchKernelGGL(k_ext_seg, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, ext);
         }
         ST_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
                            single ? nullptr : seg_start, ext, nseg, info, bigcnt);
         ST_LAUNCH_CHECK();
+        if (!single) {
+            // only segments with usable extents are keyed and sorted: the others keep their order
+            // and never recurse (ordering.ts:53-61), so their members leave the level here
+            auto *flag = wsT<uint32_t>(c, "mo.flag", n / 257 + 2);
+            auto *pos = wsT<uint32_t>(c, "mo.pos", n / 257 + 3);
+            auto *mlen = wsT<uint32_t>(c, "mo.mlen", n / 257 + 2);
+            auto *moff = wsT<uint32_t>(c, "mo.moff", n / 257 + 3);
+            hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, info, seg_len,
+                               nseg, flag, mlen);
+            ST_LAUNCH_CHECK();
+            scan_u32(c, flag, pos, nseg, pos + nseg);
+            scan_u32(c, mlen, moff, nseg, moff + nseg);
+            ST_HIP(hipMemcpyAsync(h + 1, pos + nseg, 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(h + 2, moff + nseg, 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipStreamSynchronize(c->stream));
+            const uint32_t kept = h[1];
+            if (kept == 0) break;
+            if (kept < nseg) {
+                auto *cstart = wsT<uint32_t>(c, "mo.cstart", n / 257 + 2);
+                auto *cinfo = static_cast<SegInfo *>(ws(c, "mo.cinfo", sizeof(SegInfo) * (size_t)kept));
+                hipLaunchKernelGGL(k_seg_compact, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, flag, pos,
+                                   seg_start, moff, info, nseg, cstart, seg_off, cinfo);
+                total = h[2];
+                nseg = kept;
+                info = cinfo;
+                // (seg_start is not read again this level: the next level's list comes from P)
+                hipLaunchKernelGGL(k_expand, dim3(grid_for(total, 256, 8192)), dim3(256), 0, c->stream, cstart,
+                                   seg_off, nseg, total, P, S);
+                ST_LAUNCH_CHECK();
+            }
+        }
         int seg_bits = 0;
         while ((1u << seg_bits) < nseg) ++seg_bits;
         const unsigned g = grid_for(total, 256, 8192);

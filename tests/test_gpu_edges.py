@@ -59,8 +59,8 @@ def test_morton_ragged_vs_oracle(ctx, n):
 
 
 @pytest.mark.parametrize('case', ['all_equal', 'nan_coords', 'inf_extent', 'one_axis_flat', 'big_equal_run',
-                                  'neg_zero'])
-@pytest.mark.parametrize('n', [5000, 70001])
+                                  'neg_zero', 'lattice', 'blobs', 'blobs_flat'])
+@pytest.mark.parametrize('n', [5000, 70001, 1_000_003])
 def test_morton_degenerate_vs_oracle(ctx, case, n):
     """ordering.ts:53-65: zero-length extents, non-finite extents (ordering skipped), NaN
     coordinates (key 0), equal-key runs longer than 256 (recursion with their own extents)."""
@@ -83,6 +83,17 @@ def test_morton_degenerate_vs_oracle(ctx, case, n):
     elif case == 'neg_zero':
         x[::2] = -0.0
         x[1::2] = 0.0
+    elif case == 'lattice':  # many exactly equal points: runs whose own extents are all zero
+        for a in (x, y, z):
+            a[:] = np.round(a * 0.8) / 0.8
+    elif case in ('blobs', 'blobs_flat'):  # tight blobs: several recursion levels, many segments
+        m = rng.random(n) < 0.6
+        centre = rng.integers(0, 300, n).astype(np.float32)
+        for a in (x, y, z):
+            a[m] = (centre[m] * 0.03 + a[m] * 1e-5).astype(np.float32)
+        if case == 'blobs_flat':  # some blobs flat on one axis, NaN members in others
+            z[m & (centre < 100)] = 1.0
+            x[m & (centre > 250) & (rng.random(n) < 0.01)] = np.nan
     same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
 
 

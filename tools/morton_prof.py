@@ -11,6 +11,7 @@ import torch
 import splat_hip as sh
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+kind = sys.argv[2] if len(sys.argv) > 2 else 'gauss'  # gauss | clustered | grid
 dev = torch.device('cuda', 0)
 stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
@@ -19,6 +20,16 @@ ctx.set_stream(stream.cuda_stream)
 g = torch.Generator(device=dev)
 g.manual_seed(7)
 x, y, z = (torch.randn(n, generator=g, device=dev) for _ in range(3))
+if kind == 'clustered':
+    # half the splats in 64 tight blobs (1e-5 of the extent): deep equal-key runs, many segments
+    m = torch.rand(n, generator=g, device=dev) < 0.5
+    centre = torch.randint(0, 64, (n,), generator=g, device=dev).float()
+    for a in (x, y, z):
+        a[m] = centre[m] * 0.05 + a[m] * 1e-5
+elif kind == 'grid':
+    # coordinates on a coarse lattice: many exactly equal points (runs that never split)
+    for a in (x, y, z):
+        a.copy_(torch.round(a * 4) / 4)
 order = torch.empty(n, dtype=torch.int32, device=dev)
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 best = 1e9
@@ -30,4 +41,4 @@ for r in range(12):
     stream.synchronize()
     if r >= 2:
         best = min(best, ev[0].elapsed_time(ev[1]))
-print(f'morton n={n}: {best * 1e3:.1f} us per call (best of 10)')
+print(f'morton n={n} {kind}: {best * 1e3:.1f} us per call (best of 10)')
