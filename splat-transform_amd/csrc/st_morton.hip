@@ -10,9 +10,12 @@
 //   sort      stable LSD radix sort of (key, index) -- segments keep their
 //             slots, their members are reordered in place
 //   runs      equal-key runs > 256 inside sorted segments become next level
-// Level 0 is a single segment over all n (u32 keys, 4 passes); deeper levels
-// carry only the big buckets.  Non-finite or zero extents stop a segment
-// exactly where ordering.ts:53-61 returns.
+// Level 0 is a single segment over all n: block-partial extents (k_ext), keys
+// plus the first digit's tile counts (k_keys0), and a 4-pass u32 sort that reads
+// idx as its values and writes the order back into it.  Deeper levels carry only
+// the big runs: segmented extents through per-block LDS slots (k_ext_seg), and
+// only segments with usable extents are keyed and sorted -- non-finite or zero
+// extents stop a segment exactly where ordering.ts:53-61 returns.
 #include "st_internal.h"
 #include "st_jsmath.h"
 
@@ -335,12 +338,12 @@ template <typename K>
 __global__ __launch_bounds__(256) void k_keys(const float *__restrict__ x, const float *__restrict__ y,
                                               const float *__restrict__ z, const uint32_t *__restrict__ idx,
                                               const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
-                                              const SegInfo *__restrict__ info, uint64_t total, int single,
+                                              const SegInfo *__restrict__ info, uint64_t total,
                                               K *__restrict__ keys, uint32_t *__restrict__ vals) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
-        const uint32_t p = single ? (uint32_t)j : P[j];
-        const uint32_t s = single ? 0u : S[j];
+        const uint32_t p = P[j];
+        const uint32_t s = S[j];
         const uint32_t row = idx[p];
         const SegInfo &si = info[s];
         uint32_t m = 0;
@@ -395,10 +398,10 @@ __global__ __launch_bounds__(256) void k_keys0(const float *__restrict__ x, cons
 }
 
 __global__ __launch_bounds__(256) void k_scatter_back(const uint32_t *__restrict__ P, const uint32_t *__restrict__ vals,
-                                                      uint64_t total, int single, uint32_t *__restrict__ idx) {
+                                                      uint64_t total, uint32_t *__restrict__ idx) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride)
-        idx[single ? (uint32_t)j : P[j]] = vals[j];
+        idx[P[j]] = vals[j];
 }
 
 
@@ -542,28 +545,28 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         } else if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
             hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
-                               (int)single, keys, vals);
+                               keys, vals);
             ST_LAUNCH_CHECK();
             uint32_t *skeys = keys, *svals = vals;
             radix_sort_u32_inplace_or_swap(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs32", &skeys, &svals);
-            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, svals, total, (int)single, idx);
+            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, svals, total, idx);
             hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, skeys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
-                               c->stream, skeys, total, bigpos, bigcnt, P, (int)single, nseg_start, nseg_len);
+                               c->stream, skeys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
             ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else {
             auto *keys = wsT<uint64_t>(c, "mo.k64", total + 1);
             hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
-                               (int)single, keys, vals);
+                               keys, vals);
             ST_LAUNCH_CHECK();
             radix_sort_u64(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs64");
-            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, (int)single, idx);
+            hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, idx);
             hipLaunchKernelGGL(k_big_starts<uint64_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint64_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
-                               c->stream, keys, total, bigpos, bigcnt, P, (int)single, nseg_start, nseg_len);
+                               c->stream, keys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
             ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         }
