@@ -144,7 +144,7 @@ constexpr int EXT_SLOTS = 4096 / 257 + 2;
 __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, const float *__restrict__ y,
                                                  const float *__restrict__ z, const uint32_t *__restrict__ idx,
                                                  const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
-                                                 uint64_t total, uint32_t *ext) {
+                                                 uint64_t total, uint32_t *ext, float4 *__restrict__ cxyz) {
     __shared__ uint32_t slot[EXT_SLOTS * 6];
     const uint64_t base = (uint64_t)blockIdx.x * 4096;
     if (base >= total) return;
@@ -155,19 +155,26 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
     const float *cols[3] = {x, y, z};
     const int lane = threadIdx.x & 63;
     const uint64_t wb = base + (uint64_t)(threadIdx.x >> 6) * 1024;
-    uint32_t seg_[16], rows_[16];
+    uint32_t seg_[16], pos_[16], rows_[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint64_t j = wb + (uint64_t)r * 64 + lane;
         const uint64_t jj = j > last ? last : j;
         seg_[r] = j > last ? 0xffffffffu : S[jj];
-        rows_[r] = idx[P[jj]];
+        pos_[r] = P[jj];
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rows_[r] = idx[pos_[r]];
     float vals_[16][3];
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
         for (int a = 0; a < 3; ++a) vals_[r][a] = cols[a][rows_[r]];
+    // the gathered coordinates, kept at their idx positions for the level's keys (coalesced
+    // there: a segment's positions are contiguous), so x / y / z are gathered once per level
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (seg_[r] != 0xffffffffu) cxyz[pos_[r]] = make_float4(vals_[r][0], vals_[r][1], vals_[r][2], 0.0f);
     auto take = [&](uint32_t s, const float *v) {  // one lane into its segment's slot
         const uint32_t q = s - s0;
         uint32_t *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)s * 6];
@@ -335,11 +342,11 @@ __device__ inline uint32_t axis_q(float v, double mn, double mul) {
 }
 
 template <typename K>
-__global__ __launch_bounds__(256) void k_keys(const float *__restrict__ x, const float *__restrict__ y,
-                                              const float *__restrict__ z, const uint32_t *__restrict__ idx,
+__global__ __launch_bounds__(256) void k_keys(const uint32_t *__restrict__ idx,
                                               const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
                                               const SegInfo *__restrict__ info, uint64_t total,
-                                              K *__restrict__ keys, uint32_t *__restrict__ vals) {
+                                              const float4 *__restrict__ cxyz, K *__restrict__ keys,
+                                              uint32_t *__restrict__ vals) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
         const uint32_t p = P[j];
@@ -348,9 +355,10 @@ __global__ __launch_bounds__(256) void k_keys(const float *__restrict__ x, const
         const SegInfo &si = info[s];
         uint32_t m = 0;
         if (si.ok) {
-            const uint32_t ix = axis_q(x[row], si.mn[0], si.mul[0]);
-            const uint32_t iy = axis_q(y[row], si.mn[1], si.mul[1]);
-            const uint32_t iz = axis_q(z[row], si.mn[2], si.mul[2]);
+            const float4 v = cxyz[p];
+            const uint32_t ix = axis_q(v.x, si.mn[0], si.mul[0]);
+            const uint32_t iy = axis_q(v.y, si.mn[1], si.mul[1]);
+            const uint32_t iz = axis_q(v.z, si.mn[2], si.mul[2]);
             m = (part1by2(iz) << 2) + (part1by2(iy) << 1) + part1by2(ix);
         }
         keys[j] = ((K)s << 30) | (K)m;
@@ -413,17 +421,34 @@ __global__ void k_set_sentinel(uint32_t *a, uint32_t i, uint32_t v) { a[i] = v; 
 // Runs of equal keys longer than 256 (ordering.ts:90-104) without listing every run: j
 // starts such a run iff it starts a run and keys[j + 256] == keys[j] (the keys are sorted).
 // Their order in the next level's segment list is immaterial: a segment's rows go back to
-// their own positions.  Few runs qualify, so they are appended with an atomic.
+// their own positions.
 template <typename K>
 __global__ __launch_bounds__(256) void k_big_starts(const K *__restrict__ keys, uint64_t total,
                                                     const SegInfo *__restrict__ info, uint32_t *__restrict__ starts,
                                                     uint32_t *__restrict__ count) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j + 256 < total; j += stride) {
-        const K k = keys[j];
-        if (keys[j + 256] == k && (j == 0 || keys[j - 1] != k) && info[(uint32_t)(k >> 30)].ok)
-            starts[atomicAdd(count, 1u)] = (uint32_t)j;
+    // a block's 4,096 positions hold at most 16 starts: ranked in LDS, appended with one
+    // global atomic per block (one per start serialised on the counter: 0.23 ms at 20k runs)
+    __shared__ uint32_t nloc, base;
+    if (threadIdx.x == 0) nloc = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * 4096;
+    uint32_t slot[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint64_t j = b0 + (uint64_t)r * 256 + threadIdx.x;
+        slot[r] = 0xffffffffu;
+        if (j + 256 < total) {
+            const K k = keys[j];
+            if (keys[j + 256] == k && (j == 0 || keys[j - 1] != k) && info[(uint32_t)(k >> 30)].ok)
+                slot[r] = atomicAdd(&nloc, 1u);
+        }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) base = nloc ? atomicAdd(count, nloc) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (slot[r] != 0xffffffffu) starts[base + slot[r]] = (uint32_t)(b0 + (uint64_t)r * 256 + threadIdx.x);
 }
 
 // end of each big run by binary search (first position past j whose key differs), then the
@@ -467,6 +492,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
     auto *vals = wsT<uint32_t>(c, "mo.vals", n);
     auto *bigpos = wsT<uint32_t>(c, "mo.bigpos", n / 257 + 2);  // starts of runs longer than 256
     auto *bigcnt = wsT<uint32_t>(c, "mo.bigcnt", 1);
+    float4 *cxyz = nullptr;  // deeper levels: x / y / z gathered by k_ext_seg, at idx positions
     for (int level = 0; nseg > 0; ++level) {
         const bool single = (level == 0);
         if (!single) {
@@ -486,8 +512,9 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, total, part);
             hipLaunchKernelGGL(k_ext_final, dim3(1), dim3(256), 0, c->stream, part, eb, ext);
         } else {
+            if (!cxyz) cxyz = wsT<float4>(c, "mo.cxyz", n);
             hipLaunchKernelGGL(k_ext_init, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
-            hipLaunchKernelGGL(k_ext_seg, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, ext);
+            hipLaunchKernelGGL(k_ext_seg, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, ext, cxyz);
         }
         ST_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
@@ -536,7 +563,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_keys0, dim3(nt), dim3(256), 0, c->stream, x, y, z, idx, info, n, keys, hist, nt);
             ST_LAUNCH_CHECK();
             radix_sort_u32_from(c, keys, idx, n, 0, 30, keys, idx, hist, "mo.rs32");
-            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
+            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3((unsigned)((total + 4095) / 4096)), dim3(256), 0, c->stream, keys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, keys, total, bigpos, bigcnt, P, 1, nseg_start, nseg_len);
@@ -544,13 +571,13 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
-            hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
-                               keys, vals);
+            hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
+                               cxyz, keys, vals);
             ST_LAUNCH_CHECK();
             uint32_t *skeys = keys, *svals = vals;
             radix_sort_u32_inplace_or_swap(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs32", &skeys, &svals);
             hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, svals, total, idx);
-            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3(g), dim3(256), 0, c->stream, skeys, total, info, bigpos,
+            hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3((unsigned)((total + 4095) / 4096)), dim3(256), 0, c->stream, skeys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, skeys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);
@@ -558,12 +585,12 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else {
             auto *keys = wsT<uint64_t>(c, "mo.k64", total + 1);
-            hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, x, y, z, idx, P, S, info, total,
-                               keys, vals);
+            hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
+                               cxyz, keys, vals);
             ST_LAUNCH_CHECK();
             radix_sort_u64(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs64");
             hipLaunchKernelGGL(k_scatter_back, dim3(g), dim3(256), 0, c->stream, P, vals, total, idx);
-            hipLaunchKernelGGL(k_big_starts<uint64_t>, dim3(g), dim3(256), 0, c->stream, keys, total, info, bigpos,
+            hipLaunchKernelGGL(k_big_starts<uint64_t>, dim3((unsigned)((total + 4095) / 4096)), dim3(256), 0, c->stream, keys, total, info, bigpos,
                                bigcnt);
             hipLaunchKernelGGL(k_big_segs<uint64_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, keys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);

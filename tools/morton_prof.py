@@ -11,7 +11,7 @@ import torch
 import splat_hip as sh
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-kind = sys.argv[2] if len(sys.argv) > 2 else 'gauss'  # gauss | clustered | grid
+kind = sys.argv[2] if len(sys.argv) > 2 else 'gauss'  # gauss | clustered | clumps | grid
 dev = torch.device('cuda', 0)
 stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
@@ -26,6 +26,13 @@ if kind == 'clustered':
     centre = torch.randint(0, 64, (n,), generator=g, device=dev).float()
     for a in (x, y, z):
         a[m] = centre[m] * 0.05 + a[m] * 1e-5
+elif kind == 'clumps':
+    # 80% of the splats in 20,000 small clumps (~400 each): one deeper level of many segments
+    m = torch.rand(n, generator=g, device=dev) < 0.8
+    cid = torch.randint(0, 20000, (n,), generator=g, device=dev)
+    cx, cy, cz = (torch.randn(20000, generator=g, device=dev) for _ in range(3))
+    for a, cc in ((x, cx), (y, cy), (z, cz)):
+        a[m] = cc[cid[m]] + a[m] * 1e-6
 elif kind == 'grid':
     # coordinates on a coarse lattice: many exactly equal points (runs that never split)
     for a in (x, y, z):
