@@ -283,14 +283,32 @@ __global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ 
     }
 }
 
-// segments that sort (info.ok): flags and member counts for the two scans below
+// segments that sort (info.ok), split by size: up to SMALL_SEG members sort inside one
+// workgroup (k_seg_sort_small), larger ones go through the device-wide radix sort
+constexpr uint32_t SMALL_SEG = 4096;
 __global__ void k_seg_flags(const SegInfo *__restrict__ info, const uint32_t *__restrict__ seg_len, uint32_t nseg,
-                            uint32_t *__restrict__ flag, uint32_t *__restrict__ mlen) {
+                            uint32_t *__restrict__ flag, uint32_t *__restrict__ mlen, uint32_t *__restrict__ sflag) {
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
-        const uint32_t ok = info[s].ok;
-        flag[s] = ok;
-        mlen[s] = ok ? seg_len[s] : 0u;
+        const uint32_t ok = info[s].ok, len = seg_len[s];
+        const uint32_t big = ok && len > SMALL_SEG;
+        flag[s] = big;
+        mlen[s] = big ? len : 0u;
+        sflag[s] = ok && !big;
     }
+}
+
+// the small sorting segments: start, length, info
+__global__ void k_seg_compact_small(const uint32_t *__restrict__ sflag, const uint32_t *__restrict__ spos,
+                                    const uint32_t *__restrict__ seg_start, const uint32_t *__restrict__ seg_len,
+                                    const SegInfo *__restrict__ info, uint32_t nseg, uint32_t *__restrict__ sstart,
+                                    uint32_t *__restrict__ slen, SegInfo *__restrict__ sinfo) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)
+        if (sflag[s]) {
+            const uint32_t q = spos[s];
+            sstart[q] = seg_start[s];
+            slen[q] = seg_len[s];
+            sinfo[q] = info[s];
+        }
 }
 
 // the sorting segments only (ordering.ts:53-61 returns before sorting the others): their
@@ -309,11 +327,11 @@ __global__ void k_seg_compact(const uint32_t *__restrict__ flag, const uint32_t 
 }
 
 // ordering.ts:32-65 per segment
-// (level 0: seg_start null, the one segment starts at 0); also zeroes the level's big-run count
+// (level 0: seg_start null, the one segment starts at 0); also zeroes the level's big-run counts
 __global__ void k_seg_info(const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ z,
                            const uint32_t *__restrict__ idx, const uint32_t *__restrict__ seg_start,
                            const uint32_t *__restrict__ ext, uint32_t nseg, SegInfo *info, uint32_t *bigcnt) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *bigcnt = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 2) bigcnt[threadIdx.x] = 0;  // big runs of both sort paths
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
         const uint32_t first = idx[seg_start ? seg_start[s] : 0u];
         const float f[3] = {x[first], y[first], z[first]};
@@ -405,6 +423,131 @@ __global__ __launch_bounds__(256) void k_keys0(const float *__restrict__ x, cons
     hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
+// one workgroup per small segment (257..SMALL_SEG members, contiguous positions in idx): keys
+// from the level's gathered coordinates, a stable 4-pass LSD radix sort with the elements in
+// registers between passes (wave ballots rank each 64-element row, as the device-wide
+// scatter does; LDS only for the reordering), the order written back into idx, and the
+// segment's own runs of > 256 equal keys appended to the next level's list
+__global__ __launch_bounds__(256) void k_seg_sort_small(const uint32_t *__restrict__ sstart,
+                                                        const uint32_t *__restrict__ slen,
+                                                        const SegInfo *__restrict__ sinfo, uint32_t nsmall,
+                                                        const float4 *__restrict__ cxyz, uint32_t *__restrict__ idx,
+                                                        uint32_t *__restrict__ ostart, uint32_t *__restrict__ olen,
+                                                        uint32_t *__restrict__ ocnt) {
+    constexpr int ROWS = SMALL_SEG / 256;
+    __shared__ uint32_t kL[SMALL_SEG], vL[SMALL_SEG];
+    __shared__ uint32_t wcount[4][256], wbase[4][256], dstart[256], wtot[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t sg = blockIdx.x; sg < nsmall; sg += gridDim.x) {
+        const uint32_t start = sstart[sg], len = slen[sg];
+        const SegInfo si = sinfo[sg];
+        // R rows of 64 per wave, wave w owning rows [w R, w R + R): contiguous element ranges per
+        // wave keep the ranking stable, and no wave ranks rows past the segment's end
+        const uint32_t R = ((len + 63) / 64 + 3) / 4;
+        uint32_t k[ROWS], v[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            if ((uint32_t)r >= R) continue;
+            const uint32_t e = (w * R + r) * 64 + lane;
+            k[r] = 0u;
+            v[r] = 0u;
+            if (e < len) {
+                const float4 cv = cxyz[start + e];
+                const uint32_t ix = axis_q(cv.x, si.mn[0], si.mul[0]);
+                const uint32_t iy = axis_q(cv.y, si.mn[1], si.mul[1]);
+                const uint32_t iz = axis_q(cv.z, si.mn[2], si.mul[2]);
+                k[r] = (part1by2(iz) << 2) + (part1by2(iy) << 1) + part1by2(ix);
+                v[r] = idx[start + e];
+            }
+        }
+        for (int pass = 0; pass < 4; ++pass) {
+            const int shift = 8 * pass, bits = pass == 3 ? 6 : 8;
+            for (int i = threadIdx.x; i < 4 * 256; i += 256) (&wcount[0][0])[i] = 0;
+            __syncthreads();
+            uint32_t off[ROWS], dg[ROWS];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                if ((uint32_t)r >= R) continue;
+                const uint32_t e = (w * R + r) * 64 + lane;
+                const bool valid = e < len;
+                const uint32_t d = (k[r] >> shift) & 255u;
+                dg[r] = d;
+                uint64_t peers = __ballot(valid);
+                for (int b = 0; b < bits; ++b) {
+                    const bool bit = (d >> b) & 1u;
+                    const uint64_t bb = __ballot(bit);
+                    peers &= bit ? bb : ~bb;
+                }
+                const uint32_t before = valid ? wcount[w][d] : 0u;
+                off[r] = before + (uint32_t)__popcll(peers & lt);
+                if (valid && (peers & lt) == 0) wcount[w][d] = before + (uint32_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+            }
+            __syncthreads();
+            {
+                const int d = threadIdx.x;
+                uint32_t tot = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    wbase[i][d] = tot;
+                    tot += wcount[i][d];
+                }
+                uint32_t incl = tot;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t u = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += u;
+                }
+                if (lane == 63) wtot[w] = incl;
+                __syncthreads();
+                uint32_t woff = 0;
+                for (int i = 0; i < w; ++i) woff += wtot[i];
+                dstart[d] = woff + incl - tot;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                if ((uint32_t)r >= R) continue;
+                const uint32_t e = (w * R + r) * 64 + lane;
+                if (e < len) {
+                    const uint32_t lp = dstart[dg[r]] + wbase[w][dg[r]] + off[r];
+                    kL[lp] = k[r];
+                    vL[lp] = v[r];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                if ((uint32_t)r >= R) continue;
+                const uint32_t e = (w * R + r) * 64 + lane;
+                if (e < len) {
+                    k[r] = kL[e];
+                    v[r] = vL[e];
+                }
+            }
+            __syncthreads();
+        }
+        // kL holds the sorted keys: write the order, then the segment's own big runs
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            if ((uint32_t)r >= R) continue;
+            const uint32_t e = (w * R + r) * 64 + lane;
+            if (e < len) {
+                idx[start + e] = v[r];
+                if (e + 256 < len && kL[e + 256] == k[r] && (e == 0 || kL[e - 1] != k[r])) {
+                    uint32_t end = e + 257;
+                    while (end < len && kL[end] == k[r]) ++end;
+                    const uint32_t slot = atomicAdd(ocnt, 1u);
+                    ostart[slot] = start + e;
+                    olen[slot] = end - e;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_scatter_back(const uint32_t *__restrict__ P, const uint32_t *__restrict__ vals,
                                                       uint64_t total, uint32_t *__restrict__ idx) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -491,7 +634,9 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
     auto *S = wsT<uint32_t>(c, "mo.S", n);
     auto *vals = wsT<uint32_t>(c, "mo.vals", n);
     auto *bigpos = wsT<uint32_t>(c, "mo.bigpos", n / 257 + 2);  // starts of runs longer than 256
-    auto *bigcnt = wsT<uint32_t>(c, "mo.bigcnt", 1);
+    auto *bigcnt = wsT<uint32_t>(c, "mo.bigcnt", 2);  // [0] device-wide sort, [1] small segments
+    auto *sm_start = wsT<uint32_t>(c, "mo.sm_start", n / 257 + 2);  // the small segments' big runs
+    auto *sm_len = wsT<uint32_t>(c, "mo.sm_len", n / 257 + 2);
     float4 *cxyz = nullptr;  // deeper levels: x / y / z gathered by k_ext_seg, at idx positions
     for (int level = 0; nseg > 0; ++level) {
         const bool single = (level == 0);
@@ -520,24 +665,41 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
                            single ? nullptr : seg_start, ext, nseg, info, bigcnt);
         ST_LAUNCH_CHECK();
+        bool large = true;  // the device-wide sort has members at this level
         if (!single) {
             // only segments with usable extents are keyed and sorted: the others keep their order
-            // and never recurse (ordering.ts:53-61), so their members leave the level here
+            // and never recurse (ordering.ts:53-61), so their members leave the level here.  Small
+            // ones sort inside one workgroup each; large ones keep the device-wide sort below
             auto *flag = wsT<uint32_t>(c, "mo.flag", n / 257 + 2);
             auto *pos = wsT<uint32_t>(c, "mo.pos", n / 257 + 3);
             auto *mlen = wsT<uint32_t>(c, "mo.mlen", n / 257 + 2);
             auto *moff = wsT<uint32_t>(c, "mo.moff", n / 257 + 3);
+            auto *sflag = wsT<uint32_t>(c, "mo.sflag", n / 257 + 2);
+            auto *spos = wsT<uint32_t>(c, "mo.spos", n / 257 + 3);
             hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, info, seg_len,
-                               nseg, flag, mlen);
+                               nseg, flag, mlen, sflag);
             ST_LAUNCH_CHECK();
             scan_u32(c, flag, pos, nseg, pos + nseg);
             scan_u32(c, mlen, moff, nseg, moff + nseg);
+            scan_u32(c, sflag, spos, nseg, spos + nseg);
             ST_HIP(hipMemcpyAsync(h + 1, pos + nseg, 4, hipMemcpyDeviceToHost, c->stream));
             ST_HIP(hipMemcpyAsync(h + 2, moff + nseg, 4, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(h + 3, spos + nseg, 4, hipMemcpyDeviceToHost, c->stream));
             ST_HIP(hipStreamSynchronize(c->stream));
-            const uint32_t kept = h[1];
-            if (kept == 0) break;
-            if (kept < nseg) {
+            const uint32_t kept = h[1], nsmall = h[3];
+            if (kept == 0 && nsmall == 0) break;
+            if (nsmall) {
+                auto *sstart = wsT<uint32_t>(c, "mo.sstart", n / 257 + 2);
+                auto *slen = wsT<uint32_t>(c, "mo.slen", n / 257 + 2);
+                auto *sinfo = static_cast<SegInfo *>(ws(c, "mo.sinfo", sizeof(SegInfo) * (size_t)nsmall));
+                hipLaunchKernelGGL(k_seg_compact_small, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream,
+                                   sflag, spos, seg_start, seg_len, info, nseg, sstart, slen, sinfo);
+                hipLaunchKernelGGL(k_seg_sort_small, dim3(std::min<uint32_t>(nsmall, 4096)), dim3(256), 0, c->stream,
+                                   sstart, slen, sinfo, nsmall, cxyz, idx, sm_start, sm_len, bigcnt + 1);
+                ST_LAUNCH_CHECK();
+            }
+            large = kept > 0;
+            if (large && kept < nseg) {
                 auto *cstart = wsT<uint32_t>(c, "mo.cstart", n / 257 + 2);
                 auto *cinfo = static_cast<SegInfo *>(ws(c, "mo.cinfo", sizeof(SegInfo) * (size_t)kept));
                 hipLaunchKernelGGL(k_seg_compact, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, flag, pos,
@@ -554,7 +716,9 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         int seg_bits = 0;
         while ((1u << seg_bits) < nseg) ++seg_bits;
         const unsigned g = grid_for(total, 256, 8192);
-        if (single) {
+        if (!large) {
+            // every sorting segment of this level was small
+        } else if (single) {
             // keys + first digit counts, then the sort reads idx as its values and its last
             // (fourth) pass writes the ordered rows straight back into idx
             const uint32_t nt = radix_tiles(n);
@@ -568,7 +732,6 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, keys, total, bigpos, bigcnt, P, 1, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
-            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
             hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
@@ -582,7 +745,6 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_big_segs<uint32_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, skeys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
-            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         } else {
             auto *keys = wsT<uint64_t>(c, "mo.k64", total + 1);
             hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
@@ -595,10 +757,16 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             hipLaunchKernelGGL(k_big_segs<uint64_t>, dim3(grid_for(total / 257 + 1, 256, 1024)), dim3(256), 0,
                                c->stream, keys, total, bigpos, bigcnt, P, 0, nseg_start, nseg_len);
             ST_LAUNCH_CHECK();
-            ST_HIP(hipMemcpyAsync(h, bigcnt, 4, hipMemcpyDeviceToHost, c->stream));
         }
+        // next level: the device-wide sort's big runs, then the small segments' ones
+        ST_HIP(hipMemcpyAsync(h + 4, bigcnt, 8, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
-        nseg = h[0];
+        const uint32_t nl = h[4], ns = h[5];
+        if (ns) {
+            ST_HIP(hipMemcpyAsync(nseg_start + nl, sm_start, 4ull * ns, hipMemcpyDeviceToDevice, c->stream));
+            ST_HIP(hipMemcpyAsync(nseg_len + nl, sm_len, 4ull * ns, hipMemcpyDeviceToDevice, c->stream));
+        }
+        nseg = nl + ns;
         std::swap(seg_start, nseg_start);
         std::swap(seg_len, nseg_len);
     }

@@ -59,7 +59,7 @@ def test_morton_ragged_vs_oracle(ctx, n):
 
 
 @pytest.mark.parametrize('case', ['all_equal', 'nan_coords', 'inf_extent', 'one_axis_flat', 'big_equal_run',
-                                  'neg_zero', 'lattice', 'blobs', 'blobs_flat'])
+                                  'neg_zero', 'lattice', 'blobs', 'blobs_flat', 'clumps', 'clumps_dup'])
 @pytest.mark.parametrize('n', [5000, 70001, 1_000_003])
 def test_morton_degenerate_vs_oracle(ctx, case, n):
     """ordering.ts:53-65: zero-length extents, non-finite extents (ordering skipped), NaN
@@ -94,6 +94,18 @@ def test_morton_degenerate_vs_oracle(ctx, case, n):
         if case == 'blobs_flat':  # some blobs flat on one axis, NaN members in others
             z[m & (centre < 100)] = 1.0
             x[m & (centre > 250) & (rng.random(n) < 0.01)] = np.nan
+    elif case in ('clumps', 'clumps_dup'):
+        # ~600-member clumps: deeper-level segments small enough for the one-workgroup sort;
+        # with duplicates, runs inside them recurse once more (and stop: equal coordinates)
+        m = rng.random(n) < 0.8
+        cid = rng.integers(0, max(1, int(n * 0.8) // 600), n)
+        cx, cy, cz = (rng.normal(0, 5, cid.max() + 1).astype(np.float32) for _ in range(3))
+        jit = 1e-5 if case == 'clumps' else 0.0
+        for a, cc in ((x, cx), (y, cy), (z, cz)):
+            a[m] = (cc[cid[m]] + a[m] * jit).astype(np.float32)
+        if case == 'clumps_dup':
+            half = m & (rng.random(n) < 0.5)
+            x[half] += np.float32(1e-4)
     same_bits(ctx.morton_order(x, y, z), oracle.morton_order(x, y, z))
 
 
