@@ -230,6 +230,33 @@ def test_sog_all_bands_vs_oracle(ctx, C):
         same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
 
 
+@pytest.mark.parametrize('kind', ['clumps', 'lattice'])
+def test_sog_clumped_positions_vs_oracle(ctx, kind):
+    """writeSog over positions whose Morton order recurses (ordering.ts:90-104): clumps of
+    ~600 splats at one point each (segments sorted inside one workgroup, their runs stopping on
+    all-equal extents), or a coarse lattice (runs whose extents are all zero) -- the means
+    textures place every row at its Morton position."""
+    n, C = 6000, 3
+    cols = _table(n, C, 91)
+    rng = np.random.default_rng(3)
+    if kind == 'clumps':
+        cid = rng.integers(0, 8, n)
+        for i, a in enumerate(('x', 'y', 'z')):
+            cen = rng.normal(0, 4, 8).astype(np.float32)
+            cols[a] = (cen[cid] + (rng.random(n) < 0.5) * np.float32(1e-3) * (i == 0)).astype(np.float32)
+    else:
+        for a in ('x', 'y', 'z'):
+            cols[a] = (np.round(cols[a] * 0.5) / 0.5).astype(np.float32)
+    draws = oracle.mulberry32(11, 1 << 15)
+    tex, meta, used = ctx.sog(cols, 3, draws)
+    rc, otex, ometa, oused = oracle.sog(cols, C, 3, draws)
+    assert rc == 0 and used == oused
+    for k in tex:
+        same_bits(tex[k], otex[k])
+    same_bits(np.array(meta.means_min[:]), np.array(ometa.means_min[:]))
+    same_bits(np.array(meta.means_max[:]), np.array(ometa.means_max[:]))
+
+
 @pytest.mark.parametrize('who', ['scales', 'colours', 'both', 'neither'])
 def test_sog_reseeding_cluster1d_vs_oracle(ctx, who):
     """The colours' cluster1d runs beside the scales' on a side context from draw 0 and is kept
