@@ -7,6 +7,8 @@ and priced against the 8 TB/s HBM peak with its ALGORITHMIC bytes per splat:
   filter_finite (a6)      252 B  read 62 columns + write the kept index
   permute_rows (a6)       496 B  gather 62 columns + write them
   morton_order (a8)        92 B  SURVEY 8d: extents 12 + keys 12+4 + 4-pass 8-bit LSD on 8-B pairs 64
+                                 (+ morton_order_clumped: the same over clumped positions, priced
+                                 the same way; not part of the config-3 pipeline)
   pack_compressed (a9/10) 301 B  gather 14+45 columns, write vertex 16 B + sh 45 B + chunk
 
 Prints one JSON object (also written to gpurun_out/paths.json)."""
@@ -90,6 +92,24 @@ def measure(ctx, stream, dev, n=10_000_000, reps=5):
         order.copy_(torch.arange(m, dtype=torch.int32, device=dev))
         ctx.dev_morton_order(dst['x'], dst['y'], dst['z'], order)
     report('morton_order', timed(morton), 92, rows=m)
+    # the same ordering over clumped positions (80% of the splats in 20,000 clumps of ~400 at
+    # one point each): the recursion levels real scenes reach (ordering.ts:90-104), not in config3
+    gc = torch.Generator(device=dev)
+    gc.manual_seed(1004)
+    cid = torch.randint(0, 20000, (m,), generator=gc, device=dev)
+    inclump = torch.rand(m, generator=gc, device=dev) < 0.8
+    cxyz = []
+    for a in ('x', 'y', 'z'):
+        cc = torch.randn(20000, generator=gc, device=dev)
+        cxyz.append(torch.where(inclump, cc[cid] + dst[a] * 1e-6, dst[a]).contiguous())
+
+    def morton_clumped():
+        order.copy_(torch.arange(m, dtype=torch.int32, device=dev))
+        ctx.dev_morton_order(cxyz[0], cxyz[1], cxyz[2], order)
+    report('morton_order_clumped', timed(morton_clumped), 92, rows=m)
+    out['stages']['morton_order_clumped']['what'] = ('not a config-3 stage: positions in 20,000 clumps, '
+                                                      'so the ordering recurses (deeper levels)')
+    del cxyz, cid, inclump
     chunk = torch.empty((m + 255) // 256 * 18, device=dev)
     vertex = torch.empty(m * 4, dtype=torch.int32, device=dev)
     shb = torch.empty(m * 45, dtype=torch.uint8, device=dev)
