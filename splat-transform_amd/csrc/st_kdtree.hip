@@ -12,8 +12,8 @@
 // (len 2: node lo, right child lo+1).  So each depth is one stable radix sort of
 // (segment rank, coordinate) over the active positions; the segment layout is
 // precomputed on the host per K.
-// Walk: one thread per tied point over the implicit tree, with every exact
-// distance precomputed by a wave-parallel kernel, so each visit is O(1).
+// Walk: one thread per listed point over the implicit tree, the exact distance
+// (row-major copies of points and centroids) computed at each visited node.
 #include <memory>
 #include <unordered_map>
 
@@ -103,20 +103,24 @@ __global__ __launch_bounds__(256) void k_level_scatter(const uint32_t *__restric
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) S[pos[j]] = vals[j];
 }
 
-// exact distances of one tied point to every centroid (kd-tree.ts:26-35)
-__global__ __launch_bounds__(256) void k_all_dist(const float *const *cols, int d, const float *__restrict__ cen,
-                                                  int k, const uint32_t *__restrict__ tie_pts, uint32_t first,
-                                                  double *__restrict__ dist) {
-    const uint32_t t = blockIdx.y;
-    const uint32_t p = tie_pts[first + t];
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < (uint32_t)k; c += gridDim.x * blockDim.x) {
-        double l = 0;
-        for (int i = 0; i < d; ++i) {
-            const double v = (double)cen[(uint64_t)i * k + c] - (double)cols[i][p];
-            l += v * v;
-        }
-        dist[(uint64_t)t * k + c] = l;
+// calcDistance (kd-tree.ts:26-35): f64 differences of the f32 values, squares summed in
+// dimension order (the zero padding of the rows adds +0)
+__device__ inline double kd_dist(const float *__restrict__ crow, const float *__restrict__ prow, int ld) {
+    const float4 *c4 = reinterpret_cast<const float4 *>(crow);
+    const float4 *p4 = reinterpret_cast<const float4 *>(prow);
+    double l = 0;
+    for (int q = 0; q < ld / 4; ++q) {
+        const float4 a = c4[q], b = p4[q];
+        double v = (double)a.x - (double)b.x;
+        l += v * v;
+        v = (double)a.y - (double)b.y;
+        l += v * v;
+        v = (double)a.z - (double)b.z;
+        l += v * v;
+        v = (double)a.w - (double)b.w;
+        l += v * v;
     }
+    return l;
 }
 
 struct Frame {
@@ -143,13 +147,15 @@ __device__ inline void seg_split(uint32_t lo, uint32_t hi, uint32_t &node, uint3
     }
 }
 
-__global__ void k_kd_walk(const float *const *cols, int d, const float *__restrict__ cen, int k,
-                          const uint32_t *__restrict__ S, const uint32_t *__restrict__ tie_pts, uint32_t first,
-                          uint32_t count, const double *__restrict__ dist, uint32_t *__restrict__ labels) {
+__global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict__ cen, int k,
+                                                 const uint32_t *__restrict__ S, const float *__restrict__ aos,
+                                                 const float *__restrict__ caos, int ld,
+                                                 const uint32_t *__restrict__ tie_pts, uint32_t count,
+                                                 uint32_t *__restrict__ labels) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
-    const uint32_t p = tie_pts[first + t];
-    const double *dd = dist + (uint64_t)t * k;
+    const uint32_t p = tie_pts[t];
+    const float *prow = aos + (uint64_t)p * ld;
     double mind = __builtin_inf();
     uint32_t mini = 0xffffffffu;
     Frame stack[64];
@@ -163,7 +169,7 @@ __global__ void k_kd_walk(const float *const *cols, int d, const float *__restri
                 uint32_t node, llo, lhi, rlo, rhi;
                 seg_split(clo, chi, node, llo, lhi, rlo, rhi);
                 const int axis = (int)(cdepth % (uint32_t)d);
-                const double distance = (double)cols[axis][p] - (double)cen[(uint64_t)axis * k + S[node]];
+                const double distance = (double)prow[axis] - (double)cen[(uint64_t)axis * k + S[node]];
                 if (distance > 0) {
                     clo = rlo;
                     chi = rhi;
@@ -180,8 +186,8 @@ __global__ void k_kd_walk(const float *const *cols, int d, const float *__restri
         seg_split(f.lo, f.hi, node, llo, lhi, rlo, rhi);
         const int axis = (int)(f.depth % (uint32_t)d);
         const uint32_t ci = S[node];
-        const double distance = (double)cols[axis][p] - (double)cen[(uint64_t)axis * k + ci];
-        const double thisd = dd[ci];
+        const double distance = (double)prow[axis] - (double)cen[(uint64_t)axis * k + ci];
+        const double thisd = kd_dist(caos + (uint64_t)ci * ld, prow, ld);
         if (thisd < mind) {
             mind = thisd;
             mini = ci;
@@ -201,9 +207,8 @@ __global__ void k_kd_walk(const float *const *cols, int d, const float *__restri
 
 }  // namespace
 
-void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
                      const uint32_t *tie_pts, uint32_t nties, uint32_t *labels) {
-    (void)n;
     static thread_local std::unordered_map<int64_t, std::unique_ptr<KdLayout>> layouts;
     auto &L = layouts[((int64_t)c->device << 32) | (uint32_t)k];
     if (!L) L = make_layout(k);
@@ -222,17 +227,10 @@ void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, in
                            v.count, S);
         ST_LAUNCH_CHECK();
     }
-    const uint32_t batch = 64;
-    auto *dist = wsT<double>(c, "kd.dist", (size_t)batch * k);
-    for (uint32_t first = 0; first < nties; first += batch) {
-        const uint32_t cnt = (nties - first < batch) ? (nties - first) : batch;
-        hipLaunchKernelGGL(k_all_dist, dim3(grid_for(k, 256, 64), cnt), dim3(256), 0, c->stream, dcols, d, cen, k,
-                           tie_pts, first, dist);
-        ST_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_kd_walk, dim3((cnt + 63) / 64), dim3(64), 0, c->stream, dcols, d, cen, k, S, tie_pts,
-                           first, cnt, dist, labels);
-        ST_LAUNCH_CHECK();
-    }
+    // one thread per listed point, distances computed at the visited nodes only
+    hipLaunchKernelGGL(k_kd_walk, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
+                       tie_pts, nties, labels);
+    ST_LAUNCH_CHECK();
 }
 
 }  // namespace st

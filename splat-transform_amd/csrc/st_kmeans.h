@@ -80,8 +80,10 @@ void seqsum1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start
 // (cols: host array of the device columns, dcols: the same array on the device)
 void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n);
 
-// KdTree tie-break for exact-distance ties (st_kdtree.hip)
-void kd_resolve_ties(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+// KdTree.findNearest for the points listed in tie_pts (exact-distance ties, candidate
+// overflows): cen [d][k] for the tree, the row-major copies aos (points) / caos (centroids)
+// with row stride ld (zero padded) for the distances (st_kdtree.hip)
+void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
                      const uint32_t *tie_pts, uint32_t nties, uint32_t *labels);
 
 }  // namespace st
