@@ -350,6 +350,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
     // per point tile: top-3 of the keyed tile minima seen by this lane-half (key = the tile
     // minimum with the tile index in its low kbits mantissa bits)
     float m1[PT], m2[PT], m3[PT], th[PT];
+    bool full[PT];  // MODE 1: this lane saw its point's candidate list overflow
     const uint32_t kbits = ctiles > 1 ? 32u - (uint32_t)__builtin_clz(ctiles - 1) : 0u;
     const uint32_t kmask = (1u << kbits) - 1u;
     uint32_t kmask_v;  // in a VGPR: v_bfi_b32 takes one scalar operand (the tile index)
@@ -360,6 +361,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
         m2[t] = __builtin_inff();
         m3[t] = __builtin_inff();
         th[t] = -__builtin_inff();
+        full[t] = false;
         if (MODE == 1) {
             const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
             if (slot < npts) th[t] = thr[slot];
@@ -387,15 +389,18 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                 m3[t] = __builtin_amdgcn_fmed3f(m2[t], m3[t], key);
                 m2[t] = __builtin_amdgcn_fmed3f(m1[t], m2[t], key);
                 m1[t] = fminf(m1[t], key);
-            } else if (mn <= th[t]) {
-                // candidates are rare (a handful of the K centroids per point)
+            } else if (mn <= th[t] && !full[t]) {
+                // candidates are rare (a handful of the K centroids per point); once the point's
+                // list has overflowed (coinciding centroids: thousands of candidates) this lane
+                // stops counting -- k_exact sends an overflowed point to the KdTree walk
                 const uint32_t slot = (tile0 + t) * 32 + (lane & 31);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    if (sc[r] <= th[t]) {
+                    if (sc[r] <= th[t] && !full[t]) {
                         const uint32_t ci = ctile * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
                         const uint32_t pos = atomicAdd(&cand_cnt[slot], 1u);
                         if (pos < CAND_CAP) cand[(uint64_t)slot * CAND_CAP + pos] = ci;
+                        else full[t] = true;
                     }
                 }
             }
