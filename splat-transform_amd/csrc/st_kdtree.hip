@@ -205,6 +205,63 @@ __global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict_
     labels[p] = mini;
 }
 
+// ---- equal rows walk once ----------------------------------------------------------
+// Duplicated points (e.g. all-zero SH rows) tie on every coinciding centroid and all take the
+// same walk: the listed points are sorted by a hash of their row, a point whose row equals its
+// predecessor's in that order takes its result, only the others walk.
+__device__ inline uint64_t row_hash(const float *__restrict__ row, int ld) {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int i = 0; i < ld; ++i) {
+        h ^= __builtin_bit_cast(uint32_t, row[i]);
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+    }
+    return h;
+}
+
+__global__ __launch_bounds__(256) void k_tie_hash(const float *__restrict__ aos, int ld,
+                                                  const uint32_t *__restrict__ tie_pts, uint32_t nties,
+                                                  uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nties; t += gridDim.x * blockDim.x) {
+        keys[t] = row_hash(aos + (uint64_t)tie_pts[t] * ld, ld);
+        vals[t] = t;
+    }
+}
+
+// flag[j] = 1: position j of the hash order walks (first of its hash, or a row that differs
+// from its predecessor's, bit for bit)
+__global__ __launch_bounds__(256) void k_tie_flags(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                   const uint32_t *__restrict__ tie_pts, const float *__restrict__ aos,
+                                                   int ld, uint32_t nties, uint32_t *__restrict__ flag) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nties; j += gridDim.x * blockDim.x) {
+        uint32_t f = 1u;
+        if (j > 0 && keys[j] == keys[j - 1]) {
+            const uint32_t *a = reinterpret_cast<const uint32_t *>(aos + (uint64_t)tie_pts[vals[j]] * ld);
+            const uint32_t *b = reinterpret_cast<const uint32_t *>(aos + (uint64_t)tie_pts[vals[j - 1]] * ld);
+            f = 0u;
+            for (int i = 0; i < ld && !f; ++i) f = a[i] != b[i];
+        }
+        flag[j] = f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tie_compact(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                     const uint32_t *__restrict__ vals,
+                                                     const uint32_t *__restrict__ tie_pts, uint32_t nties,
+                                                     uint32_t *__restrict__ walkers) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nties; j += gridDim.x * blockDim.x)
+        if (flag[j]) walkers[pos[j]] = tie_pts[vals[j]];
+}
+
+// a point that did not walk takes the label of the nearest walker before it in hash order
+__global__ __launch_bounds__(256) void k_tie_copy(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                  const uint32_t *__restrict__ vals,
+                                                  const uint32_t *__restrict__ tie_pts, const uint32_t *__restrict__ walkers,
+                                                  uint32_t nties, uint32_t *__restrict__ labels) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nties; j += gridDim.x * blockDim.x)
+        if (!flag[j]) labels[tie_pts[vals[j]]] = labels[walkers[pos[j] - 1]];
+}
+
 }  // namespace
 
 void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
@@ -228,8 +285,33 @@ void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos
         ST_LAUNCH_CHECK();
     }
     // one thread per listed point, distances computed at the visited nodes only
-    hipLaunchKernelGGL(k_kd_walk, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
-                       tie_pts, nties, labels);
+    if (nties < 4096) {
+        hipLaunchKernelGGL(k_kd_walk, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
+                           tie_pts, nties, labels);
+        ST_LAUNCH_CHECK();
+        return;
+    }
+    auto *hk = wsT<uint64_t>(c, "kd.hkeys", nties);
+    auto *hv = wsT<uint32_t>(c, "kd.hvals", nties);
+    auto *flag = wsT<uint32_t>(c, "kd.flag", nties);
+    auto *pos = wsT<uint32_t>(c, "kd.pos", (size_t)nties + 1);
+    auto *walkers = wsT<uint32_t>(c, "kd.walkers", nties);
+    const unsigned g = grid_for(nties, 256, 4096);
+    hipLaunchKernelGGL(k_tie_hash, dim3(g), dim3(256), 0, c->stream, aos, ld, tie_pts, nties, hk, hv);
+    ST_LAUNCH_CHECK();
+    radix_sort_u64(c, hk, hv, nties, 0, 64, "kd.hs");
+    hipLaunchKernelGGL(k_tie_flags, dim3(g), dim3(256), 0, c->stream, hk, hv, tie_pts, aos, ld, nties, flag);
+    ST_LAUNCH_CHECK();
+    scan_u32(c, flag, pos, nties, pos + nties);
+    hipLaunchKernelGGL(k_tie_compact, dim3(g), dim3(256), 0, c->stream, flag, pos, hv, tie_pts, nties, walkers);
+    ST_LAUNCH_CHECK();
+    auto *hw = static_cast<uint32_t *>(pinned_slot(c, "kd.nwalk", 4));
+    ST_HIP(hipMemcpyAsync(hw, pos + nties, 4, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t nw = hw[0];
+    hipLaunchKernelGGL(k_kd_walk, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
+                       walkers, nw, labels);
+    hipLaunchKernelGGL(k_tie_copy, dim3(g), dim3(256), 0, c->stream, flag, pos, hv, tie_pts, walkers, nties, labels);
     ST_LAUNCH_CHECK();
 }
 

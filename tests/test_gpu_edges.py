@@ -230,18 +230,22 @@ def test_sog_all_bands_vs_oracle(ctx, C):
         same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
 
 
-@pytest.mark.parametrize('n,d,k,zero_frac', [(20_000, 45, 1024, 0.05), (20_000, 45, 1024, 0.3),
-                                             (30_000, 24, 2048, 0.5), (8_000, 9, 256, 0.02)])
-def test_kmeans_duplicated_rows_vs_oracle(ctx, n, d, k, zero_frac):
+@pytest.mark.parametrize('n,d,k,zero_frac,protos', [(20_000, 45, 1024, 0.05, 0), (20_000, 45, 1024, 0.3, 0),
+                                                    (30_000, 24, 2048, 0.5, 0), (8_000, 9, 256, 0.02, 0),
+                                                    (30_000, 45, 1024, 0.4, 40)])
+def test_kmeans_duplicated_rows_vs_oracle(ctx, n, d, k, zero_frac, protos):
     """Many exactly duplicated points (all-zero rows): the init draws pick several of them, so
     several centroids coincide and every duplicated point is equidistant from all of them.
     Points with more candidates than the collect keeps go straight to the KdTree walk
-    (kd-tree.ts:39-68), as do the exact ties; labels, centroids and draws match the reference."""
+    (kd-tree.ts:39-68), as do the exact ties; equal rows walk once.  protos > 0: the duplicated
+    rows are copies of that many random rows instead of zeros.  Labels, centroids and draws
+    match the reference."""
     rng = np.random.default_rng(n + d + k)
     cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
     z = rng.random(n) < zero_frac
+    which = rng.integers(0, max(protos, 1), n)
     for c in cols:
-        c[z] = 0.0
+        c[z] = c[:protos][which[z]] if protos else 0.0
     draws = oracle.mulberry32(n + k, 8 * k * 4 + 64)
     cent, labels, used = ctx.kmeans(cols, k, 3, draws)
     rc, ocent, olabels, oused = oracle.kmeans(cols, k, 3, draws)
