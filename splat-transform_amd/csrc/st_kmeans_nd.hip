@@ -58,6 +58,12 @@ constexpr int NW = 4;          // waves per workgroup (they share the LDS centro
 constexpr int WG = 64 * NW;    // threads per workgroup
 constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
+// members above which a cluster's sum is split over a workgroup (k_sumnd_big); ST_SUMND_BIG
+// lowers it so that tests drive that path with small inputs
+uint32_t sumnd_big() {
+    const char *e = getenv("ST_SUMND_BIG");  // read per call (tests set it around one call)
+    return e ? (uint32_t)std::max(1ul, strtoul(e, nullptr, 10)) : 16384u;
+}
 
 __host__ __device__ inline int kp_of(int d) { return ((d + 3) + 15) / 16 * 16; }
 
@@ -988,12 +994,13 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
 // f64 running sum over the members in ascending point order
 __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, int d,
                                                const uint32_t *__restrict__ members,
-                                               const uint32_t *__restrict__ start, int k, float *__restrict__ cen) {
+                                               const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
+                                               uint32_t big) {
     const int lane = threadIdx.x & 63;
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    if (s0 == s1 || lane >= d) return;
+    if (s0 == s1 || lane >= d || s1 - s0 > big) return;  // huge clusters: k_sumnd_big
     const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
@@ -1008,6 +1015,84 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     }
     for (; j < s1; ++j) sum += (double)aos[(uint64_t)members[j] * ld + lane];
     cen[(uint64_t)lane * k + cl] = (float)(sum / (double)(s1 - s0));
+}
+
+// clusters of more than `big` members (duplicated points pile into one): 16 waves of a
+// workgroup sum contiguous slices of the member list, each with sum|x| and the smallest ulp
+// exponent; when the certificate holds for a dimension every partial sum is exact, so the
+// slices' sums add to the sequential result, otherwise one lane runs the sequential chain.
+// A few workgroups scan the cluster list for the huge ones.
+__global__ __launch_bounds__(1024) void k_sumnd_big(const float *__restrict__ aos, int d,
+                                                    const uint32_t *__restrict__ members,
+                                                    const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
+                                                    uint32_t big) {
+    __shared__ double ps[16][64], pa[16][64];
+    __shared__ int pe[16][64];
+    __shared__ uint32_t list[1024];
+    __shared__ uint32_t nlist;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ld = aos_ld(d);
+    for (uint32_t base = blockIdx.x * 1024u; base < (uint32_t)k; base += gridDim.x * 1024u) {
+        if (threadIdx.x == 0) nlist = 0;
+        __syncthreads();
+        const uint32_t c0 = base + threadIdx.x;
+        if (c0 < (uint32_t)k && start[c0 + 1] - start[c0] > big) list[atomicAdd(&nlist, 1u)] = c0;
+        __syncthreads();
+        const uint32_t nl = nlist;
+        for (uint32_t i = 0; i < nl; ++i) {
+            const uint32_t cl = list[i];
+            const uint32_t s0 = start[cl], s1 = start[cl + 1], m = s1 - s0;
+            const uint32_t per = (m + 15) / 16;
+            const uint32_t a = s0 + min(m, w * per), b = s0 + min(m, (w + 1) * per);
+            double sum = 0, sabs = 0;
+            int emin = 0x7fffffff;
+            auto take = [&](float x) {
+                sum += (double)x;
+                sabs += __builtin_fabs((double)x);
+                if (x != 0.0f) emin = min(emin, ulp_exp(x));
+            };
+            if (lane < d) {
+                constexpr int U = 32;  // member rows in flight, as k_sumnd
+                uint32_t j = a;
+                for (; j + U <= b; j += U) {
+                    float v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) take(v[u]);
+                }
+                for (; j < b; ++j) take(aos[(uint64_t)members[j] * ld + lane]);
+            }
+            ps[w][lane] = sum;
+            pa[w][lane] = sabs;
+            pe[w][lane] = emin;
+            __syncthreads();
+            if (w == 0 && lane < d) {
+                double S = 0, A = 0;
+                int E = 0x7fffffff;
+                for (int q = 0; q < 16; ++q) {
+                    S += ps[q][lane];
+                    A += pa[q][lane];
+                    E = min(E, pe[q][lane]);
+                }
+                if (!sum_is_exact(A, E)) {  // the sequential chain (k-means.ts:41-63)
+                    S = 0;
+                    constexpr int U = 32;
+                    uint32_t j = s0;
+                    for (; j + U <= s1; j += U) {
+                        float v[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) S += (double)v[u];
+                    }
+                    for (; j < s1; ++j) S += (double)aos[(uint64_t)members[j] * ld + lane];
+                }
+                cen[(uint64_t)lane * k + cl] = (float)(S / (double)m);
+            }
+            __syncthreads();
+        }
+    }
 }
 
 template <int KS>
@@ -1258,7 +1343,12 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         member_sort(c, labels, n, k, sorted_labels, members, start);
         {
             KTimer kt(c, "kn.sumnd");
-            hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen);
+            const uint32_t big = sumnd_big();
+            hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen,
+                               big);
+            if (n > big)
+                hipLaunchKernelGGL(k_sumnd_big, dim3(std::min<unsigned>(64u, (unsigned)((k + 1023) / 1024))),
+                                   dim3(1024), 0, c->stream, aos, d, members, start, k, cen, big);
             ST_LAUNCH_CHECK();
         }
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);

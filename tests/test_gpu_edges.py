@@ -254,6 +254,28 @@ def test_kmeans_duplicated_rows_vs_oracle(ctx, n, d, k, zero_frac, protos):
     same_bits(cent, ocent)
 
 
+@pytest.mark.parametrize('big,tiny', [(24, 0.0), (24, 0.02), (1, 0.0)])
+def test_kmeans_split_cluster_sums_vs_oracle(ctx, monkeypatch, big, tiny):
+    """calcAverage (k-means.ts:41-63) for clusters above the split threshold (ST_SUMND_BIG lowers
+    the default 16,384): slices summed in parallel under the exactness certificate, and the
+    sequential chain where tiny members break the certificate.  big = 1 splits every cluster
+    with more than one member."""
+    n, d, k = 6000, 9, 64
+    rng = np.random.default_rng(big + int(tiny * 100))
+    cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(d)]
+    for c in cols:
+        t = rng.random(n) < tiny
+        c[t] *= np.float32(1e-12)
+    draws = oracle.mulberry32(9, 1 << 12)
+    monkeypatch.setenv('ST_SUMND_BIG', str(big))
+    cent, labels, used = ctx.kmeans(cols, k, 3, draws)
+    monkeypatch.delenv('ST_SUMND_BIG')
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, 3, draws)
+    assert rc == 0 and used == oused
+    same_bits(labels, olabels)
+    same_bits(cent, ocent)
+
+
 @pytest.mark.parametrize('kind', ['clumps', 'lattice'])
 def test_sog_clumped_positions_vs_oracle(ctx, kind):
     """writeSog over positions whose Morton order recurses (ordering.ts:90-104): clumps of
