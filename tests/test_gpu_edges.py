@@ -276,6 +276,33 @@ def test_kmeans_split_cluster_sums_vs_oracle(ctx, monkeypatch, big, tiny):
     same_bits(cent, ocent)
 
 
+@pytest.mark.parametrize('n,C', [(1, 3), (2, 0), (17, 8), (85, 0), (86, 0), (300, 15), (1023, 3), (1025, 15),
+                                 (2049, 8)])
+def test_sog_small_tables_vs_oracle(ctx, n, C):
+    """writeSog on tables smaller than the default palette (write-sog.ts:310 paletteSize from n:
+    256 at n = 300, 512 at n = 1,023 ...), textures barely larger than the table.  Below 86
+    splats the scales' cluster1d has fewer than 256 values: the reference's kmeans returns a
+    plain Array there (k-means.ts:139-144) and the `.subarray` of write-sog.ts throws, so both
+    the product and the oracle report an error."""
+    cols = _table(n, C, 500 + n)
+    draws = oracle.mulberry32(n, 1 << 14)
+    rc, otex, ometa, oused = oracle.sog(cols, C, 3, draws)
+    if 3 * n < 256:
+        assert rc != 0
+        with pytest.raises(sh.StError):
+            ctx.sog(cols, 3, draws)
+        return
+    tex, meta, used = ctx.sog(cols, 3, draws)
+    assert rc == 0 and used == oused
+    assert set(tex) == set(otex)
+    for k in tex:
+        same_bits(tex[k], otex[k])
+    for f in ('width', 'height', 'sh_bands', 'palette_size', 'shn_width', 'shn_height'):
+        assert getattr(meta, f) == getattr(ometa, f), f
+    for f in ('means_min', 'means_max', 'scales_codebook', 'sh0_codebook', 'shn_codebook'):
+        same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
+
+
 @pytest.mark.parametrize('kind', ['clumps', 'lattice'])
 def test_sog_clumped_positions_vs_oracle(ctx, kind):
     """writeSog over positions whose Morton order recurses (ordering.ts:90-104): clumps of
