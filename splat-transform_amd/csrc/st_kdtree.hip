@@ -35,6 +35,7 @@ struct Level {
 struct KdLayout {
     int k = 0;
     std::vector<Level> levels;
+    uint8_t *depth = nullptr;  // device: the depth at which each position is a tree node
     std::vector<void *> allocs;
     ~KdLayout() {
         for (void *p : allocs) (void)hipFree(p);
@@ -46,7 +47,8 @@ std::unique_ptr<KdLayout> make_layout(int k) {
     auto L = std::make_unique<KdLayout>();
     L->k = k;
     std::vector<std::pair<uint32_t, uint32_t>> segs = {{0u, (uint32_t)k}}, next;
-    while (!segs.empty()) {
+    std::vector<uint8_t> depth((size_t)k, 0);
+    for (uint8_t dep = 0; !segs.empty(); ++dep) {
         std::vector<uint32_t> pos, rank;
         uint32_t r = 0;
         next.clear();
@@ -59,10 +61,15 @@ std::unique_ptr<KdLayout> make_layout(int k) {
                 }
                 ++r;
             }
-            if (len == 2) {
+            if (len == 1) {
+                depth[s.first] = dep;
+            } else if (len == 2) {
                 // right child is a single leaf: nothing further to sort
+                depth[s.first] = dep;
+                depth[s.first + 1] = (uint8_t)(dep + 1);
             } else if (len >= 3) {
                 const uint32_t mid = s.first + (len >> 1);
+                depth[mid] = dep;
                 next.push_back({s.first, mid});
                 next.push_back({mid + 1, s.second});
             }
@@ -83,6 +90,9 @@ std::unique_ptr<KdLayout> make_layout(int k) {
         }
         segs.swap(next);
     }
+    ST_HIP(hipMalloc(&L->depth, (size_t)k));
+    L->allocs.push_back(L->depth);
+    ST_HIP(hipMemcpy(L->depth, depth.data(), (size_t)k, hipMemcpyHostToDevice));
     return L;
 }
 
@@ -205,6 +215,81 @@ __global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict_
     labels[p] = mini;
 }
 
+// ---- few walkers: every distance precomputed in tree order --------------------------
+// After the equal rows have merged, a handful of points may each walk most of the tree
+// (a duplicated row meets a coinciding centroid late): their splitting values and exact
+// distances are laid out by tree position, so a visit is one load round instead of a chain
+// through S and the 45-dim distance.
+__global__ __launch_bounds__(256) void k_tree_split(const float *__restrict__ cen, int k, int d,
+                                                    const uint32_t *__restrict__ S,
+                                                    const uint8_t *__restrict__ depth, float *__restrict__ split) {
+    for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < (uint32_t)k; pos += gridDim.x * blockDim.x)
+        split[pos] = cen[(uint64_t)(depth[pos] % d) * k + S[pos]];
+}
+__global__ __launch_bounds__(256) void k_tree_dist(const float *__restrict__ aos, const float *__restrict__ caos,
+                                                   int ld, int k, const uint32_t *__restrict__ S,
+                                                   const uint32_t *__restrict__ walkers, double *__restrict__ dist) {
+    const uint32_t w = blockIdx.y;
+    const float *prow = aos + (uint64_t)walkers[w] * ld;
+    for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < (uint32_t)k; pos += gridDim.x * blockDim.x)
+        dist[(uint64_t)w * k + pos] = kd_dist(caos + (uint64_t)S[pos] * ld, prow, ld);
+}
+__global__ __launch_bounds__(64) void k_kd_walk_pre(int d, int k, const uint32_t *__restrict__ S,
+                                                    const float *__restrict__ split, const double *__restrict__ dist,
+                                                    const float *__restrict__ aos, int ld,
+                                                    const uint32_t *__restrict__ walkers, uint32_t count,
+                                                    uint32_t *__restrict__ labels) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint32_t p = walkers[t];
+    const float *prow = aos + (uint64_t)p * ld;
+    const double *dd = dist + (uint64_t)t * k;
+    double mind = __builtin_inf();
+    uint32_t mini = 0xffffffffu;
+    Frame stack[64];
+    int sp = 0;
+    uint32_t clo = 0, chi = (uint32_t)k, cdepth = 0;
+    bool descend = true;
+    while (true) {
+        if (descend) {
+            while (chi > clo) {
+                stack[sp++] = Frame{clo, chi, cdepth};
+                uint32_t node, llo, lhi, rlo, rhi;
+                seg_split(clo, chi, node, llo, lhi, rlo, rhi);
+                const double distance = (double)prow[cdepth % (uint32_t)d] - (double)split[node];
+                if (distance > 0) {
+                    clo = rlo;
+                    chi = rhi;
+                } else {
+                    clo = llo;
+                    chi = lhi;
+                }
+                ++cdepth;
+            }
+        }
+        if (sp == 0) break;
+        const Frame f = stack[--sp];
+        uint32_t node, llo, lhi, rlo, rhi;
+        seg_split(f.lo, f.hi, node, llo, lhi, rlo, rhi);
+        const double distance = (double)prow[f.depth % (uint32_t)d] - (double)split[node];
+        const double thisd = dd[node];
+        if (thisd < mind) {
+            mind = thisd;
+            mini = S[node];
+        }
+        const uint32_t olo = (distance > 0) ? llo : rlo, ohi = (distance > 0) ? lhi : rhi;
+        if (distance * distance < mind && ohi > olo) {
+            clo = olo;
+            chi = ohi;
+            cdepth = f.depth + 1;
+            descend = true;
+        } else {
+            descend = false;
+        }
+    }
+    labels[p] = mini;
+}
+
 // ---- equal rows walk once ----------------------------------------------------------
 // Duplicated points (e.g. all-zero SH rows) tie on every coinciding centroid and all take the
 // same walk: the listed points are sorted by a hash of their row, a point whose row equals its
@@ -309,8 +394,19 @@ void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos
     ST_HIP(hipMemcpyAsync(hw, pos + nties, 4, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     const uint32_t nw = hw[0];
-    hipLaunchKernelGGL(k_kd_walk, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
-                       walkers, nw, labels);
+    if (nw <= 64) {
+        auto *split = wsT<float>(c, "kd.split", (size_t)k);
+        auto *tdist = wsT<double>(c, "kd.tdist", (size_t)nw * k);
+        hipLaunchKernelGGL(k_tree_split, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, cen, k, d, S, L->depth,
+                           split);
+        hipLaunchKernelGGL(k_tree_dist, dim3(grid_for(k, 256, 256), nw), dim3(256), 0, c->stream, aos, caos, ld, k, S,
+                           walkers, tdist);
+        hipLaunchKernelGGL(k_kd_walk_pre, dim3((nw + 63) / 64), dim3(64), 0, c->stream, d, k, S, split, tdist, aos, ld,
+                           walkers, nw, labels);
+    } else {
+        hipLaunchKernelGGL(k_kd_walk, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
+                           walkers, nw, labels);
+    }
     hipLaunchKernelGGL(k_tie_copy, dim3(g), dim3(256), 0, c->stream, flag, pos, hv, tie_pts, walkers, nties, labels);
     ST_LAUNCH_CHECK();
 }
