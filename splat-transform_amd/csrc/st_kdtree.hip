@@ -157,15 +157,24 @@ __device__ inline void seg_split(uint32_t lo, uint32_t hi, uint32_t &node, uint3
     }
 }
 
+// KdTree.findNearest (kd-tree.ts:39-68) for one listed point per thread.  PRE = false: the
+// splitting values through S and the exact distance computed at each visited node; PRE = true:
+// both read from the tree-position layouts of k_tree_split / k_tree_dist (row t of dist)
+template <bool PRE>
 __global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict__ cen, int k,
                                                  const uint32_t *__restrict__ S, const float *__restrict__ aos,
                                                  const float *__restrict__ caos, int ld,
+                                                 const float *__restrict__ split, const double *__restrict__ dist,
                                                  const uint32_t *__restrict__ tie_pts, uint32_t count,
                                                  uint32_t *__restrict__ labels) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
     const uint32_t p = tie_pts[t];
     const float *prow = aos + (uint64_t)p * ld;
+    auto split_of = [&](uint32_t node, uint32_t depth) {
+        const uint32_t axis = depth % (uint32_t)d;
+        return PRE ? (double)split[node] : (double)cen[(uint64_t)axis * k + S[node]];
+    };
     double mind = __builtin_inf();
     uint32_t mini = 0xffffffffu;
     Frame stack[64];
@@ -178,8 +187,7 @@ __global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict_
                 stack[sp++] = Frame{clo, chi, cdepth};
                 uint32_t node, llo, lhi, rlo, rhi;
                 seg_split(clo, chi, node, llo, lhi, rlo, rhi);
-                const int axis = (int)(cdepth % (uint32_t)d);
-                const double distance = (double)prow[axis] - (double)cen[(uint64_t)axis * k + S[node]];
+                const double distance = (double)prow[cdepth % (uint32_t)d] - split_of(node, cdepth);
                 if (distance > 0) {
                     clo = rlo;
                     chi = rhi;
@@ -194,13 +202,11 @@ __global__ __launch_bounds__(256) void k_kd_walk(int d, const float *__restrict_
         const Frame f = stack[--sp];
         uint32_t node, llo, lhi, rlo, rhi;
         seg_split(f.lo, f.hi, node, llo, lhi, rlo, rhi);
-        const int axis = (int)(f.depth % (uint32_t)d);
-        const uint32_t ci = S[node];
-        const double distance = (double)prow[axis] - (double)cen[(uint64_t)axis * k + ci];
-        const double thisd = kd_dist(caos + (uint64_t)ci * ld, prow, ld);
+        const double distance = (double)prow[f.depth % (uint32_t)d] - split_of(node, f.depth);
+        const double thisd = PRE ? dist[(uint64_t)t * k + node] : kd_dist(caos + (uint64_t)S[node] * ld, prow, ld);
         if (thisd < mind) {
             mind = thisd;
-            mini = ci;
+            mini = S[node];
         }
         const uint32_t olo = (distance > 0) ? llo : rlo, ohi = (distance > 0) ? lhi : rhi;
         if (distance * distance < mind && ohi > olo) {
@@ -234,62 +240,6 @@ __global__ __launch_bounds__(256) void k_tree_dist(const float *__restrict__ aos
     for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < (uint32_t)k; pos += gridDim.x * blockDim.x)
         dist[(uint64_t)w * k + pos] = kd_dist(caos + (uint64_t)S[pos] * ld, prow, ld);
 }
-__global__ __launch_bounds__(64) void k_kd_walk_pre(int d, int k, const uint32_t *__restrict__ S,
-                                                    const float *__restrict__ split, const double *__restrict__ dist,
-                                                    const float *__restrict__ aos, int ld,
-                                                    const uint32_t *__restrict__ walkers, uint32_t count,
-                                                    uint32_t *__restrict__ labels) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= count) return;
-    const uint32_t p = walkers[t];
-    const float *prow = aos + (uint64_t)p * ld;
-    const double *dd = dist + (uint64_t)t * k;
-    double mind = __builtin_inf();
-    uint32_t mini = 0xffffffffu;
-    Frame stack[64];
-    int sp = 0;
-    uint32_t clo = 0, chi = (uint32_t)k, cdepth = 0;
-    bool descend = true;
-    while (true) {
-        if (descend) {
-            while (chi > clo) {
-                stack[sp++] = Frame{clo, chi, cdepth};
-                uint32_t node, llo, lhi, rlo, rhi;
-                seg_split(clo, chi, node, llo, lhi, rlo, rhi);
-                const double distance = (double)prow[cdepth % (uint32_t)d] - (double)split[node];
-                if (distance > 0) {
-                    clo = rlo;
-                    chi = rhi;
-                } else {
-                    clo = llo;
-                    chi = lhi;
-                }
-                ++cdepth;
-            }
-        }
-        if (sp == 0) break;
-        const Frame f = stack[--sp];
-        uint32_t node, llo, lhi, rlo, rhi;
-        seg_split(f.lo, f.hi, node, llo, lhi, rlo, rhi);
-        const double distance = (double)prow[f.depth % (uint32_t)d] - (double)split[node];
-        const double thisd = dd[node];
-        if (thisd < mind) {
-            mind = thisd;
-            mini = S[node];
-        }
-        const uint32_t olo = (distance > 0) ? llo : rlo, ohi = (distance > 0) ? lhi : rhi;
-        if (distance * distance < mind && ohi > olo) {
-            clo = olo;
-            chi = ohi;
-            cdepth = f.depth + 1;
-            descend = true;
-        } else {
-            descend = false;
-        }
-    }
-    labels[p] = mini;
-}
-
 // ---- equal rows walk once ----------------------------------------------------------
 // Duplicated points (e.g. all-zero SH rows) tie on every coinciding centroid and all take the
 // same walk: the listed points are sorted by a hash of their row, a point whose row equals its
@@ -371,8 +321,8 @@ void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos
     }
     // one thread per listed point, distances computed at the visited nodes only
     if (nties < 4096) {
-        hipLaunchKernelGGL(k_kd_walk, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
-                           tie_pts, nties, labels);
+        hipLaunchKernelGGL(k_kd_walk<false>, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos,
+                           caos, ld, (const float *)nullptr, (const double *)nullptr, tie_pts, nties, labels);
         ST_LAUNCH_CHECK();
         return;
     }
@@ -401,11 +351,11 @@ void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos
                            split);
         hipLaunchKernelGGL(k_tree_dist, dim3(grid_for(k, 256, 256), nw), dim3(256), 0, c->stream, aos, caos, ld, k, S,
                            walkers, tdist);
-        hipLaunchKernelGGL(k_kd_walk_pre, dim3((nw + 63) / 64), dim3(64), 0, c->stream, d, k, S, split, tdist, aos, ld,
-                           walkers, nw, labels);
+        hipLaunchKernelGGL(k_kd_walk<true>, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos,
+                           ld, split, tdist, walkers, nw, labels);
     } else {
-        hipLaunchKernelGGL(k_kd_walk, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos, caos, ld,
-                           walkers, nw, labels);
+        hipLaunchKernelGGL(k_kd_walk<false>, dim3((nw + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos,
+                           caos, ld, (const float *)nullptr, (const double *)nullptr, walkers, nw, labels);
     }
     hipLaunchKernelGGL(k_tie_copy, dim3(g), dim3(256), 0, c->stream, flag, pos, hv, tie_pts, walkers, nties, labels);
     ST_LAUNCH_CHECK();
