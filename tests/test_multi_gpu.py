@@ -62,6 +62,30 @@ def _same(got, want):
                               np.array(getattr(wmeta, f), np.float32).view(np.uint32)), f
 
 
+def test_group_duplicated_rows_and_clumps_equal_single_device(ctx):
+    """Inputs real scenes bring, sharded 3 ways: 20% of the splats share one all-zero SH row
+    (coinciding palette centroids, exact ties resolved by the KdTree walk on every rank) and
+    half sit in 40 clumps of identical positions (rank 0's Morton recursion)."""
+    n = 30_011
+    cols = _table(n, 77)
+    rng = np.random.default_rng(78)
+    dup = rng.random(n) < 0.2
+    for i in range(45):
+        cols[f'f_rest_{i}'][dup] = 0.0
+    clump = rng.random(n) < 0.5
+    cid = rng.integers(0, 40, n)
+    for a in 'xyz':
+        centre = rng.normal(0, 10, 40).astype(np.float32)
+        cols[a][clump] = centre[cid[clump]]
+    draws = np.random.default_rng(9).random(1 << 18)
+    want = ctx.sog(cols, 2, draws)
+    g = sh.Group([0] * 3, host_staged=True)
+    try:
+        _same(g.sog([cols], 2, draws, [0, 9000, 20000, n]), want)
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize('world,splits,adv', [(2, None, False), (3, 'empty0', False), (4, 'ragged', True)])
 def test_group_host_staged_equals_single_device(ctx, world, splits, adv):
     n = 30_011
