@@ -373,6 +373,60 @@ __global__ __launch_bounds__(SS_T) void k_small_sort(K *__restrict__ keys, uint3
     }
 }
 
+// stable sort of at most 256 u32-keyed pairs in one wave: a bitonic network over the
+// composite (digit bits << 32 | input position), unique keys, so the network's order is the
+// stable one; element i = r * 64 + lane, partners at distance < 64 by shuffles, larger ones
+// inside the lane's four registers.  (The rank sort above spent 23 us on the 256 centroids of
+// every 1-D k-means iteration: sixteen waves of one CU re-reading LDS.)
+__global__ __launch_bounds__(64) void k_sort256(uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t n,
+                                                int shift, int bits) {
+    const int lane = threadIdx.x;
+    const uint32_t mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+    uint64_t v[4];
+    uint32_t kin[4], vin[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t i = r * 64 + lane;
+        kin[r] = i < n ? keys[i] : 0u;
+        vin[r] = i < n ? vals[i] : 0u;
+        v[r] = i < n ? (((uint64_t)((kin[r] >> shift) & mask) << 32) | i) : ~0ull;
+    }
+#pragma unroll
+    for (uint32_t k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            uint64_t nv[4];  // every partner value is read before any is replaced
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t i = r * 64 + lane;
+                const uint64_t o = j < 64 ? __shfl_xor(v[r], (int)j, 64) : v[r ^ (int)(j >> 6)];
+                const bool up = (i & k) == 0, lower = (i & j) == 0;
+                const uint64_t lo = v[r] < o ? v[r] : o, hi = v[r] < o ? o : v[r];
+                nv[r] = (up == lower) ? lo : hi;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = nv[r];
+        }
+    }
+    // inputs to LDS, then the sorted order reads them by position
+    __shared__ uint32_t sk[256], sv[256];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sk[r * 64 + lane] = kin[r];
+        sv[r * 64 + lane] = vin[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t i = r * 64 + lane;
+        if (i < n) {
+            const uint32_t src = (uint32_t)v[r];
+            keys[i] = sk[src];
+            vals[i] = sv[src];
+        }
+    }
+}
+
 template <typename K>
 void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_bit, int end_bit,
                      const std::string &tag, K **out_keys = nullptr, uint32_t **out_vals = nullptr) {
@@ -380,6 +434,12 @@ void radix_sort_impl(st_ctx *c, K *keys, uint32_t *vals, uint64_t n, int begin_b
     if (out_vals) *out_vals = vals;
     if (n <= 1 || end_bit <= begin_bit) return;
     ST_REQUIRE(n < (1ull << 32), ST_ERR_ARG, "radix sort: n must be < 2^32");
+    if (sizeof(K) == 4 && n <= 256) {  // in place, one wave
+        hipLaunchKernelGGL(k_sort256, dim3(1), dim3(64), 0, c->stream, reinterpret_cast<uint32_t *>(keys), vals,
+                           (uint32_t)n, begin_bit, end_bit - begin_bit);
+        ST_LAUNCH_CHECK();
+        return;
+    }
     if (n <= SS_MAX) {  // in place, one launch
         hipLaunchKernelGGL(k_small_sort<K>, dim3(1), dim3(SS_T), 0, c->stream, keys, vals, (uint32_t)n, begin_bit,
                            end_bit - begin_bit);
