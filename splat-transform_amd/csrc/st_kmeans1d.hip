@@ -883,15 +883,35 @@ __global__ __launch_bounds__(CL_T) void k_chunk_list_small(const uint32_t *__res
         total += wsum[i];
     }
     uint32_t o = off + incl - mine;
+    // chunk offsets and member starts in LDS; then every thread writes chunks (a cluster of
+    // 100k+ members no longer leaves one thread writing all of its chunks)
+    __shared__ uint32_t soff[CL_MAX + 1], sst[CL_MAX + 1];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int cl = t * PER + u;
-        if (cl >= k) break;
-        first[cl] = o;
-        const uint32_t s0 = start[cl], s1 = start[cl + 1];
-        for (uint32_t b = s0; b < s1; b += SC_CH) chunks[o++] = Chunk{(uint32_t)cl, b, min(s1, b + SC_CH), 0u};
+        if (cl < k) {
+            first[cl] = o;
+            soff[cl] = o;
+            sst[cl] = start[cl];
+            o += cnt[u];
+        }
     }
-    if (t == 0) first[k] = total;
+    if (t == 0) {
+        first[k] = total;
+        soff[k] = total;
+        sst[k] = start[k];
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < total; q += CL_T) {
+        uint32_t lo = 0, hi = (uint32_t)k;  // the cluster whose chunk range holds q
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (soff[mid] <= q) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t b = sst[lo] + (q - soff[lo]) * SC_CH;
+        chunks[q] = Chunk{lo, b, min(sst[lo + 1], b + SC_CH), 0u};
+    }
 }
 
 // the chunk list of every cluster's member range (k clusters, start[k + 1]); acc (nullable):
