@@ -19,8 +19,15 @@ Workloads (BASELINE.json configs):
   --merge F             config 5: F input tables of 10M splats (--file-splats) concatenated
                         (combine, index.ts:158-210) + Morton + SOG, the rows split over the ranks
   --total-splats T      one T-splat table split over the ranks
-N > 1 is launched by torch.distributed.run (one process per GPU); torch.distributed carries
-only the RCCL unique id, the barriers and the max-over-ranks timing.
+N > 1 runs one process per GPU.  `python bench.py --gpus N` with no launcher around it starts
+the N-rank job itself (a child `python -m torch.distributed.run --nproc-per-node N ...`, spawned
+before this process touches torch or the GPU), relays rank 0's JSON line and fails unless the
+job ran N ranks; under torchrun (WORLD_SIZE set) the ranks run directly.  torch.distributed
+carries only the RCCL unique id, the barriers and the max-over-ranks timing.
+
+Synthetic tables are built from fixed-seed blocks of 10M rows (block b: seed 1002 + b), and a
+rank takes its global row range of them, so a T-splat table is the same table for every N (its
+`textures_sha256` does not depend on N); 10M splats per GPU is block `rank`.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (the MFMA assign
 sweep, measured with HIP events on its own stream), the CPU-oracle baseline timed on a
@@ -39,7 +46,7 @@ MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA peak (MI355X_MICRO
 HBM_TBPS = 8.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
@@ -63,7 +70,56 @@ def parse():
                     'over a one-rank RCCL communicator) instead of st_dev_sog: its per-rank cost')
     ap.add_argument('--dist-python', action='store_true', help='the sharded path through splat_dist.py '
                     '(torch.distributed collectives around the step API) instead of the library')
-    return ap.parse_args()
+    ap.add_argument('--launch-dry-run', action='store_true', help=argparse.SUPPRESS)  # print the launcher command
+    return ap.parse_args(argv)
+
+
+def launcher_cmd(argv, n, port):
+    """the N-rank job `bench.py --gpus N` starts when no launcher is around it"""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+            '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """parent of a self-launched N-rank job: never imports torch (nothing here touches the GPU);
+    the ranks' stdout is read here, rank 0's JSON line relayed, everything else goes to stderr"""
+    import subprocess
+    cmd = launcher_cmd(argv, args.gpus, free_port())
+    if args.launch_dry_run:
+        _RESULT.write(json.dumps({'cmd': cmd, 'torch_imported': 'torch' in sys.modules}) + '\n')
+        _RESULT.flush()
+        return 0
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '1')
+    print('bench.py: launching ' + ' '.join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    line = None
+    for ln in proc.stdout:
+        if ln.startswith('{') and '"metric"' in ln:
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+    rc = proc.wait()
+    if rc != 0:
+        print(f'bench.py: the {args.gpus}-rank job exited with {rc}', file=sys.stderr)
+        return rc
+    if line is None:
+        print('bench.py: the job printed no result line', file=sys.stderr)
+        return 3
+    if json.loads(line).get('n_gpus') != args.gpus:
+        print(f'bench.py: the job ran {json.loads(line).get("n_gpus")} ranks, not {args.gpus}', file=sys.stderr)
+        return 3
+    _RESULT.write(line + '\n')
+    _RESULT.flush()
+    return 0
 
 
 def synth_table(n, seed, device):
@@ -373,6 +429,32 @@ def sog_stage_table(stages, n, iters, K=65536, D=45):
     return out
 
 
+BLOCK = 10_000_000  # rows per fixed-seed block of the synthetic tables
+SEED = 1002
+
+
+def table_rows(T, lo, hi, dev, seed=SEED, block=BLOCK):
+    """rows [lo, hi) of the T-row synthetic table whose block b (rows [b*block, (b+1)*block)) is
+    synth_table(rows in the block, seed + b): the same T-row table whatever the rank split"""
+    import torch
+    parts = []
+    for b in range(lo // block, (hi - 1) // block + 1) if hi > lo else ():
+        a, e = b * block, min(T, (b + 1) * block)
+        full = synth_table(e - a, seed + b, dev)
+        if lo <= a and e <= hi:
+            parts.append(full)
+        else:
+            parts.append({k: v[max(lo, a) - a:min(hi, e) - a].clone() for k, v in full.items()})
+        del full
+    if not parts:
+        return synth_table(0, seed, dev)
+    if len(parts) == 1:
+        return parts[0]
+    out = {k: torch.cat([p[k] for p in parts]) for k in parts[0]}
+    del parts
+    return out
+
+
 def rank_tables(args, world, rank, dev):
     """this rank's input tables (device columns) and the workload's description"""
     if args.merge:
@@ -391,16 +473,35 @@ def rank_tables(args, world, rank, dev):
     if args.total_splats:
         T = args.total_splats
         lo, hi = T * rank // world, T * (rank + 1) // world
-        return [synth_table(hi - lo, 1002 + rank, dev)], T, (
-            f'config 4: writeSog SH3 of one {T // 1_000_000}M-splat table split {world} way(s), {args.iters} '
-            f'k-means iters'), 'strong'
+        return [table_rows(T, lo, hi, dev)], T, (
+            f'config 4: writeSog SH3 of one {T / 1e6:g}M-splat table (fixed-seed 10M blocks) split {world} way(s), '
+            f'{args.iters} k-means iters'), 'strong'
     n = args.splats
-    return [synth_table(n, 1002 + rank, dev)], n * world, (
+    return [table_rows(n * world, n * rank, n * (rank + 1), dev)], n * world, (
         f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters'), 'weak'
 
 
-def main():
-    args = parse()
+TEX_ORDER = ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels', 'shN_centroids')
+
+
+def textures_digest(tex, meta):
+    """sha256 over the seven textures (write-sog.ts order) and the meta fields: equal for every N"""
+    import hashlib
+
+    import numpy as np
+    h = hashlib.sha256()
+    for k in TEX_ORDER:
+        if k in tex:
+            h.update(tex[k].cpu().numpy().tobytes())
+    if meta is not None:
+        for f in ('width', 'height', 'sh_bands', 'palette_size', 'shn_width', 'shn_height'):
+            h.update(int(getattr(meta, f)).to_bytes(8, 'little'))
+        for f in ('means_min', 'means_max', 'scales_codebook', 'sh0_codebook', 'shn_codebook'):
+            h.update(np.array(list(getattr(meta, f)), np.float64).tobytes())
+    return h.hexdigest()
+
+
+def main(args):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -411,6 +512,9 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
+    if world > 1 and args.backend == 'nccl' and torch.cuda.device_count() < world:
+        raise SystemExit(f'bench.py: {world} RCCL ranks need {world} GPUs, this node has {torch.cuda.device_count()} '
+                         '(rehearse several ranks on one GPU with --dist-python --backend gloo)')
     torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
     if args.splats is None and args.total_splats is None and not args.merge:
         if world == 1:
@@ -492,6 +596,12 @@ def main():
             el = t.item()
         return el, meta, used
 
+    rccl_ranks = comm.count() if comm else (world if sharded and args.backend == 'nccl' else None)
+    devices = None
+    if sharded:
+        devs = [None] * world
+        dist.all_gather_object(devs, (os.uname().nodename, local))
+        devices = len(set(str(d) for d in devs))
     tabs, total, workload, scaling = rank_tables(args, world, rank, dev)
     step, tex, pal = make_step(tabs, total)
     torch.cuda.synchronize()
@@ -550,6 +660,7 @@ def main():
         if verification and not verification['ok']:
             sys.exit(1)
         return
+    tex_sha = textures_digest(tex, meta)
     # the .sog container of this step's textures on rank 0 (outside the headline's timed region)
     addr0, size0 = ctx.dev_sog_bundle_view(meta, total, tex, 0, 0)  # warm: workspace + pinned archive
     ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0))
@@ -651,6 +762,9 @@ def main():
         'sog_stages': sog_stage_table(stages, n_local, args.iters),
         'kernels': kstats,
         'draws_used_per_step': used,
+        'rccl_ranks': rccl_ranks,
+        'distinct_devices': devices if sharded else 1,
+        'textures_sha256': tex_sha,
         'weak_10M_per_gpu': weak,
         'verified': verification['ok'] if verification else None,
         'verification': verification,
@@ -670,8 +784,13 @@ def main():
 _RESULT = sys.stdout
 
 if __name__ == '__main__':
+    _args = parse()
     sys.stdout.flush()
     _RESULT = os.fdopen(os.dup(1), 'w')
     os.dup2(2, 1)
     sys.stdout = sys.stderr
-    main()
+    if _args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch(_args, sys.argv[1:]))
+    if 'WORLD_SIZE' in os.environ and int(os.environ['WORLD_SIZE']) != _args.gpus and _args.gpus != 1:
+        raise SystemExit(f'bench.py: --gpus {_args.gpus} under a launcher of WORLD_SIZE={os.environ["WORLD_SIZE"]}')
+    main(_args)

@@ -359,6 +359,8 @@ int st_get_devices(int32_t *ngpu);
 int st_comm_unique_id(uint8_t id[128]);
 int st_comm_init_rank(st_ctx *ctx, int32_t world, int32_t rank, const uint8_t id[128], st_comm **out);
 void st_comm_destroy(st_comm *comm);
+/* ranks in the communicator (ncclCommCount for RCCL): the bench reports it as `rccl_ranks` */
+int st_comm_count(const st_comm *comm, int32_t *count);
 /* one rank's part of a sharded writeSog: `locals` are this rank's tables (device columns; its
  * files or file parts, in global order); every rank calls it with the same iters and draws.
  * meta / out (device textures) are written on rank 0 only. */

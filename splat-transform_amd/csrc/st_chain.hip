@@ -338,6 +338,7 @@ int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t ele
                       int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
     if (int rc = apply_env_devices()) return rc;
+    const auto group = default_group();  // held for the whole call
     std::vector<std::vector<float>> host;  // multi-GPU: the processed columns, sharded from the host
     std::vector<float *> hcols;
     std::vector<std::string> hnames;
@@ -350,7 +351,7 @@ int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t ele
         ply_chain(c, fd, h, element, ch);
         run_actions(ch, actions, nactions);
         const st_table *t = sog_view(ch);
-        if (default_group()) {
+        if (group) {
             std::vector<HostXfer> down;
             for (int i = 0; i < t->ncol; ++i) {
                 host.emplace_back(t->n);
@@ -390,7 +391,7 @@ int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t ele
     });
     if (rc != ST_OK || !ht.ncol) return rc;
     const st_table *tp = &ht;
-    return st_group_sog_bundle(default_group(), &tp, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out,
+    return st_group_sog_bundle(group.get(), &tp, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out,
                                out_size);
 }
 

@@ -249,7 +249,7 @@ int st_cluster1d(st_ctx *c, const float *const *cols, int32_t ncols, uint64_t n,
 int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
            st_sog_meta *meta, const st_sog_textures *out) {
     if (int rc = apply_env_devices()) return rc;
-    if (st_group *g = default_group()) return st_group_sog(g, &t, 1, nullptr, iters, draws, ndraws, used, meta, out);
+    if (auto g = default_group()) return st_group_sog(g.get(), &t, 1, nullptr, iters, draws, ndraws, used, meta, out);
     return guarded_h([&] {
         ST_ARGH(c && t && meta && out, "NULL argument");
         use_device(c);
@@ -290,8 +290,8 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
 int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
                   uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
     if (int rc = apply_env_devices()) return rc;
-    if (st_group *g = default_group())
-        return st_group_sog_bundle(g, &t, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out, out_size);
+    if (auto g = default_group())
+        return st_group_sog_bundle(g.get(), &t, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out, out_size);
     return guarded_h([&] {
         ST_ARGH(c && t && out && out_size, "NULL argument");
         use_device(c);

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -280,8 +281,9 @@ struct ProcessedF32 {
 void chain_apply_f32(st_ctx *c, const st_table *in, const st_action *actions, int nactions, const std::string &tag,
                      ProcessedF32 &out);
 
-// multi-GPU writeSog (st_multi.hip): the st_set_devices group (nullptr: one device)
-st_group *default_group();
+// multi-GPU writeSog (st_multi.hip): the st_set_devices group (empty: one device); the returned
+// reference keeps the group alive for the caller's call even if st_set_devices replaces it
+std::shared_ptr<st_group> default_group();
 int apply_env_devices();  // ST_NUM_GPUS on first use; ST_OK or the error (st_last_error set)
 
 }  // namespace st

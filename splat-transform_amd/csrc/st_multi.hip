@@ -66,20 +66,30 @@ struct Coll {
     } while (0)
 
 struct RcclColl : Coll {
+    // `comm` is written once, before any rank thread runs; an abort only flips `dead` (atomic)
+    // and aborts the communicator, so a rank thread never reads a pointer another thread writes.
+    // A call that starts after the abort throws; one already inside RCCL returns the abort.
     ncclComm_t comm = nullptr;
     bool own = true;
+    std::atomic<bool> dead{false};
     ~RcclColl() override {
-        if (comm && own) ncclCommDestroy(comm);
+        if (comm && own && !dead.load()) ncclCommDestroy(comm);
+    }
+    void live() const {
+        if (dead.load()) throw Error(ST_ERR_INTERNAL, "multi-GPU: another rank failed");
     }
     static ncclDataType_t nt(Dt d) { return d == Dt::F64 ? ncclFloat64 : ncclInt32; }
     static ncclRedOp_t no(Op o) { return o == Op::Sum ? ncclSum : ncclMin; }
     void allreduce(void *buf, size_t count, Dt dt, Op op, hipStream_t s) override {
+        live();
         if (world > 1 && count) ST_NCCL(ncclAllReduce(buf, buf, count, nt(dt), no(op), comm, s));
     }
     void broadcast(void *buf, size_t bytes, int root, hipStream_t s) override {
+        live();
         if (world > 1 && bytes) ST_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm, s));
     }
     void allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        live();
         if (world == 1) {
             if (bytes && recv != send) ST_HIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
             return;
@@ -88,6 +98,7 @@ struct RcclColl : Coll {
     }
     void gatherv(const void *send, size_t mybytes, void *recv, const std::vector<size_t> &bytes,
                  const std::vector<size_t> &displ, int root, hipStream_t s) override {
+        live();
         if (rank == root && mybytes)
             ST_HIP(hipMemcpyAsync(static_cast<char *>(recv) + displ[rank], send, mybytes, hipMemcpyDeviceToDevice, s));
         if (world == 1) return;
@@ -101,13 +112,18 @@ struct RcclColl : Coll {
         ST_NCCL(ncclGroupEnd());
     }
     void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
+        live();
         if (world == 1 || from == to || !bytes || (rank != from && rank != to)) return;
         if (rank == from) ST_NCCL(ncclSend(buf, bytes, ncclUint8, to, comm, s));
         else ST_NCCL(ncclRecv(buf, bytes, ncclUint8, from, comm, s));
     }
     void abort() override {
-        if (comm) ncclCommAbort(comm);
-        comm = nullptr;
+        if (!dead.exchange(true) && comm) ncclCommAbort(comm);
+    }
+    int count() const {
+        int n = 0;
+        ST_NCCL(ncclCommCount(comm, &n));
+        return n;
     }
 };
 
@@ -579,6 +595,8 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
     LocalTable L = combine_local(c, co, tabs, ntab);
     const st_table *t = &L.t;
     const Shard sh = make_shard(c, co, t->n);
+    if (const char *f = getenv("ST_FAULT_RANK"))  // fault injection (tests): this rank fails here,
+        ST_REQUIRE(atoi(f) != co.rank, ST_ERR_INTERNAL, "ST_FAULT_RANK: injected failure");  // the others wait in a collective
     const uint64_t N = sh.N;
     if (n_global) *n_global = N;
     ST_REQUIRE(N > 0, ST_ERR_ARG, "sog: empty table");
@@ -748,14 +766,47 @@ struct st_comm {
 // a process-local set of ranks: one (context, host thread) per rank
 struct st_group {
     std::vector<st_ctx *> ctx;
+    std::vector<int32_t> devices;
+    bool host_staged = false;
     std::vector<std::unique_ptr<Coll>> coll;
+    std::mutex run_mu;    // one group call at a time (the contexts and collectives are shared)
+    std::string broken;  // non-empty: the collectives could not be rebuilt after a failure
     ~st_group() {
         coll.clear();
         for (auto *c : ctx) st_ctx_destroy(c);
     }
-    // f(rank) on every rank's thread; the first failure is rethrown, the others are aborted
+    // the collectives of every rank: RCCL communicators (ncclCommInitAll) or one host hub
+    void make_colls() {
+        const int n = (int)ctx.size();
+        coll.clear();
+        if (host_staged) {
+            auto hub = std::make_shared<HostHub>(n);
+            for (int r = 0; r < n; ++r) {
+                auto hc = std::make_unique<HostColl>();
+                hc->hub = hub;
+                hc->rank = r;
+                hc->world = n;
+                coll.push_back(std::move(hc));
+            }
+        } else {
+            std::vector<ncclComm_t> comms(n);
+            ST_NCCL(ncclCommInitAll(comms.data(), n, devices.data()));
+            for (int r = 0; r < n; ++r) {
+                auto rc = std::make_unique<RcclColl>();
+                rc->comm = comms[r];
+                rc->rank = r;
+                rc->world = n;
+                coll.push_back(std::move(rc));
+            }
+        }
+    }
+    // f(rank) on every rank's thread; the first failure aborts the other ranks' collectives and
+    // is rethrown once every thread has returned.  The aborted collectives are then rebuilt, so a
+    // recoverable error (too few draws, an unsupported column) leaves the group usable.
     template <typename F>
     void run(F &&f) {
+        std::lock_guard<std::mutex> lk(run_mu);
+        if (!broken.empty()) throw Error(ST_ERR_INTERNAL, "multi-GPU group unusable: " + broken);
         const int n = (int)ctx.size();
         std::vector<std::exception_ptr> err(n);
         std::vector<std::thread> th;
@@ -772,14 +823,42 @@ struct st_group {
                 }
             });
         for (auto &t : th) t.join();
-        for (auto &e : err)
-            if (e) std::rethrow_exception(e);
+        if (!failed.load()) return;
+        // every rank thread has returned: drain the streams, then replace the collectives
+        for (auto *c : ctx) {
+            use_device(c);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipGetLastError();
+        }
+        try {
+            make_colls();
+        } catch (const std::exception &e) {
+            broken = e.what();
+        }
+        // the first failure that is not the abort it caused in the other ranks
+        std::exception_ptr first;
+        for (auto &e : err) {
+            if (!e) continue;
+            try {
+                std::rethrow_exception(e);
+            } catch (const Error &x) {
+                if (std::string(x.what()).find("another rank failed") == std::string::npos) {
+                    first = e;
+                    break;
+                }
+            } catch (...) {
+                first = e;
+                break;
+            }
+            if (!first) first = e;
+        }
+        std::rethrow_exception(first);
     }
 };
 
 namespace {
 std::mutex g_group_mu;
-st_group *g_group = nullptr;  // st_set_devices
+std::shared_ptr<st_group> g_group;  // st_set_devices (a caller holds its own reference while it runs)
 int g_ndev = 1;
 std::atomic<bool> g_env_done{false};  // ST_NUM_GPUS applied (or overridden by st_set_devices)
 
@@ -805,27 +884,9 @@ st_group *group_new(const int32_t *devices, int n, bool host_staged) {
         if (rc != ST_OK) throw Error(rc, std::string("group: ") + st_last_error());
         g->ctx.push_back(c);
     }
-    if (host_staged) {
-        auto hub = std::make_shared<HostHub>(n);
-        for (int r = 0; r < n; ++r) {
-            auto hc = std::make_unique<HostColl>();
-            hc->hub = hub;
-            hc->rank = r;
-            hc->world = n;
-            g->coll.push_back(std::move(hc));
-        }
-    } else {
-        std::vector<ncclComm_t> comms(n);
-        std::vector<int> devs(devices, devices + n);
-        ST_NCCL(ncclCommInitAll(comms.data(), n, devs.data()));
-        for (int r = 0; r < n; ++r) {
-            auto rc = std::make_unique<RcclColl>();
-            rc->comm = comms[r];
-            rc->rank = r;
-            rc->world = n;
-            g->coll.push_back(std::move(rc));
-        }
-    }
+    g->devices.assign(devices, devices + n);
+    g->host_staged = host_staged;
+    g->make_colls();
     return g.release();
 }
 
@@ -962,6 +1023,14 @@ int st_comm_init_rank(st_ctx *c, int32_t world, int32_t rank, const uint8_t id[1
 
 void st_comm_destroy(st_comm *cm) { delete cm; }
 
+int st_comm_count(const st_comm *cm, int32_t *count) {
+    return guarded_m([&] {
+        ST_REQUIRE(cm && count, ST_ERR_ARG, "NULL argument");
+        const auto *rc = dynamic_cast<const RcclColl *>(cm->coll.get());
+        *count = rc ? rc->count() : cm->coll->world;
+    });
+}
+
 int st_dev_sog_sharded(st_ctx *c, st_comm *cm, const st_table *const *locals, int32_t nlocal, int32_t iters,
                        const double *draws, uint64_t ndraws, uint64_t *used, st_sog_meta *meta,
                        const st_sog_textures *out) {
@@ -1074,15 +1143,15 @@ int st_set_devices(int32_t ngpu) {
         ST_HIP(hipGetDeviceCount(&avail));
         ST_REQUIRE(ngpu >= 1 && ngpu <= avail, ST_ERR_ARG,
                    "st_set_devices: ngpu must be in [1, " + std::to_string(avail) + "]");
-        std::lock_guard<std::mutex> lk(g_group_mu);
-        delete g_group;
-        g_group = nullptr;
-        g_ndev = ngpu;
+        std::shared_ptr<st_group> fresh;
         if (ngpu > 1) {
             std::vector<int32_t> devs(ngpu);
             for (int i = 0; i < ngpu; ++i) devs[i] = i;
-            g_group = group_new(devs.data(), ngpu, false);
+            fresh.reset(group_new(devs.data(), ngpu, false));
         }
+        std::lock_guard<std::mutex> lk(g_group_mu);
+        g_group = std::move(fresh);  // the old group goes when its last running call returns
+        g_ndev = ngpu;
     });
 }
 
@@ -1119,12 +1188,9 @@ int apply_env_devices() {
     if (rc != ST_OK) set_last_error(msg);
     return rc;
 }
-// the process-wide group of st_set_devices (nullptr: one device)
-st_group *default_group() { return g_group; }
-uint64_t default_group_sog(const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
-                           const st_sog_textures *dev_out) {
-    const st_table *tabs[1] = {t};
-    return group_sog(g_group, tabs, 1, nullptr, iters, draws, ndraws, meta, dev_out);
+// the process-wide group of st_set_devices (empty: one device); the caller's copy keeps it alive
+std::shared_ptr<st_group> default_group() {
+    std::lock_guard<std::mutex> lk(g_group_mu);
+    return g_group;
 }
-st_ctx *default_group_root() { return g_group ? g_group->ctx[0] : nullptr; }
 }  // namespace st

@@ -101,7 +101,7 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
-    'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_destroy',
+    'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_destroy', 'st_comm_count',
     'st_dev_sog_sharded', 'st_group_create', 'st_group_destroy', 'st_group_sog', 'st_group_sog_bundle',
     'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
@@ -343,6 +343,12 @@ class Comm:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().st_comm_init_rank(ctx.h, ctypes.c_int32(world), ctypes.c_int32(rank), buf, ctypes.byref(self.h)))
         self.world, self.rank = world, rank
+
+    def count(self):
+        """ranks in the communicator (ncclCommCount)"""
+        n = ctypes.c_int32()
+        check(lib().st_comm_count(self.h, ctypes.byref(n)))
+        return n.value
 
     def close(self):
         if self.h:

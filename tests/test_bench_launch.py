@@ -1,0 +1,95 @@
+"""bench.py's multi-GPU launch contract.
+
+CPU: `python bench.py --gpus N` with no launcher around it starts the N-rank job itself (a child
+torch.distributed.run) without importing torch in the parent, relays rank 0's JSON line and fails
+unless the job reports N ranks; the synthetic tables are fixed-seed blocks sliced by global row
+range, so a T-splat table does not depend on how many ranks split it.
+
+GPU: the self-launched 2-rank rehearsal on one GPU (gloo, the torch-harness sharded path)
+prints n_gpus 2 and the same textures_sha256 as one GPU over the same table."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, 'bench.py')
+sys.path.insert(0, ROOT)
+
+
+def test_launcher_command_and_parent_never_imports_torch():
+    r = subprocess.run([sys.executable, BENCH, '--gpus', '8', '--steps', '20', '--warmup', '5', '--launch-dry-run'],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    cmd = out['cmd']
+    assert out['torch_imported'] is False
+    assert cmd[1:3] == ['-m', 'torch.distributed.run']
+    assert '--nproc-per-node=8' in cmd and '--nnodes=1' in cmd and '--master-addr=127.0.0.1' in cmd
+    i = cmd.index(BENCH)
+    assert cmd[i + 1:i + 7] == ['--gpus', '8', '--steps', '20', '--warmup', '5']
+
+
+def _fake_job(tmp_path, n_reported, rc=0):
+    script = tmp_path / 'job.py'
+    script.write_text('import json, sys\n'
+                      'print("rank chatter")\n'
+                      f'print(json.dumps({{"metric": "m", "value": 1.0, "n_gpus": {n_reported}}}))\n'
+                      f'sys.exit({rc})\n')
+    return [sys.executable, str(script)]
+
+
+@pytest.mark.parametrize('reported,rc,want_rc', [(4, 0, 0), (1, 0, 3), (4, 7, 7)])
+def test_launch_relays_rank0_line_and_checks_world(tmp_path, reported, rc, want_rc):
+    """the parent relays exactly the result line; a job that ran the wrong number of ranks or
+    failed makes the parent fail"""
+    code = ('import sys, io, json; sys.path.insert(0, %r); import bench; '
+            'bench.launcher_cmd = lambda argv, n, port: %r; '
+            'bench._RESULT = sys.stdout; sys.stdout = sys.stderr; '
+            'a = bench.parse(["--gpus", "4"]); rc = bench.launch(a, ["--gpus", "4"]); '
+            'assert "torch" not in sys.modules; sys.exit(rc)') % (ROOT, _fake_job(tmp_path, reported, rc))
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == want_rc, r.stderr
+    if want_rc == 0:
+        lines = r.stdout.strip().splitlines()
+        assert len(lines) == 1 and json.loads(lines[0])['n_gpus'] == 4
+        assert 'rank chatter' in r.stderr
+
+
+def test_table_rows_independent_of_the_split():
+    """rows [lo, hi) of a T-row table built from fixed-seed blocks: any split concatenates to the
+    same table (small blocks here; the bench uses 10M-row blocks)"""
+    import torch
+
+    import bench
+    T, blk = 2_500, 1_000
+    whole = bench.table_rows(T, 0, T, 'cpu', block=blk)
+    for cuts in ([0, 700, 2_500], [0, 1_000, 2_000, 2_500], [0, 0, 1_250, 2_499, 2_500]):
+        parts = [bench.table_rows(T, a, b, 'cpu', block=blk) for a, b in zip(cuts, cuts[1:])]
+        for k in whole:
+            assert torch.equal(torch.cat([p[k] for p in parts]), whole[k]), (cuts, k)
+    # 10M-per-GPU weak scaling: rank r's rows are block r (seed 1002 + r)
+    blk0 = bench.synth_table(1_000, bench.SEED + 1, 'cpu')
+    r1 = bench.table_rows(3_000, 1_000, 2_000, 'cpu', block=1_000)
+    assert all(torch.equal(blk0[k], r1[k]) for k in blk0)
+
+
+@pytest.mark.gpu
+def test_self_launched_two_ranks_match_one_gpu(tmp_path):
+    """`bench.py --gpus 2` (no torchrun on the command line) rehearsed on one GPU over gloo: two
+    ranks, and the textures of the 4M-splat table equal one GPU's"""
+    common = ['--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-e2e', '--no-paths', '--no-verify']
+    env = dict(os.environ, PYTHONUNBUFFERED='1')
+    r2 = subprocess.run([sys.executable, BENCH, '--gpus', '2', '--dist-python', '--backend', 'gloo',
+                         '--splats', '2000000'] + common, capture_output=True, text=True, timeout=600, env=env)
+    assert r2.returncode == 0, r2.stderr[-4000:]
+    two = json.loads(r2.stdout.strip().splitlines()[-1])
+    r1 = subprocess.run([sys.executable, BENCH, '--gpus', '1', '--splats', '4000000'] + common,
+                        capture_output=True, text=True, timeout=600, env=env)
+    assert r1.returncode == 0, r1.stderr[-4000:]
+    one = json.loads(r1.stdout.strip().splitlines()[-1])
+    assert two['n_gpus'] == 2 and two['distinct_devices'] == 1 and one['n_gpus'] == 1
+    assert two['config']['splats_total'] == one['config']['splats_total'] == 4_000_000
+    assert two['textures_sha256'] == one['textures_sha256']

@@ -207,3 +207,51 @@ def test_group_bundle_with_input_actions_equals_single_device(ctx, world, splits
     finally:
         g.close()
     assert used == wused and got == want
+
+
+@pytest.mark.parametrize('host_staged,world', [(True, 3), (False, 1)])
+def test_group_usable_after_a_failed_call(ctx, host_staged, world):
+    """a recoverable error inside a group call (draws exhausted on one rank's init) aborts that
+    call's collectives; the group rebuilds them, and the next call succeeds bit for bit"""
+    cols = _table(20_000, 15)
+    draws = np.random.default_rng(17).random(1 << 18)
+    want = ctx.sog(cols, 2, draws)
+    g = sh.Group([0] * world, host_staged=host_staged)
+    try:
+        with pytest.raises(sh.StError) as e:
+            g.sog([cols], 2, draws[:100])  # too few draws for the 1-D and palette inits
+        assert 'another rank failed' not in str(e.value)
+        _same(g.sog([cols], 2, draws), want)
+        with pytest.raises(sh.StError):
+            g.sog([cols], 2, draws[:100])
+        _same(g.sog([cols], 2, draws), want)
+    finally:
+        g.close()
+
+
+def test_comm_count(ctx):
+    comm = sh.Comm(ctx, 1, 0, sh.comm_unique_id())
+    try:
+        assert comm.count() == 1
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize('host_staged,world', [(True, 3), (False, 1)])
+def test_group_one_rank_fails_the_others_are_released(ctx, host_staged, world, monkeypatch):
+    """ST_FAULT_RANK: the last rank throws after the first exchange while the others wait in the
+    next collective; the abort releases them, the caller gets the injected error (not the abort),
+    and the rebuilt group's next call is exact"""
+    cols = _table(20_000, 16)
+    draws = np.random.default_rng(18).random(1 << 18)
+    want = ctx.sog(cols, 2, draws)
+    g = sh.Group([0] * world, host_staged=host_staged)
+    try:
+        monkeypatch.setenv('ST_FAULT_RANK', str(world - 1))
+        with pytest.raises(sh.StError) as e:
+            g.sog([cols], 2, draws)
+        assert 'injected failure' in str(e.value)
+        monkeypatch.delenv('ST_FAULT_RANK')
+        _same(g.sog([cols], 2, draws), want)
+    finally:
+        g.close()
