@@ -61,7 +61,10 @@ def parse(argv=None):
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo with '
                     '--dist-python rehearses several ranks on one GPU)')
-    ap.add_argument('--cpu-assign-sample', type=int, default=3000)
+    ap.add_argument('--cpu-assign-sample', type=int, default=20_000,
+                    help='points of the 1-thread KdTree assign sample (cpu_baseline)')
+    ap.add_argument('--cpu-assign-sample-mt', type=int, default=100_000,
+                    help='points of the all-cores assign sample (cpu_baseline_all_cores; BASELINE.md: 100k rows)')
     ap.add_argument('--cpu-rest-sample', type=int, default=200_000)
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')
@@ -149,8 +152,9 @@ def synth_table(n, seed, device):
 
 
 def cpu_baseline(args):
-    """Time the CPU restatement (oracle/, the reference algorithm in C, 1 thread)
-    on a bounded sample and extrapolate to the bench workload."""
+    """Time the CPU restatement (oracle/, the reference algorithm in C) on a bounded sample and
+    extrapolate to the bench workload: 1 thread (the reference is single-threaded JS) and every
+    host core this job may use (OpenMP over points: assign and the SH0 pipeline's 1-D k-means)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import numpy as np
 
@@ -158,23 +162,24 @@ def cpu_baseline(args):
     oracle.build()
     rng = np.random.default_rng(1002)
     K, D = 65536, 45
-    # (a) one clusterKdTreeCpu pass at K = 65,536 over a point sample; centroids are data rows
-    data = [rng.normal(0, 0.1, K + args.cpu_assign_sample).astype(np.float32) for _ in range(D)]
+    # (a) one clusterKdTreeCpu pass at K = 65,536 over a fixed point sample; centroids are data
+    # rows (the reference's init, k-means.ts:8-20)
+    n1, nmt = args.cpu_assign_sample, args.cpu_assign_sample_mt
+    data = [rng.normal(0, 0.1, K + max(n1, nmt)).astype(np.float32) for _ in range(D)]
     cen = np.stack([c[:K] for c in data])
-    pts = [c[K:] for c in data]
+    oracle.set_threads(1)
     t0 = time.perf_counter()
-    rc, lab1 = oracle.kmeans_assign(pts, cen)
-    ta = (time.perf_counter() - t0) / args.cpu_assign_sample
-    # the same assign on every host core this job may use (OpenMP over points); the box sets
-    # OMP_NUM_THREADS to its CPU share
+    rc, lab1 = oracle.kmeans_assign([c[K:K + n1] for c in data], cen)
+    ta = (time.perf_counter() - t0) / n1
+    # the same assign on every host core this job may use; the box sets OMP_NUM_THREADS to its CPU
+    # share.  The first n1 labels must equal the 1-thread ones.
     threads = int(os.environ.get('OMP_NUM_THREADS') or os.cpu_count() or 1)
-    mt_n = args.cpu_assign_sample * max(1, min(threads, 8))
-    data_mt = [rng.normal(0, 0.1, mt_n).astype(np.float32) for _ in range(D)]
     t0 = time.perf_counter()
-    rc_mt, _ = oracle.kmeans_assign(data_mt, cen, threads=threads)
-    ta_mt = (time.perf_counter() - t0) / mt_n
+    rc_mt, lab_mt = oracle.kmeans_assign([c[K:K + nmt] for c in data], cen, threads=threads)
+    ta_mt = (time.perf_counter() - t0) / nmt
+    same = bool(np.array_equal(np.asarray(lab_mt)[:min(n1, nmt)], np.asarray(lab1)[:min(n1, nmt)]))
     # (b) everything else: the SH0 writeSog pipeline (Morton, means/quats, two cluster1d k-means of
-    # 10 iterations, textures) on a splat sample
+    # 10 iterations, textures) on a splat sample, 1 thread and then with the assign loops threaded
     n = args.cpu_rest_sample
     names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'scale_0', 'scale_1', 'scale_2',
              'rot_0', 'rot_1', 'rot_2', 'rot_3']
@@ -182,24 +187,33 @@ def cpu_baseline(args):
     t0 = time.perf_counter()
     oracle.sog(cols, 0, args.iters, oracle.mulberry32(3, 200_000))
     tb = (time.perf_counter() - t0) / n
+    oracle.set_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        oracle.sog(cols, 0, args.iters, oracle.mulberry32(3, 200_000))
+        tb_mt = (time.perf_counter() - t0) / n
+    finally:
+        oracle.set_threads(1)
     per_splat = args.iters * ta + tb
-    per_splat_mt = args.iters * ta_mt + tb
+    per_splat_mt = args.iters * ta_mt + tb_mt
     all_cores = {
         'value': 1e-6 / per_splat_mt,
         'unit': 'Msplats/s',
         'cores': threads,
         'kind': 'port',
-        'sample': (f'as cpu_baseline with the KdTree assign split over {threads} OpenMP threads on {mt_n} points '
-                   f'({ta_mt * 1e3:.3f} ms/point/iter); the SH0 pipeline part single-threaded'),
+        'sample': (f'oracle/ C restatement on {threads} OpenMP threads: KdTree assign at K=65536, D=45 on a fixed '
+                   f'{nmt}-point sample ({ta_mt * 1e3:.3f} ms/point/iter, labels of the first {min(n1, nmt)} equal '
+                   f'to the 1-thread run: {same}) x {args.iters} iters + SH0 writeSog pipeline with threaded assign '
+                   f'loops on {n} splats ({tb_mt * 1e6:.2f} us/splat); extrapolated per splat'),
     }
     return {
         'value': 1e-6 / per_splat,
         'unit': 'Msplats/s',
         'cores': 1,
         'kind': 'port',
-        'sample': (f'oracle/ C restatement, 1 thread: KdTree assign at K=65536, D=45 timed on '
-                   f'{args.cpu_assign_sample} points ({ta * 1e3:.2f} ms/point/iter) x {args.iters} iters + SH0 '
-                   f'writeSog pipeline timed on {n} splats ({tb * 1e6:.2f} us/splat); extrapolated per splat'),
+        'sample': (f'oracle/ C restatement, 1 thread: KdTree assign at K=65536, D=45 timed on a fixed {n1}-point '
+                   f'sample ({ta * 1e3:.2f} ms/point/iter) x {args.iters} iters + SH0 writeSog pipeline timed on '
+                   f'{n} splats ({tb * 1e6:.2f} us/splat); extrapolated per splat'),
     }, all_cores
 
 

@@ -93,8 +93,10 @@ void use_device(st_ctx *c) { ST_HIP(hipSetDevice(c->device)); }
 namespace {
 constexpr int XF_SLOTS = 4;                 // pinned slots (st_ctx::xfer_ev)
 // bytes per slot and host threads copying one slot (ST_XFER_CHUNK_MB / ST_XFER_THREADS: experiments)
-const size_t XF_CHUNK = (getenv("ST_XFER_CHUNK_MB") ? std::strtoull(getenv("ST_XFER_CHUNK_MB"), nullptr, 10) : 16ull) << 20;
-const int XF_THREADS = getenv("ST_XFER_THREADS") ? std::atoi(getenv("ST_XFER_THREADS")) : 8;
+// (clamped when parsed: a zero chunk would make the piece loop below spin forever)
+const size_t XF_CHUNK = std::max<size_t>(1, std::min<size_t>(1024, getenv("ST_XFER_CHUNK_MB") ?
+    std::strtoull(getenv("ST_XFER_CHUNK_MB"), nullptr, 10) : 16ull)) << 20;
+const int XF_THREADS = std::max(1, std::min(64, getenv("ST_XFER_THREADS") ? std::atoi(getenv("ST_XFER_THREADS")) : 8));
 constexpr size_t XF_DIRECT = 1ull << 20;     // smaller copies go through the runtime as they are
 
 // host threads that run one job at a time, each thread taking its share

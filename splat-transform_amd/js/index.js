@@ -75,6 +75,9 @@ const giveBack = (draws, used) => {
     pending = Array.from(draws.subarray(used)).concat(pending);
 };
 
+// error.code of a call that ran out of draws (ST_ERR_DRAWS = -4, st_abi.h; the addon's throw_st)
+const ST_ERR_DRAWS_CODE = 'ST_STATUS_4';
+
 // run fn(draws) with enough draws; a short buffer (ST_ERR_DRAWS) is retried with
 // a longer one that starts with the same values, so the stream is unchanged
 const withDraws = (estimate, fn) => {
@@ -87,7 +90,7 @@ const withDraws = (estimate, fn) => {
             return res;
         } catch (e) {
             giveBack(draws, 0);
-            if (!/status -4\)/.test(e.message)) throw e;
+            if (e.code !== ST_ERR_DRAWS_CODE) throw e;
             count *= 2;
         }
     }
@@ -243,11 +246,32 @@ const processSchema = (dataTable, actions) => {
 };
 
 // processDataTable(dataTable, processActions) -> DataTable: the whole action list on the device
-// with one upload and one download (transform passes, filters and the row gathers in HBM)
+// with one upload and one download (transform passes, filters and the row gathers in HBM).
+// As in the reference, the transforms before the first filter mutate the caller's columns
+// (process.ts:65-83: `result` is the input table until a filter copies it; filterBands only
+// renames, its columns keep the input's arrays): those run first and are written back into the
+// input arrays, the rest runs on the mutated table.
+const isTransform = a => a.kind === 'translate' || a.kind === 'rotate' || a.kind === 'scale';
+const isFilter = a => a.kind === 'filterNaN' || a.kind === 'filterByValue';
 const processDataTable = (dataTable, processActions) => {
-    const schema = processSchema(dataTable, processActions);
-    const out = addon.process(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
-        normaliseActions(processActions), schema.map(s => s[0]), schema.map(s => s[1]));
+    const cols = () => dataTable.columns.map(c => c.data);
+    const names = dataTable.columns.map(c => c.name);
+    let first = processActions.findIndex(isFilter);
+    if (first < 0) first = processActions.length;
+    const region = processActions.slice(0, first);
+    const rs = processSchema(dataTable, region);
+    if (region.some(isTransform)) {
+        const out = addon.process(cols(), names, normaliseActions(region), rs.map(s => s[0]), rs.map(s => s[1]));
+        rs.forEach((s, j) => dataTable.columns[s[1]].data.set(out[j]));
+    }
+    if (first === processActions.length) {
+        // no filter: the result shares the input's (mutated) arrays, renamed by filterBands
+        return rs.length === dataTable.columns.length && rs.every((s, j) => s[1] === j && s[0] === names[j]) ?
+            dataTable : new DataTable(rs.map(s => new Column(s[0], dataTable.columns[s[1]].data)));
+    }
+    const rest = processActions.filter((a, i) => i >= first || !isTransform(a));  // filterBands re-applied
+    const schema = processSchema(dataTable, rest);
+    const out = addon.process(cols(), names, normaliseActions(rest), schema.map(s => s[0]), schema.map(s => s[1]));
     return new DataTable(schema.map((s, j) => new Column(s[0], out[j])));
 };
 

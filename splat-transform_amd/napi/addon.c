@@ -61,8 +61,10 @@ static st_ctx *g_ctx = NULL;
 
 static napi_value throw_st(napi_env env, int rc) {
     char buf[600];
+    char code[32];
     snprintf(buf, sizeof buf, "splat-hip: %s (status %d)", st_last_error(), rc);
-    napi_throw_error(env, NULL, buf);
+    snprintf(code, sizeof code, "ST_STATUS_%d", -rc);  /* error.code: the st_status, tested by the host */
+    napi_throw_error(env, code, buf);
     return NULL;
 }
 
@@ -130,15 +132,36 @@ static float **f32_list(napi_env env, napi_value arr, uint32_t *count, uint64_t 
     return p;
 }
 
+static void free_strs(char **s, uint32_t m);
+
+/* a JS string as a NUL-terminated heap copy; NULL (TypeError thrown) when v is not a string */
+static char *dup_str(napi_env env, napi_value v, const char *what) {
+    size_t len = 0;
+    char *s;
+    if (napi_get_value_string_utf8(env, v, NULL, 0, &len) != napi_ok) {
+        napi_throw_type_error(env, NULL, what);
+        return NULL;
+    }
+    s = (char *)malloc(len + 1);
+    if (napi_get_value_string_utf8(env, v, s, len + 1, &len) != napi_ok) {
+        free(s);
+        napi_throw_type_error(env, NULL, what);
+        return NULL;
+    }
+    s[len] = 0;
+    return s;
+}
+
+/* array of m strings (caller frees); NULL (TypeError thrown) when an element is not a string */
 static char **str_list(napi_env env, napi_value arr, uint32_t m) {
     char **s = (char **)calloc(m ? m : 1, sizeof(char *));
     for (uint32_t i = 0; i < m; ++i) {
         napi_value e;
-        size_t len = 0;
-        napi_get_element(env, arr, i, &e);
-        napi_get_value_string_utf8(env, e, NULL, 0, &len);
-        s[i] = (char *)malloc(len + 1);
-        napi_get_value_string_utf8(env, e, s[i], len + 1, &len);
+        if (napi_get_element(env, arr, i, &e) != napi_ok ||
+            !(s[i] = dup_str(env, e, "splat-hip: column names must be strings"))) {
+            free_strs(s, i);
+            return NULL;
+        }
     }
     return s;
 }
@@ -204,7 +227,7 @@ static napi_value js_transform(napi_env env, napi_callback_info info) {
     double t[3], r[4];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
-    names = str_list(env, argv[1], m);
+    if (!(names = str_list(env, argv[1], m))) goto fail;
     for (uint32_t i = 0; i < 3; ++i) {
         napi_get_element(env, argv[2], i, &e);
         t[i] = num(env, e);
@@ -421,7 +444,7 @@ static int chain_parse(napi_env env, napi_value cols, napi_value names, napi_val
             return 0;
         }
     }
-    a->names = str_list(env, names, a->m);
+    if (!(a->names = str_list(env, names, a->m))) return 0;
     return parse_actions(env, actions, a);
 }
 
@@ -438,10 +461,7 @@ static int parse_actions(napi_env env, napi_value actions, chain_args *a) {
         x->value = prop_num(env, o, "value");
         x->bands = (int32_t)prop_num(env, o, "bands");
         if (x->kind == ST_ACTION_FILTER_VALUE && napi_get_named_property(env, o, "column", &v) == napi_ok) {
-            size_t len = 0;
-            napi_get_value_string_utf8(env, v, NULL, 0, &len);
-            a->acols[i] = (char *)malloc(len + 1);
-            napi_get_value_string_utf8(env, v, a->acols[i], len + 1, &len);
+            if (!(a->acols[i] = dup_str(env, v, "splat-hip: filterByValue needs a column name string"))) return 0;
             x->column = a->acols[i];
         }
         if (x->kind == ST_ACTION_TRANSFORM) {
@@ -635,7 +655,7 @@ static napi_value js_process(napi_env env, napi_callback_info info) {
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
     if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
     if (napi_get_array_length(env, argv[3], &mo) != napi_ok) goto fail;
-    onames = str_list(env, argv[3], mo);
+    if (!(onames = str_list(env, argv[3], mo))) goto fail;
     dst = (void **)calloc(mo + 1, sizeof(void *));
     otypes = (int32_t *)calloc(mo + 1, sizeof(int32_t));
     osrc = (uint32_t *)calloc(mo + 1, sizeof(uint32_t));
@@ -709,7 +729,7 @@ static napi_value js_combine_layout(napi_env env, napi_callback_info info) {
         NAPI_OK(napi_get_named_property(env, tab, "names", &nv));
         NAPI_OK(napi_get_named_property(env, tab, "types", &tv));
         NAPI_OK(napi_get_array_length(env, nv, &ncols[t]));
-        names[t] = str_list(env, nv, ncols[t]);
+        if (!(names[t] = str_list(env, nv, ncols[t]))) goto fail;
         types[t] = (int32_t *)calloc(ncols[t] + 1, sizeof(int32_t));
         for (uint32_t j = 0; j < ncols[t]; ++j) {
             NAPI_OK(napi_get_element(env, tv, j, &e));
@@ -785,7 +805,7 @@ static napi_value js_pack_compressed(napi_env env, napi_callback_info info) {
     st_ctx *ctx;
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
-    names = str_list(env, argv[1], m);
+    if (!(names = str_list(env, argv[1], m))) goto fail;
     {
         uint32_t *order = (uint32_t *)ta_data(env, argv[2], napi_uint32_array, &no);
         int32_t nsh = (int32_t)num(env, argv[3]);
@@ -918,7 +938,7 @@ static napi_value js_sog(napi_env env, napi_callback_info info) {
     st_ctx *ctx;
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
-    names = str_list(env, argv[1], m);
+    if (!(names = str_list(env, argv[1], m))) goto fail;
     {
         const int32_t iters = (int32_t)num(env, argv[2]);
         double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);
@@ -1033,7 +1053,7 @@ static napi_value js_sog_bundle(napi_env env, napi_callback_info info) {
     st_ctx *ctx;
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (!(cols = f32_list(env, argv[0], &m, &n))) return NULL;
-    names = str_list(env, argv[1], m);
+    if (!(names = str_list(env, argv[1], m))) goto fail;
     {
         const int32_t iters = (int32_t)num(env, argv[2]);
         double *draws = (double *)ta_data(env, argv[3], napi_float64_array, &nd);

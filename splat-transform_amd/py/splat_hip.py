@@ -407,13 +407,14 @@ def make_actions(actions):
     return arr
 
 
-def process_schema(items, actions):
+def process_schema(items, actions, with_source=False):
     """the (name, dtype) columns processDataTable leaves (filterBands renames / drops f_rest
-    columns against the ORIGINAL table's band, process.ts:110-134)"""
+    columns against the ORIGINAL table's band, process.ts:110-134); with_source: (name, dtype,
+    index of the input column it is)"""
     names = [k for k, _ in items]
     first_missing = next((i for i in range(45) if f'f_rest_{i}' not in names), -1)
     in_coeffs = {9: 3, 24: 8, -1: 15}.get(first_missing, 0)
-    cols = [(k, np.dtype(a.dtype)) for k, a in items]
+    cols = [(k, np.dtype(a.dtype), i) for i, (k, a) in enumerate(items)]
     for act in actions:
         if act['kind'] != 'filterBands':
             continue
@@ -424,8 +425,12 @@ def process_schema(items, actions):
         for i in range(in_coeffs):
             for j in range(3):
                 mp[f'f_rest_{i + j * in_coeffs}'] = f'f_rest_{i + j * out_coeffs}' if i < out_coeffs else None
-        cols = [(mp[k], t) if k in mp else (k, t) for k, t in cols if k not in mp or mp[k] is not None]
-    return cols
+        cols = [(mp[k], t, i) if k in mp else (k, t, i) for k, t, i in cols if k not in mp or mp[k] is not None]
+    return cols if with_source else [(k, t) for k, t, _ in cols]
+
+
+TRANSFORM_KINDS = ('translate', 'rotate', 'scale')
+FILTER_KINDS = ('filterNaN', 'filterByValue')
 
 
 def sog_geometry(n, sh_coeffs):
@@ -771,8 +776,24 @@ class Context:
 
     def process(self, cols, actions):
         """processDataTable (process.ts:64-145) on host columns (list of (name, numpy array) or a
-        dict) in one upload -> the processed table as a list of (name, array)"""
+        dict) in one upload -> the processed table as a list of (name, array).  As in the
+        reference, the transforms before the first filter mutate the input arrays (`result` is
+        the input table until a filter copies it; filterBands renames its columns without copying
+        them): that region runs first and is written back, the rest runs on the mutated columns.
+        Without a filter the result's arrays ARE the input's."""
         items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        first = next((i for i, a in enumerate(actions) if a['kind'] in FILTER_KINDS), len(actions))
+        region = actions[:first]
+        rs = process_schema(items, region, with_source=True)
+        if any(a['kind'] in TRANSFORM_KINDS for a in region):
+            for (_, a), (_, src) in zip(self._process(items, region), rs):
+                np.copyto(items[src][1], a)
+        if first == len(actions):
+            return [(k, items[src][1]) for k, _, src in rs]
+        return self._process(items, [a for i, a in enumerate(actions) if i >= first or a['kind'] not in TRANSFORM_KINDS])
+
+    def _process(self, items, actions):
+        """st_process: the action list in one upload, the input untouched"""
         n = len(items[0][1]) if items else 0
         out = [(k, np.empty(n, t)) for k, t in process_schema(items, actions)]
         ts, td = make_ttable(items), make_ttable(out, n)

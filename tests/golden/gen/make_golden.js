@@ -718,6 +718,17 @@ cases.process_chain = async () => {
         specs.push(['sh0_two_filters', names, cols, [{ kind: 'filterBands', value: 3 }, { kind: 'filterNaN' },
             { kind: 'filterByValue', columnName: 'opacity', comparator: 'lt', value: 2 }, { kind: 'scale', value: 0.5 }]]);
     }
+    {   // transforms after a filterBands (before any filter) rotate the renamed band-1 view, whose
+        // columns are the input's arrays (process.ts:110-134): the input is mutated through them
+        const { names, cols } = makeSplats(1800, 15, 909);
+        cols.z[5] = NaN;
+        specs.push(['bands_rotate_nan', names, cols, [{ kind: 'filterBands', value: 1 },
+            { kind: 'rotate', value: V(10, 20, 30) }, { kind: 'translate', value: V(1, 0, 0) }, { kind: 'filterNaN' }]]);
+    }
+    {   // transforms only: the result IS the input table, mutated
+        const { names, cols } = makeSplats(1000, 8, 910);
+        specs.push(['transforms_only', names, cols, [{ kind: 'scale', value: 1.5 }, { kind: 'rotate', value: V(0, 0, 90) }]]);
+    }
     fx.meta.cases = specs.map(s => s[0]);
     const actionsMeta = (acts) => acts.map(a => (a.value && a.value.x !== undefined)
         ? Object.assign({}, a, { value: [a.value.x, a.value.y, a.value.z] }) : a);
@@ -728,6 +739,8 @@ cases.process_chain = async () => {
         const out = processDataTable(table, acts);
         fx.meta[`${name}_out_types`] = out.columns.map(c => c.dataType);
         addTable(fx, `${name}_out_`, out);
+        // the input table afterwards: the transforms before the first filter mutate it in place
+        addTable(fx, `${name}_after_`, table);
         const { writes, handle } = captureHandle();
         try {
             await quiet(() => writeCompressedPly(handle, out));

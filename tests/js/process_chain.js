@@ -29,7 +29,10 @@ const tableOf = c => new host.DataTable(man.meta[`${c}_in_columns`].map(n => new
     const out = {};
     for (const c of man.meta.cases) {
         const r = {};
-        const res = host.processDataTable(tableOf(c), actionsOf(c));
+        const input = tableOf(c);
+        const res = host.processDataTable(input, actionsOf(c));
+        // the caller's table afterwards (transforms before the first filter mutate it in place)
+        r.after = input.columns.every(col => sameBytes(col.data, arr(`${c}_after_${col.name}`)));
         r.names = JSON.stringify(res.columns.map(col => col.name)) === JSON.stringify(man.meta[`${c}_out_columns`]);
         r.table = res.columns.every(col => sameBytes(col.data, arr(`${c}_out_${col.name}`)));
         const writes = [];

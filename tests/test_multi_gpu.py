@@ -197,8 +197,9 @@ def test_group_bundle_with_input_actions_equals_single_device(ctx, world, splits
             [{'kind': 'scale', 'value': 2.0}, {'kind': 'filterByValue', 'columnName': 'opacity', 'comparator': 'gt',
                                                'value': 0.0}, {'kind': 'filterBands', 'value': 1}]]
     draws = np.random.default_rng(13).random(1 << 18)
-    pa = ctx.process(list(a.items()), acts[0])
-    pb = ctx.process(list(b.items()), acts[1])
+    # (copies: processDataTable's leading transforms mutate their input, as the reference's do)
+    pa = ctx.process([(k, v.copy()) for k, v in a.items()], acts[0])
+    pb = ctx.process([(k, v.copy()) for k, v in b.items()], acts[1])
     combined = dict(oracle.combine([pa, pb]))
     want, wused = ctx.sog_bundle(combined, 2, draws, 0x6000, 0x5a21)
     g = sh.Group([0] * world, host_staged=True)

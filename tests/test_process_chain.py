@@ -81,6 +81,23 @@ def test_process_matches_reference(ctx, case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES)
+def test_process_mutates_input_like_reference(ctx, case):
+    """the transforms before the first filter change the caller's columns in place (process.ts:65-83,
+    filterBands' renamed columns included): the input afterwards equals the reference's"""
+    src, acts, want = _case(G, case)
+    src = [(k, a.copy()) for k, a in src]
+    out = ctx.process(src, acts)
+    for k, a in src:
+        _bytes_equal(a, G[f'{case}_after_{k}'], k)
+    for (k, a), (_, b) in zip(out, want):
+        _bytes_equal(a, b, k)
+    if not any(a['kind'] in ('filterNaN', 'filterByValue') for a in acts):
+        srcs = {id(a) for _, a in src}
+        assert all(id(a) in srcs for _, a in out), 'without a filter the result shares the input arrays'
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('case', ['config3', 'bands2_lte', 'empty'])
 def test_dev_compressed_ply_matches_reference(ctx, case):
     import torch
