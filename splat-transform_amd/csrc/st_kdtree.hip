@@ -297,19 +297,170 @@ __global__ __launch_bounds__(256) void k_tie_copy(const uint32_t *__restrict__ f
         if (!flag[j]) labels[tie_pts[vals[j]]] = labels[walkers[pos[j] - 1]];
 }
 
+// ---- coinciding centroids ----------------------------------------------------------
+// Duplicated input rows make the init (and re-seeds) draw several centroids with the same
+// row.  They are at exactly the same distance from every point, so a point whose nearest row
+// is such a group ties on all of its members and the reference's answer is the member its
+// KdTree walk meets first.  The assign therefore sweeps one representative per distinct row
+// (the group's lowest index) and settles a point that lands on a group of several with a
+// descent of the reference's tree (k_group_descent) instead of a walk over it.
+//
+// Rows compare as the distance sees them: -0 and +0 are the same coordinate (every difference
+// and square, and the tree's sort key, treat them alike).
+__device__ inline uint32_t canon_bits(float x) { return __builtin_bit_cast(uint32_t, x == 0.0f ? 0.0f : x); }
+
+// open-addressing table keyed by a 64-bit hash of the canonical row; the slot keeps the
+// lowest index that inserted it
+__global__ __launch_bounds__(256) void k_cen_hash(const float *__restrict__ cen, int d, int k,
+                                                  unsigned long long *__restrict__ tkey, uint32_t *__restrict__ tval,
+                                                  uint32_t tmask, uint32_t *__restrict__ gslot) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)k; i += gridDim.x * blockDim.x) {
+        uint64_t h = 0x9e3779b97f4a7c15ull;
+        for (int a = 0; a < d; ++a) {
+            h ^= canon_bits(cen[(uint64_t)a * k + i]);
+            h *= 0xff51afd7ed558ccdull;
+            h ^= h >> 33;
+        }
+        h |= 1ull;  // 0 marks an empty slot
+        uint32_t slot = (uint32_t)(h >> 17) & tmask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&tkey[slot], 0ull, (unsigned long long)h);
+            if (prev == 0ull || prev == h) {
+                atomicMin(&tval[slot], i);
+                gslot[i] = slot;
+                break;
+            }
+            slot = (slot + 1) & tmask;
+        }
+    }
+}
+
+// rep[i] = the lowest index with i's row; a hash collision between different rows (a member
+// whose row differs from its representative's) is reported and the caller keeps every centroid
+__global__ __launch_bounds__(256) void k_cen_group(const float *__restrict__ cen, int d, int k,
+                                                   const uint32_t *__restrict__ tval, const uint32_t *__restrict__ gslot,
+                                                   uint32_t *__restrict__ rep, uint32_t *__restrict__ is_rep,
+                                                   uint32_t *__restrict__ stat) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)k; i += gridDim.x * blockDim.x) {
+        const uint32_t r = tval[gslot[i]];
+        bool same = r <= i;
+        for (int a = 0; a < d && same; ++a) same = canon_bits(cen[(uint64_t)a * k + i]) == canon_bits(cen[(uint64_t)a * k + r]);
+        if (!same) atomicOr(&stat[1], 1u);
+        rep[i] = r;
+        is_rep[i] = r == i ? 1u : 0u;
+        if (r != i) atomicAdd(&stat[0], 1u);
+    }
+}
+
+// the representatives' rows as a [d][kr] centroid table; grp[i] = the slot of i's group
+__global__ __launch_bounds__(256) void k_cen_compact(const float *__restrict__ cen, int d, int k,
+                                                     const uint32_t *__restrict__ rep,
+                                                     const uint32_t *__restrict__ rslot, uint32_t kr,
+                                                     float *__restrict__ cen_r, uint32_t *__restrict__ map_r2c,
+                                                     uint32_t *__restrict__ grp) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)k; i += gridDim.x * blockDim.x) {
+        const uint32_t g = rslot[rep[i]];
+        grp[i] = g;
+        if (rep[i] == i) {
+            map_r2c[g] = i;
+            for (int a = 0; a < d; ++a) cen_r[(uint64_t)a * kr + g] = cen[(uint64_t)a * k + i];
+        }
+    }
+}
+
+// (group slot << 32 | tree position) of every centroid: sorted, each group's positions ascend
+__global__ __launch_bounds__(256) void k_group_keys(const uint32_t *__restrict__ S, const uint32_t *__restrict__ grp,
+                                                    int k, uint64_t *__restrict__ keys) {
+    for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < (uint32_t)k; pos += gridDim.x * blockDim.x)
+        keys[pos] = ((uint64_t)grp[S[pos]] << 32) | pos;
+}
+__global__ __launch_bounds__(256) void k_group_starts(const uint64_t *__restrict__ keys, int k, uint32_t kr,
+                                                      uint32_t *__restrict__ gstart, uint32_t *__restrict__ gpos) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < (uint32_t)k; j += gridDim.x * blockDim.x) {
+        const uint32_t g = (uint32_t)(keys[j] >> 32);
+        gpos[j] = (uint32_t)keys[j];
+        if (j == 0 || (uint32_t)(keys[j - 1] >> 32) != g) gstart[g] = j;
+        if (j == 0) gstart[kr] = (uint32_t)k;
+    }
+}
+
+// labels[p] holds the slot of p's nearest distinct row (the unique minimum).  A group of one:
+// its centroid.  A group of several: every member is at p's minimal distance and no other
+// centroid is, so the reference's walk (kd-tree.ts:39-68) returns the first member it visits.
+// Its pruning never skips a member before one is found (a subtree is skipped only when every
+// node in it is at least the current best away), so that member is the first in the walk's
+// visit order: at each node the near side's subtree, then the node, then the far side.  The
+// descent follows that order, asking at each node whether the near subtree -- a contiguous
+// range of tree positions -- holds a member (binary search in the group's sorted positions).
+__global__ __launch_bounds__(256) void k_group_descent(int d, int k, const uint32_t *__restrict__ S,
+                                                       const float *__restrict__ split,
+                                                       const uint32_t *__restrict__ gstart,
+                                                       const uint32_t *__restrict__ gpos,
+                                                       const uint32_t *__restrict__ map_r2c,
+                                                       const float *__restrict__ aos, int ld, uint64_t n,
+                                                       uint32_t *__restrict__ labels, uint32_t *__restrict__ err) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = labels[p];
+        const uint32_t s = gstart[g], e = gstart[g + 1];
+        if (e - s == 1) {
+            labels[p] = map_r2c[g];
+            continue;
+        }
+        auto any_in = [&](uint32_t a, uint32_t b) {
+            if (b <= a) return false;
+            uint32_t lo = s, hi = e;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (gpos[mid] < a) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo < e && gpos[lo] < b;
+        };
+        const float *prow = aos + p * ld;
+        uint32_t lo = 0, hi = (uint32_t)k, depth = 0, got = 0xffffffffu;
+        while (hi > lo && depth < 64) {
+            uint32_t node, llo, lhi, rlo, rhi;
+            seg_split(lo, hi, node, llo, lhi, rlo, rhi);
+            const double distance = (double)prow[depth % (uint32_t)d] - (double)split[node];
+            const bool right = distance > 0;
+            const uint32_t nlo = right ? rlo : llo, nhi = right ? rhi : lhi;
+            if (any_in(nlo, nhi)) {
+                lo = nlo, hi = nhi;
+            } else if (any_in(node, node + 1)) {
+                got = S[node];
+                break;
+            } else {
+                lo = right ? llo : rlo, hi = right ? lhi : rhi;
+            }
+            ++depth;
+        }
+        if (got == 0xffffffffu) atomicOr(err, ERR_INTERNAL);  // cannot happen: the group is in the tree
+        labels[p] = got;
+    }
+}
+
+std::unordered_map<int64_t, std::unique_ptr<KdLayout>> &layouts() {
+    static thread_local std::unordered_map<int64_t, std::unique_ptr<KdLayout>> m;
+    return m;
+}
+
+KdLayout &layout_of(st_ctx *c, int k) {
+    auto &L = layouts()[((int64_t)c->device << 32) | (uint32_t)k];
+    if (!L) L = make_layout(k);
+    return *L;
+}
+
 }  // namespace
 
-void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
-                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels) {
-    static thread_local std::unordered_map<int64_t, std::unique_ptr<KdLayout>> layouts;
-    auto &L = layouts[((int64_t)c->device << 32) | (uint32_t)k];
-    if (!L) L = make_layout(k);
+// KdTree.build (kd-tree.ts:73-99) of the centroids cen [d][k]: S[tree position] = centroid
+const uint32_t *kd_build(st_ctx *c, int d, int k, const float *cen) {
+    KdLayout &L = layout_of(c, k);
     auto *S = wsT<uint32_t>(c, "kd.S", (size_t)k);
     auto *keys = wsT<uint64_t>(c, "kd.keys", (size_t)k);
     auto *vals = wsT<uint32_t>(c, "kd.vals", (size_t)k);
     iota_u32(c, S, (uint64_t)k);
-    for (size_t lv = 0; lv < L->levels.size(); ++lv) {
-        const Level &v = L->levels[lv];
+    for (size_t lv = 0; lv < L.levels.size(); ++lv) {
+        const Level &v = L.levels[lv];
         const int axis = (int)(lv % (size_t)d);
         hipLaunchKernelGGL(k_level_keys, dim3(grid_for(v.count, 256, 1024)), dim3(256), 0, c->stream, cen, k, axis, S,
                            v.pos, v.rank, v.count, keys, vals);
@@ -319,6 +470,68 @@ void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos
                            v.count, S);
         ST_LAUNCH_CHECK();
     }
+    return S;
+}
+
+bool cen_groups(st_ctx *c, int d, int k, const float *cen, CenGroups *out) {
+    uint32_t tsize = 1024;
+    while (tsize < 4u * (uint32_t)k) tsize <<= 1;
+    auto *tkey = wsT<unsigned long long>(c, "cg.tkey", tsize);
+    auto *tval = wsT<uint32_t>(c, "cg.tval", tsize);
+    auto *gslot = wsT<uint32_t>(c, "cg.gslot", (size_t)k);
+    auto *rep = wsT<uint32_t>(c, "cg.rep", (size_t)k);
+    auto *is_rep = wsT<uint32_t>(c, "cg.isrep", (size_t)k + 1);
+    auto *stat = wsT<uint32_t>(c, "cg.stat", 4);  // [0] non-representatives [1] collision [2] kr
+    ST_HIP(hipMemsetAsync(tkey, 0, (size_t)tsize * 8, c->stream));
+    ST_HIP(hipMemsetAsync(tval, 0xff, (size_t)tsize * 4, c->stream));
+    ST_HIP(hipMemsetAsync(stat, 0, 16, c->stream));
+    const unsigned g = grid_for((uint64_t)k, 256, 1024);
+    hipLaunchKernelGGL(k_cen_hash, dim3(g), dim3(256), 0, c->stream, cen, d, k, tkey, tval, tsize - 1, gslot);
+    hipLaunchKernelGGL(k_cen_group, dim3(g), dim3(256), 0, c->stream, cen, d, k, tval, gslot, rep, is_rep, stat);
+    ST_LAUNCH_CHECK();
+    auto *h = static_cast<uint32_t *>(pinned_slot(c, "cg.stat", 16));
+    ST_HIP(hipMemcpyAsync(h, stat, 8, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    if (h[0] == 0 || h[1] != 0) return false;  // all rows distinct (or a hash collision: keep all)
+    auto *rslot = wsT<uint32_t>(c, "cg.rslot", (size_t)k + 1);
+    scan_u32(c, is_rep, rslot, (uint64_t)k, rslot + k);
+    const uint32_t kr = (uint32_t)k - h[0];
+    out->kr = kr;
+    out->cen_r = wsT<float>(c, "cg.cen", (size_t)kr * d);
+    out->map_r2c = wsT<uint32_t>(c, "cg.map", kr);
+    out->grp = wsT<uint32_t>(c, "cg.grp", (size_t)k);
+    hipLaunchKernelGGL(k_cen_compact, dim3(g), dim3(256), 0, c->stream, cen, d, k, rep, rslot, kr, out->cen_r,
+                       out->map_r2c, out->grp);
+    ST_LAUNCH_CHECK();
+    return true;
+}
+
+void kd_group_labels(st_ctx *c, int d, int k, const float *cen, const CenGroups &g, const float *aos, int ld,
+                     uint64_t n, uint32_t *labels, uint32_t *err) {
+    KdLayout &L = layout_of(c, k);
+    const uint32_t *S = kd_build(c, d, k, cen);
+    auto *split = wsT<float>(c, "kd.split", (size_t)k);
+    auto *keys = wsT<uint64_t>(c, "cg.keys", (size_t)k);
+    auto *vals = wsT<uint32_t>(c, "cg.vals", (size_t)k);
+    auto *gstart = wsT<uint32_t>(c, "cg.gstart", (size_t)g.kr + 1);
+    auto *gpos = wsT<uint32_t>(c, "cg.gpos", (size_t)k);
+    const unsigned gk = grid_for((uint64_t)k, 256, 1024);
+    hipLaunchKernelGGL(k_tree_split, dim3(gk), dim3(256), 0, c->stream, cen, k, d, S, L.depth, split);
+    hipLaunchKernelGGL(k_group_keys, dim3(gk), dim3(256), 0, c->stream, S, g.grp, k, keys);
+    ST_LAUNCH_CHECK();
+    int bits = 0;
+    while ((1u << bits) < g.kr) ++bits;
+    radix_sort_u64(c, keys, vals, (uint64_t)k, 0, 32 + bits, "cg.rs");
+    hipLaunchKernelGGL(k_group_starts, dim3(gk), dim3(256), 0, c->stream, keys, k, g.kr, gstart, gpos);
+    hipLaunchKernelGGL(k_group_descent, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, d, k, S, split,
+                       gstart, gpos, g.map_r2c, aos, ld, n, labels, err);
+    ST_LAUNCH_CHECK();
+}
+
+void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
+                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels, bool tree_built) {
+    KdLayout *L = &layout_of(c, k);
+    const uint32_t *S = tree_built ? wsT<uint32_t>(c, "kd.S", (size_t)k) : kd_build(c, d, k, cen);
     // one thread per listed point, distances computed at the visited nodes only
     if (nties < 4096) {
         hipLaunchKernelGGL(k_kd_walk<false>, dim3((nties + 255) / 256), dim3(256), 0, c->stream, d, cen, k, S, aos,

@@ -83,7 +83,25 @@ void check_finite(st_ctx *c, const float *const *cols, const float *const *dcols
 // KdTree.findNearest for the points listed in tie_pts (exact-distance ties, candidate
 // overflows): cen [d][k] for the tree, the row-major copies aos (points) / caos (centroids)
 // with row stride ld (zero padded) for the distances (st_kdtree.hip)
+// (tree_built: kd_build already ran on these centroids in this call)
 void kd_resolve_ties(st_ctx *c, int d, int k, const float *cen, const float *aos, const float *caos, int ld,
-                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels);
+                     const uint32_t *tie_pts, uint32_t nties, uint32_t *labels, bool tree_built = false);
+// KdTree.build of cen [d][k]: the device array S[tree position] = centroid index (workspace kd.S)
+const uint32_t *kd_build(st_ctx *c, int d, int k, const float *cen);
+
+// coinciding centroids (identical rows, -0 == +0): one representative per distinct row
+struct CenGroups {
+    uint32_t kr = 0;        // distinct rows
+    float *cen_r = nullptr;     // [d][kr] the representatives' rows (each group's lowest index)
+    uint32_t *map_r2c = nullptr;  // [kr] representative slot -> centroid index
+    uint32_t *grp = nullptr;      // [k] centroid -> its group's slot
+};
+// false when every row is distinct (nothing written); one host sync
+bool cen_groups(st_ctx *c, int d, int k, const float *cen, CenGroups *g);
+// labels[p] = slot of p's nearest distinct row (a unique minimum) -> the reference's centroid:
+// the group's only member, or the member KdTree.findNearest meets first (a descent of the tree)
+// (err: ERR_INTERNAL if a point's group is not found in the tree)
+void kd_group_labels(st_ctx *c, int d, int k, const float *cen, const CenGroups &g, const float *aos, int ld,
+                     uint64_t n, uint32_t *labels, uint32_t *err);
 
 }  // namespace st

@@ -58,7 +58,7 @@ constexpr int NW = 4;          // waves per workgroup (they share the LDS centro
 constexpr int WG = 64 * NW;    // threads per workgroup
 constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
-// members above which a cluster's sum is split over a workgroup (k_sumnd_big); ST_SUMND_BIG
+// members above which a cluster's sum is split over many workgroups (k_big_*); ST_SUMND_BIG
 // lowers it so that tests drive that path with small inputs
 uint32_t sumnd_big() {
     const char *e = getenv("ST_SUMND_BIG");  // read per call (tests set it around one call)
@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    if (s0 == s1 || lane >= d || s1 - s0 > big) return;  // huge clusters: k_sumnd_big
+    if (s0 == s1 || lane >= d || s1 - s0 > big) return;  // huge clusters: k_big_*
     const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
@@ -1017,81 +1017,131 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     cen[(uint64_t)lane * k + cl] = (float)(sum / (double)(s1 - s0));
 }
 
-// clusters of more than `big` members (duplicated points pile into one): 16 waves of a
-// workgroup sum contiguous slices of the member list, each with sum|x| and the smallest ulp
-// exponent; when the certificate holds for a dimension every partial sum is exact, so the
-// slices' sums add to the sequential result, otherwise one lane runs the sequential chain.
-// A few workgroups scan the cluster list for the huge ones.
-__global__ __launch_bounds__(1024) void k_sumnd_big(const float *__restrict__ aos, int d,
-                                                    const uint32_t *__restrict__ members,
-                                                    const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
-                                                    uint32_t big) {
-    __shared__ double ps[16][64], pa[16][64];
-    __shared__ int pe[16][64];
-    __shared__ uint32_t list[1024];
-    __shared__ uint32_t nlist;
+// clusters of more than `big` members (duplicated points pile into one, e.g. every all-zero
+// row of a table in one cluster) are cut into slices of SB_SLICE members summed by many
+// workgroups at once, each slice with sum|x| and the smallest ulp exponent; when the
+// certificate holds for a dimension every partial sum is exact, so the slices' sums add to the
+// sequential result, otherwise one lane runs the sequential chain over the whole cluster.
+constexpr uint32_t SB_SLICE = 4096;
+
+// one workgroup: the clusters above `big` and the running count of their slices
+__global__ __launch_bounds__(1024) void k_big_list(const uint32_t *__restrict__ start, int k, uint32_t big,
+                                                   uint32_t cap, uint32_t *__restrict__ list,
+                                                   uint32_t *__restrict__ soff, uint32_t *__restrict__ nlist) {
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (uint32_t c0 = threadIdx.x; c0 < (uint32_t)k; c0 += 1024)
+        if (start[c0 + 1] - start[c0] > big) {
+            const uint32_t i = atomicAdd(&cnt, 1u);
+            if (i < cap) list[i] = c0;
+        }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m = min(cnt, cap);  // cap = n / (big + 1) + 1 clusters can exceed big
+        uint32_t o = 0;
+        for (uint32_t i = 0; i < m; ++i) {
+            soff[i] = o;
+            o += (start[list[i] + 1] - start[list[i]] + SB_SLICE - 1) / SB_SLICE;
+        }
+        soff[m] = o;
+        *nlist = m;
+    }
+}
+
+// slice s of the listed clusters: 4 waves, lane = dimension; (sum, sum|x|, min ulp exponent)
+__global__ __launch_bounds__(256) void k_big_partial(const float *__restrict__ aos, int d,
+                                                     const uint32_t *__restrict__ members,
+                                                     const uint32_t *__restrict__ start,
+                                                     const uint32_t *__restrict__ list,
+                                                     const uint32_t *__restrict__ soff,
+                                                     const uint32_t *__restrict__ nlist, double *__restrict__ psum,
+                                                     double *__restrict__ pabs, int *__restrict__ pemin) {
+    __shared__ double ls[4][64], la[4][64];
+    __shared__ int le[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ld = aos_ld(d);
-    for (uint32_t base = blockIdx.x * 1024u; base < (uint32_t)k; base += gridDim.x * 1024u) {
-        if (threadIdx.x == 0) nlist = 0;
-        __syncthreads();
-        const uint32_t c0 = base + threadIdx.x;
-        if (c0 < (uint32_t)k && start[c0 + 1] - start[c0] > big) list[atomicAdd(&nlist, 1u)] = c0;
-        __syncthreads();
-        const uint32_t nl = nlist;
-        for (uint32_t i = 0; i < nl; ++i) {
-            const uint32_t cl = list[i];
-            const uint32_t s0 = start[cl], s1 = start[cl + 1], m = s1 - s0;
-            const uint32_t per = (m + 15) / 16;
-            const uint32_t a = s0 + min(m, w * per), b = s0 + min(m, (w + 1) * per);
-            double sum = 0, sabs = 0;
-            int emin = 0x7fffffff;
-            auto take = [&](float x) {
-                sum += (double)x;
-                sabs += __builtin_fabs((double)x);
-                if (x != 0.0f) emin = min(emin, ulp_exp(x));
-            };
-            if (lane < d) {
-                constexpr int U = 32;  // member rows in flight, as k_sumnd
-                uint32_t j = a;
-                for (; j + U <= b; j += U) {
-                    float v[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) take(v[u]);
-                }
-                for (; j < b; ++j) take(aos[(uint64_t)members[j] * ld + lane]);
-            }
-            ps[w][lane] = sum;
-            pa[w][lane] = sabs;
-            pe[w][lane] = emin;
-            __syncthreads();
-            if (w == 0 && lane < d) {
-                double S = 0, A = 0;
-                int E = 0x7fffffff;
-                for (int q = 0; q < 16; ++q) {
-                    S += ps[q][lane];
-                    A += pa[q][lane];
-                    E = min(E, pe[q][lane]);
-                }
-                if (!sum_is_exact(A, E)) {  // the sequential chain (k-means.ts:41-63)
-                    S = 0;
-                    constexpr int U = 32;
-                    uint32_t j = s0;
-                    for (; j + U <= s1; j += U) {
-                        float v[U];
-#pragma unroll
-                        for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
-#pragma unroll
-                        for (int u = 0; u < U; ++u) S += (double)v[u];
-                    }
-                    for (; j < s1; ++j) S += (double)aos[(uint64_t)members[j] * ld + lane];
-                }
-                cen[(uint64_t)lane * k + cl] = (float)(S / (double)m);
-            }
-            __syncthreads();
+    const uint32_t nl = *nlist, total = soff[nl];
+    for (uint32_t sl = blockIdx.x; sl < total; sl += gridDim.x) {
+        uint32_t lo = 0, hi = nl;  // the listed cluster whose slices hold sl
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (soff[mid] <= sl) lo = mid;
+            else hi = mid;
         }
+        const uint32_t cl = list[lo];
+        const uint32_t s0 = start[cl] + (sl - soff[lo]) * SB_SLICE;
+        const uint32_t s1 = min(start[cl + 1], s0 + SB_SLICE);
+        const uint32_t per = (s1 - s0 + 3) / 4;
+        const uint32_t a = s0 + min(s1 - s0, w * per), b = s0 + min(s1 - s0, (w + 1) * per);
+        double sum = 0, sabs = 0;
+        int emin = 0x7fffffff;
+        auto take = [&](float x) {
+            sum += (double)x;
+            sabs += __builtin_fabs((double)x);
+            if (x != 0.0f) emin = min(emin, ulp_exp(x));
+        };
+        if (lane < d) {
+            constexpr int U = 32;  // member rows in flight, as k_sumnd
+            uint32_t j = a;
+            for (; j + U <= b; j += U) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+                for (int u = 0; u < U; ++u) take(v[u]);
+            }
+            for (; j < b; ++j) take(aos[(uint64_t)members[j] * ld + lane]);
+        }
+        ls[w][lane] = sum;
+        la[w][lane] = sabs;
+        le[w][lane] = emin;
+        __syncthreads();
+        if (w == 0 && lane < d) {
+            psum[(uint64_t)sl * 64 + lane] = ((ls[0][lane] + ls[1][lane]) + ls[2][lane]) + ls[3][lane];
+            pabs[(uint64_t)sl * 64 + lane] = ((la[0][lane] + la[1][lane]) + la[2][lane]) + la[3][lane];
+            pemin[(uint64_t)sl * 64 + lane] = min(min(le[0][lane], le[1][lane]), min(le[2][lane], le[3][lane]));
+        }
+        __syncthreads();
+    }
+}
+
+// one wave per listed cluster, lane = dimension: the slices' sums under the certificate, else
+// the sequential chain (k-means.ts:41-63)
+__global__ __launch_bounds__(64) void k_big_final(const float *__restrict__ aos, int d,
+                                                  const uint32_t *__restrict__ members,
+                                                  const uint32_t *__restrict__ start, int k,
+                                                  const uint32_t *__restrict__ list, const uint32_t *__restrict__ soff,
+                                                  const uint32_t *__restrict__ nlist, const double *__restrict__ psum,
+                                                  const double *__restrict__ pabs, const int *__restrict__ pemin,
+                                                  float *__restrict__ cen) {
+    const int lane = threadIdx.x;
+    const int ld = aos_ld(d);
+    const uint32_t nl = *nlist;
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        if (lane >= d) continue;
+        const uint32_t cl = list[i], s0 = start[cl], s1 = start[cl + 1], m = s1 - s0;
+        double S = 0, A = 0;
+        int E = 0x7fffffff;
+        for (uint32_t sl = soff[i]; sl < soff[i + 1]; ++sl) {
+            S += psum[(uint64_t)sl * 64 + lane];
+            A += pabs[(uint64_t)sl * 64 + lane];
+            E = min(E, pemin[(uint64_t)sl * 64 + lane]);
+        }
+        if (!sum_is_exact(A, E)) {
+            S = 0;
+            constexpr int U = 32;
+            uint32_t j = s0;
+            for (; j + U <= s1; j += U) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+#pragma unroll
+                for (int u = 0; u < U; ++u) S += (double)v[u];
+            }
+            for (; j < s1; ++j) S += (double)aos[(uint64_t)members[j] * ld + lane];
+        }
+        cen[(uint64_t)lane * k + cl] = (float)(S / (double)m);
     }
 }
 
@@ -1187,8 +1237,55 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     mark(c, "kn.prep");
 }
 
+namespace {
+__global__ __launch_bounds__(256) void k_rows_aos(const float *__restrict__ cen, int d, int k, float *__restrict__ caos) {
+    const int ld = aos_ld(d);
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < (uint64_t)k * ld;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(f / ld), a = (uint32_t)(f % ld);
+        caos[f] = a < (uint32_t)d ? cen[(uint64_t)a * k + r] : 0.0f;
+    }
+}
+
+uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+                        uint32_t *labels, km::State *dstate, bool walk_ties);
+}  // namespace
+
+// The assign over the distinct centroid rows: when several centroids share a row (duplicated
+// input rows drawn by the init or a re-seed), the sweep and its fix-ups see one representative
+// per row and a point that lands on a shared row takes the member the reference's KdTree walk
+// meets first (kd_group_labels, a descent of the tree); exact ties between distinct rows go to
+// the walk over the whole tree.  Without shared rows this is the plain assign.
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
                km::State *dstate) {
+    CenGroups g;
+    if (k > 1 && !getenv("ST_NO_CEN_GROUPS") && cen_groups(c, d, k, cen, &g)) {
+        const uint32_t nties = nd_assign_core(c, dcols, d, n, (int)g.kr, g.cen_r, labels, dstate, false);
+        const int ld = aos_ld(d);
+        auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
+        {
+            KTimer kt(c, "kn.groups");
+            kd_group_labels(c, d, k, cen, g, aos, ld, n, labels, &dstate->err);
+        }
+        if (nties) {
+            KTimer kt(c, "kn.ties");
+            auto *caos = wsT<float>(c, "kn.caosfull", (size_t)k * ld);
+            hipLaunchKernelGGL(k_rows_aos, dim3(grid_for((uint64_t)k * ld, 256, 2048)), dim3(256), 0, c->stream, cen, d,
+                               k, caos);
+            ST_LAUNCH_CHECK();
+            kd_resolve_ties(c, d, k, cen, aos, caos, ld, wsT<uint32_t>(c, "kn.ties", n), nties, labels, true);
+        }
+        mark(c, "kn.exact");
+        return;
+    }
+    nd_assign_core(c, dcols, d, n, k, cen, labels, dstate, true);
+}
+
+namespace {
+// the exact assign against the k centroids cen; exact ties go to the KdTree walk over these
+// centroids (walk_ties) or are left listed in kn.ties for the caller: returns their count
+uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
+                        uint32_t *labels, km::State *dstate, bool walk_ties) {
     ST_REQUIRE(c->kn_n == n && c->kn_d == d, ST_ERR_ARG, "kmeans assign: point set not prepared");
     ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
     const int ks = kp_of(d) / 16;
@@ -1319,12 +1416,15 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
                 (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
     // exact ties from k_fixrow, k_fixpair and k_exact (and candidate overflows): the KdTree walk
+    if (!walk_ties) return h->ties;
     if (h->ties) {
         KTimer kt(c, "kn.ties");
         kd_resolve_ties(c, d, k, cen, aos, caos, ld, ties, h->ties, labels);
     }
     mark(c, "kn.exact");
+    return h->ties;
 }
+}  // namespace
 
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
@@ -1346,9 +1446,21 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
             const uint32_t big = sumnd_big();
             hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen,
                                big);
-            if (n > big)
-                hipLaunchKernelGGL(k_sumnd_big, dim3(std::min<unsigned>(64u, (unsigned)((k + 1023) / 1024))),
-                                   dim3(1024), 0, c->stream, aos, d, members, start, k, cen, big);
+            if (n > big) {
+                const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
+                const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
+                auto *list = wsT<uint32_t>(c, "kn.blist", cap);
+                auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
+                auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
+                auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
+                auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
+                auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
+                hipLaunchKernelGGL(k_big_list, dim3(1), dim3(1024), 0, c->stream, start, k, big, cap, list, soff, nlist);
+                hipLaunchKernelGGL(k_big_partial, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d,
+                                   members, start, list, soff, nlist, psum, pabs, pemin);
+                hipLaunchKernelGGL(k_big_final, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d,
+                                   members, start, k, list, soff, nlist, psum, pabs, pemin, cen);
+            }
             ST_LAUNCH_CHECK();
         }
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);

@@ -230,22 +230,35 @@ def test_sog_all_bands_vs_oracle(ctx, C):
         same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
 
 
-@pytest.mark.parametrize('n,d,k,zero_frac,protos', [(20_000, 45, 1024, 0.05, 0), (20_000, 45, 1024, 0.3, 0),
-                                                    (30_000, 24, 2048, 0.5, 0), (8_000, 9, 256, 0.02, 0),
-                                                    (30_000, 45, 1024, 0.4, 40)])
-def test_kmeans_duplicated_rows_vs_oracle(ctx, n, d, k, zero_frac, protos):
+@pytest.mark.parametrize('n,d,k,zero_frac,protos,mode', [(20_000, 45, 1024, 0.05, 0, ''), (20_000, 45, 1024, 0.3, 0, ''),
+                                                         (30_000, 24, 2048, 0.5, 0, ''), (8_000, 9, 256, 0.02, 0, ''),
+                                                         (30_000, 45, 1024, 0.4, 40, ''),
+                                                         (20_000, 45, 1024, 0.3, 0, 'signed_zeros'),
+                                                         (20_000, 45, 4096, 0.3, 3, 'signed_zeros'),
+                                                         (20_000, 45, 1024, 0.3, 0, 'no_groups'),
+                                                         (30_000, 45, 1024, 0.4, 40, 'no_groups')])
+def test_kmeans_duplicated_rows_vs_oracle(ctx, monkeypatch, n, d, k, zero_frac, protos, mode):
     """Many exactly duplicated points (all-zero rows): the init draws pick several of them, so
-    several centroids coincide and every duplicated point is equidistant from all of them.
-    Points with more candidates than the collect keeps go straight to the KdTree walk
-    (kd-tree.ts:39-68), as do the exact ties; equal rows walk once.  protos > 0: the duplicated
-    rows are copies of that many random rows instead of zeros.  Labels, centroids and draws
-    match the reference."""
+    several centroids coincide and every point whose nearest row is theirs is equidistant from
+    all of them.  The assign sweeps one representative per distinct centroid row and settles such
+    a point with a descent of the reference's tree (the member KdTree.findNearest meets first,
+    kd-tree.ts:39-68); exact ties between distinct rows go to the walk.  protos > 0: the
+    duplicated rows are copies of that many random rows instead of zeros; signed_zeros: the
+    duplicated rows' zeros carry random signs (-0 and +0 are one coordinate to the distance and
+    the tree); no_groups: every centroid swept (ST_NO_CEN_GROUPS), the ties walked.  Labels,
+    centroids and draws match the reference."""
     rng = np.random.default_rng(n + d + k)
     cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
     z = rng.random(n) < zero_frac
     which = rng.integers(0, max(protos, 1), n)
     for c in cols:
+        if mode == 'signed_zeros':
+            c[:protos][rng.random(protos) < 0.3] = 0.0
         c[z] = c[:protos][which[z]] if protos else 0.0
+        if mode == 'signed_zeros':
+            c[z & (c == 0) & (rng.random(n) < 0.5)] = np.float32(-0.0)
+    if mode == 'no_groups':
+        monkeypatch.setenv('ST_NO_CEN_GROUPS', '1')
     draws = oracle.mulberry32(n + k, 8 * k * 4 + 64)
     cent, labels, used = ctx.kmeans(cols, k, 3, draws)
     rc, ocent, olabels, oused = oracle.kmeans(cols, k, 3, draws)

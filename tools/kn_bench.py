@@ -39,6 +39,6 @@ t0 = time.perf_counter()
 used = ctx.dev_kmeans(cols, a.k, a.iters, draws, cen, lab)
 torch.cuda.synchronize()
 print(f'kmeans total {(time.perf_counter() - t0) * 1e3:.1f} ms ({a.iters} iters, zero-frac {a.zero_frac})')
-for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.exact', 'kn.ties', 'kn.sumnd'):
+for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.exact', 'kn.groups', 'kn.ties', 'kn.sumnd'):
     ms, cnt = ctx.kernel_stats(name)
     print(f'{name}: {ms / max(cnt, 1):.3f} ms x {cnt}')
