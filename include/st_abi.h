@@ -245,8 +245,8 @@ int st_dev_sog(st_ctx *ctx, const st_table *table, int32_t iters, const double *
 /* ---- processDataTable + writeCompressedPly in one upload (BASELINE config 3) -----
  * The reference's action list (process.ts:64-145) applied to a typed table in order:
  *   ST_ACTION_TRANSFORM     one transform() pass (translate / rotate / scale, process.ts:72-83),
- *                           params from st_transform_params_make; the transformed columns
- *                           (x y z rot_* scale_* f_rest_*) must be float32 (ST_ERR_UNSUPPORTED)
+ *                           params from st_transform_params_make; columns of any type (as
+ *                           st_transform_t)
  *   ST_ACTION_FILTER_NAN    filterNaN (process.ts:84-95)
  *   ST_ACTION_FILTER_VALUE  filterByValue (process.ts:97-109): row[column] <compare> value;
  *                           compare outside ST_CMP_LT..ST_CMP_NEQ keeps every row (:108)
@@ -290,6 +290,39 @@ int st_ply_compressed_ply(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32
 int st_ply_sog_bundle(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
                       int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size);
+
+/* ---- every column type on the writers' path ---------------------------------
+ * The reference reads its columns through getRow (data-table.ts:63-68: each element as a JS
+ * number, whatever the TypedArray) and writes through setRow (:70-76: a TypedArray store), so
+ * a PLY with double (or integer) x / y / z / rot / scale / f_rest properties transforms, orders
+ * and compresses.  These forms take typed tables (st_ttable, ST_PLY_* types):
+ *   st_transform_t / st_dev_transform_t   transform() in place (transform.ts:12-65): f64
+ *       arithmetic on the numbers, TypedArray stores (Float32 rounds, Float64 keeps, integers
+ *       take ToInt32 cut to their width); SH through the Float32Array shCoeffs (transform.ts:21)
+ *   st_morton_order_t / st_dev_morton_order_t   generateOrdering (ordering.ts:4-110) of x / y / z
+ *       of any types (keys from the JS numbers)
+ *   st_sog_process / st_sog_bundle_process   processDataTable (the actions, as st_process) then
+ *       writeSog (write-sog.ts:110-370) of a typed host table: the textures + meta (as st_sog)
+ *       or the .sog archive (as st_sog_bundle, malloc'd, st_free).  Positions, rotations and
+ *       opacity are read as numbers; cluster1d and the k-means points through Float32Arrays;
+ *       calcAverage (k-means.ts:41-63) sums the numbers.  With st_set_devices(n > 1) the
+ *       processed columns must be float32 (the sharded path moves float32 columns)
+ *   st_dev_sog_t   writeSog's device part over a typed device table
+ * st_process / st_compressed_ply / st_dev_compressed_ply / st_ply_* take every type too
+ * (transform actions, the writer's Morton order, chunk members and SH bytes). */
+int st_transform_t(st_ctx *ctx, const st_ttable *table, const st_transform_params *p);
+int st_dev_transform_t(st_ctx *ctx, const st_ttable *table, const st_transform_params *p);
+int st_morton_order_t(st_ctx *ctx, const void *const xyz[3], const int32_t types[3], uint32_t *indices, uint64_t n);
+int st_dev_morton_order_t(st_ctx *ctx, const void *const xyz[3], const int32_t types[3], uint32_t *indices,
+                          uint64_t n);
+int st_sog_process(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions, int32_t iters,
+                   const double *draws, uint64_t ndraws, uint64_t *used, st_sog_meta *meta,
+                   const st_sog_textures *out);
+int st_sog_bundle_process(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions,
+                          int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time,
+                          uint16_t dos_date, uint8_t **out, uint64_t *out_size);
+int st_dev_sog_t(st_ctx *ctx, const st_ttable *table, int32_t iters, const double *draws, uint64_t ndraws,
+                 uint64_t *used, st_sog_meta *meta, const st_sog_textures *out);
 
 /* ---- multi-GPU building blocks -----------------------------------
  * One process per GPU; rows are sharded in contiguous ranges in rank order; the

@@ -11,6 +11,7 @@
 #include <cstring>
 
 #include "st_internal.h"
+#include "st_typed.h"
 #include "st_webp.h"
 
 namespace st {
@@ -93,17 +94,14 @@ int band_coeffs(const std::vector<ChainCol> &cols) {
 }
 
 void run_actions(Chain &ch, const st_action *actions, int nactions) {
-    static const char *tcols[] = {"x", "y", "z", "rot_0", "rot_1", "rot_2", "rot_3", "scale_0", "scale_1", "scale_2"};
     const int in_coeffs = band_coeffs(ch.cols);  // filterBands reads the ORIGINAL table (process.ts:111)
     for (int a = 0; a < nactions; ++a) {
         const st_action &act = actions[a];
         switch (act.kind) {
-            case ST_ACTION_TRANSFORM: {
-                for (auto *nm : tcols) ch.require_f32(nm, "transform");
-                for (int i = 0; i < 45; ++i) ch.require_f32("f_rest_" + std::to_string(i), "transform");
-                transform_dev(ch.c, ch.f32(), &act.transform);
+            case ST_ACTION_TRANSFORM:
+                // every column type, as getRow / setRow (transform.ts:24-63)
+                transform_tdev(ch.c, ch.typed(), &act.transform);
                 break;
-            }
             case ST_ACTION_FILTER_NAN:
             case ST_ACTION_FILTER_VALUE: {
                 if (ch.n == 0) break;
@@ -144,19 +142,48 @@ void run_actions(Chain &ch, const st_action *actions, int nactions) {
 
 // writeCompressedPly's device part on the processed table: Morton order of the identity
 // (write-compressed-ply.ts:59-64), then the chunk loop
+// (any column types: the chunk members go through CompressedChunk's Float32Arrays
+// (compressed-chunk.ts:28-41), the ordering and the SH bytes read the row's JS numbers
+// (ordering.ts:32-47, write-compressed-ply.ts:85))
+const char *const SH_NAMES[45] = {
+    "f_rest_0",  "f_rest_1",  "f_rest_2",  "f_rest_3",  "f_rest_4",  "f_rest_5",  "f_rest_6",  "f_rest_7",  "f_rest_8",
+    "f_rest_9",  "f_rest_10", "f_rest_11", "f_rest_12", "f_rest_13", "f_rest_14", "f_rest_15", "f_rest_16", "f_rest_17",
+    "f_rest_18", "f_rest_19", "f_rest_20", "f_rest_21", "f_rest_22", "f_rest_23", "f_rest_24", "f_rest_25", "f_rest_26",
+    "f_rest_27", "f_rest_28", "f_rest_29", "f_rest_30", "f_rest_31", "f_rest_32", "f_rest_33", "f_rest_34", "f_rest_35",
+    "f_rest_36", "f_rest_37", "f_rest_38", "f_rest_39", "f_rest_40", "f_rest_41", "f_rest_42", "f_rest_43", "f_rest_44"};
+
 void compressed_tail(Chain &ch, float *chunk, uint32_t *vertex, uint8_t *sh, int32_t *out_coeffs) {
     static const char *pcols[] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
                                   "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
-    for (auto *nm : pcols) ch.require_f32(nm, "writeCompressedPly");
     const int C = band_coeffs(ch.cols);
-    for (int i = 0; i < 3 * C; ++i) ch.require_f32("f_rest_" + std::to_string(i), "writeCompressedPly");
     *out_coeffs = C;
     if (ch.n == 0) return;
-    const st_table *t = ch.f32();
+    const st_ttable *tt = ch.typed();
+    std::vector<const char *> fn;
+    std::vector<float *> fp;
+    TCol xyz[3];
+    for (int i = 0; i < 14; ++i) {
+        const TCol col = tcol_or_null(tt, pcols[i]);
+        ST_REQUIRE(col.p, ST_ERR_ARG, std::string("pack_compressed: missing column ") + pcols[i]);
+        if (i < 3) xyz[i] = col;
+        fn.push_back(pcols[i]);
+        fp.push_back(const_cast<float *>(as_f32_dev(ch.c, col, ch.n, ch.tag + ".m32." + std::to_string(i))));
+    }
+    bool sh32 = true;
+    std::vector<const double *> sh64;
+    for (int i = 0; i < 3 * C; ++i) sh32 = sh32 && tcol_or_null(tt, SH_NAMES[i]).t == ST_PLY_FLOAT;
+    for (int i = 0; i < 3 * C; ++i) {
+        const TCol col = tcol_or_null(tt, SH_NAMES[i]);
+        if (sh32) fn.push_back(SH_NAMES[i]), fp.push_back(static_cast<float *>(col.p));
+        else sh64.push_back(as_f64_dev(ch.c, col, ch.n, ch.tag + ".sh64." + std::to_string(i)));
+    }
+    const st_table t{ch.n, (int32_t)fp.size(), fn.data(), fp.data()};
     auto *order = wsT<uint32_t>(ch.c, "chain.order", ch.n);
     iota_u32(ch.c, order, ch.n);
-    morton_order_dev(ch.c, col_or_null(t, "x"), col_or_null(t, "y"), col_or_null(t, "z"), order, ch.n);
-    pack_compressed_dev(ch.c, t, order, chunk, vertex, sh);
+    const void *xp[3] = {xyz[0].p, xyz[1].p, xyz[2].p};
+    const int32_t xt[3] = {xyz[0].t, xyz[1].t, xyz[2].t};
+    morton_order_tdev(ch.c, xp, xt, order, ch.n);
+    pack_compressed_dev(ch.c, &t, order, chunk, vertex, sh, sh32 ? nullptr : sh64.data(), C);
 }
 
 void check_src(const st_ttable *src) {
@@ -198,13 +225,118 @@ void ply_chain(st_ctx *c, int fd, const st_ply_header *h, int element, Chain &ch
     ply_read_dev(c, fd, *h, element, cols.data());
 }
 
-// the processed table as writeSog reads it: float32 columns by name (write-sog.ts:110-370)
+// the processed table as the multi-GPU writeSog takes it: float32 columns by name (the sharded
+// path moves float32 columns only; a single device takes every type through sog_tdev)
 const st_table *sog_view(Chain &ch) {
     static const char *scols[] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0", "f_dc_1", "f_dc_2",
                                   "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
-    for (auto *nm : scols) ch.require_f32(nm, "writeSog");
-    for (int i = 0; i < 45; ++i) ch.require_f32("f_rest_" + std::to_string(i), "writeSog");
+    for (auto *nm : scols) ch.require_f32(nm, "multi-GPU writeSog");
+    for (int i = 0; i < 45; ++i) ch.require_f32("f_rest_" + std::to_string(i), "multi-GPU writeSog");
     return ch.f32();
+}
+
+// device textures of writeSog for n rows of band C (workspace slots h.s.*)
+st_sog_textures sog_textures(st_ctx *c, uint64_t n, int C, uint64_t *tex_bytes, uint64_t *cen_bytes) {
+    int32_t W, H, pal, cw, chh;
+    ST_REQUIRE(st_sog_geometry(n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
+    const uint64_t tex = (uint64_t)W * H * 4;
+    st_sog_textures dt{};
+    dt.means_l = wsT<uint8_t>(c, "h.s.ml", tex);
+    dt.means_u = wsT<uint8_t>(c, "h.s.mu", tex);
+    dt.quats = wsT<uint8_t>(c, "h.s.q", tex);
+    dt.scales = wsT<uint8_t>(c, "h.s.sc", tex);
+    dt.sh0 = wsT<uint8_t>(c, "h.s.sh0", tex);
+    if (C) {
+        dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
+        dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
+    }
+    *tex_bytes = tex;
+    *cen_bytes = (uint64_t)cw * chh * 4;
+    return dt;
+}
+
+
+
+#define ST_REQUIRE_RC(cond, msg)           \
+    do {                                   \
+        if (!(cond)) {                     \
+            set_last_error(msg);           \
+            return ST_ERR_ARG;             \
+        }                                  \
+    } while (0)
+
+// processDataTable + writeSog on a table the loader puts in the chain: the .sog archive
+// (out / out_size) or the textures and meta on the host (tex_meta / tex_out).  One device takes
+// every column type (sog_tdev); with the st_set_devices group the processed float32 columns are
+// sharded over it from the host.
+template <typename Load>
+int sog_chain(st_ctx *c, Load load, const st_action *actions, int32_t nactions, int32_t iters, const double *draws,
+              uint64_t ndraws, uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out,
+              uint64_t *out_size, st_sog_meta *tex_meta, const st_sog_textures *tex_out) {
+    if (int rc = apply_env_devices()) return rc;
+    const auto group = default_group();  // held for the whole call
+    std::vector<std::vector<float>> host;  // multi-GPU: the processed columns, sharded from the host
+    std::vector<float *> hcols;
+    std::vector<std::string> hnames;
+    std::vector<const char *> hcn;
+    st_table ht{};
+    int rc = guard([&] {
+        ST_REQUIRE(c && ((out && out_size) || (tex_meta && tex_out)), ST_ERR_ARG, "NULL argument");
+        ST_REQUIRE(actions || nactions == 0, ST_ERR_ARG, "NULL argument");
+        use_device(c);
+        Chain ch{c};
+        load(ch);
+        run_actions(ch, actions, nactions);
+        if (group) {
+            const st_table *t = sog_view(ch);
+            std::vector<HostXfer> down;
+            for (int i = 0; i < t->ncol; ++i) {
+                host.emplace_back(t->n);
+                hnames.push_back(t->names[i]);
+                down.push_back(HostXfer{host.back().data(), t->cols[i], t->n * 4});
+            }
+            staged_d2h(c, down);
+            for (size_t i = 0; i < host.size(); ++i) hcols.push_back(host[i].data()), hcn.push_back(hnames[i].c_str());
+            ht = st_table{t->n, t->ncol, hcn.data(), hcols.data()};
+            return;
+        }
+        const int C = band_coeffs(ch.cols);
+        uint64_t tex, cbytes;
+        const st_sog_textures dt = sog_textures(c, ch.n, C, &tex, &cbytes);
+        st_sog_meta meta{};
+        const uint64_t u = sog_tdev(c, ch.typed(), iters, draws, ndraws, &meta, &dt);
+        if (tex_out) {
+            std::vector<HostXfer> down;
+            for (auto pr : {std::make_pair(tex_out->means_l, dt.means_l), std::make_pair(tex_out->means_u, dt.means_u),
+                            std::make_pair(tex_out->quats, dt.quats), std::make_pair(tex_out->scales, dt.scales),
+                            std::make_pair(tex_out->sh0, dt.sh0)}) {
+                ST_REQUIRE(pr.first, ST_ERR_ARG, "sog: texture output is NULL");
+                down.push_back(HostXfer{pr.first, pr.second, tex});
+            }
+            if (C) {
+                ST_REQUIRE(tex_out->shn_labels && tex_out->shn_centroids, ST_ERR_ARG, "sog: shN outputs are NULL");
+                down.push_back(HostXfer{tex_out->shn_labels, dt.shn_labels, tex});
+                down.push_back(HostXfer{tex_out->shn_centroids, dt.shn_centroids, cbytes});
+            }
+            staged_d2h(c, down);
+            *tex_meta = meta;
+        } else {
+            const uint8_t *view;
+            uint64_t nb;
+            sog_bundle_dev(c, meta, ch.n, dt, dos_time, dos_date, &view, &nb);
+            uint8_t *buf = (uint8_t *)std::malloc(nb);
+            ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
+            std::memcpy(buf, view, nb);
+            *out = buf;
+            *out_size = nb;
+        }
+        if (used) *used = u;
+    });
+    if (rc != ST_OK || !ht.ncol) return rc;
+    const st_table *tp = &ht;
+    if (tex_out) return st_group_sog(group.get(), &tp, 1, nullptr, iters, draws, ndraws, used, tex_meta, tex_out);
+    return st_group_sog_bundle(group.get(), &tp, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out,
+                               out_size);
 }
 
 }  // namespace
@@ -337,62 +469,48 @@ int st_ply_compressed_ply(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t
 int st_ply_sog_bundle(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
                       int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size) {
-    if (int rc = apply_env_devices()) return rc;
-    const auto group = default_group();  // held for the whole call
-    std::vector<std::vector<float>> host;  // multi-GPU: the processed columns, sharded from the host
-    std::vector<float *> hcols;
-    std::vector<std::string> hnames;
-    std::vector<const char *> hcn;
-    st_table ht{};
-    int rc = guard([&] {
-        ST_REQUIRE(c && h && fd >= 0 && out && out_size && (actions || nactions == 0), ST_ERR_ARG, "NULL argument");
+    return sog_chain(
+        c, [&](Chain &ch) {
+            ST_REQUIRE(c && h && fd >= 0, ST_ERR_ARG, "NULL argument");
+            ply_chain(c, fd, h, element, ch);
+        },
+        actions, nactions, iters, draws, ndraws, used, dos_time, dos_date, out, out_size, nullptr, nullptr);
+}
+
+int st_sog_bundle_process(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions, int32_t iters,
+                          const double *draws, uint64_t ndraws, uint64_t *used, uint16_t dos_time, uint16_t dos_date,
+                          uint8_t **out, uint64_t *out_size) {
+    return sog_chain(
+        c, [&](Chain &ch) {
+            ST_REQUIRE(c && src, ST_ERR_ARG, "NULL argument");
+            check_src(src);
+            upload_chain(c, src, ch);
+        },
+        actions, nactions, iters, draws, ndraws, used, dos_time, dos_date, out, out_size, nullptr, nullptr);
+}
+
+int st_sog_process(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions, int32_t iters,
+                   const double *draws, uint64_t ndraws, uint64_t *used, st_sog_meta *meta,
+                   const st_sog_textures *out) {
+    ST_REQUIRE_RC(meta && out, "NULL argument");
+    return sog_chain(
+        c, [&](Chain &ch) {
+            ST_REQUIRE(c && src, ST_ERR_ARG, "NULL argument");
+            check_src(src);
+            upload_chain(c, src, ch);
+        },
+        actions, nactions, iters, draws, ndraws, used, 0, 0, nullptr, nullptr, meta, out);
+}
+
+int st_dev_sog_t(st_ctx *c, const st_ttable *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                 st_sog_meta *meta, const st_sog_textures *out) {
+    return guard([&] {
+        ST_REQUIRE(c && t && meta && out, ST_ERR_ARG, "NULL argument");
+        check_src(t);
         use_device(c);
-        Chain ch{c};
-        ply_chain(c, fd, h, element, ch);
-        run_actions(ch, actions, nactions);
-        const st_table *t = sog_view(ch);
-        if (group) {
-            std::vector<HostXfer> down;
-            for (int i = 0; i < t->ncol; ++i) {
-                host.emplace_back(t->n);
-                hnames.push_back(t->names[i]);
-                down.push_back(HostXfer{host.back().data(), t->cols[i], t->n * 4});
-            }
-            staged_d2h(c, down);
-            for (size_t i = 0; i < host.size(); ++i) hcols.push_back(host[i].data()), hcn.push_back(hnames[i].c_str());
-            ht = st_table{t->n, t->ncol, hcn.data(), hcols.data()};
-            return;
-        }
-        const int C = sh_coeffs_of(t);
-        int32_t W, H, pal, cw, chh;
-        ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
-        const uint64_t tex = (uint64_t)W * H * 4;
-        st_sog_textures dt{};
-        dt.means_l = wsT<uint8_t>(c, "h.s.ml", tex);
-        dt.means_u = wsT<uint8_t>(c, "h.s.mu", tex);
-        dt.quats = wsT<uint8_t>(c, "h.s.q", tex);
-        dt.scales = wsT<uint8_t>(c, "h.s.sc", tex);
-        dt.sh0 = wsT<uint8_t>(c, "h.s.sh0", tex);
-        if (C) {
-            dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
-            dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
-        }
-        st_sog_meta meta{};
-        const uint64_t u = sog_dev(c, t, iters, draws, ndraws, &meta, &dt);
-        const uint8_t *view;
-        uint64_t nb;
-        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, &view, &nb);
-        uint8_t *buf = (uint8_t *)std::malloc(nb);
-        ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
-        std::memcpy(buf, view, nb);
-        *out = buf;
-        *out_size = nb;
+        const uint64_t u = sog_tdev(c, t, iters, draws, ndraws, meta, out);
         if (used) *used = u;
     });
-    if (rc != ST_OK || !ht.ncol) return rc;
-    const st_table *tp = &ht;
-    return st_group_sog_bundle(group.get(), &tp, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, out,
-                               out_size);
 }
 
 }  // extern "C"

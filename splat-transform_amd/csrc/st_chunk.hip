@@ -169,6 +169,34 @@ __global__ __launch_bounds__(256) void k_sh_rows(const TransposeArgs a, int nsh,
     for (uint64_t e = t; e < nrows * SHB / 16; e += 256) dst[e] = s4[e];
 }
 
+// the same from float64 values (the JS numbers of SH columns of another type than float32:
+// write-compressed-ply.ts:85 divides the row's number itself)
+struct ShRowsD {
+    const double *src[45];
+    uint64_t n;
+};
+__global__ __launch_bounds__(256) void k_sh_rows_d(const ShRowsD a, int nsh, uint8_t *__restrict__ shrows) {
+    __shared__ uint32_t stage[256 * SHB / 4];
+    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t t = threadIdx.x;
+    uint8_t *st8 = reinterpret_cast<uint8_t *>(stage);
+    const bool real = r0 + t < a.n;
+    const uint64_t rsafe = real ? r0 + t : a.n - 1;
+    for (int k = 0; k < SHB; ++k) {
+        uint8_t b = 0;
+        if (k < nsh && real) {
+            const double nv = a.src[k][rsafe] / 8 + 0.5;
+            b = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
+        }
+        st8[t * SHB + k] = b;
+    }
+    __syncthreads();
+    const uint64_t nrows = (a.n - r0 < 256) ? (a.n - r0) : 256;
+    uint4 *dst = reinterpret_cast<uint4 *>(shrows + r0 * SHB);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
+    for (uint64_t e = t; e < nrows * SHB / 16; e += 256) dst[e] = s4[e];
+}
+
 struct ChunkArgs {
     const float *rows;  // AoS rows of RL = 16 floats: x y z scale_0..2 f_dc_0..2 opacity rot_0..3
     const uint8_t *shrows;  // SH bytes, SHB per row (k_sh_rows)
@@ -264,7 +292,7 @@ __global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
 }  // namespace
 
 void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
-                         uint8_t *sh) {
+                         uint8_t *sh, const double *const *sh64, int sh_coeffs) {
     const uint64_t n = t->n;
     if (n == 0) return;
     static const char *members[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
@@ -274,13 +302,13 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
         ta.src[i] = col_or_null(t, members[i]);
         ST_REQUIRE(ta.src[i], ST_ERR_ARG, std::string("pack_compressed: missing column ") + members[i]);
     }
-    const int C = sh_coeffs_of(t);
+    const int C = sh64 ? sh_coeffs : sh_coeffs_of(t);
     const int nsh = 3 * C;
     if (nsh) ST_REQUIRE(sh, ST_ERR_ARG, "pack_compressed: sh output is NULL");
     char nm[32];
     for (int i = 0; i < nsh; ++i) {
         snprintf(nm, sizeof nm, "f_rest_%d", i);
-        ta.src[14 + i] = col_or_null(t, nm);
+        ta.src[14 + i] = sh64 ? nullptr : col_or_null(t, nm);
     }
     ta.ncol = 14;
     ta.rl = 16;
@@ -300,7 +328,14 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
     const uint64_t nchunks = (n + 255) / 256;
     KTimer kt(c, "chunk.pack");
     hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + RA_ROWS - 1) / RA_ROWS)), dim3(256), 0, c->stream, ta);
-    if (nsh) hipLaunchKernelGGL(k_sh_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, ta, nsh, shrows);
+    if (nsh && sh64) {
+        ShRowsD sd{};
+        for (int i = 0; i < nsh; ++i) sd.src[i] = sh64[i];
+        sd.n = n;
+        hipLaunchKernelGGL(k_sh_rows_d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, sd, nsh, shrows);
+    } else if (nsh) {
+        hipLaunchKernelGGL(k_sh_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, ta, nsh, shrows);
+    }
     hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();
 }

@@ -123,6 +123,64 @@ int st_transform(st_ctx *c, const st_table *t, const st_transform_params *p) {
     });
 }
 
+// transform() on a typed host table, in place: the transformed columns (x y z rot_* scale_*
+// f_rest_*, any type) go up, through the typed kernel, and back
+int st_transform_t(st_ctx *c, const st_ttable *t, const st_transform_params *p) {
+    return guarded_h([&] {
+        ST_ARGH(c && t && p && (t->ncol == 0 || (t->names && t->types && t->cols)), "NULL argument");
+        use_device(c);
+        const auto want = transform_columns();
+        std::vector<const char *> names;
+        std::vector<int32_t> types;
+        std::vector<void *> dcols;
+        std::vector<int> src;
+        Batch b{c};
+        for (int i = 0; i < t->ncol; ++i) {
+            bool hit = false;
+            for (auto &w : want) hit = hit || (w == t->names[i]);
+            if (!hit) continue;
+            const int sz = type_size(t->types[i]);
+            ST_ARGH(sz > 0 && (t->cols[i] || t->n == 0), "transform: bad column");
+            void *d = ws(c, "h.tt" + std::to_string(i), t->n * sz + 16);
+            b.add(static_cast<const char *>(t->cols[i]), static_cast<char *>(d), t->n * sz);
+            names.push_back(t->names[i]);
+            types.push_back(t->types[i]);
+            dcols.push_back(d);
+            src.push_back(i);
+        }
+        b.h2d();
+        const st_ttable d{t->n, (int32_t)names.size(), names.data(), types.data(), dcols.data()};
+        transform_tdev(c, &d, p);
+        for (size_t j = 0; j < src.size(); ++j)
+            b.add_d2h(static_cast<char *>(t->cols[src[j]]), static_cast<const char *>(dcols[j]),
+                      t->n * type_size(types[j]));
+        b.d2h();
+    });
+}
+
+// generateOrdering of x / y / z columns of any types (ST_PLY_*)
+int st_morton_order_t(st_ctx *c, const void *const xyz[3], const int32_t types[3], uint32_t *idx, uint64_t n) {
+    return guarded_h([&] {
+        ST_ARGH(c && xyz && types && ((xyz[0] && xyz[1] && xyz[2] && idx) || n == 0), "NULL argument");
+        if (n == 0) return;
+        use_device(c);
+        Batch b{c};
+        const void *d[3];
+        for (int a = 0; a < 3; ++a) {
+            const int sz = type_size(types[a]);
+            ST_ARGH(sz > 0, "morton: bad column type");
+            char *p = static_cast<char *>(ws(c, "h.mt" + std::to_string(a), n * sz + 16));
+            b.add(static_cast<const char *>(xyz[a]), p, n * sz);
+            d[a] = p;
+        }
+        uint32_t *di = to_dev(b, "h.mi", idx, n);
+        b.h2d();
+        morton_order_tdev(c, d, types, di, n);
+        b.add_d2h(idx, di, n);
+        b.d2h();
+    });
+}
+
 int st_filter_finite(st_ctx *c, const st_table *t, uint32_t *out_idx, uint64_t *out_n) {
     return guarded_h([&] {
         ST_ARGH(c && t && out_idx && out_n, "NULL argument");

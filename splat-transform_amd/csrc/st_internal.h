@@ -229,8 +229,16 @@ void permute_rows_tdev(st_ctx *c, const st_ttable *src, const uint32_t *idx, uin
 int combine_layout(const st_ttable *const *srcs, int nsrc, int32_t *col_table, int32_t *col_index);
 void combine_tdev(st_ctx *c, const st_ttable *const *srcs, int nsrc, const st_ttable *dst);
 void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *indices, uint64_t n);
+void morton_order_dev_f64(st_ctx *c, const double *x, const double *y, const double *z, uint32_t *indices,
+                          uint64_t n);
+// x / y / z of any column types (ST_PLY_*): float64 keys when any is not float32 (st_morton.hip)
+void morton_order_tdev(st_ctx *c, const void *const xyz[3], const int32_t types[3], uint32_t *indices, uint64_t n);
+// transform() over a typed table in place (st_transform.hip)
+void transform_tdev(st_ctx *c, const st_ttable *t, const st_transform_params *p);
+// (sh64: the 3 sh_coeffs SH columns' JS numbers as float64 when they are not all float32; the
+// SH bytes are computed from those and t's f_rest columns are not read)
 void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, float *chunk, uint32_t *vertex,
-                         uint8_t *sh);
+                         uint8_t *sh, const double *const *sh64 = nullptr, int sh_coeffs = 0);
 // returns draws consumed
 // initializeCentroids over a table of n rows: rows (device) = the k distinct floor(draw * n) in
 // draw order, *used = draws consumed (device window with the host loop as fallback)
@@ -240,12 +248,19 @@ void kmeans_init_rows(st_ctx *c, const double *draws, uint64_t ndraws, uint64_t 
 void gather_owned_rows(st_ctx *c, const float *const *cols, int d, uint64_t n_local, uint64_t offset,
                        const uint32_t *rows, int k, float *out);
 // (host_init: initializeCentroids by the host's loop instead of on the device)
+// (sum64: float64 columns (host array of device pointers) summed by calcAverage instead of cols:
+// the JS numbers of columns that are not float32, D > 1)
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
-                    uint64_t ndraws, float *centroids, uint32_t *labels, bool host_init = false);
+                    uint64_t ndraws, float *centroids, uint32_t *labels, bool host_init = false,
+                    const double *const *sum64 = nullptr);
 uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, int iters, const double *draws,
                        uint64_t ndraws, float *centroids256, uint8_t *labels);
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
                  const st_sog_textures *out);
+// writeSog's device part over a table of any column types (write-sog.ts reads the members as JS
+// numbers, cluster1d and the k-means points through Float32Arrays): float32 tables take sog_dev
+uint64_t sog_tdev(st_ctx *c, const st_ttable *t, int iters, const double *draws, uint64_t ndraws,
+                  st_sog_meta *meta, const st_sog_textures *out);
 void codebook_dev(st_ctx *c, const float *cen, const uint32_t *lab, uint64_t total, float *centroids256,
                   uint8_t *labels);
 void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const double lo[3], const double hi[3],

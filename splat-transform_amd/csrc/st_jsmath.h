@@ -44,6 +44,15 @@ __host__ __device__ inline uint8_t to_uint8(double v) { return (uint8_t)(to_uint
 // Math.min / Math.max with a NaN operand return V8's NaN: the x86-64 default NaN, sign bit set
 // (0xffc00000 once stored to a Float32Array; reference fixture process_chain)
 __host__ __device__ inline double nan_() { return mkd(0xfff80000u, 0u); }
+// V8 on x86-64: an invalid operation (Inf - Inf, 0 * Inf, 0 / 0, log of a negative) on operands
+// that are not NaN yields the default NaN with the sign bit set (0xFFF8000000000000, 0xFFC00000
+// once stored to a Float32Array); the GPU's default NaN is positive.  A NaN operand propagates on
+// both.  r: an expression's result, nan_in: whether any of its operands was NaN.
+__host__ __device__ inline double x86_nan(double r, bool nan_in) { return (r != r && !nan_in) ? nan_() : r; }
+__host__ __device__ inline float x86_nanf(float r, bool nan_in) {
+    return (r != r && !nan_in) ? __builtin_bit_cast(float, 0xffc00000u) : r;
+}
+
 __host__ __device__ inline double min_(double a, double b) {
     if (isnan_(a) || isnan_(b)) return nan_();
     if (a == 0 && b == 0) return signbit_(a) ? a : b;

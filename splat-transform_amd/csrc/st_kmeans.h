@@ -34,6 +34,10 @@ __device__ inline int ulp_exp(float x) {
     const uint32_t e = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;
     return e == 0 ? -149 : (int)e - 150;
 }
+__device__ inline int ulp_exp(double x) {
+    const uint32_t e = (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 52) & 0x7ffu;
+    return e == 0 ? -1074 : (int)e - 1075;
+}
 // certificate that every partial sum of a set of f32 values is exact in f64: all are
 // multiples of 2^emin and |partial sums| <= sum|x| < 2^(emin + 53) (slack for sum|x|'s own rounding)
 __host__ __device__ inline bool sum_is_exact(double sabs, int emin) {
@@ -55,8 +59,11 @@ void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t 
 
 void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint64_t n, int k, int iters,
                    const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
+// (sum64: host array of device float64 columns whose values calcAverage sums instead of the
+// float32 points -- the JS numbers of columns that are not float32)
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
-                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels);
+                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels,
+                   const double *const *sum64 = nullptr);
 
 // step form of the loops (shared with the distributed step API, st_dist.hip)
 void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n);  // workspace: kn.pfrag/kn.pnorm/kn.aos

@@ -396,7 +396,7 @@ void gather_owned_rows(st_ctx *c, const float *const *cols, int d, uint64_t n_lo
 }
 
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
-                    uint64_t ndraws, float *cen, uint32_t *labels, bool host_init) {
+                    uint64_t ndraws, float *cen, uint32_t *labels, bool host_init, const double *const *sum64) {
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "kmeans: n must be < 2^31 per device");
     if (n < (uint64_t)k) {  // k-means.ts:139-144
         for (int j = 0; j < d; ++j)
@@ -456,12 +456,12 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     if (d == 1)
         kmeans1d_loop(c, cols[0], dcols, n, k, iters, ddraws, ndraws, dstate, cen, labels);
     else
-        kmeansnd_loop(c, cols, dcols, d, n, k, iters, ddraws, ndraws, dstate, cen, labels);
+        kmeansnd_loop(c, cols, dcols, d, n, k, iters, ddraws, ndraws, dstate, cen, labels, sum64);
 
     ST_HIP(hipMemcpyAsync(&hs, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     if (hs.err & ERR_INIT_WINDOW)  // the device window held fewer than k distinct rows
-        return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, true);
+        return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, true, sum64);
     ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
     ST_REQUIRE(!(hs.err & ERR_DRAW_RANGE), ST_ERR_ARG, "kmeans: a re-seed draw outside [0, 1)");
     ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");

@@ -992,7 +992,10 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
 
 // calcAverage (k-means.ts:41-63): one wave per cluster, lane = dimension,
 // f64 running sum over the members in ascending point order
-__global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, int d,
+// (T = double: the members' JS numbers when the SH columns are not float32 -- calcAverage sums
+// the row's numbers, k-means.ts:49-55, while the assign sees Float32Array points)
+template <typename T>
+__global__ __launch_bounds__(256) void k_sumnd(const T *__restrict__ aos, int d,
                                                const uint32_t *__restrict__ members,
                                                const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
                                                uint32_t big) {
@@ -1007,7 +1010,7 @@ __global__ __launch_bounds__(256) void k_sumnd(const float *__restrict__ aos, in
     // 32 member rows in flight per wave (the adds stay in ascending point order)
     constexpr int U = 32;
     for (; j + U <= s1; j += U) {
-        float v[U];
+        T v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
 #pragma unroll
@@ -1050,7 +1053,8 @@ __global__ __launch_bounds__(1024) void k_big_list(const uint32_t *__restrict__ 
 }
 
 // slice s of the listed clusters: 4 waves, lane = dimension; (sum, sum|x|, min ulp exponent)
-__global__ __launch_bounds__(256) void k_big_partial(const float *__restrict__ aos, int d,
+template <typename T>
+__global__ __launch_bounds__(256) void k_big_partial(const T *__restrict__ aos, int d,
                                                      const uint32_t *__restrict__ members,
                                                      const uint32_t *__restrict__ start,
                                                      const uint32_t *__restrict__ list,
@@ -1076,16 +1080,16 @@ __global__ __launch_bounds__(256) void k_big_partial(const float *__restrict__ a
         const uint32_t a = s0 + min(s1 - s0, w * per), b = s0 + min(s1 - s0, (w + 1) * per);
         double sum = 0, sabs = 0;
         int emin = 0x7fffffff;
-        auto take = [&](float x) {
+        auto take = [&](T x) {
             sum += (double)x;
             sabs += __builtin_fabs((double)x);
-            if (x != 0.0f) emin = min(emin, ulp_exp(x));
+            if (x != 0) emin = min(emin, ulp_exp(x));
         };
         if (lane < d) {
             constexpr int U = 32;  // member rows in flight, as k_sumnd
             uint32_t j = a;
             for (; j + U <= b; j += U) {
-                float v[U];
+                T v[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
 #pragma unroll
@@ -1108,7 +1112,8 @@ __global__ __launch_bounds__(256) void k_big_partial(const float *__restrict__ a
 
 // one wave per listed cluster, lane = dimension: the slices' sums under the certificate, else
 // the sequential chain (k-means.ts:41-63)
-__global__ __launch_bounds__(64) void k_big_final(const float *__restrict__ aos, int d,
+template <typename T>
+__global__ __launch_bounds__(64) void k_big_final(const T *__restrict__ aos, int d,
                                                   const uint32_t *__restrict__ members,
                                                   const uint32_t *__restrict__ start, int k,
                                                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ soff,
@@ -1133,7 +1138,7 @@ __global__ __launch_bounds__(64) void k_big_final(const float *__restrict__ aos,
             constexpr int U = 32;
             uint32_t j = s0;
             for (; j + U <= s1; j += U) {
-                float v[U];
+                T v[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
 #pragma unroll
@@ -1143,6 +1148,39 @@ __global__ __launch_bounds__(64) void k_big_final(const float *__restrict__ aos,
         }
         cen[(uint64_t)lane * k + cl] = (float)(S / (double)m);
     }
+}
+
+// the float64 member rows (row stride aos_ld(d), zero padded) for the sums of k_sumnd<double>
+__global__ __launch_bounds__(256) void k_aos64(const double *const *cols, int d, uint64_t n, double *__restrict__ aos) {
+    const int ld = aos_ld(d);
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n * ld; f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = f / ld;
+        const int a = (int)(f % ld);
+        aos[f] = a < d ? cols[a][r] : 0.0;
+    }
+}
+
+template <typename T>
+void launch_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32_t *members, const uint32_t *start,
+                 float *cen) {
+    const uint32_t big = sumnd_big();
+    hipLaunchKernelGGL(k_sumnd<T>, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen, big);
+    if (n > big) {
+        const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
+        const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
+        auto *list = wsT<uint32_t>(c, "kn.blist", cap);
+        auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
+        auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
+        auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
+        auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
+        auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
+        hipLaunchKernelGGL(k_big_list, dim3(1), dim3(1024), 0, c->stream, start, k, big, cap, list, soff, nlist);
+        hipLaunchKernelGGL(k_big_partial<T>, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d, members,
+                           start, list, soff, nlist, psum, pabs, pemin);
+        hipLaunchKernelGGL(k_big_final<T>, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d,
+                           members, start, k, list, soff, nlist, psum, pabs, pemin, cen);
+    }
+    ST_LAUNCH_CHECK();
 }
 
 template <int KS>
@@ -1427,9 +1465,19 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
 }  // namespace
 
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
-                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels) {
+                   int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels,
+                   const double *const *sum64) {
     (void)cols;
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
+    double *aos64 = nullptr;
+    if (sum64) {  // the members' float64 numbers for the sums
+        aos64 = wsT<double>(c, "kn.aos64", n * (size_t)aos_ld(d));
+        auto **d64 = wsT<const double *>(c, "kn.cols64", (size_t)d);
+        ST_HIP(hipMemcpyAsync(d64, sum64, sizeof(double *) * d, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_aos64, dim3(grid_for(n * aos_ld(d), 256, 8192)), dim3(256), 0, c->stream, d64, d, n,
+                           aos64);
+        ST_LAUNCH_CHECK();
+    }
     auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
     auto *members = wsT<uint32_t>(c, "kn.members", n);
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
@@ -1443,25 +1491,8 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         member_sort(c, labels, n, k, sorted_labels, members, start);
         {
             KTimer kt(c, "kn.sumnd");
-            const uint32_t big = sumnd_big();
-            hipLaunchKernelGGL(k_sumnd, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen,
-                               big);
-            if (n > big) {
-                const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
-                const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
-                auto *list = wsT<uint32_t>(c, "kn.blist", cap);
-                auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
-                auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
-                auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
-                auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
-                auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
-                hipLaunchKernelGGL(k_big_list, dim3(1), dim3(1024), 0, c->stream, start, k, big, cap, list, soff, nlist);
-                hipLaunchKernelGGL(k_big_partial, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d,
-                                   members, start, list, soff, nlist, psum, pabs, pemin);
-                hipLaunchKernelGGL(k_big_final, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d,
-                                   members, start, k, list, soff, nlist, psum, pabs, pemin, cen);
-            }
-            ST_LAUNCH_CHECK();
+            if (aos64) launch_sums<double>(c, aos64, d, n, k, members, start, cen);
+            else launch_sums<float>(c, aos, d, n, k, members, start, cen);
         }
         reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "kn.update");

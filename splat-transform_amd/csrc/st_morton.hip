@@ -18,6 +18,7 @@
 // extents stop a segment exactly where ordering.ts:53-61 returns.
 #include "st_internal.h"
 #include "st_jsmath.h"
+#include "st_typed.h"
 
 namespace st {
 namespace {
@@ -40,6 +41,32 @@ __device__ inline float fkey_inv(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return __builtin_bit_cast(float, u);
 }
+
+// coordinate traits: float32 columns (the splat table) or float64 ones (the JS numbers of any
+// other column type): extents as order-preserving integer keys of the coordinate's width
+template <typename T>
+struct MC;
+template <>
+struct MC<float> {
+    using K = uint32_t;
+    using V = float4;
+    static constexpr K KMAX = 0xffffffffu;
+    __device__ static K key(float f) { return fkey(f); }
+    __device__ static double inv(K k) { return (double)fkey_inv(k); }
+    __device__ static V pack(float a, float b, float c) { return make_float4(a, b, c, 0.0f); }
+};
+template <>
+struct MC<double> {
+    using K = unsigned long long;
+    using V = double4;
+    static constexpr K KMAX = ~0ull;
+    __device__ static K key(double d) {
+        const K u = __builtin_bit_cast(K, d);
+        return (u >> 63) ? ~u : (u | (1ull << 63));
+    }
+    __device__ static double inv(K k) { return __builtin_bit_cast(double, (k >> 63) ? (k & ~(1ull << 63)) : ~k); }
+    __device__ static V pack(double a, double b, double c) { return make_double4(a, b, c, 0.0); }
+};
 
 struct SegInfo {
     double mn[3];
@@ -64,26 +91,29 @@ __global__ __launch_bounds__(256) void k_expand(const uint32_t *__restrict__ seg
     }
 }
 
-__global__ void k_ext_init(uint32_t *ext, uint32_t nseg) {
+template <typename K>
+__global__ void k_ext_init(K *ext, uint32_t nseg) {
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
         for (int a = 0; a < 3; ++a) {
-            ext[s * 6 + a] = 0xffffffffu;  // min key
-            ext[s * 6 + 3 + a] = 0u;       // max key
+            ext[s * 6 + a] = ~(K)0;  // min key
+            ext[s * 6 + 3 + a] = 0;  // max key
         }
     }
 }
 
 // level 0 (one segment, P = identity, S = 0 -- neither is read): each block leaves its six
 // extents (NaN-ignoring min / max as ordered ints) in part[block]; k_ext_final reduces them
-__global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const float *__restrict__ y,
-                                             const float *__restrict__ z, const uint32_t *__restrict__ idx,
-                                             uint64_t total, uint32_t *part) {
-    __shared__ uint32_t red[6][4];
+template <typename T>
+__global__ __launch_bounds__(256) void k_ext(const T *__restrict__ x, const T *__restrict__ y,
+                                             const T *__restrict__ z, const uint32_t *__restrict__ idx,
+                                             uint64_t total, typename MC<T>::K *part) {
+    using K = typename MC<T>::K;
+    __shared__ K red[6][4];
     const uint64_t base = (uint64_t)blockIdx.x * 4096;
     if (base >= total) return;
     const uint64_t last = (base + 4096 < total ? base + 4096 : total) - 1;
-    const float *cols[3] = {x, y, z};
-    uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    const T *cols[3] = {x, y, z};
+    K mn[3] = {MC<T>::KMAX, MC<T>::KMAX, MC<T>::KMAX}, mx[3] = {0, 0, 0};
     // all 16 rows' indices, then all their coordinates, in flight before the first test
     uint32_t rows_[16];
 #pragma unroll
@@ -91,7 +121,7 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
         const uint64_t j = base + (uint64_t)r * 256 + threadIdx.x;
         rows_[r] = idx[j > last ? last : j];
     }
-    float vals_[16][3];
+    T vals_[16][3];
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
@@ -102,9 +132,9 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
         if (j > last) break;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float v = vals_[r][a];
+            const T v = vals_[r][a];
             if (v == v) {
-                const uint32_t k = fkey(v);
+                const K k = MC<T>::key(v);
                 mn[a] = k < mn[a] ? k : mn[a];
                 mx[a] = k > mx[a] ? k : mx[a];
             }
@@ -115,7 +145,7 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
     for (int a = 0; a < 3; ++a) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            uint32_t t0 = __shfl_xor(mn[a], o, 64), t1 = __shfl_xor(mx[a], o, 64);
+            K t0 = __shfl_xor(mn[a], o, 64), t1 = __shfl_xor(mx[a], o, 64);
             mn[a] = t0 < mn[a] ? t0 : mn[a];
             mx[a] = t1 > mx[a] ? t1 : mx[a];
         }
@@ -127,7 +157,7 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
     __syncthreads();
     if (threadIdx.x < 6) {
         const int q = threadIdx.x;
-        uint32_t v = red[q][0];
+        K v = red[q][0];
         for (int i = 1; i < 4; ++i) v = q < 3 ? (red[q][i] < v ? red[q][i] : v) : (red[q][i] > v ? red[q][i] : v);
         part[(uint64_t)blockIdx.x * 6 + q] = v;
     }
@@ -141,18 +171,21 @@ __global__ __launch_bounds__(256) void k_ext(const float *__restrict__ x, const 
 // slots into the global extents with one atomic per (segment, value).  (Per-element global
 // atomics on a handful of addresses took 2.5 ms at 10M on a lattice input.)
 constexpr int EXT_SLOTS = 4096 / 257 + 2;
-__global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, const float *__restrict__ y,
-                                                 const float *__restrict__ z, const uint32_t *__restrict__ idx,
+template <typename T>
+__global__ __launch_bounds__(256) void k_ext_seg(const T *__restrict__ x, const T *__restrict__ y,
+                                                 const T *__restrict__ z, const uint32_t *__restrict__ idx,
                                                  const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
-                                                 uint64_t total, uint32_t *ext, float4 *__restrict__ cxyz) {
-    __shared__ uint32_t slot[EXT_SLOTS * 6];
+                                                 uint64_t total, typename MC<T>::K *ext,
+                                                 typename MC<T>::V *__restrict__ cxyz) {
+    using K = typename MC<T>::K;
+    __shared__ K slot[EXT_SLOTS * 6];
     const uint64_t base = (uint64_t)blockIdx.x * 4096;
     if (base >= total) return;
     const uint64_t last = (base + 4096 < total ? base + 4096 : total) - 1;
     const uint32_t s0 = S[base], s1 = S[last];
-    for (int i = threadIdx.x; i < EXT_SLOTS * 6; i += 256) slot[i] = (i % 6) < 3 ? 0xffffffffu : 0u;
+    for (int i = threadIdx.x; i < EXT_SLOTS * 6; i += 256) slot[i] = (i % 6) < 3 ? MC<T>::KMAX : (K)0;
     __syncthreads();
-    const float *cols[3] = {x, y, z};
+    const T *cols[3] = {x, y, z};
     const int lane = threadIdx.x & 63;
     const uint64_t wb = base + (uint64_t)(threadIdx.x >> 6) * 1024;
     uint32_t seg_[16], pos_[16], rows_[16];
@@ -165,7 +198,7 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) rows_[r] = idx[pos_[r]];
-    float vals_[16][3];
+    T vals_[16][3];
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
@@ -174,24 +207,24 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
     // there: a segment's positions are contiguous), so x / y / z are gathered once per level
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-        if (seg_[r] != 0xffffffffu) cxyz[pos_[r]] = make_float4(vals_[r][0], vals_[r][1], vals_[r][2], 0.0f);
-    auto take = [&](uint32_t s, const float *v) {  // one lane into its segment's slot
+        if (seg_[r] != 0xffffffffu) cxyz[pos_[r]] = MC<T>::pack(vals_[r][0], vals_[r][1], vals_[r][2]);
+    auto take = [&](uint32_t s, const T *v) {  // one lane into its segment's slot
         const uint32_t q = s - s0;
-        uint32_t *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)s * 6];
+        K *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)s * 6];
 #pragma unroll
         for (int a = 0; a < 3; ++a)
             if (v[a] == v[a]) {
-                atomicMin(&dst[a], fkey(v[a]));
-                atomicMax(&dst[3 + a], fkey(v[a]));
+                atomicMin(&dst[a], MC<T>::key(v[a]));
+                atomicMax(&dst[3 + a], MC<T>::key(v[a]));
             }
     };
     uint32_t cur = 0xffffffffu;  // wave-uniform
-    uint32_t mn[3], mx[3];
+    K mn[3], mx[3];
     auto reset = [&] {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            mn[a] = 0xffffffffu;
-            mx[a] = 0u;
+            mn[a] = MC<T>::KMAX;
+            mx[a] = 0;
         }
     };
     auto flush = [&] {
@@ -200,17 +233,17 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
         for (int a = 0; a < 3; ++a)
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
-                const uint32_t t0 = __shfl_xor(mn[a], o, 64), t1 = __shfl_xor(mx[a], o, 64);
+                const K t0 = __shfl_xor(mn[a], o, 64), t1 = __shfl_xor(mx[a], o, 64);
                 mn[a] = t0 < mn[a] ? t0 : mn[a];
                 mx[a] = t1 > mx[a] ? t1 : mx[a];
             }
         if (lane == 0) {
             const uint32_t q = cur - s0;
-            uint32_t *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)cur * 6];
+            K *dst = q < (uint32_t)EXT_SLOTS ? &slot[q * 6] : &ext[(uint64_t)cur * 6];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                if (mn[a] != 0xffffffffu) atomicMin(&dst[a], mn[a]);
-                if (mx[a] != 0u) atomicMax(&dst[3 + a], mx[a]);
+                if (mn[a] != MC<T>::KMAX) atomicMin(&dst[a], mn[a]);
+                if (mx[a] != 0) atomicMax(&dst[3 + a], mx[a]);
             }
         }
         cur = 0xffffffffu;
@@ -229,9 +262,9 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
             }
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const float v = vals_[r][a];
+                const T v = vals_[r][a];
                 if (v == v) {
-                    const uint32_t k = fkey(v);
+                    const K k = MC<T>::key(v);
                     mn[a] = k < mn[a] ? k : mn[a];
                     mx[a] = k > mx[a] ? k : mx[a];
                 }
@@ -246,30 +279,32 @@ __global__ __launch_bounds__(256) void k_ext_seg(const float *__restrict__ x, co
     __syncthreads();
     const uint32_t used = (s1 - s0 + 1) * 6;
     for (uint32_t i = threadIdx.x; i < used && i < (uint32_t)EXT_SLOTS * 6; i += 256) {
-        const uint32_t v = slot[i], q = i / 6, a = i % 6;
+        const K v = slot[i];
+        const uint32_t q = i / 6, a = i % 6;
         if (a < 3) {
-            if (v != 0xffffffffu) atomicMin(&ext[(uint64_t)(s0 + q) * 6 + a], v);
-        } else if (v != 0u) {
+            if (v != MC<T>::KMAX) atomicMin(&ext[(uint64_t)(s0 + q) * 6 + a], v);
+        } else if (v != 0) {
             atomicMax(&ext[(uint64_t)(s0 + q) * 6 + a], v);
         }
     }
 }
 
 // level 0: the six extents from the per-block partials
-__global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ part, uint32_t nb, uint32_t *ext) {
-    __shared__ uint32_t red[6][4];
-    uint32_t v[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+template <typename K>
+__global__ __launch_bounds__(256) void k_ext_final(const K *__restrict__ part, uint32_t nb, K *ext) {
+    __shared__ K red[6][4];
+    K v[6] = {~(K)0, ~(K)0, ~(K)0, 0, 0, 0};
     for (uint32_t b = threadIdx.x; b < nb; b += 256)
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            const uint32_t t = part[(uint64_t)b * 6 + q];
+            const K t = part[(uint64_t)b * 6 + q];
             v[q] = q < 3 ? (t < v[q] ? t : v[q]) : (t > v[q] ? t : v[q]);
         }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
         for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t t = __shfl_xor(v[q], o, 64);
+            const K t = __shfl_xor(v[q], o, 64);
             v[q] = q < 3 ? (t < v[q] ? t : v[q]) : (t > v[q] ? t : v[q]);
         }
         if (lane == 0) red[q][w] = v[q];
@@ -277,7 +312,7 @@ __global__ __launch_bounds__(256) void k_ext_final(const uint32_t *__restrict__ 
     __syncthreads();
     if (threadIdx.x < 6) {
         const int q = threadIdx.x;
-        uint32_t r = red[q][0];
+        K r = red[q][0];
         for (int i = 1; i < 4; ++i) r = q < 3 ? (red[q][i] < r ? red[q][i] : r) : (red[q][i] > r ? red[q][i] : r);
         ext[q] = r;
     }
@@ -328,21 +363,23 @@ __global__ void k_seg_compact(const uint32_t *__restrict__ flag, const uint32_t 
 
 // ordering.ts:32-65 per segment
 // (level 0: seg_start null, the one segment starts at 0); also zeroes the level's big-run counts
-__global__ void k_seg_info(const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ z,
+template <typename T>
+__global__ void k_seg_info(const T *__restrict__ x, const T *__restrict__ y, const T *__restrict__ z,
                            const uint32_t *__restrict__ idx, const uint32_t *__restrict__ seg_start,
-                           const uint32_t *__restrict__ ext, uint32_t nseg, SegInfo *info, uint32_t *bigcnt) {
+                           const typename MC<T>::K *__restrict__ ext, uint32_t nseg, SegInfo *info,
+                           uint32_t *bigcnt) {
     if (blockIdx.x == 0 && threadIdx.x < 2) bigcnt[threadIdx.x] = 0;  // big runs of both sort paths
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
         const uint32_t first = idx[seg_start ? seg_start[s] : 0u];
-        const float f[3] = {x[first], y[first], z[first]};
+        const T f[3] = {x[first], y[first], z[first]};
         SegInfo si{};
         bool valid = true, all_zero = true;
         for (int a = 0; a < 3; ++a) {
             double len;
-            if (f[a] != f[a] || ext[s * 6 + a] == 0xffffffffu) {
+            if (f[a] != f[a] || ext[s * 6 + a] == MC<T>::KMAX) {
                 len = __builtin_nan("");  // NaN first element -> extents NaN (ordering.ts:38-41)
             } else {
-                const double lo = fkey_inv(ext[s * 6 + a]), hi = fkey_inv(ext[s * 6 + 3 + a]);
+                const double lo = MC<T>::inv(ext[s * 6 + a]), hi = MC<T>::inv(ext[s * 6 + 3 + a]);
                 len = hi - lo;
                 si.mn[a] = lo;
             }
@@ -355,15 +392,16 @@ __global__ void k_seg_info(const float *__restrict__ x, const float *__restrict_
     }
 }
 
-__device__ inline uint32_t axis_q(float v, double mn, double mul) {
+template <typename T>
+__device__ inline uint32_t axis_q(T v, double mn, double mul) {
     return js::to_uint32(js::min_(1023, ((double)v - mn) * mul));
 }
 
-template <typename K>
+template <typename K, typename T>
 __global__ __launch_bounds__(256) void k_keys(const uint32_t *__restrict__ idx,
                                               const uint32_t *__restrict__ P, const uint32_t *__restrict__ S,
                                               const SegInfo *__restrict__ info, uint64_t total,
-                                              const float4 *__restrict__ cxyz, K *__restrict__ keys,
+                                              const typename MC<T>::V *__restrict__ cxyz, K *__restrict__ keys,
                                               uint32_t *__restrict__ vals) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
@@ -373,7 +411,7 @@ __global__ __launch_bounds__(256) void k_keys(const uint32_t *__restrict__ idx,
         const SegInfo &si = info[s];
         uint32_t m = 0;
         if (si.ok) {
-            const float4 v = cxyz[p];
+            const typename MC<T>::V v = cxyz[p];
             const uint32_t ix = axis_q(v.x, si.mn[0], si.mul[0]);
             const uint32_t iy = axis_q(v.y, si.mn[1], si.mul[1]);
             const uint32_t iz = axis_q(v.z, si.mn[2], si.mul[2]);
@@ -387,8 +425,9 @@ __global__ __launch_bounds__(256) void k_keys(const uint32_t *__restrict__ idx,
 // level 0: one segment, P = identity -- keys only (the sort takes idx itself as its values) and
 // the first radix digit's count per sort tile (RADIX_TILE keys per workgroup), so the sort
 // skips its first histogram pass
-__global__ __launch_bounds__(256) void k_keys0(const float *__restrict__ x, const float *__restrict__ y,
-                                               const float *__restrict__ z, const uint32_t *__restrict__ idx,
+template <typename T>
+__global__ __launch_bounds__(256) void k_keys0(const T *__restrict__ x, const T *__restrict__ y,
+                                               const T *__restrict__ z, const uint32_t *__restrict__ idx,
                                                const SegInfo *__restrict__ info, uint64_t n,
                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ hist,
                                                uint32_t ntiles) {
@@ -428,10 +467,12 @@ __global__ __launch_bounds__(256) void k_keys0(const float *__restrict__ x, cons
 // registers between passes (wave ballots rank each 64-element row, as the device-wide
 // scatter does; LDS only for the reordering), the order written back into idx, and the
 // segment's own runs of > 256 equal keys appended to the next level's list
+template <typename T>
 __global__ __launch_bounds__(256) void k_seg_sort_small(const uint32_t *__restrict__ sstart,
                                                         const uint32_t *__restrict__ slen,
                                                         const SegInfo *__restrict__ sinfo, uint32_t nsmall,
-                                                        const float4 *__restrict__ cxyz, uint32_t *__restrict__ idx,
+                                                        const typename MC<T>::V *__restrict__ cxyz,
+                                                        uint32_t *__restrict__ idx,
                                                         uint32_t *__restrict__ ostart, uint32_t *__restrict__ olen,
                                                         uint32_t *__restrict__ ocnt) {
     constexpr int ROWS = SMALL_SEG / 256;
@@ -453,7 +494,7 @@ __global__ __launch_bounds__(256) void k_seg_sort_small(const uint32_t *__restri
             k[r] = 0u;
             v[r] = 0u;
             if (e < len) {
-                const float4 cv = cxyz[start + e];
+                const typename MC<T>::V cv = cxyz[start + e];
                 const uint32_t ix = axis_q(cv.x, si.mn[0], si.mul[0]);
                 const uint32_t iy = axis_q(cv.y, si.mn[1], si.mul[1]);
                 const uint32_t iz = axis_q(cv.z, si.mn[2], si.mul[2]);
@@ -616,9 +657,10 @@ __global__ __launch_bounds__(256) void k_big_segs(const K *__restrict__ keys, ui
     }
 }
 
-}  // namespace
-
-void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *idx, uint64_t n) {
+template <typename T>
+void morton_order_impl(st_ctx *c, const T *x, const T *y, const T *z, uint32_t *idx, uint64_t n) {
+    using K = typename MC<T>::K;
+    using V = typename MC<T>::V;
     if (n == 0) return;
     ST_REQUIRE(n < (1ull << 32) - 1, ST_ERR_ARG, "morton: n must be < 2^32-1");
     auto *h = static_cast<uint32_t *>(pinned(c, 64));
@@ -637,7 +679,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
     auto *bigcnt = wsT<uint32_t>(c, "mo.bigcnt", 2);  // [0] device-wide sort, [1] small segments
     auto *sm_start = wsT<uint32_t>(c, "mo.sm_start", n / 257 + 2);  // the small segments' big runs
     auto *sm_len = wsT<uint32_t>(c, "mo.sm_len", n / 257 + 2);
-    float4 *cxyz = nullptr;  // deeper levels: x / y / z gathered by k_ext_seg, at idx positions
+    V *cxyz = nullptr;  // deeper levels: x / y / z gathered by k_ext_seg, at idx positions
     for (int level = 0; nseg > 0; ++level) {
         const bool single = (level == 0);
         if (!single) {
@@ -649,20 +691,20 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
                                nseg, total, P, S);
             ST_LAUNCH_CHECK();
         }  // level 0: P = identity, S = 0, never materialised
-        auto *ext = wsT<uint32_t>(c, "mo.ext", (size_t)nseg * 6);
+        auto *ext = wsT<K>(c, "mo.ext", (size_t)nseg * 6);
         auto *info = static_cast<SegInfo *>(ws(c, "mo.info", sizeof(SegInfo) * (size_t)nseg));
         const unsigned eb = (unsigned)((total + 4095) / 4096);
         if (single) {
-            auto *part = wsT<uint32_t>(c, "mo.extpart", (size_t)eb * 6);
-            hipLaunchKernelGGL(k_ext, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, total, part);
-            hipLaunchKernelGGL(k_ext_final, dim3(1), dim3(256), 0, c->stream, part, eb, ext);
+            auto *part = wsT<K>(c, "mo.extpart", (size_t)eb * 6);
+            hipLaunchKernelGGL(k_ext<T>, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, total, part);
+            hipLaunchKernelGGL(k_ext_final<K>, dim3(1), dim3(256), 0, c->stream, part, eb, ext);
         } else {
-            if (!cxyz) cxyz = wsT<float4>(c, "mo.cxyz", n);
-            hipLaunchKernelGGL(k_ext_init, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
-            hipLaunchKernelGGL(k_ext_seg, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, ext, cxyz);
+            if (!cxyz) cxyz = wsT<V>(c, "mo.cxyz", n);
+            hipLaunchKernelGGL(k_ext_init<K>, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream, ext, nseg);
+            hipLaunchKernelGGL(k_ext_seg<T>, dim3(eb), dim3(256), 0, c->stream, x, y, z, idx, P, S, total, ext, cxyz);
         }
         ST_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_seg_info, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
+        hipLaunchKernelGGL(k_seg_info<T>, dim3(grid_for(nseg, 64, 1024)), dim3(64), 0, c->stream, x, y, z, idx,
                            single ? nullptr : seg_start, ext, nseg, info, bigcnt);
         ST_LAUNCH_CHECK();
         bool large = true;  // the device-wide sort has members at this level
@@ -694,7 +736,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
                 auto *sinfo = static_cast<SegInfo *>(ws(c, "mo.sinfo", sizeof(SegInfo) * (size_t)nsmall));
                 hipLaunchKernelGGL(k_seg_compact_small, dim3(grid_for(nseg, 256, 1024)), dim3(256), 0, c->stream,
                                    sflag, spos, seg_start, seg_len, info, nseg, sstart, slen, sinfo);
-                hipLaunchKernelGGL(k_seg_sort_small, dim3(std::min<uint32_t>(nsmall, 4096)), dim3(256), 0, c->stream,
+                hipLaunchKernelGGL(k_seg_sort_small<T>, dim3(std::min<uint32_t>(nsmall, 4096)), dim3(256), 0, c->stream,
                                    sstart, slen, sinfo, nsmall, cxyz, idx, sm_start, sm_len, bigcnt + 1);
                 ST_LAUNCH_CHECK();
             }
@@ -724,7 +766,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             const uint32_t nt = radix_tiles(n);
             auto *keys = wsT<uint32_t>(c, "mo.k32", n + 1);
             auto *hist = wsT<uint32_t>(c, "mo.hist0", (size_t)256 * nt);
-            hipLaunchKernelGGL(k_keys0, dim3(nt), dim3(256), 0, c->stream, x, y, z, idx, info, n, keys, hist, nt);
+            hipLaunchKernelGGL(k_keys0<T>, dim3(nt), dim3(256), 0, c->stream, x, y, z, idx, info, n, keys, hist, nt);
             ST_LAUNCH_CHECK();
             radix_sort_u32_from(c, keys, idx, n, 0, 30, keys, idx, hist, "mo.rs32");
             hipLaunchKernelGGL(k_big_starts<uint32_t>, dim3((unsigned)((total + 4095) / 4096)), dim3(256), 0, c->stream, keys, total, info, bigpos,
@@ -734,7 +776,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_LAUNCH_CHECK();
         } else if (seg_bits + 30 <= 32) {
             auto *keys = wsT<uint32_t>(c, "mo.k32", total + 1);
-            hipLaunchKernelGGL(k_keys<uint32_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
+            hipLaunchKernelGGL((k_keys<uint32_t, T>), dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
                                cxyz, keys, vals);
             ST_LAUNCH_CHECK();
             uint32_t *skeys = keys, *svals = vals;
@@ -747,7 +789,7 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
             ST_LAUNCH_CHECK();
         } else {
             auto *keys = wsT<uint64_t>(c, "mo.k64", total + 1);
-            hipLaunchKernelGGL(k_keys<uint64_t>, dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
+            hipLaunchKernelGGL((k_keys<uint64_t, T>), dim3(g), dim3(256), 0, c->stream, idx, P, S, info, total,
                                cxyz, keys, vals);
             ST_LAUNCH_CHECK();
             radix_sort_u64(c, keys, vals, total, 0, 30 + seg_bits, "mo.rs64");
@@ -770,6 +812,30 @@ void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z,
         std::swap(seg_start, nseg_start);
         std::swap(seg_len, nseg_len);
     }
+}
+
+}  // namespace
+
+void morton_order_dev(st_ctx *c, const float *x, const float *y, const float *z, uint32_t *idx, uint64_t n) {
+    morton_order_impl<float>(c, x, y, z, idx, n);
+}
+
+void morton_order_dev_f64(st_ctx *c, const double *x, const double *y, const double *z, uint32_t *idx, uint64_t n) {
+    morton_order_impl<double>(c, x, y, z, idx, n);
+}
+
+// generateOrdering over x / y / z columns of any type: ordering.ts:32-47 reads them as JS
+// numbers, so float32 columns take the float32 path and any other type (or a mix) the float64
+// one, whose values are the exact JS numbers of every type
+void morton_order_tdev(st_ctx *c, const void *const xyz[3], const int32_t types[3], uint32_t *idx, uint64_t n) {
+    if (types[0] == ST_PLY_FLOAT && types[1] == ST_PLY_FLOAT && types[2] == ST_PLY_FLOAT) {
+        morton_order_impl<float>(c, static_cast<const float *>(xyz[0]), static_cast<const float *>(xyz[1]),
+                                 static_cast<const float *>(xyz[2]), idx, n);
+        return;
+    }
+    const double *d[3];
+    for (int a = 0; a < 3; ++a) d[a] = as_f64_dev(c, TCol{const_cast<void *>(xyz[a]), types[a]}, n, "mo.f64." + std::to_string(a));
+    morton_order_impl<double>(c, d[0], d[1], d[2], idx, n);
 }
 
 }  // namespace st

@@ -528,6 +528,23 @@ int st_dev_transform(st_ctx *c, const st_table *t, const st_transform_params *p)
     });
 }
 
+int st_dev_transform_t(st_ctx *c, const st_ttable *t, const st_transform_params *p) {
+    return guarded([&] {
+        ST_REQUIRE(c && t && p && (t->ncol == 0 || (t->names && t->types && t->cols)), ST_ERR_ARG, "NULL argument");
+        use_device(c);
+        transform_tdev(c, t, p);
+    });
+}
+
+int st_dev_morton_order_t(st_ctx *c, const void *const xyz[3], const int32_t types[3], uint32_t *idx, uint64_t n) {
+    return guarded([&] {
+        ST_REQUIRE(c && xyz && types && ((xyz[0] && xyz[1] && xyz[2] && idx) || n == 0), ST_ERR_ARG, "NULL argument");
+        for (int a = 0; a < 3; ++a) ST_REQUIRE(type_size(types[a]) > 0, ST_ERR_ARG, "morton: bad column type");
+        use_device(c);
+        morton_order_tdev(c, xyz, types, idx, n);
+    });
+}
+
 int st_dev_filter_finite(st_ctx *c, const st_table *t, uint32_t *out_idx, uint64_t *out_n) {
     return guarded([&] {
         ST_ARG(c && out_n, "NULL argument");

@@ -13,6 +13,7 @@
 
 #include "st_jsmath.h"
 #include "st_kmeans.h"
+#include "st_typed.h"
 
 namespace st {
 namespace {
@@ -46,8 +47,9 @@ __global__ __launch_bounds__(256) void k_remap_labels(const uint32_t *lab, const
 }
 
 
+template <typename T>
 struct MeansArgs {
-    const float *c[3];
+    const T *c[3];
     double mn[3], mx[3];
 };
 
@@ -64,7 +66,8 @@ __device__ inline void tex_slot(const uint32_t *idx, const uint32_t *pos, uint64
     o = pos ? (uint64_t)pos[i] : i;
 }
 
-__global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint32_t *__restrict__ idx,
+template <typename T>
+__global__ __launch_bounds__(256) void k_means_tex(const MeansArgs<T> a, const uint32_t *__restrict__ idx,
                                                   const uint32_t *__restrict__ pos, uint64_t n,
                                                   uint32_t *__restrict__ ml, uint32_t *__restrict__ mu) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -85,8 +88,9 @@ __global__ __launch_bounds__(256) void k_means_tex(const MeansArgs a, const uint
     }
 }
 
-__global__ __launch_bounds__(256) void k_quats_tex(const float *__restrict__ q0, const float *__restrict__ q1,
-                                                  const float *__restrict__ q2, const float *__restrict__ q3,
+template <typename T>
+__global__ __launch_bounds__(256) void k_quats_tex(const T *__restrict__ q0, const T *__restrict__ q1,
+                                                  const T *__restrict__ q2, const T *__restrict__ q3,
                                                   const uint32_t *__restrict__ idx, const uint32_t *__restrict__ pos,
                                                   uint64_t n, uint32_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -122,8 +126,9 @@ __global__ __launch_bounds__(256) void k_quats_tex(const float *__restrict__ q0,
 }
 
 // writeTableData (write-sog.ts:142-157): rgb from u8 label columns, alpha = 4th column or 255
+template <typename T>
 __global__ __launch_bounds__(256) void k_table_tex(const uint8_t *__restrict__ l0, const uint8_t *__restrict__ l1,
-                                                  const uint8_t *__restrict__ l2, const float *__restrict__ opacity,
+                                                  const uint8_t *__restrict__ l2, const T *__restrict__ opacity,
                                                   const uint32_t *__restrict__ idx, const uint32_t *__restrict__ pos,
                                                   uint64_t n, uint32_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(256) void k_table_tex(const uint8_t *__restrict__ l
         uint64_t o;
         tex_slot(idx, pos, i, r, o);
         uint32_t a = 255;
-        if (opacity) a = js::to_uint8(js::max_(0, js::min_(255, js::sigmoid(opacity[r]) * 255)));
+        if (opacity) a = js::to_uint8(js::max_(0, js::min_(255, js::sigmoid((double)opacity[r]) * 255)));
         out[o] = (uint32_t)l0[r] | ((uint32_t)l1[r] << 8) | ((uint32_t)l2[r] << 16) | (a << 24);
     }
 }
@@ -160,6 +165,42 @@ __global__ __launch_bounds__(256) void k_shn_centroids_tex(const uint8_t *__rest
         const uint64_t i = t / C, j = t % C;
         out[t] = (uint32_t)cl[j * pal + i] | ((uint32_t)cl[(C + j) * pal + i] << 8) |
                  ((uint32_t)cl[(2 * C + j) * pal + i] << 16) | 0xff000000u;
+    }
+}
+
+// calcMinMax (write-sog.ts:15-31) of float64 columns: NaN-ignoring min / max as ordered keys,
+// one atomic per block and column
+__device__ inline unsigned long long dkey(double d) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, d);
+    return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__host__ inline double dkey_inv(unsigned long long k) {
+    return __builtin_bit_cast(double, (k >> 63) ? (k & ~(1ull << 63)) : ~k);
+}
+__global__ __launch_bounds__(256) void k_mm64(const double *__restrict__ a, const double *__restrict__ b,
+                                              const double *__restrict__ cc, uint64_t n,
+                                              unsigned long long *__restrict__ out) {
+    const double *cols[3] = {a, b, cc};
+    unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        for (int q = 0; q < 3; ++q) {
+            const double v = cols[q][i];
+            if (v == v) {
+                const unsigned long long k = dkey(v);
+                mn[q] = k < mn[q] ? k : mn[q];
+                mx[q] = k > mx[q] ? k : mx[q];
+            }
+        }
+    for (int q = 0; q < 3; ++q) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long t0 = __shfl_xor(mn[q], o, 64), t1 = __shfl_xor(mx[q], o, 64);
+            mn[q] = t0 < mn[q] ? t0 : mn[q];
+            mx[q] = t1 > mx[q] ? t1 : mx[q];
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (mn[q] != ~0ull) atomicMin(&out[2 * q], mn[q]);
+            if (mx[q] != 0ull) atomicMax(&out[2 * q + 1], mx[q]);
+        }
     }
 }
 
@@ -221,7 +262,7 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
         // an empty shard's columns may be NULL (no rows to read): only the meta is computed
         ST_REQUIRE(m[i] || n == 0, ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
     }
-    MeansArgs ma{};
+    MeansArgs<float> ma{};
     for (int a = 0; a < 3; ++a) {
         ma.c[a] = m[a];
         ma.mn[a] = js::log_transform(lo[a]);
@@ -232,16 +273,16 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
     if (!n) return;
     const unsigned g = grid_for(n, 256, 8192);
     if (out->means_l && out->means_u)
-        hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
+        hipLaunchKernelGGL(k_means_tex<float>, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
                            (uint32_t *)out->means_l, (uint32_t *)out->means_u);
     if (out->quats)
-        hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[4], m[5], m[6], m[7],
+        hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, c->stream, m[4], m[5], m[6], m[7],
                            (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
     if (out->scales && scale_lab)
-        hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, scale_lab, scale_lab + n, scale_lab + 2 * n,
+        hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, scale_lab, scale_lab + n, scale_lab + 2 * n,
                            (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
     if (out->sh0 && color_lab)
-        hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, color_lab, color_lab + n, color_lab + 2 * n,
+        hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, color_lab, color_lab + n, color_lab + 2 * n,
                            m[3], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     if (out->shn_labels && shn_lab)
         hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, shn_lab, (const uint32_t *)nullptr,
@@ -255,19 +296,91 @@ void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *ou
     ST_LAUNCH_CHECK();
 }
 
+namespace {
+const char *const SOG_MEMBERS[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
+                                     "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+
+// the columns writeSog reads: Float32Array values (cluster1d data, k-means points) and, where a
+// column is not float32, the JS numbers the reference computes with (positions, rotations,
+// opacity, and the SH values calcAverage sums)
+struct SogSrc {
+    uint64_t n = 0;
+    int C = 0;
+    const float *m[14] = {};
+    const double *pos64[3] = {};  // all three set or none
+    const double *rot64[4] = {};  // all four set or none
+    const double *op64 = nullptr;
+    const float *sh[45] = {};
+    const double *sh64[45] = {};  // all 3C set or none
+};
+
+uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, uint64_t ndraws,
+                  st_sog_meta *meta, const st_sog_textures *out);
+}  // namespace
+
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,
                  const st_sog_textures *out) {
-    const uint64_t n = t->n;
+    SogSrc src;
+    src.n = t->n;
+    for (int i = 0; i < 14; ++i) {
+        src.m[i] = col_or_null(t, SOG_MEMBERS[i]);
+        ST_REQUIRE(src.m[i], ST_ERR_ARG, std::string("sog: missing column ") + SOG_MEMBERS[i]);
+    }
+    src.C = sh_coeffs_of(t);
+    char nm[32];
+    for (int i = 0; i < 3 * src.C; ++i) {
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        src.sh[i] = col_or_null(t, nm);
+    }
+    return sog_impl(c, src, iters, draws, ndraws, meta, out);
+}
+
+uint64_t sog_tdev(st_ctx *c, const st_ttable *t, int iters, const double *draws, uint64_t ndraws,
+                  st_sog_meta *meta, const st_sog_textures *out) {
+    SogSrc src;
+    src.n = t->n;
+    TCol tc[14];
+    for (int i = 0; i < 14; ++i) {
+        tc[i] = tcol_or_null(t, SOG_MEMBERS[i]);
+        ST_REQUIRE(tc[i].p, ST_ERR_ARG, std::string("sog: missing column ") + SOG_MEMBERS[i]);
+        src.m[i] = as_f32_dev(c, tc[i], src.n, "sogt.m32." + std::to_string(i));
+    }
+    const auto f64 = [&](int i) { return as_f64_dev(c, tc[i], src.n, "sogt.m64." + std::to_string(i)); };
+    if (tc[0].t != ST_PLY_FLOAT || tc[1].t != ST_PLY_FLOAT || tc[2].t != ST_PLY_FLOAT)
+        for (int a = 0; a < 3; ++a) src.pos64[a] = f64(a);
+    if (tc[10].t != ST_PLY_FLOAT || tc[11].t != ST_PLY_FLOAT || tc[12].t != ST_PLY_FLOAT || tc[13].t != ST_PLY_FLOAT)
+        for (int a = 0; a < 4; ++a) src.rot64[a] = f64(10 + a);
+    if (tc[9].t != ST_PLY_FLOAT) src.op64 = f64(9);
+    int first_missing = -1;
+    char nm[32];
+    for (int i = 0; i < 45 && first_missing < 0; ++i) {
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        if (!tcol_or_null(t, nm).p) first_missing = i;
+    }
+    src.C = first_missing == 9 ? 3 : first_missing == 24 ? 8 : first_missing == -1 ? 15 : 0;
+    bool sh32 = true;
+    for (int i = 0; i < 3 * src.C; ++i) {
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        const TCol col = tcol_or_null(t, nm);
+        sh32 = sh32 && col.t == ST_PLY_FLOAT;
+        src.sh[i] = as_f32_dev(c, col, src.n, "sogt.sh32." + std::to_string(i));
+    }
+    if (!sh32)
+        for (int i = 0; i < 3 * src.C; ++i) {
+            snprintf(nm, sizeof nm, "f_rest_%d", i);
+            src.sh64[i] = as_f64_dev(c, tcol_or_null(t, nm), src.n, "sogt.sh64." + std::to_string(i));
+        }
+    return sog_impl(c, src, iters, draws, ndraws, meta, out);
+}
+
+namespace {
+uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, uint64_t ndraws,
+                  st_sog_meta *meta, const st_sog_textures *out) {
+    const uint64_t n = src.n;
     ST_REQUIRE(n > 0, ST_ERR_ARG, "sog: empty table");
     ST_REQUIRE(n < (1ull << 31), ST_ERR_ARG, "sog: n must be < 2^31 per device");
-    static const char *members[14] = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
-                                      "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
-    const float *m[14];
-    for (int i = 0; i < 14; ++i) {
-        m[i] = col_or_null(t, members[i]);
-        ST_REQUIRE(m[i], ST_ERR_ARG, std::string("sog: missing column ") + members[i]);
-    }
-    const int C = sh_coeffs_of(t);
+    const float *const *m = src.m;
+    const int C = src.C;
     int32_t W, H, pal, cw, chh;
     st_sog_geometry(n, C, &W, &H, &pal, &cw, &chh);
     const uint64_t texels = (uint64_t)W * H;
@@ -317,7 +430,8 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     // Morton order (write-sog.ts:42-49)
     auto *idx = wsT<uint32_t>(c, "sog.idx", n);
     iota_u32(c, idx, n);
-    morton_order_dev(c, m[0], m[1], m[2], idx, n);
+    if (src.pos64[0]) morton_order_dev_f64(c, src.pos64[0], src.pos64[1], src.pos64[2], idx, n);
+    else morton_order_dev(c, m[0], m[1], m[2], idx, n);
     // the texture kernels run in scatter form: row r (read in input order, coalesced) writes
     // texel pos[r], one 4-byte store, instead of gathering 3-4 values per texel at random
     auto *pos = wsT<uint32_t>(c, "sog.pos", n);
@@ -327,25 +441,53 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     const unsigned g = grid_for(n, 256, 8192);
 
     // means (write-sog.ts:161-187)
-    auto *mm = wsT<uint32_t>(c, "sog.mm", 6);
-    minmax_keys_dev(c, m, 3, n, mm);  // [min, max] keys of x, y, z (NaN skipped)
-    uint32_t hmm[6];
-    ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
-    MeansArgs ma{};
-    for (int a = 0; a < 3; ++a) {
-        ma.c[a] = m[a];
-        const double lo = hmm[2 * a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[2 * a]);
-        const double hi = hmm[2 * a + 1] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[2 * a + 1]);
-        ma.mn[a] = js::log_transform(lo);
-        ma.mx[a] = js::log_transform(hi);
-        meta->means_min[a] = ma.mn[a];
-        meta->means_max[a] = ma.mx[a];
+    double lo[3], hi[3];
+    if (src.pos64[0]) {
+        auto *mm = wsT<unsigned long long>(c, "sog.mm64", 6);
+        const unsigned long long init[6] = {~0ull, 0ull, ~0ull, 0ull, ~0ull, 0ull};
+        unsigned long long hmm[6];
+        ST_HIP(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_mm64, dim3(grid_for(n, 256, 1024)), dim3(256), 0, c->stream, src.pos64[0], src.pos64[1],
+                           src.pos64[2], n, mm);
+        ST_LAUNCH_CHECK();
+        ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = hmm[2 * a] == ~0ull ? HUGE_VAL : dkey_inv(hmm[2 * a]);
+            hi[a] = hmm[2 * a + 1] == 0ull ? -HUGE_VAL : dkey_inv(hmm[2 * a + 1]);
+        }
+    } else {
+        auto *mm = wsT<uint32_t>(c, "sog.mm", 6);
+        minmax_keys_dev(c, m, 3, n, mm);  // [min, max] keys of x, y, z (NaN skipped)
+        uint32_t hmm[6];
+        ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = hmm[2 * a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[2 * a]);
+            hi[a] = hmm[2 * a + 1] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[2 * a + 1]);
+        }
     }
-    hipLaunchKernelGGL(k_means_tex, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
-                       (uint32_t *)out->means_l, (uint32_t *)out->means_u);
-    hipLaunchKernelGGL(k_quats_tex, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13],
-                       (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
+    for (int a = 0; a < 3; ++a) {
+        meta->means_min[a] = js::log_transform(lo[a]);
+        meta->means_max[a] = js::log_transform(hi[a]);
+    }
+    if (src.pos64[0]) {
+        MeansArgs<double> ma{};
+        for (int a = 0; a < 3; ++a) ma.c[a] = src.pos64[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
+        hipLaunchKernelGGL(k_means_tex<double>, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos,
+                           n, (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+    } else {
+        MeansArgs<float> ma{};
+        for (int a = 0; a < 3; ++a) ma.c[a] = m[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
+        hipLaunchKernelGGL(k_means_tex<float>, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
+                           (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+    }
+    if (src.rot64[0])
+        hipLaunchKernelGGL(k_quats_tex<double>, dim3(g), dim3(256), 0, c->stream, src.rot64[0], src.rot64[1],
+                           src.rot64[2], src.rot64[3], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
+    else
+        hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13],
+                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
     ST_LAUNCH_CHECK();
     mark(c, "sog.means_quats");
 
@@ -355,7 +497,7 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     // scales (write-sog.ts:245-251)
     cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
+    hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
                        (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
     ST_LAUNCH_CHECK();
     mark(c, "sog.scales");
@@ -372,8 +514,12 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
         ccb = cb;
     }
     ST_HIP(hipMemcpyAsync(meta->sh0_codebook, ccb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    hipLaunchKernelGGL(k_table_tex, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n, m[9],
-                       (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+    if (src.op64)
+        hipLaunchKernelGGL(k_table_tex<double>, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n,
+                           src.op64, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+    else
+        hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n, m[9],
+                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
 
@@ -384,15 +530,10 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
         meta->shn_width = cw;
         meta->shn_height = chh;
         const int D = 3 * C;
-        std::vector<const float *> sh(D);
-        char nm[32];
-        for (int i = 0; i < D; ++i) {
-            snprintf(nm, sizeof nm, "f_rest_%d", i);
-            sh[i] = col_or_null(t, nm);
-        }
         auto *cen = wsT<float>(c, "sog.shcen", (size_t)pal * D);
         auto *labels = wsT<uint32_t>(c, "sog.shlab", n);
-        cursor += kmeans_dev(c, sh.data(), D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels);
+        cursor += kmeans_dev(c, src.sh, D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels, false,
+                             src.sh64[0] ? src.sh64 : nullptr);
         mark(c, "sog.shkmeans");
         std::vector<const float *> ccols(D);
         for (int i = 0; i < D; ++i) ccols[i] = cen + (uint64_t)i * pal;
@@ -411,6 +552,7 @@ uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, u
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;
 }
+}  // namespace
 
 }  // namespace st
 

@@ -20,7 +20,8 @@
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
 //   cluster1d(dataTable, iterations)        write-sog.ts:56-99
 //   sogTextures(dataTable, iterations)      write-sog.ts:110-370 (textures + meta, before WebP/ZIP)
-//   writeSogBundle(dataTable, iterations)   write-sog.ts:110-370 to a .sog (WebP + CRC + ZIP on the device)
+//   writeSogBundle(dataTable, iterations[, actions])  write-sog.ts:110-370 to a .sog (WebP + CRC + ZIP on
+//                                           the device; actions first, same device call)
 //   WebpEncoder                             utils/webp.ts:19-41 (encodeLosslessRGBA)
 //   readPly(fileHandle)                     readers/read-ply.ts:111-191
 //   isCompressedPly / decompressPly(ply)    readers/decompress-ply.ts:6-232
@@ -74,6 +75,10 @@ const takeDraws = (count) => {
 const giveBack = (draws, used) => {
     pending = Array.from(draws.subarray(used)).concat(pending);
 };
+
+// drop the draws taken from Math.random but not consumed yet (call after re-seeding Math.random:
+// the next call then starts on the new stream)
+const resetRandomStream = () => { pending = []; };
 
 // error.code of a call that ran out of draws (ST_ERR_DRAWS = -4, st_abi.h; the addon's throw_st)
 const ST_ERR_DRAWS_CODE = 'ST_STATUS_4';
@@ -130,14 +135,14 @@ const transformColumns = (dataTable) => {
 };
 
 // t: {x, y, z} (Vec3), r: {x, y, z, w} (Quat), s: number -- mutates the columns in place.
-// The device path computes in f64 and stores float32 (the PLY 3DGS layout); a transformed column
-// of another type throws instead of being skipped.
+// The device path computes in f64 on the columns' numbers and stores as the TypedArray does
+// (float32 tables: float32 stores; other types through st_transform_t, as getRow / setRow).
 const transform = (dataTable, t, r, s) => {
-    for (const name of transformColumns(dataTable)) {
-        const c = dataTable.getColumnByName(name);
-        if (!(c.data instanceof Float32Array)) {
-            throw new Error(`splat-hip: transform supports float32 columns only ('${name}' is ${c.data.constructor.name})`);
-        }
+    const typed = transformColumns(dataTable).some(n => !(dataTable.getColumnByName(n).data instanceof Float32Array));
+    if (typed) {
+        addon.transformTyped(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+            [t.x, t.y, t.z], [r.x, r.y, r.z, r.w], s);
+        return;
     }
     const { cols, names } = f32Columns(dataTable);
     addon.transform(cols, names, [t.x, t.y, t.z], [r.x, r.y, r.z, r.w], s);
@@ -152,6 +157,10 @@ const generateOrdering = (dataTable, indices) => {
     const x = dataTable.getColumnByName('x').data;
     const y = dataTable.getColumnByName('y').data;
     const z = dataTable.getColumnByName('z').data;
+    // ordering.ts:32-47 reads the numbers of any column type
+    if (!(x instanceof Float32Array && y instanceof Float32Array && z instanceof Float32Array)) {
+        return addon.mortonOrderTyped(x, y, z, indices);
+    }
     return addon.mortonOrder(x, y, z, indices);
 };
 
@@ -187,6 +196,11 @@ const combine = (dataTables) => {
 
 // the chunk / vertex / sh arrays writeCompressedPly writes after its header
 const packCompressed = (dataTable) => {
+    if (dataTable.columns.some(c => !(c.data instanceof Float32Array))) {
+        // any column type: the writer's device path over the typed table (no actions)
+        const res = addon.compressedPly(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name), []);
+        return { chunk: res.chunk, vertex: res.vertex, sh: res.sh };
+    }
     const n = dataTable.numRows;
     const order = new Uint32Array(n);
     for (let i = 0; i < n; ++i) order[i] = i;
@@ -343,12 +357,14 @@ const cluster1d = (dataTable, iterations) => {
     return Promise.resolve({ centroids, labels });
 };
 
-// writeSog's device work: the seven RGBA textures and the meta.json fields
+// writeSog's device work: the seven RGBA textures and the meta.json fields (columns of any type:
+// write-sog.ts reads positions, rotations and opacity as numbers, cluster1d and the k-means
+// points through Float32Arrays)
 const sogTextures = (dataTable, iterations) => {
-    const { cols, names } = f32Columns(dataTable);
     const k = 65536;
     return Promise.resolve(withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
-        draws => addon.sog(cols, names, iterations, draws)));
+        draws => addon.sogProcess(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name), [],
+            iterations, draws)));
 };
 
 // utils/webp.ts:19-41: same class shape; the stream is a valid lossless WebP of the same
@@ -363,14 +379,15 @@ class WebpEncoder {
 
 // writeSog to a .sog bundle (write-sog.ts:110-370 with its ZipWriter): the archive bytes.
 // The ZIP clock is taken like zip-writer.ts:39-41 when the archive is written.
-const writeSogBundle = (dataTable, iterations) => {
-    const { cols, names } = f32Columns(dataTable);
+const writeSogBundle = (dataTable, iterations, processActions) => {
     const k = 65536;
     const date = new Date();
     const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
     const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
+    const acts = normaliseActions(processActions || []);
     const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
-        draws => addon.sogBundle(cols, names, iterations, draws, dosTime, dosDate));
+        draws => addon.sogBundleProcess(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name), acts,
+            iterations, draws, dosTime, dosDate));
     return Promise.resolve(res.archive);
 };
 
@@ -437,6 +454,7 @@ const setDevices = (n) => addon.setDevices(n);
 const getDevices = () => addon.getDevices();
 
 module.exports = {
+    resetRandomStream,
     setDevices,
     getDevices,
     Column,

@@ -1014,6 +1014,209 @@ fail:
     return NULL;
 }
 
+/* the band rule of the reference (write-sog.ts:296) over column names */
+static int32_t sh_coeffs_of_names(char **names, uint32_t m) {
+    int first_missing = -1;
+    char nm[16];
+    for (int i = 0; i < 45 && first_missing < 0; ++i) {
+        int hit = 0;
+        snprintf(nm, sizeof nm, "f_rest_%d", i);
+        for (uint32_t j = 0; j < m && !hit; ++j) hit = strcmp(names[j], nm) == 0;
+        if (!hit) first_missing = i;
+    }
+    return first_missing == 9 ? 3 : first_missing == 24 ? 8 : first_missing == -1 ? 15 : 0;
+}
+
+/* sogProcess(columns: TypedArray[] of any of the eight types, names, actions, iters, draws) ->
+ * as sog(): processDataTable then writeSog's textures and meta (st_sog_process) */
+static napi_value js_sog_process(napi_env env, napi_callback_info info) {
+    size_t argc = 5, nd = 0;
+    napi_value argv[5], out = NULL, tex;
+    chain_args a;
+    st_ctx *ctx;
+    uint8_t *hb[7] = {NULL, NULL, NULL, NULL, NULL, NULL, NULL};
+    static const char *tn[7] = {"means_l", "means_u", "quats", "scales", "sh0", "shN_centroids", "shN_labels"};
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
+    {
+        const int32_t iters = (int32_t)num(env, argv[3]);
+        double *draws = (double *)ta_data(env, argv[4], napi_float64_array, &nd);
+        int32_t W = 0, H = 0, pal = 0, cw = 0, ch = 0;
+        uint64_t used = 0;
+        st_sog_meta meta;
+        st_sog_textures t;
+        if (!draws || !get_ctx(env, &ctx)) goto fail;
+        /* sized for the input rows and band (the actions only remove rows or bands) */
+        if (st_sog_geometry(a.n, sh_coeffs_of_names(a.names, a.m), &W, &H, &pal, &cw, &ch) != ST_OK) {
+            napi_throw_range_error(env, NULL, "splat-hip: empty table");
+            goto fail;
+        }
+        for (int i = 0; i < 7; ++i) hb[i] = (uint8_t *)malloc(((i == 5) ? (size_t)cw * ch * 4 : (size_t)W * H * 4) + 1);
+        t.means_l = hb[0], t.means_u = hb[1], t.quats = hb[2], t.scales = hb[3], t.sh0 = hb[4];
+        t.shn_centroids = hb[5], t.shn_labels = hb[6];
+        {
+            st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+            int rc = st_sog_process(ctx, &ts, a.acts, (int32_t)a.na, iters, draws, nd, &used, &meta, &t);
+            if (rc != ST_OK) {
+                throw_st(env, rc);
+                goto fail;
+            }
+        }
+        {
+            /* the processed table's geometry (its rows and band after the actions) */
+            const int has_sh = meta.sh_bands > 0;
+            if (napi_create_object(env, &out) != napi_ok || napi_create_object(env, &tex) != napi_ok) goto fail;
+            for (int i = 0; i < 7; ++i) {
+                const size_t b = (i == 5) ? (size_t)meta.shn_width * meta.shn_height * 4
+                                          : (size_t)meta.width * meta.height * 4;
+                void *p;
+                napi_value v;
+                if (i >= 5 && !has_sh) continue;
+                if (!(v = new_typed(env, napi_uint8_array, b, 1, &p))) goto fail;
+                memcpy(p, hb[i], b);
+                set_named(env, tex, tn[i], v);
+            }
+        }
+        set_named(env, out, "textures", tex);
+        set_named(env, out, "width", make_num(env, meta.width));
+        set_named(env, out, "height", make_num(env, meta.height));
+        {
+            napi_value mins, maxs;
+            napi_create_array_with_length(env, 3, &mins);
+            napi_create_array_with_length(env, 3, &maxs);
+            for (uint32_t i = 0; i < 3; ++i) {
+                napi_set_element(env, mins, i, make_num(env, meta.means_min[i]));
+                napi_set_element(env, maxs, i, make_num(env, meta.means_max[i]));
+            }
+            set_named(env, out, "meansMins", mins);
+            set_named(env, out, "meansMaxs", maxs);
+        }
+        set_named(env, out, "scalesCodebook", f32_copy(env, meta.scales_codebook, 256));
+        set_named(env, out, "sh0Codebook", f32_copy(env, meta.sh0_codebook, 256));
+        set_named(env, out, "shBands", make_num(env, meta.sh_bands));
+        set_named(env, out, "paletteSize", make_num(env, meta.palette_size));
+        set_named(env, out, "shNCodebook", f32_copy(env, meta.shn_codebook, 256));
+        set_named(env, out, "shNWidth", make_num(env, meta.shn_width));
+        set_named(env, out, "shNHeight", make_num(env, meta.shn_height));
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    for (int i = 0; i < 7; ++i) free(hb[i]);
+    chain_free(&a);
+    return out;
+fail:
+    for (int i = 0; i < 7; ++i) free(hb[i]);
+    chain_free(&a);
+    return NULL;
+}
+
+/* sogBundleProcess(columns: TypedArray[] of any type, names, actions, iters, draws, dosTime,
+ * dosDate) -> {archive, used}: processDataTable then writeSog to .sog bytes (st_sog_bundle_process) */
+static napi_value js_sog_bundle_process(napi_env env, napi_callback_info info) {
+    size_t argc = 7, nd = 0;
+    napi_value argv[7], out = NULL, buf;
+    chain_args a;
+    st_ctx *ctx;
+    uint8_t *arch = NULL;
+    uint64_t size = 0, used = 0;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
+    {
+        double *draws = (double *)ta_data(env, argv[4], napi_float64_array, &nd);
+        if (!draws || !get_ctx(env, &ctx)) goto fail;
+        st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+        int rc = st_sog_bundle_process(ctx, &ts, a.acts, (int32_t)a.na, (int32_t)num(env, argv[3]), draws, nd, &used,
+                                       (uint16_t)num(env, argv[5]), (uint16_t)num(env, argv[6]), &arch, &size);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        void *p;
+        if (napi_create_buffer_copy(env, size, arch, &p, &buf) != napi_ok) goto fail;
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "archive", buf);
+        set_named(env, out, "used", make_num(env, (double)used));
+    }
+    st_free(arch);
+    chain_free(&a);
+    return out;
+fail:
+    st_free(arch);
+    chain_free(&a);
+    return NULL;
+}
+
+/* transformTyped(columns: TypedArray[] of any type, names, t[3], r[4], s): transform() in place
+ * (st_transform_t) */
+static napi_value js_transform_typed(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5], e, none;
+    chain_args a;
+    st_ctx *ctx;
+    double t[3], r[4];
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (napi_create_array_with_length(env, 0, &none) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], none, &a)) goto fail;
+    for (uint32_t i = 0; i < 3; ++i) napi_get_element(env, argv[2], i, &e), t[i] = num(env, e);
+    for (uint32_t i = 0; i < 4; ++i) napi_get_element(env, argv[3], i, &e), r[i] = num(env, e);
+    {
+        st_transform_params p;
+        st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+        int rc = st_transform_params_make(t, r, num(env, argv[4]), &p);
+        if (rc == ST_OK) {
+            if (!get_ctx(env, &ctx)) goto fail;
+            rc = st_transform_t(ctx, &ts, &p);
+        }
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+    }
+    chain_free(&a);
+    return NULL;
+fail:
+    chain_free(&a);
+    return NULL;
+}
+
+/* mortonOrderTyped(x, y, z: TypedArrays of any type, indices: Uint32Array) -> indices
+ * (st_morton_order_t) */
+static napi_value js_morton_typed(napi_env env, napi_callback_info info) {
+    size_t argc = 4, ni = 0;
+    napi_value argv[4];
+    st_ctx *ctx;
+    const void *xyz[3];
+    int32_t types[3];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    {
+        uint32_t *idx = (uint32_t *)ta_data(env, argv[3], napi_uint32_array, &ni);
+        if (!idx) return NULL;
+        for (int a = 0; a < 3; ++a) {
+            napi_typedarray_type nt;
+            napi_value ab;
+            size_t len = 0, off = 0, es = 0;
+            void *data;
+            bool is_ta = false;
+            if (napi_is_typedarray(env, argv[a], &is_ta) != napi_ok || !is_ta ||
+                napi_get_typedarray_info(env, argv[a], &nt, &len, &data, &ab, &off) != napi_ok ||
+                !(types[a] = ply_type_of(nt, &es))) {
+                napi_throw_type_error(env, NULL, "splat-hip: expected the reference's TypedArray columns");
+                return NULL;
+            }
+            if (len != ni) {
+                napi_throw_range_error(env, NULL, "splat-hip: x/y/z/indices lengths differ");
+                return NULL;
+            }
+            xyz[a] = data;
+        }
+        if (!get_ctx(env, &ctx)) return NULL;
+        int rc = st_morton_order_t(ctx, xyz, types, idx, (uint64_t)ni);
+        if (rc != ST_OK) return throw_st(env, rc);
+    }
+    return argv[3];
+fail:
+    return NULL;
+}
+
 static napi_value js_webp_lossless(napi_env env, napi_callback_info info) {
     size_t argc = 4, len = 0;
     napi_value argv[4], out;
@@ -1251,7 +1454,11 @@ static napi_value init(napi_env env, napi_value exports) {
                {"compressedPly", js_compressed_ply},
                {"compressedPlyFromFile", js_compressed_ply_file},
                {"sogBundleFromFile", js_sog_bundle_file},
-               {"process", js_process}};
+               {"process", js_process},
+               {"sogProcess", js_sog_process},
+               {"sogBundleProcess", js_sog_bundle_process},
+               {"transformTyped", js_transform_typed},
+               {"mortonOrderTyped", js_morton_typed}};
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;
         if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok) return NULL;

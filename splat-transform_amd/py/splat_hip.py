@@ -114,6 +114,8 @@ EXPORTS = [
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
     'st_group_sog_bundle_process',
+    'st_transform_t', 'st_dev_transform_t', 'st_morton_order_t', 'st_dev_morton_order_t', 'st_sog_process',
+    'st_sog_bundle_process', 'st_dev_sog_t',
 ]
 
 
@@ -559,6 +561,12 @@ class Context:
 
     # ---- host-memory seams ----------------------------------------------------
     def transform(self, cols, params):
+        """transform() in place on host columns (dict name -> array); columns that are not float32
+        take st_transform_t (the reference's getRow / setRow on any type)"""
+        if any(np.dtype(a.dtype) != np.float32 for a in cols.values()):
+            t = make_ttable(cols)
+            check(lib().st_transform_t(self.h, ctypes.byref(t), ctypes.byref(params)))
+            return
         t = make_table(cols)
         check(lib().st_transform(self.h, ctypes.byref(t), ctypes.byref(params)))
 
@@ -572,6 +580,12 @@ class Context:
     def morton_order(self, x, y, z, indices=None):
         n = len(x)
         idx = np.arange(n, dtype=np.uint32) if indices is None else np.ascontiguousarray(indices, np.uint32).copy()
+        if any(np.dtype(a.dtype) != np.float32 for a in (x, y, z)):  # ordering.ts reads any type's numbers
+            xyz = [np.ascontiguousarray(a) for a in (x, y, z)]
+            ptrs = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in xyz])
+            types = (ctypes.c_int32 * 3)(*[ply_type_of(a) for a in xyz])
+            check(lib().st_morton_order_t(self.h, ptrs, types, _vp(idx), ctypes.c_uint64(n)))
+            return idx
         check(lib().st_morton_order(self.h, _vp(x), _vp(y), _vp(z), _vp(idx), ctypes.c_uint64(n)))
         return idx
 
@@ -629,6 +643,42 @@ class Context:
         if C:
             res['shN_centroids'] = tex['shN_centroids'].reshape(ch, cw, 4)
         return res, meta, used.value
+
+    def sog_process(self, cols, actions, iters, draws):
+        """processDataTable then writeSog's textures + meta on a host table of any column types
+        (list of (name, array) or dict): (textures, meta, draws used) as sog()"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        names = [k for k, _ in items]
+        first_missing = next((i for i in range(45) if f'f_rest_{i}' not in names), -1)
+        C = {9: 3, 24: 8, -1: 15}.get(first_missing, 0)
+        t = make_ttable(items)
+        tex, out, _ = _sog_out(t.n, C)
+        meta = SogMeta()
+        used = ctypes.c_uint64(0)
+        acts = make_actions(actions)
+        check(lib().st_sog_process(self.h, ctypes.byref(t), acts, ctypes.c_int32(len(actions)), ctypes.c_int32(iters),
+                                   _vp(draws), ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                                   ctypes.byref(out)))
+        W, H, cw, ch = meta.width, meta.height, meta.shn_width, meta.shn_height
+        res = {k: v[:W * H * 4].reshape(H, W, 4) for k, v in tex.items() if k != 'shN_centroids'}
+        if meta.sh_bands:
+            res['shN_centroids'] = tex['shN_centroids'][:cw * ch * 4].reshape(ch, cw, 4)
+        else:
+            res.pop('shN_labels', None)
+        return res, meta, used.value
+
+    def sog_bundle_process(self, cols, actions, iters, draws, dos_time, dos_date):
+        """processDataTable then writeSog to a .sog bundle, any column types: (archive, draws used)"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        t = make_ttable(items)
+        acts = make_actions(actions)
+        used = ctypes.c_uint64(0)
+        out, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+        check(lib().st_sog_bundle_process(self.h, ctypes.byref(t), acts, ctypes.c_int32(len(actions)),
+                                          ctypes.c_int32(iters), _vp(draws), ctypes.c_uint64(len(draws)),
+                                          ctypes.byref(used), ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date),
+                                          ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size), used.value
 
     def webp_lossless(self, rgba):
         """WebPEncodeLosslessRGBA of a host (H, W, 4) uint8 array -> .webp bytes"""
@@ -786,7 +836,7 @@ class Context:
         region = actions[:first]
         rs = process_schema(items, region, with_source=True)
         if any(a['kind'] in TRANSFORM_KINDS for a in region):
-            for (_, a), (_, src) in zip(self._process(items, region), rs):
+            for (_, a), (_, _, src) in zip(self._process(items, region), rs):
                 np.copyto(items[src][1], a)
         if first == len(actions):
             return [(k, items[src][1]) for k, _, src in rs]

@@ -449,6 +449,93 @@ cases.sog = async () => {
     fx.save();
 };
 
+// Tables whose columns are not float32 -- a PLY with `double` properties, and integer ones:
+// the reference reads every column through getRow as numbers and stores through setRow
+// (data-table.ts:63-76), so transform, ordering, the compressed-PLY writer and writeSog take
+// them.  Per case: processDataTable + writeCompressedPly (as process_chain: input, processed
+// table, the input afterwards, the four writes) and writeSog of the input (textures + meta).
+cases.typed_columns = async () => {
+    const fx = new Fixture('typed_columns');
+    // values in each column's own type: float64 columns hold unrounded numbers, integer columns
+    // the truncated (scaled) values a TypedArray store keeps
+    const makeTyped = (n, shCoeffs, seed, typeOf, scaleOf, cubeFrac) => {
+        const g = new Gen(seed);
+        const names = gsColumnNames(shCoeffs);
+        const cols = {};
+        names.forEach((nm) => { cols[nm] = new (typeOf(nm))(n); });
+        const put = (nm, i, v) => { cols[nm][i] = v * scaleOf(nm); };
+        for (let i = 0; i < n; ++i) {
+            if (g.u() < cubeFrac) {
+                put('x', i, 1 + g.uniform(0, 1e-3)); put('y', i, -2 + g.uniform(0, 1e-3)); put('z', i, 3 + g.uniform(0, 1e-3));
+            } else {
+                put('x', i, g.normal(0, 10)); put('y', i, g.normal(0, 10)); put('z', i, g.normal(0, 10));
+            }
+            for (let c = 0; c < 3; ++c) put(`f_dc_${c}`, i, g.normal(0, 1));
+            for (let c = 0; c < shCoeffs * 3; ++c) put(`f_rest_${c}`, i, g.normal(0, 0.1));
+            put('opacity', i, g.normal(0, 2));
+            for (let c = 0; c < 3; ++c) put(`scale_${c}`, i, g.uniform(-7, -2));
+            for (let c = 0; c < 4; ++c) put(`rot_${c}`, i, g.normal(0, 1));
+        }
+        return { names, cols };
+    };
+    const V = (x, y, z) => new pc.Vec3(x, y, z);
+    const mixedType = (nm) => ({ x: Float64Array, y: Int16Array, z: Int32Array, rot_0: Float64Array, opacity: Float64Array,
+        scale_0: Int8Array, scale_1: Int8Array, scale_2: Float64Array, f_dc_2: Uint16Array, f_rest_1: Float64Array,
+        f_rest_4: Float64Array, f_rest_7: Uint8Array, f_rest_8: Int8Array }[nm] || Float32Array);
+    const mixedScale = (nm) => ({ y: 100, z: 1000, f_dc_2: 1000, f_rest_7: 300, f_rest_8: 300 }[nm] || 1);
+    const specs = [
+        ['f64', () => makeTyped(1500, 15, 951, () => Float64Array, () => 1, 0.2),
+            [{ kind: 'rotate', value: V(0, 45, 0) }, { kind: 'filterNaN' }], 2500],
+        ['mixed', () => makeTyped(1400, 3, 952, mixedType, mixedScale, 0.25),
+            [{ kind: 'translate', value: V(1.5, -2.25, 3) }, { kind: 'scale', value: 2 }, { kind: 'filterNaN' }], 2500],
+        ['f64_sh1_bands', () => makeTyped(1900, 8, 953, () => Float64Array, () => 1, 0.0),
+            [{ kind: 'filterBands', value: 1 }, { kind: 'rotate', value: V(30, -60, 10) },
+                { kind: 'filterByValue', columnName: 'opacity', comparator: 'gt', value: -1 }], 0],
+    ];
+    fx.meta.cases = specs.map(s => s[0]);
+    for (const [name, make, acts, sogN] of specs) {
+        const { names, cols } = make();
+        if (name === 'f64') { cols.x[10] = NaN; cols.f_rest_40[11] = Infinity; cols.rot_2[12] = -Infinity; }
+        const table = toTable(names, cols);
+        fx.meta[`${name}_actions`] = acts.map(a => (a.value && a.value.x !== undefined)
+            ? Object.assign({}, a, { value: [a.value.x, a.value.y, a.value.z] }) : a);
+        fx.meta[`${name}_in_types`] = table.columns.map(c => c.dataType);
+        addTable(fx, `${name}_in_`, table);
+        const out = processDataTable(table, acts);
+        fx.meta[`${name}_out_types`] = out.columns.map(c => c.dataType);
+        addTable(fx, `${name}_out_`, out);
+        addTable(fx, `${name}_after_`, table);
+        const { writes, handle } = captureHandle();
+        await quiet(() => writeCompressedPly(handle, out));
+        const u8 = (b) => new Uint8Array(b.buffer.slice(b.byteOffset, b.byteOffset + b.length));
+        fx.add(`${name}_header`, u8(writes[0]));
+        fx.add(`${name}_chunk`, new Float32Array(u8(writes[1]).buffer));
+        fx.add(`${name}_vertex`, new Uint32Array(u8(writes[2]).buffer));
+        fx.add(`${name}_sh`, u8(writes[3]));
+        if (!sogN) continue;
+        // writeSog of a fresh table of the same types (sogN rows; iters 2)
+        const st = make === specs[0][1] ? makeTyped(sogN, 15, 961, () => Float64Array, () => 1, 0.05)
+            : makeTyped(sogN, 3, 962, mixedType, mixedScale, 0.05);
+        const stable = toTable(st.names, st.cols);
+        addTable(fx, `${name}_sog_in_`, stable);
+        fx.meta[`${name}_sog_in_types`] = stable.columns.map(c => c.dataType);
+        const dir = fs.mkdtempSync('/tmp/st_sogt_');
+        const metaPath = path.join(dir, 'meta.json');
+        const fh = await fs.promises.open(metaPath, 'w');
+        seedRandom(970 + sogN);
+        await quiet(() => writeSog(fh, stable, metaPath, 2, 'cpu'));
+        await fh.close();
+        const meta = JSON.parse(fs.readFileSync(metaPath, 'utf8'));
+        fx.meta[`${name}_sog`] = { n: sogN, iters: 2, seed: 970 + sogN, draws: drawCount, meta };
+        ['means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels'].forEach((f) => {
+            const t = readRGBA(path.join(dir, `${f}.webp`));
+            fx.add(`${name}_sog_${f}`, t.data, [t.h, t.w, 4]);
+        });
+        fs.rmSync ? fs.rmSync(dir, { recursive: true }) : fs.rmdirSync(dir, { recursive: true });
+    }
+    fx.save();
+};
+
 // .sog bundle (write-sog.ts:110-140,361-366 + serialize/zip-writer.ts + crc.ts): the
 // whole ZIP with a pinned clock, so the container layout, the CRC-32 of every entry
 // and the raw meta.json text are fixed.  Entries hold the identity WebP stand-in's

@@ -1,7 +1,7 @@
 'use strict';
 // Node host: filterNaN / combine / transform's column-type rule on the reference's own vectors
 // (tests/golden/filter_combine.*).  Prints one JSON object of check results.
-//   node table_ops.js combine|filter|transform_f64
+//   node table_ops.js combine|filter|devices
 const fs = require('fs');
 const path = require('path');
 
@@ -40,16 +40,6 @@ if (what === 'combine') {
     const splats = new host.DataTable(man.meta.in_columns.map(n => new host.Column(n, arr(`in_${n}`))));
     const res2 = host.filterNaN(splats);
     out.same2 = res2.columns.map(c => sameBytes(c.data, arr(`out_${c.name}`)));
-} else if (what === 'transform_f64') {
-    const t = new host.DataTable([new host.Column('x', new Float64Array(4)), new host.Column('y', new Float32Array(4)),
-        new host.Column('z', new Float32Array(4))]);
-    try {
-        host.transform(t, { x: 1, y: 0, z: 0 }, { x: 0, y: 0, z: 0, w: 1 }, 1);
-        out.threw = false;
-    } catch (e) {
-        out.threw = true;
-        out.message = e.message;
-    }
 } else if (what === 'devices') {
     out.before = host.getDevices();
     host.setDevices(1);

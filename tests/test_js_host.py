@@ -40,7 +40,8 @@ def test_addon_exports(addon_built):
     assert json.loads(keys) == sorted(['version', 'deviceCount', 'quatFromEuler', 'transform', 'filterFinite',
                                        'filterNaN', 'combineLayout', 'setDevices', 'getDevices', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
-                                       'process', 'compressedPlyFromFile', 'sogBundleFromFile'])
+                                       'process', 'compressedPlyFromFile', 'sogBundleFromFile',
+                                       'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped'])
     assert ver == '1'
 
 
@@ -78,9 +79,18 @@ def test_js_combine_matches_reference(addon_built):
     assert all(out['same']) and all(out['same3']), out
 
 
-def test_js_transform_rejects_non_f32(addon_built):
-    out = _table_ops('transform_f64')
-    assert out['threw'] and "'x' is Float64Array" in out['message'], out
+@pytest.mark.gpu
+def test_js_typed_columns_match_reference(addon_built):
+    """columns that are not float32 through the Node host (processDataTable, writeCompressedPly,
+    transform, writeSog's textures / meta / draws) against the reference's own outputs
+    (tests/golden/typed_columns.*)"""
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'typed_columns.js')], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout)
+    assert out.pop('transform_f64') is True
+    bad = {c: v for c, v in out.items() if not all(v.values())}
+    assert not bad, bad
 
 
 @pytest.mark.gpu

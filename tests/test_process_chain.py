@@ -161,11 +161,12 @@ def test_process_typed_filter_by_value_vs_oracle(ctx):
 
 @pytest.mark.gpu
 def test_chain_errors(ctx):
+    """the reference's own failures only: a bad filterBands value and a missing chunk member (its
+    other column types are accepted, tests/test_typed_columns.py)"""
     src, acts, _ = _case(G, 'config3')
-    typed = [(k, a.astype(np.float64) if k == 'rot_1' else a) for k, a in src]
     with pytest.raises(sh.StError) as e:
-        ctx.compressed_ply(typed, acts)
-    assert e.value.code == -6  # ST_ERR_UNSUPPORTED: transform reads float32 columns
+        ctx.compressed_ply([(k, a) for k, a in src if k != 'opacity'], [])
+    assert e.value.code == sh.ST_ERR_ARG and 'opacity' in str(e.value)
     with pytest.raises(sh.StError) as e:
         ctx.compressed_ply(src, [{'kind': 'filterBands', 'value': 4}])
     assert e.value.code == sh.ST_ERR_ARG
