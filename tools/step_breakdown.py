@@ -35,7 +35,7 @@ def main():
             mt[name] += dur / 1e6
             mc[name] += 1
     print(f'library kernels: {sum(tot.values()) / steps:.2f} ms per step')
-    for k, v in sorted(tot.items(), key=lambda x: -x[1])[:45]:
+    for k, v in sorted(tot.items(), key=lambda x: -x[1])[:70]:
         print(f'{v / steps:9.3f} ms {cnt[k] / steps:7.1f}x  {k}')
     for k, v in sorted(mt.items(), key=lambda x: -x[1])[:8]:
         print(f'copy {v / steps:9.3f} ms {mc[k] / steps:7.1f}x  {k}')
