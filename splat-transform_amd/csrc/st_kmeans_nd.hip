@@ -998,12 +998,20 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_sumnd(const T *__restrict__ aos, int d,
                                                const uint32_t *__restrict__ members,
                                                const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
-                                               uint32_t big) {
+                                               uint32_t big, uint32_t cap, uint32_t *__restrict__ big_list,
+                                               uint32_t *__restrict__ nbig) {
     const int lane = threadIdx.x & 63;
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    if (s0 == s1 || lane >= d || s1 - s0 > big) return;  // huge clusters: k_big_*
+    if (s1 - s0 > big) {  // huge clusters: listed for k_big_* (at most cap of them exist)
+        if (lane == 0) {
+            const uint32_t i = atomicAdd(nbig, 1u);
+            if (i < cap) big_list[i] = cl;
+        }
+        return;
+    }
+    if (s0 == s1 || lane >= d) return;
     const int ld = aos_ld(d);
     double sum = 0;
     uint32_t j = s0;
@@ -1027,29 +1035,18 @@ __global__ __launch_bounds__(256) void k_sumnd(const T *__restrict__ aos, int d,
 // sequential result, otherwise one lane runs the sequential chain over the whole cluster.
 constexpr uint32_t SB_SLICE = 4096;
 
-// one workgroup: the clusters above `big` and the running count of their slices
-__global__ __launch_bounds__(1024) void k_big_list(const uint32_t *__restrict__ start, int k, uint32_t big,
-                                                   uint32_t cap, uint32_t *__restrict__ list,
-                                                   uint32_t *__restrict__ soff, uint32_t *__restrict__ nlist) {
-    __shared__ uint32_t cnt;
-    if (threadIdx.x == 0) cnt = 0;
-    __syncthreads();
-    for (uint32_t c0 = threadIdx.x; c0 < (uint32_t)k; c0 += 1024)
-        if (start[c0 + 1] - start[c0] > big) {
-            const uint32_t i = atomicAdd(&cnt, 1u);
-            if (i < cap) list[i] = c0;
-        }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t m = min(cnt, cap);  // cap = n / (big + 1) + 1 clusters can exceed big
-        uint32_t o = 0;
-        for (uint32_t i = 0; i < m; ++i) {
-            soff[i] = o;
-            o += (start[list[i] + 1] - start[list[i]] + SB_SLICE - 1) / SB_SLICE;
-        }
-        soff[m] = o;
-        *nlist = m;
+// the listed clusters' running slice counts (one thread: the list is short, usually empty)
+__global__ void k_big_prefix(const uint32_t *__restrict__ start, uint32_t cap, const uint32_t *__restrict__ list,
+                             uint32_t *__restrict__ soff, uint32_t *__restrict__ nlist) {
+    if (threadIdx.x != 0) return;
+    const uint32_t m = min(*nlist, cap);  // cap = n / (big + 1) + 1 clusters can exceed big
+    uint32_t o = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        soff[i] = o;
+        o += (start[list[i] + 1] - start[list[i]] + SB_SLICE - 1) / SB_SLICE;
     }
+    soff[m] = o;
+    *nlist = m;
 }
 
 // slice s of the listed clusters: 4 waves, lane = dimension; (sum, sum|x|, min ulp exponent)
@@ -1164,17 +1161,19 @@ template <typename T>
 void launch_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32_t *members, const uint32_t *start,
                  float *cen) {
     const uint32_t big = sumnd_big();
-    hipLaunchKernelGGL(k_sumnd<T>, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen, big);
+    const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
+    auto *list = wsT<uint32_t>(c, "kn.blist", cap);
+    auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
+    ST_HIP(hipMemsetAsync(nlist, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_sumnd<T>, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen, big,
+                       cap, list, nlist);
     if (n > big) {
-        const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
         const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
-        auto *list = wsT<uint32_t>(c, "kn.blist", cap);
         auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
-        auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
         auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
         auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
         auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
-        hipLaunchKernelGGL(k_big_list, dim3(1), dim3(1024), 0, c->stream, start, k, big, cap, list, soff, nlist);
+        hipLaunchKernelGGL(k_big_prefix, dim3(1), dim3(64), 0, c->stream, start, cap, list, soff, nlist);
         hipLaunchKernelGGL(k_big_partial<T>, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d, members,
                            start, list, soff, nlist, psum, pabs, pemin);
         hipLaunchKernelGGL(k_big_final<T>, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d,
