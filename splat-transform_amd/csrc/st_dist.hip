@@ -206,6 +206,19 @@ void dist_assign(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, 
     nd_assign(c, dcols, d, n, k, cen, labels, dstate);
 }
 
+void dist_assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k, const float *cen,
+                            uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
+    ST_REQUIRE(n < (1ull << 31) && (uint64_t)nseg * k < (1ull << 31), ST_ERR_ARG, "kmeans partials: too large");
+    assign_partials1d(c, pts, n, nseg, k, cen, labels, sums, sabs, emin, counts);
+    c->ds_nseg = nseg;
+    c->ds_k = k;
+    c->ds_d = 1;
+    c->ds_n = n;
+    c->ds_pts = pts;
+    c->ds_labels = labels;
+    c->ds_sorted = false;
+}
+
 void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
                    double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
     ST_REQUIRE(nseg >= 1 && n % (uint64_t)nseg == 0, ST_ERR_ARG, "kmeans partials: n must split into nseg segments");
@@ -240,6 +253,7 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
     c->ds_k = k;
     c->ds_d = d;
     c->ds_n = n;
+    c->ds_sorted = true;
 }
 
 void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running,
@@ -251,6 +265,10 @@ void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32
     auto *payload = wsT<uint32_t>(c, "ds.payload", n);
     auto *start = wsT<uint32_t>(c, "ds.start", nk + 1);
     if (d == 1) {
+        if (!c->ds_sorted) {  // partials came from the accumulating assign: order the members now
+            seg_label_sort1d(c, c->ds_pts, c->ds_labels, n, c->ds_nseg, k, payload, start);
+            c->ds_sorted = true;
+        }
         auto *flag = wsT<uint32_t>(c, "ds.sflag", npairs);
         seqsum1d(c, payload, n, start + (uint64_t)seg * k, k, pairs, npairs, running, emin, sabs, flag);
         hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, flag,

@@ -94,6 +94,11 @@ struct st_ctx {
     // the last st_dev_kmeans_partials call (member lists kept for st_dev_kmeans_seqsum)
     int ds_nseg = 0, ds_k = 0, ds_d = 0;
     uint64_t ds_n = 0;
+    // 1-D partials taken without the member sort (dist_assign_partials1d): the (segment,
+    // label) order is built from these only if a pending chain needs it
+    const float *ds_pts = nullptr;
+    const uint32_t *ds_labels = nullptr;
+    bool ds_sorted = true;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     st::Workspace ws;
@@ -277,6 +282,9 @@ void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const 
 void minmax_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, double *lo, double *hi);
 void dist_prepare(st_ctx *c, const float *const *cols, int d, uint64_t n);
 void dist_assign(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen, uint32_t *labels);
+// dist_assign + dist_partials of a 1-D point set with k <= 256 in one pass (no member sort)
+void dist_assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k, const float *cen,
+                            uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts);
 void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
                    double *sums, double *sabs, int32_t *emin, uint32_t *counts);
 void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32_t npairs, double *running,

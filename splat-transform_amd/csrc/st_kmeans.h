@@ -81,6 +81,10 @@ void seg_label_sort1d(st_ctx *c, const float *pts, const uint32_t *labels, uint6
                       uint32_t *vals, uint32_t *start);
 void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int nk, double *sums, double *sabs,
                 int32_t *emin, uint32_t *counts);
+// the labels and the same partials straight from the accumulating assign, segment by segment
+// (n = nseg equal segments, k <= 256)
+void assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k, const float *cen, uint32_t *labels,
+                       double *sums, double *sabs, int32_t *emin, uint32_t *counts);
 void seqsum1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int k, const uint32_t *pairs,
               uint32_t npairs, double *running, const int32_t *emin, const double *sabs, uint32_t *pflag);
 // throws ST_ERR_NONFINITE on a non-finite value; also leaves max |x| in c->km_absmax

@@ -518,8 +518,8 @@ __global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ v
 // few (256) and uneven (the one straddling 0 can hold 1.5% of 30M points), so a
 // per-cluster workgroup leaves the chip idle behind the largest cluster.
 constexpr uint32_t SC_CH = 4096;  // members per chunk
+constexpr uint32_t FL_CH = 512;   // members per chunk of the flagged clusters' replay
 constexpr int SC_T = 256;         // threads per chunk (16 members each)
-constexpr int SC_PER = SC_CH / SC_T;
 
 struct Chunk {
     uint32_t cl, begin, end, pad;
@@ -690,37 +690,45 @@ __global__ __launch_bounds__(SC_T) void k_rp_sums(const uint32_t *__restrict__ v
     if (threadIdx.x == 0) csum[blockIdx.x] = tot;
 }
 
-// B / D: one thread per flagged cluster walks its chunks in order (exclusive prefixes)
-__global__ __launch_bounds__(256) void k_rp_prefix(const uint32_t *__restrict__ first, int k,
+// B / D: one workgroup per flagged cluster scans its chunks in order (exclusive prefixes)
+__global__ __launch_bounds__(SC_T) void k_rp_prefix(const uint32_t *__restrict__ first, int k,
                                                    uint32_t *__restrict__ seq_flag, const double *__restrict__ sabs_c,
                                                    const int32_t *__restrict__ emin_c, __int128 *__restrict__ csum,
                                                    __int128 *__restrict__ total, const double *__restrict__ base) {
-    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
-        if (seq_flag[cl] != 1u) continue;
-        if (!(rp_bound(sabs_c, base, cl) * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin_c[cl] + 118))) {  // int128 range
-            seq_flag[cl] = 2u;
-            continue;
-        }
-        __int128 run = 0;
-        for (uint32_t c = first[cl]; c < first[cl + 1]; ++c) {
-            const __int128 v = csum[c];
-            csum[c] = run;  // in place: exclusive prefix of the chunk
-            run += v;
-        }
-        total[cl] = run;
+    const int cl = blockIdx.x;
+    if (cl >= k || seq_flag[cl] != 1u) return;  // uniform per workgroup
+    __syncthreads();  // every thread has read the flag before thread 0 may change it
+    if (!(rp_bound(sabs_c, base, cl) * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, emin_c[cl] + 118))) {  // int128 range
+        if (threadIdx.x == 0) seq_flag[cl] = 2u;
+        return;
     }
+    __int128 run = 0;
+    for (uint32_t c0 = first[cl]; c0 < first[cl + 1]; c0 += SC_T) {
+        const uint32_t c = c0 + threadIdx.x;
+        const __int128 v = c < first[cl + 1] ? csum[c] : (__int128)0;
+        __int128 tot;
+        const __int128 ex = sc_exscan_i128(v, &tot);
+        if (c < first[cl + 1]) csum[c] = run + ex;  // in place: exclusive prefix of the chunk
+        run += tot;
+    }
+    if (threadIdx.x == 0) total[cl] = run;
 }
-__global__ __launch_bounds__(256) void k_rp_cprefix(const uint32_t *__restrict__ first, int k,
+__global__ __launch_bounds__(SC_T) void k_rp_cprefix(const uint32_t *__restrict__ first, int k,
                                                     uint32_t *__restrict__ seq_flag, const uint32_t *__restrict__ ccnt,
                                                     uint32_t *__restrict__ cof, uint32_t *__restrict__ ctot,
                                                     uint32_t cap) {
-    for (int cl = blockIdx.x * blockDim.x + threadIdx.x; cl < k; cl += gridDim.x * blockDim.x) {
-        if (seq_flag[cl] != 1u) continue;
-        uint32_t run = 0;
-        for (uint32_t c = first[cl]; c < first[cl + 1]; ++c) {
-            cof[c] = run;
-            run += ccnt[c];
-        }
+    const int cl = blockIdx.x;
+    if (cl >= k || seq_flag[cl] != 1u) return;  // uniform per workgroup
+    uint32_t run = 0;
+    for (uint32_t c0 = first[cl]; c0 < first[cl + 1]; c0 += SC_T) {
+        const uint32_t c = c0 + threadIdx.x;
+        const uint32_t v = c < first[cl + 1] ? ccnt[c] : 0u;
+        uint32_t tot;
+        const uint32_t ex = sc_exscan_u32(v, &tot);
+        if (c < first[cl + 1]) cof[c] = run + ex;
+        run += tot;
+    }
+    if (threadIdx.x == 0) {
         ctot[cl] = run;
         if (run > cap) seq_flag[cl] = 2u;  // the sequential chain
     }
@@ -741,7 +749,8 @@ __global__ __launch_bounds__(SC_T) void k_rp_cands(const uint32_t *__restrict__ 
     const int e_lo = emin_c[ch.cl];
     const __int128 margin = rp_margin(rp_bound(sabs_c, base, ch.cl), e_lo);
     // this thread's contiguous slice of the chunk
-    const uint32_t a = min(ch.end, ch.begin + threadIdx.x * SC_PER), b = min(ch.end, a + SC_PER);
+    const uint32_t per = (ch.end - ch.begin + SC_T - 1) / SC_T;
+    const uint32_t a = min(ch.end, ch.begin + threadIdx.x * per), b = min(ch.end, a + per);
     __int128 local = 0;
     for (uint32_t j = a; j < b; ++j) local += f32_units(vals[j], e_lo);
     __int128 tot;
@@ -836,14 +845,13 @@ void chunked_replay(st_ctx *c, const uint32_t *vals, const uint32_t *start, int 
                     const uint32_t *ch_first, uint32_t *seq_flag, const int32_t *emin_c, const double *sabs_c,
                     __int128 *csum, __int128 *total, uint32_t *ccnt, uint32_t *cof, uint32_t *ctot, __int128 *cands,
                     float *cen, const double *base, double *sum_out) {
-    const unsigned gk = grid_for((uint64_t)k, 256, 1024);
     hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag, emin_c,
                        csum);
-    hipLaunchKernelGGL(k_rp_prefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, sabs_c, emin_c, csum,
+    hipLaunchKernelGGL(k_rp_prefix, dim3(k), dim3(SC_T), 0, c->stream, ch_first, k, seq_flag, sabs_c, emin_c, csum,
                        total, base);
     hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
                        emin_c, sabs_c, csum, ccnt, cands, base);
-    hipLaunchKernelGGL(k_rp_cprefix, dim3(gk), dim3(256), 0, c->stream, ch_first, k, seq_flag, ccnt, cof, ctot,
+    hipLaunchKernelGGL(k_rp_cprefix, dim3(k), dim3(SC_T), 0, c->stream, ch_first, k, seq_flag, ccnt, cof, ctot,
                        replay_cap());
     hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
                        emin_c, sabs_c, csum, cof, cands, base);
@@ -857,7 +865,7 @@ void chunked_replay(st_ctx *c, const uint32_t *vals, const uint32_t *start, int 
 constexpr int CL_T = 1024, CL_MAX = 4096;
 __global__ __launch_bounds__(CL_T) void k_chunk_list_small(const uint32_t *__restrict__ start, int k,
                                                            uint32_t *__restrict__ first, Chunk *__restrict__ chunks,
-                                                           SumAcc *acc) {
+                                                           SumAcc *acc, uint32_t chsz) {
     constexpr int PER = CL_MAX / CL_T;
     __shared__ uint32_t wsum[CL_T / 64];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -865,7 +873,7 @@ __global__ __launch_bounds__(CL_T) void k_chunk_list_small(const uint32_t *__res
 #pragma unroll
     for (int u = 0; u < PER; ++u) {  // thread t owns clusters t*PER .. t*PER+PER-1
         const int cl = t * PER + u;
-        cnt[u] = cl < k ? (start[cl + 1] - start[cl] + SC_CH - 1) / SC_CH : 0u;
+        cnt[u] = cl < k ? (start[cl + 1] - start[cl] + chsz - 1) / chsz : 0u;
         mine += cnt[u];
         if (acc && cl < k) acc[cl] = SumAcc{0.0, 0.0, 1 << 20, 0};
     }
@@ -909,17 +917,18 @@ __global__ __launch_bounds__(CL_T) void k_chunk_list_small(const uint32_t *__res
             if (soff[mid] <= q) lo = mid;
             else hi = mid;
         }
-        const uint32_t b = sst[lo] + (q - soff[lo]) * SC_CH;
-        chunks[q] = Chunk{lo, b, min(sst[lo + 1], b + SC_CH), 0u};
+        const uint32_t b = sst[lo] + (q - soff[lo]) * chsz;
+        chunks[q] = Chunk{lo, b, min(sst[lo + 1], b + chsz), 0u};
     }
 }
 
 // the chunk list of every cluster's member range (k clusters, start[k + 1]); acc (nullable):
 // the per-cluster accumulators to reset
 void chunk_list(st_ctx *c, const uint32_t *start, int k, uint32_t *ch_cnt, uint32_t *ch_first, Chunk *chunks,
-                SumAcc *acc = nullptr) {
+                SumAcc *acc = nullptr, uint32_t chsz = SC_CH) {
     if (k <= CL_MAX) {
-        hipLaunchKernelGGL(k_chunk_list_small, dim3(1), dim3(CL_T), 0, c->stream, start, k, ch_first, chunks, acc);
+        hipLaunchKernelGGL(k_chunk_list_small, dim3(1), dim3(CL_T), 0, c->stream, start, k, ch_first, chunks, acc,
+                           chsz);
         ST_LAUNCH_CHECK();
         return;
     }
@@ -960,6 +969,525 @@ __global__ __launch_bounds__(256) void k_pend_out(const uint32_t *__restrict__ p
         const uint32_t f = flag_cl[pairs[p]];
         if (f == 0u) running[p] = sum_cl[pairs[p]];
         pflag[p] = f == 2u ? 1u : 0u;
+    }
+}
+
+// ---- sort-free iteration for k <= 256 (cluster1d's codebooks) --------------------------
+// Under the certificate every partial sum of a cluster is exact, so the members' order only
+// matters for the clusters that fail it.  The assign therefore accumulates each cluster's
+// count, sum, sum|x| and smallest ulp exponent in LDS while it labels the points (one partial
+// per workgroup), and one launch reduces the partials, certifies, scans the cluster starts
+// and re-seeds the empty clusters.  Only when a cluster fails the certificate are its members
+// laid out in point order -- from the byte labels, moving that cluster's values only -- for
+// the chunked replay above.  Two launches and one 8-byte read-back per iteration instead of
+// the member sort's ~20 launches.
+struct Part1 {
+    double sum, sabs;
+    int32_t emin;
+    uint32_t cnt;
+};
+constexpr uint32_t A1_G = 1024;  // most workgroups (partials) of the accumulating assign
+
+// workgroups for ntiles tiles: at most A1_G, every workgroup the same number of tiles
+uint32_t a1_grid(uint32_t ntiles) {
+    const uint32_t per = (ntiles + A1_G - 1) / A1_G;
+    return (ntiles + per - 1) / per;
+}
+
+// k_kd1_assign_hist's bracket assign with the centroid order built in the workgroup (the
+// stable sort of KdTree's build is a rank by (sort key, index)), over the tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ...; part[blockIdx.x * 256 + c] = cluster c's partial
+__global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict__ pts, uint64_t n,
+                                                        const float *__restrict__ cen, int k,
+                                                        uint32_t *__restrict__ labels, uint8_t *__restrict__ lab8,
+                                                        uint32_t ntiles, Part1 *__restrict__ part) {
+    __shared__ float sv[256];
+    __shared__ uint32_t si[256], skey[256];
+    __shared__ uint16_t cc[256];
+    __shared__ uint32_t first[KD1_CELLS + 1];
+    __shared__ double hs[256], ha[256];
+    __shared__ int32_t he[256];
+    __shared__ uint32_t hc[256];
+    const int t = threadIdx.x;
+    const float mine = t < k ? cen[t] : 0.f;
+    const uint32_t key = t < k ? sortkey_(mine) : 0u;
+    skey[t] = key;
+    hs[t] = 0.0;
+    ha[t] = 0.0;
+    he[t] = 1 << 20;
+    hc[t] = 0u;
+    __syncthreads();
+    if (t < k) {
+        uint32_t r = 0;
+        for (int j = 0; j < k; ++j) {
+            const uint32_t kj = skey[j];
+            r += (kj < key || (kj == key && j < t)) ? 1u : 0u;
+        }
+        sv[r] = mine;
+        si[r] = (uint32_t)t;
+    }
+    __syncthreads();
+    const float lo = sv[0], hi = sv[k - 1];
+    const float span = hi - lo;
+    const float inv = (span > 0.f && span < __builtin_inff()) ? (float)KD1_CELLS / span : 0.f;
+    auto cell = [&](float x) -> int {
+        const float u = (x - lo) * inv;
+        return (int)__builtin_fminf(__builtin_fmaxf(u, 0.f), (float)(KD1_CELLS - 1));
+    };
+    if (t < k) cc[t] = (uint16_t)cell(sv[t]);
+    __syncthreads();
+    for (int g = t; g <= KD1_CELLS; g += F1_T) {
+        int a = 0, b = k;
+        while (a < b) {
+            const int m = (a + b) >> 1;
+            if ((int)cc[m] < g) a = m + 1;
+            else b = m;
+        }
+        first[g] = (uint32_t)a;
+    }
+    __syncthreads();
+    auto dist = [&](int pos, double p) {
+        const double v = (double)sv[pos] - p;
+        return 0.0 + v * v;
+    };
+    auto val = [&](uint32_t pos) -> float { return sv[pos]; };
+    auto idx = [&](uint32_t pos) -> uint32_t { return si[pos]; };
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t base = (uint64_t)tile * F1_TILE;
+        float pv[F1_ROWS];
+#pragma unroll
+        for (int r = 0; r < F1_ROWS; ++r) {
+            const uint64_t i = base + (uint64_t)r * F1_T + t;
+            pv[r] = i < n ? pts[i] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < F1_ROWS; ++r) {
+            const uint64_t i = base + (uint64_t)r * F1_T + t;
+            if (i >= n) break;
+            const float pf = pv[r];
+            const double p = pf;
+            const int g = cell(pf);
+            int u = (int)first[g];
+            const int ue = (int)first[g + 1];
+            while (u < ue && sv[u] <= pf) ++u;
+            const int L = u - 1, R = u;
+            const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
+            const double dr = R < k ? dist(R, p) : __builtin_inf();
+            const double m = __builtin_fmin(dl, dr);
+            const bool tie = dl == dr || (L >= 1 && dist(L - 1, p) == m) || (R + 1 < k && dist(R + 1, p) == m);
+            const uint32_t lab = !tie ? si[dl < dr ? L : R] : kd1_walk(p, k, val, idx);
+            if (lab8) lab8[i] = (uint8_t)lab;
+            if (labels) labels[i] = lab;
+            atomicAdd(&hc[lab], 1u);
+            atomicAdd(&hs[lab], p);
+            atomicAdd(&ha[lab], __builtin_fabs(p));
+            if (pf != 0.0f) atomicMin(&he[lab], ulp_exp(pf));
+        }
+    }
+    __syncthreads();
+    part[(uint64_t)t * gridDim.x + blockIdx.x] = Part1{hs[t], ha[t], he[t], hc[t]};  // cluster-major
+}
+
+// one workgroup per cluster reduces its G partials: the count, and the centroid when the
+// certificate holds (seq_flag 0) or flag 1 for the replay.  The last workgroup to finish then
+// scans the cluster starts (start: every member, fstart: the flagged clusters' members only,
+// the replay's compact layout), re-seeds the empty clusters as k_reseed_small does, and
+// leaves {flagged clusters, their members} in info.
+__global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ part, uint32_t G, int k, uint64_t n,
+                                                   float *cen, uint32_t *seq_flag, int32_t *__restrict__ emin_c,
+                                                   double *__restrict__ sabs_c, uint32_t *cnt_c,
+                                                   uint32_t *__restrict__ start, uint32_t *__restrict__ fstart,
+                                                   uint32_t *ticket, uint32_t *__restrict__ info,
+                                                   const float *const *cols, const double *__restrict__ draws,
+                                                   uint64_t ndraws, State *st) {
+    const int cl = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    double s = 0, a = 0;
+    int e = 1 << 20;
+    uint32_t c = 0;
+    for (uint32_t g = t; g < G; g += 256) {
+        const Part1 p = part[(uint64_t)cl * G + g];
+        s += p.sum;
+        a += p.sabs;
+        e = min(e, p.emin);
+        c += p.cnt;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        a += __shfl_xor(a, o, 64);
+        e = min(e, __shfl_xor(e, o, 64));
+        c += __shfl_xor(c, o, 64);
+    }
+    __shared__ double rs[4], ra[4];
+    __shared__ int re[4];
+    __shared__ uint32_t rc[4];
+    __shared__ bool last;
+    if (lane == 0) {
+        rs[w] = s;
+        ra[w] = a;
+        re[w] = e;
+        rc[w] = c;
+    }
+    __syncthreads();
+    if (t == 0) {
+        s = (rs[0] + rs[1]) + (rs[2] + rs[3]);  // exact whenever it is used (the certificate)
+        a = (ra[0] + ra[1]) + (ra[2] + ra[3]);
+        e = min(min(re[0], re[1]), min(re[2], re[3]));
+        c = (rc[0] + rc[1]) + (rc[2] + rc[3]);
+        uint32_t f = 0;
+        if (c) {
+            const bool exact = sum_is_exact(a, e);
+            f = exact ? 0u : 1u;
+            emin_c[cl] = e;
+            sabs_c[cl] = a;
+            if (exact) cen[cl] = (float)(s / (double)c);
+        }
+        __hip_atomic_store(&cnt_c[cl], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&seq_flag[cl], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const uint32_t cnt = t < k ? __hip_atomic_load(&cnt_c[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t fl = t < k ? __hip_atomic_load(&seq_flag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t tot, ftot, nempty, nflag;
+    const uint32_t off = sc_exscan_u32(cnt, &tot);
+    const uint32_t foff = sc_exscan_u32(fl ? cnt : 0u, &ftot);
+    const bool empty = t < k && cnt == 0;
+    const uint32_t rank = sc_exscan_u32(empty ? 1u : 0u, &nempty);
+    sc_exscan_u32(fl, &nflag);
+    if (t < k) {
+        start[t] = off;
+        fstart[t] = foff;
+    }
+    const uint64_t cursor = st->cursor;
+    if (empty) {  // k-means.ts:174-178, as k_reseed_small
+        const uint64_t di = cursor + rank;
+        if (di >= ndraws) {
+            atomicOr(&st->err, ERR_DRAWS);
+        } else {
+            const double dr = draws[di];
+            if (!(dr >= 0.0 && dr < 1.0))
+                atomicOr(&st->err, ERR_DRAW_RANGE);
+            else
+                cen[t] = cols[0][(uint64_t)__builtin_floor(dr * (double)n)];
+        }
+    }
+    __syncthreads();  // every thread has read st->cursor
+    if (t == 0) {
+        start[k] = (uint32_t)n;
+        fstart[k] = ftot;
+        st->cursor = cursor + nempty;
+        info[0] = nflag;
+        info[1] = ftot;
+        if (tot != (uint32_t)n) atomicOr(&st->err, ERR_INTERNAL);
+        *ticket = 0u;
+    }
+}
+
+// the multi-GPU update's partials: segment s's G workgroup partials -> (s, cluster) entries
+// of partials1d's layout (sums / sabs / emin / counts[s * k + c])
+__global__ __launch_bounds__(256) void k_part_fold(const Part1 *__restrict__ part, uint32_t G, int k,
+                                                   double *__restrict__ sums, double *__restrict__ sabs,
+                                                   int32_t *__restrict__ emin, uint32_t *__restrict__ counts) {
+    const uint32_t sc = blockIdx.x, seg = sc / (uint32_t)k, cl = sc % (uint32_t)k;
+    const Part1 *p = part + (uint64_t)seg * G * 256;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    double s = 0, a = 0;
+    int e = 1 << 20;
+    uint32_t c = 0;
+    for (uint32_t g = t; g < G; g += 256) {
+        const Part1 q = p[(uint64_t)cl * G + g];
+        s += q.sum;
+        a += q.sabs;
+        e = min(e, q.emin);
+        c += q.cnt;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        a += __shfl_xor(a, o, 64);
+        e = min(e, __shfl_xor(e, o, 64));
+        c += __shfl_xor(c, o, 64);
+    }
+    __shared__ double rs[4], ra[4];
+    __shared__ int re[4];
+    __shared__ uint32_t rc[4];
+    if (lane == 0) {
+        rs[w] = s;
+        ra[w] = a;
+        re[w] = e;
+        rc[w] = c;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    sums[sc] = (rs[0] + rs[1]) + (rs[2] + rs[3]);  // only used under the certificate
+    sabs[sc] = (ra[0] + ra[1]) + (ra[2] + ra[3]);
+    emin[sc] = min(min(re[0], re[1]), min(re[2], re[3]));
+    counts[sc] = (rc[0] + rc[1]) + (rc[2] + rc[3]);
+}
+
+// ---- the flagged clusters' members when there are few of them (the usual case: the one or
+// two clusters whose range holds values near zero).  A wave takes 1,024 consecutive points
+// (16 byte labels per lane, one 16-byte load); per flagged cluster it counts (k_ff_count) or
+// places (k_ff_scatter) that cluster's members with a wave prefix sum: no tile histogram.
+constexpr int FF_MAX = 8;        // flagged clusters the wave kernels take (more: the tile kernels)
+constexpr uint32_t FF_CH = 1024;  // points per wave chunk
+
+// the flagged clusters in ascending order into list (LDS), their count into *nl
+__device__ inline void ff_list(const uint32_t *__restrict__ seq_flag, int k, uint32_t *list, uint32_t *nl) {
+    __shared__ uint32_t wcnt[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const bool f = t < k && seq_flag[t] == 1u;
+    const uint64_t b = __ballot(f);
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t o = 0;
+    for (int i = 0; i < w; ++i) o += wcnt[i];
+    o += (uint32_t)__popcll(b & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    if (f && o < (uint32_t)FF_MAX) list[o] = (uint32_t)t;
+    if (t == 0) *nl = min(wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3], (uint32_t)FF_MAX);
+    __syncthreads();
+}
+
+// the lane's 16 byte labels of chunk ch (bytes past n read as `none`)
+__device__ inline uint4 ff_labels(const uint8_t *__restrict__ lab8, uint64_t n, uint32_t ch, int lane) {
+    const uint64_t p = (uint64_t)ch * FF_CH + (uint64_t)lane * 16;
+    if (p + 16 <= n) return *reinterpret_cast<const uint4 *>(lab8 + p);
+    uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    for (int i = 0; i < 16; ++i)
+        if (p + i < n) w[i >> 2] = (w[i >> 2] & ~(0xffu << (8 * (i & 3)))) | ((uint32_t)lab8[p + i] << (8 * (i & 3)));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// 0x80 in each byte of x equal to v (callers mask the bytes past n: ff_valid_mask)
+__device__ inline uint32_t ff_match(uint32_t x, uint32_t v) {
+    const uint32_t y = x ^ (v * 0x01010101u);
+    return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);  // exact zero-byte test
+}
+__device__ inline uint32_t ff_valid_mask(uint64_t n, uint32_t ch, int lane, int word) {
+    const uint64_t p = (uint64_t)ch * FF_CH + (uint64_t)lane * 16 + 4 * word;
+    if (p + 4 <= n) return 0x80808080u;
+    uint32_t m = 0;
+    for (int i = 0; i < 4; ++i)
+        if (p + i < n) m |= 0x80u << (8 * i);
+    return m;
+}
+
+__global__ __launch_bounds__(256) void k_ff_count(const uint8_t *__restrict__ lab8, uint64_t n, uint32_t nch, int k,
+                                                  const uint32_t *__restrict__ seq_flag, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t list[FF_MAX], nl;
+    ff_list(seq_flag, k, list, &nl);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t nf = nl;
+    for (uint32_t ch = blockIdx.x * 4 + w; ch < nch; ch += gridDim.x * 4) {
+        const uint4 L = ff_labels(lab8, n, ch, lane);
+        const uint32_t v[4] = {L.x, L.y, L.z, L.w};
+        for (uint32_t f = 0; f < nf; ++f) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c += __popc(ff_match(v[q], list[f]) & ff_valid_mask(n, ch, lane, q));
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            if (lane == 0) cnt[(uint64_t)f * nch + ch] = c;
+        }
+    }
+}
+
+// slot f's chunk counts -> the chunks' first positions in the compact layout (exclusive scan
+// from fstart of its cluster); one 1,024-thread workgroup per flagged slot, each thread a
+// contiguous run of the counts
+constexpr int FS_T = 1024;
+__global__ __launch_bounds__(FS_T) void k_ff_scan(uint32_t *__restrict__ cnt, uint32_t nch, int k,
+                                                  const uint32_t *__restrict__ seq_flag,
+                                                  const uint32_t *__restrict__ fstart) {
+    __shared__ uint32_t list[FF_MAX], nl;
+    __shared__ uint32_t wsum[FS_T / 64];
+    {  // the flagged clusters in ascending order (ff_list over 1,024 threads)
+        __shared__ uint32_t wcnt[4];
+        const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+        const bool f = t < k && t < 256 && seq_flag[t] == 1u;
+        const uint64_t b = __ballot(f);
+        if (lane == 0 && w < 4) wcnt[w] = (uint32_t)__popcll(b);
+        __syncthreads();
+        uint32_t o = 0;
+        for (int i = 0; i < w && i < 4; ++i) o += wcnt[i];
+        o += (uint32_t)__popcll(b & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        if (f && o < (uint32_t)FF_MAX) list[o] = (uint32_t)t;
+        if (t == 0) nl = min(wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3], (uint32_t)FF_MAX);
+        __syncthreads();
+    }
+    const uint32_t f = blockIdx.x;
+    if (f >= nl) return;  // uniform
+    uint32_t *row = cnt + (uint64_t)f * nch;
+    const uint32_t per = (nch + FS_T - 1) / FS_T;
+    const uint32_t a = min(nch, threadIdx.x * per), b = min(nch, a + per);
+    uint32_t mine = 0;
+    for (uint32_t i = a; i < b; ++i) mine += row[i];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t o = fstart[list[f]];
+    for (int i = 0; i < w; ++i) o += wsum[i];
+    o += incl - mine;
+    for (uint32_t i = a; i < b; ++i) {
+        const uint32_t v = row[i];
+        row[i] = o;
+        o += v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ff_scatter(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
+                                                    uint64_t n, uint32_t nch, int k,
+                                                    const uint32_t *__restrict__ seq_flag,
+                                                    const uint32_t *__restrict__ off, uint32_t *__restrict__ fvals) {
+    __shared__ uint32_t list[FF_MAX], nl;
+    ff_list(seq_flag, k, list, &nl);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t nf = nl;
+    for (uint32_t ch = blockIdx.x * 4 + w; ch < nch; ch += gridDim.x * 4) {
+        const uint4 L = ff_labels(lab8, n, ch, lane);
+        const uint32_t v[4] = {L.x, L.y, L.z, L.w};
+        const uint64_t p0 = (uint64_t)ch * FF_CH + (uint64_t)lane * 16;
+        for (uint32_t f = 0; f < nf; ++f) {
+            uint32_t m[4], c = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                m[q] = ff_match(v[q], list[f]) & ff_valid_mask(n, ch, lane, q);
+                c += __popc(m[q]);
+            }
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += u;
+            }
+            uint32_t pos = off[(uint64_t)f * nch + ch] + incl - c;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t mm = m[q];
+                while (mm) {
+                    const int byte = __builtin_ctz(mm) >> 3;
+                    fvals[pos++] = __builtin_bit_cast(uint32_t, pts[p0 + 4 * q + byte]);
+                    mm &= mm - 1;
+                }
+            }
+        }
+    }
+}
+
+// per-tile member counts of the flagged clusters: tcnt[c * ntiles + tile] for flagged c
+__global__ __launch_bounds__(F1_T) void k_flag_tiles(const uint8_t *__restrict__ lab8, uint64_t n, uint32_t ntiles,
+                                                    int k, const uint32_t *__restrict__ seq_flag,
+                                                    uint32_t *__restrict__ tcnt) {
+    __shared__ uint32_t h[256];
+    __shared__ uint8_t fl[256];
+    const int t = threadIdx.x;
+    fl[t] = (t < k && seq_flag[t] == 1u) ? 1 : 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        h[t] = 0u;
+        __syncthreads();
+        const uint64_t base = (uint64_t)tile * F1_TILE;
+#pragma unroll 4
+        for (int r = 0; r < F1_ROWS; ++r) {
+            const uint64_t i = base + (uint64_t)r * F1_T + t;
+            if (i < n) {
+                const uint32_t d = lab8[i];
+                if (fl[d]) atomicAdd(&h[d], 1u);
+            }
+        }
+        __syncthreads();
+        if (fl[t]) tcnt[(uint64_t)t * ntiles + tile] = h[t];
+        __syncthreads();
+    }
+}
+
+// a flagged cluster's tile counts -> its members' first positions per tile in the compact
+// layout (exclusive scan from fstart[c]); one workgroup per cluster
+__global__ __launch_bounds__(SC_T) void k_flag_scan(uint32_t *__restrict__ tcnt, uint32_t ntiles,
+                                                    const uint32_t *__restrict__ seq_flag,
+                                                    const uint32_t *__restrict__ fstart) {
+    const int cl = blockIdx.x;
+    if (seq_flag[cl] != 1u) return;  // uniform per workgroup
+    uint32_t *row = tcnt + (uint64_t)cl * ntiles;
+    uint32_t carry = fstart[cl];
+    constexpr int PER = 4;
+    for (uint32_t b = 0; b < ntiles; b += SC_T * PER) {
+        uint32_t v[PER], mine = 0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = b + threadIdx.x * PER + u;
+            v[u] = i < ntiles ? row[i] : 0u;
+            mine += v[u];
+        }
+        uint32_t tot;
+        uint32_t o = carry + sc_exscan_u32(mine, &tot);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = b + threadIdx.x * PER + u;
+            if (i < ntiles) row[i] = o;
+            o += v[u];
+        }
+        carry += tot;
+    }
+}
+
+// the flagged clusters' values in point order at their compact positions: each wave ranks
+// its 1,024 points of the tile by ballots over the label bits (as k_lab_scatter), the waves
+// of a tile take consecutive runs
+__global__ __launch_bounds__(F1_T) void k_flag_scatter(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
+                                                      uint64_t n, uint32_t ntiles, int k, int bits,
+                                                      const uint32_t *__restrict__ seq_flag,
+                                                      const uint32_t *__restrict__ toff, uint32_t *__restrict__ fvals) {
+    __shared__ uint32_t wcount[F1_WAVES][256];
+    __shared__ uint32_t wpos[F1_WAVES][256];
+    __shared__ uint8_t fl[256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    fl[t] = (t < k && seq_flag[t] == 1u) ? 1 : 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = t; i < F1_WAVES * 256; i += F1_T) (&wcount[0][0])[i] = 0u;
+        __syncthreads();
+        const uint64_t wb = (uint64_t)tile * F1_TILE + (uint64_t)w * 64 * F1_ROWS;
+        uint32_t dg[F1_ROWS];
+#pragma unroll
+        for (int r = 0; r < F1_ROWS; ++r) {
+            const uint64_t e = wb + (uint64_t)r * 64 + lane;
+            dg[r] = e < n ? (uint32_t)lab8[e] : 0u;
+            if (e < n && fl[dg[r]]) atomicAdd(&wcount[w][dg[r]], 1u);
+        }
+        __syncthreads();
+        if (fl[t]) {
+            uint32_t s = toff[(uint64_t)t * ntiles + tile];
+#pragma unroll
+            for (int i = 0; i < F1_WAVES; ++i) {
+                wpos[i][t] = s;
+                s += wcount[i][t];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < F1_ROWS; ++r) {
+            const uint64_t e = wb + (uint64_t)r * 64 + lane;
+            const uint32_t d = dg[r];
+            const bool valid = e < n && fl[d];
+            uint64_t peers = __ballot(valid);
+            if (peers == 0) continue;  // uniform
+            for (int b = 0; b < bits; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            const uint32_t before = valid ? wpos[w][d] : 0u;
+            if (valid) fvals[before + __popcll(peers & lt)] = __builtin_bit_cast(uint32_t, pts[e]);
+            if (valid && (peers & lt) == 0) wpos[w][d] = before + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
     }
 }
 
@@ -1017,7 +1545,74 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     const bool fused = k <= 256 && n > 0 && n < (1ull << 32) && !getenv("ST_KD1_WALK") && !getenv("ST_K1_PAIRS");
     const uint32_t ntiles = (uint32_t)((n + F1_TILE - 1) / F1_TILE);
     uint8_t *lab8 = fused ? wsT<uint8_t>(c, "k1.lab8", n) : nullptr;
+    // the sort-free iteration (k_kd1_assign_acc; ST_K1_SORT=1 keeps the member sort)
+    const bool accum = fused && !getenv("ST_K1_SORT");
     uint32_t *fhist = fused ? wsT<uint32_t>(c, "k1.fhist", (size_t)256 * ntiles) : nullptr;
+    if (accum) {
+        const uint32_t G = a1_grid(ntiles);
+        auto *part = wsT<Part1>(c, "k1.part", (size_t)G * 256);
+        auto *cnt_c = wsT<uint32_t>(c, "k1.cnt", (size_t)k);
+        auto *fstart = wsT<uint32_t>(c, "k1.fstart", (size_t)k + 1);
+        auto *ticket = wsT<uint32_t>(c, "k1.ticket", 1);
+        auto *dinfo = wsT<uint32_t>(c, "k1.info", 2);
+        auto *hinfo = static_cast<uint32_t *>(pinned_slot(c, "k1.info", 8));
+        ST_HIP(hipMemsetAsync(ticket, 0, sizeof(uint32_t), c->stream));
+        for (int it = 0; it < iters; ++it) {
+            {
+                KTimer kt(c, "k1.assign");
+                hipLaunchKernelGGL(k_kd1_assign_acc, dim3(G), dim3(F1_T), 0, c->stream, pts, n, cen, k,
+                                   it == iters - 1 ? labels : (uint32_t *)nullptr, lab8, ntiles, part);
+                ST_LAUNCH_CHECK();
+            }
+            mark(c, "k1.assign");
+            KTimer kt(c, "k1.sum");
+            hipLaunchKernelGGL(k_kd1_final, dim3(k), dim3(256), 0, c->stream, part, G, k, n, cen, seq_flag, emin_c,
+                               sabs_c, cnt_c, start, fstart, ticket, dinfo, dcols, ddraws, ndraws, dstate);
+            ST_LAUNCH_CHECK();
+            ST_HIP(hipMemcpyAsync(hinfo, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipStreamSynchronize(c->stream));
+            const uint32_t nflag = hinfo[0], ftotal = hinfo[1];
+            uint32_t nseq = 0;
+            if (nflag) {
+                // the flagged clusters' members in point order (fvals, starts fstart), then
+                // the chunked replay and, where it gives up, the sequential chain
+                if (nflag <= (uint32_t)FF_MAX && !getenv("ST_K1_TILES")) {
+                    const uint32_t nch = (uint32_t)((n + FF_CH - 1) / FF_CH);
+                    hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nch, k, seq_flag, fhist);
+                    hipLaunchKernelGGL(k_ff_scan, dim3(nflag), dim3(FS_T), 0, c->stream, fhist, nch, k, seq_flag,
+                                       fstart);
+                    hipLaunchKernelGGL(k_ff_scatter, dim3(G), dim3(256), 0, c->stream, lab8, pts, n, nch, k, seq_flag,
+                                       fhist, vals);
+                } else {
+                    hipLaunchKernelGGL(k_flag_tiles, dim3(G), dim3(F1_T), 0, c->stream, lab8, n, ntiles, k, seq_flag,
+                                       fhist);
+                    hipLaunchKernelGGL(k_flag_scan, dim3(k), dim3(SC_T), 0, c->stream, fhist, ntiles, seq_flag, fstart);
+                    hipLaunchKernelGGL(k_flag_scatter, dim3(G), dim3(F1_T), 0, c->stream, lab8, pts, n, ntiles, k,
+                                       kbits, seq_flag, fhist, vals);
+                }
+                ST_LAUNCH_CHECK();
+                // short chunks: the flagged clusters are few, their replay passes run over many
+                // workgroups at once
+                const uint64_t fch = ftotal / FL_CH + nflag + 1;
+                chunk_list(c, fstart, k, ch_cnt, ch_first, chunks, nullptr, FL_CH);
+                chunked_replay(c, vals, fstart, k, fch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum, rp_total,
+                               rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr);
+                if (getenv("ST_DEBUG")) {
+                    std::vector<uint32_t> f2(k);
+                    ST_HIP(hipMemcpyAsync(f2.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost, c->stream));
+                    ST_HIP(hipStreamSynchronize(c->stream));
+                    for (int i = 0; i < k; ++i) nseq += f2[i] == 2;
+                }
+                hipLaunchKernelGGL(k_sum1d_seq, dim3(k), dim3(64), 0, c->stream, vals, fstart, seq_flag, cen);
+                ST_LAUNCH_CHECK();
+            }
+            if (getenv("ST_DEBUG"))
+                fprintf(stderr, "[st k1] n=%llu uncertified=%u sequential-fallback=%u\n", (unsigned long long)n, nflag,
+                        nseq);
+            mark(c, "k1.update");
+        }
+        return;
+    }
     for (int it = 0; it < iters; ++it) {
         const uint32_t *vals_s = nullptr;
         if (fused) {
@@ -1126,6 +1721,27 @@ void seg_label_sort1d(st_ctx *c, const float *pts, const uint32_t *labels, uint6
         }
         ST_LAUNCH_CHECK();
     }
+}
+
+void assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k, const float *cen, uint32_t *labels,
+                       double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
+    ST_REQUIRE(k >= 1 && k <= 256 && nseg >= 1 && n % (uint64_t)nseg == 0, ST_ERR_ARG,
+               "1-D partials: k <= 256 and n in equal segments");
+    const uint64_t ns = n / (uint64_t)nseg;
+    const uint32_t ntiles = (uint32_t)((ns + F1_TILE - 1) / F1_TILE);
+    const uint32_t G = ntiles ? a1_grid(ntiles) : 1;
+    auto *part = wsT<Part1>(c, "d1.part", (size_t)nseg * G * 256);
+    for (int sg = 0; sg < nseg; ++sg) {
+        const uint64_t o = (uint64_t)sg * ns;
+        if (ns)
+            hipLaunchKernelGGL(k_kd1_assign_acc, dim3(G), dim3(F1_T), 0, c->stream, pts + o, ns, cen, k, labels + o,
+                               (uint8_t *)nullptr, ntiles, part + (uint64_t)sg * G * 256);
+        else
+            ST_HIP(hipMemsetAsync(part + (uint64_t)sg * G * 256, 0, sizeof(Part1) * 256 * G, c->stream));
+    }
+    hipLaunchKernelGGL(k_part_fold, dim3((unsigned)nseg * k), dim3(256), 0, c->stream, part, G, k, sums, sabs, emin,
+                       counts);
+    ST_LAUNCH_CHECK();
 }
 
 void partials1d(st_ctx *c, const uint32_t *vals, uint64_t n, const uint32_t *start, int nk, double *sums, double *sabs,

@@ -14,8 +14,10 @@
 //     Math.random: every rank holds the same draws and consumes them identically; a drawn row
 //     is supplied by its owner (bit patterns, integer SUM all-reduce).
 //   * Morton order (ordering.ts:4-110) is global: rank 0 gathers x/y/z and orders the whole
-//     table on a side stream (its own host thread) while the k-means run; every rank writes the
-//     texels of its rows in row order and rank 0 places them at their Morton positions.
+//     table; every rank writes the texels of its rows in row order and rank 0 places them at
+//     their Morton positions.  Both run beside the k-means: a side host thread per rank moves
+//     the rows over a second channel (Coll::side, an ncclCommSplit) on its side stream, so only
+//     the shN labels' gather and placement follow the SH k-means.
 //
 // Transports (Coll): RCCL (one process per GPU via a unique id, or one process driving
 // several GPUs via ncclCommInitAll), and a host-staged exchange between threads of one process
@@ -56,6 +58,10 @@ struct Coll {
     // rank `to` receives rank `from`'s buf (every rank makes the call; the others pass through)
     virtual void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) = 0;
     virtual void abort() {}
+    // a second channel over the same ranks, whose calls may run beside this one's (from another
+    // host thread, on another stream): the bulk texel traffic of the writer.  Collective: every
+    // rank asks for it at the same point; made once and kept.
+    virtual Coll *side() = 0;
 };
 
 #define ST_NCCL(expr)                                                                             \
@@ -72,8 +78,23 @@ struct RcclColl : Coll {
     ncclComm_t comm = nullptr;
     bool own = true;
     std::atomic<bool> dead{false};
+    std::mutex side_mu;
+    std::unique_ptr<RcclColl> side_;  // ncclCommSplit of comm
     ~RcclColl() override {
+        side_.reset();
         if (comm && own && !dead.load()) ncclCommDestroy(comm);
+    }
+    Coll *side() override {
+        live();
+        std::lock_guard<std::mutex> lk(side_mu);
+        if (!side_) {
+            auto sc = std::make_unique<RcclColl>();
+            ST_NCCL(ncclCommSplit(comm, 0, rank, &sc->comm, nullptr));
+            sc->rank = rank;
+            sc->world = world;
+            side_ = std::move(sc);
+        }
+        return side_.get();
     }
     void live() const {
         if (dead.load()) throw Error(ST_ERR_INTERNAL, "multi-GPU: another rank failed");
@@ -118,6 +139,10 @@ struct RcclColl : Coll {
         else ST_NCCL(ncclRecv(buf, bytes, ncclUint8, from, comm, s));
     }
     void abort() override {
+        {
+            std::lock_guard<std::mutex> lk(side_mu);
+            if (side_) side_->abort();
+        }
         if (!dead.exchange(true) && comm) ncclCommAbort(comm);
     }
     int count() const {
@@ -136,6 +161,7 @@ struct HostHub {
     uint64_t gen = 0;
     bool aborted = false;
     std::vector<std::vector<char>> slot;
+    std::shared_ptr<HostHub> side;  // the second channel's hub (made by the first rank asking)
     explicit HostHub(int w) : world(w), slot(w) {}
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -151,14 +177,36 @@ struct HostHub {
         if (aborted) throw Error(ST_ERR_INTERNAL, "multi-GPU: another rank failed");
     }
     void abort() {
+        std::shared_ptr<HostHub> sd;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            aborted = true;
+            cv.notify_all();
+            sd = side;
+        }
+        if (sd) sd->abort();
+    }
+    std::shared_ptr<HostHub> side_hub() {
         std::lock_guard<std::mutex> lk(mu);
-        aborted = true;
-        cv.notify_all();
+        if (!side) side = std::make_shared<HostHub>(world);
+        if (aborted) side->abort();
+        return side;
     }
 };
 
 struct HostColl : Coll {
     std::shared_ptr<HostHub> hub;
+    std::unique_ptr<HostColl> side_;
+    Coll *side() override {
+        if (!side_) {
+            auto sc = std::make_unique<HostColl>();
+            sc->hub = hub->side_hub();
+            sc->rank = rank;
+            sc->world = world;
+            side_ = std::move(sc);
+        }
+        return side_.get();
+    }
     void put(const void *dev, size_t bytes, hipStream_t s) {
         auto &v = hub->slot[rank];
         v.resize(bytes);
@@ -437,7 +485,9 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     for (int it = 0; it < iters; ++it) {
         if (c->verify && d > 1 && it == iters - 1)  // st_ctx_set_verify: the last assign's centroids
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
-        if (P.n) {
+        if (P.n && d == 1 && k <= 256 && !getenv("ST_K1_SORT")) {
+            dist_assign_partials1d(c, P.pts[0], P.n, P.nseg, k, cen, labels, sums, sabs, emin, counts);
+        } else if (P.n) {
             dist_assign(c, P.pts.data(), d, P.n, k, cen, labels);
             dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
         } else {  // empty shard: neutral partials
@@ -616,56 +666,100 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
     }
     const float *m[14];
     for (int i = 0; i < 14; ++i) m[i] = t->cols[i];
+    static const char *texn[6] = {"means_l", "means_u", "quats", "scales", "sh0", "shN_labels"};
+    const int ntex = C ? 6 : 5;
 
-    // Morton order of the global table on rank 0: x/y/z gathered, ordered on a side context from
-    // its own host thread (it overlaps the k-means below), texel positions pos[g]
+    // The global Morton order and the texel placement on rank 0 leave the critical path: a side
+    // host thread per rank moves x/y/z and the first five textures over the side channel on the
+    // side context's stream, rank 0's orders the table and places those texels, all beside the
+    // k-means on this thread.  Only the shN labels (known after the SH k-means) are gathered
+    // and placed after it.
     std::vector<size_t> bytes(co.world), displ(co.world);
     for (int r = 0; r < co.world; ++r) {
         bytes[r] = 4 * sh.counts[r];
         displ[r] = 4 * sh.offsets[r];
     }
+    Coll *bk = co.side();
+    if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    st_ctx *aux = c->aux;
     float *gx = nullptr, *gy = nullptr, *gz = nullptr;
-    uint32_t *pos = nullptr;
+    uint32_t *pos = nullptr, *gath = nullptr;
     if (root) {
         gx = wsT<float>(c, "mg.gx", N);
         gy = wsT<float>(c, "mg.gy", N);
         gz = wsT<float>(c, "mg.gz", N);
         pos = wsT<uint32_t>(c, "mg.pos", N);
+        gath = wsT<uint32_t>(c, "mg.gath", N * 5);
     }
-    co.gatherv(m[0], 4 * sh.n, gx, bytes, displ, 0, c->stream);
-    co.gatherv(m[1], 4 * sh.n, gy, bytes, displ, 0, c->stream);
-    co.gatherv(m[2], 4 * sh.n, gz, bytes, displ, 0, c->stream);
-    std::thread morton;
-    std::exception_ptr morton_err;
+    uint8_t *loc[6];
+    for (int i = 0; i < ntex; ++i) loc[i] = wsT<uint8_t>(c, std::string("mg.loc.") + texn[i], sh.n * 4 + 4);
+    uint8_t *dst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (root) {
-        hipEvent_t ev;
-        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ST_HIP(hipEventRecord(ev, c->stream));
-        if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
-        st_ctx *aux = c->aux;
-        ST_HIP(hipStreamWaitEvent(aux->stream, ev, 0));
-        ST_HIP(hipEventDestroy(ev));
-        morton = std::thread([&, aux] {
-            try {
-                use_device(aux);
+        uint8_t *o[6] = {out->means_l, out->means_u, out->quats, out->scales, out->sh0, out->shn_labels};
+        for (int i = 0; i < 6; ++i) dst[i] = o[i];
+    }
+    hipEvent_t ev_cols, ev_tex;
+    ST_HIP(hipEventCreateWithFlags(&ev_cols, hipEventDisableTiming));
+    ST_HIP(hipEventCreateWithFlags(&ev_tex, hipEventDisableTiming));
+    ST_HIP(hipEventRecord(ev_cols, c->stream));  // the member columns are in place
+    std::mutex tex_mu;
+    std::condition_variable tex_cv;
+    int tex_state = 0;  // 1: the five textures are written (ev_tex recorded), -1: abandoned
+    std::exception_ptr side_err;
+    std::thread side([&] {
+        try {
+            use_device(aux);
+            ST_HIP(hipStreamWaitEvent(aux->stream, ev_cols, 0));
+            bk->gatherv(m[0], 4 * sh.n, gx, bytes, displ, 0, aux->stream);
+            bk->gatherv(m[1], 4 * sh.n, gy, bytes, displ, 0, aux->stream);
+            bk->gatherv(m[2], 4 * sh.n, gz, bytes, displ, 0, aux->stream);
+            if (root) {
                 auto *idx = wsT<uint32_t>(aux, "mg.idx", N);
                 iota_u32(aux, idx, N);
                 morton_order_dev(aux, gx, gy, gz, idx, N);
                 hipLaunchKernelGGL(k_invert_u32, dim3(grid_for(N, 256, 8192)), dim3(256), 0, aux->stream, idx, N,
                                    pos);
                 ST_LAUNCH_CHECK();
-                ST_HIP(hipStreamSynchronize(aux->stream));
-            } catch (...) {
-                morton_err = std::current_exception();
             }
-        });
-    }
-    struct Joiner {
-        std::thread &th;
-        ~Joiner() {
-            if (th.joinable()) th.join();
+            {
+                std::unique_lock<std::mutex> lk(tex_mu);
+                tex_cv.wait(lk, [&] { return tex_state != 0; });
+                if (tex_state < 0) return;
+            }
+            ST_HIP(hipStreamWaitEvent(aux->stream, ev_tex, 0));
+            for (int i = 0; i < 5; ++i) bk->gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0,
+                                                   aux->stream);
+            if (root) {
+                for (int i = 0; i < 5; ++i) {
+                    ST_HIP(hipMemsetAsync(dst[i], 0, texels * 4, aux->stream));
+                    hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, aux->stream, gath + N * i,
+                                       pos, N, (uint32_t *)dst[i]);
+                    ST_LAUNCH_CHECK();
+                }
+            }
+            ST_HIP(hipStreamSynchronize(aux->stream));
+        } catch (...) {
+            side_err = std::current_exception();
+            co.abort();  // the main channel's peers must not wait for this rank
         }
-    } joiner{morton};
+    });
+    struct SideGuard {  // on every exit: release the side thread if it still waits, join it
+        std::thread &th;
+        std::mutex &mu;
+        std::condition_variable &cv;
+        int &state;
+        hipEvent_t a, b;
+        ~SideGuard() {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (state == 0) state = -1;
+            }
+            cv.notify_all();
+            if (th.joinable()) th.join();
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    } side_guard{side, tex_mu, tex_cv, tex_state, ev_cols, ev_tex};
 
     // global NaN-ignoring extents of x, y, z (write-sog.ts:161-187)
     double lo[3], hi[3];
@@ -694,10 +788,6 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
     ST_HIP(hipStreamSynchronize(c->stream));
 
     // this rank's texels in local row order (4 bytes per row and texture)
-    static const char *texn[6] = {"means_l", "means_u", "quats", "scales", "sh0", "shN_labels"};
-    const int ntex = C ? 6 : 5;
-    uint8_t *loc[6];
-    for (int i = 0; i < ntex; ++i) loc[i] = wsT<uint8_t>(c, std::string("mg.loc.") + texn[i], sh.n * 4 + 4);
     auto *rows = wsT<uint32_t>(c, "mg.iota", sh.n + 1);
     if (sh.n) iota_u32(c, rows, sh.n);
     st_sog_textures lt{loc[0], loc[1], loc[2], loc[3], loc[4], nullptr, nullptr};
@@ -708,11 +798,15 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
             meta->means_max[a] = lm.means_max[a];
         }
     }
-    auto *gath = root ? wsT<uint32_t>(c, "mg.gath", N * ntex) : nullptr;
-    for (int i = 0; i < 5; ++i)
-        co.gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0, c->stream);
+    ST_HIP(hipEventRecord(ev_tex, c->stream));
+    {
+        std::lock_guard<std::mutex> lk(tex_mu);
+        tex_state = 1;
+    }
+    tex_cv.notify_all();
 
     if (root) meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
+    uint32_t *gath5 = nullptr;
     if (C) {
         const int D = 3 * C;
         auto *cen = wsT<float>(c, "mg.shcen", (size_t)pal * D);
@@ -728,7 +822,8 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
         st_sog_textures lt2{};
         lt2.shn_labels = loc[5];
         sog_scatter_dev(c, t, rows, lo, hi, nullptr, nullptr, labels, &lm, &lt2);
-        co.gatherv(loc[5], 4 * sh.n, gath ? gath + N * 5 : nullptr, bytes, displ, 0, c->stream);
+        gath5 = root ? wsT<uint32_t>(c, "mg.gath5", N) : nullptr;
+        co.gatherv(loc[5], 4 * sh.n, gath5, bytes, displ, 0, c->stream);
         if (root) {
             meta->palette_size = pal;
             meta->shn_width = cw;
@@ -738,16 +833,13 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
             shn_centroids_dev(c, cl, C, pal, out->shn_centroids);
         }
     }
-    if (root) {
-        morton.join();
-        if (morton_err) std::rethrow_exception(morton_err);
-        uint8_t *dst[6] = {out->means_l, out->means_u, out->quats, out->scales, out->sh0, out->shn_labels};
-        for (int i = 0; i < ntex; ++i) {
-            ST_HIP(hipMemsetAsync(dst[i], 0, texels * 4, c->stream));
-            hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, c->stream, gath + N * i, pos, N,
-                               (uint32_t *)dst[i]);
-            ST_LAUNCH_CHECK();
-        }
+    side.join();
+    if (side_err) std::rethrow_exception(side_err);
+    if (root && C) {  // pos is in place (the side thread synchronised its stream)
+        ST_HIP(hipMemsetAsync(dst[5], 0, texels * 4, c->stream));
+        hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, c->stream, gath5, pos, N,
+                           (uint32_t *)dst[5]);
+        ST_LAUNCH_CHECK();
     }
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;

@@ -11,11 +11,9 @@ namespace km {
 // ---- exact replay of a sequential f64 sum ----------------------------------------------
 // Every member is a multiple of 2^e_lo (e_lo = the smallest ulp exponent), so the exact
 // prefix sums P_j are integers in units of 2^e_lo; with |P_j| <= sum|x| < 2^(e_lo+120)
-// they fit an int128.  Let B be the binade of |P_j|.  If x_j is a multiple of ulp(B) and
-// P_{j-1}, P_j lie in B at least M away from its ends (M bounds the accumulated rounding
-// drift |s - P|), the sequential step j cannot round: s_{j-1} and x_j are multiples of
-// ulp(B) and s_j stays in B.  Every other position is a "candidate" (tiny members, binade
-// changes, near-boundary prefixes).  One parallel pass computes P_j and lists the
+// they fit an int128.  M bounds the accumulated rounding drift |s - P|; replay_candidate
+// lists the positions where the sequential step may round (tiny members, moves up a
+// binade, prefixes within M of a binade's bottom); every other step is exact.  One parallel pass computes P_j and lists the
 // candidates in order; one lane then replays the candidates only,
 //     V_c = s_prev + (P_c - P_prev),   s_c = RN(V_c),
 // and the final sum is s_last + (P_end - P_last).  The drift is checked against M; a
@@ -103,17 +101,23 @@ __device__ inline int binade_of(__int128 P, int e_lo) {  // floor(log2 |P * 2^e_
     return m ? bitlen128(m) - 1 + e_lo : -1000;
 }
 
-// position j can round (see above): tiny member, binade change, or near a binade end
+// Position j can round unless all of: P_{j-1} is nonzero and at least M above the bottom of
+// its binade bp (so |s_{j-1}| >= 2^bp and s_{j-1} is a multiple of 2^(bp-52)); x_j is a
+// multiple of 2^(bp-52); |P_j| + M < 2^(bp+1).  Then s_{j-1} + x_j is a multiple of
+// 2^(bp-52) below 2^(bp+1) in magnitude: exactly representable.  Moves down a binade (and
+// through zero) are exact steps by this rule, moves up past 2^(bp+1) are candidates.
 __device__ inline bool replay_candidate(__int128 Pprev, __int128 P, uint32_t xbits, int e_lo, __int128 margin) {
-    const int b = binade_of(P, e_lo);
-    if (b == -1000 || b != binade_of(Pprev, e_lo)) return true;
+    const unsigned __int128 mp = Pprev < 0 ? (unsigned __int128)(-Pprev) : (unsigned __int128)Pprev;
+    if (mp == 0) return true;
+    const int blp = bitlen128(mp);  // |P_{j-1}| in [2^(blp-1), 2^blp) units
+    const unsigned __int128 lo_end = ((unsigned __int128)1) << (blp - 1), hi_end = ((unsigned __int128)1) << blp;
+    if (mp - lo_end < (unsigned __int128)margin) return true;
+    const int bp = blp - 1 + e_lo;
     const uint32_t ex = (xbits >> 23) & 0xffu;
     const int xulp = ex ? (int)ex - 150 : -149;
-    if ((xbits & 0x7fffffffu) != 0 && xulp < b - 52) return true;
+    if ((xbits & 0x7fffffffu) != 0 && xulp < bp - 52) return true;
     const unsigned __int128 m = P < 0 ? (unsigned __int128)(-P) : (unsigned __int128)P;
-    const int bl = bitlen128(m);
-    const unsigned __int128 lo_end = ((unsigned __int128)1) << (bl - 1), hi_end = ((unsigned __int128)1) << bl;
-    return (m - lo_end) < (unsigned __int128)margin || (hi_end - m) <= (unsigned __int128)margin;
+    return m + (unsigned __int128)margin >= hi_end;
 }
 
 // The replay of one member range [s0, s1) starting from the f64 value s_in (a multiple of

@@ -141,11 +141,16 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters):
     same_bits(cent, ocent)
 
 
+@pytest.mark.parametrize('mode', ['', 'ST_K1_TILES', 'ST_K1_SORT'])
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
-def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac):
+def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
     """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
-    hold tiny members, so the sequential f64 sum rounds -- a few events (k_sum1d_replay) or
-    many (the sequential fallback)."""
+    hold tiny members, so the sequential f64 sum rounds -- a few events (the replay) or many
+    (the sequential fallback).  mode: the flagged clusters' members gathered by the wave
+    kernels (default), the tile kernels (ST_K1_TILES), or every iteration's member sort
+    (ST_K1_SORT)."""
+    if mode:
+        monkeypatch.setenv(mode, '1')
     rng = np.random.default_rng(77)
     n = 300_000
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
@@ -155,6 +160,26 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac):
     draws = oracle.mulberry32(5, 1 << 14)
     cent, labels, used = ctx.cluster1d(cols, 4, draws)
     rc, ocent, olabels, oused = oracle.cluster1d(cols, 4, draws)
+    assert rc == 0 and used == oused
+    assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
+    assert np.array_equal(labels, olabels)
+
+
+@pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
+def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac):
+    """The sort-free 1-D iteration at a size where every accumulating workgroup takes several
+    4,096-point tiles and the flagged clusters' members are gathered from hundreds of tiles
+    (1.5M points per column, 4.5M values); 0.02 drives sums with many rounding events into
+    the sequential chain."""
+    rng = np.random.default_rng(78)
+    n = 1_500_000
+    cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
+    for c in cols:
+        tiny = rng.random(n) < tiny_frac
+        c[tiny] *= np.float32(1e-9)
+    draws = oracle.mulberry32(6, 1 << 14)
+    cent, labels, used = ctx.cluster1d(cols, 3, draws)
+    rc, ocent, olabels, oused = oracle.cluster1d(cols, 3, draws)
     assert rc == 0 and used == oused
     assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
     assert np.array_equal(labels, olabels)
