@@ -415,17 +415,18 @@ def sog_stage_table(stages, n, iters, K=65536, D=45):
                          '(the sweep); 184 B/splat/iter of HBM besides'),
         'sog.shn': ('hbm', 5 * iters * cb + 8 * n, 'codebook cluster1d over K x D values + shN labels texels'),
     }
-    # the colours' cluster1d runs on a side context beside Morton, means/quats and the scales'
-    # cluster1d (st_sog.hip): those four marks time one overlapped block, priced as one
-    block = ('sog.morton', 'sog.means_quats', 'sog.scales', 'sog.sh0')
-    if all(stages.get(k) for k in block):
+    # the colours' cluster1d and the Morton order + means/quats run on side contexts beside the
+    # scales' cluster1d (st_sog.hip): the marks up to sog.sh0 time one overlapped block, priced
+    # as one
+    block = tuple(k for k in ('sog.morton', 'sog.means_quats', 'sog.scales', 'sog.sh0') if k in stages)
+    if stages.get('sog.scales') and stages.get('sog.sh0'):
         stages = dict(stages)
         spec = dict(spec)
         ms_b = sum(stages.pop(k) for k in block)
-        work_b = sum(spec.pop(k)[1] for k in block)
+        work_b = sum(spec.pop(k)[1] for k in ('sog.morton', 'sog.means_quats', 'sog.scales', 'sog.sh0'))
         stages['sog.morton..sh0'] = ms_b
-        spec['sog.morton..sh0'] = ('hbm', work_b, 'Morton + means/quats + scales cluster1d on the main stream, the '
-                                   'colours cluster1d beside them on a side context (one overlapped block): '
+        spec['sog.morton..sh0'] = ('hbm', work_b, 'scales cluster1d on the main stream, the colours cluster1d and '
+                                   'Morton + means/quats beside it on side contexts (one overlapped block): '
                                    '92 + 40 + (15 iters + 7) + (15 iters + 11) B per splat')
     out = {}
     for k, (bound, work, what) in spec.items():

@@ -99,6 +99,9 @@ struct st_ctx {
     const float *ds_pts = nullptr;
     const uint32_t *ds_labels = nullptr;
     bool ds_sorted = true;
+    // 1-D k-means: read the uncertified-cluster count back every iteration (set for a rerun
+    // after ERR_K1_MANY)
+    bool k1_sync = false;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     st::Workspace ws;

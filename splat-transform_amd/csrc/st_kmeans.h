@@ -6,7 +6,14 @@
 namespace st {
 namespace km {
 
-enum : uint32_t { ERR_DRAWS = 1u, ERR_TIE = 2u, ERR_INTERNAL = 4u, ERR_INIT_WINDOW = 8u, ERR_DRAW_RANGE = 16u };
+enum : uint32_t {
+    ERR_DRAWS = 1u,
+    ERR_TIE = 2u,
+    ERR_INTERNAL = 4u,
+    ERR_INIT_WINDOW = 8u,
+    ERR_DRAW_RANGE = 16u,
+    ERR_K1_MANY = 32u,  // 1-D: more uncertified clusters than the queued path takes (rerun synchronised)
+};
 
 // device-resident k-means state (one per call)
 struct State {
@@ -52,6 +59,9 @@ __host__ __device__ inline uint32_t sortkey_(float f) { return fkey_(f == 0.0f ?
 // shared by the 1-D and N-D loops
 void reseed_empty(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *start,
                   const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen);
+// the same from the clusters' member counts
+void reseed_empty_counts(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *counts,
+                         const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen);
 // start[c] = first index with sorted_labels >= c, start[k] = n
 void bounds_from_sorted(st_ctx *c, const uint32_t *sorted_labels, uint64_t n, int k, uint32_t *start);
 void member_sort(st_ctx *c, const uint32_t *labels, uint64_t n, int k, uint32_t *sorted_labels, uint32_t *members,
@@ -67,8 +77,14 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
 
 // step form of the loops (shared with the distributed step API, st_dist.hip)
 void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n);  // workspace: kn.pfrag/kn.pnorm/kn.aos
+// the fix-up pass's share of the update (kmeansnd_loop): set by nd_assign when the fused
+// fix-up ran (partials of the decided points; the other points' counts)
+struct NdFused {
+    bool want = false, valid = false;
+    uint32_t npair = 0, namb = 0, nties_fix = 0, ncodes = 0;
+};
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
-               km::State *dstate);
+               km::State *dstate, NdFused *fz = nullptr);
 // returns true when it also wrote the update's (label, value bits) pairs into keys/vals
 // (need_labels = false with keys: the labels are not written, only the pairs)
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,

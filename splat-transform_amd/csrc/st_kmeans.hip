@@ -207,6 +207,58 @@ __global__ __launch_bounds__(256) void k_reseed(const float *const *cols, int d,
 
 __global__ void k_advance_cursor(State *st, const uint32_t *total_empty) { st->cursor += *total_empty; }
 
+// k_reseed_small from member counts for any k: one 1,024-thread workgroup, each thread a run of
+// consecutive clusters (the j-th empty cluster in ascending order takes draw cursor + j)
+constexpr int RC_T = 1024;
+__global__ __launch_bounds__(RC_T) void k_reseed_counts(const float *const *cols, int d, uint64_t n, int k,
+                                                        const uint32_t *__restrict__ counts,
+                                                        const double *__restrict__ draws, uint64_t ndraws, State *st,
+                                                        float *__restrict__ cen) {
+    __shared__ uint32_t wsum[RC_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int per = (k + RC_T - 1) / RC_T;
+    const int a = min(k, t * per), b = min(k, a + per);
+    uint32_t mine = 0;
+    for (int c = a; c < b; ++c) mine += counts[c] == 0u ? 1u : 0u;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (int i = 0; i < RC_T / 64; ++i) {
+        if (i < w) off += wsum[i];
+        total += wsum[i];
+    }
+    const uint64_t cursor = st->cursor;
+    uint32_t rank = off + incl - mine;
+    for (int c = a; c < b && mine; ++c) {
+        if (counts[c] != 0u) continue;
+        const uint64_t di = cursor + rank++;
+        if (di >= ndraws) {
+            atomicOr(&st->err, ERR_DRAWS);
+            continue;
+        }
+        const double dr = draws[di];
+        if (!(dr >= 0.0 && dr < 1.0)) {
+            atomicOr(&st->err, ERR_DRAW_RANGE);
+            continue;
+        }
+        const uint64_t row = (uint64_t)__builtin_floor(dr * (double)n);
+        for (int j = 0; j < d; ++j) cen[(uint64_t)j * k + c] = cols[j][row];
+    }
+    __syncthreads();  // every thread has read st->cursor
+    if (t == 0) st->cursor = cursor + total;
+}
+
+__global__ __launch_bounds__(256) void k_empty_flags_cnt(const uint32_t *counts, int k, uint32_t *flags) {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < k; c += gridDim.x * blockDim.x)
+        flags[c] = counts[c] == 0u ? 1u : 0u;
+}
+
 // the three steps above in one workgroup for k <= RS1_MAX (the 1-D codebooks, k = 256):
 // empty flags, their exclusive scan in LDS, the re-seeds, the cursor
 constexpr int RS1_T = 1024, RS1_MAX = 4096;
@@ -300,6 +352,24 @@ void reseed_empty(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k
     auto *flags = wsT<uint32_t>(c, "km.eflags", (size_t)k + 1);
     auto *rank = wsT<uint32_t>(c, "km.erank", (size_t)k + 1);
     hipLaunchKernelGGL(k_empty_flags, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, start, k, flags);
+    scan_u32(c, flags, rank, (uint64_t)k, rank + k);
+    hipLaunchKernelGGL(k_reseed, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, n, k, flags, rank,
+                       ddraws, ndraws, dstate, cen);
+    hipLaunchKernelGGL(k_advance_cursor, dim3(1), dim3(1), 0, c->stream, dstate, rank + k);
+    ST_LAUNCH_CHECK();
+}
+
+void reseed_empty_counts(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const uint32_t *counts,
+                         const double *ddraws, uint64_t ndraws, State *dstate, float *cen) {
+    if (k <= RC_T * 256) {
+        hipLaunchKernelGGL(k_reseed_counts, dim3(1), dim3(RC_T), 0, c->stream, dcols, d, n, k, counts, ddraws, ndraws,
+                           dstate, cen);
+        ST_LAUNCH_CHECK();
+        return;
+    }
+    auto *flags = wsT<uint32_t>(c, "km.eflags", (size_t)k + 1);
+    auto *rank = wsT<uint32_t>(c, "km.erank", (size_t)k + 1);
+    hipLaunchKernelGGL(k_empty_flags_cnt, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, counts, k, flags);
     scan_u32(c, flags, rank, (uint64_t)k, rank + k);
     hipLaunchKernelGGL(k_reseed, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, dcols, d, n, k, flags, rank,
                        ddraws, ndraws, dstate, cen);
@@ -462,6 +532,16 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     ST_HIP(hipStreamSynchronize(c->stream));
     if (hs.err & ERR_INIT_WINDOW)  // the device window held fewer than k distinct rows
         return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, true, sum64);
+    if (hs.err & ERR_K1_MANY) {  // more uncertified 1-D clusters than the queued iteration takes
+        const bool was = c->k1_sync;
+        c->k1_sync = true;
+        struct Reset {
+            st_ctx *c;
+            bool was;
+            ~Reset() { c->k1_sync = was; }
+        } reset{c, was};
+        return kmeans_dev(c, cols, d, n, k, iters, draws, ndraws_all, cen, labels, host_init, sum64);
+    }
     ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
     ST_REQUIRE(!(hs.err & ERR_DRAW_RANGE), ST_ERR_ARG, "kmeans: a re-seed draw outside [0, 1)");
     ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");

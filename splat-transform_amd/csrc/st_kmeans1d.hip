@@ -467,13 +467,9 @@ __global__ __launch_bounds__(RT) void k_sum1d_replay(const uint32_t *__restrict_
     seq_flag[cl] = 0u;
 }
 
-// the sequential f64 sum of a flagged cluster: one lane walks the members in order, the
-// loads run PF x 16 bytes ahead of the dependent add chain
-__global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
-                                                  const uint32_t *__restrict__ seq_flag, float *__restrict__ cen) {
-    const int cl = blockIdx.x;
-    if (seq_flag[cl] != 2u || threadIdx.x != 0) return;
-    const uint32_t s0 = start[cl], s1 = start[cl + 1];
+// the sequential f64 sum of members [s0, s1) on the calling lane: the loads run PF x 16 bytes
+// ahead of the dependent add chain
+__device__ inline double seq_sum1d(const uint32_t *__restrict__ vals, uint32_t s0, uint32_t s1) {
     double s = 0;
     uint32_t j = s0;
     for (; j < s1 && (j & 3u); ++j) s += (double)__builtin_bit_cast(float, vals[j]);
@@ -510,7 +506,16 @@ __global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ v
         }
     }
     for (j += nq * 4; j < s1; ++j) s += (double)__builtin_bit_cast(float, vals[j]);
-    cen[cl] = (float)(s / (double)(s1 - s0));
+    return s;
+}
+
+// the sequential f64 sum of a flagged cluster (flag 2): one lane walks the members in order
+__global__ __launch_bounds__(64) void k_sum1d_seq(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
+                                                  const uint32_t *__restrict__ seq_flag, float *__restrict__ cen) {
+    const int cl = blockIdx.x;
+    if (seq_flag[cl] != 2u || threadIdx.x != 0) return;
+    const uint32_t s0 = start[cl], s1 = start[cl + 1];
+    cen[cl] = (float)(seq_sum1d(vals, s0, s1) / (double)(s1 - s0));
 }
 
 // ---- chunked update: every cluster's members split into SC_CH-member chunks ----------
@@ -679,15 +684,17 @@ __global__ __launch_bounds__(SC_T) void k_rp_sums(const uint32_t *__restrict__ v
                                                  const uint32_t *__restrict__ nchunks,
                                                  const uint32_t *__restrict__ seq_flag,
                                                  const int32_t *__restrict__ emin_c, __int128 *__restrict__ csum) {
-    if (blockIdx.x >= *nchunks) return;
-    const Chunk ch = chunks[blockIdx.x];
-    if (seq_flag[ch.cl] != 1u) return;
-    const int e_lo = emin_c[ch.cl];
-    __int128 local = 0;
-    for (uint32_t j = ch.begin + threadIdx.x; j < ch.end; j += SC_T) local += f32_units(vals[j], e_lo);
-    __int128 tot;
-    sc_exscan_i128(local, &tot);
-    if (threadIdx.x == 0) csum[blockIdx.x] = tot;
+    const uint32_t nch = *nchunks;
+    for (uint32_t bi = blockIdx.x; bi < nch; bi += gridDim.x) {
+        const Chunk ch = chunks[bi];
+        if (seq_flag[ch.cl] != 1u) continue;  // uniform per workgroup
+        const int e_lo = emin_c[ch.cl];
+        __int128 local = 0;
+        for (uint32_t j = ch.begin + threadIdx.x; j < ch.end; j += SC_T) local += f32_units(vals[j], e_lo);
+        __int128 tot;
+        sc_exscan_i128(local, &tot);
+        if (threadIdx.x == 0) csum[bi] = tot;
+    }
 }
 
 // B / D: one workgroup per flagged cluster scans its chunks in order (exclusive prefixes)
@@ -743,40 +750,42 @@ __global__ __launch_bounds__(SC_T) void k_rp_cands(const uint32_t *__restrict__ 
                                                   const double *__restrict__ sabs_c,
                                                   const __int128 *__restrict__ coff, uint32_t *__restrict__ ccnt,
                                                   __int128 *__restrict__ cand_all, const double *__restrict__ base) {
-    if (blockIdx.x >= *nchunks) return;
-    const Chunk ch = chunks[blockIdx.x];
-    if (seq_flag[ch.cl] != 1u) return;
-    const int e_lo = emin_c[ch.cl];
-    const __int128 margin = rp_margin(rp_bound(sabs_c, base, ch.cl), e_lo);
-    // this thread's contiguous slice of the chunk
-    const uint32_t per = (ch.end - ch.begin + SC_T - 1) / SC_T;
-    const uint32_t a = min(ch.end, ch.begin + threadIdx.x * per), b = min(ch.end, a + per);
-    __int128 local = 0;
-    for (uint32_t j = a; j < b; ++j) local += f32_units(vals[j], e_lo);
-    __int128 tot;
-    const __int128 off = rp_base(base, ch.cl, e_lo) + coff[blockIdx.x] + sc_exscan_i128(local, &tot);
-    uint32_t mine = 0;
-    __int128 P = off;
-    for (uint32_t j = a; j < b; ++j) {
-        const uint32_t xb = vals[j];
-        const __int128 Pn = P + f32_units(xb, e_lo);
-        mine += replay_candidate(P, Pn, xb, e_lo, margin) ? 1u : 0u;
-        P = Pn;
-    }
-    uint32_t ctot;
-    const uint32_t cof = sc_exscan_u32(mine, &ctot);
-    if (!WRITE) {
-        if (threadIdx.x == 0) ccnt[blockIdx.x] = ctot;
-        return;
-    }
-    uint32_t o = ccnt[blockIdx.x] + cof;
-    __int128 *cand = cand_all + (uint64_t)ch.cl * CAND_MAX;
-    P = off;
-    for (uint32_t j = a; j < b; ++j) {
-        const uint32_t xb = vals[j];
-        const __int128 Pn = P + f32_units(xb, e_lo);
-        if (replay_candidate(P, Pn, xb, e_lo, margin)) cand[o++] = Pn;
-        P = Pn;
+    const uint32_t nch = *nchunks;
+    for (uint32_t bi = blockIdx.x; bi < nch; bi += gridDim.x) {
+        const Chunk ch = chunks[bi];
+        if (seq_flag[ch.cl] != 1u) continue;  // uniform per workgroup
+        const int e_lo = emin_c[ch.cl];
+        const __int128 margin = rp_margin(rp_bound(sabs_c, base, ch.cl), e_lo);
+        // this thread's contiguous slice of the chunk
+        const uint32_t per = (ch.end - ch.begin + SC_T - 1) / SC_T;
+        const uint32_t a = min(ch.end, ch.begin + threadIdx.x * per), b = min(ch.end, a + per);
+        __int128 local = 0;
+        for (uint32_t j = a; j < b; ++j) local += f32_units(vals[j], e_lo);
+        __int128 tot;
+        const __int128 off = rp_base(base, ch.cl, e_lo) + coff[bi] + sc_exscan_i128(local, &tot);
+        uint32_t mine = 0;
+        __int128 P = off;
+        for (uint32_t j = a; j < b; ++j) {
+            const uint32_t xb = vals[j];
+            const __int128 Pn = P + f32_units(xb, e_lo);
+            mine += replay_candidate(P, Pn, xb, e_lo, margin) ? 1u : 0u;
+            P = Pn;
+        }
+        uint32_t ctot;
+        const uint32_t cof = sc_exscan_u32(mine, &ctot);
+        if (!WRITE) {
+            if (threadIdx.x == 0) ccnt[bi] = ctot;
+            continue;
+        }
+        uint32_t o = ccnt[bi] + cof;
+        __int128 *cand = cand_all + (uint64_t)ch.cl * CAND_MAX;
+        P = off;
+        for (uint32_t j = a; j < b; ++j) {
+            const uint32_t xb = vals[j];
+            const __int128 Pn = P + f32_units(xb, e_lo);
+            if (replay_candidate(P, Pn, xb, e_lo, margin)) cand[o++] = Pn;
+            P = Pn;
+        }
     }
 }
 
@@ -787,11 +796,21 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
                                                   const int32_t *__restrict__ emin_c, const double *__restrict__ sabs_c,
                                                   const __int128 *__restrict__ total, const __int128 *__restrict__ cand_all,
                                                   float *__restrict__ cen, const double *__restrict__ base,
-                                                  double *__restrict__ sum_out) {
+                                                  double *__restrict__ sum_out, const uint32_t *__restrict__ seq_vals) {
     // one workgroup per cluster: the wave stages the candidates in LDS 256 at a time, lane 0
-    // replays them (the chain is sequential; its loads need not be)
+    // replays them (the chain is sequential; its loads need not be).  seq_vals (non-null): the
+    // clusters left to the sequential chain (flag 2) take it here too
     const int cl = blockIdx.x;
-    if (cl >= k || seq_flag[cl] != 1u) return;  // uniform per workgroup
+    if (cl >= k) return;
+    const uint32_t flag0 = seq_flag[cl];
+    if (flag0 == 2u && seq_vals) {
+        if (threadIdx.x == 0) {
+            const uint32_t s0 = start[cl], s1 = start[cl + 1];
+            cen[cl] = (float)(seq_sum1d(seq_vals, s0, s1) / (double)(s1 - s0));
+        }
+        return;
+    }
+    if (flag0 != 1u) return;  // uniform per workgroup
     __shared__ __int128 buf[256];
     const int e_lo = emin_c[cl];
     const __int128 margin = rp_margin(rp_bound(sabs_c, base, cl), e_lo);
@@ -820,6 +839,10 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
     const __int128 fin = sv + (b0 + total[cl] - Pprev);
     if (!ok || !f64_representable(fin)) {
         seq_flag[cl] = 2u;
+        if (seq_vals) {
+            const uint32_t s0 = start[cl], s1 = start[cl + 1];
+            cen[cl] = (float)(seq_sum1d(seq_vals, s0, s1) / (double)(s1 - s0));
+        }
         return;
     }
     if (sum_out)
@@ -844,19 +867,20 @@ uint32_t replay_cap() {
 void chunked_replay(st_ctx *c, const uint32_t *vals, const uint32_t *start, int k, uint64_t maxch, const Chunk *chunks,
                     const uint32_t *ch_first, uint32_t *seq_flag, const int32_t *emin_c, const double *sabs_c,
                     __int128 *csum, __int128 *total, uint32_t *ccnt, uint32_t *cof, uint32_t *ctot, __int128 *cands,
-                    float *cen, const double *base, double *sum_out) {
-    hipLaunchKernelGGL(k_rp_sums, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag, emin_c,
+                    float *cen, const double *base, double *sum_out, bool seq_inline = false) {
+    const unsigned gch = (unsigned)std::min<uint64_t>(maxch, 2048);  // grid-stride over the chunks
+    hipLaunchKernelGGL(k_rp_sums, dim3(gch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag, emin_c,
                        csum);
     hipLaunchKernelGGL(k_rp_prefix, dim3(k), dim3(SC_T), 0, c->stream, ch_first, k, seq_flag, sabs_c, emin_c, csum,
                        total, base);
-    hipLaunchKernelGGL(k_rp_cands<false>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
+    hipLaunchKernelGGL(k_rp_cands<false>, dim3(gch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
                        emin_c, sabs_c, csum, ccnt, cands, base);
     hipLaunchKernelGGL(k_rp_cprefix, dim3(k), dim3(SC_T), 0, c->stream, ch_first, k, seq_flag, ccnt, cof, ctot,
                        replay_cap());
-    hipLaunchKernelGGL(k_rp_cands<true>, dim3(maxch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
+    hipLaunchKernelGGL(k_rp_cands<true>, dim3(gch), dim3(SC_T), 0, c->stream, vals, chunks, ch_first + k, seq_flag,
                        emin_c, sabs_c, csum, cof, cands, base);
     hipLaunchKernelGGL(k_rp_finish, dim3(k), dim3(64), 0, c->stream, start, ctot, k, seq_flag, emin_c, sabs_c, total,
-                       cands, cen, base, sum_out);
+                       cands, cen, base, sum_out, seq_inline ? vals : (const uint32_t *)nullptr);
     ST_LAUNCH_CHECK();
 }
 
@@ -987,6 +1011,7 @@ struct Part1 {
     uint32_t cnt;
 };
 constexpr uint32_t A1_G = 1024;  // most workgroups (partials) of the accumulating assign
+constexpr int FF_MAX = 8;         // flagged clusters the wave kernels take (more: the tile kernels)
 
 // workgroups for ntiles tiles: at most A1_G, every workgroup the same number of tiles
 uint32_t a1_grid(uint32_t ntiles) {
@@ -1004,6 +1029,7 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
     __shared__ float sv[256];
     __shared__ uint32_t si[256], skey[256];
     __shared__ uint16_t cc[256];
+    __shared__ uint8_t chk_l[256], chk_r[256];
     __shared__ uint32_t first[KD1_CELLS + 1];
     __shared__ double hs[256], ha[256];
     __shared__ int32_t he[256];
@@ -1034,7 +1060,18 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
         const float u = (x - lo) * inv;
         return (int)__builtin_fminf(__builtin_fmaxf(u, 0.f), (float)(KD1_CELLS - 1));
     };
-    if (t < k) cc[t] = (uint16_t)cell(sv[t]);
+    if (t < k) {
+        cc[t] = (uint16_t)cell(sv[t]);
+        // can the outer neighbour of bracket end t share the minimum's rounded distance?  With
+        // L = t, a = p - sv[t] < the gap to sv[t + 1], and RN((a + gl)^2) = RN(a^2) needs
+        // a > 2^52 gl: only for equal values, a missing right neighbour or a gap ratio past
+        // 2^48 (likewise for R = t).  Elsewhere the outer distance is strictly larger.
+        const double gl = t >= 1 ? (double)sv[t] - (double)sv[t - 1] : -1.0;
+        const double gr = t + 1 < k ? (double)sv[t + 1] - (double)sv[t] : -1.0;
+        constexpr double R48 = 281474976710656.0;  // 2^48
+        chk_l[t] = (t >= 1 && (gl == 0.0 || gr < 0.0 || gr >= gl * R48)) ? 1 : 0;
+        chk_r[t] = (t + 1 < k && (gr == 0.0 || gl < 0.0 || gl >= gr * R48)) ? 1 : 0;
+    }
     __syncthreads();
     for (int g = t; g <= KD1_CELLS; g += F1_T) {
         int a = 0, b = k;
@@ -1074,7 +1111,8 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
             const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
             const double dr = R < k ? dist(R, p) : __builtin_inf();
             const double m = __builtin_fmin(dl, dr);
-            const bool tie = dl == dr || (L >= 1 && dist(L - 1, p) == m) || (R + 1 < k && dist(R + 1, p) == m);
+            const bool tie = dl == dr || (L >= 1 && chk_l[L] && dist(L - 1, p) == m) ||
+                             (R + 1 < k && chk_r[R] && dist(R + 1, p) == m);
             const uint32_t lab = !tie ? si[dl < dr ? L : R] : kd1_walk(p, k, val, idx);
             if (lab8) lab8[i] = (uint8_t)lab;
             if (labels) labels[i] = lab;
@@ -1099,7 +1137,7 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
                                                    uint32_t *__restrict__ start, uint32_t *__restrict__ fstart,
                                                    uint32_t *ticket, uint32_t *__restrict__ info,
                                                    const float *const *cols, const double *__restrict__ draws,
-                                                   uint64_t ndraws, State *st) {
+                                                   uint64_t ndraws, State *st, uint32_t many_above) {
     const int cl = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     double s = 0, a = 0;
     int e = 1 << 20;
@@ -1181,6 +1219,7 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
         st->cursor = cursor + nempty;
         info[0] = nflag;
         info[1] = ftot;
+        if (nflag > many_above) atomicOr(&st->err, ERR_K1_MANY);
         if (tot != (uint32_t)n) atomicOr(&st->err, ERR_INTERNAL);
         *ticket = 0u;
     }
@@ -1231,7 +1270,6 @@ __global__ __launch_bounds__(256) void k_part_fold(const Part1 *__restrict__ par
 // two clusters whose range holds values near zero).  A wave takes 1,024 consecutive points
 // (16 byte labels per lane, one 16-byte load); per flagged cluster it counts (k_ff_count) or
 // places (k_ff_scatter) that cluster's members with a wave prefix sum: no tile histogram.
-constexpr int FF_MAX = 8;        // flagged clusters the wave kernels take (more: the tile kernels)
 constexpr uint32_t FF_CH = 1024;  // points per wave chunk
 
 // the flagged clusters in ascending order into list (LDS), their count into *nl
@@ -1279,6 +1317,7 @@ __global__ __launch_bounds__(256) void k_ff_count(const uint8_t *__restrict__ la
     ff_list(seq_flag, k, list, &nl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t nf = nl;
+    if (nf == 0) return;
     for (uint32_t ch = blockIdx.x * 4 + w; ch < nch; ch += gridDim.x * 4) {
         const uint4 L = ff_labels(lab8, n, ch, lane);
         const uint32_t v[4] = {L.x, L.y, L.z, L.w};
@@ -1317,27 +1356,52 @@ __global__ __launch_bounds__(FS_T) void k_ff_scan(uint32_t *__restrict__ cnt, ui
     }
     const uint32_t f = blockIdx.x;
     if (f >= nl) return;  // uniform
+    // pieces of FS_T * FS_PER counts staged in LDS by coalesced loads; each thread scans
+    // FS_PER consecutive ones, then one block scan
+    constexpr int FS_PER = 16;
+    __shared__ uint32_t piece[FS_T * (FS_PER + 1)];  // element e at e + e / FS_PER: no bank conflicts
+    auto at = [](uint32_t e) { return e + e / FS_PER; };
     uint32_t *row = cnt + (uint64_t)f * nch;
-    const uint32_t per = (nch + FS_T - 1) / FS_T;
-    const uint32_t a = min(nch, threadIdx.x * per), b = min(nch, a + per);
-    uint32_t mine = 0;
-    for (uint32_t i = a; i < b; ++i) mine += row[i];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t incl = mine;
+    uint32_t carry = fstart[list[f]];
+    for (uint32_t b0 = 0; b0 < nch; b0 += FS_T * FS_PER) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t o = fstart[list[f]];
-    for (int i = 0; i < w; ++i) o += wsum[i];
-    o += incl - mine;
-    for (uint32_t i = a; i < b; ++i) {
-        const uint32_t v = row[i];
-        row[i] = o;
-        o += v;
+        for (int u = 0; u < FS_PER; ++u) {
+            const uint32_t i = b0 + u * FS_T + threadIdx.x;
+            piece[at(u * FS_T + threadIdx.x)] = i < nch ? row[i] : 0u;
+        }
+        __syncthreads();
+        uint32_t mine = 0;
+#pragma unroll
+        for (int u = 0; u < FS_PER; ++u) mine += piece[at(threadIdx.x * FS_PER + u)];
+        uint32_t incl = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t o = carry, tot = 0;
+        for (int i = 0; i < FS_T / 64; ++i) {
+            if (i < w) o += wsum[i];
+            tot += wsum[i];
+        }
+        o += incl - mine;
+#pragma unroll
+        for (int u = 0; u < FS_PER; ++u) {
+            const uint32_t v = piece[at(threadIdx.x * FS_PER + u)];
+            piece[at(threadIdx.x * FS_PER + u)] = o;
+            o += v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < FS_PER; ++u) {
+            const uint32_t i = b0 + u * FS_T + threadIdx.x;
+            if (i < nch) row[i] = piece[at(u * FS_T + threadIdx.x)];
+        }
+        carry += tot;
+        __syncthreads();
     }
 }
 
@@ -1349,6 +1413,7 @@ __global__ __launch_bounds__(256) void k_ff_scatter(const uint8_t *__restrict__ 
     ff_list(seq_flag, k, list, &nl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t nf = nl;
+    if (nf == 0) return;
     for (uint32_t ch = blockIdx.x * 4 + w; ch < nch; ch += gridDim.x * 4) {
         const uint4 L = ff_labels(lab8, n, ch, lane);
         const uint32_t v[4] = {L.x, L.y, L.z, L.w};
@@ -1529,13 +1594,14 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     // chunked update (ST_K1_BLOCK=1 selects the one-workgroup-per-cluster kernels)
     const bool chunked = !getenv("ST_K1_BLOCK");
     const uint64_t maxch = n / SC_CH + (uint64_t)k + 1;
+    const uint64_t chcap = n / FL_CH + (uint64_t)k + 1;  // the flagged replay's shorter chunks
     auto *ch_cnt = wsT<uint32_t>(c, "k1.chcnt", (size_t)k);
     auto *ch_first = wsT<uint32_t>(c, "k1.chfirst", (size_t)k + 1);
-    auto *chunks = wsT<Chunk>(c, "k1.chunks", maxch);
+    auto *chunks = wsT<Chunk>(c, "k1.chunks", chcap);
     auto *acc = wsT<SumAcc>(c, "k1.acc", (size_t)k);
-    auto *rp_csum = wsT<__int128>(c, "k1.rpcsum", maxch);
-    auto *rp_ccnt = wsT<uint32_t>(c, "k1.rpccnt", maxch);
-    auto *rp_cof = wsT<uint32_t>(c, "k1.rpcof", maxch);
+    auto *rp_csum = wsT<__int128>(c, "k1.rpcsum", chcap);
+    auto *rp_ccnt = wsT<uint32_t>(c, "k1.rpccnt", chcap);
+    auto *rp_cof = wsT<uint32_t>(c, "k1.rpcof", chcap);
     auto *rp_ctot = wsT<uint32_t>(c, "k1.rpctot", (size_t)k);
     auto *rp_total = wsT<__int128>(c, "k1.rptotal", (size_t)k);
     int kbits = 1;
@@ -1557,6 +1623,14 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         auto *dinfo = wsT<uint32_t>(c, "k1.info", 2);
         auto *hinfo = static_cast<uint32_t *>(pinned_slot(c, "k1.info", 8));
         ST_HIP(hipMemsetAsync(ticket, 0, sizeof(uint32_t), c->stream));
+        // queued: no read-back per iteration (more than FF_MAX flagged clusters -> ERR_K1_MANY,
+        // and kmeans_dev reruns with k1_sync); otherwise the count decides the flagged path
+        const bool queued = !c->k1_sync && !getenv("ST_K1_TILES") && !getenv("ST_K1_SYNC");
+        // flagged clusters the wave kernels take (ST_K1_FF_MAX lowers it: tests of the rerun)
+        const uint32_t ff_max = getenv("ST_K1_FF_MAX") ? std::min<uint32_t>((uint32_t)atoi(getenv("ST_K1_FF_MAX")),
+                                                                            (uint32_t)FF_MAX)
+                                                       : (uint32_t)FF_MAX;
+        const uint64_t fl_maxch = chcap;
         for (int it = 0; it < iters; ++it) {
             {
                 KTimer kt(c, "k1.assign");
@@ -1567,8 +1641,34 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             mark(c, "k1.assign");
             KTimer kt(c, "k1.sum");
             hipLaunchKernelGGL(k_kd1_final, dim3(k), dim3(256), 0, c->stream, part, G, k, n, cen, seq_flag, emin_c,
-                               sabs_c, cnt_c, start, fstart, ticket, dinfo, dcols, ddraws, ndraws, dstate);
+                               sabs_c, cnt_c, start, fstart, ticket, dinfo, dcols, ddraws, ndraws, dstate,
+                               queued ? ff_max : 0xffffffffu);
             ST_LAUNCH_CHECK();
+            if (queued) {
+                // the flagged path queued behind the final with no read-back: its kernels find
+                // the flagged clusters on the device and return at once when there are none
+                const uint32_t nch = (uint32_t)((n + FF_CH - 1) / FF_CH);
+                hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nch, k, seq_flag, fhist);
+                hipLaunchKernelGGL(k_ff_scan, dim3(FF_MAX), dim3(FS_T), 0, c->stream, fhist, nch, k, seq_flag, fstart);
+                hipLaunchKernelGGL(k_ff_scatter, dim3(G), dim3(256), 0, c->stream, lab8, pts, n, nch, k, seq_flag, fhist,
+                                   vals);
+                ST_LAUNCH_CHECK();
+                chunk_list(c, fstart, k, ch_cnt, ch_first, chunks, nullptr, FL_CH);
+                chunked_replay(c, vals, fstart, k, fl_maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum,
+                               rp_total, rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr, true);
+                if (getenv("ST_DEBUG")) {
+                    std::vector<uint32_t> f2(k);
+                    ST_HIP(hipMemcpyAsync(hinfo, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
+                    ST_HIP(hipMemcpyAsync(f2.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost, c->stream));
+                    ST_HIP(hipStreamSynchronize(c->stream));
+                    uint32_t nseq = 0;
+                    for (int i = 0; i < k; ++i) nseq += f2[i] == 2;
+                    fprintf(stderr, "[st k1] n=%llu uncertified=%u sequential-fallback=%u\n", (unsigned long long)n,
+                            hinfo[0], nseq);
+                }
+                mark(c, "k1.update");
+                continue;
+            }
             ST_HIP(hipMemcpyAsync(hinfo, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
             ST_HIP(hipStreamSynchronize(c->stream));
             const uint32_t nflag = hinfo[0], ftotal = hinfo[1];
@@ -1576,7 +1676,7 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             if (nflag) {
                 // the flagged clusters' members in point order (fvals, starts fstart), then
                 // the chunked replay and, where it gives up, the sequential chain
-                if (nflag <= (uint32_t)FF_MAX && !getenv("ST_K1_TILES")) {
+                if (nflag <= ff_max && !getenv("ST_K1_TILES")) {
                     const uint32_t nch = (uint32_t)((n + FF_CH - 1) / FF_CH);
                     hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nch, k, seq_flag, fhist);
                     hipLaunchKernelGGL(k_ff_scan, dim3(nflag), dim3(FS_T), 0, c->stream, fhist, nch, k, seq_flag,

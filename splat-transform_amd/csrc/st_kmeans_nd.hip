@@ -614,10 +614,16 @@ __device__ inline uint32_t code_row(uint32_t code, int rr) {
     return (code >> 1) * 32 + 4 * (code & 1) + (rr & 3) + 8 * (rr >> 2);
 }
 
+// the group's decision (every lane of the group holds it): the label, and whether it is an
+// exact tie left to the KdTree walk (the label then provisional)
+struct FixOut {
+    uint32_t label;
+    bool tie;
+};
 template <int G>
-__device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
-                                  const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
-                                  uint32_t *__restrict__ ties, State *st);
+__device__ inline FixOut fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
+                                    const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
+                                    uint32_t *__restrict__ ties, State *st);
 
 // all-reduce over a 16-lane DPP row (every lane of the row active): quad_perm xor 1, xor 2,
 // then row_ror 4 and 8 -- DPP moves folded into the VALU op, no LDS round trips
@@ -683,9 +689,9 @@ __device__ inline void fix_group(const float *__restrict__ aos, int d, const flo
 // the decision of a G-lane group from each lane's f32 screen s of row c: a unique interval
 // minimum decides; otherwise the exact f64 distances of the surviving rows
 template <int G>
-__device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
-                                  const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
-                                  uint32_t *__restrict__ ties, State *st) {
+__device__ inline FixOut fix_decide(float s, bool valid, uint32_t c, int d, const float *__restrict__ caos,
+                                    const float *__restrict__ prow, uint64_t p, int r, uint32_t *__restrict__ labels,
+                                    uint32_t *__restrict__ ties, State *st) {
     const int ld = aos_ld(d);
     // the screen's error: (d + 2) u T for any summation order of the d non-negative terms
     const float rel = (float)(d + 4) * 0x1p-24f, ab = (float)(d + 2) * 0x1p-126f;
@@ -724,7 +730,7 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
             for (int o = G / 2; o > 0; o >>= 1) w = min(w, __shfl_xor(w, o, 64));
         }
         if (r == 0) labels[p] = w;
-        return;
+        return FixOut{w, false};
     }
     if (ncand == 0) cand = valid;
     const double mine = cand ? ref_dist(caos + (uint64_t)c * ld, prow, ld) : __builtin_inf();
@@ -747,6 +753,7 @@ __device__ inline void fix_decide(float s, bool valid, uint32_t c, int d, const 
         labels[p] = bidx;  // provisional on a tie; the KdTree pass decides
         if (cnt > 1) ties[atomicAdd(&st->ties, 1u)] = (uint32_t)p;
     }
+    return FixOut{bidx, cnt > 1};
 }
 
 // decided points (one tile-half): 16 lanes per point
@@ -893,6 +900,318 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
     }
 }
 
+// ---- k_fixrow_b with the update folded in ---------------------------------------------
+// calcAverage (k-means.ts:41-63) adds a cluster's members in ascending point order in f64.
+// Where every member of a (cluster, dimension) is a multiple of 2^e_min and sum|x| <
+// 2^(e_min+53), every partial sum is exact, so the order is immaterial: the fix-up pass, which
+// already holds each decided point's row and label, accumulates (sum, sum|x|, e_min, count) per
+// cluster and dimension in LDS.  One workgroup takes a slice of one tile-half's decided points
+// (that tile-half's 16 clusters: no atomics outside LDS).  The other points (pairs, ambiguous,
+// exact ties) are summed by k_nd_combine from a short label sort; clusters failing the
+// certificate take the sequential sum over their members in point order (k_nd_seq).
+constexpr uint32_t FA_SL = 8192;  // decided points per slice (one workgroup)
+// accumulator slot of dimension j inside a cluster's LD slots: lane q adds dimensions 4q..4q+3,
+// stored q-consecutive so that one atomic instruction's lanes hit consecutive doubles
+template <int LD>
+__host__ __device__ inline int fa_slot(int j) { return (j & 3) * (LD / 4) + (j >> 2); }
+constexpr uint32_t OTHER_TIE = 0x80000000u;  // others' value bit: a fix-up tie (also in the slices' range)
+
+// local index (0..15) of centroid c inside its tile-half (code_row's inverse)
+__device__ inline uint32_t code_local(uint32_t c) { return (c & 3u) | (((c & 31u) >> 3) << 2); }
+__device__ inline uint32_t code_of(uint32_t c) { return (c >> 5) * 2 + ((c >> 2) & 1u); }
+
+// slice offsets of the codes' decided points: soff[c] = sum over codes < c of ceil(hist / FA_SL)
+constexpr int FS_T = 1024, FS_CODES = FB_MAX_CODES / FS_T;
+// ... and the codes' first positions in the grouped order (cursor: exclusive scan of hist,
+// k_code_scatter's start) with their total in *ndec: one workgroup (ncodes <= FB_MAX_CODES)
+__global__ __launch_bounds__(FS_T) void k_fa_slices(const uint32_t *__restrict__ hist, uint32_t ncodes,
+                                                    uint32_t *__restrict__ soff, uint32_t *__restrict__ cursor,
+                                                    uint32_t *__restrict__ ndec) {
+    __shared__ uint32_t wsum[FS_T / 64], wsum2[FS_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t v[FS_CODES], h[FS_CODES], mine = 0, mine2 = 0;
+#pragma unroll
+    for (int u = 0; u < FS_CODES; ++u) {
+        const uint32_t cd = t * FS_CODES + u;
+        h[u] = cd < ncodes ? hist[cd] : 0u;
+        v[u] = (h[u] + FA_SL - 1) / FA_SL;
+        mine += v[u];
+        mine2 += h[u];
+    }
+    uint32_t incl = mine, incl2 = mine2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o, 64), x2 = __shfl_up(incl2, o, 64);
+        if (lane >= o) {
+            incl += x;
+            incl2 += x2;
+        }
+    }
+    if (lane == 63) {
+        wsum[w] = incl;
+        wsum2[w] = incl2;
+    }
+    __syncthreads();
+    uint32_t o = 0, tot = 0, o2 = 0, tot2 = 0;
+    for (int i = 0; i < FS_T / 64; ++i) {
+        if (i < w) {
+            o += wsum[i];
+            o2 += wsum2[i];
+        }
+        tot += wsum[i];
+        tot2 += wsum2[i];
+    }
+    o += incl - mine;
+    o2 += incl2 - mine2;
+#pragma unroll
+    for (int u = 0; u < FS_CODES; ++u) {
+        const uint32_t cd = t * FS_CODES + u;
+        if (cd < ncodes) {
+            soff[cd] = o;
+            cursor[cd] = o2;
+        }
+        o += v[u];
+        o2 += h[u];
+    }
+    if (t == 0) {
+        soff[ncodes] = tot;
+        *ndec = tot2;
+    }
+}
+
+template <int LD>
+__global__ __launch_bounds__(256) void k_fixrow_acc(const float *__restrict__ aos, int d, const float *__restrict__ caos,
+                                                    int k, const uint2 *__restrict__ grouped,
+                                                    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ cend,
+                                                    const uint32_t *__restrict__ soff, uint32_t ncodes,
+                                                    uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                                    State *st, double *__restrict__ psum, double *__restrict__ pabs,
+                                                    int *__restrict__ pemin, uint32_t *__restrict__ pcnt) {
+    static_assert(FB_RUN == 32, "two run slots per lane");
+    __shared__ double S[16 * LD], A[16 * LD];
+    __shared__ int E[16 * LD];
+    __shared__ uint32_t C[16];
+    const uint32_t sl = blockIdx.x;
+    if (sl >= soff[ncodes]) return;  // uniform
+    uint32_t lo = 0, hi = ncodes;  // the code whose slices hold sl
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (soff[mid] <= sl) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t code = lo;
+    const uint32_t b0 = cend[code] - hist[code] + (sl - soff[code]) * FA_SL;
+    const uint32_t b1 = min(cend[code], b0 + FA_SL);
+    for (int e = threadIdx.x; e < 16 * LD; e += 256) {
+        S[e] = 0.0;
+        A[e] = 0.0;
+        E[e] = 1 << 20;
+    }
+    if (threadIdx.x < 16) C[threadIdx.x] = 0u;
+    __syncthreads();
+    const int rr = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int gl = (threadIdx.x & 63) & ~15;
+    const uint32_t c = code_row(code, rr);
+    const bool valid = c < (uint32_t)k;
+    float4 row[LD / 4];
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(caos + (uint64_t)(valid ? c : 0) * LD);
+#pragma unroll
+        for (int q = 0; q < LD / 4; ++q) row[q] = src[q];
+    }
+    const int sq = rr % (LD / 4);
+    for (uint32_t j0 = b0 + grp * FB_RUN; j0 < b1; j0 += 16 * FB_RUN) {  // uniform per 16-lane group
+        const int cnt = (int)min(b1 - j0, (uint32_t)FB_RUN);
+        const uint32_t pa = rr < cnt ? grouped[j0 + rr].x : 0u;
+        const uint32_t pb = 16 + rr < cnt ? grouped[j0 + 16 + rr].x : 0u;
+        auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
+        uint32_t p = point_of(0);
+        float4 cur = reinterpret_cast<const float4 *>(aos + (uint64_t)p * LD)[sq];
+        for (int i = 0; i < cnt; ++i) {
+            const uint32_t pn = point_of(i + 1 < cnt ? i + 1 : i);
+            float4 nxt;
+            {
+                const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn * LD) + sq;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt) : "v"(src) : "memory");
+            }
+            f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+            static_for<LD / 4>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const f32x2 t01 = {row_bcast<q>(cur.x) - row[q].x, row_bcast<q>(cur.y) - row[q].y};
+                const f32x2 t23 = {row_bcast<q>(cur.z) - row[q].z, row_bcast<q>(cur.w) - row[q].w};
+                a01 = __builtin_elementwise_fma(t01, t01, a01);
+                a23 = __builtin_elementwise_fma(t23, t23, a23);
+            });
+            const FixOut fo = fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos,
+                                             aos + (uint64_t)p * LD, p, rr, labels, ties, st);
+            if (!fo.tie && rr < LD / 4) {  // lane rr adds dimensions 4 rr .. 4 rr + 3 (padding adds 0)
+                const uint32_t base = code_local(fo.label) * LD + rr;
+                const float v[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    atomicAdd(&S[base + u * (LD / 4)], (double)v[u]);
+                    atomicAdd(&A[base + u * (LD / 4)], (double)__builtin_fabsf(v[u]));
+                    if (v[u] != 0.0f) atomicMin(&E[base + u * (LD / 4)], ulp_exp(v[u]));
+                }
+                if (rr == 0) atomicAdd(&C[code_local(fo.label)], 1u);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            cur = nxt;
+            p = pn;
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 16 * LD; e += 256) {
+        psum[(uint64_t)sl * 16 * LD + e] = S[e];
+        pabs[(uint64_t)sl * 16 * LD + e] = A[e];
+        pemin[(uint64_t)sl * 16 * LD + e] = E[e];
+    }
+    if (threadIdx.x < 16) pcnt[(uint64_t)sl * 16 + threadIdx.x] = C[threadIdx.x];
+}
+
+// the points the fused fix-up did not sum (pairs, ambiguous, its own exact ties), keyed by
+// their final label
+__global__ __launch_bounds__(256) void k_others_keys(const uint32_t *__restrict__ pair_pts, uint32_t npair,
+                                                     const uint32_t *__restrict__ amb, uint32_t namb,
+                                                     const uint32_t *__restrict__ ties, uint32_t nties,
+                                                     const uint32_t *__restrict__ labels, uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    const uint32_t m = npair + namb + nties;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t p = i < npair ? pair_pts[i] : i < npair + namb ? amb[i - npair] : ties[i - npair - namb];
+        keys[i] = labels[p];
+        vals[i] = i < npair + namb ? p : p | OTHER_TIE;
+    }
+}
+
+// one wave per cluster, lane = dimension: the slices' partials of its tile-half plus its other
+// members (ostart / ovals: the label-sorted others); the centroid where every dimension is
+// certified, otherwise the cluster is listed for k_nd_seq.  counts[cl] = its members.
+template <int LD>
+__global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ aos, int d, int k,
+                                                    const uint32_t *__restrict__ soff,
+                                                    const double *__restrict__ psum, const double *__restrict__ pabs,
+                                                    const int *__restrict__ pemin, const uint32_t *__restrict__ pcnt,
+                                                    const uint32_t *__restrict__ ostart,
+                                                    const uint32_t *__restrict__ ovals, float *__restrict__ cen,
+                                                    uint32_t *__restrict__ counts, uint32_t *__restrict__ flagged,
+                                                    uint32_t *__restrict__ nflagged) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (cl >= (uint32_t)k) return;  // uniform per wave
+    const uint32_t code = code_of(cl), loc = code_local(cl);
+    double sum = 0, sabs = 0;
+    int emin = 1 << 20;
+    uint32_t cnt = 0;
+    for (uint32_t sl = soff[code]; sl < soff[code + 1]; ++sl) {
+        if (lane < LD) {
+            const uint64_t e = (uint64_t)sl * 16 * LD + loc * LD + fa_slot<LD>(lane);
+            sum += psum[e];
+            sabs += pabs[e];
+            emin = min(emin, pemin[e]);
+        }
+        cnt += pcnt[(uint64_t)sl * 16 + loc];
+    }
+    const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
+    constexpr int U = 8;  // member rows in flight
+    uint32_t j = o0;
+    for (; j + U <= o1; j += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = lane < LD ? aos[(uint64_t)(ovals[j + u] & ~OTHER_TIE) * LD + lane] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            sum += (double)v[u];
+            sabs += (double)__builtin_fabsf(v[u]);
+            if (v[u] != 0.0f) emin = min(emin, ulp_exp(v[u]));
+        }
+    }
+    for (; j < o1; ++j) {
+        const float v = lane < LD ? aos[(uint64_t)(ovals[j] & ~OTHER_TIE) * LD + lane] : 0.0f;
+        sum += (double)v;
+        sabs += (double)__builtin_fabsf(v);
+        if (v != 0.0f) emin = min(emin, ulp_exp(v));
+    }
+    cnt += o1 - o0;
+    if (lane == 0) counts[cl] = cnt;
+    if (cnt == 0) return;  // empty: re-seeded
+    const bool exact = lane >= d || sum_is_exact(sabs, emin);
+    if (__ballot(!exact) == 0) {
+        if (lane < d) cen[(uint64_t)lane * k + cl] = (float)(sum / (double)cnt);
+    } else if (lane == 0) {
+        flagged[atomicAdd(nflagged, 1u)] = cl;
+    }
+}
+
+// one workgroup per cluster the certificate fails: its members are the decided points of its
+// tile-half's grouped range that carry its label (fix-up ties included, with their final
+// label) and its pair / ambiguous points among the label-sorted others; sorted into point
+// order (bitonic, LDS), then lane = dimension runs calcAverage's sequential f64 sum.  More
+// than NS_CAP members: listed in big (the caller sums those over the member sort).
+constexpr uint32_t NS_CAP = 4096;
+__global__ __launch_bounds__(256) void k_nd_seq(const float *__restrict__ aos, int d, int k,
+                                                const uint32_t *__restrict__ flagged, const uint32_t *__restrict__ nflagged,
+                                                const uint2 *__restrict__ grouped, const uint32_t *__restrict__ hist,
+                                                const uint32_t *__restrict__ cend, const uint32_t *__restrict__ labels,
+                                                const uint32_t *__restrict__ ostart,
+                                                const uint32_t *__restrict__ ovals, float *__restrict__ cen,
+                                                uint32_t *__restrict__ big, uint32_t *__restrict__ nbig) {
+    __shared__ uint32_t m[NS_CAP];
+    __shared__ uint32_t cnt_s;
+    const uint32_t nf = *nflagged;
+    for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    const uint32_t cl = flagged[f], code = code_of(cl);
+    if (threadIdx.x == 0) cnt_s = 0u;
+    __syncthreads();
+    auto put = [&](uint32_t p) {
+        const uint32_t i = atomicAdd(&cnt_s, 1u);
+        if (i < NS_CAP) m[i] = p;
+    };
+    for (uint32_t i = cend[code] - hist[code] + threadIdx.x; i < cend[code]; i += 256) {
+        const uint32_t p = grouped[i].x;
+        if (labels[p] == cl) put(p);
+    }
+    for (uint32_t j = ostart[cl] + threadIdx.x; j < ostart[cl + 1]; j += 256) {
+        const uint32_t v = ovals[j];
+        if (!(v & OTHER_TIE)) put(v);
+    }
+    __syncthreads();
+    const uint32_t cnt = cnt_s;
+    if (cnt > NS_CAP) {  // summed over the member sort (nd_fused_update)
+        if (threadIdx.x == 0) big[atomicAdd(nbig, 1u)] = cl;
+        __syncthreads();
+        continue;
+    }
+    uint32_t np2 = 1;
+    while (np2 < cnt) np2 <<= 1;
+    for (uint32_t i = cnt + threadIdx.x; i < np2; i += 256) m[i] = 0xffffffffu;
+    __syncthreads();
+    for (uint32_t sz = 2; sz <= np2; sz <<= 1)
+        for (uint32_t st = sz >> 1; st > 0; st >>= 1) {
+            for (uint32_t i = threadIdx.x; i < np2; i += 256) {
+                const uint32_t j = i ^ st;
+                if (j > i) {
+                    const bool up = (i & sz) == 0;
+                    const uint32_t a = m[i], b = m[j];
+                    if ((a > b) == up) {
+                        m[i] = b;
+                        m[j] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const int lane = threadIdx.x;
+    if (lane < d && cnt) {
+        const int ld = aos_ld(d);
+        double sum = 0;
+        for (uint32_t i = 0; i < cnt; ++i) sum += (double)aos[(uint64_t)m[i] * ld + lane];
+        cen[(uint64_t)lane * k + cl] = (float)(sum / (double)cnt);
+    }
+    __syncthreads();  // m and cnt_s are reused by the next flagged cluster
+    }
+}
+
 // pair points with the point row broadcast by DPP: lanes 0-15 score the rows of the first
 // tile-half, lanes 16-31 the second (two DPP rows); each lane loads one float4 slice of the
 // point, rows come from the coalesced cfix layout
@@ -999,10 +1318,12 @@ __global__ __launch_bounds__(256) void k_sumnd(const T *__restrict__ aos, int d,
                                                const uint32_t *__restrict__ members,
                                                const uint32_t *__restrict__ start, int k, float *__restrict__ cen,
                                                uint32_t big, uint32_t cap, uint32_t *__restrict__ big_list,
-                                               uint32_t *__restrict__ nbig) {
+                                               uint32_t *__restrict__ nbig, const uint32_t *__restrict__ only,
+                                               const uint32_t *__restrict__ nonly) {
     const int lane = threadIdx.x & 63;
-    const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (cl >= (uint32_t)k) return;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (only ? w >= *nonly : w >= (uint32_t)k) return;
+    const uint32_t cl = only ? only[w] : w;  // only: the listed clusters (one wave each)
     const uint32_t s0 = start[cl], s1 = start[cl + 1];
     if (s1 - s0 > big) {  // huge clusters: listed for k_big_* (at most cap of them exist)
         if (lane == 0) {
@@ -1166,7 +1487,7 @@ void launch_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32
     auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
     ST_HIP(hipMemsetAsync(nlist, 0, 4, c->stream));
     hipLaunchKernelGGL(k_sumnd<T>, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen, big,
-                       cap, list, nlist);
+                       cap, list, nlist, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     if (n > big) {
         const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
         auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
@@ -1285,7 +1606,7 @@ __global__ __launch_bounds__(256) void k_rows_aos(const float *__restrict__ cen,
 }
 
 uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
-                        uint32_t *labels, km::State *dstate, bool walk_ties);
+                        uint32_t *labels, km::State *dstate, bool walk_ties, NdFused *fz = nullptr);
 }  // namespace
 
 // The assign over the distinct centroid rows: when several centroids share a row (duplicated
@@ -1294,7 +1615,8 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
 // meets first (kd_group_labels, a descent of the tree); exact ties between distinct rows go to
 // the walk over the whole tree.  Without shared rows this is the plain assign.
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
-               km::State *dstate) {
+               km::State *dstate, NdFused *fz) {
+    if (fz) fz->valid = false;
     CenGroups g;
     if (k > 1 && !getenv("ST_NO_CEN_GROUPS") && cen_groups(c, d, k, cen, &g)) {
         const uint32_t nties = nd_assign_core(c, dcols, d, n, (int)g.kr, g.cen_r, labels, dstate, false);
@@ -1315,14 +1637,14 @@ void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, c
         mark(c, "kn.exact");
         return;
     }
-    nd_assign_core(c, dcols, d, n, k, cen, labels, dstate, true);
+    nd_assign_core(c, dcols, d, n, k, cen, labels, dstate, true, fz);
 }
 
 namespace {
 // the exact assign against the k centroids cen; exact ties go to the KdTree walk over these
 // centroids (walk_ties) or are left listed in kn.ties for the caller: returns their count
 uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
-                        uint32_t *labels, km::State *dstate, bool walk_ties) {
+                        uint32_t *labels, km::State *dstate, bool walk_ties, NdFused *fz) {
     ST_REQUIRE(c->kn_n == n && c->kn_d == d, ST_ERR_ARG, "kmeans assign: point set not prepared");
     ST_REQUIRE(k <= (1 << 24), ST_ERR_UNSUPPORTED, "kmeans: K too large");
     const int ks = kp_of(d) / 16;
@@ -1373,12 +1695,35 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
         auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
         auto *grouped = wsT<uint2>(c, "kn.fbpts2", n);
-        scan_u32(c, hist, cursor, ncodes, ndec);
+        const bool fused = fz && fz->want && walk_ties;
+        auto *soff = fused ? wsT<uint32_t>(c, "kn.fasoff", (size_t)ncodes + 1) : nullptr;
+        if (fused)  // slice offsets and the codes' starts in one workgroup
+            hipLaunchKernelGGL(k_fa_slices, dim3(1), dim3(FS_T), 0, c->stream, hist, ncodes, soff, cursor, ndec);
+        else
+            scan_u32(c, hist, cursor, ncodes, ndec);
         hipLaunchKernelGGL(k_code_scatter, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream, labels,
                            (uint32_t)n, ncodes, cursor, grouped);
         ST_LAUNCH_CHECK();
         const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
-        if (ld == 48)
+        if (fused) {
+            // the fix-up with the decided points' sums (k_fixrow_acc), one slice per workgroup
+            const uint64_t slices = ncodes + n / FA_SL + 1;
+            auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
+            auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
+            auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
+            auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+            if (ld == 48)
+                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+            else if (ld == 24)
+                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+            else
+                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+            fz->valid = true;
+            fz->ncodes = ncodes;
+        } else if (ld == 48)
             hipLaunchKernelGGL(k_fixrow_b<48>, g, dim3(256), 0, c->stream, aos, d, caos, k, grouped, ndec, labels,
                                ties, dstate);
         else if (ld == 24)
@@ -1397,6 +1742,11 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     const uint32_t npair = h->pairs;
+    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
+        fz->nties_fix = h->ties;
+        fz->npair = npair;
+        fz->namb = h->amb;
+    }
     if (npair) {
         KTimer kt(c, "kn.fixpair");
         const dim3 g((npair * 32 + 255) / 256);
@@ -1463,6 +1813,75 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
 }
 }  // namespace
 
+namespace {
+// the update after a fused fix-up: the other points' sums by label, the certified centroids,
+// the sequential sums of the clusters the certificate fails.  Returns false when a flagged
+// cluster has more members than k_nd_seq takes: those are summed over the member sort.
+bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, float *cen,
+                     uint32_t *counts, State *dstate) {
+    KTimer kt(c, "kn.sumnd");
+    const int ld = aos_ld(d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
+    const uint64_t slices = fz.ncodes + n / FA_SL + 1;
+    auto *soff = wsT<uint32_t>(c, "kn.fasoff", (size_t)fz.ncodes + 1);
+    auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
+    auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
+    auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
+    auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+    const uint32_t m = fz.npair + fz.namb + fz.nties_fix;
+    auto *okeys = wsT<uint32_t>(c, "kn.okeys", (size_t)m + 1);
+    auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
+    auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
+    if (m) {
+        hipLaunchKernelGGL(k_others_keys, dim3(grid_for(m, 256, 4096)), dim3(256), 0, c->stream,
+                           wsT<uint32_t>(c, "kn.pairpts", n), fz.npair, wsT<uint32_t>(c, "kn.amb", n), fz.namb,
+                           wsT<uint32_t>(c, "kn.ties", n), fz.nties_fix, labels, okeys, ovals);
+        ST_LAUNCH_CHECK();
+        int bits = 1;
+        while ((1ull << bits) < (uint64_t)k) ++bits;
+        radix_sort_u32(c, okeys, ovals, m, 0, bits, "kn.osort");
+    }
+    bounds_from_sorted(c, okeys, m, k, ostart);
+    auto *flagged = wsT<uint32_t>(c, "kn.flagged", (size_t)k);
+    auto *nflag = wsT<uint32_t>(c, "kn.nflag", 2);  // [0] flagged clusters, [1] collect overflow
+    ST_HIP(hipMemsetAsync(nflag, 0, 8, c->stream));
+    const dim3 g((k + 3) / 4);
+    if (ld == 48)
+        hipLaunchKernelGGL(k_nd_combine<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, cen, counts, flagged, nflag);
+    else if (ld == 24)
+        hipLaunchKernelGGL(k_nd_combine<24>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, cen, counts, flagged, nflag);
+    else
+        hipLaunchKernelGGL(k_nd_combine<12>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, cen, counts, flagged, nflag);
+    ST_LAUNCH_CHECK();
+    // the clusters the certificate fails: their members in point order, the sequential sums
+    // (grid-stride over the flagged list; none: every workgroup returns at once)
+    auto *big = wsT<uint32_t>(c, "kn.big", (size_t)k);
+    hipLaunchKernelGGL(k_nd_seq, dim3(256), dim3(256), 0, c->stream, aos, d, k, flagged, nflag,
+                       wsT<uint2>(c, "kn.fbpts2", n), wsT<uint32_t>(c, "kn.fbhist", fz.ncodes),
+                       wsT<uint32_t>(c, "kn.fbcur", fz.ncodes), labels, ostart, ovals, cen, big, nflag + 1);
+    ST_LAUNCH_CHECK();
+    auto *h = static_cast<uint32_t *>(pinned_slot(c, "kn.hflag", 8));
+    ST_HIP(hipMemcpyAsync(h, nflag, 8, hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipStreamSynchronize(c->stream));
+    if (getenv("ST_DEBUG"))
+        fprintf(stderr, "[st kmeans] fused update: others=%u uncertified clusters=%u over %u members=%u\n", m, h[0],
+                NS_CAP, h[1]);
+    if (h[1]) {  // uncertified clusters too large for k_nd_seq: the member sort, then their sums
+        auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
+        auto *members = wsT<uint32_t>(c, "kn.members", n);
+        auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
+        member_sort(c, labels, n, k, sorted_labels, members, start);
+        hipLaunchKernelGGL(k_sumnd<float>, dim3((h[1] + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k,
+                           cen, 0xffffffffu, 0u, (uint32_t *)nullptr, (uint32_t *)nullptr, big, nflag + 1);
+        ST_LAUNCH_CHECK();
+    }
+    return true;
+}
+}  // namespace
+
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels,
                    const double *const *sum64) {
@@ -1480,20 +1899,27 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
     auto *members = wsT<uint32_t>(c, "kn.members", n);
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
+    auto *counts = wsT<uint32_t>(c, "kn.counts", (size_t)k);
     nd_prepare(c, dcols, d, n);
     const size_t cbytes = (size_t)k * d * sizeof(float);
     for (int it = 0; it < iters; ++it) {
         if (c->verify && it == iters - 1)
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
-        nd_assign(c, dcols, d, n, k, cen, labels, dstate);
+        NdFused fz;
+        fz.want = !aos64 && !getenv("ST_ND_SORT");
+        nd_assign(c, dcols, d, n, k, cen, labels, dstate, &fz);
         // update
-        member_sort(c, labels, n, k, sorted_labels, members, start);
-        {
-            KTimer kt(c, "kn.sumnd");
-            if (aos64) launch_sums<double>(c, aos64, d, n, k, members, start, cen);
-            else launch_sums<float>(c, aos, d, n, k, members, start, cen);
+        if (fz.valid && nd_fused_update(c, d, n, k, fz, labels, cen, counts, dstate)) {
+            reseed_empty_counts(c, dcols, d, n, k, counts, ddraws, ndraws, dstate, cen);
+        } else {
+            member_sort(c, labels, n, k, sorted_labels, members, start);
+            {
+                KTimer kt(c, "kn.sumnd");
+                if (aos64) launch_sums<double>(c, aos64, d, n, k, members, start, cen);
+                else launch_sums<float>(c, aos, d, n, k, members, start, cen);
+            }
+            reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);
         }
-        reseed_empty(c, dcols, d, n, k, start, ddraws, ndraws, dstate, cen);
         mark(c, "kn.update");
     }
     if (c->verify && iters > 0) {

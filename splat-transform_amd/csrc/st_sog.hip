@@ -427,69 +427,99 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         }
     } joiner{colours};
 
-    // Morton order (write-sog.ts:42-49)
-    auto *idx = wsT<uint32_t>(c, "sog.idx", n);
-    iota_u32(c, idx, n);
-    if (src.pos64[0]) morton_order_dev_f64(c, src.pos64[0], src.pos64[1], src.pos64[2], idx, n);
-    else morton_order_dev(c, m[0], m[1], m[2], idx, n);
-    // the texture kernels run in scatter form: row r (read in input order, coalesced) writes
-    // texel pos[r], one 4-byte store, instead of gathering 3-4 values per texel at random
+    // Morton order, extents and the means / quats textures on a third context from their own
+    // host thread (c->aux->aux), beside the scales' cluster1d here: only the texture writes
+    // after the k-means wait for the texel positions
     auto *pos = wsT<uint32_t>(c, "sog.pos", n);
-    hipLaunchKernelGGL(k_invert, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, idx, n, pos);
-    ST_LAUNCH_CHECK();
-    mark(c, "sog.morton");
     const unsigned g = grid_for(n, 256, 8192);
+    if (!aux->aux) ST_REQUIRE(st_ctx_create(c->device, &aux->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    st_ctx *mc = aux->aux;
+    hipEvent_t ev_pos;
+    ST_HIP(hipEventCreateWithFlags(&ev_pos, hipEventDisableTiming));
+    {
+        hipEvent_t ev;  // the textures' clears above and the caller's columns
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, c->stream));
+        ST_HIP(hipStreamWaitEvent(mc->stream, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+    }
+    std::exception_ptr err_m;
+    std::thread order_th([&] {
+        try {
+            use_device(mc);
+            // Morton order (write-sog.ts:42-49)
+            auto *idx = wsT<uint32_t>(mc, "sog.idx", n);
+            iota_u32(mc, idx, n);
+            if (src.pos64[0]) morton_order_dev_f64(mc, src.pos64[0], src.pos64[1], src.pos64[2], idx, n);
+            else morton_order_dev(mc, m[0], m[1], m[2], idx, n);
+            // the texture kernels run in scatter form: row r (read in input order, coalesced) writes
+            // texel pos[r], one 4-byte store, instead of gathering 3-4 values per texel at random
+            hipLaunchKernelGGL(k_invert, dim3(grid_for(n, 256, 8192)), dim3(256), 0, mc->stream, idx, n, pos);
+            ST_LAUNCH_CHECK();
 
-    // means (write-sog.ts:161-187)
-    double lo[3], hi[3];
-    if (src.pos64[0]) {
-        auto *mm = wsT<unsigned long long>(c, "sog.mm64", 6);
-        const unsigned long long init[6] = {~0ull, 0ull, ~0ull, 0ull, ~0ull, 0ull};
-        unsigned long long hmm[6];
-        ST_HIP(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(k_mm64, dim3(grid_for(n, 256, 1024)), dim3(256), 0, c->stream, src.pos64[0], src.pos64[1],
-                           src.pos64[2], n, mm);
-        ST_LAUNCH_CHECK();
-        ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = hmm[2 * a] == ~0ull ? HUGE_VAL : dkey_inv(hmm[2 * a]);
-            hi[a] = hmm[2 * a + 1] == 0ull ? -HUGE_VAL : dkey_inv(hmm[2 * a + 1]);
+            // means (write-sog.ts:161-187)
+            double lo[3], hi[3];
+            if (src.pos64[0]) {
+                auto *mm = wsT<unsigned long long>(mc, "sog.mm64", 6);
+                const unsigned long long init[6] = {~0ull, 0ull, ~0ull, 0ull, ~0ull, 0ull};
+                unsigned long long hmm[6];
+                ST_HIP(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, mc->stream));
+                hipLaunchKernelGGL(k_mm64, dim3(grid_for(n, 256, 1024)), dim3(256), 0, mc->stream, src.pos64[0], src.pos64[1],
+                                   src.pos64[2], n, mm);
+                ST_LAUNCH_CHECK();
+                ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, mc->stream));
+                ST_HIP(hipStreamSynchronize(mc->stream));
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = hmm[2 * a] == ~0ull ? HUGE_VAL : dkey_inv(hmm[2 * a]);
+                    hi[a] = hmm[2 * a + 1] == 0ull ? -HUGE_VAL : dkey_inv(hmm[2 * a + 1]);
+                }
+            } else {
+                auto *mm = wsT<uint32_t>(mc, "sog.mm", 6);
+                minmax_keys_dev(mc, m, 3, n, mm);  // [min, max] keys of x, y, z (NaN skipped)
+                uint32_t hmm[6];
+                ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, mc->stream));
+                ST_HIP(hipStreamSynchronize(mc->stream));
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = hmm[2 * a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[2 * a]);
+                    hi[a] = hmm[2 * a + 1] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[2 * a + 1]);
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                meta->means_min[a] = js::log_transform(lo[a]);
+                meta->means_max[a] = js::log_transform(hi[a]);
+            }
+            if (src.pos64[0]) {
+                MeansArgs<double> ma{};
+                for (int a = 0; a < 3; ++a) ma.c[a] = src.pos64[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
+                hipLaunchKernelGGL(k_means_tex<double>, dim3(g), dim3(256), 0, mc->stream, ma, (const uint32_t *)nullptr, pos,
+                                   n, (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+            } else {
+                MeansArgs<float> ma{};
+                for (int a = 0; a < 3; ++a) ma.c[a] = m[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
+                hipLaunchKernelGGL(k_means_tex<float>, dim3(g), dim3(256), 0, mc->stream, ma, (const uint32_t *)nullptr, pos, n,
+                                   (uint32_t *)out->means_l, (uint32_t *)out->means_u);
+            }
+            if (src.rot64[0])
+                hipLaunchKernelGGL(k_quats_tex<double>, dim3(g), dim3(256), 0, mc->stream, src.rot64[0], src.rot64[1],
+                                   src.rot64[2], src.rot64[3], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
+            else
+                hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, mc->stream, m[10], m[11], m[12], m[13],
+                                   (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
+            ST_LAUNCH_CHECK();
+            ST_HIP(hipEventRecord(ev_pos, mc->stream));
+            ST_HIP(hipStreamSynchronize(mc->stream));
+        } catch (...) {
+            err_m = std::current_exception();
         }
-    } else {
-        auto *mm = wsT<uint32_t>(c, "sog.mm", 6);
-        minmax_keys_dev(c, m, 3, n, mm);  // [min, max] keys of x, y, z (NaN skipped)
-        uint32_t hmm[6];
-        ST_HIP(hipMemcpyAsync(hmm, mm, sizeof hmm, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = hmm[2 * a] == 0xffffffffu ? HUGE_VAL : (double)fkey_inv_(hmm[2 * a]);
-            hi[a] = hmm[2 * a + 1] == 0u ? -HUGE_VAL : (double)fkey_inv_(hmm[2 * a + 1]);
+    });
+    struct Joiner2 {
+        std::thread &th;
+        hipEvent_t ev;
+        ~Joiner2() {
+            if (th.joinable()) th.join();
+            (void)hipEventDestroy(ev);
         }
-    }
-    for (int a = 0; a < 3; ++a) {
-        meta->means_min[a] = js::log_transform(lo[a]);
-        meta->means_max[a] = js::log_transform(hi[a]);
-    }
-    if (src.pos64[0]) {
-        MeansArgs<double> ma{};
-        for (int a = 0; a < 3; ++a) ma.c[a] = src.pos64[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
-        hipLaunchKernelGGL(k_means_tex<double>, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos,
-                           n, (uint32_t *)out->means_l, (uint32_t *)out->means_u);
-    } else {
-        MeansArgs<float> ma{};
-        for (int a = 0; a < 3; ++a) ma.c[a] = m[a], ma.mn[a] = meta->means_min[a], ma.mx[a] = meta->means_max[a];
-        hipLaunchKernelGGL(k_means_tex<float>, dim3(g), dim3(256), 0, c->stream, ma, (const uint32_t *)nullptr, pos, n,
-                           (uint32_t *)out->means_l, (uint32_t *)out->means_u);
-    }
-    if (src.rot64[0])
-        hipLaunchKernelGGL(k_quats_tex<double>, dim3(g), dim3(256), 0, c->stream, src.rot64[0], src.rot64[1],
-                           src.rot64[2], src.rot64[3], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
-    else
-        hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, c->stream, m[10], m[11], m[12], m[13],
-                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
-    ST_LAUNCH_CHECK();
-    mark(c, "sog.means_quats");
+    } joiner2{order_th, ev_pos};
 
     uint64_t cursor = 0;
     auto *lab = wsT<uint8_t>(c, "sog.lab", n * 3);
@@ -497,6 +527,10 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
     // scales (write-sog.ts:245-251)
     cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    order_th.join();
+    if (err_m) std::rethrow_exception(err_m);
+    ST_HIP(hipStreamWaitEvent(c->stream, ev_pos, 0));
+    mark(c, "sog.morton");
     hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
                        (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
     ST_LAUNCH_CHECK();

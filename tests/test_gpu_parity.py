@@ -129,6 +129,29 @@ def test_sog_golden(ctx):
             same_bits(np.array(meta.shn_codebook, np.float32), np.array(ref['shN']['codebook'], np.float32))
 
 
+@pytest.mark.parametrize('mode', ['', 'ST_ND_SORT'])
+@pytest.mark.parametrize('n,d,k,tiny', [(30_000, 9, 256, 0.002), (40_000, 9, 8, 0.002), (20_000, 45, 1024, 0.0005)])
+def test_kmeans_nd_uncertified_sums_vs_oracle(ctx, n, d, k, tiny, mode, monkeypatch):
+    """N-D k-means whose cluster sums fail the exactness certificate in some dimensions (tiny
+    members): the fused fix-up's partials are discarded for those clusters and their members
+    are summed in point order (k_nd_seq); with K = 8 the flagged clusters hold more members
+    than that kernel takes and the iteration falls back to the member sort.  ST_ND_SORT: the
+    member-sort update every iteration."""
+    if mode:
+        monkeypatch.setenv(mode, '1')
+    rng = np.random.default_rng(n + k)
+    cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
+    for c in cols:
+        m = rng.random(n) < tiny
+        c[m] *= np.float32(1e-9)
+    draws = oracle.mulberry32(n + k + 1, 4 * k * 4 + 64)
+    cent, labels, used = ctx.kmeans(cols, k, 3, draws)
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, 3, draws)
+    assert rc == 0 and used == oused
+    same_bits(labels, olabels)
+    same_bits(cent, ocent)
+
+
 @pytest.mark.parametrize('n,d,k,iters', [(20_000, 45, 1024, 2), (30_000, 9, 2048, 2), (60_000, 1, 256, 4)])
 def test_kmeans_vs_oracle(ctx, n, d, k, iters):
     rng = np.random.default_rng(n + d)
@@ -141,16 +164,17 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters):
     same_bits(cent, ocent)
 
 
-@pytest.mark.parametrize('mode', ['', 'ST_K1_TILES', 'ST_K1_SORT'])
+@pytest.mark.parametrize('mode', ['', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX'])
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
 def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
     """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
     hold tiny members, so the sequential f64 sum rounds -- a few events (the replay) or many
-    (the sequential fallback).  mode: the flagged clusters' members gathered by the wave
-    kernels (default), the tile kernels (ST_K1_TILES), or every iteration's member sort
-    (ST_K1_SORT)."""
+    (the sequential fallback).  mode: the iteration queued without read-backs (default), the
+    flagged count read back each iteration (ST_K1_SYNC), the flagged clusters' members gathered
+    by the tile kernels (ST_K1_TILES), every iteration's member sort (ST_K1_SORT), or the queued
+    run abandoned at the first flagged cluster and rerun synchronised (ST_K1_FF_MAX=0)."""
     if mode:
-        monkeypatch.setenv(mode, '1')
+        monkeypatch.setenv(mode, '0' if mode == 'ST_K1_FF_MAX' else '1')
     rng = np.random.default_rng(77)
     n = 300_000
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
