@@ -1011,6 +1011,7 @@ struct Part1 {
     uint32_t cnt;
 };
 constexpr uint32_t A1_G = 1024;  // most workgroups (partials) of the accumulating assign
+constexpr int A1_CELLS = 4096;   // bracket cells of the accumulating assign
 constexpr int FF_MAX = 8;         // flagged clusters the wave kernels take (more: the tile kernels)
 
 // workgroups for ntiles tiles: at most A1_G, every workgroup the same number of tiles
@@ -1030,7 +1031,7 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
     __shared__ uint32_t si[256], skey[256];
     __shared__ uint16_t cc[256];
     __shared__ uint8_t chk_l[256], chk_r[256];
-    __shared__ uint32_t first[KD1_CELLS + 1];
+    __shared__ uint32_t first[A1_CELLS + 1];
     __shared__ double hs[256], ha[256];
     __shared__ int32_t he[256];
     __shared__ uint32_t hc[256];
@@ -1055,10 +1056,10 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
     __syncthreads();
     const float lo = sv[0], hi = sv[k - 1];
     const float span = hi - lo;
-    const float inv = (span > 0.f && span < __builtin_inff()) ? (float)KD1_CELLS / span : 0.f;
+    const float inv = (span > 0.f && span < __builtin_inff()) ? (float)A1_CELLS / span : 0.f;
     auto cell = [&](float x) -> int {
         const float u = (x - lo) * inv;
-        return (int)__builtin_fminf(__builtin_fmaxf(u, 0.f), (float)(KD1_CELLS - 1));
+        return (int)__builtin_fminf(__builtin_fmaxf(u, 0.f), (float)(A1_CELLS - 1));
     };
     if (t < k) {
         cc[t] = (uint16_t)cell(sv[t]);
@@ -1073,7 +1074,7 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
         chk_r[t] = (t + 1 < k && (gr == 0.0 || gl < 0.0 || gl >= gr * R48)) ? 1 : 0;
     }
     __syncthreads();
-    for (int g = t; g <= KD1_CELLS; g += F1_T) {
+    for (int g = t; g <= A1_CELLS; g += F1_T) {
         int a = 0, b = k;
         while (a < b) {
             const int m = (a + b) >> 1;
@@ -1108,12 +1109,26 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
             const int ue = (int)first[g + 1];
             while (u < ue && sv[u] <= pf) ++u;
             const int L = u - 1, R = u;
-            const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
-            const double dr = R < k ? dist(R, p) : __builtin_inf();
-            const double m = __builtin_fmin(dl, dr);
-            const bool tie = dl == dr || (L >= 1 && chk_l[L] && dist(L - 1, p) == m) ||
-                             (R + 1 < k && chk_r[R] && dist(R + 1, p) == m);
-            const uint32_t lab = !tie ? si[dl < dr ? L : R] : kd1_walk(p, k, val, idx);
+            // f32 screen: a, b are p - sv[L], sv[R] - p up to 2^-24 relative; a clear winner with
+            // unflagged outer neighbours has a strictly smaller rounded f64 distance than any
+            // other centroid, so no f64 work (chk_l / chk_r: see above)
+            int win = -1;
+            if (L >= 0 && R < k && !chk_l[L] && !chk_r[R]) {
+                const float a = pf - sv[L], b = sv[R] - pf;
+                if (a < b * 0.99999f) win = L;
+                else if (b < a * 0.99999f) win = R;
+            }
+            uint32_t lab;
+            if (win >= 0) {
+                lab = si[win];
+            } else {
+                const double dl = L >= 0 ? dist(L, p) : __builtin_inf();
+                const double dr = R < k ? dist(R, p) : __builtin_inf();
+                const double m = __builtin_fmin(dl, dr);
+                const bool tie = dl == dr || (L >= 1 && chk_l[L] && dist(L - 1, p) == m) ||
+                                 (R + 1 < k && chk_r[R] && dist(R + 1, p) == m);
+                lab = !tie ? si[dl < dr ? L : R] : kd1_walk(p, k, val, idx);
+            }
             if (lab8) lab8[i] = (uint8_t)lab;
             if (labels) labels[i] = lab;
             atomicAdd(&hc[lab], 1u);

@@ -228,16 +228,15 @@ void build_header(int width, int height, bool alpha_used, const uint32_t *hist, 
     // main image
     bw.put(0, 1);  // no colour cache
     bw.put(0, 1);  // one prefix-code group
-    out.tab.assign(4 * 256, 0);
-    std::vector<uint64_t> dist(kDistAlphabet, 0);
-    for (int ch = 0; ch < 4; ++ch) {
-        const int alphabet = ch == 0 ? kGreenAlphabet : 256;
-        std::vector<uint64_t> cnt(alphabet, 0);
-        for (int s = 0; s < 256; ++s) cnt[s] = hist[ch * 256 + s];
-        Code code = write_code(bw, cnt.data(), alphabet);
-        for (int s = 0; s < 256; ++s) out.tab[ch * 256 + s] = ((uint32_t)code.len[s] << 16) | code.rev[s];
+    out.tab.assign(kTabSize, 0);
+    const int off[5] = {kOffG, kOffR, kOffB, kOffA, kOffD};
+    const int size[5] = {kGreenAlphabet, 256, 256, 256, kDistAlphabet};
+    for (int ch = 0; ch < 5; ++ch) {
+        std::vector<uint64_t> cnt(size[ch], 0);
+        for (int s = 0; s < size[ch]; ++s) cnt[s] = hist[off[ch] + s];
+        Code code = write_code(bw, cnt.data(), size[ch]);
+        for (int s = 0; s < size[ch]; ++s) out.tab[off[ch] + s] = ((uint32_t)code.len[s] << 16) | code.rev[s];
     }
-    write_code(bw, dist.data(), kDistAlphabet);
 }
 
 }  // namespace vp8l

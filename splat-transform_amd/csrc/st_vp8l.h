@@ -20,6 +20,10 @@ constexpr int kPredBits = 4;           // predictor blocks of 16 x 16 pixels
 constexpr int kGreenAlphabet = 280;    // 256 literals + 24 length prefixes (no colour cache)
 constexpr int kDistAlphabet = 40;
 constexpr int kMaxCodeLen = 15;
+// the device histogram / code-table layout: G (280: literals + length prefixes), R, B, A (256
+// each), distance (40)
+constexpr int kOffG = 0, kOffR = kGreenAlphabet, kOffB = kOffR + 256, kOffA = kOffB + 256, kOffD = kOffA + 256;
+constexpr int kTabSize = kOffD + kDistAlphabet;
 
 // LSB-first bit writer (the VP8L bit order)
 struct BitWriter {
@@ -49,9 +53,9 @@ Code write_code(BitWriter &bw, const uint64_t *counts, int alphabet);
 // The header bits of one image: everything before the main image's pixel
 // stream (VP8L signature, size, predictor transform with its entropy-coded
 // sub-image, colour-cache and meta-code flags, the five prefix codes).
-// hist: residual histograms in channel order G, R, B, A (256 bins each);
-// modes: the predictor sub-image (one byte per 16 x 16 block, row-major).
-// tab (out): 4 x 256 device table entries (len << 16 | reversed code), G, R, B, A.
+// hist: symbol histograms in the kOff* layout (kTabSize bins: G with the length prefixes,
+// R, B, A, distance); modes: the predictor sub-image (one byte per 16 x 16 block, row-major).
+// tab (out): kTabSize device table entries (len << 16 | reversed code) in the same layout.
 struct Header {
     BitWriter bw;
     std::vector<uint32_t> tab;

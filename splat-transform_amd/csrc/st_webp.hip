@@ -11,7 +11,11 @@
 //                   scored on the block (sum of |signed residual|), the cheapest
 //                   wins, residuals (pixel - prediction per channel, mod 256) are
 //                   written as ARGB words                  read 4 B (+ neighbours), write 4 B
-//   k_vp8l_hist     4 x 256 residual histograms (LDS-private, one flush per group)  read 4 B
+//   k_vp8l_runs     per 4,096-pixel group: runs of >= 3 residuals equal to their left
+//                   neighbour become one LZ77 copy (distance code 2: the pixel to the
+//                   left; length <= 4,096), tokens: literal / copy length / covered
+//   k_vp8l_hist     symbol histograms (literal channels, length prefixes, distance;
+//                   LDS-private, one flush per group)                  read 4 + 2 B
 //   host            canonical length-limited prefix codes + header bits (st_vp8l.cpp)
 //   k_vp8l_bits     bits per 4,096-pixel group (table lookups in LDS)     read 4 B
 //   k_vp8l_scan     exclusive bit offsets of the groups (one workgroup) + RIFF sizes
@@ -35,6 +39,28 @@ constexpr int PB = 1 << vp8l::kPredBits;  // predictor block edge (16)
 constexpr int EMIT_PP = 16;               // pixels per thread in the bit kernels
 constexpr int EMIT_PIX = 256 * EMIT_PP;   // pixels per group
 constexpr int EMIT_WORDS = EMIT_PIX * 60 / 32 + 2;
+
+// tokens: a literal pixel, the start of an LZ77 copy (its length), or a pixel a copy covers
+constexpr uint16_t TOK_LIT = 0, TOK_COVERED = 0xffffu;
+constexpr uint32_t RUN_MIN = 3;                // shortest run coded as a copy
+constexpr uint32_t DIST_LEFT_PREFIX = 1;       // distance code 2 = (1, 0): the pixel to the left
+
+// LZ77 prefix coding of a length or distance value v >= 1 (RFC 9649 5.2.2): prefix code and
+// extra bits
+__device__ inline void prefix_of(uint32_t v, uint32_t &prefix, uint32_t &nextra, uint32_t &extra) {
+    if (v <= 4) {
+        prefix = v - 1;
+        nextra = 0;
+        extra = 0;
+        return;
+    }
+    const uint32_t d = v - 1;
+    const uint32_t hb = 31 - __builtin_clz(d);
+    const uint32_t second = (d >> (hb - 1)) & 1u;
+    nextra = hb - 1;
+    extra = d & ((1u << nextra) - 1);
+    prefix = 2 * hb + second;
+}
 
 // RGBA8 bytes (little endian word R | G<<8 | B<<16 | A<<24) -> VP8L ARGB word
 __device__ inline uint32_t to_argb(uint32_t v) { return (v & 0xff00ff00u) | ((v & 0xffu) << 16) | ((v >> 16) & 0xffu); }
@@ -178,29 +204,56 @@ __global__ __launch_bounds__(256) void k_vp8l_predict(const uint8_t *__restrict_
     resid[(size_t)y * w + x] = sub_pixels(C, pred);
 }
 
-// histograms in channel order G, R, B, A
-__global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ resid, uint64_t npix,
+// symbol histograms in the vp8l::kOff* layout
+__global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ resid,
+                                                   const uint16_t *__restrict__ tok, uint64_t npix,
                                                    uint32_t *__restrict__ hist) {
-    __shared__ uint32_t hs[4 * 256];
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) hs[i] = 0;
+    __shared__ uint32_t hs[vp8l::kTabSize];
+    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) hs[i] = 0;
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += stride) {
+        const uint32_t t = tok[i];
+        if (t == TOK_COVERED) continue;
+        if (t != TOK_LIT) {
+            uint32_t lp, ne, ex;
+            prefix_of(t, lp, ne, ex);
+            atomicAdd(&hs[vp8l::kOffG + 256 + lp], 1u);
+            atomicAdd(&hs[vp8l::kOffD + DIST_LEFT_PREFIX], 1u);
+            continue;
+        }
         const uint32_t r = resid[i];
-        atomicAdd(&hs[0 * 256 + ((r >> 8) & 0xff)], 1u);
-        atomicAdd(&hs[1 * 256 + ((r >> 16) & 0xff)], 1u);
-        atomicAdd(&hs[2 * 256 + (r & 0xff)], 1u);
-        atomicAdd(&hs[3 * 256 + (r >> 24)], 1u);
+        atomicAdd(&hs[vp8l::kOffG + ((r >> 8) & 0xff)], 1u);
+        atomicAdd(&hs[vp8l::kOffR + ((r >> 16) & 0xff)], 1u);
+        atomicAdd(&hs[vp8l::kOffB + (r & 0xff)], 1u);
+        atomicAdd(&hs[vp8l::kOffA + (r >> 24)], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 4 * 256; i += 256)
+    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256)
         if (hs[i]) atomicAdd(&hist[i], hs[i]);
 }
 
-// code of one residual: (bits, length) with G, R, B, A concatenated LSB-first
-__device__ inline uint64_t pixel_code(const uint32_t *tab, uint32_t r, int &n) {
-    const uint32_t eg = tab[0 * 256 + ((r >> 8) & 0xff)], er = tab[1 * 256 + ((r >> 16) & 0xff)];
-    const uint32_t eb = tab[2 * 256 + (r & 0xff)], ea = tab[3 * 256 + (r >> 24)];
+
+// code of one token: (bits, length) LSB-first -- a literal's G, R, B, A codes, or a copy's
+// length prefix (green alphabet), length extra bits and distance prefix (no extra bits)
+__device__ inline uint64_t token_code(const uint32_t *tab, uint32_t r, uint32_t t, int &n) {
+    if (t == TOK_COVERED) {
+        n = 0;
+        return 0;
+    }
+    if (t != TOK_LIT) {
+        uint32_t lp, ne, ex;
+        prefix_of(t, lp, ne, ex);
+        const uint32_t eg = tab[vp8l::kOffG + 256 + lp], ed = tab[vp8l::kOffD + DIST_LEFT_PREFIX];
+        const int lg = eg >> 16, ld = ed >> 16;
+        uint64_t v = (uint64_t)(eg & 0xffffu);
+        v |= (uint64_t)ex << lg;
+        v |= (uint64_t)(ed & 0xffffu) << (lg + (int)ne);
+        n = lg + (int)ne + ld;
+        return v;
+    }
+    const uint32_t eg = tab[vp8l::kOffG + ((r >> 8) & 0xff)], er = tab[vp8l::kOffR + ((r >> 16) & 0xff)];
+    const uint32_t eb = tab[vp8l::kOffB + (r & 0xff)], ea = tab[vp8l::kOffA + (r >> 24)];
     const int lg = eg >> 16, lr = er >> 16, lb = eb >> 16, la = ea >> 16;
     uint64_t v = (uint64_t)(eg & 0xffffu);
     v |= (uint64_t)(er & 0xffffu) << lg;
@@ -210,21 +263,87 @@ __device__ inline uint64_t pixel_code(const uint32_t *tab, uint32_t r, int &n) {
     return v;
 }
 
-__device__ inline int pixel_len(const uint32_t *tab, uint32_t r) {
-    return (int)((tab[0 * 256 + ((r >> 8) & 0xff)] >> 16) + (tab[1 * 256 + ((r >> 16) & 0xff)] >> 16) +
-                 (tab[2 * 256 + (r & 0xff)] >> 16) + (tab[3 * 256 + (r >> 24)] >> 16));
+__device__ inline int token_len(const uint32_t *tab, uint32_t r, uint32_t t) {
+    if (t == TOK_COVERED) return 0;
+    if (t != TOK_LIT) {
+        uint32_t lp, ne, ex;
+        prefix_of(t, lp, ne, ex);
+        return (int)((tab[vp8l::kOffG + 256 + lp] >> 16) + ne + (tab[vp8l::kOffD + DIST_LEFT_PREFIX] >> 16));
+    }
+    return (int)((tab[vp8l::kOffG + ((r >> 8) & 0xff)] >> 16) + (tab[vp8l::kOffR + ((r >> 16) & 0xff)] >> 16) +
+                 (tab[vp8l::kOffB + (r & 0xff)] >> 16) + (tab[vp8l::kOffA + (r >> 24)] >> 16));
 }
 
-__global__ __launch_bounds__(256) void k_vp8l_bits(const uint32_t *__restrict__ resid, uint64_t npix,
+// the tokens of one EMIT_PIX group: thread t owns EMIT_PP consecutive pixels; the first pixel
+// after (before) each slice that is not a repeat comes from block suffix (prefix) scans
+__global__ __launch_bounds__(256) void k_vp8l_runs(const uint32_t *__restrict__ resid, uint64_t npix,
+                                                   uint16_t *__restrict__ tok) {
+    __shared__ uint32_t nxt[256];
+    __shared__ int prv[256];
+    const int t = threadIdx.x;
+    const uint64_t g0 = (uint64_t)blockIdx.x * EMIT_PIX;
+    const uint32_t cnt = (uint32_t)min((uint64_t)EMIT_PIX, npix - g0);
+    const uint32_t a = (uint32_t)t * EMIT_PP;
+    bool dup[EMIT_PP];
+    uint32_t first_nd = cnt;  // local indices; none: cnt
+    int last_nd = -1;         // none: -1 (the run may start before this slice)
+#pragma unroll
+    for (int j = 0; j < EMIT_PP; ++j) {
+        const uint32_t i = a + j;
+        const uint64_t p = g0 + i;
+        dup[j] = i < cnt && p > 0 && resid[p] == resid[p - 1];
+        if (i < cnt && !dup[j]) {
+            if (first_nd == cnt) first_nd = i;
+            last_nd = (int)i;
+        }
+    }
+    // nxt[t] = first non-repeat at or after slice t; prv[t] = last non-repeat at or before slice t
+    nxt[t] = first_nd;
+    prv[t] = last_nd;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t vn = t + o < 256 ? nxt[t + o] : cnt;
+        const int vp = t >= o ? prv[t - o] : -1;
+        __syncthreads();
+        nxt[t] = min(nxt[t], vn);
+        prv[t] = max(prv[t], vp);
+        __syncthreads();
+    }
+    uint32_t nb = t + 1 < 256 ? nxt[t + 1] : cnt;  // first non-repeat after this slice
+    int pb = t > 0 ? prv[t - 1] : -1;              // last non-repeat before this slice
+    uint32_t nbr[EMIT_PP];
+#pragma unroll
+    for (int j = EMIT_PP - 1; j >= 0; --j) {  // first non-repeat strictly after a + j
+        nbr[j] = nb;
+        if (a + j < cnt && !dup[j]) nb = a + j;
+    }
+#pragma unroll
+    for (int j = 0; j < EMIT_PP; ++j) {
+        const uint32_t i = a + j;
+        if (i >= cnt) break;
+        uint16_t v = TOK_LIT;
+        if (dup[j]) {
+            const uint32_t s = (uint32_t)(pb + 1);  // the run's first repeat
+            const uint32_t L = nbr[j] - s;
+            if (L >= RUN_MIN) v = i == s ? (uint16_t)L : TOK_COVERED;
+        } else {
+            pb = (int)i;
+        }
+        tok[g0 + i] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vp8l_bits(const uint32_t *__restrict__ resid,
+                                                   const uint16_t *__restrict__ tok, uint64_t npix,
                                                    const uint32_t *__restrict__ tab_g, uint32_t *__restrict__ wg_bits) {
-    __shared__ uint32_t tab[4 * 256];
+    __shared__ uint32_t tab[vp8l::kTabSize];
     __shared__ uint32_t red[4];
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = tab_g[i];
+    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
     __syncthreads();
     const uint64_t p0 = (uint64_t)blockIdx.x * EMIT_PIX + (uint64_t)threadIdx.x * EMIT_PP;
     uint32_t bits = 0;
     for (int j = 0; j < EMIT_PP; ++j)
-        if (p0 + j < npix) bits += pixel_len(tab, resid[p0 + j]);
+        if (p0 + j < npix) bits += token_len(tab, resid[p0 + j], tok[p0 + j]);
     for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
     __syncthreads();
@@ -268,22 +387,24 @@ __global__ __launch_bounds__(1024) void k_vp8l_scan(const uint32_t *__restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ resid, uint64_t npix,
+__global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ resid,
+                                                   const uint16_t *__restrict__ tok, uint64_t npix,
                                                    const uint32_t *__restrict__ tab_g,
                                                    const uint64_t *__restrict__ wg_off, uint32_t *__restrict__ out) {
-    __shared__ uint32_t tab[4 * 256];
+    __shared__ uint32_t tab[vp8l::kTabSize];
     __shared__ uint32_t words[EMIT_WORDS];
     __shared__ uint32_t tsum[256];
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = tab_g[i];
+    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
     for (int i = threadIdx.x; i < EMIT_WORDS; i += 256) words[i] = 0;
     __syncthreads();
     const uint64_t p0 = (uint64_t)blockIdx.x * EMIT_PIX + (uint64_t)threadIdx.x * EMIT_PP;
-    uint32_t r[EMIT_PP];
+    uint32_t r[EMIT_PP], tk[EMIT_PP];
     uint32_t mine = 0;
 #pragma unroll
     for (int j = 0; j < EMIT_PP; ++j) {
         r[j] = (p0 + j < npix) ? resid[p0 + j] : 0u;
-        if (p0 + j < npix) mine += pixel_len(tab, r[j]);
+        tk[j] = (p0 + j < npix) ? tok[p0 + j] : TOK_COVERED;
+        if (p0 + j < npix) mine += token_len(tab, r[j], tk[j]);
     }
     // inclusive scan of the threads' bit counts
     tsum[threadIdx.x] = mine;
@@ -302,7 +423,7 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
     for (int j = 0; j < EMIT_PP; ++j) {
         if (p0 + j >= npix) break;
         int n;
-        const uint64_t v = pixel_code(tab, r[j], n);
+        const uint64_t v = token_code(tab, r[j], tk[j], n);
         if (n) {
             const uint32_t wi = pos >> 5, s = pos & 31;
             atomicOr(&words[wi], (uint32_t)(v << s));
@@ -438,8 +559,8 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         ST_REQUIRE(((uintptr_t)jb.out & 3) == 0, ST_ERR_ARG, "webp: output must be 4-byte aligned");
         ST_REQUIRE(jb.cap >= webp_max_size(jb.w, jb.h), ST_ERR_ARG, "webp: output capacity below st_webp_max_size");
         const size_t blocks = (size_t)((jb.w + PB - 1) / PB) * ((jb.h + PB - 1) / PB);
-        stage.push_back({pin, pin + 4 * 256 * 4 + 16});
-        pin += (4 * 256 * 4 + 16 + blocks + 255) & ~(size_t)255;
+        stage.push_back({pin, pin + vp8l::kTabSize * 4 + 16});
+        pin += (vp8l::kTabSize * 4 + 16 + blocks + 255) & ~(size_t)255;
     }
     // phase A: predictors, residuals, histograms
     for (int j = 0; j < njobs; ++j) {
@@ -449,8 +570,9 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         const uint64_t npix = (uint64_t)jb.w * jb.h;
         uint32_t *resid = wsT<uint32_t>(c, tag + ".res", npix);
         uint8_t *modes = wsT<uint8_t>(c, tag + ".modes", (size_t)bw * bh);
-        uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", 4 * 256);
-        ST_HIP(hipMemsetAsync(hist, 0, 4 * 256 * 4, c->stream));
+        uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", vp8l::kTabSize);
+        uint16_t *tok = wsT<uint16_t>(c, tag + ".tok", npix);
+        ST_HIP(hipMemsetAsync(hist, 0, vp8l::kTabSize * 4, c->stream));
         {
             KTimer kt(c, "webp.predict");
             hipLaunchKernelGGL(k_vp8l_predict, dim3(bw * bh), dim3(256), 0, c->stream, jb.rgba, jb.w, jb.h, jb.stride,
@@ -459,7 +581,9 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         }
         {
             KTimer kt(c, "webp.hist");
-            hipLaunchKernelGGL(k_vp8l_hist, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid,
+            hipLaunchKernelGGL(k_vp8l_runs, dim3((unsigned)((npix + EMIT_PIX - 1) / EMIT_PIX)), dim3(256), 0,
+                               c->stream, resid, npix, tok);
+            hipLaunchKernelGGL(k_vp8l_hist, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid, tok,
                                npix, hist);
             ST_LAUNCH_CHECK();
         }
@@ -468,8 +592,8 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     for (int j = 0; j < njobs; ++j) {
         const std::string tag = "wp" + std::to_string(j);
         const size_t blocks = (size_t)((jobs[j].w + PB - 1) / PB) * ((jobs[j].h + PB - 1) / PB);
-        ST_HIP(hipMemcpyAsync(hp + stage[j].first, wsT<uint32_t>(c, tag + ".hist", 4 * 256), 4 * 256 * 4,
-                              hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemcpyAsync(hp + stage[j].first, wsT<uint32_t>(c, tag + ".hist", vp8l::kTabSize),
+                              vp8l::kTabSize * 4, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipMemcpyAsync(hp + stage[j].second, wsT<uint8_t>(c, tag + ".modes", blocks), blocks,
                               hipMemcpyDeviceToHost, c->stream));
     }
@@ -501,17 +625,18 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         std::memcpy(head[j].data() + 8, "WEBPVP8L", 8);
         const std::vector<uint8_t> hb = hdr[j].bw.bytes();
         head[j].insert(head[j].end(), hb.begin(), hb.end());
-        uint32_t *tab = wsT<uint32_t>(c, tags[j] + ".tab", 4 * 256);
+        uint32_t *tab = wsT<uint32_t>(c, tags[j] + ".tab", vp8l::kTabSize);
         uint32_t *wg_bits = wsT<uint32_t>(c, tags[j] + ".wgb", nwg);
         uint64_t *wg_off = wsT<uint64_t>(c, tags[j] + ".wgo", (size_t)nwg + 1);
         uint64_t *fsize = wsT<uint64_t>(c, tags[j] + ".fsz", 1);
         const uint32_t *resid = wsT<uint32_t>(c, tags[j] + ".res", npix);
+        const uint16_t *tok = wsT<uint16_t>(c, tags[j] + ".tok", npix);
         ST_HIP(hipMemsetAsync(jb.out, 0, webp_max_size(jb.w, jb.h), c->stream));
         ST_HIP(hipMemcpyAsync(jb.out, head[j].data(), head[j].size(), hipMemcpyHostToDevice, c->stream));
-        ST_HIP(hipMemcpyAsync(tab, hdr[j].tab.data(), 4 * 256 * 4, hipMemcpyHostToDevice, c->stream));
+        ST_HIP(hipMemcpyAsync(tab, hdr[j].tab.data(), vp8l::kTabSize * 4, hipMemcpyHostToDevice, c->stream));
         {
             KTimer kt(c, "webp.bits");
-            hipLaunchKernelGGL(k_vp8l_bits, dim3(nwg), dim3(256), 0, c->stream, resid, npix, tab, wg_bits);
+            hipLaunchKernelGGL(k_vp8l_bits, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, tab, wg_bits);
             ST_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(k_vp8l_scan, dim3(1), dim3(1024), 0, c->stream, wg_bits, nwg,
@@ -519,7 +644,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         ST_LAUNCH_CHECK();
         {
             KTimer kt(c, "webp.emit");
-            hipLaunchKernelGGL(k_vp8l_emit, dim3(nwg), dim3(256), 0, c->stream, resid, npix, tab, wg_off,
+            hipLaunchKernelGGL(k_vp8l_emit, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, tab, wg_off,
                                (uint32_t *)jb.out);
             ST_LAUNCH_CHECK();
         }

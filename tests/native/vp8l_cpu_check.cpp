@@ -5,6 +5,7 @@
 // output with Pillow/libwebp).  Never linked into libsplat_hip.
 //
 //   vp8l_cpu_check in.rgba W H out.webp
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -102,7 +103,7 @@ int main(int argc, char **argv) {
                 if (cost[m] < cost[best]) best = m;
             modes[(size_t)by * bw + bx] = (uint8_t)best;
         }
-    std::vector<uint32_t> hist(4 * 256, 0);
+    std::vector<uint32_t> hist(kTabSize, 0);
     for (int y = 0; y < h; ++y)
         for (int x = 0; x < w; ++x) {
             uint32_t p;
@@ -114,19 +115,71 @@ int main(int argc, char **argv) {
                 const uint32_t TR = (x + 1 < w) ? at(x + 1, y - 1) : at(0, y);
                 p = pred(modes[(size_t)(y / B) * bw + x / B], at(x - 1, y), at(x, y - 1), at(x - 1, y - 1), TR);
             }
-            const uint32_t r = sub(at(x, y), p);
-            res[(size_t)y * w + x] = r;
-            hist[0 * 256 + ch(r, 1)]++;
-            hist[1 * 256 + ch(r, 2)]++;
-            hist[2 * 256 + ch(r, 0)]++;
-            hist[3 * 256 + ch(r, 3)]++;
+            res[(size_t)y * w + x] = sub(at(x, y), p);
         }
+    // tokens as k_vp8l_runs: inside each 4,096-pixel group, a run of >= 3 residuals equal to
+    // their left neighbour is one copy (distance code 2, the pixel to the left)
+    const size_t npix = res.size();
+    std::vector<uint32_t> tok(npix, 0);  // 0 literal, 0xffff covered, else copy length
+    for (size_t g0 = 0; g0 < npix; g0 += 4096) {
+        const size_t g1 = std::min(npix, g0 + 4096);
+        for (size_t i = g0; i < g1;) {
+            if (i > 0 && res[i] == res[i - 1]) {
+                size_t j = i;
+                while (j < g1 && res[j] == res[j - 1]) ++j;
+                if (j - i >= 3) {
+                    tok[i] = (uint32_t)(j - i);
+                    for (size_t q = i + 1; q < j; ++q) tok[q] = 0xffff;
+                }
+                i = j;
+            } else {
+                ++i;
+            }
+        }
+    }
+    auto prefix_of = [](uint32_t v, uint32_t &pfx, uint32_t &ne, uint32_t &ex) {
+        if (v <= 4) {
+            pfx = v - 1, ne = 0, ex = 0;
+            return;
+        }
+        const uint32_t d = v - 1;
+        uint32_t hb = 31 - __builtin_clz(d);
+        ne = hb - 1;
+        ex = d & ((1u << ne) - 1);
+        pfx = 2 * hb + ((d >> (hb - 1)) & 1u);
+    };
+    for (size_t i = 0; i < npix; ++i) {
+        const uint32_t r = res[i];
+        if (tok[i] == 0xffff) continue;
+        if (tok[i]) {
+            uint32_t pfx, ne, ex;
+            prefix_of(tok[i], pfx, ne, ex);
+            hist[kOffG + 256 + pfx]++;
+            hist[kOffD + 1]++;
+            continue;
+        }
+        hist[kOffG + ch(r, 1)]++;
+        hist[kOffR + ch(r, 2)]++;
+        hist[kOffB + ch(r, 0)]++;
+        hist[kOffA + ch(r, 3)]++;
+    }
     Header hd;
     build_header(w, h, alpha, hist.data(), modes.data(), hd);
     BitWriter &bw_ = hd.bw;
-    for (uint32_t r : res) {
-        const uint32_t e[4] = {hd.tab[0 * 256 + ch(r, 1)], hd.tab[1 * 256 + ch(r, 2)], hd.tab[2 * 256 + ch(r, 0)],
-                               hd.tab[3 * 256 + ch(r, 3)]};
+    for (size_t i = 0; i < npix; ++i) {
+        const uint32_t r = res[i];
+        if (tok[i] == 0xffff) continue;
+        if (tok[i]) {
+            uint32_t pfx, ne, ex;
+            prefix_of(tok[i], pfx, ne, ex);
+            const uint32_t eg = hd.tab[kOffG + 256 + pfx], ed = hd.tab[kOffD + 1];
+            bw_.put(eg & 0xffffu, (int)(eg >> 16));
+            bw_.put(ex, (int)ne);
+            bw_.put(ed & 0xffffu, (int)(ed >> 16));
+            continue;
+        }
+        const uint32_t e[4] = {hd.tab[kOffG + ch(r, 1)], hd.tab[kOffR + ch(r, 2)], hd.tab[kOffB + ch(r, 0)],
+                               hd.tab[kOffA + ch(r, 3)]};
         for (int k = 0; k < 4; ++k) bw_.put(e[k] & 0xffffu, (int)(e[k] >> 16));
     }
     std::vector<uint8_t> body = bw_.bytes();
