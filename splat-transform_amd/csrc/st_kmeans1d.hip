@@ -1010,6 +1010,12 @@ struct Part1 {
     int32_t emin;
     uint32_t cnt;
 };
+// a cluster's member-magnitude bounds from the centroid order (k_kd1_assign_acc<true>): used
+// by k_kd1_final instead of the accumulated sum|x| / e_min unless acc
+struct Bnd1 {
+    float maxabs, minabs;
+    uint32_t acc;
+};
 constexpr uint32_t A1_G = 1024;  // most workgroups (partials) of the accumulating assign
 constexpr int A1_CELLS = 4096;   // bracket cells of the accumulating assign
 constexpr int FF_MAX = 8;         // flagged clusters the wave kernels take (more: the tile kernels)
@@ -1023,16 +1029,19 @@ uint32_t a1_grid(uint32_t ntiles) {
 // k_kd1_assign_hist's bracket assign with the centroid order built in the workgroup (the
 // stable sort of KdTree's build is a rank by (sort key, index)), over the tiles
 // blockIdx.x, blockIdx.x + gridDim.x, ...; part[blockIdx.x * 256 + c] = cluster c's partial
+template <bool BOUNDS>
 __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict__ pts, uint64_t n,
                                                         const float *__restrict__ cen, int k,
                                                         uint32_t *__restrict__ labels, uint8_t *__restrict__ lab8,
-                                                        uint32_t ntiles, Part1 *__restrict__ part) {
+                                                        uint32_t ntiles, Part1 *__restrict__ part,
+                                                        const uint32_t *__restrict__ mm, Bnd1 *__restrict__ bnd) {
     __shared__ float sv[256];
     __shared__ uint32_t si[256], skey[256];
     __shared__ uint16_t cc[256];
     __shared__ uint8_t chk_l[256], chk_r[256];
     __shared__ uint32_t first[A1_CELLS + 1];
     __shared__ double hs[256], ha[256];
+    __shared__ uint8_t acc_abs[256];  // cluster: accumulate sum|x| and e_min (no bounds known)
     __shared__ int32_t he[256];
     __shared__ uint32_t hc[256];
     const int t = threadIdx.x;
@@ -1072,6 +1081,22 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
         constexpr double R48 = 281474976710656.0;  // 2^48
         chk_l[t] = (t >= 1 && (gl == 0.0 || gr < 0.0 || gr >= gl * R48)) ? 1 : 0;
         chk_r[t] = (t + 1 < k && (gr == 0.0 || gl < 0.0 || gl >= gr * R48)) ? 1 : 0;
+        // BOUNDS: the members of the cluster at sorted position t lie in [sv[t - 1], sv[t + 1]]
+        // when both gaps are positive and no point lies 2^48 gaps beyond a neighbour (a point
+        // outside is strictly nearer, in rounded f64, to that neighbour); if that interval
+        // excludes 0, count x max|end| bounds sum|x| and the inner end's ulp bounds e_min, so
+        // the certificate needs no per-point sum|x| / e_min
+        bool bounded = false;
+        float mx = 0.f, mn = 0.f;
+        if (BOUNDS && mm && t >= 1 && t + 1 < k && gl > 0.0 && gr > 0.0) {
+            const double xmin = (double)fkey_inv_(mm[0]), xmax = (double)fkey_inv_(mm[1]);
+            const float l = sv[t - 1], h = sv[t + 1];
+            bounded = ((double)l - xmin) <= gl * R48 && (xmax - (double)h) <= gr * R48 && (l > 0.f || h < 0.f);
+            mx = __builtin_fmaxf(__builtin_fabsf(l), __builtin_fabsf(h));
+            mn = __builtin_fminf(__builtin_fabsf(l), __builtin_fabsf(h));
+        }
+        acc_abs[si[t]] = bounded ? 0 : 1;
+        if (BOUNDS && blockIdx.x == 0) bnd[si[t]] = Bnd1{mx, mn, bounded ? 0u : 1u};
     }
     __syncthreads();
     for (int g = t; g <= A1_CELLS; g += F1_T) {
@@ -1133,8 +1158,10 @@ __global__ __launch_bounds__(F1_T) void k_kd1_assign_acc(const float *__restrict
             if (labels) labels[i] = lab;
             atomicAdd(&hc[lab], 1u);
             atomicAdd(&hs[lab], p);
-            atomicAdd(&ha[lab], __builtin_fabs(p));
-            if (pf != 0.0f) atomicMin(&he[lab], ulp_exp(pf));
+            if (!BOUNDS || acc_abs[lab]) {
+                atomicAdd(&ha[lab], __builtin_fabs(p));
+                if (pf != 0.0f) atomicMin(&he[lab], ulp_exp(pf));
+            }
         }
     }
     __syncthreads();
@@ -1152,7 +1179,8 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
                                                    uint32_t *__restrict__ start, uint32_t *__restrict__ fstart,
                                                    uint32_t *ticket, uint32_t *__restrict__ info,
                                                    const float *const *cols, const double *__restrict__ draws,
-                                                   uint64_t ndraws, State *st, uint32_t many_above) {
+                                                   uint64_t ndraws, State *st, uint32_t many_above,
+                                                   const Bnd1 *__restrict__ bnd) {
     const int cl = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     double s = 0, a = 0;
     int e = 1 << 20;
@@ -1187,6 +1215,10 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
         e = min(min(re[0], re[1]), min(re[2], re[3]));
         c = (rc[0] + rc[1]) + (rc[2] + rc[3]);
         uint32_t f = 0;
+        if (c && bnd && !bnd[cl].acc) {  // bounds in place of the accumulated sum|x| / e_min
+            a = (double)c * (double)bnd[cl].maxabs * (1.0 + 0x1p-50);
+            e = ulp_exp(bnd[cl].minabs);
+        }
         if (c) {
             const bool exact = sum_is_exact(a, e);
             f = exact ? 0u : 1u;
@@ -1636,6 +1668,9 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         auto *fstart = wsT<uint32_t>(c, "k1.fstart", (size_t)k + 1);
         auto *ticket = wsT<uint32_t>(c, "k1.ticket", 1);
         auto *dinfo = wsT<uint32_t>(c, "k1.info", 2);
+        auto *bnd = wsT<Bnd1>(c, "k1.bnd", 256);
+        // the points' min / max keys (kmeans_dev's 1-D init); none: every cluster accumulates
+        const uint32_t *mm = getenv("ST_K1_NO_BOUNDS") ? nullptr : wsT<uint32_t>(c, "km.mm", 2);
         auto *hinfo = static_cast<uint32_t *>(pinned_slot(c, "k1.info", 8));
         ST_HIP(hipMemsetAsync(ticket, 0, sizeof(uint32_t), c->stream));
         // queued: no read-back per iteration (more than FF_MAX flagged clusters -> ERR_K1_MANY,
@@ -1649,15 +1684,15 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         for (int it = 0; it < iters; ++it) {
             {
                 KTimer kt(c, "k1.assign");
-                hipLaunchKernelGGL(k_kd1_assign_acc, dim3(G), dim3(F1_T), 0, c->stream, pts, n, cen, k,
-                                   it == iters - 1 ? labels : (uint32_t *)nullptr, lab8, ntiles, part);
+                hipLaunchKernelGGL(k_kd1_assign_acc<true>, dim3(G), dim3(F1_T), 0, c->stream, pts, n, cen, k,
+                                   it == iters - 1 ? labels : (uint32_t *)nullptr, lab8, ntiles, part, mm, bnd);
                 ST_LAUNCH_CHECK();
             }
             mark(c, "k1.assign");
             KTimer kt(c, "k1.sum");
             hipLaunchKernelGGL(k_kd1_final, dim3(k), dim3(256), 0, c->stream, part, G, k, n, cen, seq_flag, emin_c,
                                sabs_c, cnt_c, start, fstart, ticket, dinfo, dcols, ddraws, ndraws, dstate,
-                               queued ? ff_max : 0xffffffffu);
+                               queued ? ff_max : 0xffffffffu, bnd);
             ST_LAUNCH_CHECK();
             if (queued) {
                 // the flagged path queued behind the final with no read-back: its kernels find
@@ -1849,8 +1884,9 @@ void assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k,
     for (int sg = 0; sg < nseg; ++sg) {
         const uint64_t o = (uint64_t)sg * ns;
         if (ns)
-            hipLaunchKernelGGL(k_kd1_assign_acc, dim3(G), dim3(F1_T), 0, c->stream, pts + o, ns, cen, k, labels + o,
-                               (uint8_t *)nullptr, ntiles, part + (uint64_t)sg * G * 256);
+            hipLaunchKernelGGL(k_kd1_assign_acc<false>, dim3(G), dim3(F1_T), 0, c->stream, pts + o, ns, cen, k,
+                               labels + o, (uint8_t *)nullptr, ntiles, part + (uint64_t)sg * G * 256,
+                               (const uint32_t *)nullptr, (Bnd1 *)nullptr);
         else
             ST_HIP(hipMemsetAsync(part + (uint64_t)sg * G * 256, 0, sizeof(Part1) * 256 * G, c->stream));
     }
