@@ -710,18 +710,20 @@ def main(args):
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
     traffic, tsrc = None, None
-    tfile = os.path.join(ROOT, 'profiles', 'r02', 'pmc_sweep_traffic.json')
-    if not os.path.exists(tfile):
-        tfile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_traffic.json')
+    def latest(name):  # the newest round's committed profile of that name
+        for rnd in ('r03', 'r02', 'r01'):
+            f = os.path.join(ROOT, 'profiles', rnd, name)
+            if os.path.exists(f):
+                return f
+        return os.path.join(ROOT, 'profiles', 'r01', name)
+    tfile = latest('pmc_sweep_traffic.json')
     if os.path.exists(tfile) and n_local == 10_000_000:
         traffic = json.load(open(tfile))['hbm_bytes_per_launch']
         tsrc = os.path.relpath(tfile, ROOT)
     # the engine clock the chip holds under the sweep (PMC GRBM_GUI_ACTIVE, tools/pmc.sh + pmc_util.py):
     # beside `frac` (against the 2.4 GHz headline peak), the fraction of the peak at that clock
     clock = None
-    ufile = os.path.join(ROOT, 'profiles', 'r02', 'pmc_sweep_util.json')
-    if not os.path.exists(ufile):
-        ufile = os.path.join(ROOT, 'profiles', 'r01', 'pmc_sweep_util.json')
+    ufile = latest('pmc_sweep_util.json')
     if os.path.exists(ufile) and achieved:
         u = json.load(open(ufile))
         clock = {'engine_clock_GHz': u['engine_clock_GHz'], 'mfma_busy_frac': u['mfma_busy_frac'],
