@@ -7,6 +7,7 @@
 #include "st_vp8l.h"
 
 #include <algorithm>
+#include <cmath>
 #include <queue>
 #include <stdexcept>
 
@@ -197,9 +198,26 @@ Code write_code(BitWriter &bw, const uint64_t *counts, int alphabet) {
     return c;
 }
 
-void build_header(int width, int height, bool alpha_used, const uint32_t *hist, const uint8_t *modes, Header &out) {
+// a sub-image (predictor modes, entropy image): green = the value, no colour cache
+static void write_subimage(BitWriter &bw, const uint8_t *v, size_t n) {
+    std::vector<uint64_t> g(kGreenAlphabet, 0), zero(256, 0), dist(kDistAlphabet, 0);
+    for (size_t i = 0; i < n; ++i) g[v[i]]++;
+    zero[0] = 1;
+    bw.put(0, 1);  // no colour cache
+    Code cg = write_code(bw, g.data(), kGreenAlphabet);
+    write_code(bw, zero.data(), 256);  // red 0
+    write_code(bw, zero.data(), 256);  // blue 0
+    write_code(bw, zero.data(), 256);  // alpha 0
+    write_code(bw, dist.data(), kDistAlphabet);
+    for (size_t i = 0; i < n; ++i) bw.put(cg.rev[v[i]], cg.len[v[i]]);
+}
+
+void build_header(int width, int height, bool alpha_used, const uint32_t *hist, int ngroups, const uint8_t *groups,
+                  int group_bits, const uint8_t *modes, Header &out) {
     if (width < 1 || height < 1 || width > 16384 || height > 16384)
         throw std::invalid_argument("vp8l: image size out of range");
+    if (ngroups < 1 || ngroups > 256 || (ngroups > 1 && (group_bits < 2 || group_bits > 9)))
+        throw std::invalid_argument("vp8l: prefix-code groups out of range");
     BitWriter &bw = out.bw;
     bw.put(0x2f, 8);
     bw.put((uint32_t)(width - 1), 14);
@@ -212,31 +230,42 @@ void build_header(int width, int height, bool alpha_used, const uint32_t *hist, 
     bw.put(kPredBits - 2, 3);
     const int bw_ = (width + (1 << kPredBits) - 1) >> kPredBits;
     const int bh_ = (height + (1 << kPredBits) - 1) >> kPredBits;
-    {
-        std::vector<uint64_t> g(kGreenAlphabet, 0), zero(256, 0), dist(kDistAlphabet, 0);
-        for (int i = 0; i < bw_ * bh_; ++i) g[modes[i]]++;
-        zero[0] = 1;
-        bw.put(0, 1);  // no colour cache
-        Code cg = write_code(bw, g.data(), kGreenAlphabet);
-        write_code(bw, zero.data(), 256);  // red 0
-        write_code(bw, zero.data(), 256);  // blue 0
-        write_code(bw, zero.data(), 256);  // alpha 0
-        write_code(bw, dist.data(), kDistAlphabet);
-        for (int i = 0; i < bw_ * bh_; ++i) bw.put(cg.rev[modes[i]], cg.len[modes[i]]);
-    }
+    write_subimage(bw, modes, (size_t)bw_ * bh_);
     bw.put(0, 1);  // no more transforms
     // main image
     bw.put(0, 1);  // no colour cache
-    bw.put(0, 1);  // one prefix-code group
-    out.tab.assign(kTabSize, 0);
+    if (ngroups > 1) {  // meta prefix codes: the entropy image (green = group)
+        bw.put(1, 1);
+        bw.put((uint32_t)(group_bits - 2), 3);
+        const int gw = (width + (1 << group_bits) - 1) >> group_bits;
+        const int gh = (height + (1 << group_bits) - 1) >> group_bits;
+        write_subimage(bw, groups, (size_t)gw * gh);
+    } else {
+        bw.put(0, 1);  // one prefix-code group
+    }
+    out.tab.assign((size_t)ngroups * kTabSize, 0);
     const int off[5] = {kOffG, kOffR, kOffB, kOffA, kOffD};
     const int size[5] = {kGreenAlphabet, 256, 256, 256, kDistAlphabet};
-    for (int ch = 0; ch < 5; ++ch) {
-        std::vector<uint64_t> cnt(size[ch], 0);
-        for (int s = 0; s < size[ch]; ++s) cnt[s] = hist[off[ch] + s];
-        Code code = write_code(bw, cnt.data(), size[ch]);
-        for (int s = 0; s < size[ch]; ++s) out.tab[off[ch] + s] = ((uint32_t)code.len[s] << 16) | code.rev[s];
+    for (int g = 0; g < ngroups; ++g)
+        for (int ch = 0; ch < 5; ++ch) {
+            std::vector<uint64_t> cnt(size[ch], 0);
+            for (int s = 0; s < size[ch]; ++s) cnt[s] = hist[(size_t)g * kTabSize + off[ch] + s];
+            Code code = write_code(bw, cnt.data(), size[ch]);
+            for (int s = 0; s < size[ch]; ++s)
+                out.tab[(size_t)g * kTabSize + off[ch] + s] = ((uint32_t)code.len[s] << 16) | code.rev[s];
+        }
+}
+
+double literal_bits(const uint32_t *hist) {
+    const int off[4] = {kOffG, kOffR, kOffB, kOffA};
+    double bits = 0;
+    for (int ch = 0; ch < 4; ++ch) {
+        double n = 0;
+        for (int s = 0; s < 256; ++s) n += hist[off[ch] + s];
+        for (int s = 0; s < 256; ++s)
+            if (hist[off[ch] + s]) bits -= hist[off[ch] + s] * std::log2(hist[off[ch] + s] / n);
     }
+    return bits;
 }
 
 }  // namespace vp8l

@@ -52,15 +52,22 @@ Code write_code(BitWriter &bw, const uint64_t *counts, int alphabet);
 
 // The header bits of one image: everything before the main image's pixel
 // stream (VP8L signature, size, predictor transform with its entropy-coded
-// sub-image, colour-cache and meta-code flags, the five prefix codes).
-// hist: symbol histograms in the kOff* layout (kTabSize bins: G with the length prefixes,
-// R, B, A, distance); modes: the predictor sub-image (one byte per 16 x 16 block, row-major).
-// tab (out): kTabSize device table entries (len << 16 | reversed code) in the same layout.
+// sub-image, colour-cache and meta-code flags, the entropy image when there are
+// several prefix-code groups, then five prefix codes per group).
+// hist: ngroups x kTabSize symbol histograms (each in the kOff* layout: G with the
+// length prefixes, R, B, A, distance); groups (ngroups > 1): the entropy image, one
+// group index per 2^group_bits-square block (row-major); modes: the predictor
+// sub-image (one byte per 16 x 16 block, row-major).
+// tab (out): ngroups x kTabSize device table entries (len << 16 | reversed code).
 struct Header {
     BitWriter bw;
     std::vector<uint32_t> tab;
 };
-void build_header(int width, int height, bool alpha_used, const uint32_t *hist, const uint8_t *modes, Header &out);
+void build_header(int width, int height, bool alpha_used, const uint32_t *hist, int ngroups, const uint8_t *groups,
+                  int group_bits, const uint8_t *modes, Header &out);
+// Shannon bits of the literal symbols of a kTabSize histogram (channels G, R, B, A): the
+// cost estimate that decides between predictors for a whole image
+double literal_bits(const uint32_t *hist);
 
 }  // namespace vp8l
 }  // namespace st

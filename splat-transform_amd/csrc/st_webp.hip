@@ -40,6 +40,12 @@ constexpr int EMIT_PP = 16;               // pixels per thread in the bit kernel
 constexpr int EMIT_PIX = 256 * EMIT_PP;   // pixels per group
 constexpr int EMIT_WORDS = EMIT_PIX * 60 / 32 + 2;
 
+// prefix-code groups (the entropy image): blocks of 2^GROUP_BITS pixels where a literal carries
+// a non-zero alpha residual (the edge of the zero padding after the last splat) take group 1,
+// so every other pixel's alpha stays a one-symbol (zero-bit) code
+constexpr int GROUP_BITS = 5;
+constexpr int CODE_GROUPS = 2;
+
 // tokens: a literal pixel, the start of an LZ77 copy (its length), or a pixel a copy covers
 constexpr uint16_t TOK_LIT = 0, TOK_COVERED = 0xffffu;
 constexpr uint32_t RUN_MIN = 3;                // shortest run coded as a copy
@@ -142,7 +148,7 @@ __device__ inline uint32_t residual_cost(uint32_t r) {
 
 __global__ __launch_bounds__(256) void k_vp8l_predict(const uint8_t *__restrict__ rgba, int w, int h, int stride,
                                                       int bw, uint8_t *__restrict__ modes,
-                                                      uint32_t *__restrict__ resid) {
+                                                      uint32_t *__restrict__ resid, int force_mode) {
     __shared__ uint32_t part[4][14];
     __shared__ uint32_t alpha_any;
     if (threadIdx.x == 0) alpha_any = 0;
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(256) void k_vp8l_predict(const uint8_t *__restrict_
         }
     }
     if (__ballot(valid && (C >> 24) != 0xffu) && lane == 0) atomicOr(&alpha_any, 1u);
-    const bool interior = valid && x > 0 && y > 0;
+    const bool interior = valid && x > 0 && y > 0 && force_mode < 0;
     uint32_t cost[14];
 #pragma unroll
     for (int m = 0; m < 14; ++m) cost[m] = interior ? residual_cost(sub_pixels(C, predict(m, L, T, TL, TR))) : 0u;
@@ -188,6 +194,7 @@ __global__ __launch_bounds__(256) void k_vp8l_predict(const uint8_t *__restrict_
                 best = m;
             }
         }
+        if (force_mode >= 0) best = force_mode;
         best_s = best;
         // bit 7: some pixel of the block has alpha != 255 (the header's alpha hint)
         modes[blockIdx.x] = (uint8_t)(best | (alpha_any ? 0x80 : 0));
@@ -205,32 +212,60 @@ __global__ __launch_bounds__(256) void k_vp8l_predict(const uint8_t *__restrict_
 }
 
 // symbol histograms in the vp8l::kOff* layout
+// group of pixel p (the block's flag), from its row and column
+__device__ inline uint32_t group_of(const uint8_t *gflag, uint32_t p, int w, int gw) {
+    const uint32_t y = p / (uint32_t)w, x = p - y * (uint32_t)w;
+    return gflag[(y >> GROUP_BITS) * (uint32_t)gw + (x >> GROUP_BITS)];
+}
+
+// symbol histograms per prefix-code group (CODE_GROUPS x kTabSize, the vp8l::kOff* layout) and,
+// with raw, the histogram of the pixels themselves as predictor 0 leaves them (pixel - 0xff000000):
+// the host's per-image choice between the chosen predictors and none
 __global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ resid,
-                                                   const uint16_t *__restrict__ tok, uint64_t npix,
-                                                   uint32_t *__restrict__ hist) {
-    __shared__ uint32_t hs[vp8l::kTabSize];
-    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) hs[i] = 0;
+                                                   const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
+                                                   const uint8_t *__restrict__ gflag,
+                                                   const uint8_t *__restrict__ rgba, int stride,
+                                                   uint32_t *__restrict__ hist, uint32_t *__restrict__ raw) {
+    __shared__ uint32_t hs[CODE_GROUPS * vp8l::kTabSize];
+    __shared__ uint32_t hr[4 * 256];
+    for (int i = threadIdx.x; i < CODE_GROUPS * vp8l::kTabSize; i += 256) hs[i] = 0;
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) hr[i] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += stride) {
+    const uint64_t stride_ = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += stride_) {
+        if (raw) {
+            const uint32_t y = (uint32_t)i / (uint32_t)w, x = (uint32_t)i - y * (uint32_t)w;
+            const uint32_t v = sub_pixels(to_argb(*(const uint32_t *)(rgba + (size_t)y * stride + (size_t)x * 4)),
+                                          0xff000000u);
+            atomicAdd(&hr[0 * 256 + ((v >> 8) & 0xff)], 1u);
+            atomicAdd(&hr[1 * 256 + ((v >> 16) & 0xff)], 1u);
+            atomicAdd(&hr[2 * 256 + (v & 0xff)], 1u);
+            atomicAdd(&hr[3 * 256 + (v >> 24)], 1u);
+        }
         const uint32_t t = tok[i];
         if (t == TOK_COVERED) continue;
+        uint32_t *H = hs + group_of(gflag, (uint32_t)i, w, gw) * vp8l::kTabSize;
         if (t != TOK_LIT) {
             uint32_t lp, ne, ex;
             prefix_of(t, lp, ne, ex);
-            atomicAdd(&hs[vp8l::kOffG + 256 + lp], 1u);
-            atomicAdd(&hs[vp8l::kOffD + DIST_LEFT_PREFIX], 1u);
+            atomicAdd(&H[vp8l::kOffG + 256 + lp], 1u);
+            atomicAdd(&H[vp8l::kOffD + DIST_LEFT_PREFIX], 1u);
             continue;
         }
         const uint32_t r = resid[i];
-        atomicAdd(&hs[vp8l::kOffG + ((r >> 8) & 0xff)], 1u);
-        atomicAdd(&hs[vp8l::kOffR + ((r >> 16) & 0xff)], 1u);
-        atomicAdd(&hs[vp8l::kOffB + (r & 0xff)], 1u);
-        atomicAdd(&hs[vp8l::kOffA + (r >> 24)], 1u);
+        atomicAdd(&H[vp8l::kOffG + ((r >> 8) & 0xff)], 1u);
+        atomicAdd(&H[vp8l::kOffR + ((r >> 16) & 0xff)], 1u);
+        atomicAdd(&H[vp8l::kOffB + (r & 0xff)], 1u);
+        atomicAdd(&H[vp8l::kOffA + (r >> 24)], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256)
+    for (int i = threadIdx.x; i < CODE_GROUPS * vp8l::kTabSize; i += 256)
         if (hs[i]) atomicAdd(&hist[i], hs[i]);
+    if (raw) {
+        const int off[4] = {vp8l::kOffG, vp8l::kOffR, vp8l::kOffB, vp8l::kOffA};
+        for (int i = threadIdx.x; i < 4 * 256; i += 256)
+            if (hr[i]) atomicAdd(&raw[off[i >> 8] + (i & 255)], hr[i]);
+    }
 }
 
 
@@ -277,7 +312,8 @@ __device__ inline int token_len(const uint32_t *tab, uint32_t r, uint32_t t) {
 // the tokens of one EMIT_PIX group: thread t owns EMIT_PP consecutive pixels; the first pixel
 // after (before) each slice that is not a repeat comes from block suffix (prefix) scans
 __global__ __launch_bounds__(256) void k_vp8l_runs(const uint32_t *__restrict__ resid, uint64_t npix,
-                                                   uint16_t *__restrict__ tok) {
+                                                   uint16_t *__restrict__ tok, int w, int gw,
+                                                   uint8_t *__restrict__ gflag) {
     __shared__ uint32_t nxt[256];
     __shared__ int prv[256];
     const int t = threadIdx.x;
@@ -330,20 +366,28 @@ __global__ __launch_bounds__(256) void k_vp8l_runs(const uint32_t *__restrict__ 
             pb = (int)i;
         }
         tok[g0 + i] = v;
+        if (v == TOK_LIT && (resid[g0 + i] >> 24) != 0u) {  // a literal alpha residual: group 1
+            const uint32_t p = (uint32_t)(g0 + i), y = p / (uint32_t)w, x = p - y * (uint32_t)w;
+            gflag[(y >> GROUP_BITS) * (uint32_t)gw + (x >> GROUP_BITS)] = 1;
+        }
     }
 }
 
 __global__ __launch_bounds__(256) void k_vp8l_bits(const uint32_t *__restrict__ resid,
-                                                   const uint16_t *__restrict__ tok, uint64_t npix,
+                                                   const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
+                                                   const uint8_t *__restrict__ gflag, int ngroups,
                                                    const uint32_t *__restrict__ tab_g, uint32_t *__restrict__ wg_bits) {
-    __shared__ uint32_t tab[vp8l::kTabSize];
+    __shared__ uint32_t tab[CODE_GROUPS * vp8l::kTabSize];
     __shared__ uint32_t red[4];
-    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
+    for (int i = threadIdx.x; i < ngroups * vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
     __syncthreads();
     const uint64_t p0 = (uint64_t)blockIdx.x * EMIT_PIX + (uint64_t)threadIdx.x * EMIT_PP;
     uint32_t bits = 0;
     for (int j = 0; j < EMIT_PP; ++j)
-        if (p0 + j < npix) bits += token_len(tab, resid[p0 + j], tok[p0 + j]);
+        if (p0 + j < npix) {
+            const uint32_t g = ngroups > 1 ? group_of(gflag, (uint32_t)(p0 + j), w, gw) : 0u;
+            bits += token_len(tab + g * vp8l::kTabSize, resid[p0 + j], tok[p0 + j]);
+        }
     for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
     __syncthreads();
@@ -388,23 +432,25 @@ __global__ __launch_bounds__(1024) void k_vp8l_scan(const uint32_t *__restrict__
 }
 
 __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ resid,
-                                                   const uint16_t *__restrict__ tok, uint64_t npix,
+                                                   const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
+                                                   const uint8_t *__restrict__ gflag, int ngroups,
                                                    const uint32_t *__restrict__ tab_g,
                                                    const uint64_t *__restrict__ wg_off, uint32_t *__restrict__ out) {
-    __shared__ uint32_t tab[vp8l::kTabSize];
+    __shared__ uint32_t tab[CODE_GROUPS * vp8l::kTabSize];
     __shared__ uint32_t words[EMIT_WORDS];
     __shared__ uint32_t tsum[256];
-    for (int i = threadIdx.x; i < vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
+    for (int i = threadIdx.x; i < ngroups * vp8l::kTabSize; i += 256) tab[i] = tab_g[i];
     for (int i = threadIdx.x; i < EMIT_WORDS; i += 256) words[i] = 0;
     __syncthreads();
     const uint64_t p0 = (uint64_t)blockIdx.x * EMIT_PIX + (uint64_t)threadIdx.x * EMIT_PP;
-    uint32_t r[EMIT_PP], tk[EMIT_PP];
+    uint32_t r[EMIT_PP], tk[EMIT_PP], gt[EMIT_PP];
     uint32_t mine = 0;
 #pragma unroll
     for (int j = 0; j < EMIT_PP; ++j) {
         r[j] = (p0 + j < npix) ? resid[p0 + j] : 0u;
         tk[j] = (p0 + j < npix) ? tok[p0 + j] : TOK_COVERED;
-        if (p0 + j < npix) mine += token_len(tab, r[j], tk[j]);
+        gt[j] = (ngroups > 1 && p0 + j < npix) ? group_of(gflag, (uint32_t)(p0 + j), w, gw) * vp8l::kTabSize : 0u;
+        if (p0 + j < npix) mine += token_len(tab + gt[j], r[j], tk[j]);
     }
     // inclusive scan of the threads' bit counts
     tsum[threadIdx.x] = mine;
@@ -423,7 +469,7 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
     for (int j = 0; j < EMIT_PP; ++j) {
         if (p0 + j >= npix) break;
         int n;
-        const uint64_t v = token_code(tab, r[j], tk[j], n);
+        const uint64_t v = token_code(tab + gt[j], r[j], tk[j], n);
         if (n) {
             const uint32_t wi = pos >> 5, s = pos & 31;
             atomicOr(&words[wi], (uint32_t)(v << s));
@@ -548,8 +594,16 @@ uint64_t webp_max_size(int w, int h) {
 }
 
 void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
-    std::vector<std::pair<size_t, size_t>> stage;  // (hist/flag offset, modes offset) in pinned staging
+    // per job in pinned staging: group histograms, the raw histogram, predictor modes, group flags
+    struct Stage {
+        size_t hist, raw, modes, flags;
+    };
+    std::vector<Stage> stage;
     size_t pin = 0;
+    auto geom = [](const WebpJob &jb, int &bw, int &bh, int &gw, int &gh) {
+        bw = (jb.w + PB - 1) / PB, bh = (jb.h + PB - 1) / PB;
+        gw = (jb.w + (1 << GROUP_BITS) - 1) >> GROUP_BITS, gh = (jb.h + (1 << GROUP_BITS) - 1) >> GROUP_BITS;
+    };
     for (int j = 0; j < njobs; ++j) {
         WebpJob &jb = jobs[j];
         ST_REQUIRE(jb.w >= 1 && jb.h >= 1 && jb.w <= 16384 && jb.h <= 16384, ST_ERR_ARG,
@@ -558,58 +612,100 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
                    "webp: rgba rows must be 4-byte aligned");
         ST_REQUIRE(((uintptr_t)jb.out & 3) == 0, ST_ERR_ARG, "webp: output must be 4-byte aligned");
         ST_REQUIRE(jb.cap >= webp_max_size(jb.w, jb.h), ST_ERR_ARG, "webp: output capacity below st_webp_max_size");
-        const size_t blocks = (size_t)((jb.w + PB - 1) / PB) * ((jb.h + PB - 1) / PB);
-        stage.push_back({pin, pin + vp8l::kTabSize * 4 + 16});
-        pin += (vp8l::kTabSize * 4 + 16 + blocks + 255) & ~(size_t)255;
+        int bw, bh, gw, gh;
+        geom(jb, bw, bh, gw, gh);
+        Stage st;
+        st.hist = pin;
+        st.raw = st.hist + CODE_GROUPS * vp8l::kTabSize * 4;
+        st.modes = st.raw + vp8l::kTabSize * 4;
+        st.flags = st.modes + (size_t)bw * bh;
+        stage.push_back(st);
+        pin = (st.flags + (size_t)gw * gh + 255) & ~(size_t)255;
     }
-    // phase A: predictors, residuals, histograms
-    for (int j = 0; j < njobs; ++j) {
+    // phase A: predictors, residuals, tokens, group flags, histograms (raw = the pixels as no
+    // predictor leaves them, for the choice below)
+    auto phase_a = [&](int j, int force_mode) {
         WebpJob &jb = jobs[j];
         const std::string tag = "wp" + std::to_string(j);
-        const int bw = (jb.w + PB - 1) / PB, bh = (jb.h + PB - 1) / PB;
+        int bw, bh, gw, gh;
+        geom(jb, bw, bh, gw, gh);
         const uint64_t npix = (uint64_t)jb.w * jb.h;
         uint32_t *resid = wsT<uint32_t>(c, tag + ".res", npix);
         uint8_t *modes = wsT<uint8_t>(c, tag + ".modes", (size_t)bw * bh);
-        uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", vp8l::kTabSize);
+        uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", (size_t)CODE_GROUPS * vp8l::kTabSize);
+        uint32_t *raw = wsT<uint32_t>(c, tag + ".raw", vp8l::kTabSize);
         uint16_t *tok = wsT<uint16_t>(c, tag + ".tok", npix);
-        ST_HIP(hipMemsetAsync(hist, 0, vp8l::kTabSize * 4, c->stream));
+        uint8_t *gflag = wsT<uint8_t>(c, tag + ".gfl", (size_t)gw * gh);
+        ST_HIP(hipMemsetAsync(hist, 0, (size_t)CODE_GROUPS * vp8l::kTabSize * 4, c->stream));
+        ST_HIP(hipMemsetAsync(raw, 0, vp8l::kTabSize * 4, c->stream));
+        ST_HIP(hipMemsetAsync(gflag, 0, (size_t)gw * gh, c->stream));
         {
             KTimer kt(c, "webp.predict");
             hipLaunchKernelGGL(k_vp8l_predict, dim3(bw * bh), dim3(256), 0, c->stream, jb.rgba, jb.w, jb.h, jb.stride,
-                               bw, modes, resid);
+                               bw, modes, resid, force_mode);
             ST_LAUNCH_CHECK();
         }
         {
             KTimer kt(c, "webp.hist");
             hipLaunchKernelGGL(k_vp8l_runs, dim3((unsigned)((npix + EMIT_PIX - 1) / EMIT_PIX)), dim3(256), 0,
-                               c->stream, resid, npix, tok);
+                               c->stream, resid, npix, tok, jb.w, gw, gflag);
             hipLaunchKernelGGL(k_vp8l_hist, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid, tok,
-                               npix, hist);
+                               npix, jb.w, gw, gflag, jb.rgba, jb.stride, hist, force_mode < 0 ? raw : nullptr);
             ST_LAUNCH_CHECK();
         }
-    }
-    uint8_t *hp = (uint8_t *)pinned(c, pin);
-    for (int j = 0; j < njobs; ++j) {
-        const std::string tag = "wp" + std::to_string(j);
-        const size_t blocks = (size_t)((jobs[j].w + PB - 1) / PB) * ((jobs[j].h + PB - 1) / PB);
-        ST_HIP(hipMemcpyAsync(hp + stage[j].first, wsT<uint32_t>(c, tag + ".hist", vp8l::kTabSize),
-                              vp8l::kTabSize * 4, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipMemcpyAsync(hp + stage[j].second, wsT<uint8_t>(c, tag + ".modes", blocks), blocks,
+        uint8_t *hp = (uint8_t *)pinned(c, pin);
+        ST_HIP(hipMemcpyAsync(hp + stage[j].hist, hist, (size_t)CODE_GROUPS * vp8l::kTabSize * 4,
                               hipMemcpyDeviceToHost, c->stream));
-    }
+        ST_HIP(hipMemcpyAsync(hp + stage[j].raw, raw, vp8l::kTabSize * 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemcpyAsync(hp + stage[j].modes, modes, (size_t)bw * bh, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemcpyAsync(hp + stage[j].flags, gflag, (size_t)gw * gh, hipMemcpyDeviceToHost, c->stream));
+    };
+    for (int j = 0; j < njobs; ++j) phase_a(j, -1);
     ST_HIP(hipStreamSynchronize(c->stream));
-    // host: prefix codes + header bits
-    std::vector<vp8l::Header> hdr(njobs);
+    // per image: when the pixels themselves code in fewer literal bits than the chosen
+    // predictors' residuals (no spatial correlation: codebook indices of independent
+    // attributes), predict nothing (mode 0 everywhere) and redo phase A for that image
+    uint8_t *hp = (uint8_t *)pinned(c, pin);
+    bool again = false;
+    std::vector<int> forced(njobs, 0);
     for (int j = 0; j < njobs; ++j) {
-        const uint32_t *hist = (const uint32_t *)(hp + stage[j].first);
-        uint8_t *modes = hp + stage[j].second;
-        const size_t blocks = (size_t)((jobs[j].w + PB - 1) / PB) * ((jobs[j].h + PB - 1) / PB);
+        const uint32_t *h = (const uint32_t *)(hp + stage[j].hist);
+        const double sel = vp8l::literal_bits(h) + vp8l::literal_bits(h + vp8l::kTabSize);
+        const double raw = vp8l::literal_bits((const uint32_t *)(hp + stage[j].raw));
+        if (raw < 0.995 * sel && !getenv("ST_WEBP_NO_MODE0")) {
+            forced[j] = 1;
+            again = true;
+        }
+    }
+    if (again) {
+        for (int j = 0; j < njobs; ++j)
+            if (forced[j]) phase_a(j, 0);
+        ST_HIP(hipStreamSynchronize(c->stream));
+    }
+    // host: prefix codes + header bits (two groups when some block holds a literal alpha residual)
+    std::vector<vp8l::Header> hdr(njobs);
+    std::vector<int> ngroups(njobs, 1);
+    for (int j = 0; j < njobs; ++j) {
+        int bw, bh, gw, gh;
+        geom(jobs[j], bw, bh, gw, gh);
+        const uint32_t *hist = (const uint32_t *)(hp + stage[j].hist);
+        uint8_t *modes = hp + stage[j].modes;
+        const uint8_t *flags = hp + stage[j].flags;
         bool alpha_used = false;
-        for (size_t i = 0; i < blocks; ++i) {
+        for (int i = 0; i < bw * bh; ++i) {
             alpha_used = alpha_used || (modes[i] & 0x80);
             modes[i] &= 0x7f;
         }
-        vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, hist, modes, hdr[j]);
+        for (int i = 0; i < gw * gh && ngroups[j] == 1; ++i)
+            if (flags[i]) ngroups[j] = CODE_GROUPS;
+        if (ngroups[j] > 1 && !getenv("ST_WEBP_ONE_GROUP")) {
+            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, hist, ngroups[j], flags, GROUP_BITS, modes, hdr[j]);
+        } else {  // one group: group 1's symbols (if any) join group 0
+            ngroups[j] = 1;
+            std::vector<uint32_t> merged(vp8l::kTabSize);
+            for (int s = 0; s < vp8l::kTabSize; ++s) merged[s] = hist[s] + hist[vp8l::kTabSize + s];
+            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, merged.data(), 1, flags, GROUP_BITS, modes, hdr[j]);
+        }
     }
     // phase C: bit counts, offsets, emission
     std::vector<std::vector<uint8_t>> head(njobs);
@@ -617,6 +713,8 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     for (int j = 0; j < njobs; ++j) {
         WebpJob &jb = jobs[j];
         tags[j] = "wp" + std::to_string(j);
+        int bw, bh, gw, gh;
+        geom(jb, bw, bh, gw, gh);
         const uint64_t npix = (uint64_t)jb.w * jb.h;
         const uint32_t nwg = (uint32_t)((npix + EMIT_PIX - 1) / EMIT_PIX);
         // RIFF header (sizes patched by k_vp8l_scan) + the VP8L header bits
@@ -625,18 +723,20 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         std::memcpy(head[j].data() + 8, "WEBPVP8L", 8);
         const std::vector<uint8_t> hb = hdr[j].bw.bytes();
         head[j].insert(head[j].end(), hb.begin(), hb.end());
-        uint32_t *tab = wsT<uint32_t>(c, tags[j] + ".tab", vp8l::kTabSize);
+        uint32_t *tab = wsT<uint32_t>(c, tags[j] + ".tab", (size_t)CODE_GROUPS * vp8l::kTabSize);
         uint32_t *wg_bits = wsT<uint32_t>(c, tags[j] + ".wgb", nwg);
         uint64_t *wg_off = wsT<uint64_t>(c, tags[j] + ".wgo", (size_t)nwg + 1);
         uint64_t *fsize = wsT<uint64_t>(c, tags[j] + ".fsz", 1);
         const uint32_t *resid = wsT<uint32_t>(c, tags[j] + ".res", npix);
         const uint16_t *tok = wsT<uint16_t>(c, tags[j] + ".tok", npix);
+        const uint8_t *gflag = wsT<uint8_t>(c, tags[j] + ".gfl", (size_t)gw * gh);
         ST_HIP(hipMemsetAsync(jb.out, 0, webp_max_size(jb.w, jb.h), c->stream));
         ST_HIP(hipMemcpyAsync(jb.out, head[j].data(), head[j].size(), hipMemcpyHostToDevice, c->stream));
-        ST_HIP(hipMemcpyAsync(tab, hdr[j].tab.data(), vp8l::kTabSize * 4, hipMemcpyHostToDevice, c->stream));
+        ST_HIP(hipMemcpyAsync(tab, hdr[j].tab.data(), hdr[j].tab.size() * 4, hipMemcpyHostToDevice, c->stream));
         {
             KTimer kt(c, "webp.bits");
-            hipLaunchKernelGGL(k_vp8l_bits, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, tab, wg_bits);
+            hipLaunchKernelGGL(k_vp8l_bits, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, jb.w, gw, gflag,
+                               ngroups[j], tab, wg_bits);
             ST_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(k_vp8l_scan, dim3(1), dim3(1024), 0, c->stream, wg_bits, nwg,
@@ -644,12 +744,12 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         ST_LAUNCH_CHECK();
         {
             KTimer kt(c, "webp.emit");
-            hipLaunchKernelGGL(k_vp8l_emit, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, tab, wg_off,
-                               (uint32_t *)jb.out);
+            hipLaunchKernelGGL(k_vp8l_emit, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, jb.w, gw, gflag,
+                               ngroups[j], tab, wg_off, (uint32_t *)jb.out);
             ST_LAUNCH_CHECK();
         }
     }
-    uint64_t *sizes = (uint64_t *)pinned(c, 8 * (size_t)njobs);
+    uint64_t *sizes = (uint64_t *)pinned_slot(c, "wp.sizes", 8 * (size_t)njobs);
     for (int j = 0; j < njobs; ++j)
         ST_HIP(hipMemcpyAsync(sizes + j, wsT<uint64_t>(c, tags[j] + ".fsz", 1), 8, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));  // also keeps head[] alive until the copies ran

@@ -103,40 +103,11 @@ int main(int argc, char **argv) {
                 if (cost[m] < cost[best]) best = m;
             modes[(size_t)by * bw + bx] = (uint8_t)best;
         }
-    std::vector<uint32_t> hist(kTabSize, 0);
-    for (int y = 0; y < h; ++y)
-        for (int x = 0; x < w; ++x) {
-            uint32_t p;
-            if (y == 0)
-                p = x == 0 ? 0xff000000u : at(x - 1, y);
-            else if (x == 0)
-                p = at(x, y - 1);
-            else {
-                const uint32_t TR = (x + 1 < w) ? at(x + 1, y - 1) : at(0, y);
-                p = pred(modes[(size_t)(y / B) * bw + x / B], at(x - 1, y), at(x, y - 1), at(x - 1, y - 1), TR);
-            }
-            res[(size_t)y * w + x] = sub(at(x, y), p);
-        }
-    // tokens as k_vp8l_runs: inside each 4,096-pixel group, a run of >= 3 residuals equal to
-    // their left neighbour is one copy (distance code 2, the pixel to the left)
-    const size_t npix = res.size();
-    std::vector<uint32_t> tok(npix, 0);  // 0 literal, 0xffff covered, else copy length
-    for (size_t g0 = 0; g0 < npix; g0 += 4096) {
-        const size_t g1 = std::min(npix, g0 + 4096);
-        for (size_t i = g0; i < g1;) {
-            if (i > 0 && res[i] == res[i - 1]) {
-                size_t j = i;
-                while (j < g1 && res[j] == res[j - 1]) ++j;
-                if (j - i >= 3) {
-                    tok[i] = (uint32_t)(j - i);
-                    for (size_t q = i + 1; q < j; ++q) tok[q] = 0xffff;
-                }
-                i = j;
-            } else {
-                ++i;
-            }
-        }
-    }
+    // the device encoder's choices, restated: residuals of the chosen predictors; tokens (runs of
+    // >= 3 residuals equal to their left neighbour inside each 4,096-pixel group become copies at
+    // distance code 2); blocks of 32 x 32 holding a literal alpha residual form prefix-code group 1;
+    // when the pixels themselves (predictor 0) take fewer literal bits, everything is redone with
+    // predictor 0
     auto prefix_of = [](uint32_t v, uint32_t &pfx, uint32_t &ne, uint32_t &ex) {
         if (v <= 4) {
             pfx = v - 1, ne = 0, ex = 0;
@@ -148,38 +119,94 @@ int main(int argc, char **argv) {
         ex = d & ((1u << ne) - 1);
         pfx = 2 * hb + ((d >> (hb - 1)) & 1u);
     };
-    for (size_t i = 0; i < npix; ++i) {
-        const uint32_t r = res[i];
-        if (tok[i] == 0xffff) continue;
-        if (tok[i]) {
-            uint32_t pfx, ne, ex;
-            prefix_of(tok[i], pfx, ne, ex);
-            hist[kOffG + 256 + pfx]++;
-            hist[kOffD + 1]++;
-            continue;
+    const size_t npix = res.size();
+    const int GB = 5, gw = (w + (1 << GB) - 1) >> GB, gh = (h + (1 << GB) - 1) >> GB;
+    std::vector<uint32_t> tok(npix, 0);  // 0 literal, 0xffff covered, else copy length
+    std::vector<uint8_t> gfl((size_t)gw * gh, 0);
+    std::vector<uint32_t> hist(2 * kTabSize, 0), raw(kTabSize, 0);
+    auto encode_pass = [&](bool force0) {
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) {
+                uint32_t p;
+                if (y == 0)
+                    p = x == 0 ? 0xff000000u : at(x - 1, y);
+                else if (x == 0)
+                    p = at(x, y - 1);
+                else {
+                    const uint32_t TR = (x + 1 < w) ? at(x + 1, y - 1) : at(0, y);
+                    const int m = force0 ? 0 : modes[(size_t)(y / B) * bw + x / B];
+                    p = pred(m, at(x - 1, y), at(x, y - 1), at(x - 1, y - 1), TR);
+                }
+                res[(size_t)y * w + x] = sub(at(x, y), p);
+            }
+        std::fill(tok.begin(), tok.end(), 0u);
+        for (size_t g0 = 0; g0 < npix; g0 += 4096) {
+            const size_t g1 = std::min(npix, g0 + 4096);
+            for (size_t i = g0; i < g1;) {
+                if (i > 0 && res[i] == res[i - 1]) {
+                    size_t j = i;
+                    while (j < g1 && res[j] == res[j - 1]) ++j;
+                    if (j - i >= 3) {
+                        tok[i] = (uint32_t)(j - i);
+                        for (size_t q = i + 1; q < j; ++q) tok[q] = 0xffff;
+                    }
+                    i = j;
+                } else {
+                    ++i;
+                }
+            }
         }
-        hist[kOffG + ch(r, 1)]++;
-        hist[kOffR + ch(r, 2)]++;
-        hist[kOffB + ch(r, 0)]++;
-        hist[kOffA + ch(r, 3)]++;
+        std::fill(gfl.begin(), gfl.end(), 0);
+        for (size_t i = 0; i < npix; ++i)
+            if (tok[i] == 0 && (res[i] >> 24) != 0) gfl[(i / w >> GB) * gw + ((i % w) >> GB)] = 1;
+        std::fill(hist.begin(), hist.end(), 0u);
+        std::fill(raw.begin(), raw.end(), 0u);
+        for (size_t i = 0; i < npix; ++i) {
+            const uint32_t v = sub(argb[i], 0xff000000u);
+            raw[kOffG + ch(v, 1)]++, raw[kOffR + ch(v, 2)]++, raw[kOffB + ch(v, 0)]++, raw[kOffA + ch(v, 3)]++;
+            if (tok[i] == 0xffff) continue;
+            uint32_t *H = hist.data() + (size_t)gfl[(i / w >> GB) * gw + ((i % w) >> GB)] * kTabSize;
+            if (tok[i]) {
+                uint32_t pfx, ne, ex;
+                prefix_of(tok[i], pfx, ne, ex);
+                H[kOffG + 256 + pfx]++;
+                H[kOffD + 1]++;
+                continue;
+            }
+            const uint32_t r = res[i];
+            H[kOffG + ch(r, 1)]++, H[kOffR + ch(r, 2)]++, H[kOffB + ch(r, 0)]++, H[kOffA + ch(r, 3)]++;
+        }
+    };
+    encode_pass(false);
+    if (literal_bits(raw.data()) < 0.995 * (literal_bits(hist.data()) + literal_bits(hist.data() + kTabSize))) {
+        std::fill(modes.begin(), modes.end(), 0);
+        encode_pass(true);
     }
+    int ngroups = 1;
+    for (uint8_t f : gfl) ngroups = f ? 2 : ngroups;
     Header hd;
-    build_header(w, h, alpha, hist.data(), modes.data(), hd);
+    if (ngroups == 2) {
+        build_header(w, h, alpha, hist.data(), 2, gfl.data(), GB, modes.data(), hd);
+    } else {
+        std::vector<uint32_t> merged(kTabSize);
+        for (int q = 0; q < kTabSize; ++q) merged[q] = hist[q] + hist[kTabSize + q];
+        build_header(w, h, alpha, merged.data(), 1, gfl.data(), GB, modes.data(), hd);
+    }
     BitWriter &bw_ = hd.bw;
     for (size_t i = 0; i < npix; ++i) {
         const uint32_t r = res[i];
         if (tok[i] == 0xffff) continue;
+        const uint32_t *T = hd.tab.data() + (ngroups == 2 ? (size_t)gfl[(i / w >> GB) * gw + ((i % w) >> GB)] : 0) * kTabSize;
         if (tok[i]) {
             uint32_t pfx, ne, ex;
             prefix_of(tok[i], pfx, ne, ex);
-            const uint32_t eg = hd.tab[kOffG + 256 + pfx], ed = hd.tab[kOffD + 1];
+            const uint32_t eg = T[kOffG + 256 + pfx], ed = T[kOffD + 1];
             bw_.put(eg & 0xffffu, (int)(eg >> 16));
             bw_.put(ex, (int)ne);
             bw_.put(ed & 0xffffu, (int)(ed >> 16));
             continue;
         }
-        const uint32_t e[4] = {hd.tab[kOffG + ch(r, 1)], hd.tab[kOffR + ch(r, 2)], hd.tab[kOffB + ch(r, 0)],
-                               hd.tab[kOffA + ch(r, 3)]};
+        const uint32_t e[4] = {T[kOffG + ch(r, 1)], T[kOffR + ch(r, 2)], T[kOffB + ch(r, 0)], T[kOffA + ch(r, 3)]};
         for (int k = 0; k < 4; ++k) bw_.put(e[k] & 0xffffu, (int)(e[k] >> 16));
     }
     std::vector<uint8_t> body = bw_.bytes();

@@ -82,6 +82,11 @@ def main(n=10_000_000, reps=3, pil=True):
         out['libwebp_total_ms'] = sum(v['ms'] for v in ref.values())
         out['libwebp_total_bytes'] = sum(v['bytes'] for v in ref.values())
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+    if '--crops' in sys.argv:  # the first 256 rows of each texture, for encoder experiments on the host
+        for key, (w, h) in [(k, (W, H)) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')] + \
+                [('shN_centroids', (cw, ch))]:
+            a = tex[key].cpu().numpy().reshape(h, w, 4)[:256]
+            np.save(os.path.join(ROOT, 'gpurun_out', f'crop_{key}.npy'), a)
     with open(os.path.join(ROOT, 'gpurun_out', 'bundle.json'), 'w') as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
