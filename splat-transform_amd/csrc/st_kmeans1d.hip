@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
                                                    uint32_t *ticket, uint32_t *__restrict__ info,
                                                    const float *const *cols, const double *__restrict__ draws,
                                                    uint64_t ndraws, State *st, uint32_t many_above,
-                                                   const Bnd1 *__restrict__ bnd) {
+                                                   const Bnd1 *__restrict__ bnd, uint32_t *__restrict__ ffz) {
     const int cl = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     double s = 0, a = 0;
     int e = 1 << 20;
@@ -1269,6 +1269,8 @@ __global__ __launch_bounds__(256) void k_kd1_final(const Part1 *__restrict__ par
         if (nflag > many_above) atomicOr(&st->err, ERR_K1_MANY);
         if (tot != (uint32_t)n) atomicOr(&st->err, ERR_INTERNAL);
         *ticket = 0u;
+        if (ffz)  // k_ff_place's candidate-pool cursors
+            for (int i = 0; i < FF_MAX; ++i) ffz[i] = 0u;
     }
 }
 
@@ -1492,6 +1494,359 @@ __global__ __launch_bounds__(256) void k_ff_scatter(const uint8_t *__restrict__ 
     }
 }
 
+// ---- the flagged clusters' update in three passes (the queued path) -------------------
+// What count / scan / scatter, the chunk list and the replay's five passes do above, in three
+// launches and a finish.  k_ff_batch: each wave takes a batch of FB_B chunks of FF_CH points
+// (each lane 16 points of a chunk: one 16-byte label load, four 16-byte value loads), and per
+// flagged cluster (slot f) writes the batch's members in point order into its own region of
+// scr and the batch's count and exact sum (int128 units of 2^e_lo) into agg.  k_ff_bscan: one
+// workgroup per slot scans the batches' (count, sum) into exclusive prefixes.  k_ff_place: one
+// wave per (slot, batch) places the batch's members in vals (the sequential chain's input)
+// from its prefix and lists the replay candidates P_j of st_replay.h into the slot's pool
+// (ccnt / cpos: the batch's candidates and their pool position).  k_ff_finish gathers the
+// candidates in batch order and replays them as k_rp_finish does.
+constexpr int FB_B = 4;
+constexpr uint32_t FB_PTS = FB_B * FF_CH;
+struct FAgg {
+    __int128 sum;   // exact, units of 2^e_lo (0 when the cluster is past the int128 range)
+    uint32_t cnt;   // members
+    uint32_t base;  // the slot's first member in the batch's scr region
+    uint32_t pad[2];
+};
+
+__device__ inline __int128 wave_sum_i128(__int128 v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t lo = __shfl_xor((uint64_t)v, o, 64), hi = __shfl_xor((uint64_t)(v >> 64), o, 64);
+        v += (__int128)(((unsigned __int128)hi << 64) | lo);
+    }
+    return v;
+}
+// the slot table the three passes share: fl[0] = slots, fl[1 + f] = cluster
+__device__ inline bool ff_live(double sabs, int e_lo) {  // the int128 range of the replay
+    return sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, e_lo + 118);
+}
+
+__global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
+                                                  uint64_t n, uint32_t nbt, int k,
+                                                  const uint32_t *__restrict__ seq_flag,
+                                                  const int32_t *__restrict__ emin_c,
+                                                  const double *__restrict__ sabs_c, float *__restrict__ scr,
+                                                  FAgg *__restrict__ agg, uint32_t *__restrict__ fl) {
+    __shared__ uint32_t list[FF_MAX], nl;
+    ff_list(seq_flag, k, list, &nl);
+    __shared__ int32_t s_elo[FF_MAX];
+    __shared__ uint32_t s_live[FF_MAX];
+    __shared__ float s_val[4][FB_B][64][17];  // [wave][chunk][lane][point]; 17: no bank conflicts
+    const uint32_t nf = nl;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (blockIdx.x == 0 && t <= (int)nf) fl[t] = t == 0 ? nf : list[t - 1];
+    if (nf == 0) return;  // uniform
+    if (t < (int)nf) {
+        const uint32_t cl = list[t];
+        s_elo[t] = emin_c[cl];
+        s_live[t] = ff_live(sabs_c[cl], emin_c[cl]) ? 1u : 0u;
+    }
+    __syncthreads();
+    const float *row = &s_val[w][0][lane][0];  // chunk j, point e: row[j * 64 * 17 + e]
+    for (uint32_t b = blockIdx.x * 4 + (uint32_t)w; b < nbt; b += gridDim.x * 4) {
+        // the lane's labels and (where it holds a member of any flagged cluster) values
+        uint4 L[FB_B];
+        const uint64_t p0 = (uint64_t)b * FB_PTS + (uint64_t)lane * 16;
+#pragma unroll
+        for (int j = 0; j < FB_B; ++j) L[j] = ff_labels(lab8, n, b * FB_B + j, lane);
+        float4 vv[FB_B][4];
+        bool got[FB_B];
+#pragma unroll
+        for (int j = 0; j < FB_B; ++j) {
+            uint32_t any = 0;
+            const uint32_t x[4] = {L[j].x, L[j].y, L[j].z, L[j].w};
+            for (uint32_t f = 0; f < nf; ++f)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) any |= ff_match(x[q], list[f]);
+            const uint64_t pj = p0 + (uint64_t)j * FF_CH;
+            got[j] = any && pj + 16 <= n;
+            if (got[j]) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) vv[j][q] = *reinterpret_cast<const float4 *>(pts + pj + 4 * q);
+            } else if (any) {
+                for (int e = 0; e < 16; ++e) s_val[w][j][lane][e] = pj + e < n ? pts[pj + e] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < FB_B; ++j)
+            if (got[j]) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    s_val[w][j][lane][4 * q] = vv[j][q].x;
+                    s_val[w][j][lane][4 * q + 1] = vv[j][q].y;
+                    s_val[w][j][lane][4 * q + 2] = vv[j][q].z;
+                    s_val[w][j][lane][4 * q + 3] = vv[j][q].w;
+                }
+            }
+        uint32_t base = 0;  // the slot's first member in the batch's region
+        float *out = scr + (uint64_t)b * FB_PTS;
+        for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t cl = list[f];
+            const int e_lo = s_elo[f];
+            const bool live = s_live[f] != 0u;
+            uint32_t o = base;
+            __int128 s = 0;
+#pragma unroll
+            for (int j = 0; j < FB_B; ++j) {
+                const uint32_t x[4] = {L[j].x, L[j].y, L[j].z, L[j].w};
+                uint32_t msk = 0;  // bit e: point e of the lane's 16 is a member
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t m = ff_match(x[q], cl) & ff_valid_mask(n, b * FB_B + j, lane, q);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) msk |= ((m >> (8 * e + 7)) & 1u) << (4 * q + e);
+                }
+                const uint32_t c = __popc(msk);
+                uint32_t ci = c;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t u = __shfl_up(ci, d, 64);
+                    if (lane >= d) ci += u;
+                }
+                uint32_t at = o + ci - c;
+                for (uint32_t mm = msk; mm; mm &= mm - 1) {
+                    const float x = row[j * 64 * 17 + __builtin_ctz(mm)];
+                    out[at++] = x;
+                    if (live) s += f32_units(__builtin_bit_cast(uint32_t, x), e_lo);
+                }
+                o += __shfl(ci, 63, 64);
+            }
+            const __int128 S = live ? wave_sum_i128(s) : (__int128)0;
+            if (lane == 0) agg[(uint64_t)f * nbt + b] = FAgg{S, o - base, base, {0u, 0u}};
+            base = o;
+        }
+    }
+}
+
+// one 1,024-thread workgroup per slot: the batches' exclusive prefixes (in place: agg[.].sum and
+// .cnt become the prefix before the batch; .base stays) and the slot's totals
+constexpr int FN_T = 1024;
+__global__ __launch_bounds__(FN_T) void k_ff_bscan(uint32_t nbt, const uint32_t *__restrict__ fl,
+                                                   FAgg *__restrict__ agg, FAgg *__restrict__ tot) {
+    const uint32_t f = blockIdx.x;
+    if (f >= fl[0]) return;  // uniform
+    __shared__ __int128 ws[FN_T / 64];
+    __shared__ uint32_t wc[FN_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    FAgg *a = agg + (uint64_t)f * nbt;
+    __int128 run = 0;
+    uint32_t runc = 0;
+    for (uint32_t b0 = 0; b0 < nbt; b0 += FN_T) {
+        const uint32_t b = b0 + (uint32_t)t;
+        const FAgg v = b < nbt ? a[b] : FAgg{0, 0u, 0u, {0u, 0u}};
+        __int128 incl = v.sum;
+        uint32_t ic = v.cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const __int128 u = shfl_up_i128(incl, d);
+            const uint32_t uc = __shfl_up(ic, d, 64);
+            if (lane >= d) {
+                incl += u;
+                ic += uc;
+            }
+        }
+        if (lane == 63) {
+            ws[w] = incl;
+            wc[w] = ic;
+        }
+        __syncthreads();
+        __int128 off = run, all = 0;
+        uint32_t offc = runc, allc = 0;
+        for (int i = 0; i < FN_T / 64; ++i) {
+            if (i < w) {
+                off += ws[i];
+                offc += wc[i];
+            }
+            all += ws[i];
+            allc += wc[i];
+        }
+        __syncthreads();
+        if (b < nbt) a[b] = FAgg{off + incl - v.sum, offc + ic - v.cnt, v.base, {0u, 0u}};
+        run += all;
+        runc += allc;
+    }
+    if (t == 0) tot[f] = FAgg{run, runc, 0u, {0u, 0u}};
+}
+
+// one wave per (slot, batch) with members: each lane a contiguous run of the batch's members;
+// their exact running sums give the candidates
+__global__ __launch_bounds__(256) void k_ff_place(uint32_t nbt, const uint32_t *__restrict__ fl,
+                                                  const uint32_t *__restrict__ fstart,
+                                                  const int32_t *__restrict__ emin_c,
+                                                  const double *__restrict__ sabs_c, const float *__restrict__ scr,
+                                                  const FAgg *__restrict__ agg, uint32_t *__restrict__ ffz,
+                                                  uint32_t *__restrict__ vals, __int128 *__restrict__ pool,
+                                                  uint32_t *__restrict__ ccnt, uint32_t *__restrict__ cpos,
+                                                  const FAgg *__restrict__ tot) {
+    const uint32_t nf = fl[0];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint64_t q = (uint64_t)blockIdx.x * 4 + w; q < (uint64_t)nf * nbt; q += (uint64_t)gridDim.x * 4) {
+        const uint32_t f = (uint32_t)(q / nbt), b = (uint32_t)(q % nbt);
+        const FAgg a = agg[q];
+        const uint32_t C = (b + 1 < nbt ? agg[q + 1].cnt : tot[f].cnt) - a.cnt;  // the batch's members
+        if (C == 0) {
+            if (lane == 0) ccnt[q] = 0u;
+            continue;
+        }
+        const uint32_t cl = fl[1 + f];
+        const int e_lo = emin_c[cl];
+        const double sabs = sabs_c[cl];
+        const bool live = ff_live(sabs, e_lo);
+        const __int128 margin = rp_margin(sabs, e_lo);
+        const float *in = scr + (uint64_t)b * FB_PTS + a.base;
+        const uint32_t per = (C + 63) / 64, i0 = min(C, (uint32_t)lane * per), i1 = min(C, i0 + per);
+        uint32_t *dst = vals + fstart[cl] + a.cnt;
+        __int128 s = 0;
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint32_t xb = __builtin_bit_cast(uint32_t, in[i]);
+            dst[i] = xb;
+            if (live) s += f32_units(xb, e_lo);
+        }
+        if (!live) {
+            if (lane == 0) ccnt[q] = 0u;
+            continue;
+        }
+        __int128 si = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const __int128 u = shfl_up_i128(si, d);
+            if (lane >= d) si += u;
+        }
+        const __int128 P0 = a.sum + (si - s);
+        uint32_t nc = 0;
+        {
+            __int128 P = P0;
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t xb = __builtin_bit_cast(uint32_t, in[i]);
+                const __int128 Pn = P + f32_units(xb, e_lo);
+                nc += replay_candidate(P, Pn, xb, e_lo, margin) ? 1u : 0u;
+                P = Pn;
+            }
+        }
+        uint32_t nci = nc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(nci, d, 64);
+            if (lane >= d) nci += u;
+        }
+        const uint32_t CT = __shfl(nci, 63, 64);
+        uint32_t pos = 0;
+        if (lane == 0) {
+            if (CT) pos = atomicAdd(&ffz[f], CT);
+            ccnt[q] = CT;
+            cpos[q] = pos;
+        }
+        pos = __shfl(pos, 0, 64);
+        if (nc) {  // past CAND_MAX: dropped (k_ff_finish then takes the sequential chain)
+            uint32_t o = pos + (nci - nc);
+            __int128 *pl = pool + (uint64_t)f * CAND_MAX;
+            __int128 P = P0;
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t xb = __builtin_bit_cast(uint32_t, in[i]);
+                const __int128 Pn = P + f32_units(xb, e_lo);
+                if (replay_candidate(P, Pn, xb, e_lo, margin)) {
+                    if (o < (uint32_t)CAND_MAX) pl[o] = Pn;
+                    ++o;
+                }
+                P = Pn;
+            }
+        }
+    }
+}
+
+// one 1,024-thread workgroup per slot: the batches' candidates in batch order into the
+// cluster's cand_all row, then the replay of k_rp_finish (the sequential chain for a cluster
+// past the int128 range, with more than cap candidates, or whose replay gives up)
+__global__ __launch_bounds__(FN_T) void k_ff_finish(uint32_t nbt, const uint32_t *__restrict__ fl,
+                                                    uint32_t *__restrict__ seq_flag,
+                                                    const uint32_t *__restrict__ fstart,
+                                                    const int32_t *__restrict__ emin_c,
+                                                    const double *__restrict__ sabs_c, const FAgg *__restrict__ tot,
+                                                    const uint32_t *__restrict__ vals,
+                                                    const __int128 *__restrict__ pool,
+                                                    const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ cpos,
+                                                    __int128 *__restrict__ cand_all, uint32_t cap,
+                                                    float *__restrict__ cen, State *st) {
+    const uint32_t f = blockIdx.x;
+    if (f >= fl[0]) return;  // uniform
+    const uint32_t cl = fl[1 + f];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t s0 = fstart[cl], s1 = fstart[cl + 1];
+    const int e_lo = emin_c[cl];
+    const double sabs = sabs_c[cl];
+    const FAgg tf = tot[f];
+    if (t == 0 && tf.cnt != s1 - s0) atomicOr(&st->err, ERR_INTERNAL);
+    bool seq = !ff_live(sabs, e_lo);
+    __shared__ uint32_t wsum[FN_T / 64];
+    __shared__ __int128 buf[FN_T];
+    uint32_t ctot = 0;
+    __int128 *cand = cand_all + (uint64_t)cl * CAND_MAX;
+    if (!seq) {
+        const __int128 *pl = pool + (uint64_t)f * CAND_MAX;
+        for (uint32_t b0 = 0; b0 < nbt; b0 += FN_T) {
+            const uint32_t i = b0 + (uint32_t)t;
+            const uint32_t c = i < nbt ? ccnt[(uint64_t)f * nbt + i] : 0u;
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += u;
+            }
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            uint32_t off = ctot, all = 0;
+            for (int j = 0; j < FN_T / 64; ++j) {
+                if (j < w) off += wsum[j];
+                all += wsum[j];
+            }
+            __syncthreads();
+            off += incl - c;
+            if (c) {
+                const uint32_t ps = cpos[(uint64_t)f * nbt + i];
+                for (uint32_t j = 0; j < c; ++j)
+                    if (off + j < cap && ps + j < (uint32_t)CAND_MAX) cand[off + j] = pl[ps + j];
+            }
+            ctot += all;
+        }
+        seq = ctot > cap;
+    }
+    __syncthreads();  // the candidates written above, read below by other threads
+    bool ok = !seq;
+    __int128 sv = 0, Pprev = 0;
+    const __int128 margin = rp_margin(sabs, e_lo);
+    for (uint32_t b = 0; !seq && b < ctot; b += FN_T) {  // seq, ctot uniform; thread 0 keeps ok
+        const uint32_t m = min((uint32_t)FN_T, ctot - b);
+        if ((uint32_t)t < m) buf[t] = cand[b + t];
+        __syncthreads();
+        if (t == 0) {
+            for (uint32_t i = 0; i < m; ++i) {
+                const __int128 Pc = buf[i];
+                const __int128 V = sv + (Pc - Pprev);
+                sv = f64_representable(V) ? V : f64_units(f64_round(V, e_lo), e_lo);
+                Pprev = Pc;
+                const __int128 dev = sv - Pc;
+                ok = ok && (dev < 0 ? -dev : dev) < margin;
+            }
+        }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    const __int128 fin = sv + (tf.sum - Pprev);
+    if (!ok || !f64_representable(fin)) {
+        seq_flag[cl] = 2u;
+        cen[cl] = (float)(seq_sum1d(vals, s0, s1) / (double)(s1 - s0));
+        return;
+    }
+    cen[cl] = (float)(f64_round(fin, e_lo) / (double)(s1 - s0));
+    seq_flag[cl] = 0u;
+}
+
 // per-tile member counts of the flagged clusters: tcnt[c * ntiles + tile] for flagged c
 __global__ __launch_bounds__(F1_T) void k_flag_tiles(const uint8_t *__restrict__ lab8, uint64_t n, uint32_t ntiles,
                                                     int k, const uint32_t *__restrict__ seq_flag,
@@ -1673,6 +2028,24 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         const uint32_t *mm = getenv("ST_K1_NO_BOUNDS") ? nullptr : wsT<uint32_t>(c, "km.mm", 2);
         auto *hinfo = static_cast<uint32_t *>(pinned_slot(c, "k1.info", 8));
         ST_HIP(hipMemsetAsync(ticket, 0, sizeof(uint32_t), c->stream));
+        // the three-pass flagged update (k_ff_batch / k_ff_bscan / k_ff_place + k_ff_finish);
+        // ST_K1_FF_CHAIN=1 keeps the count / scan / scatter / chunked-replay chain
+        const bool three_pass = !getenv("ST_K1_FF_CHAIN");
+        const uint32_t nbt = (uint32_t)((n + FB_PTS - 1) / FB_PTS);
+        uint32_t *ffz = nullptr, *ffcnt = nullptr, *ffpos = nullptr, *fflist = nullptr;
+        __int128 *ffpool = nullptr;
+        FAgg *ffagg = nullptr, *fftot = nullptr;
+        float *ffscr = nullptr;
+        if (three_pass) {
+            ffz = wsT<uint32_t>(c, "k1.ffz", FF_MAX);
+            ffcnt = wsT<uint32_t>(c, "k1.ffcnt", (size_t)FF_MAX * nbt);
+            ffpos = wsT<uint32_t>(c, "k1.ffpos", (size_t)FF_MAX * nbt);
+            fflist = wsT<uint32_t>(c, "k1.fflist", FF_MAX + 1);
+            ffpool = wsT<__int128>(c, "k1.ffpool", (size_t)FF_MAX * CAND_MAX);
+            ffagg = wsT<FAgg>(c, "k1.ffagg", (size_t)FF_MAX * nbt);
+            fftot = wsT<FAgg>(c, "k1.fftot", FF_MAX);
+            ffscr = wsT<float>(c, "k1.ffscr", (size_t)nbt * FB_PTS);
+        }
         // queued: no read-back per iteration (more than FF_MAX flagged clusters -> ERR_K1_MANY,
         // and kmeans_dev reruns with k1_sync); otherwise the count decides the flagged path
         const bool queued = !c->k1_sync && !getenv("ST_K1_TILES") && !getenv("ST_K1_SYNC");
@@ -1692,16 +2065,31 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             KTimer kt(c, "k1.sum");
             hipLaunchKernelGGL(k_kd1_final, dim3(k), dim3(256), 0, c->stream, part, G, k, n, cen, seq_flag, emin_c,
                                sabs_c, cnt_c, start, fstart, ticket, dinfo, dcols, ddraws, ndraws, dstate,
-                               queued ? ff_max : 0xffffffffu, bnd);
+                               queued ? ff_max : 0xffffffffu, bnd, ffz);
             ST_LAUNCH_CHECK();
             if (queued) {
                 // the flagged path queued behind the final with no read-back: its kernels find
                 // the flagged clusters on the device and return at once when there are none
-                const uint32_t nch = (uint32_t)((n + FF_CH - 1) / FF_CH);
-                hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nch, k, seq_flag, fhist);
-                hipLaunchKernelGGL(k_ff_scan, dim3(FF_MAX), dim3(FS_T), 0, c->stream, fhist, nch, k, seq_flag, fstart);
-                hipLaunchKernelGGL(k_ff_scatter, dim3(G), dim3(256), 0, c->stream, lab8, pts, n, nch, k, seq_flag, fhist,
-                                   vals);
+                if (three_pass) {
+                    const unsigned gb = (unsigned)std::min<uint64_t>((nbt + 3) / 4, 2048);
+                    hipLaunchKernelGGL(k_ff_batch, dim3(gb), dim3(256), 0, c->stream, lab8, pts, n, nbt, k, seq_flag,
+                                       emin_c, sabs_c, ffscr, ffagg, fflist);
+                    hipLaunchKernelGGL(k_ff_bscan, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, ffagg, fftot);
+                    const unsigned gp = (unsigned)std::min<uint64_t>(((uint64_t)FF_MAX * nbt + 3) / 4, 4096);
+                    hipLaunchKernelGGL(k_ff_place, dim3(gp), dim3(256), 0, c->stream, nbt, fflist, fstart, emin_c,
+                                       sabs_c, ffscr, ffagg, ffz, vals, ffpool, ffcnt, ffpos, fftot);
+                    hipLaunchKernelGGL(k_ff_finish, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, seq_flag,
+                                       fstart, emin_c, sabs_c, fftot, vals, ffpool, ffcnt, ffpos, cand_buf,
+                                       replay_cap(), cen, dstate);
+                    ST_LAUNCH_CHECK();
+                    mark(c, "k1.update");
+                    continue;
+                }
+                const uint32_t nchf = (uint32_t)((n + FF_CH - 1) / FF_CH);
+                hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nchf, k, seq_flag, fhist);
+                hipLaunchKernelGGL(k_ff_scan, dim3(FF_MAX), dim3(FS_T), 0, c->stream, fhist, nchf, k, seq_flag, fstart);
+                hipLaunchKernelGGL(k_ff_scatter, dim3(G), dim3(256), 0, c->stream, lab8, pts, n, nchf, k, seq_flag,
+                                   fhist, vals);
                 ST_LAUNCH_CHECK();
                 chunk_list(c, fstart, k, ch_cnt, ch_first, chunks, nullptr, FL_CH);
                 chunked_replay(c, vals, fstart, k, fl_maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum,

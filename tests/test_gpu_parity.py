@@ -164,17 +164,29 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters):
     same_bits(cent, ocent)
 
 
-@pytest.mark.parametrize('mode', ['', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX'])
+K1_MODES = ['', 'ST_K1_FF_CHAIN', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX=0', 'ST_REPLAY_CAP=0',
+            'ST_REPLAY_CAP=2']
+
+
+def set_mode(monkeypatch, mode):
+    if mode:
+        name, _, val = mode.partition('=')
+        monkeypatch.setenv(name, val or '1')
+
+
+@pytest.mark.parametrize('mode', K1_MODES)
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
 def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
     """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
     hold tiny members, so the sequential f64 sum rounds -- a few events (the replay) or many
-    (the sequential fallback).  mode: the iteration queued without read-backs (default), the
-    flagged count read back each iteration (ST_K1_SYNC), the flagged clusters' members gathered
-    by the tile kernels (ST_K1_TILES), every iteration's member sort (ST_K1_SORT), or the queued
-    run abandoned at the first flagged cluster and rerun synchronised (ST_K1_FF_MAX=0)."""
-    if mode:
-        monkeypatch.setenv(mode, '0' if mode == 'ST_K1_FF_MAX' else '1')
+    (the sequential fallback).  mode: the iteration queued without read-backs, the flagged
+    clusters updated by the one-pass look-back kernel (default) or by the count / scan /
+    scatter / replay chain (ST_K1_FF_CHAIN); the flagged count read back each iteration
+    (ST_K1_SYNC), the flagged clusters' members gathered by the tile kernels (ST_K1_TILES),
+    every iteration's member sort (ST_K1_SORT), the queued run abandoned at the first flagged
+    cluster and rerun synchronised (ST_K1_FF_MAX=0), or the replay capped at 0 / 2 candidates so
+    that the sequential chain takes over (ST_REPLAY_CAP)."""
+    set_mode(monkeypatch, mode)
     rng = np.random.default_rng(77)
     n = 300_000
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
@@ -189,12 +201,14 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch)
     assert np.array_equal(labels, olabels)
 
 
+@pytest.mark.parametrize('mode', ['', 'ST_K1_FF_CHAIN'])
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
-def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac):
+def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
     """The sort-free 1-D iteration at a size where every accumulating workgroup takes several
     4,096-point tiles and the flagged clusters' members are gathered from hundreds of tiles
-    (1.5M points per column, 4.5M values); 0.02 drives sums with many rounding events into
-    the sequential chain."""
+    (1.5M points per column, 4.5M values, 4,395 look-back chunks); 0.02 drives sums with many
+    rounding events into the sequential chain."""
+    set_mode(monkeypatch, mode)
     rng = np.random.default_rng(78)
     n = 1_500_000
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
@@ -202,6 +216,29 @@ def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac):
         tiny = rng.random(n) < tiny_frac
         c[tiny] *= np.float32(1e-9)
     draws = oracle.mulberry32(6, 1 << 14)
+    cent, labels, used = ctx.cluster1d(cols, 3, draws)
+    rc, ocent, olabels, oused = oracle.cluster1d(cols, 3, draws)
+    assert rc == 0 and used == oused
+    assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
+    assert np.array_equal(labels, olabels)
+
+
+@pytest.mark.parametrize('mode', ['', 'ST_K1_FF_CHAIN'])
+def test_cluster1d_sorted_columns_vs_oracle(ctx, mode, monkeypatch):
+    """Sorted columns (ascending, descending, ascending): every cluster's members are one
+    contiguous run of points, so the flagged cluster straddling 0 fills a few hundred chunks
+    and every other chunk of the one-pass update's look-back holds none of its members."""
+    set_mode(monkeypatch, mode)
+    rng = np.random.default_rng(79)
+    n = 2_000_000
+    cols = []
+    for j in range(3):
+        c = rng.normal(0, 1, n).astype(np.float32)
+        tiny = rng.random(n) < 2e-4
+        c[tiny] *= np.float32(1e-9)
+        c.sort()
+        cols.append(np.ascontiguousarray(c[::-1]) if j == 1 else c)
+    draws = oracle.mulberry32(7, 1 << 14)
     cent, labels, used = ctx.cluster1d(cols, 3, draws)
     rc, ocent, olabels, oused = oracle.cluster1d(cols, 3, draws)
     assert rc == 0 and used == oused

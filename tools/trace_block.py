@@ -23,7 +23,7 @@ def main():
         return re.sub(r'\(.*', '', n)[:48]
     starts = [i for i, r in enumerate(rows) if re.search(start, r[0])]
     i0 = starts[nth]
-    i1 = next(i for i in range(i0, len(rows)) if re.search(end, rows[i][0]))
+    i1 = next((i for i in range(i0, len(rows)) if re.search(end, rows[i][0])), len(rows) - 1)
     t0 = rows[i0][1]
     last = {}
     for i in range(i0, i1 + 1):
