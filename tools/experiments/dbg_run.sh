@@ -1,3 +1,3 @@
 #!/bin/bash
 # k-means diagnostics: ambiguous / tie / overflow counts per iteration + parity vs the oracle
-ST_DEBUG=1 python tools/dbg_kmeans.py > gpurun_out/dbg.log 2>&1
+ST_DEBUG=1 python tools/experiments/dbg_kmeans.py > gpurun_out/dbg.log 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # build a variant of libsplat_hip.so with one source file replaced:
-#   tools/mkvar.sh NAME TARGET SRC.hip   (TARGET = basename of the replaced csrc file, e.g. st_kmeans_nd)
+#   tools/experiments/mkvar.sh NAME TARGET SRC.hip   (TARGET = basename of the replaced csrc file, e.g. st_kmeans_nd)
 # (experiments only; load it with ST_LIB=tools/var/NAME.so)
 set -e
 name=$1; base=$2; src=$3

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Summary of tools/pmc_ab.sh: per library, the sweep launch's clock, matrix-pipe busy and
-wave-cycle split.   python tools/pmc_ab.py base cur"""
+"""Summary of tools/experiments/pmc_ab.sh: per library, the sweep launch's clock, matrix-pipe busy and
+wave-cycle split.   python tools/experiments/pmc_ab.py base cur"""
 import collections
 import csv
 import glob

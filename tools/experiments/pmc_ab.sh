@@ -1,6 +1,6 @@
 #!/bin/bash
 # sweep utilisation counters for the baseline library (tools/var/base.so) and the current one:
-# two --pmc passes each (kernel trace only), summarised by tools/pmc_ab.py
+# two --pmc passes each (kernel trace only), summarised by tools/experiments/pmc_ab.py
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -14,4 +14,4 @@ for v in ${PMC_LIBS:-base cur}; do
     timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pab_${v}_$i -o pmc --output-format csv -- python3 tools/kn_bench.py --n 10000000 --iters 1 > gpurun_out/pab_${v}_$i.log 2>&1 || { tail -20 gpurun_out/pab_${v}_$i.log; exit 1; }
   done
 done
-python3 tools/pmc_ab.py ${PMC_LIBS:-base cur}
+python3 tools/experiments/pmc_ab.py ${PMC_LIBS:-base cur}

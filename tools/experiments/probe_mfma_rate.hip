@@ -1,7 +1,7 @@
 // MFMA issue rate and held clock per f16 instruction shape on random operands (DVFS probe).
 // Every wave keeps its operands in registers and issues NACC independent accumulation chains;
 // the in-kernel clock is d(s_memtime) / d(s_memrealtime) x 100 MHz (MI355X_MICROARCH.md DVFS (6)).
-//   hipcc --offload-arch=gfx950 -O3 tools/probe_mfma_rate.hip -o tools/var/probe_mfma_rate
+//   hipcc --offload-arch=gfx950 -O3 tools/experiments/probe_mfma_rate.hip -o tools/var/probe_mfma_rate
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -1,6 +1,6 @@
 // Probe: rocPRIM's radix_sort_pairs on n (u32 key < 2^bits, u32 value) pairs -- the Morton
 // level-0 shape -- timed with HIP events, to compare with the library's 8-bit LSD passes.
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probe_sort.hip -o tools/var/probe_sort
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/experiments/probe_sort.hip -o tools/var/probe_sort
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>

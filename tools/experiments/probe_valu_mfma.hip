@@ -1,7 +1,7 @@
 // Cost of VALU fillers beside MFMAs (the sweep epilogue's budget): SIMD cycles per 16x16x48
 // pair (v_mfma_f32_16x16x32_f16 + v_mfma_f32_16x16x16_f16) and per 32x32x48 slot
 // (3 x v_mfma_f32_32x32x16_f16) with NV v_min3_f32 per pair / slot, at WPS waves per SIMD.
-//   hipcc --offload-arch=gfx950 -O3 tools/probe_valu_mfma.hip -o tools/var/probe_valu_mfma
+//   hipcc --offload-arch=gfx950 -O3 tools/experiments/probe_valu_mfma.hip -o tools/var/probe_valu_mfma
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -1,5 +1,5 @@
 #!/bin/bash
-# operand-data experiments on the assign sweep (variants built by tools/mkvar.sh; results of
+# operand-data experiments on the assign sweep (variants built by tools/experiments/mkvar.sh; results of
 # the variants are not labels, only the sweep's time is read)
 mkdir -p gpurun_out
 for v in ${@:-base tileconst allsame allzero base}; do

@@ -1,5 +1,5 @@
 #!/bin/bash
-# time the N-D k-means kernels of each variant library: tools/var_run.sh v0 v1 ...
+# time the N-D k-means kernels of each variant library: tools/experiments/var_run.sh v0 v1 ...
 set -o pipefail
 for v in "$@"; do
   echo "== $v"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# one pytest selection against several variant libraries: tools/var_tests.sh "-k expr" v1 v2 ...
+# one pytest selection against several variant libraries: tools/experiments/var_tests.sh "-k expr" v1 v2 ...
 sel=$1; shift
 for v in "$@"; do
   echo "== $v"
