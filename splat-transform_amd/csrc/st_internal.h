@@ -104,6 +104,10 @@ struct st_ctx {
     bool k1_sync = false;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    // a second stream of this context (side_stream): independent work of one call that
+    // overlaps latency-bound chains on `stream`, joined by the two events
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev[2] = {nullptr, nullptr};
     st::Workspace ws;
     // pinned host staging for small readbacks
     void *pinned = nullptr;
@@ -148,6 +152,7 @@ inline T *wsT(st_ctx *c, const std::string &slot, size_t count) {
     return static_cast<T *>(c->ws.get(slot, count * sizeof(T) + 16));
 }
 void *pinned(st_ctx *c, size_t bytes);  // host pinned scratch (reused)
+hipStream_t side_stream(st_ctx *c);     // c->side, created on first use (non-blocking)
 void *pinned_slot(st_ctx *c, const std::string &name, size_t bytes);  // named, grow-only
 void *archive_buf(st_ctx *c, size_t bytes);  // host pinned archive buffer (reused, grow-only)
 void *io_buf(st_ctx *c, size_t bytes);       // host pinned file-chunk buffer (reused, grow-only)

@@ -1527,6 +1527,17 @@ __device__ inline bool ff_live(double sabs, int e_lo) {  // the int128 range of 
     return sabs * (1.0 + 1.0e-6) < __builtin_ldexp(1.0, e_lo + 118);
 }
 
+// v[e] for a run-time e in [0, 16) by a tree of selects (no scratch indexing)
+__device__ inline float pick16(const float (&v)[16], int e) {
+    float a[8], b[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = (e & 1) ? v[2 * i + 1] : v[2 * i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (e & 2) ? a[2 * i + 1] : a[2 * i];
+    const float c0 = (e & 4) ? b[1] : b[0], c1 = (e & 4) ? b[3] : b[2];
+    return (e & 8) ? c1 : c0;
+}
+
 __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ lab8, const float *__restrict__ pts,
                                                   uint64_t n, uint32_t nbt, int k,
                                                   const uint32_t *__restrict__ seq_flag,
@@ -1537,7 +1548,6 @@ __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ la
     ff_list(seq_flag, k, list, &nl);
     __shared__ int32_t s_elo[FF_MAX];
     __shared__ uint32_t s_live[FF_MAX];
-    __shared__ float s_val[4][FB_B][64][17];  // [wave][chunk][lane][point]; 17: no bank conflicts
     const uint32_t nf = nl;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (blockIdx.x == 0 && t <= (int)nf) fl[t] = t == 0 ? nf : list[t - 1];
@@ -1548,42 +1558,15 @@ __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ la
         s_live[t] = ff_live(sabs_c[cl], emin_c[cl]) ? 1u : 0u;
     }
     __syncthreads();
-    const float *row = &s_val[w][0][lane][0];  // chunk j, point e: row[j * 64 * 17 + e]
     for (uint32_t b = blockIdx.x * 4 + (uint32_t)w; b < nbt; b += gridDim.x * 4) {
-        // the lane's labels and (where it holds a member of any flagged cluster) values
-        uint4 L[FB_B];
+        // the lane's 16 labels of each chunk; per slot and chunk it loads its 16 values only
+        // where it holds members of that slot (L2 serves a second slot's reload), then picks
+        // each member's value with a select tree: no LDS staging, no register arrays indexed at
+        // run time
         const uint64_t p0 = (uint64_t)b * FB_PTS + (uint64_t)lane * 16;
+        uint4 L[FB_B];
 #pragma unroll
         for (int j = 0; j < FB_B; ++j) L[j] = ff_labels(lab8, n, b * FB_B + j, lane);
-        float4 vv[FB_B][4];
-        bool got[FB_B];
-#pragma unroll
-        for (int j = 0; j < FB_B; ++j) {
-            uint32_t any = 0;
-            const uint32_t x[4] = {L[j].x, L[j].y, L[j].z, L[j].w};
-            for (uint32_t f = 0; f < nf; ++f)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) any |= ff_match(x[q], list[f]);
-            const uint64_t pj = p0 + (uint64_t)j * FF_CH;
-            got[j] = any && pj + 16 <= n;
-            if (got[j]) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) vv[j][q] = *reinterpret_cast<const float4 *>(pts + pj + 4 * q);
-            } else if (any) {
-                for (int e = 0; e < 16; ++e) s_val[w][j][lane][e] = pj + e < n ? pts[pj + e] : 0.f;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < FB_B; ++j)
-            if (got[j]) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    s_val[w][j][lane][4 * q] = vv[j][q].x;
-                    s_val[w][j][lane][4 * q + 1] = vv[j][q].y;
-                    s_val[w][j][lane][4 * q + 2] = vv[j][q].z;
-                    s_val[w][j][lane][4 * q + 3] = vv[j][q].w;
-                }
-            }
         uint32_t base = 0;  // the slot's first member in the batch's region
         float *out = scr + (uint64_t)b * FB_PTS;
         for (uint32_t f = 0; f < nf; ++f) {
@@ -1592,9 +1575,11 @@ __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ la
             const bool live = s_live[f] != 0u;
             uint32_t o = base;
             __int128 s = 0;
-#pragma unroll
+#pragma unroll 1
             for (int j = 0; j < FB_B; ++j) {
-                const uint32_t x[4] = {L[j].x, L[j].y, L[j].z, L[j].w};
+                static_assert(FB_B == 4, "the label select below");
+                const uint4 Lj = j == 0 ? L[0] : j == 1 ? L[1] : j == 2 ? L[2] : L[3];
+                const uint32_t x[4] = {Lj.x, Lj.y, Lj.z, Lj.w};
                 uint32_t msk = 0;  // bit e: point e of the lane's 16 is a member
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1610,10 +1595,27 @@ __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ la
                     if (lane >= d) ci += u;
                 }
                 uint32_t at = o + ci - c;
-                for (uint32_t mm = msk; mm; mm &= mm - 1) {
-                    const float x = row[j * 64 * 17 + __builtin_ctz(mm)];
-                    out[at++] = x;
-                    if (live) s += f32_units(__builtin_bit_cast(uint32_t, x), e_lo);
+                if (msk) {
+                    const uint64_t pj = p0 + (uint64_t)j * FF_CH;
+                    float v[16];
+                    if (pj + 16 <= n) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float4 u = *reinterpret_cast<const float4 *>(pts + pj + 4 * q);
+                            v[4 * q] = u.x;
+                            v[4 * q + 1] = u.y;
+                            v[4 * q + 2] = u.z;
+                            v[4 * q + 3] = u.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) v[e] = pj + e < n ? pts[pj + e] : 0.f;
+                    }
+                    for (uint32_t mm = msk; mm; mm &= mm - 1) {
+                        const float x = pick16(v, __builtin_ctz(mm));
+                        out[at++] = x;
+                        if (live) s += f32_units(__builtin_bit_cast(uint32_t, x), e_lo);
+                    }
                 }
                 o += __shfl(ci, 63, 64);
             }
@@ -1625,53 +1627,71 @@ __global__ __launch_bounds__(256) void k_ff_batch(const uint8_t *__restrict__ la
 }
 
 // one 1,024-thread workgroup per slot: the batches' exclusive prefixes (in place: agg[.].sum and
-// .cnt become the prefix before the batch; .base stays) and the slot's totals
+// .cnt become the prefix before the batch; .base stays) and the slot's totals.  Each thread
+// takes a contiguous run of batches (its sums in registers), so the workgroup scans once.
 constexpr int FN_T = 1024;
+// block-wide exclusive scan of (int128, u32) pairs over FN_T threads
+__device__ inline void fn_exscan(__int128 v, uint32_t c, __int128 &ex, uint32_t &exc, __int128 &all,
+                                 uint32_t &allc) {
+    __shared__ __int128 ws[FN_T / 64];
+    __shared__ uint32_t wc[FN_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    __int128 incl = v;
+    uint32_t ic = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const __int128 u = shfl_up_i128(incl, d);
+        const uint32_t uc = __shfl_up(ic, d, 64);
+        if (lane >= d) {
+            incl += u;
+            ic += uc;
+        }
+    }
+    if (lane == 63) {
+        ws[w] = incl;
+        wc[w] = ic;
+    }
+    __syncthreads();
+    __int128 off = 0, tot = 0;
+    uint32_t offc = 0, totc = 0;
+    for (int i = 0; i < FN_T / 64; ++i) {
+        if (i < w) {
+            off += ws[i];
+            offc += wc[i];
+        }
+        tot += ws[i];
+        totc += wc[i];
+    }
+    __syncthreads();
+    ex = off + incl - v;
+    exc = offc + ic - c;
+    all = tot;
+    allc = totc;
+}
+
 __global__ __launch_bounds__(FN_T) void k_ff_bscan(uint32_t nbt, const uint32_t *__restrict__ fl,
                                                    FAgg *__restrict__ agg, FAgg *__restrict__ tot) {
     const uint32_t f = blockIdx.x;
     if (f >= fl[0]) return;  // uniform
-    __shared__ __int128 ws[FN_T / 64];
-    __shared__ uint32_t wc[FN_T / 64];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t t = threadIdx.x, per = (nbt + FN_T - 1) / FN_T;
+    const uint32_t b0 = min(nbt, t * per), b1 = min(nbt, b0 + per);
     FAgg *a = agg + (uint64_t)f * nbt;
-    __int128 run = 0;
-    uint32_t runc = 0;
-    for (uint32_t b0 = 0; b0 < nbt; b0 += FN_T) {
-        const uint32_t b = b0 + (uint32_t)t;
-        const FAgg v = b < nbt ? a[b] : FAgg{0, 0u, 0u, {0u, 0u}};
-        __int128 incl = v.sum;
-        uint32_t ic = v.cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const __int128 u = shfl_up_i128(incl, d);
-            const uint32_t uc = __shfl_up(ic, d, 64);
-            if (lane >= d) {
-                incl += u;
-                ic += uc;
-            }
-        }
-        if (lane == 63) {
-            ws[w] = incl;
-            wc[w] = ic;
-        }
-        __syncthreads();
-        __int128 off = run, all = 0;
-        uint32_t offc = runc, allc = 0;
-        for (int i = 0; i < FN_T / 64; ++i) {
-            if (i < w) {
-                off += ws[i];
-                offc += wc[i];
-            }
-            all += ws[i];
-            allc += wc[i];
-        }
-        __syncthreads();
-        if (b < nbt) a[b] = FAgg{off + incl - v.sum, offc + ic - v.cnt, v.base, {0u, 0u}};
-        run += all;
-        runc += allc;
+    __int128 ls = 0;
+    uint32_t lc = 0;
+    for (uint32_t b = b0; b < b1; ++b) {
+        ls += a[b].sum;
+        lc += a[b].cnt;
     }
-    if (t == 0) tot[f] = FAgg{run, runc, 0u, {0u, 0u}};
+    __int128 ex, all;
+    uint32_t exc, allc;
+    fn_exscan(ls, lc, ex, exc, all, allc);
+    for (uint32_t b = b0; b < b1; ++b) {
+        const FAgg v = a[b];
+        a[b] = FAgg{ex, exc, v.base, {0u, 0u}};
+        ex += v.sum;
+        exc += v.cnt;
+    }
+    if (t == 0) tot[f] = FAgg{all, allc, 0u, {0u, 0u}};
 }
 
 // one wave per (slot, batch) with members: each lane a contiguous run of the batch's members;
@@ -1776,44 +1796,38 @@ __global__ __launch_bounds__(FN_T) void k_ff_finish(uint32_t nbt, const uint32_t
     const uint32_t f = blockIdx.x;
     if (f >= fl[0]) return;  // uniform
     const uint32_t cl = fl[1 + f];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int t = threadIdx.x;
     const uint32_t s0 = fstart[cl], s1 = fstart[cl + 1];
     const int e_lo = emin_c[cl];
     const double sabs = sabs_c[cl];
     const FAgg tf = tot[f];
     if (t == 0 && tf.cnt != s1 - s0) atomicOr(&st->err, ERR_INTERNAL);
-    bool seq = !ff_live(sabs, e_lo);
-    __shared__ uint32_t wsum[FN_T / 64];
+    bool seq = !ff_live(sabs, e_lo);  // uniform: fn_exscan's barriers below
     __shared__ __int128 buf[FN_T];
     uint32_t ctot = 0;
     __int128 *cand = cand_all + (uint64_t)cl * CAND_MAX;
     if (!seq) {
+        // each thread a contiguous run of batches: their candidate counts scanned once, then
+        // the run's candidates copied in batch order
         const __int128 *pl = pool + (uint64_t)f * CAND_MAX;
-        for (uint32_t b0 = 0; b0 < nbt; b0 += FN_T) {
-            const uint32_t i = b0 + (uint32_t)t;
-            const uint32_t c = i < nbt ? ccnt[(uint64_t)f * nbt + i] : 0u;
-            uint32_t incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += u;
-            }
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            uint32_t off = ctot, all = 0;
-            for (int j = 0; j < FN_T / 64; ++j) {
-                if (j < w) off += wsum[j];
-                all += wsum[j];
-            }
-            __syncthreads();
-            off += incl - c;
+        const uint32_t per = (nbt + FN_T - 1) / FN_T;
+        const uint32_t b0 = min(nbt, (uint32_t)t * per), b1 = min(nbt, b0 + per);
+        const uint32_t *cc = ccnt + (uint64_t)f * nbt, *cp = cpos + (uint64_t)f * nbt;
+        uint32_t lc = 0;
+        for (uint32_t b = b0; b < b1; ++b) lc += cc[b];
+        __int128 ex_unused, all_unused;
+        uint32_t off, all;
+        fn_exscan(0, lc, ex_unused, off, all_unused, all);
+        for (uint32_t b = b0; b < b1 && lc; ++b) {
+            const uint32_t c = cc[b];
             if (c) {
-                const uint32_t ps = cpos[(uint64_t)f * nbt + i];
+                const uint32_t ps = cp[b];
                 for (uint32_t j = 0; j < c; ++j)
                     if (off + j < cap && ps + j < (uint32_t)CAND_MAX) cand[off + j] = pl[ps + j];
             }
-            ctot += all;
+            off += c;
         }
+        ctot = all;
         seq = ctot > cap;
     }
     __syncthreads();  // the candidates written above, read below by other threads
@@ -2082,6 +2096,20 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                                        fstart, emin_c, sabs_c, fftot, vals, ffpool, ffcnt, ffpos, cand_buf,
                                        replay_cap(), cen, dstate);
                     ST_LAUNCH_CHECK();
+                    if (getenv("ST_DEBUG")) {  // flagged clusters, their members and replay candidates
+                        uint32_t hfl[FF_MAX + 1], hz[FF_MAX];
+                        std::vector<uint32_t> f2(k), fs(k + 1);
+                        ST_HIP(hipMemcpyAsync(hfl, fflist, sizeof hfl, hipMemcpyDeviceToHost, c->stream));
+                        ST_HIP(hipMemcpyAsync(hz, ffz, sizeof hz, hipMemcpyDeviceToHost, c->stream));
+                        ST_HIP(hipMemcpyAsync(f2.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost, c->stream));
+                        ST_HIP(hipMemcpyAsync(fs.data(), fstart, 4 * (k + 1), hipMemcpyDeviceToHost, c->stream));
+                        ST_HIP(hipStreamSynchronize(c->stream));
+                        fprintf(stderr, "[st k1] n=%llu flagged=%u", (unsigned long long)n, hfl[0]);
+                        for (uint32_t f = 0; f < hfl[0] && f < (uint32_t)FF_MAX; ++f)
+                            fprintf(stderr, " c%u:members=%u,cands=%u,seq=%u", hfl[1 + f],
+                                    fs[hfl[1 + f] + 1] - fs[hfl[1 + f]], hz[f], f2[hfl[1 + f]] == 2u ? 1u : 0u);
+                        fprintf(stderr, "\n");
+                    }
                     mark(c, "k1.update");
                     continue;
                 }

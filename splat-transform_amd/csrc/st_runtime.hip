@@ -52,6 +52,14 @@ void *pinned(st_ctx *c, size_t bytes) {
     return c->pinned;
 }
 
+hipStream_t side_stream(st_ctx *c) {
+    if (!c->side) {
+        ST_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        for (auto &e : c->side_ev) ST_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    return c->side;
+}
+
 void *pinned_slot(st_ctx *c, const std::string &name, size_t bytes) {
     auto &b = c->pinned_slots[name];
     if (b.second < bytes) {
@@ -431,6 +439,12 @@ void st_ctx_destroy(st_ctx *c) {
         (void)hipEventDestroy(k.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+    }
+    for (auto e : c->side_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -569,18 +569,33 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         cursor += kmeans_dev(c, src.sh, D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels, false,
                              src.sh64[0] ? src.sh64 : nullptr);
         mark(c, "sog.shkmeans");
+        // the shN labels texels (random 4-byte stores at the Morton positions) do not wait for
+        // the codebook: they run on the side stream beside its latency-bound 1-D iterations,
+        // on few workgroups so that those kernels still find free CUs
+        const hipStream_t ss = side_stream(c);
+        ST_HIP(hipEventRecord(c->side_ev[0], c->stream));
+        ST_HIP(hipStreamWaitEvent(ss, c->side_ev[0], 0));
+        ST_HIP(hipMemsetAsync(out->shn_labels, 0, texels * 4, ss));
+        // one workgroup per CU: the rest of each CU stays free for the codebook's kernels
+        hipLaunchKernelGGL(k_shn_labels_tex, dim3(std::min(g, 256u)), dim3(256), 0, ss, labels,
+                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->shn_labels);
+        ST_LAUNCH_CHECK();
+        ST_HIP(hipEventRecord(c->side_ev[1], ss));
         std::vector<const float *> ccols(D);
         for (int i = 0; i < D; ++i) ccols[i] = cen + (uint64_t)i * pal;
         auto *cl = wsT<uint8_t>(c, "sog.cl", (size_t)pal * D);
-        cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cb, cl);
+        try {
+            cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cb, cl);
+        } catch (...) {
+            (void)hipStreamWaitEvent(c->stream, c->side_ev[1], 0);
+            throw;
+        }
         ST_HIP(hipMemcpyAsync(meta->shn_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipMemsetAsync(out->shn_centroids, 0, (size_t)cw * chh * 4, c->stream));
-        ST_HIP(hipMemsetAsync(out->shn_labels, 0, texels * 4, c->stream));
         hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
                            cl, C, pal, (uint32_t *)out->shn_centroids);
-        hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, labels, (const uint32_t *)nullptr,
-                           pos, n, (uint32_t *)out->shn_labels);
         ST_LAUNCH_CHECK();
+        ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
         mark(c, "sog.shn");
     }
     ST_HIP(hipStreamSynchronize(c->stream));
