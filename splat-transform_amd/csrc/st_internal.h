@@ -87,6 +87,9 @@ struct st_ctx {
     // max |x| over the k-means point set, found by check_finite in the same pass as the
     // finiteness test (negative: not known, nd_prepare computes it)
     float km_absmax = -1.0f;
+    // the next kmeans_dev's points are finite by construction (the SOG writer's codebook over
+    // the SH centroids: data rows and means of finite rows): no finiteness pass and read-back
+    bool km_finite_known = false;
     // the N-D k-means point set prepared by nd_prepare (fp16 scale and shape)
     float kn_sigma = 1.0f;
     uint64_t kn_n = 0;

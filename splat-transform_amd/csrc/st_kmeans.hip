@@ -477,7 +477,9 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     }
     auto **dcols = wsT<const float *>(c, "km.cols", (size_t)d);
     ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
-    check_finite(c, cols, dcols, d, n);
+    const bool finite_known = c->km_finite_known && d == 1;
+    c->km_finite_known = false;
+    if (!finite_known) check_finite(c, cols, dcols, d, n);
     mark(c, "km.check");
 
     // Math.random stream: uploaded once, consumed on device in reference order

@@ -585,8 +585,12 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         for (int i = 0; i < D; ++i) ccols[i] = cen + (uint64_t)i * pal;
         auto *cl = wsT<uint8_t>(c, "sog.cl", (size_t)pal * D);
         try {
+            // the SH centroids are initial rows, means of finite rows or re-seeded rows: finite
+            c->km_finite_known = true;
             cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cb, cl);
+            c->km_finite_known = false;
         } catch (...) {
+            c->km_finite_known = false;
             (void)hipStreamWaitEvent(c->stream, c->side_ev[1], 0);
             throw;
         }

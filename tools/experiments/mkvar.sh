@@ -4,7 +4,7 @@
 # (experiments only; load it with ST_LIB=tools/var/NAME.so)
 set -e
 name=$1; base=$2; src=$3
-R=$(cd "$(dirname "$0")/.." && pwd)
+R=$(cd "$(dirname "$0")/../.." && pwd)
 B=$R/splat-transform_amd/build
 mkdir -p $R/tools/var
 flags="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result"
