@@ -219,6 +219,44 @@ void dist_assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, i
     c->ds_sorted = false;
 }
 
+namespace {
+// the (segment, label) member order of an N-D shard: payload = point indices, start = ranges
+void member_order_nd(st_ctx *c, const uint32_t *labels, uint64_t n, int nseg, int k) {
+    const uint64_t nk = (uint64_t)nseg * k;
+    auto *keys = wsT<uint32_t>(c, "ds.keys", n);
+    auto *payload = wsT<uint32_t>(c, "ds.payload", n);
+    auto *start = wsT<uint32_t>(c, "ds.start", nk + 1);
+    int bits = 1;
+    while ((1ull << bits) < nk) ++bits;
+    hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                       (uint32_t)(n / nseg), k, (const float *)nullptr, keys, payload);
+    ST_LAUNCH_CHECK();
+    radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
+    bounds_from_sorted(c, keys, n, (int)nk, start);
+}
+}  // namespace
+
+bool dist_assign_partials_nd(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen,
+                             uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
+    ST_REQUIRE(d > 1 && n < (1ull << 31), ST_ERR_ARG, "kmeans partials: N-D shard of fewer than 2^31 points");
+    auto **dcols = wsT<const float *>(c, "ds.cols", (size_t)d);
+    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
+    auto *dstate = static_cast<State *>(ws(c, "ds.state", sizeof(State)));
+    ST_HIP(hipMemsetAsync(dstate, 0, sizeof(State), c->stream));
+    NdFused fz;
+    fz.want = true;
+    nd_assign(c, dcols, d, n, k, cen, labels, dstate, &fz);
+    if (!fz.valid) return false;  // no fused fix-up (coinciding centroids, other shapes)
+    nd_fused_partials(c, d, n, k, fz, labels, sums, sabs, emin, counts);
+    c->ds_nseg = 1;
+    c->ds_k = k;
+    c->ds_d = d;
+    c->ds_n = n;
+    c->ds_labels = labels;
+    c->ds_sorted = false;  // the member order is built only if a pending pair needs it
+    return true;
+}
+
 void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
                    double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
     ST_REQUIRE(nseg >= 1 && n % (uint64_t)nseg == 0, ST_ERR_ARG, "kmeans partials: n must split into nseg segments");
@@ -234,11 +272,15 @@ void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int n
         // stable by label inside each (contiguous) segment: one value-only counting pass per segment
         seg_label_sort1d(c, cols[0], labels, n, nseg, k, payload, start);
     } else {
-        hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
-                           (uint32_t)(n / nseg), k, d == 1 ? cols[0] : (const float *)nullptr, keys, payload);
-        ST_LAUNCH_CHECK();
-        radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
-        bounds_from_sorted(c, keys, n, (int)nk, start);
+        if (d == 1) {
+            hipLaunchKernelGGL(k_seg_keys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                               (uint32_t)(n / nseg), k, cols[0], keys, payload);
+            ST_LAUNCH_CHECK();
+            radix_sort_u32(c, keys, payload, n, 0, bits, "ds.sort");
+            bounds_from_sorted(c, keys, n, (int)nk, start);
+        } else {
+            member_order_nd(c, labels, n, nseg, k);
+        }
     }
     if (d == 1) {
         partials1d(c, payload, n, start, (int)nk, sums, sabs, emin, counts);
@@ -274,6 +316,10 @@ void dist_seqsum(st_ctx *c, int d, int k, int seg, const uint32_t *pairs, uint32
         hipLaunchKernelGGL(k_seqsum_1d, dim3(npairs), dim3(64), 0, c->stream, payload, start, k, seg, pairs, flag,
                            running);
     } else {
+        if (!c->ds_sorted) {  // partials came from the fused fix-up: order the members now
+            member_order_nd(c, c->ds_labels, n, c->ds_nseg, k);
+            c->ds_sorted = true;
+        }
         auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
         hipLaunchKernelGGL(k_seqsum_nd, dim3((npairs + 63) / 64), dim3(64), 0, c->stream, aos, d, payload, start, k,
                            seg, pairs, npairs, running);

@@ -85,6 +85,11 @@ struct NdFused {
 };
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
                km::State *dstate, NdFused *fz = nullptr);
+// after a fused nd_assign (fz.valid): the (dimension, cluster) partials of the shard -- f64 sum,
+// sum|x|, smallest ulp exponent ([dim][k]) and counts -- from the fix-up's slices and the other
+// points, without the member sort (the sharded writer's N-D update)
+void nd_fused_partials(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, double *sums,
+                       double *sabs, int32_t *emin, uint32_t *counts);
 // returns true when it also wrote the update's (label, value bits) pairs into keys/vals
 // (need_labels = false with keys: the labels are not written, only the pairs)
 bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, uint32_t *labels,

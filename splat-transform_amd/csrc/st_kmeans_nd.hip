@@ -1143,6 +1143,64 @@ __global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ ao
     }
 }
 
+// the sharded writer's form of k_nd_combine (one segment: the whole shard): the same sums over
+// the slices' partials and the other members, written as the (dimension, cluster) partials the
+// all-reduce takes (dist_partials' layout [dim][k]) instead of certified centroids
+template <int LD>
+__global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ aos, int d, int k,
+                                                     const uint32_t *__restrict__ soff,
+                                                     const double *__restrict__ psum, const double *__restrict__ pabs,
+                                                     const int *__restrict__ pemin, const uint32_t *__restrict__ pcnt,
+                                                     const uint32_t *__restrict__ ostart,
+                                                     const uint32_t *__restrict__ ovals, double *__restrict__ sums,
+                                                     double *__restrict__ sabs_out, int32_t *__restrict__ emin_out,
+                                                     uint32_t *__restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (cl >= (uint32_t)k) return;  // uniform per wave
+    const uint32_t code = code_of(cl), loc = code_local(cl);
+    double sum = 0, sabs = 0;
+    int emin = 1 << 20;
+    uint32_t cnt = 0;
+    for (uint32_t sl = soff[code]; sl < soff[code + 1]; ++sl) {
+        if (lane < LD) {
+            const uint64_t e = (uint64_t)sl * 16 * LD + loc * LD + fa_slot<LD>(lane);
+            sum += psum[e];
+            sabs += pabs[e];
+            emin = min(emin, pemin[e]);
+        }
+        cnt += pcnt[(uint64_t)sl * 16 + loc];
+    }
+    const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
+    constexpr int U = 8;  // member rows in flight
+    uint32_t j = o0;
+    for (; j + U <= o1; j += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = lane < LD ? aos[(uint64_t)(ovals[j + u] & ~OTHER_TIE) * LD + lane] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            sum += (double)v[u];
+            sabs += (double)__builtin_fabsf(v[u]);
+            if (v[u] != 0.0f) emin = min(emin, ulp_exp(v[u]));
+        }
+    }
+    for (; j < o1; ++j) {
+        const float v = lane < LD ? aos[(uint64_t)(ovals[j] & ~OTHER_TIE) * LD + lane] : 0.0f;
+        sum += (double)v;
+        sabs += (double)__builtin_fabsf(v);
+        if (v != 0.0f) emin = min(emin, ulp_exp(v));
+    }
+    cnt += o1 - o0;
+    if (lane == 0) counts[cl] = cnt;
+    if (lane < d) {
+        const uint64_t o = (uint64_t)lane * k + cl;
+        sums[o] = sum;
+        sabs_out[o] = sabs;
+        emin_out[o] = emin;
+    }
+}
+
 // one workgroup per cluster the certificate fails: its members are the decided points of its
 // tile-half's grouped range that carry its label (fix-up ties included, with their final
 // label) and its pair / ambiguous points among the label-sorted others; sorted into point
@@ -1814,20 +1872,9 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
 }  // namespace
 
 namespace {
-// the update after a fused fix-up: the other points' sums by label, the certified centroids,
-// the sequential sums of the clusters the certificate fails.  Returns false when a flagged
-// cluster has more members than k_nd_seq takes: those are summed over the member sort.
-bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, float *cen,
-                     uint32_t *counts, State *dstate) {
-    KTimer kt(c, "kn.sumnd");
-    const int ld = aos_ld(d);
-    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
-    const uint64_t slices = fz.ncodes + n / FA_SL + 1;
-    auto *soff = wsT<uint32_t>(c, "kn.fasoff", (size_t)fz.ncodes + 1);
-    auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
-    auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
-    auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
-    auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+// the points the fused fix-up did not sum (pairs, ambiguous, its own exact ties), sorted by final
+// label: kn.ovals in label order, kn.ostart their cluster ranges; returns their count
+uint32_t others_sort(st_ctx *c, uint64_t n, int k, const NdFused &fz, const uint32_t *labels) {
     const uint32_t m = fz.npair + fz.namb + fz.nties_fix;
     auto *okeys = wsT<uint32_t>(c, "kn.okeys", (size_t)m + 1);
     auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
@@ -1842,6 +1889,28 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
         radix_sort_u32(c, okeys, ovals, m, 0, bits, "kn.osort");
     }
     bounds_from_sorted(c, okeys, m, k, ostart);
+    return m;
+}
+}  // namespace
+
+namespace {
+// the update after a fused fix-up: the other points' sums by label, the certified centroids,
+// the sequential sums of the clusters the certificate fails.  Returns false when a flagged
+// cluster has more members than k_nd_seq takes: those are summed over the member sort.
+bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, float *cen,
+                     uint32_t *counts, State *dstate) {
+    KTimer kt(c, "kn.sumnd");
+    const int ld = aos_ld(d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
+    const uint64_t slices = fz.ncodes + n / FA_SL + 1;
+    auto *soff = wsT<uint32_t>(c, "kn.fasoff", (size_t)fz.ncodes + 1);
+    auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
+    auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
+    auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
+    auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+    const uint32_t m = others_sort(c, n, k, fz, labels);
+    auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
+    auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
     auto *flagged = wsT<uint32_t>(c, "kn.flagged", (size_t)k);
     auto *nflag = wsT<uint32_t>(c, "kn.nflag", 2);  // [0] flagged clusters, [1] collect overflow
     ST_HIP(hipMemsetAsync(nflag, 0, 8, c->stream));
@@ -1881,6 +1950,33 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
     return true;
 }
 }  // namespace
+
+void nd_fused_partials(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, double *sums,
+                       double *sabs, int32_t *emin, uint32_t *counts) {
+    KTimer kt(c, "kn.partials");
+    const int ld = aos_ld(d);
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
+    const uint64_t slices = fz.ncodes + n / FA_SL + 1;
+    auto *soff = wsT<uint32_t>(c, "kn.fasoff", (size_t)fz.ncodes + 1);
+    auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
+    auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
+    auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
+    auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+    const uint32_t m = others_sort(c, n, k, fz, labels);
+    auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
+    auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
+    const dim3 g((k + 3) / 4);
+    if (ld == 48)
+        hipLaunchKernelGGL(k_nd_partials<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, sums, sabs, emin, counts);
+    else if (ld == 24)
+        hipLaunchKernelGGL(k_nd_partials<24>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, sums, sabs, emin, counts);
+    else
+        hipLaunchKernelGGL(k_nd_partials<12>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
+                           ostart, ovals, sums, sabs, emin, counts);
+    ST_LAUNCH_CHECK();
+}
 
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels,

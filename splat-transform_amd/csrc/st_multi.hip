@@ -487,6 +487,10 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         if (P.n && d == 1 && k <= 256 && !getenv("ST_K1_SORT")) {
             dist_assign_partials1d(c, P.pts[0], P.n, P.nseg, k, cen, labels, sums, sabs, emin, counts);
+        } else if (P.n && d > 1 && P.nseg == 1 && !getenv("ST_ND_SORT")) {
+            // the fused fix-up's partials (ST_ND_SORT=1: the member sort)
+            if (!dist_assign_partials_nd(c, P.pts.data(), d, P.n, k, cen, labels, sums, sabs, emin, counts))
+                dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
         } else if (P.n) {
             dist_assign(c, P.pts.data(), d, P.n, k, cen, labels);
             dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
