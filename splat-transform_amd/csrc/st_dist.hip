@@ -236,11 +236,9 @@ void member_order_nd(st_ctx *c, const uint32_t *labels, uint64_t n, int nseg, in
 }
 }  // namespace
 
-bool dist_assign_partials_nd(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen,
+bool dist_assign_partials_nd(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
                              uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
     ST_REQUIRE(d > 1 && n < (1ull << 31), ST_ERR_ARG, "kmeans partials: N-D shard of fewer than 2^31 points");
-    auto **dcols = wsT<const float *>(c, "ds.cols", (size_t)d);
-    ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
     auto *dstate = static_cast<State *>(ws(c, "ds.state", sizeof(State)));
     ST_HIP(hipMemsetAsync(dstate, 0, sizeof(State), c->stream));
     NdFused fz;
@@ -339,10 +337,10 @@ uint32_t dist_finish(st_ctx *c, int d, int k, const double *sums, const double *
     hipLaunchKernelGGL(k_compact_pairs, dim3(grid_for(total, 256, 4096)), dim3(256), 0, c->stream, flags, pos, total,
                        pending);
     ST_LAUNCH_CHECK();
-    uint32_t np = 0;
-    ST_HIP(hipMemcpyAsync(&np, pos + total, 4, hipMemcpyDeviceToHost, c->stream));
+    auto *np = static_cast<uint32_t *>(pinned_slot(c, "ds.np", 4));
+    ST_HIP(hipMemcpyAsync(np, pos + total, 4, hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
-    return np;
+    return *np;
 }
 
 void dist_average(st_ctx *c, int d, int k, const uint32_t *pairs, uint32_t npairs, const double *running,

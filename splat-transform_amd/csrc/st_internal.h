@@ -299,7 +299,8 @@ void dist_assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, i
 // dist_assign + dist_partials of an N-D shard (one segment) in one pass: the fused fix-up's
 // sums, the member order built only for pending pairs; false (nothing written but the labels):
 // the assign could not fuse, the caller takes dist_partials
-bool dist_assign_partials_nd(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, const float *cen,
+// (dcols: the shard's column pointers, a device array)
+bool dist_assign_partials_nd(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen,
                              uint32_t *labels, double *sums, double *sabs, int32_t *emin, uint32_t *counts);
 void dist_partials(st_ctx *c, const float *const *cols, int d, uint64_t n, int nseg, int k, const uint32_t *labels,
                    double *sums, double *sabs, int32_t *emin, uint32_t *counts);

@@ -482,6 +482,10 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     // the counts come back with dist_finish's readback (one stream sync per iteration)
     auto *hC = static_cast<uint32_t *>(pinned_slot(c, t + ".hC", 4 * (size_t)k));
     const size_t cbytes = 4 * dk;
+    // the shard's column pointers on the device, uploaded once for the N-D iterations
+    auto **dpts = wsT<const float *>(c, t + ".dpts", (size_t)d);
+    if (P.n && d > 1)
+        ST_HIP(hipMemcpyAsync(dpts, P.pts.data(), sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
     for (int it = 0; it < iters; ++it) {
         if (c->verify && d > 1 && it == iters - 1)  // st_ctx_set_verify: the last assign's centroids
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
@@ -489,7 +493,7 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
             dist_assign_partials1d(c, P.pts[0], P.n, P.nseg, k, cen, labels, sums, sabs, emin, counts);
         } else if (P.n && d > 1 && P.nseg == 1 && !getenv("ST_ND_SORT")) {
             // the fused fix-up's partials (ST_ND_SORT=1: the member sort)
-            if (!dist_assign_partials_nd(c, P.pts.data(), d, P.n, k, cen, labels, sums, sabs, emin, counts))
+            if (!dist_assign_partials_nd(c, dpts, d, P.n, k, cen, labels, sums, sabs, emin, counts))
                 dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
         } else if (P.n) {
             dist_assign(c, P.pts.data(), d, P.n, k, cen, labels);
