@@ -6,9 +6,8 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 for v in "$@"; do
   rm -rf $R/gpurun_out/fab_$v
-  ST_LIB=$R/tools/var/$v.so timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/fab_$v -o k -- python3 $R/tools/kn_bench.py --n 10000000 --iters 3 > $R/gpurun_out/fab_$v.log 2>&1 || { echo "$v failed"; tail -5 $R/gpurun_out/fab_$v.log; exit 1; }
+  ST_LIB=$R/tools/var/$v.so timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/fab_$v -o k --output-format csv -- python3 $R/tools/kn_bench.py --n 10000000 --iters 3 > $R/gpurun_out/fab_$v.log 2>&1 || { echo "$v failed"; tail -5 $R/gpurun_out/fab_$v.log; exit 1; }
   f=$(find $R/gpurun_out/fab_$v -name '*kernel_stats.csv' | head -1)
-  echo "== $v"; grep -E "k_fixrow_acc|k_sweep<3, 0>|k_nd_combine|k_nd_seq|k_code_scatter|k_fixpair" $f | awk -F'"' '{print $2}' | head -0
   python3 - "$f" <<'P'
 import csv,sys
 for r in csv.DictReader(open(sys.argv[1])):
