@@ -516,12 +516,30 @@ def textures_digest(tex, meta):
     return h.hexdigest()
 
 
+_PHASE = ['start']
+
+
+def heartbeat(period=30.0):
+    """a progress line on stderr every `period` s: the long quiet phases (the CPU baseline's ~2 min
+    of single-thread KdTree work, the table builds) never look like a hung run"""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f'bench.py: {_PHASE[0]} ({time.time() - t0:.0f} s)', file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main(args):
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import splat_hip as sh
+
+    heartbeat()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -617,11 +635,14 @@ def main(args):
         devs = [None] * world
         dist.all_gather_object(devs, (os.uname().nodename, local))
         devices = len(set(str(d) for d in devs))
+    _PHASE[0] = 'building the tables'
     tabs, total, workload, scaling = rank_tables(args, world, rank, dev)
     step, tex, pal = make_step(tabs, total)
     torch.cuda.synchronize()
+    _PHASE[0] = 'warmup steps'
     for _ in range(args.warmup):
         step()
+    _PHASE[0] = 'timed steps'
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     os.environ.pop('ST_TIMING', None)
@@ -646,6 +667,7 @@ def main(args):
 
     # the last timed step's output checked against the reference's definitions
     verification = None
+    _PHASE[0] = 'stage table and verification'
     if not args.no_verify:
         if not sharded:
             verification = verify_step(ctx, tabs[0], tex, step)
@@ -697,16 +719,20 @@ def main(args):
     flops_per_launch = 2.0 * n_local * pal * D  # nearest-centroid dot products, one assign pass (this rank)
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
     e2e = None
+    _PHASE[0] = 'end-to-end file run'
     if not sharded and not args.no_e2e:
         e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive)
     paths = None
+    _PHASE[0] = 'config-3 stage table'
     if not sharded and not args.no_paths:
         # BASELINE config 3 (-r 0,45,0, filterNaN, Morton, chunk pack -> .compressed.ply) on its own
         # 10M SH-3 table: each HBM-bound stage priced by its algorithmic bytes (tools/bench_paths.py)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import bench_paths
         paths = bench_paths.measure(ctx, stream, dev, n=10_000_000, reps=5)
+    _PHASE[0] = 'CPU baseline (oracle on the host cores)'
     cpu, cpu_all = (None, None) if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+    _PHASE[0] = 'writing the result'
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
     traffic, tsrc = None, None
