@@ -74,6 +74,15 @@ def parse(argv=None):
     ap.add_argument('--dist-python', action='store_true', help='the sharded path through splat_dist.py '
                     '(torch.distributed collectives around the step API) instead of the library')
     ap.add_argument('--launch-dry-run', action='store_true', help=argparse.SUPPRESS)  # print the launcher command
+    ap.add_argument('--launch-budget', type=float, default=1500.0,
+                    help='self-launched N-rank job: seconds before it is killed (then rerun once with the side '
+                         'channel off)')
+    ap.add_argument('--launch-stall', type=float, default=300.0,
+                    help='self-launched N-rank job: seconds without a progress line from any rank before it is '
+                         'killed (600 s before the first one: imports, RCCL set-up)')
+    ap.add_argument('--rank-watchdog', type=float, default=900.0,
+                    help='N > 1: a rank that makes no progress for this many seconds reports its phase and exits '
+                         '(124), so a hung job ends with a diagnosis instead of at the driver\'s limit; 0 = off')
     return ap.parse_args(argv)
 
 
@@ -90,10 +99,66 @@ def free_port():
         return s.getsockname()[1]
 
 
+def run_job(cmd, env, budget, stall, first_stall=600.0):
+    """run the N-rank job, relaying its output; returns (exit code, result line or None, why it was
+    stopped or None).  Ranks write '@@progress' lines to stdout (BENCH_PROGRESS=1); the job is
+    killed (its whole process group) after `budget` seconds, or after `stall` seconds without a
+    progress line (`first_stall` before the first one)."""
+    import queue
+    import signal
+    import subprocess
+    import threading
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
+    q = queue.Queue()
+
+    def reader():
+        for ln in proc.stdout:
+            q.put(ln)
+        q.put(None)
+    threading.Thread(target=reader, daemon=True).start()
+    t0 = time.time()
+    last, seen, line, why = t0, False, None, None
+    while True:
+        try:
+            ln = q.get(timeout=1.0)
+        except queue.Empty:
+            ln = ''
+        now = time.time()
+        if ln is None:
+            break
+        if ln.startswith('@@progress'):
+            last, seen = now, True
+            sys.stderr.write('bench.py: ' + ln[2:])
+        elif ln.startswith('{') and '"metric"' in ln:
+            line = ln.strip()
+        elif ln:
+            sys.stderr.write(ln)
+        if now - t0 > budget:
+            why = f'no result within the {budget:.0f} s budget'
+        elif now - last > (stall if seen else first_stall):
+            why = f'no progress line for {now - last:.0f} s'
+        if why:
+            print(f'bench.py: killing the job: {why}', file=sys.stderr, flush=True)
+            for sig, wait in ((signal.SIGTERM, 15), (signal.SIGKILL, 30)):
+                try:
+                    os.killpg(proc.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    proc.wait(timeout=wait)
+                    break
+                except subprocess.TimeoutExpired:
+                    pass
+            break
+    rc = proc.wait()
+    return rc, line, why
+
+
 def launch(args, argv):
     """parent of a self-launched N-rank job: never imports torch (nothing here touches the GPU);
-    the ranks' stdout is read here, rank 0's JSON line relayed, everything else goes to stderr"""
-    import subprocess
+    the ranks' stdout is read here, rank 0's JSON line relayed, everything else goes to stderr.
+    A job that stalls or fails is rerun once with the side channel off (ST_SIDE_CHANNEL=0: every
+    exchange on the main communicator, in one host thread's program order), and the line says so."""
     cmd = launcher_cmd(argv, args.gpus, free_port())
     if args.launch_dry_run:
         _RESULT.write(json.dumps({'cmd': cmd, 'torch_imported': 'torch' in sys.modules}) + '\n')
@@ -102,27 +167,67 @@ def launch(args, argv):
     env = dict(os.environ)
     env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
     env.setdefault('OMP_NUM_THREADS', '1')
+    env['BENCH_PROGRESS'] = '1'
     print('bench.py: launching ' + ' '.join(cmd), file=sys.stderr, flush=True)
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
-    line = None
-    for ln in proc.stdout:
-        if ln.startswith('{') and '"metric"' in ln:
-            line = ln.strip()
-        else:
-            sys.stderr.write(ln)
-    rc = proc.wait()
+    rc, line, why = run_job(cmd, env, args.launch_budget, args.launch_stall)
+    fallback = None
+    if line is None:
+        first = why or f'exit code {rc}'
+        print(f'bench.py: the {args.gpus}-rank job ended without a result ({first}); rerunning it once with the '
+              'side channel off (ST_SIDE_CHANNEL=0)', file=sys.stderr, flush=True)
+        env['ST_SIDE_CHANNEL'] = '0'
+        cmd = launcher_cmd(argv, args.gpus, free_port())
+        rc, line, why = run_job(cmd, env, args.launch_budget, args.launch_stall)
+        fallback = {'side_channel': 'off', 'first_job': first}
+    if line is None:
+        print(f'bench.py: the {args.gpus}-rank job exited with {rc}' + (f' ({why})' if why else ''), file=sys.stderr)
+        return rc or 3
     if rc != 0:
         print(f'bench.py: the {args.gpus}-rank job exited with {rc}', file=sys.stderr)
         return rc
-    if line is None:
-        print('bench.py: the job printed no result line', file=sys.stderr)
+    res = json.loads(line)
+    if res.get('n_gpus') != args.gpus:
+        print(f'bench.py: the job ran {res.get("n_gpus")} ranks, not {args.gpus}', file=sys.stderr)
         return 3
-    if json.loads(line).get('n_gpus') != args.gpus:
-        print(f'bench.py: the job ran {json.loads(line).get("n_gpus")} ranks, not {args.gpus}', file=sys.stderr)
-        return 3
+    if fallback:
+        res['fallback'] = fallback
+        line = json.dumps(res)
     _RESULT.write(line + '\n')
     _RESULT.flush()
     return 0
+
+
+_LAST_PROGRESS = [0.0]
+
+
+def progress(what):
+    """a progress mark: a '@@progress' line for the self-launching parent's watchdog (only when it
+    asked for them: stdout otherwise carries exactly the one JSON line) and the rank watchdog's
+    clock"""
+    _LAST_PROGRESS[0] = time.time()
+    _PHASE[0] = what
+    if os.environ.get('BENCH_PROGRESS') == '1':
+        _RESULT.write(f'@@progress rank={os.environ.get("RANK", "0")} {what}\n')
+        _RESULT.flush()
+
+
+def rank_watchdog(limit):
+    """N > 1: a rank whose progress marks stop for `limit` seconds (a hung collective) prints its
+    phase and exits with 124; the launcher then ends the other ranks"""
+    import threading
+    if limit <= 0:
+        return
+    _LAST_PROGRESS[0] = time.time()
+
+    def run():
+        while True:
+            time.sleep(5)
+            idle = time.time() - _LAST_PROGRESS[0]
+            if idle > limit:
+                print(f'bench.py: rank {os.environ.get("RANK", "0")} made no progress for {idle:.0f} s in phase '
+                      f'"{_PHASE[0]}"; exiting (124)', file=sys.stderr, flush=True)
+                os._exit(124)
+    threading.Thread(target=run, daemon=True).start()
 
 
 def synth_table(n, seed, device):
@@ -540,6 +645,7 @@ def main(args):
     import splat_hip as sh
 
     heartbeat()
+    progress('started')
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -547,7 +653,10 @@ def main(args):
     local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a gloo rehearsal
     if world > 1 and args.backend == 'nccl' and torch.cuda.device_count() < world:
         raise SystemExit(f'bench.py: {world} RCCL ranks need {world} GPUs, this node has {torch.cuda.device_count()} '
-                         '(rehearse several ranks on one GPU with --dist-python --backend gloo)')
+                         '(rehearse several ranks on one GPU with --backend gloo: the library\'s host shared-memory '
+                         'transport)')
+    if world > 1:
+        rank_watchdog(args.rank_watchdog)
     torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
     if args.splats is None and args.total_splats is None and not args.merge:
         if world == 1:
@@ -574,10 +683,18 @@ def main(args):
     draws = np.random.default_rng(42).random(2 * 65536 * (args.iters + 2))
     comm = None
     if sharded and not args.dist_python:
-        # the library's own RCCL communicator (st_comm_init_rank); torch.distributed hands out the id
-        uid = [sh.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = sh.Comm(ctx, world, rank, uid[0])
+        if args.backend == 'gloo':
+            # several ranks on one GPU: the library's host shared-memory transport (st_comm_init_host),
+            # the same st_dev_sog_sharded calls; torch.distributed hands out the job's name
+            import uuid
+            name = [f'bench-{uuid.uuid4().hex[:16]}' if rank == 0 else None]
+            dist.broadcast_object_list(name, src=0)
+            comm = sh.Comm.host(ctx, world, rank, name[0])
+        else:
+            # the library's own RCCL communicator (st_comm_init_rank); torch.distributed hands out the id
+            uid = [sh.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = sh.Comm(ctx, world, rank, uid[0])
 
     def make_step(tabs, total):
         """the step closure over this rank's tables and rank 0's device outputs"""
@@ -611,14 +728,16 @@ def main(args):
         return step, tex, pal
 
     def timed(step, steps, warmup):
-        for _ in range(warmup):
+        for i in range(warmup):
             step()
+            progress(f'warmup step {i + 1}/{warmup}')
         if sharded:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for i in range(steps):
             meta, used = step()
+            progress(f'timed step {i + 1}/{steps}')
         torch.cuda.synchronize()
         if sharded:
             dist.barrier()
@@ -629,20 +748,26 @@ def main(args):
             el = t.item()
         return el, meta, used
 
-    rccl_ranks = comm.count() if comm else (world if sharded and args.backend == 'nccl' else None)
+    if comm:
+        rccl_ranks = comm.count() if comm.transport == 'rccl' else None
+        transport = comm.transport
+    else:
+        rccl_ranks = world if sharded and args.backend == 'nccl' else None
+        transport = ('torch.distributed ' + args.backend) if sharded else None
     devices = None
     if sharded:
         devs = [None] * world
         dist.all_gather_object(devs, (os.uname().nodename, local))
         devices = len(set(str(d) for d in devs))
-    _PHASE[0] = 'building the tables'
+    progress('building the tables')
     tabs, total, workload, scaling = rank_tables(args, world, rank, dev)
     step, tex, pal = make_step(tabs, total)
     torch.cuda.synchronize()
-    _PHASE[0] = 'warmup steps'
-    for _ in range(args.warmup):
+    progress('warmup steps')
+    for i in range(args.warmup):
         step()
-    _PHASE[0] = 'timed steps'
+        progress(f'warmup step {i + 1}/{args.warmup}')
+    progress('timed steps')
     ctx.set_profiling(True)
     ctx.reset_kernel_stats()
     os.environ.pop('ST_TIMING', None)
@@ -667,7 +792,7 @@ def main(args):
 
     # the last timed step's output checked against the reference's definitions
     verification = None
-    _PHASE[0] = 'stage table and verification'
+    progress('stage table and verification')
     if not args.no_verify:
         if not sharded:
             verification = verify_step(ctx, tabs[0], tex, step)
@@ -719,20 +844,20 @@ def main(args):
     flops_per_launch = 2.0 * n_local * pal * D  # nearest-centroid dot products, one assign pass (this rank)
     achieved = flops_per_launch / avg_sweep_s / 1e12 if sweep_launches else None
     e2e = None
-    _PHASE[0] = 'end-to-end file run'
+    progress('end-to-end file run')
     if not sharded and not args.no_e2e:
         e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive)
     paths = None
-    _PHASE[0] = 'config-3 stage table'
+    progress('config-3 stage table')
     if not sharded and not args.no_paths:
         # BASELINE config 3 (-r 0,45,0, filterNaN, Morton, chunk pack -> .compressed.ply) on its own
         # 10M SH-3 table: each HBM-bound stage priced by its algorithmic bytes (tools/bench_paths.py)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import bench_paths
         paths = bench_paths.measure(ctx, stream, dev, n=10_000_000, reps=5)
-    _PHASE[0] = 'CPU baseline (oracle on the host cores)'
+    progress('CPU baseline (oracle on the host cores)')
     cpu, cpu_all = (None, None) if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
-    _PHASE[0] = 'writing the result'
+    progress('writing the result')
     # HBM bytes per sweep launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
     traffic, tsrc = None, None
@@ -806,6 +931,8 @@ def main(args):
         'kernels': kstats,
         'draws_used_per_step': used,
         'rccl_ranks': rccl_ranks,
+        'transport': transport,
+        'side_channel': (os.environ.get('ST_SIDE_CHANNEL') != '0') if comm else None,
         'distinct_devices': devices if sharded else 1,
         'textures_sha256': tex_sha,
         'weak_10M_per_gpu': weak,

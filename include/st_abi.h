@@ -391,6 +391,15 @@ int st_get_devices(int32_t *ngpu);
 /* one process per GPU: rank 0 creates the id, the launcher distributes it, every rank joins */
 int st_comm_unique_id(uint8_t id[128]);
 int st_comm_init_rank(st_ctx *ctx, int32_t world, int32_t rank, const uint8_t id[128], st_comm **out);
+/* the same job of one-rank processes with the bytes exchanged through host shared memory
+ * instead of RCCL (several ranks on one GPU, which RCCL refuses: the process layout of the
+ * N-GPU job rehearsed on one card).  Every rank passes the same `name` ([A-Za-z0-9_.-], unique
+ * per job; rank 0 creates /dev/shm/st_<name>, which is unlinked once every rank has attached),
+ * slot_bytes (per-rank staging slot, multiple of 4096; 0 = 32 MiB) and timeout_s (longest wait
+ * for a peer before the job is aborted; <= 0 = 600 s).  A peer process that exits, or a rank
+ * that fails, makes every rank's next exchange fail. */
+int st_comm_init_host(st_ctx *ctx, int32_t world, int32_t rank, const char *name, uint64_t slot_bytes,
+                      double timeout_s, st_comm **out);
 void st_comm_destroy(st_comm *comm);
 /* ranks in the communicator (ncclCommCount for RCCL): the bench reports it as `rccl_ranks` */
 int st_comm_count(const st_comm *comm, int32_t *count);

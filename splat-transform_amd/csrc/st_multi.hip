@@ -25,13 +25,18 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <thread>
 
+#include "st_coll.h"
 #include "st_internal.h"
 #include "st_kmeans.h"
 #include "st_webp.h"
@@ -39,30 +44,6 @@
 namespace st {
 
 int palette_of(uint64_t n);
-
-enum class Dt { F64, I32 };
-enum class Op { Sum, Min };
-
-// ---------------------------------------------------------------------------
-// collectives of one rank; every call is stream-ordered on `s` (the rank's context stream)
-struct Coll {
-    int rank = 0, world = 1;
-    virtual ~Coll() = default;
-    virtual void allreduce(void *buf, size_t count, Dt dt, Op op, hipStream_t s) = 0;
-    virtual void broadcast(void *buf, size_t bytes, int root, hipStream_t s) = 0;
-    // recv (every rank) = the ranks' `bytes`-sized sends, rank order
-    virtual void allgather(const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
-    // root: recv[r] (at offset displ[r]) = rank r's send of bytes[r]; recv ignored elsewhere
-    virtual void gatherv(const void *send, size_t mybytes, void *recv, const std::vector<size_t> &bytes,
-                         const std::vector<size_t> &displ, int root, hipStream_t s) = 0;
-    // rank `to` receives rank `from`'s buf (every rank makes the call; the others pass through)
-    virtual void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) = 0;
-    virtual void abort() {}
-    // a second channel over the same ranks, whose calls may run beside this one's (from another
-    // host thread, on another stream): the bulk texel traffic of the writer.  Collective: every
-    // rank asks for it at the same point; made once and kept.
-    virtual Coll *side() = 0;
-};
 
 #define ST_NCCL(expr)                                                                             \
     do {                                                                                          \
@@ -80,6 +61,7 @@ struct RcclColl : Coll {
     std::atomic<bool> dead{false};
     std::mutex side_mu;
     std::unique_ptr<RcclColl> side_;  // ncclCommSplit of comm
+    bool enqueues() const override { return true; }
     ~RcclColl() override {
         side_.reset();
         if (comm && own && !dead.load()) ncclCommDestroy(comm);
@@ -197,6 +179,7 @@ struct HostHub {
 struct HostColl : Coll {
     std::shared_ptr<HostHub> hub;
     std::unique_ptr<HostColl> side_;
+    bool enqueues() const override { return false; }
     Coll *side() override {
         if (!side_) {
             auto sc = std::make_unique<HostColl>();
@@ -643,12 +626,99 @@ LocalTable combine_local(st_ctx *c, Coll &co, const st_table *const *tabs, int n
     return L;
 }
 
+// the events one sharded writeSog orders its streams with
+struct Events {
+    hipEvent_t e[6] = {};
+    Events() {
+        for (auto &x : e) ST_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    }
+    ~Events() {
+        for (auto x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+    hipEvent_t operator[](int i) const { return e[i]; }
+};
+
+// a rank's side worker: one host thread runs the pushed tasks in order.  The first failure
+// aborts both channels (the peers must not wait for this rank) and the remaining tasks are
+// skipped; drain() waits for the tasks and rethrows it.  Destroyed without drain() (this rank's
+// main thread failed), it aborts both channels first, so a task blocked in an exchange returns.
+struct SideWorker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    bool stop = false, drained = false;
+    std::exception_ptr err;
+    Coll *a, *b;
+    std::thread th;
+    // ST_FAULT_SIDE_DELAY_MS=<ms> (fault injection, tests): a random delay before each task, so the
+    // side channel's calls interleave differently with the main thread's
+    int delay_ms = 0;
+    std::minstd_rand rng{12345};
+    SideWorker(int device, Coll *main, Coll *side) : a(main), b(side) {
+        if (const char *d = getenv("ST_FAULT_SIDE_DELAY_MS")) delay_ms = std::max(0, atoi(d));
+        rng.seed(12345u + (unsigned)main->rank * 7919u);
+        th = std::thread([this, device] {
+            bool dev_ok = hipSetDevice(device) == hipSuccess;
+            for (;;) {
+                std::function<void()> f;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || !q.empty(); });
+                    if (q.empty()) return;
+                    f = std::move(q.front());
+                    q.pop_front();
+                }
+                if (err) continue;
+                try {
+                    ST_REQUIRE(dev_ok, ST_ERR_HIP, "side worker: hipSetDevice failed");
+                    if (delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(rng() % (delay_ms + 1)));
+                    f();
+                } catch (...) {
+                    err = std::current_exception();
+                    a->abort();
+                    if (b != a) b->abort();
+                }
+            }
+        });
+    }
+    void push(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(std::move(f));
+        }
+        cv.notify_all();
+    }
+    void drain() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+        drained = true;
+        if (err) std::rethrow_exception(err);
+    }
+    ~SideWorker() {
+        if (!drained) {
+            a->abort();
+            if (b != a) b->abort();
+            std::lock_guard<std::mutex> lk(mu);
+            q.clear();
+            stop = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+    }
+};
+
 }  // namespace
 
 // writeSog's textures + meta (write-sog.ts:110-370) of the global table, on rank 0's device
 // (`out`/`meta` are read on rank 0 only).  Returns the draws consumed.
-uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab, int iters, const double *draws,
-                     uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out, uint64_t *n_global = nullptr) {
+static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab, int iters,
+                                 const double *draws, uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out,
+                                 uint64_t *n_global) {
     use_device(c);
     LocalTable L = combine_local(c, co, tabs, ntab);
     const st_table *t = &L.t;
@@ -677,19 +747,35 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
     static const char *texn[6] = {"means_l", "means_u", "quats", "scales", "sh0", "shN_labels"};
     const int ntex = C ? 6 : 5;
 
-    // The global Morton order and the texel placement on rank 0 leave the critical path: a side
-    // host thread per rank moves x/y/z and the first five textures over the side channel on the
-    // side context's stream, rank 0's orders the table and places those texels, all beside the
-    // k-means on this thread.  Only the shN labels (known after the SH k-means) are gathered
-    // and placed after it.
+    // The global Morton order and the texel placement on rank 0 leave the critical path: x/y/z
+    // and the first five textures move over the side channel (Coll::side) on the side stream, and
+    // rank 0 orders the table and places those texels on its side context from a worker thread,
+    // all beside the k-means on this thread.  Only the shN labels (known after the SH k-means) are
+    // gathered and placed after it.  Who issues the side channel's calls (Coll::enqueues):
+    //   * RCCL: this thread, at fixed points of its program (before the cluster1d k-means and
+    //     before the SH k-means), so every rank enqueues the two communicators' collectives in the
+    //     same order -- blocking collective kernels that share a hardware queue can then never
+    //     wait on each other in opposite orders on two ranks; the worker only runs rank 0's
+    //     Morton order and placement (no collective);
+    //   * host-staged transports (calls return when the bytes have moved): the worker, in order;
+    //     their channels' hubs are independent.
+    // ST_SIDE_CHANNEL=0 (the launcher's fallback) moves all of it onto the main channel, stream
+    // and thread, in the same program order.
     std::vector<size_t> bytes(co.world), displ(co.world);
     for (int r = 0; r < co.world; ++r) {
         bytes[r] = 4 * sh.counts[r];
         displ[r] = 4 * sh.offsets[r];
     }
-    Coll *bk = co.side();
-    if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
-    st_ctx *aux = c->aux;
+    const char *sc = getenv("ST_SIDE_CHANNEL");
+    const bool side_on = !(sc && std::strcmp(sc, "0") == 0);
+    Coll *bk = side_on ? co.side() : &co;
+    const bool inline_coll = !side_on || bk->enqueues();
+    const hipStream_t cs = side_on ? side_stream(c) : c->stream;  // the side channel's stream
+    st_ctx *mc = c;  // rank 0: Morton order and placement
+    if (root && side_on) {
+        if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+        mc = c->aux;
+    }
     float *gx = nullptr, *gy = nullptr, *gz = nullptr;
     uint32_t *pos = nullptr, *gath = nullptr;
     if (root) {
@@ -706,68 +792,34 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
         uint8_t *o[6] = {out->means_l, out->means_u, out->quats, out->scales, out->sh0, out->shn_labels};
         for (int i = 0; i < 6; ++i) dst[i] = o[i];
     }
-    hipEvent_t ev_cols, ev_tex;
-    ST_HIP(hipEventCreateWithFlags(&ev_cols, hipEventDisableTiming));
-    ST_HIP(hipEventCreateWithFlags(&ev_tex, hipEventDisableTiming));
-    ST_HIP(hipEventRecord(ev_cols, c->stream));  // the member columns are in place
-    std::mutex tex_mu;
-    std::condition_variable tex_cv;
-    int tex_state = 0;  // 1: the five textures are written (ev_tex recorded), -1: abandoned
-    std::exception_ptr side_err;
-    std::thread side([&] {
-        try {
-            use_device(aux);
-            ST_HIP(hipStreamWaitEvent(aux->stream, ev_cols, 0));
-            bk->gatherv(m[0], 4 * sh.n, gx, bytes, displ, 0, aux->stream);
-            bk->gatherv(m[1], 4 * sh.n, gy, bytes, displ, 0, aux->stream);
-            bk->gatherv(m[2], 4 * sh.n, gz, bytes, displ, 0, aux->stream);
-            if (root) {
-                auto *idx = wsT<uint32_t>(aux, "mg.idx", N);
-                iota_u32(aux, idx, N);
-                morton_order_dev(aux, gx, gy, gz, idx, N);
-                hipLaunchKernelGGL(k_invert_u32, dim3(grid_for(N, 256, 8192)), dim3(256), 0, aux->stream, idx, N,
-                                   pos);
-                ST_LAUNCH_CHECK();
-            }
-            {
-                std::unique_lock<std::mutex> lk(tex_mu);
-                tex_cv.wait(lk, [&] { return tex_state != 0; });
-                if (tex_state < 0) return;
-            }
-            ST_HIP(hipStreamWaitEvent(aux->stream, ev_tex, 0));
-            for (int i = 0; i < 5; ++i) bk->gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0,
-                                                   aux->stream);
-            if (root) {
-                for (int i = 0; i < 5; ++i) {
-                    ST_HIP(hipMemsetAsync(dst[i], 0, texels * 4, aux->stream));
-                    hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, aux->stream, gath + N * i,
-                                       pos, N, (uint32_t *)dst[i]);
-                    ST_LAUNCH_CHECK();
-                }
-            }
-            ST_HIP(hipStreamSynchronize(aux->stream));
-        } catch (...) {
-            side_err = std::current_exception();
-            co.abort();  // the main channel's peers must not wait for this rank
-        }
+    Events ev;  // cols, xyz, tex, gath, side done, placed
+    ST_HIP(hipEventRecord(ev[0], c->stream));  // the member columns are in place
+    std::unique_ptr<SideWorker> wk;
+    if (side_on) wk = std::make_unique<SideWorker>(c->device, &co, bk);
+    auto on_side = [&](std::function<void()> f) {  // rank 0's ordering work
+        if (wk) wk->push(std::move(f));
+        else f();
+    };
+    auto side_coll = [&](std::function<void()> f) {  // the side channel's collectives
+        if (inline_coll) f();
+        else wk->push(std::move(f));
+    };
+    side_coll([&] {
+        ST_HIP(hipStreamWaitEvent(cs, ev[0], 0));
+        bk->gatherv(m[0], 4 * sh.n, gx, bytes, displ, 0, cs);
+        bk->gatherv(m[1], 4 * sh.n, gy, bytes, displ, 0, cs);
+        bk->gatherv(m[2], 4 * sh.n, gz, bytes, displ, 0, cs);
+        ST_HIP(hipEventRecord(ev[1], cs));
     });
-    struct SideGuard {  // on every exit: release the side thread if it still waits, join it
-        std::thread &th;
-        std::mutex &mu;
-        std::condition_variable &cv;
-        int &state;
-        hipEvent_t a, b;
-        ~SideGuard() {
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                if (state == 0) state = -1;
-            }
-            cv.notify_all();
-            if (th.joinable()) th.join();
-            (void)hipEventDestroy(a);
-            (void)hipEventDestroy(b);
-        }
-    } side_guard{side, tex_mu, tex_cv, tex_state, ev_cols, ev_tex};
+    if (root)
+        on_side([&] {
+            ST_HIP(hipStreamWaitEvent(mc->stream, ev[1], 0));
+            auto *idx = wsT<uint32_t>(mc, "mg.idx", N);
+            iota_u32(mc, idx, N);
+            morton_order_dev(mc, gx, gy, gz, idx, N);
+            hipLaunchKernelGGL(k_invert_u32, dim3(grid_for(N, 256, 8192)), dim3(256), 0, mc->stream, idx, N, pos);
+            ST_LAUNCH_CHECK();
+        });
 
     // global NaN-ignoring extents of x, y, z (write-sog.ts:161-187)
     double lo[3], hi[3];
@@ -806,12 +858,23 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
             meta->means_max[a] = lm.means_max[a];
         }
     }
-    ST_HIP(hipEventRecord(ev_tex, c->stream));
-    {
-        std::lock_guard<std::mutex> lk(tex_mu);
-        tex_state = 1;
-    }
-    tex_cv.notify_all();
+    ST_HIP(hipEventRecord(ev[2], c->stream));
+    side_coll([&] {
+        ST_HIP(hipStreamWaitEvent(cs, ev[2], 0));
+        for (int i = 0; i < 5; ++i) bk->gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0, cs);
+        ST_HIP(hipEventRecord(ev[3], cs));
+    });
+    if (root)
+        on_side([&] {
+            ST_HIP(hipStreamWaitEvent(mc->stream, ev[3], 0));
+            for (int i = 0; i < 5; ++i) {
+                ST_HIP(hipMemsetAsync(dst[i], 0, texels * 4, mc->stream));
+                hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, mc->stream, gath + N * i, pos,
+                                   N, (uint32_t *)dst[i]);
+                ST_LAUNCH_CHECK();
+            }
+            ST_HIP(hipEventRecord(ev[5], mc->stream));
+        });
 
     if (root) meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
     uint32_t *gath5 = nullptr;
@@ -841,9 +904,13 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
             shn_centroids_dev(c, cl, C, pal, out->shn_centroids);
         }
     }
-    side.join();
-    if (side_err) std::rethrow_exception(side_err);
-    if (root && C) {  // pos is in place (the side thread synchronised its stream)
+    if (wk) wk->drain();  // every side task has been issued (and, host-staged, has completed)
+    if (side_on) {  // this stream continues after the side stream's gathers and rank 0's placement
+        ST_HIP(hipEventRecord(ev[4], cs));
+        ST_HIP(hipStreamWaitEvent(c->stream, ev[4], 0));
+        if (root) ST_HIP(hipStreamWaitEvent(c->stream, ev[5], 0));
+    }
+    if (root && C) {  // pos is in place: on c->stream or behind ev[5]
         ST_HIP(hipMemsetAsync(dst[5], 0, texels * 4, c->stream));
         hipLaunchKernelGGL(k_place, dim3(grid_for(N, 256, 8192)), dim3(256), 0, c->stream, gath5, pos, N,
                            (uint32_t *)dst[5]);
@@ -851,6 +918,18 @@ uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab,
     }
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;
+}
+
+// a failure on this rank aborts the job's channels: the peers' collectives fail instead of
+// waiting for this rank (the communicator is not usable afterwards)
+uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab, int iters, const double *draws,
+                     uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out, uint64_t *n_global = nullptr) {
+    try {
+        return sog_sharded_rank(c, co, tabs, ntab, iters, draws, ndraws, meta, out, n_global);
+    } catch (...) {
+        co.abort();
+        throw;
+    }
 }
 
 }  // namespace st
@@ -1117,6 +1196,22 @@ int st_comm_init_rank(st_ctx *c, int32_t world, int32_t rank, const uint8_t id[1
         rc->world = world;
         auto *cm = new st_comm();
         cm->coll = std::move(rc);
+        *out = cm;
+    });
+}
+
+int st_comm_init_host(st_ctx *c, int32_t world, int32_t rank, const char *name, uint64_t slot_bytes,
+                      double timeout_s, st_comm **out) {
+    return guarded_m([&] {
+        ST_REQUIRE(c && name && out && world >= 1 && rank >= 0 && rank < world, ST_ERR_ARG, "bad argument");
+        use_device(c);
+        auto *cm = new st_comm();
+        try {
+            cm->coll = make_shm_coll(world, rank, name, slot_bytes ? (size_t)slot_bytes : (size_t)32 << 20, timeout_s);
+        } catch (...) {
+            delete cm;
+            throw;
+        }
         *out = cm;
     });
 }

@@ -452,7 +452,20 @@ void st_ctx_destroy(st_ctx *c) {
 int st_ctx_set_stream(st_ctx *c, void *s) {
     return guarded([&] {
         ST_ARG(c, "ctx is NULL");
-        c->stream = s ? (hipStream_t)s : c->own_stream;
+        use_device(c);
+        if (s) {
+            // the caller's stream replaces the context's own: release it (one hardware queue fewer;
+            // GPU_MAX_HW_QUEUES bounds them per process)
+            if (c->own_stream) {
+                ST_HIP(hipStreamSynchronize(c->own_stream));
+                ST_HIP(hipStreamDestroy(c->own_stream));
+                c->own_stream = nullptr;
+            }
+            c->stream = (hipStream_t)s;
+        } else {
+            if (!c->own_stream) ST_HIP(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+            c->stream = c->own_stream;
+        }
     });
 }
 

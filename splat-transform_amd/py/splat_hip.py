@@ -101,7 +101,8 @@ EXPORTS = [
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
-    'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_destroy', 'st_comm_count',
+    'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_init_host', 'st_comm_destroy',
+    'st_comm_count',
     'st_dev_sog_sharded', 'st_group_create', 'st_group_destroy', 'st_group_sog', 'st_group_sog_bundle',
     'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
@@ -338,16 +339,31 @@ class Group:
 
 
 class Comm:
-    """st_comm: this process's rank of a one-process-per-GPU RCCL job"""
+    """st_comm: this process's rank of a one-rank-per-process job: over RCCL (one GPU per rank,
+    `uid` from comm_unique_id on rank 0) or, with Comm.host, over host shared memory (any number
+    of ranks on one GPU)"""
 
-    def __init__(self, ctx, world, rank, uid):
+    def __init__(self, ctx, world, rank, uid=None, _host=None):
         self.h = ctypes.c_void_p()
+        self.world, self.rank = world, rank
+        if _host is not None:
+            name, slot_bytes, timeout_s = _host
+            check(lib().st_comm_init_host(ctx.h, ctypes.c_int32(world), ctypes.c_int32(rank), name.encode(),
+                                          ctypes.c_uint64(slot_bytes), ctypes.c_double(timeout_s),
+                                          ctypes.byref(self.h)))
+            self.transport = 'host-shm'
+            return
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().st_comm_init_rank(ctx.h, ctypes.c_int32(world), ctypes.c_int32(rank), buf, ctypes.byref(self.h)))
-        self.world, self.rank = world, rank
+        self.transport = 'rccl'
+
+    @classmethod
+    def host(cls, ctx, world, rank, name, slot_bytes=0, timeout_s=600.0):
+        """st_comm_init_host: every rank passes the same job `name` (unique per job)"""
+        return cls(ctx, world, rank, _host=(name, slot_bytes, timeout_s))
 
     def count(self):
-        """ranks in the communicator (ncclCommCount)"""
+        """ranks in the communicator (ncclCommCount for RCCL)"""
         n = ctypes.c_int32()
         check(lib().st_comm_count(self.h, ctypes.byref(n)))
         return n.value

@@ -5,8 +5,9 @@ torch.distributed.run) without importing torch in the parent, relays rank 0's JS
 unless the job reports N ranks; the synthetic tables are fixed-seed blocks sliced by global row
 range, so a T-splat table does not depend on how many ranks split it.
 
-GPU: the self-launched 2-rank rehearsal on one GPU (gloo, the torch-harness sharded path)
-prints n_gpus 2 and the same textures_sha256 as one GPU over the same table."""
+GPU: the self-launched 2-rank rehearsal on one GPU (--backend gloo: the library's own sharded
+path, st_dev_sog_sharded in two processes over its host shared-memory transport) prints n_gpus 2
+and the same textures_sha256 as one GPU over the same table."""
 import json
 import os
 import subprocess
@@ -58,6 +59,44 @@ def test_launch_relays_rank0_line_and_checks_world(tmp_path, reported, rc, want_
         assert 'rank chatter' in r.stderr
 
 
+def _launch(tmp_path, script_text, extra=()):
+    script = tmp_path / 'job.py'
+    script.write_text(script_text)
+    code = ('import sys, io, json; sys.path.insert(0, %r); import bench; '
+            'bench.launcher_cmd = lambda argv, n, port: %r; '
+            'bench._RESULT = sys.stdout; sys.stdout = sys.stderr; '
+            'a = bench.parse(["--gpus", "2"] + %r); rc = bench.launch(a, ["--gpus", "2"]); '
+            'assert "torch" not in sys.modules; sys.exit(rc)') % (ROOT, [sys.executable, str(script)], list(extra))
+    return subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+
+
+def test_launch_kills_a_stalled_job_and_reruns_without_side_channel(tmp_path):
+    """a job whose progress lines stop is killed (its process group) after --launch-stall seconds
+    and rerun once with ST_SIDE_CHANNEL=0; the relayed line says so"""
+    r = _launch(tmp_path, 'import json, os, sys, time\n'
+                          'print("@@progress rank=0 started", flush=True)\n'
+                          'if os.environ.get("ST_SIDE_CHANNEL") != "0":\n'
+                          '    time.sleep(60)\n'
+                          'print(json.dumps({"metric": "m", "value": 1.0, "n_gpus": 2}))\n',
+                ['--launch-stall', '2'])
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out['fallback']['side_channel'] == 'off' and 'no progress' in out['fallback']['first_job']
+    assert 'killing the job' in r.stderr
+
+
+def test_launch_budget_and_a_failing_fallback(tmp_path):
+    """a job that keeps reporting progress but never finishes hits --launch-budget; when the rerun
+    fails too the parent exits non-zero"""
+    r = _launch(tmp_path, 'import time\n'
+                          'for i in range(100):\n'
+                          '    print("@@progress rank=0 step", i, flush=True)\n'
+                          '    time.sleep(0.5)\n',
+                ['--launch-budget', '3', '--launch-stall', '30'])
+    assert r.returncode != 0
+    assert r.stderr.count('killing the job') == 2 and 'budget' in r.stderr
+
+
 def test_table_rows_independent_of_the_split():
     """rows [lo, hi) of a T-row table built from fixed-seed blocks: any split concatenates to the
     same table (small blocks here; the bench uses 10M-row blocks)"""
@@ -78,14 +117,17 @@ def test_table_rows_independent_of_the_split():
 
 @pytest.mark.gpu
 def test_self_launched_two_ranks_match_one_gpu(tmp_path):
-    """`bench.py --gpus 2` (no torchrun on the command line) rehearsed on one GPU over gloo: two
-    ranks, and the textures of the 4M-splat table equal one GPU's"""
+    """`bench.py --gpus 2 --backend gloo` (no torchrun on the command line) rehearsed on one GPU:
+    two processes running the library's st_dev_sog_sharded over its host shared-memory transport,
+    and the textures of the 4M-splat table equal one GPU's"""
     common = ['--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-e2e', '--no-paths', '--no-verify']
     env = dict(os.environ, PYTHONUNBUFFERED='1')
-    r2 = subprocess.run([sys.executable, BENCH, '--gpus', '2', '--dist-python', '--backend', 'gloo',
+    r2 = subprocess.run([sys.executable, BENCH, '--gpus', '2', '--backend', 'gloo', '--no-weak',
                          '--splats', '2000000'] + common, capture_output=True, text=True, timeout=600, env=env)
     assert r2.returncode == 0, r2.stderr[-4000:]
     two = json.loads(r2.stdout.strip().splitlines()[-1])
+    assert two['config']['parallelism'] == 'rowshard2-native' and two['transport'] == 'host-shm'
+    assert 'fallback' not in two
     r1 = subprocess.run([sys.executable, BENCH, '--gpus', '1', '--splats', '4000000'] + common,
                         capture_output=True, text=True, timeout=600, env=env)
     assert r1.returncode == 0, r1.stderr[-4000:]

@@ -1,0 +1,134 @@
+"""The one-rank-per-process sharded writeSog (st_comm_init_host + st_dev_sog_sharded: the calls
+bench.py --gpus N makes on an N-GPU node, with host shared memory instead of RCCL carrying the
+bytes) run as 2 and 3 separate processes on cuda:0, against the single-device st_dev_sog of the
+whole table, bit for bit (write-sog.ts:110-370).
+
+Each rank is its own process (tests/mp_sog_rank.py, started before it touches the GPU), so the
+main channel's all-reduces, the side channel's texel gathers from the rank's worker thread, rank
+0's global Morton order and the sequential hand-off of uncertified cluster sums
+(tests/mp_table.py builds columns that need it) all run across process boundaries, as they do
+on the 8-GPU node."""
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
+sys.path.insert(0, HERE)
+
+import mp_sog_rank  # noqa: E402
+import mp_table  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N = 1_000_000
+SEED = 11
+
+
+@pytest.fixture(scope='module')
+def ref():
+    """the single-device writeSog of the whole table: digest -> draws consumed"""
+    import torch
+
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    out = {}
+    ctx = sh.Context(0)
+
+    def run(n, iters=10):
+        key = (n, iters)
+        if key not in out:
+            full = mp_table.table(n, SEED)
+            cols = {k: torch.from_numpy(v).to(dev) for k, v in full.items()}
+            W, H, pal, cw, ch = sh.sog_geometry(n, 15)
+            u8 = dict(device=dev, dtype=torch.uint8)
+            tex = {k: torch.empty(W * H * 4, **u8) for k in mp_sog_rank.TEX[:6]}
+            tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
+            meta, used = ctx.dev_sog(cols, iters, mp_table.draws(SEED), tex)
+            torch.cuda.synchronize()
+            out[key] = (mp_sog_rank.digest(tex, meta), used)
+        return out[key]
+    yield run
+    ctx.close()
+
+
+def run_job(tmp_path, cuts, n=N, iters=10, slot=0, env=None, repeat=1, timeout=420):
+    """start one process per rank (each before it touches the GPU), wait for all of them; returns
+    (exit codes, per-rank results, stderr tails)"""
+    world = len(cuts) - 1
+    name = 'pytest-' + uuid.uuid4().hex[:12]
+    e = dict(os.environ)
+    e.update(env or {})
+    procs = []
+    for r in range(world):
+        cmd = [sys.executable, os.path.join(HERE, 'mp_sog_rank.py'), '--world', str(world), '--rank', str(r),
+               '--name', name, '--n', str(n), '--cuts', ','.join(map(str, cuts)), '--seed', str(SEED),
+               '--iters', str(iters), '--slot', str(slot), '--out', str(tmp_path), '--repeat', str(repeat)]
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    codes, errs = [], []
+    try:
+        for p in procs:
+            _, err = p.communicate(timeout=timeout)
+            codes.append(p.returncode)
+            errs.append(err[-3000:])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    res = []
+    for r in range(world):
+        f = tmp_path / f'rank{r}.json'
+        res.append(json.load(open(f)) if f.exists() else None)
+    assert not os.path.exists(f'/dev/shm/st_{name}'), 'the job left its segment in /dev/shm'
+    return codes, res, errs
+
+
+def check(codes, res, errs, want):
+    assert codes == [0] * len(codes), '\n'.join(errs)
+    digest, used = want
+    for r in res:
+        assert r is not None
+        assert all(u == used for u in r['used']), (r['used'], used)
+    assert all(d == digest for d in res[0]['sha256'])
+
+
+@pytest.mark.parametrize('cuts', [[0, N * 3 // 7, N], [0, N // 5, N * 3 // 5, N]], ids=['2ranks', '3ranks'])
+def test_processes_match_single_device(tmp_path, ref, cuts):
+    """uneven shards, 10 iterations, SH-3, 1M splats; two calls on the same communicators"""
+    check(*run_job(tmp_path, cuts, repeat=2), ref(N))
+
+
+def test_small_slots_and_side_delays(tmp_path, ref):
+    """1 MiB staging slots (every exchange moves in several rounds) and random delays before each
+    of the side worker's tasks: the channels' interleaving changes, the output does not"""
+    check(*run_job(tmp_path, [0, N // 3, N * 2 // 3, N], slot=1 << 20, env={'ST_FAULT_SIDE_DELAY_MS': '40'}),
+          ref(N))
+
+
+def test_side_channel_off(tmp_path, ref):
+    """ST_SIDE_CHANNEL=0 (the launcher's fallback): every exchange on the main channel and thread"""
+    check(*run_job(tmp_path, [0, N // 2, N], env={'ST_SIDE_CHANNEL': '0'}), ref(N))
+
+
+def test_empty_shard(tmp_path, ref):
+    """a rank without rows"""
+    n = 200_000
+    check(*run_job(tmp_path, [0, n // 2, n // 2, n], n=n, iters=3), ref(n, 3))
+
+
+def test_failing_rank_ends_the_job(tmp_path):
+    """a rank that fails after the first exchange aborts the job: every rank exits with an error
+    (nothing waits forever), and the peers report the abort"""
+    n = 50_000
+    codes, res, errs = run_job(tmp_path, [0, n // 3, n], n=n, iters=2, env={'ST_FAULT_RANK': '1'}, timeout=240)
+    assert all(c != 0 for c in codes), codes
+    assert 'ST_FAULT_RANK: injected failure' in errs[1]
+    assert 'another rank failed' in errs[0] or 'exited' in errs[0], errs[0]
+    assert res == [None, None]
+
