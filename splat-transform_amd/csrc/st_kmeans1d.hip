@@ -854,12 +854,10 @@ __global__ __launch_bounds__(64) void k_rp_finish(const uint32_t *__restrict__ s
 
 // candidates one replay takes (CAND_MAX); ST_REPLAY_CAP lowers it so that tests can drive
 // the sequential chain with small inputs
+// (read per call: a test sets it around one call)
 uint32_t replay_cap() {
-    static const uint32_t cap = [] {
-        const char *e = getenv("ST_REPLAY_CAP");
-        return e ? std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 10), (uint32_t)CAND_MAX) : (uint32_t)CAND_MAX;
-    }();
-    return cap;
+    const char *e = getenv("ST_REPLAY_CAP");
+    return e ? std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 10), (uint32_t)CAND_MAX) : (uint32_t)CAND_MAX;
 }
 
 // stages A-F of the chunked replay for the clusters flagged 1 (left 0 when replayed, 2 when
@@ -2289,6 +2287,10 @@ void seg_label_sort1d(st_ctx *c, const float *pts, const uint32_t *labels, uint6
     }
 }
 
+__global__ __launch_bounds__(256) void k_part_neutral(Part1 *part) {
+    part[(uint64_t)blockIdx.x * 256 + threadIdx.x] = Part1{0.0, 0.0, 1 << 20, 0u};
+}
+
 void assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k, const float *cen, uint32_t *labels,
                        double *sums, double *sabs, int32_t *emin, uint32_t *counts) {
     ST_REQUIRE(k >= 1 && k <= 256 && nseg >= 1 && n % (uint64_t)nseg == 0, ST_ERR_ARG,
@@ -2303,8 +2305,8 @@ void assign_partials1d(st_ctx *c, const float *pts, uint64_t n, int nseg, int k,
             hipLaunchKernelGGL(k_kd1_assign_acc<false>, dim3(G), dim3(F1_T), 0, c->stream, pts + o, ns, cen, k,
                                labels + o, (uint8_t *)nullptr, ntiles, part + (uint64_t)sg * G * 256,
                                (const uint32_t *)nullptr, (Bnd1 *)nullptr);
-        else
-            ST_HIP(hipMemsetAsync(part + (uint64_t)sg * G * 256, 0, sizeof(Part1) * 256 * G, c->stream));
+        else  // an empty segment: neutral partials (no members, e_min above any real exponent)
+            hipLaunchKernelGGL(k_part_neutral, dim3(G), dim3(256), 0, c->stream, part + (uint64_t)sg * G * 256);
     }
     hipLaunchKernelGGL(k_part_fold, dim3((unsigned)nseg * k), dim3(256), 0, c->stream, part, G, k, sums, sabs, emin,
                        counts);

@@ -58,6 +58,8 @@ constexpr int NW = 4;          // waves per workgroup (they share the LDS centro
 constexpr int WG = 64 * NW;    // threads per workgroup
 constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
+constexpr int CAND_CAP2 = 2048;  // ... per point whose list overflowed (a second collect)
+constexpr int OVF_BATCH = 32768;  // overflowed points per second collect (256 MiB of lists)
 // members above which a cluster's sum is split over many workgroups (k_big_*); ST_SUMND_BIG
 // lowers it so that tests drive that path with small inputs
 uint32_t sumnd_big() {
@@ -101,11 +103,69 @@ __device__ inline float err_bound(const Bound &B, float pn, float dp, float cn, 
     return B.r * (pn * dc + dp * ct) + B.a * pt * ct + B.b * ct * ct + B.ec * (pt + ct) + B.ep;
 }
 
-// the decision window: the best row's error bounded by its own tile-half's largest norm cb and
-// residual dcb, the rows that can beat it by the palette's cm / dcm
-__device__ inline float wbound2(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float dcm) {
-    const float s = pn + cm;
-    return (err_bound(B, pn, dp, cb, dcb) + err_bound(B, pn, dp, cm, dcm) + 2.0f * B.rel * s * s) * 1.0001f;
+// Norm table: tab[b] = the largest rounding-residual norm among the rows whose norm falls in
+// buckets 0..b of [0, cm] (prefix maxima; bucket(x) = min(NB - 1, floor(x NB / cm)), monotone in x)
+constexpr int NTAB = 1024;
+__device__ inline uint32_t norm_bucket(float x, float scale) {
+    return (uint32_t)fminf(x * scale, (float)(NTAB - 1));
+}
+__global__ __launch_bounds__(NTAB) void k_norm_table(const float *__restrict__ cnorm, const float *__restrict__ cdn,
+                                                     uint32_t rows, const uint32_t *__restrict__ cmax_bits,
+                                                     float *__restrict__ tab) {
+    __shared__ uint32_t m[NTAB];
+    const uint32_t t = threadIdx.x;
+    m[t] = 0u;
+    __syncthreads();
+    const float cm = __builtin_bit_cast(float, cmax_bits[0]);
+    const float scale = cm > 0.f ? (float)NTAB / cm : 0.f;
+    for (uint32_t r = t; r < rows; r += NTAB) {
+        // non-negative floats: bit order; the read skips the atomics that cannot raise the slot
+        // (the norms crowd into few buckets)
+        const uint32_t b = norm_bucket(cnorm[r], scale), v = __builtin_bit_cast(uint32_t, cdn[r]);
+        if (v > __hip_atomic_load(&m[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) atomicMax(&m[b], v);
+    }
+    __syncthreads();
+    for (uint32_t o = 1; o < (uint32_t)NTAB; o <<= 1) {
+        const uint32_t v = t >= o ? m[t - o] : 0u;
+        __syncthreads();
+        m[t] = max(m[t], v);
+        __syncthreads();
+    }
+    tab[t] = __builtin_bit_cast(float, m[t]);
+}
+
+// The largest norm a row c can have when its score |c|^2 - 2 p.c is at most t: the score is at
+// least |c|^2 - 2 pn |c| (pn >= |p|), so |c| <= pn + sqrt(pn^2 + t).  Rounded up past the f32
+// arithmetic (q's rounding covered by the 2^-19 term, sqrt and the sum by the factor) and the
+// 1e-6 the stored norms carry.
+__device__ inline float norm_reach(float pn, float t) {
+    const float q = pn * pn + t;
+    const float qe = q + 0x1p-19f * (pn * pn + __builtin_fabsf(t));
+    return (pn + __builtin_sqrtf(fmaxf(0.f, qe))) * (1.0f + 0x1p-18f);
+}
+
+// The decision window with the errors bounded by the norms that can matter (kd-tree.ts:22-70
+// finds the exact f64 argmin; a row matters only if it might beat the best):
+//   * the best row c1 of the best tile-half scores at most m1u + E(cb, dcb) (cb, dcb: the
+//     half's largest norm and residual), so |c1| <= R1 = norm_reach(m1u + E(cb)); its own error
+//     takes min(R1, cb) and the largest residual among rows of norm <= R1 (the norm table) --
+//     an outlying row in the same tile-half no longer widens it;
+//   * a competitor c can reach the best's score (m1u + that error, plus both rows' f64
+//     roundings: t) only if |c| <= R = norm_reach(t); its error takes min(R, cm) and the norm
+//     table's residual at R instead of the palette's cm / dcm -- one outlying centroid no longer
+//     widens every point's window.
+// With R1 >= cb and R >= cm this is the palette-wide window of round 3.
+__device__ inline float wbound_r(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float ntab_scale,
+                                 const float *__restrict__ ntab, float m1u) {
+    const float e0 = err_bound(B, pn, dp, cb, dcb);
+    const float c1 = fminf(norm_reach(pn, m1u + e0 * 1.0001f), cb);
+    const float eb = err_bound(B, pn, dp, c1, fminf(dcb, ntab[norm_bucket(c1, ntab_scale)]));
+    const float sb = pn + c1, sm = pn + cm;
+    const float t = m1u + eb * 1.0001f + B.rel * (sb * sb + sm * sm);
+    const float cr = fminf(norm_reach(pn, t), cm);
+    const float dcr = ntab[norm_bucket(cr, ntab_scale)];
+    const float sr = pn + cr;
+    return (eb + err_bound(B, pn, dp, cr, dcr) + B.rel * (sb * sb + sr * sr)) * 1.0001f;
 }
 
 // the window between two given tile-halves (largest norms ca, cb and residuals dca, dcb)
@@ -326,10 +386,11 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
                                                const float *__restrict__ pnorm, const float *__restrict__ pdn,
                                                const uint32_t *__restrict__ cmax_bits, const float *__restrict__ chalf,
-                                               const float *__restrict__ chalf_d,
+                                               const float *__restrict__ chalf_d, const float *__restrict__ ntab,
                                                const Bound bnd, uint32_t *__restrict__ labels,
                                                float *__restrict__ thr, uint32_t *__restrict__ amb, State *st,
                                                uint32_t *__restrict__ cand_cnt, uint32_t *__restrict__ cand,
+                                               uint32_t cand_cap,
                                                uint32_t *__restrict__ pair_pts, uint2 *__restrict__ pair_codes,
                                                uint32_t *__restrict__ code_hist) {
     constexpr int STAGE_U4 = CT_STAGE * KS * 64;  // uint4 per stage
@@ -405,7 +466,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                     if (sc[r] <= th[t] && !full[t]) {
                         const uint32_t ci = ctile * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
                         const uint32_t pos = atomicAdd(&cand_cnt[slot], 1u);
-                        if (pos < CAND_CAP) cand[(uint64_t)slot * CAND_CAP + pos] = ci;
+                        if (pos < cand_cap) cand[(uint64_t)slot * cand_cap + pos] = ci;
                         else full[t] = true;
                     }
                 }
@@ -491,7 +552,8 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
     });
     if (MODE == 1) return;
 
-    const float cm = __builtin_bit_cast(float, cmax_bits[0]), dcm = __builtin_bit_cast(float, cmax_bits[1]);
+    const float cm = __builtin_bit_cast(float, cmax_bits[0]);
+    const float ntab_scale = cm > 0.f ? (float)NTAB / cm : 0.f;
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         // merge the two lane-halves' top-3 (sorted) into the point's top-3; codes =
@@ -514,7 +576,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float pn = pnorm[p], dp = pdn[p];
-            const float W = wbound2(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, dcm);
+            const float W = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
                 if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
@@ -910,6 +972,7 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
 // exact ties) are summed by k_nd_combine from a short label sort; clusters failing the
 // certificate take the sequential sum over their members in point order (k_nd_seq).
 constexpr uint32_t FA_SL = 8192;  // decided points per slice (one workgroup)
+constexpr int FA_B = 4;           // point rows per prefetch batch of a 16-lane group
 // accumulator slot of dimension j inside a cluster's LD slots: lane q adds dimensions 4q..4q+3,
 // stored q-consecutive so that one atomic instruction's lanes hit consecutive doubles
 template <int LD>
@@ -1020,44 +1083,63 @@ __global__ __launch_bounds__(256) void k_fixrow_acc(const float *__restrict__ ao
         for (int q = 0; q < LD / 4; ++q) row[q] = src[q];
     }
     const int sq = rr % (LD / 4);
+    // the point rows move in batches of FA_B: the next batch's rows are in flight while this
+    // batch is scored and summed (one row in flight per group left the kernel bound by the
+    // gather latency: ~2 TB/s of random 192-B rows)
     for (uint32_t j0 = b0 + grp * FB_RUN; j0 < b1; j0 += 16 * FB_RUN) {  // uniform per 16-lane group
         const int cnt = (int)min(b1 - j0, (uint32_t)FB_RUN);
         const uint32_t pa = rr < cnt ? grouped[j0 + rr].x : 0u;
         const uint32_t pb = 16 + rr < cnt ? grouped[j0 + 16 + rr].x : 0u;
         auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
-        uint32_t p = point_of(0);
-        float4 cur = reinterpret_cast<const float4 *>(aos + (uint64_t)p * LD)[sq];
-        for (int i = 0; i < cnt; ++i) {
-            const uint32_t pn = point_of(i + 1 < cnt ? i + 1 : i);
-            float4 nxt;
-            {
-                const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn * LD) + sq;
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt) : "v"(src) : "memory");
-            }
-            f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
-            static_for<LD / 4>([&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                const f32x2 t01 = {row_bcast<q>(cur.x) - row[q].x, row_bcast<q>(cur.y) - row[q].y};
-                const f32x2 t23 = {row_bcast<q>(cur.z) - row[q].z, row_bcast<q>(cur.w) - row[q].w};
-                a01 = __builtin_elementwise_fma(t01, t01, a01);
-                a23 = __builtin_elementwise_fma(t23, t23, a23);
-            });
-            const FixOut fo = fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos,
-                                             aos + (uint64_t)p * LD, p, rr, labels, ties, st);
-            if (!fo.tie && rr < LD / 4) {  // lane rr adds dimensions 4 rr .. 4 rr + 3 (padding adds 0)
-                const uint32_t base = code_local(fo.label) * LD + rr;
-                const float v[4] = {cur.x, cur.y, cur.z, cur.w};
+        float4 cur[FA_B], nxt[FA_B];
+        uint32_t pc[FA_B];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    atomicAdd(&S[base + u * (LD / 4)], (double)v[u]);
-                    atomicAdd(&A[base + u * (LD / 4)], (double)__builtin_fabsf(v[u]));
-                    if (v[u] != 0.0f) atomicMin(&E[base + u * (LD / 4)], ulp_exp(v[u]));
+        for (int u = 0; u < FA_B; ++u) {
+            pc[u] = point_of(u < cnt ? u : cnt - 1);
+            cur[u] = reinterpret_cast<const float4 *>(aos + (uint64_t)pc[u] * LD)[sq];
+        }
+        for (int i0 = 0; i0 < cnt; i0 += FA_B) {
+            uint32_t pn[FA_B];
+#pragma unroll
+            for (int u = 0; u < FA_B; ++u) {
+                const int i = i0 + FA_B + u;
+                pn[u] = point_of(i < cnt ? i : cnt - 1);
+                // by hand, so the compiler cannot sink the loads below the scoring; the wait at
+                // the end of the batch covers them
+                const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn[u] * LD) + sq;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt[u]) : "v"(src) : "memory");
+            }
+#pragma unroll
+            for (int u = 0; u < FA_B; ++u) {
+                if (i0 + u >= cnt) break;  // uniform per group
+                f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+                static_for<LD / 4>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const f32x2 t01 = {row_bcast<q>(cur[u].x) - row[q].x, row_bcast<q>(cur[u].y) - row[q].y};
+                    const f32x2 t23 = {row_bcast<q>(cur[u].z) - row[q].z, row_bcast<q>(cur[u].w) - row[q].w};
+                    a01 = __builtin_elementwise_fma(t01, t01, a01);
+                    a23 = __builtin_elementwise_fma(t23, t23, a23);
+                });
+                const FixOut fo = fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos,
+                                                 aos + (uint64_t)pc[u] * LD, pc[u], rr, labels, ties, st);
+                if (!fo.tie && rr < LD / 4) {  // lane rr adds dimensions 4 rr .. 4 rr + 3 (padding adds 0)
+                    const uint32_t base = code_local(fo.label) * LD + rr;
+                    const float v[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        atomicAdd(&S[base + w * (LD / 4)], (double)v[w]);
+                        atomicAdd(&A[base + w * (LD / 4)], (double)__builtin_fabsf(v[w]));
+                        if (v[w] != 0.0f) atomicMin(&E[base + w * (LD / 4)], ulp_exp(v[w]));
+                    }
+                    if (rr == 0) atomicAdd(&C[code_local(fo.label)], 1u);
                 }
-                if (rr == 0) atomicAdd(&C[code_local(fo.label)], 1u);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            cur = nxt;
-            p = pn;
+#pragma unroll
+            for (int u = 0; u < FA_B; ++u) {
+                cur[u] = nxt[u];
+                pc[u] = pn[u];
+            }
         }
     }
     __syncthreads();
@@ -1310,8 +1392,9 @@ __global__ __launch_bounds__(256) void k_fixpair_b(const float *__restrict__ aos
 __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, int d, const float *__restrict__ caos,
                                                int k, const uint32_t *__restrict__ amb, uint32_t namb,
                                                const uint32_t *__restrict__ cand_cnt,
-                                               const uint32_t *__restrict__ cand, uint32_t *__restrict__ labels,
-                                               uint32_t *__restrict__ ties, State *st) {
+                                               const uint32_t *__restrict__ cand, uint32_t cap,
+                                               uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
+                                               uint32_t *__restrict__ ovf, State *st) {
     const int lane = threadIdx.x & 63;
     const uint32_t a = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (a >= namb) return;
@@ -1319,11 +1402,15 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     const int ld = aos_ld(d);
     const float *prow = aos + (uint64_t)p * ld;
     const uint32_t cnt = cand_cnt[a];
-    if (cnt > CAND_CAP) {  // uniform per wave
+    if (cnt > cap) {  // uniform per wave
         if (lane == 0) {
-            atomicAdd(&st->overflow, 1u);
-            labels[p] = 0;  // the walk decides
-            ties[atomicAdd(&st->ties, 1u)] = p;
+            const uint32_t o = atomicAdd(&st->overflow, 1u);
+            if (ovf) {
+                ovf[o] = p;  // collected again with a larger list
+            } else {
+                labels[p] = 0;  // the walk decides
+                ties[atomicAdd(&st->ties, 1u)] = p;
+            }
         }
         return;
     }
@@ -1331,7 +1418,7 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     uint32_t bidx = 0xffffffffu;
     const uint32_t limit = cnt;
     for (uint32_t j = lane; j < limit; j += 64) {
-        const uint32_t c = cand[(uint64_t)a * CAND_CAP + j];
+        const uint32_t c = cand[(uint64_t)a * cap + j];
         const double dd = ref_dist(caos + (uint64_t)c * ld, prow, ld);
         if (dd < best || (dd == best && c < bidx)) {
             best = dd;
@@ -1344,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_exact(const float *__restrict__ aos, in
     uint32_t mine = 0;
     uint32_t lowest = 0xffffffffu;
     for (uint32_t j = lane; j < limit; j += 64) {
-        const uint32_t c = cand[(uint64_t)a * CAND_CAP + j];
+        const uint32_t c = cand[(uint64_t)a * cap + j];
         if (ref_dist(caos + (uint64_t)c * ld, prow, ld) == m) {
             ++mine;
             lowest = min(lowest, c);
@@ -1565,19 +1652,21 @@ template <int KS>
 struct Sweep {
     static void main(st_ctx *c, const uint4 *pfrag, uint32_t ntiles, uint32_t n, const uint4 *cfrag, uint32_t ctiles,
                      const float *pnorm, const float *pdn, const uint32_t *cmax, const float *chalf,
-                     const float *chalf_d, const Bound &bnd,
+                     const float *chalf_d, const float *ntab, const Bound &bnd,
                      uint32_t *labels, float *thr, uint32_t *amb, State *st, uint32_t *pair_pts, uint2 *pair_codes,
                      uint32_t *code_hist) {
         const uint32_t per_block = NW * PT;
         const dim3 grid((ntiles + per_block - 1) / per_block);
         KTimer kt(c, "kn.sweep");
         hipLaunchKernelGGL((k_sweep<KS, 0>), grid, dim3(WG), 0, c->stream, pfrag, ntiles, n, cfrag, ctiles, pnorm,
-                           pdn, cmax, chalf, chalf_d, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, pair_pts,
+                           pdn, cmax, chalf, chalf_d, ntab, bnd, labels, thr, amb, st, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                           pair_pts,
                            pair_codes, code_hist);
         ST_LAUNCH_CHECK();
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
-                        uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand) {
+                        uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand,
+                        uint32_t cap) {
         const uint32_t per_block = NW * PT;
         const uint32_t blocks = (atiles + per_block - 1) / per_block;
         // enough workgroups to cover the chip twice over
@@ -1586,9 +1675,9 @@ struct Sweep {
         KTimer kt(c, "kn.collect");
         hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const float *)nullptr, (const uint32_t *)nullptr,
-                           (const float *)nullptr, (const float *)nullptr, bnd,
+                           (const float *)nullptr, (const float *)nullptr, (const float *)nullptr, bnd,
                            (uint32_t *)nullptr, thr_slot,
-                           (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, (uint32_t *)nullptr,
+                           (uint32_t *)nullptr, (State *)nullptr, cand_cnt, cand, cap, (uint32_t *)nullptr,
                            (uint2 *)nullptr, (uint32_t *)nullptr);
         ST_LAUNCH_CHECK();
     }
@@ -1733,6 +1822,8 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
                        cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix, cnorm, cdn);
     hipLaunchKernelGGL(k_half_max, dim3(grid_for((uint64_t)ctiles * 2, 256, 1024)), dim3(256), 0, c->stream, cnorm,
                        cdn, ctiles * 2, chalf, chalf_d);
+    auto *ntab = wsT<float>(c, "kn.ntab", NTAB);
+    hipLaunchKernelGGL(k_norm_table, dim3(1), dim3(NTAB), 0, c->stream, cnorm, cdn, ctiles * 32, scal + 1, ntab);
     ST_LAUNCH_CHECK();
     auto *pair_pts = wsT<uint32_t>(c, "kn.pairpts", n);
     auto *pair_codes = wsT<uint2>(c, "kn.paircodes", n);
@@ -1745,7 +1836,7 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     auto *hist = grouped_fix ? wsT<uint32_t>(c, "kn.fbhist", ncodes) : nullptr;
     if (hist) ST_HIP(hipMemsetAsync(hist, 0, ncodes * sizeof(uint32_t), c->stream));
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
-                                        chalf_d, bnd,
+                                        chalf_d, ntab, bnd,
                                         labels, thr, amb, dstate, pair_pts, pair_codes, hist)));
     if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
@@ -1833,16 +1924,42 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, c->stream,
                            pfrag, amb, thr, namb, ks, afrag, thr_slot, cand_cnt);
         ST_LAUNCH_CHECK();
-        ST_KS_DISPATCH(ks,
-                       (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt, cand)));
+        auto *ovf = wsT<uint32_t>(c, "kn.ovf", namb);
+        ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt, cand,
+                                               (uint32_t)CAND_CAP)));
         {
             KTimer kt(c, "kn.exact");
             hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, caos, k, amb, namb,
-                               cand_cnt, cand, labels, ties, dstate);
+                               cand_cnt, cand, (uint32_t)CAND_CAP, labels, ties, ovf, dstate);
             ST_LAUNCH_CHECK();
         }
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
+        if (h->overflow) {
+            // points whose window holds more than CAND_CAP rows (wide windows: outlying points of
+            // heavy-tailed data): collected again with lists of CAND_CAP2, in batches; only those
+            // that overflow these too take the KdTree walk
+            const uint32_t nov = h->overflow, batch = std::min(nov, (uint32_t)OVF_BATCH);
+            const uint32_t btiles = (batch + 31) / 32;
+            auto *afrag2 = wsT<uint4>(c, "kn.afrag2", (size_t)btiles * ks * 64);
+            auto *thr2 = wsT<float>(c, "kn.thrslot2", (size_t)btiles * 32);
+            auto *cnt2 = wsT<uint32_t>(c, "kn.ccnt2", (size_t)btiles * 32);
+            auto *cand2 = wsT<uint32_t>(c, "kn.cand2", (size_t)batch * CAND_CAP2);
+            for (uint32_t b0 = 0; b0 < nov; b0 += batch) {
+                const uint32_t m = std::min(batch, nov - b0), mt = (m + 31) / 32;
+                hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)mt * 32, 256, 4096)), dim3(256), 0,
+                                   c->stream, pfrag, ovf + b0, thr, m, ks, afrag2, thr2, cnt2);
+                ST_LAUNCH_CHECK();
+                ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag2, mt, m, cfrag, ctiles, bnd, thr2, cnt2, cand2,
+                                                       (uint32_t)CAND_CAP2)));
+                KTimer kt(c, "kn.exact");
+                hipLaunchKernelGGL(k_exact, dim3((m + 3) / 4), dim3(256), 0, c->stream, aos, d, caos, k, ovf + b0, m,
+                                   cnt2, cand2, (uint32_t)CAND_CAP2, labels, ties, (uint32_t *)nullptr, dstate);
+                ST_LAUNCH_CHECK();
+            }
+            ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipStreamSynchronize(c->stream));
+        }
         if (getenv("ST_DEBUG")) {  // candidate-count histogram of the ambiguous points
             std::vector<uint32_t> cc(namb);
             ST_HIP(hipMemcpy(cc.data(), cand_cnt, namb * 4, hipMemcpyDeviceToHost));

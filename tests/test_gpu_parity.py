@@ -152,10 +152,20 @@ def test_kmeans_nd_uncertified_sums_vs_oracle(ctx, n, d, k, tiny, mode, monkeypa
     same_bits(cent, ocent)
 
 
-@pytest.mark.parametrize('n,d,k,iters', [(20_000, 45, 1024, 2), (30_000, 9, 2048, 2), (60_000, 1, 256, 4)])
-def test_kmeans_vs_oracle(ctx, n, d, k, iters):
+def heavy_tailed(rng, n, d, scale=0.1):
+    """Student-t (nu = 3) coordinates through a fixed mixing matrix: heavy-tailed, correlated SH
+    rows like trained scenes carry (outlying rows become outlying centroids)"""
+    m = np.eye(d) + 0.5 * np.random.default_rng(3).normal(0, 1, (d, d)) / np.sqrt(d)
+    t = rng.normal(0, 1, (n, d)) / np.sqrt((rng.normal(0, 1, (n, 3)) ** 2).sum(1, keepdims=True) / 3)
+    return [np.ascontiguousarray(c) for c in (t @ m.T * scale).astype(np.float32).T]
+
+
+@pytest.mark.parametrize('n,d,k,iters,dist', [(20_000, 45, 1024, 2, 'gauss'), (30_000, 9, 2048, 2, 'gauss'),
+                                              (60_000, 1, 256, 4, 'gauss'), (20_000, 45, 1024, 3, 't3')])
+def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
     rng = np.random.default_rng(n + d)
-    cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
+    cols = ([rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)] if dist == 'gauss'
+            else heavy_tailed(rng, n, d))
     draws = oracle.mulberry32(n + k, 4 * k * (iters + 1) + 64)
     cent, labels, used = ctx.kmeans(cols, k, iters, draws)
     rc, ocent, olabels, oused = oracle.kmeans(cols, k, iters, draws)
@@ -176,7 +186,7 @@ def set_mode(monkeypatch, mode):
 
 @pytest.mark.parametrize('mode', K1_MODES)
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
-def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
+def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch, capfd):
     """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
     hold tiny members, so the sequential f64 sum rounds -- a few events (the replay) or many
     (the sequential fallback).  mode: the iteration queued without read-backs, the flagged
@@ -185,8 +195,12 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch)
     (ST_K1_SYNC), the flagged clusters' members gathered by the tile kernels (ST_K1_TILES),
     every iteration's member sort (ST_K1_SORT), the queued run abandoned at the first flagged
     cluster and rerun synchronised (ST_K1_FF_MAX=0), or the replay capped at 0 / 2 candidates so
-    that the sequential chain takes over (ST_REPLAY_CAP)."""
+    that the sequential chain takes over (ST_REPLAY_CAP; ST_DEBUG's counts show that it did)."""
     set_mode(monkeypatch, mode)
+    capped = mode.startswith('ST_REPLAY_CAP') and (tiny_frac > 0 if mode.endswith('=0') else tiny_frac >= 0.02)
+    if capped:
+        monkeypatch.setenv('ST_DEBUG', '1')
+        capfd.readouterr()
     rng = np.random.default_rng(77)
     n = 300_000
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(3)]
@@ -195,6 +209,11 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch)
         c[tiny] *= np.float32(1e-9)
     draws = oracle.mulberry32(5, 1 << 14)
     cent, labels, used = ctx.cluster1d(cols, 4, draws)
+    if capped:  # the capped replay sent clusters down the sequential chain
+        import re
+        err = capfd.readouterr().err
+        seq = sum(int(x) for x in re.findall(r'sequential-fallback=(\d+)', err)) + len(re.findall(r',seq=1', err))
+        assert seq > 0, err[-2000:]
     rc, ocent, olabels, oused = oracle.cluster1d(cols, 4, draws)
     assert rc == 0 and used == oused
     assert np.array_equal(cent.view(np.uint32), ocent.view(np.uint32))
@@ -246,20 +265,29 @@ def test_cluster1d_sorted_columns_vs_oracle(ctx, mode, monkeypatch):
     assert np.array_equal(labels, olabels)
 
 
-@pytest.mark.parametrize('n,k,dup', [(40_000, 65536, 0.0), (30_000, 65536, 0.3), (20_000, 131072, 0.0)])
-def test_nd_assign_full_palette_argmin(ctx, n, k, dup):
+@pytest.mark.parametrize('n,k,dup,dist', [(40_000, 65536, 0.0, 'gauss'), (30_000, 65536, 0.3, 'gauss'),
+                                          (20_000, 131072, 0.0, 'gauss'), (40_000, 65536, 0.0, 't3'),
+                                          (30_000, 65536, 0.3, 't3')])
+def test_nd_assign_full_palette_argmin(ctx, n, k, dup, dist):
     """One assign pass at the SOG palette size (K = 65,536 / 131,072, D = 45) against a
     brute-force f64 distance computed on the device in the reference's own order
     (kd-tree.ts:26-35: l += (c - p)^2 sequentially over the dimensions, each op rounded
     like a JS number): every label must reach the exact minimum.  dup > 0 makes a share of
-    the points copies of centroids (distance 0 and near-ties between neighbouring rows)."""
+    the points copies of centroids (distance 0 and near-ties between neighbouring rows).
+    t3: heavy-tailed correlated points, the centroids data rows of the same distribution
+    (outlying centroids: the decision window must not widen for every point)."""
     import torch
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev)
     g.manual_seed(n + k)
     d = 45
-    cen = (torch.randn(d, k, generator=g, device=dev) * 0.05).contiguous()
-    pts = torch.randn(d, n, generator=g, device=dev) * 0.1
+    if dist == 'gauss':
+        cen = (torch.randn(d, k, generator=g, device=dev) * 0.05).contiguous()
+        pts = torch.randn(d, n, generator=g, device=dev) * 0.1
+    else:
+        rows = heavy_tailed(np.random.default_rng(n + k), n + k, d)
+        cen = torch.from_numpy(np.stack([r[:k] for r in rows])).to(dev).contiguous()
+        pts = torch.from_numpy(np.stack([r[k:] for r in rows])).to(dev)
     if dup:
         m = int(n * dup)
         pick = torch.randint(0, k, (m,), generator=g, device=dev)

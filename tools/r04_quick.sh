@@ -1,0 +1,16 @@
+#!/bin/bash
+# k-means parity tests + the window / heavy-tailed measurement + a short headline bench
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+tag=${1:-q}
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_sog65k.py -v -x --timeout 300 --timeout-method thread \
+    -k "kmeans or argmin or sog65k or sog_golden" > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -2 gpurun_out/${tag}_tests.log
+bash tools/kn_window.sh ${tag} || exit 1
+timeout -k 10 400 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-paths > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
+python3 -c "
+import json; r=json.load(open('gpurun_out/${tag}_bench.json'))
+print('value', r['value'], 'ms', r['ms_per_step'], 'sweep', r['roofline']['avg_launch_ms'], 'verified', r['verified'])
+print({k: round(v['avg_ms'], 3) for k, v in r['kernels'].items()})
+print(r['stages_ms'])"
