@@ -155,8 +155,14 @@ __device__ inline float norm_reach(float pn, float t) {
 //     table's residual at R instead of the palette's cm / dcm -- one outlying centroid no longer
 //     widens every point's window.
 // With R1 >= cb and R >= cm this is the palette-wide window of round 3.
-__device__ inline float wbound_r(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float ntab_scale,
-                                 const float *__restrict__ ntab, float m1u) {
+struct WinR {
+    float W;    // the window against every other tile-half
+    float eb;   // the best row's error bound
+    float sb2;  // its f64-rounding term rel (pn + |c1|)^2
+    float cr;   // the largest norm a competitor can have (<= cm)
+};
+__device__ inline WinR wbound_r(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float ntab_scale,
+                                const float *__restrict__ ntab, float m1u) {
     const float e0 = err_bound(B, pn, dp, cb, dcb);
     const float c1 = fminf(norm_reach(pn, m1u + e0 * 1.0001f), cb);
     const float eb = err_bound(B, pn, dp, c1, fminf(dcb, ntab[norm_bucket(c1, ntab_scale)]));
@@ -165,13 +171,17 @@ __device__ inline float wbound_r(const Bound &B, float pn, float dp, float cb, f
     const float cr = fminf(norm_reach(pn, t), cm);
     const float dcr = ntab[norm_bucket(cr, ntab_scale)];
     const float sr = pn + cr;
-    return (eb + err_bound(B, pn, dp, cr, dcr) + B.rel * (sb * sb + sr * sr)) * 1.0001f;
+    return WinR{(eb + err_bound(B, pn, dp, cr, dcr) + B.rel * (sb * sb + sr * sr)) * 1.0001f, eb, B.rel * sb * sb, cr};
 }
 
-// the window between two given tile-halves (largest norms ca, cb and residuals dca, dcb)
-__device__ inline float wbound_pair(const Bound &B, float pn, float dp, float ca, float dca, float cb, float dcb) {
-    const float s = pn + fmaxf(ca, cb);
-    return (err_bound(B, pn, dp, ca, dca) + err_bound(B, pn, dp, cb, dcb) + 2.0f * B.rel * s * s) * 1.0001f;
+// the window against one given tile-half (largest norm c2, residual dc2): its rows compete with
+// the norm bound of wbound_r too
+__device__ inline float wbound_half(const Bound &B, const WinR &w, float pn, float dp, float c2, float dc2,
+                                    float ntab_scale, const float *__restrict__ ntab) {
+    const float cn = fminf(w.cr, c2);
+    const float dn = fminf(dc2, ntab[norm_bucket(cn, ntab_scale)]);
+    const float s2 = pn + cn;
+    return (w.eb + err_bound(B, pn, dp, cn, dn) + w.sb2 + B.rel * s2 * s2) * 1.0001f;
 }
 
 // largest norm and largest rounding-residual norm (rounded up) among the 16 rows of each tile-half
@@ -576,7 +586,8 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float pn = pnorm[p], dp = pdn[p];
-            const float W = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
+            const WinR wr = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
+            const float W = wr.W;
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
                 if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
@@ -584,7 +595,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                 // every candidate lies in the two best tile-halves.  Only the second one competes
                 // with the first, so its own largest norm bounds its rows' error instead of the
                 // palette's (chalf[code2] <= cm): often that already decides the point
-                const float W2 = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], chalf[code2], chalf_d[code2]);
+                const float W2 = wbound_half(bnd, wr, pn, dp, chalf[code2], chalf_d[code2], ntab_scale, ntab);
                 if (nm2 > nm1 + W2 + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                     labels[p] = code1;
                     if (code_hist) atomicAdd(&code_hist[code1], 1u);
