@@ -1,13 +1,15 @@
 // st_chunk.hip -- compressed-PLY chunk packing (write-compressed-ply.ts:56-109,
 // CompressedChunk.pack compressed-chunk.ts:44-180).
 //
-// One 256-thread workgroup per 256-splat chunk, one lane per splat of the
-// Morton order.  Per-chunk min/max use Math.min/Math.max semantics (NaN
-// propagates, -0 < +0) through wave64 shuffles + LDS; the quantisers run in
-// f64 exactly as the JS; the final partial chunk is padded with its last
-// splat (write-compressed-ply.ts:90-93).  HBM traffic per splat: the column
-// transpose (14 + 3C floats read, the padded row written), one gathered row,
-// 16 B vertex + 3C bytes SH out.
+// Two passes.  k_pack_rows reads the 14 member columns and the 3C SH columns in input order
+// (coalesced) and writes one packed row per splat with everything that does not depend on the
+// chunk (positions, scales, the colour and opacity bytes' inputs, the rotation word, the SH
+// bytes).  k_pack_rows_chunk takes one 256-splat chunk of the Morton order per wave: each lane
+// gathers four rows, the chunk's min / max reduce with Math.min / Math.max semantics (NaN
+// propagates, -0 < +0) in registers and wave64 shuffles, the quantisers run in f64 exactly as
+// the JS, and the final partial chunk is padded with its last splat
+// (write-compressed-ply.ts:90-93).  HBM traffic per splat: 59 columns read and a 96-B row
+// written, then the row gathered and 16 B vertex + 3C bytes SH written.
 #include <cstdlib>
 
 #include "st_internal.h"
@@ -33,32 +35,6 @@ __device__ inline float jmax(float a, float b) {
     return a > b ? a : b;
 }
 
-// JS min and max over the 256 lanes of the block for NV values each
-template <int NV>
-__device__ inline void block_minmax(float (&mn)[NV], float (&mx)[NV]) {
-    __shared__ float smn[NV][4], smx[NV][4];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mn[v] = jmin(mn[v], __shfl_xor(mn[v], o, 64));
-            mx[v] = jmax(mx[v], __shfl_xor(mx[v], o, 64));
-        }
-        if (lane == 0) {
-            smn[v][w] = mn[v];
-            smx[v][w] = mx[v];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        mn[v] = jmin(jmin(smn[v][0], smn[v][1]), jmin(smn[v][2], smn[v][3]));
-        mx[v] = jmax(jmax(smx[v][0], smx[v][1]), jmax(smx[v][2], smx[v][3]));
-    }
-    __syncthreads();
-}
-
 __device__ inline double normalize01(double x, double mn, double mx) {
     if (x <= mn) return 0;
     if (x >= mx) return 1;
@@ -72,10 +48,6 @@ __device__ inline uint32_t pack_unorm(double value, int bits) {
 
 __device__ inline uint32_t pack111011(double x, double y, double z) {
     return (pack_unorm(x, 11) << 21) | (pack_unorm(y, 10) << 11) | pack_unorm(z, 11);
-}
-
-__device__ inline uint32_t pack8888(double x, double y, double z, double w) {
-    return (pack_unorm(x, 8) << 24) | (pack_unorm(y, 8) << 16) | (pack_unorm(z, 8) << 8) | pack_unorm(w, 8);
 }
 
 // packRot: Quat(x=rot_0, y=rot_1, z=rot_2, w=rot_3).normalize(), smallest-three 2+10+10+10
@@ -118,178 +90,6 @@ struct TransposeArgs {
     uint64_t n;
     float *rows;
 };
-
-// RA_ROWS rows per block through LDS: coalesced column reads (all of a thread's loads issued
-// before the first LDS store), coalesced row writes
-constexpr int RA_ROWS = 256;
-__global__ __launch_bounds__(256) void k_rows_aos(const TransposeArgs a) {
-    __shared__ float tile[RA_ROWS * 16];  // rl <= 16
-    const uint64_t r0 = (uint64_t)blockIdx.x * RA_ROWS;
-    const int t = threadIdx.x;
-    const uint64_t row = r0 + t;
-    const uint64_t rsafe = row < a.n ? row : a.n - 1;  // every load in bounds, no branch around it
-    float v[16];
-#pragma unroll
-    for (int col = 0; col < 16; ++col) v[col] = (col < a.ncol) ? a.src[col][rsafe] : 0.0f;
-#pragma unroll
-    for (int col = 0; col < 16; ++col)
-        if (col < a.rl) tile[t * a.rl + col] = (col < a.ncol && row < a.n) ? v[col] : 0.0f;
-    __syncthreads();
-    const uint64_t nrows = (a.n - r0 < RA_ROWS) ? (a.n - r0) : RA_ROWS;
-    float4 *dst = reinterpret_cast<float4 *>(a.rows + r0 * a.rl);
-    const float4 *s4 = reinterpret_cast<const float4 *>(tile);
-    for (uint64_t e = t; e < nrows * a.rl / 4; e += 256) dst[e] = s4[e];
-}
-
-// SH bytes (write-compressed-ply.ts:83-87) in the input's row order: a value depends on its
-// own splat only, so it is computed while the columns stream in (coalesced), then gathered
-// with the row as SHB contiguous bytes (3C bytes, padded to 16-byte rows)
-constexpr int SHB = 48;  // byte row stride of the SH rows (3C <= 45)
-__device__ inline uint8_t sh_byte(float v) {
-    const double nv = (double)v / 8 + 0.5;
-    return js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
-}
-__global__ __launch_bounds__(256) void k_sh_rows(const TransposeArgs a, int nsh, uint8_t *__restrict__ shrows) {
-    __shared__ uint32_t stage[256 * SHB / 4];
-    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
-    const uint32_t t = threadIdx.x;
-    uint8_t *st8 = reinterpret_cast<uint8_t *>(stage);
-    const bool real = r0 + t < a.n;
-    const uint64_t rsafe = real ? r0 + t : a.n - 1;  // loads stay in bounds without a branch
-    // batches of 12 columns: the loads of a batch are in flight together
-    for (int k0 = 0; k0 < SHB; k0 += 12) {
-        float v[12];
-#pragma unroll
-        for (int u = 0; u < 12; ++u) v[u] = a.src[14 + min(k0 + u, nsh - 1)][rsafe];
-#pragma unroll
-        for (int u = 0; u < 12; ++u) st8[t * SHB + k0 + u] = (k0 + u < nsh && real) ? sh_byte(v[u]) : 0u;
-    }
-    __syncthreads();
-    const uint64_t nrows = (a.n - r0 < 256) ? (a.n - r0) : 256;
-    uint4 *dst = reinterpret_cast<uint4 *>(shrows + r0 * SHB);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
-    for (uint64_t e = t; e < nrows * SHB / 16; e += 256) dst[e] = s4[e];
-}
-
-// the same from float64 values (the JS numbers of SH columns of another type than float32:
-// write-compressed-ply.ts:85 divides the row's number itself)
-struct ShRowsD {
-    const double *src[45];
-    uint64_t n;
-};
-__global__ __launch_bounds__(256) void k_sh_rows_d(const ShRowsD a, int nsh, uint8_t *__restrict__ shrows) {
-    __shared__ uint32_t stage[256 * SHB / 4];
-    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
-    const uint32_t t = threadIdx.x;
-    uint8_t *st8 = reinterpret_cast<uint8_t *>(stage);
-    const bool real = r0 + t < a.n;
-    const uint64_t rsafe = real ? r0 + t : a.n - 1;
-    for (int k = 0; k < SHB; ++k) {
-        uint8_t b = 0;
-        if (k < nsh && real) {
-            const double nv = a.src[k][rsafe] / 8 + 0.5;
-            b = js::to_uint8(js::max_(0, js::min_(255, __builtin_trunc(nv * 256))));
-        }
-        st8[t * SHB + k] = b;
-    }
-    __syncthreads();
-    const uint64_t nrows = (a.n - r0 < 256) ? (a.n - r0) : 256;
-    uint4 *dst = reinterpret_cast<uint4 *>(shrows + r0 * SHB);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
-    for (uint64_t e = t; e < nrows * SHB / 16; e += 256) dst[e] = s4[e];
-}
-
-struct ChunkArgs {
-    const float *rows;  // AoS rows of RL = 16 floats: x y z scale_0..2 f_dc_0..2 opacity rot_0..3
-    const uint8_t *shrows;  // SH bytes, SHB per row (k_sh_rows)
-    int rl, nsh;
-    uint64_t n;
-    const uint32_t *order;
-    float *chunk;
-    uint4 *vertex;
-    uint8_t *sh_out;
-};
-
-__global__ __launch_bounds__(256) void k_pack_chunk(const ChunkArgs a) {
-    enum { X, Y, Z, S0, S1, S2, R, G, B, OP, Q0, Q1, Q2, Q3 };
-    __shared__ uint32_t sh_stage[256 * 45 / 4];
-    const uint64_t c = blockIdx.x;
-    const uint64_t base = c * 256;
-    const uint32_t num = (uint32_t)((a.n < base + 256 ? a.n : base + 256) - base);
-    const uint32_t j = threadIdx.x;
-    const bool real = j < num;
-    const uint32_t row = a.order[base + (real ? j : num - 1)];
-    const float4 *r4 = reinterpret_cast<const float4 *>(a.rows + (uint64_t)row * a.rl);
-    // both gathered rows are requested before anything waits on them (the padded lanes
-    // read the chunk's last row, always in bounds)
-    float4 mv[4];
-    uint4 sv[SHB / 16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) mv[q] = r4[q];
-    if (a.nsh) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.shrows + (uint64_t)row * SHB);
-#pragma unroll
-        for (int q = 0; q < SHB / 16; ++q) sv[q] = src[q];
-    }
-    float d[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        d[4 * q] = mv[q].x;
-        d[4 * q + 1] = mv[q].y;
-        d[4 * q + 2] = mv[q].z;
-        d[4 * q + 3] = mv[q].w;
-    }
-    // 8-bit SH (write-compressed-ply.ts:83-87), staged in LDS for coalesced stores
-    if (a.nsh) {
-        uint8_t *stage = reinterpret_cast<uint8_t *>(sh_stage);
-        if (real) {
-            uint32_t w[SHB / 4];
-#pragma unroll
-            for (int q = 0; q < SHB / 16; ++q) {
-                w[4 * q] = sv[q].x;
-                w[4 * q + 1] = sv[q].y;
-                w[4 * q + 2] = sv[q].z;
-                w[4 * q + 3] = sv[q].w;
-            }
-            for (int k = 0; k < a.nsh; ++k) stage[j * a.nsh + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-        }
-        __syncthreads();
-        uint8_t *o = a.sh_out + base * (uint64_t)a.nsh;
-        const uint32_t bytes = num * (uint32_t)a.nsh;
-        // chunk bases are multiples of 256 * nsh bytes, so o is 4-byte aligned
-        for (uint32_t e = j; e < bytes / 4; e += 256) reinterpret_cast<uint32_t *>(o)[e] = sh_stage[e];
-        for (uint32_t e = (bytes / 4) * 4 + j; e < bytes; e += 256) o[e] = stage[e];
-    }
-    float mn[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
-    float mx[6] = {d[X], d[Y], d[Z], d[S0], d[S1], d[S2]};
-    block_minmax<6>(mn, mx);
-    double smn[3], smx[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {  // clamp(v, -20, 20) = Math.max(-20, Math.min(20, v))
-        smn[i] = js::max_(-20, js::min_(20, (double)mn[3 + i]));
-        smx[i] = js::max_(-20, js::min_(20, (double)mx[3 + i]));
-    }
-    const float col[3] = {(float)((double)d[R] * SH_C0 + 0.5), (float)((double)d[G] * SH_C0 + 0.5),
-                          (float)((double)d[B] * SH_C0 + 0.5)};
-    float cmn[3] = {col[0], col[1], col[2]}, cmx[3] = {col[0], col[1], col[2]};
-    block_minmax<3>(cmn, cmx);
-    if (real) {
-        uint4 v;
-        v.x = pack111011(normalize01(d[X], mn[0], mx[0]), normalize01(d[Y], mn[1], mx[1]),
-                         normalize01(d[Z], mn[2], mx[2]));
-        v.y = pack_rot(d[Q0], d[Q1], d[Q2], d[Q3]);
-        v.z = pack111011(normalize01(d[S0], smn[0], smx[0]), normalize01(d[S1], smn[1], smx[1]),
-                         normalize01(d[S2], smn[2], smx[2]));
-        v.w = pack8888(normalize01(col[0], cmn[0], cmx[0]), normalize01(col[1], cmn[1], cmx[1]),
-                       normalize01(col[2], cmn[2], cmx[2]), js::sigmoid(d[OP]));
-        a.vertex[base + j] = v;
-    }
-    if (j < 18) {
-        const double cd[18] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2], smn[0], smn[1], smn[2],
-                               smx[0], smx[1], smx[2], cmn[0], cmn[1], cmn[2], cmx[0], cmx[1], cmx[2]};
-        a.chunk[c * 18 + j] = (float)cd[j];
-    }
-}
 
 // ---- packed rows, one wave per chunk --------------------------------------------------
 // Everything of a splat that does not depend on its chunk is computed once, in input order,
@@ -498,53 +298,21 @@ void pack_compressed_dev(st_ctx *c, const st_table *t, const uint32_t *order, fl
         ta.src[14 + i] = sh64 ? nullptr : col_or_null(t, nm);
     }
     KTimer kt(c, "chunk.pack");
-    if (!getenv("ST_PACK_WG")) {
-        // packed rows (k_pack_rows), one wave per chunk (k_pack_rows_chunk)
-        PackRowsArgs pa{};
-        for (int i = 0; i < 14; ++i) pa.m[i] = ta.src[i];
-        for (int i = 0; i < nsh; ++i) {
-            if (sh64) pa.sh64[i] = sh64[i];
-            else pa.sh[i] = ta.src[14 + i];
-        }
-        pa.n = n;
-        pa.rows = wsT<uint32_t>(c, "chunk.prows", n * (uint64_t)(nsh > 23 ? 24 : 16));
-        switch (nsh) {
-            case 0: launch_pack_rows<0>(c, pa, order, chunk, vertex, sh); break;
-            case 9: launch_pack_rows<9>(c, pa, order, chunk, vertex, sh); break;
-            case 24: launch_pack_rows<24>(c, pa, order, chunk, vertex, sh); break;
-            default: launch_pack_rows<45>(c, pa, order, chunk, vertex, sh); break;
-        }
-        ST_LAUNCH_CHECK();
-        return;
+    // packed rows (k_pack_rows), one wave per chunk (k_pack_rows_chunk)
+    PackRowsArgs pa{};
+    for (int i = 0; i < 14; ++i) pa.m[i] = ta.src[i];
+    for (int i = 0; i < nsh; ++i) {
+        if (sh64) pa.sh64[i] = sh64[i];
+        else pa.sh[i] = ta.src[14 + i];
     }
-    // one workgroup per chunk over a 64-B member row and a 48-B SH row (the round-2 kernels;
-    // ST_PACK_WG=1, experiments)
-    ta.ncol = 14;
-    ta.rl = 16;
-    ta.n = n;
-    ta.rows = wsT<float>(c, "chunk.rows", n * (uint64_t)ta.rl);
-    uint8_t *shrows = nsh ? wsT<uint8_t>(c, "chunk.shrows", n * (uint64_t)SHB) : nullptr;
-    ChunkArgs a{};
-    a.rows = ta.rows;
-    a.shrows = shrows;
-    a.rl = ta.rl;
-    a.nsh = nsh;
-    a.n = n;
-    a.order = order;
-    a.chunk = chunk;
-    a.vertex = reinterpret_cast<uint4 *>(vertex);
-    a.sh_out = sh;
-    const uint64_t nchunks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_rows_aos, dim3((unsigned)((n + RA_ROWS - 1) / RA_ROWS)), dim3(256), 0, c->stream, ta);
-    if (nsh && sh64) {
-        ShRowsD sd{};
-        for (int i = 0; i < nsh; ++i) sd.src[i] = sh64[i];
-        sd.n = n;
-        hipLaunchKernelGGL(k_sh_rows_d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, sd, nsh, shrows);
-    } else if (nsh) {
-        hipLaunchKernelGGL(k_sh_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, ta, nsh, shrows);
+    pa.n = n;
+    pa.rows = wsT<uint32_t>(c, "chunk.prows", n * (uint64_t)(nsh > 23 ? 24 : 16));
+    switch (nsh) {
+        case 0: launch_pack_rows<0>(c, pa, order, chunk, vertex, sh); break;
+        case 9: launch_pack_rows<9>(c, pa, order, chunk, vertex, sh); break;
+        case 24: launch_pack_rows<24>(c, pa, order, chunk, vertex, sh); break;
+        default: launch_pack_rows<45>(c, pa, order, chunk, vertex, sh); break;
     }
-    hipLaunchKernelGGL(k_pack_chunk, dim3((unsigned)nchunks), dim3(256), 0, c->stream, a);
     ST_LAUNCH_CHECK();
 }
 

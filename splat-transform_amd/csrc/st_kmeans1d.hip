@@ -398,75 +398,6 @@ __global__ __launch_bounds__(256) void k_pairs1d(const float *pts, const uint32_
 }
 
 
-// calcAverage (k-means.ts:41-63) for one cluster: the reference adds the members' values
-// in ascending point order into one f64.  When every partial sum is exactly representable
-// (certificate: sum|x| < 2^(emin+53), emin = the smallest ulp exponent among the values)
-// the order is immaterial and the block sums in parallel; otherwise the cluster is
-// flagged (1) for k_sum1d_replay, which replays the sequential sum exactly from one
-// rounding event to the next.
-__global__ __launch_bounds__(256) void k_sum1d(const uint32_t *__restrict__ vals, const uint32_t *__restrict__ start,
-                                               int k, float *__restrict__ cen, uint32_t *__restrict__ seq_flag,
-                                               int32_t *__restrict__ emin_c, double *__restrict__ sabs_c) {
-    const int cl = blockIdx.x;
-    const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    if (s1 == s0) {  // empty: re-seeded separately
-        if (threadIdx.x == 0) seq_flag[cl] = 0;
-        return;
-    }
-    __shared__ double red_s[4], red_a[4];
-    __shared__ int red_e[4];
-    double sum = 0, sabs = 0;
-    int emin = 1 << 20;
-    for (uint32_t j = s0 + threadIdx.x; j < s1; j += blockDim.x) {
-        const float x = __builtin_bit_cast(float, vals[j]);
-        sum += (double)x;
-        sabs += (double)__builtin_fabsf(x);
-        if (x != 0.0f) emin = min(emin, ulp_exp(x));
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int o = 32; o > 0; o >>= 1) {
-        sum += __shfl_xor(sum, o, 64);
-        sabs += __shfl_xor(sabs, o, 64);
-        emin = min(emin, __shfl_xor(emin, o, 64));
-    }
-    if (lane == 0) {
-        red_s[w] = sum;
-        red_a[w] = sabs;
-        red_e[w] = emin;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    sum = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);
-    sabs = (red_a[0] + red_a[1]) + (red_a[2] + red_a[3]);
-    emin = min(min(red_e[0], red_e[1]), min(red_e[2], red_e[3]));
-    // sum|x| bounded above with slack for its own rounding
-    const bool exact = sum_is_exact(sabs, emin);
-    seq_flag[cl] = exact ? 0u : 1u;
-    emin_c[cl] = emin;
-    sabs_c[cl] = sabs;
-    if (exact) cen[cl] = (float)(sum / (double)(s1 - s0));
-}
-
-__global__ __launch_bounds__(RT) void k_sum1d_replay(const uint32_t *__restrict__ vals,
-                                                     const uint32_t *__restrict__ start,
-                                                     uint32_t *__restrict__ seq_flag,
-                                                     const int32_t *__restrict__ emin_c,
-                                                     const double *__restrict__ sabs_c, float *__restrict__ cen,
-                                                     __int128 *__restrict__ cand_all) {
-    const int cl = blockIdx.x;
-    if (seq_flag[cl] != 1u) return;
-    const uint32_t s0 = start[cl], s1 = start[cl + 1];
-    double sum = 0;
-    const bool ok = replay_sum(vals, s0, s1, emin_c[cl], sabs_c[cl], 0.0, cand_all + (uint64_t)cl * CAND_MAX, &sum);
-    if (threadIdx.x != 0) return;
-    if (!ok) {
-        seq_flag[cl] = 2u;  // sequential chain (k_sum1d_seq)
-        return;
-    }
-    cen[cl] = (float)(sum / (double)(s1 - s0));
-    seq_flag[cl] = 0u;
-}
-
 // the sequential f64 sum of members [s0, s1) on the calling lane: the loads run PF x 16 bytes
 // ahead of the dependent add chain
 __device__ inline double seq_sum1d(const uint32_t *__restrict__ vals, uint32_t s0, uint32_t s1) {
@@ -1983,15 +1914,13 @@ bool assign1d(st_ctx *c, const float *pts, uint64_t n, int k, const float *cen, 
     radix_sort_u32(c, ckeys, corder, (uint64_t)k, 0, 32, "k1.csort");
     const unsigned g = grid_for(n, 256, 256 * 16);
     KTimer kt(c, "k1.assign");
-    if (k <= KD1_LDS && !getenv("ST_KD1_WALK")) {
+    if (k <= KD1_LDS) {
         hipLaunchKernelGGL(k_kd1_assign_fast, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k,
                            (keys && !need_labels) ? (uint32_t *)nullptr : labels, keys, vals);
         ST_LAUNCH_CHECK();
         return keys != nullptr;
-    } else if (k <= KD1_LDS)
-        hipLaunchKernelGGL(k_kd1_assign<true>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
-    else
-        hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
+    }
+    hipLaunchKernelGGL(k_kd1_assign<false>, dim3(g), dim3(256), 0, c->stream, pts, n, cen, corder, k, labels);
     ST_LAUNCH_CHECK();
     return false;
 }
@@ -2005,8 +1934,6 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     auto *emin_c = wsT<int32_t>(c, "k1.emin", (size_t)k);
     auto *sabs_c = wsT<double>(c, "k1.sabs", (size_t)k);
     auto *cand_buf = wsT<__int128>(c, "k1.cands", (size_t)k * CAND_MAX);
-    // chunked update (ST_K1_BLOCK=1 selects the one-workgroup-per-cluster kernels)
-    const bool chunked = !getenv("ST_K1_BLOCK");
     const uint64_t maxch = n / SC_CH + (uint64_t)k + 1;
     const uint64_t chcap = n / FL_CH + (uint64_t)k + 1;  // the flagged replay's shorter chunks
     auto *ch_cnt = wsT<uint32_t>(c, "k1.chcnt", (size_t)k);
@@ -2020,9 +1947,9 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
     auto *rp_total = wsT<__int128>(c, "k1.rptotal", (size_t)k);
     int kbits = 1;
     while ((1ull << kbits) < (uint64_t)k) ++kbits;
-    // the fused iteration (k <= 256, no ST_KD1_WALK / ST_K1_PAIRS): byte labels + tile counts,
-    // scan, value-only scatter
-    const bool fused = k <= 256 && n > 0 && n < (1ull << 32) && !getenv("ST_KD1_WALK") && !getenv("ST_K1_PAIRS");
+    // the fused iteration (k <= 256; ST_K1_PAIRS forces the general one, test hook): byte labels
+    // + tile counts, scan, value-only scatter
+    const bool fused = k <= 256 && n > 0 && n < (1ull << 32) && !getenv("ST_K1_PAIRS");
     const uint32_t ntiles = (uint32_t)((n + F1_TILE - 1) / F1_TILE);
     uint8_t *lab8 = fused ? wsT<uint8_t>(c, "k1.lab8", n) : nullptr;
     // the sort-free iteration (k_kd1_assign_acc; ST_K1_SORT=1 keeps the member sort)
@@ -2036,28 +1963,20 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         auto *ticket = wsT<uint32_t>(c, "k1.ticket", 1);
         auto *dinfo = wsT<uint32_t>(c, "k1.info", 2);
         auto *bnd = wsT<Bnd1>(c, "k1.bnd", 256);
-        // the points' min / max keys (kmeans_dev's 1-D init); none: every cluster accumulates
-        const uint32_t *mm = getenv("ST_K1_NO_BOUNDS") ? nullptr : wsT<uint32_t>(c, "km.mm", 2);
+        // the points' min / max keys (kmeans_dev's 1-D init)
+        const uint32_t *mm = wsT<uint32_t>(c, "km.mm", 2);
         auto *hinfo = static_cast<uint32_t *>(pinned_slot(c, "k1.info", 8));
         ST_HIP(hipMemsetAsync(ticket, 0, sizeof(uint32_t), c->stream));
-        // the three-pass flagged update (k_ff_batch / k_ff_bscan / k_ff_place + k_ff_finish);
-        // ST_K1_FF_CHAIN=1 keeps the count / scan / scatter / chunked-replay chain
-        const bool three_pass = !getenv("ST_K1_FF_CHAIN");
+        // the three-pass flagged update (k_ff_batch / k_ff_bscan / k_ff_place + k_ff_finish)
         const uint32_t nbt = (uint32_t)((n + FB_PTS - 1) / FB_PTS);
-        uint32_t *ffz = nullptr, *ffcnt = nullptr, *ffpos = nullptr, *fflist = nullptr;
-        __int128 *ffpool = nullptr;
-        FAgg *ffagg = nullptr, *fftot = nullptr;
-        float *ffscr = nullptr;
-        if (three_pass) {
-            ffz = wsT<uint32_t>(c, "k1.ffz", FF_MAX);
-            ffcnt = wsT<uint32_t>(c, "k1.ffcnt", (size_t)FF_MAX * nbt);
-            ffpos = wsT<uint32_t>(c, "k1.ffpos", (size_t)FF_MAX * nbt);
-            fflist = wsT<uint32_t>(c, "k1.fflist", FF_MAX + 1);
-            ffpool = wsT<__int128>(c, "k1.ffpool", (size_t)FF_MAX * CAND_MAX);
-            ffagg = wsT<FAgg>(c, "k1.ffagg", (size_t)FF_MAX * nbt);
-            fftot = wsT<FAgg>(c, "k1.fftot", FF_MAX);
-            ffscr = wsT<float>(c, "k1.ffscr", (size_t)nbt * FB_PTS);
-        }
+        auto *ffz = wsT<uint32_t>(c, "k1.ffz", FF_MAX);
+        auto *ffcnt = wsT<uint32_t>(c, "k1.ffcnt", (size_t)FF_MAX * nbt);
+        auto *ffpos = wsT<uint32_t>(c, "k1.ffpos", (size_t)FF_MAX * nbt);
+        auto *fflist = wsT<uint32_t>(c, "k1.fflist", FF_MAX + 1);
+        auto *ffpool = wsT<__int128>(c, "k1.ffpool", (size_t)FF_MAX * CAND_MAX);
+        auto *ffagg = wsT<FAgg>(c, "k1.ffagg", (size_t)FF_MAX * nbt);
+        auto *fftot = wsT<FAgg>(c, "k1.fftot", FF_MAX);
+        auto *ffscr = wsT<float>(c, "k1.ffscr", (size_t)nbt * FB_PTS);
         // queued: no read-back per iteration (more than FF_MAX flagged clusters -> ERR_K1_MANY,
         // and kmeans_dev reruns with k1_sync); otherwise the count decides the flagged path
         const bool queued = !c->k1_sync && !getenv("ST_K1_TILES") && !getenv("ST_K1_SYNC");
@@ -2065,7 +1984,6 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         const uint32_t ff_max = getenv("ST_K1_FF_MAX") ? std::min<uint32_t>((uint32_t)atoi(getenv("ST_K1_FF_MAX")),
                                                                             (uint32_t)FF_MAX)
                                                        : (uint32_t)FF_MAX;
-        const uint64_t fl_maxch = chcap;
         for (int it = 0; it < iters; ++it) {
             {
                 KTimer kt(c, "k1.assign");
@@ -2082,53 +2000,30 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
             if (queued) {
                 // the flagged path queued behind the final with no read-back: its kernels find
                 // the flagged clusters on the device and return at once when there are none
-                if (three_pass) {
-                    const unsigned gb = (unsigned)std::min<uint64_t>((nbt + 3) / 4, 2048);
-                    hipLaunchKernelGGL(k_ff_batch, dim3(gb), dim3(256), 0, c->stream, lab8, pts, n, nbt, k, seq_flag,
-                                       emin_c, sabs_c, ffscr, ffagg, fflist);
-                    hipLaunchKernelGGL(k_ff_bscan, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, ffagg, fftot);
-                    const unsigned gp = (unsigned)std::min<uint64_t>(((uint64_t)FF_MAX * nbt + 3) / 4, 4096);
-                    hipLaunchKernelGGL(k_ff_place, dim3(gp), dim3(256), 0, c->stream, nbt, fflist, fstart, emin_c,
-                                       sabs_c, ffscr, ffagg, ffz, vals, ffpool, ffcnt, ffpos, fftot);
-                    hipLaunchKernelGGL(k_ff_finish, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, seq_flag,
-                                       fstart, emin_c, sabs_c, fftot, vals, ffpool, ffcnt, ffpos, cand_buf,
-                                       replay_cap(), cen, dstate);
-                    ST_LAUNCH_CHECK();
-                    if (getenv("ST_DEBUG")) {  // flagged clusters, their members and replay candidates
-                        uint32_t hfl[FF_MAX + 1], hz[FF_MAX];
-                        std::vector<uint32_t> f2(k), fs(k + 1);
-                        ST_HIP(hipMemcpyAsync(hfl, fflist, sizeof hfl, hipMemcpyDeviceToHost, c->stream));
-                        ST_HIP(hipMemcpyAsync(hz, ffz, sizeof hz, hipMemcpyDeviceToHost, c->stream));
-                        ST_HIP(hipMemcpyAsync(f2.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost, c->stream));
-                        ST_HIP(hipMemcpyAsync(fs.data(), fstart, 4 * (k + 1), hipMemcpyDeviceToHost, c->stream));
-                        ST_HIP(hipStreamSynchronize(c->stream));
-                        fprintf(stderr, "[st k1] n=%llu flagged=%u", (unsigned long long)n, hfl[0]);
-                        for (uint32_t f = 0; f < hfl[0] && f < (uint32_t)FF_MAX; ++f)
-                            fprintf(stderr, " c%u:members=%u,cands=%u,seq=%u", hfl[1 + f],
-                                    fs[hfl[1 + f] + 1] - fs[hfl[1 + f]], hz[f], f2[hfl[1 + f]] == 2u ? 1u : 0u);
-                        fprintf(stderr, "\n");
-                    }
-                    mark(c, "k1.update");
-                    continue;
-                }
-                const uint32_t nchf = (uint32_t)((n + FF_CH - 1) / FF_CH);
-                hipLaunchKernelGGL(k_ff_count, dim3(G), dim3(256), 0, c->stream, lab8, n, nchf, k, seq_flag, fhist);
-                hipLaunchKernelGGL(k_ff_scan, dim3(FF_MAX), dim3(FS_T), 0, c->stream, fhist, nchf, k, seq_flag, fstart);
-                hipLaunchKernelGGL(k_ff_scatter, dim3(G), dim3(256), 0, c->stream, lab8, pts, n, nchf, k, seq_flag,
-                                   fhist, vals);
+                const unsigned gb = (unsigned)std::min<uint64_t>((nbt + 3) / 4, 2048);
+                hipLaunchKernelGGL(k_ff_batch, dim3(gb), dim3(256), 0, c->stream, lab8, pts, n, nbt, k, seq_flag,
+                                   emin_c, sabs_c, ffscr, ffagg, fflist);
+                hipLaunchKernelGGL(k_ff_bscan, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, ffagg, fftot);
+                const unsigned gp = (unsigned)std::min<uint64_t>(((uint64_t)FF_MAX * nbt + 3) / 4, 4096);
+                hipLaunchKernelGGL(k_ff_place, dim3(gp), dim3(256), 0, c->stream, nbt, fflist, fstart, emin_c,
+                                   sabs_c, ffscr, ffagg, ffz, vals, ffpool, ffcnt, ffpos, fftot);
+                hipLaunchKernelGGL(k_ff_finish, dim3(FF_MAX), dim3(FN_T), 0, c->stream, nbt, fflist, seq_flag,
+                                   fstart, emin_c, sabs_c, fftot, vals, ffpool, ffcnt, ffpos, cand_buf,
+                                   replay_cap(), cen, dstate);
                 ST_LAUNCH_CHECK();
-                chunk_list(c, fstart, k, ch_cnt, ch_first, chunks, nullptr, FL_CH);
-                chunked_replay(c, vals, fstart, k, fl_maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum,
-                               rp_total, rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr, true);
-                if (getenv("ST_DEBUG")) {
-                    std::vector<uint32_t> f2(k);
-                    ST_HIP(hipMemcpyAsync(hinfo, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
+                if (getenv("ST_DEBUG")) {  // flagged clusters, their members and replay candidates
+                    uint32_t hfl[FF_MAX + 1], hz[FF_MAX];
+                    std::vector<uint32_t> f2(k), fs(k + 1);
+                    ST_HIP(hipMemcpyAsync(hfl, fflist, sizeof hfl, hipMemcpyDeviceToHost, c->stream));
+                    ST_HIP(hipMemcpyAsync(hz, ffz, sizeof hz, hipMemcpyDeviceToHost, c->stream));
                     ST_HIP(hipMemcpyAsync(f2.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost, c->stream));
+                    ST_HIP(hipMemcpyAsync(fs.data(), fstart, 4 * (k + 1), hipMemcpyDeviceToHost, c->stream));
                     ST_HIP(hipStreamSynchronize(c->stream));
-                    uint32_t nseq = 0;
-                    for (int i = 0; i < k; ++i) nseq += f2[i] == 2;
-                    fprintf(stderr, "[st k1] n=%llu uncertified=%u sequential-fallback=%u\n", (unsigned long long)n,
-                            hinfo[0], nseq);
+                    fprintf(stderr, "[st k1] n=%llu flagged=%u", (unsigned long long)n, hfl[0]);
+                    for (uint32_t f = 0; f < hfl[0] && f < (uint32_t)FF_MAX; ++f)
+                        fprintf(stderr, " c%u:members=%u,cands=%u,seq=%u", hfl[1 + f],
+                                fs[hfl[1 + f] + 1] - fs[hfl[1 + f]], hz[f], f2[hfl[1 + f]] == 2u ? 1u : 0u);
+                    fprintf(stderr, "\n");
                 }
                 mark(c, "k1.update");
                 continue;
@@ -2215,17 +2110,13 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
         }
         {
             KTimer kt(c, "k1.sum");
-            if (chunked) {
+            {
                 const unsigned gk = grid_for((uint64_t)k, 256, 1024);
                 chunk_list(c, start, k, ch_cnt, ch_first, chunks, acc);
                 hipLaunchKernelGGL(k_sum1d_chunks, dim3(maxch), dim3(SC_T), 0, c->stream, vals_s, chunks, ch_first + k,
                                    acc);
                 hipLaunchKernelGGL(k_sum1d_final, dim3(gk), dim3(256), 0, c->stream, acc, start, k, cen, seq_flag,
                                    emin_c, sabs_c);
-                ST_LAUNCH_CHECK();
-            } else {
-                hipLaunchKernelGGL(k_sum1d, dim3(k), dim3(256), 0, c->stream, vals_s, start, k, cen, seq_flag, emin_c,
-                                   sabs_c);
                 ST_LAUNCH_CHECK();
             }
             std::vector<uint32_t> f1;
@@ -2234,14 +2125,8 @@ void kmeans1d_loop(st_ctx *c, const float *pts, const float *const *dcols, uint6
                 f1.resize(k);
                 ST_HIP(hipMemcpy(f1.data(), seq_flag, 4 * k, hipMemcpyDeviceToHost));
             }
-            if (chunked) {
-                chunked_replay(c, vals_s, start, k, maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum,
-                               rp_total, rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr);
-            } else {
-                hipLaunchKernelGGL(k_sum1d_replay, dim3(k), dim3(RT), 0, c->stream, vals_s, start, seq_flag, emin_c,
-                                   sabs_c, cen, cand_buf);
-                ST_LAUNCH_CHECK();
-            }
+            chunked_replay(c, vals_s, start, k, maxch, chunks, ch_first, seq_flag, emin_c, sabs_c, rp_csum, rp_total,
+                           rp_ccnt, rp_cof, rp_ctot, cand_buf, cen, nullptr, nullptr);
             if (getenv("ST_DEBUG")) {
                 ST_HIP(hipStreamSynchronize(c->stream));
                 std::vector<uint32_t> f2(k);

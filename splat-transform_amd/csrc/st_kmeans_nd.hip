@@ -1849,6 +1849,28 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
                                         chalf_d, ntab, bnd,
                                         labels, thr, amb, dstate, pair_pts, pair_codes, hist)));
+    hipStream_t ss = nullptr;      // the fused fix-up's stream (side_ev[1] marks its end)
+    State *st_fix = nullptr;       // ... its exact-tie count
+    uint32_t *ties_fix = nullptr;  // ... and list
+    // joins the fused fix-up to this stream and appends its ties to the list the walk takes;
+    // returns their count
+    auto join_fix = [&](uint32_t nties) -> uint32_t {
+        if (!ss) return 0;
+        ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+        ss = nullptr;
+        uint32_t *hn = static_cast<uint32_t *>(pinned_slot(c, "kn.nfix", 4));
+        ST_HIP(hipMemcpyAsync(hn, &st_fix->ties, 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        if (*hn) ST_HIP(hipMemcpyAsync(ties + nties, ties_fix, 4 * (size_t)*hn, hipMemcpyDeviceToDevice, c->stream));
+        return *hn;
+    };
+    struct FixJoin {  // an exception must not leave the side stream running into the next call
+        hipStream_t &ss;
+        st_ctx *c;
+        ~FixJoin() {
+            if (ss) (void)hipStreamWaitEvent(c->stream, c->side_ev[1], 0);
+        }
+    } fix_join{ss, c};
     if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
         KTimer kt(c, "kn.fixrow");
@@ -1872,15 +1894,30 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
             auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
             auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+            // the fused fix-up runs on the side stream, beside the pair fix-up and the ambiguous
+            // points' collect / exact on this one: the three touch disjoint points (their labels
+            // were read by k_code_scatter above, before either side writes any).  Its exact ties go
+            // to their own list (kn.tiesfix, counted in its own State): the others' sum needs them
+            // apart, the walk takes both lists
+            ss = side_stream(c);
+            st_fix = wsT<State>(c, "kn.stfix", 1);
+            ties_fix = wsT<uint32_t>(c, "kn.tiesfix", n);
+            ST_HIP(hipMemsetAsync(st_fix, 0, sizeof(State), c->stream));
+            ST_HIP(hipEventRecord(c->side_ev[0], c->stream));
+            ST_HIP(hipStreamWaitEvent(ss, c->side_ev[0], 0));
             if (ld == 48)
-                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
+                                   pcnt);
             else if (ld == 24)
-                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
+                                   pcnt);
             else
-                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
+                                   pcnt);
+            ST_HIP(hipEventRecord(c->side_ev[1], ss));
             fz->valid = true;
             fz->ncodes = ncodes;
         } else if (ld == 48)
@@ -1902,8 +1939,7 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     const uint32_t npair = h->pairs;
-    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
-        fz->nties_fix = h->ties;
+    if (fz && fz->valid) {  // the fix-up's own ties (kn.tiesfix, counted when it joins), pairs, ambiguous
         fz->npair = npair;
         fz->namb = h->amb;
     }
@@ -1985,17 +2021,21 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
     }
+    uint32_t nties = h->ties;
+    const uint32_t nfix = join_fix(nties);
+    if (fz && fz->valid) fz->nties_fix = nfix;
+    nties += nfix;
     if (getenv("ST_DEBUG"))
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
-                (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
+                (unsigned long long)n, k, npair, namb, nties, h->overflow, sigma);
     // exact ties from k_fixrow, k_fixpair and k_exact (and candidate overflows): the KdTree walk
-    if (!walk_ties) return h->ties;
-    if (h->ties) {
+    if (!walk_ties) return nties;
+    if (nties) {
         KTimer kt(c, "kn.ties");
-        kd_resolve_ties(c, d, k, cen, aos, caos, ld, ties, h->ties, labels);
+        kd_resolve_ties(c, d, k, cen, aos, caos, ld, ties, nties, labels);
     }
     mark(c, "kn.exact");
-    return h->ties;
+    return nties;
 }
 }  // namespace
 
@@ -2010,7 +2050,7 @@ uint32_t others_sort(st_ctx *c, uint64_t n, int k, const NdFused &fz, const uint
     if (m) {
         hipLaunchKernelGGL(k_others_keys, dim3(grid_for(m, 256, 4096)), dim3(256), 0, c->stream,
                            wsT<uint32_t>(c, "kn.pairpts", n), fz.npair, wsT<uint32_t>(c, "kn.amb", n), fz.namb,
-                           wsT<uint32_t>(c, "kn.ties", n), fz.nties_fix, labels, okeys, ovals);
+                           wsT<uint32_t>(c, "kn.tiesfix", n), fz.nties_fix, labels, okeys, ovals);
         ST_LAUNCH_CHECK();
         int bits = 1;
         while ((1ull << bits) < (uint64_t)k) ++bits;

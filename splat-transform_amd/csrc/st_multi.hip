@@ -770,12 +770,14 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
     const bool side_on = !(sc && std::strcmp(sc, "0") == 0);
     Coll *bk = side_on ? co.side() : &co;
     const bool inline_coll = !side_on || bk->enqueues();
-    const hipStream_t cs = side_on ? side_stream(c) : c->stream;  // the side channel's stream
-    st_ctx *mc = c;  // rank 0: Morton order and placement
-    if (root && side_on) {
+    // the side context's stream carries the side channel's collectives and, on rank 0, the Morton
+    // order and placement behind them (the context's side stream is the N-D fix-up's)
+    st_ctx *mc = c;
+    if (side_on) {
         if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
         mc = c->aux;
     }
+    const hipStream_t cs = mc->stream;
     float *gx = nullptr, *gy = nullptr, *gz = nullptr;
     uint32_t *pos = nullptr, *gath = nullptr;
     if (root) {

@@ -672,7 +672,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         const uint32_t *h = (const uint32_t *)(hp + stage[j].hist);
         const double sel = vp8l::literal_bits(h) + vp8l::literal_bits(h + vp8l::kTabSize);
         const double raw = vp8l::literal_bits((const uint32_t *)(hp + stage[j].raw));
-        if (raw < 0.995 * sel && !getenv("ST_WEBP_NO_MODE0")) {
+        if (raw < 0.995 * sel) {
             forced[j] = 1;
             again = true;
         }
@@ -698,7 +698,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         }
         for (int i = 0; i < gw * gh && ngroups[j] == 1; ++i)
             if (flags[i]) ngroups[j] = CODE_GROUPS;
-        if (ngroups[j] > 1 && !getenv("ST_WEBP_ONE_GROUP")) {
+        if (ngroups[j] > 1) {
             vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, hist, ngroups[j], flags, GROUP_BITS, modes, hdr[j]);
         } else {  // one group: group 1's symbols (if any) join group 0
             ngroups[j] = 1;

@@ -174,7 +174,7 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
     same_bits(cent, ocent)
 
 
-K1_MODES = ['', 'ST_K1_FF_CHAIN', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX=0', 'ST_REPLAY_CAP=0',
+K1_MODES = ['', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX=0', 'ST_REPLAY_CAP=0',
             'ST_REPLAY_CAP=2']
 
 
@@ -190,9 +190,8 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch,
     """1-D k-means whose cluster sums fail the exactness certificate: clusters straddling 0
     hold tiny members, so the sequential f64 sum rounds -- a few events (the replay) or many
     (the sequential fallback).  mode: the iteration queued without read-backs, the flagged
-    clusters updated by the one-pass look-back kernel (default) or by the count / scan /
-    scatter / replay chain (ST_K1_FF_CHAIN); the flagged count read back each iteration
-    (ST_K1_SYNC), the flagged clusters' members gathered by the tile kernels (ST_K1_TILES),
+    clusters updated by the three-pass flagged update (default); the flagged count read back
+    each iteration (ST_K1_SYNC), the flagged clusters' members gathered by the tile kernels (ST_K1_TILES),
     every iteration's member sort (ST_K1_SORT), the queued run abandoned at the first flagged
     cluster and rerun synchronised (ST_K1_FF_MAX=0), or the replay capped at 0 / 2 candidates so
     that the sequential chain takes over (ST_REPLAY_CAP; ST_DEBUG's counts show that it did)."""
@@ -220,7 +219,7 @@ def test_cluster1d_uncertified_sums_vs_oracle(ctx, tiny_frac, mode, monkeypatch,
     assert np.array_equal(labels, olabels)
 
 
-@pytest.mark.parametrize('mode', ['', 'ST_K1_FF_CHAIN'])
+@pytest.mark.parametrize('mode', ['', 'ST_K1_SYNC'])
 @pytest.mark.parametrize('tiny_frac', [0.0, 2e-5, 0.02])
 def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac, mode, monkeypatch):
     """The sort-free 1-D iteration at a size where every accumulating workgroup takes several
@@ -242,7 +241,7 @@ def test_cluster1d_uncertified_many_tiles_vs_oracle(ctx, tiny_frac, mode, monkey
     assert np.array_equal(labels, olabels)
 
 
-@pytest.mark.parametrize('mode', ['', 'ST_K1_FF_CHAIN'])
+@pytest.mark.parametrize('mode', ['', 'ST_K1_SYNC'])
 def test_cluster1d_sorted_columns_vs_oracle(ctx, mode, monkeypatch):
     """Sorted columns (ascending, descending, ascending): every cluster's members are one
     contiguous run of points, so the flagged cluster straddling 0 fills a few hundred chunks
