@@ -326,16 +326,13 @@ PLY_ORDER = (['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [
              ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3'])
 
 
-def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2, split=False):
+def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
     """The CLI's work for `splat-transform in.ply out.sog` on this table: the step's table is
     written once as a binary little-endian 3DGS PLY (62 float properties, 248 B per splat,
     normals 0; untimed), then each timed rep reads the file into device columns
     (st_dev_ply_read: page cache -> pinned chunks -> HBM -> k_ply_cols), runs the same
     writeSog step, builds the .sog archive (WebP x7 + CRC + ZIP) and writes it to a file.
-    The archive must equal the in-memory step's byte for byte.  split=False: step and archive in
-    one call (st_dev_sog_bundle_step: the five textures ready before the SH k-means are encoded
-    beside it) and st_file_write; split=True: st_dev_sog then st_dev_sog_bundle_view, timed apart,
-    and one write(2)."""
+    The archive must equal the in-memory step's byte for byte."""
     import tempfile
 
     import numpy as np
@@ -365,20 +362,12 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2, split=False):
             table = {k: v for k, v in vc.items() if not k.startswith('n')}
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            if split:  # the step, then the container
-                meta, _ = ctx.dev_sog(table, iters, draws, tex)
-                t2 = time.perf_counter()
-                addr, size = ctx.dev_sog_bundle_view(meta, n, tex, 0, 0)
-            else:  # one call: the early textures encoded beside the SH k-means
-                meta, _, addr, size = ctx.dev_sog_bundle_step(table, iters, draws, tex)
-                t2 = time.perf_counter()
+            meta, _ = ctx.dev_sog(table, iters, draws, tex)
+            t2 = time.perf_counter()
+            addr, size = ctx.dev_sog_bundle_view(meta, n, tex, 0, 0)
             t3 = time.perf_counter()
-            if split:  # one write(2)
-                with open(dst, 'wb') as f:
-                    f.write((ctypes_char_array(size)).from_address(addr))
-            else:  # st_file_write: mapped, filled by several threads
-                import splat_hip
-                splat_hip.file_write(dst, addr, size)
+            with open(dst, 'wb') as f:
+                f.write((ctypes_char_array(size)).from_address(addr))
             t4 = time.perf_counter()
             if r:
                 times.append(t4 - t0)
@@ -389,10 +378,8 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2, split=False):
         ms = times[i] * 1e3
         return {'what': 'PLY file (page cache) -> device columns -> writeSog step -> .sog archive -> file, rank 0',
                 'ply_bytes': file_bytes, 'sog_bytes': size, 'ms': ms, 'Msplats_per_s': n / ms / 1e3,
-                'split_ms': dict(zip(('ply_ingest', 'sog_step' if split else 'sog_step_with_container',
-                                      'container' if split else 'container_rest', 'file_write'),
+                'split_ms': dict(zip(('ply_ingest', 'sog_step', 'container', 'file_write'),
                                      (x * 1e3 for x in parts[i]))),
-                'one_call': not split,
                 'reps': reps, 'archive_equals_in_memory_step': same}
     finally:
         for f in (src, dst):
@@ -868,7 +855,6 @@ def main(args):
     progress('end-to-end file run')
     if not sharded and not args.no_e2e:
         e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive)
-        e2e['separate_calls'] = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive, reps=1, split=True)
     paths = None
     progress('config-3 stage table')
     if not sharded and not args.no_paths:

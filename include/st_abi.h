@@ -451,10 +451,6 @@ int st_dev_crc32(st_ctx *ctx, const uint8_t *data, uint64_t n, uint32_t crc_in, 
 int st_zip_store(const char *const *names, const uint8_t *const *data, const uint64_t *sizes,
                  const uint32_t *crcs, int32_t count, uint16_t dos_time, uint16_t dos_date,
                  uint8_t **out, uint64_t *out_size);
-/* host: writes n bytes to the file at path (created or truncated): the file is sized, mapped and
- * filled by up to 8 threads (fs.writeFile of the .sog archive, index.ts:101-154, without the
- * single-core copy of write(2)); ST_ERR_ARG if it cannot be opened */
-int st_file_write(const char *path, const void *data, uint64_t n);
 /* host: meta.json text of writeSog (JS number formatting); *out malloc'd, NUL-terminated */
 int st_sog_meta_json(const st_sog_meta *meta, uint64_t count, char **out, uint64_t *out_size);
 /* the .sog archive of textures resident on the device (st_dev_sog's outputs):
@@ -466,15 +462,6 @@ int st_dev_sog_bundle(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, cons
  * until the next bundle call on ctx; no copy) -- what a writer hands to write(2) */
 int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
                            uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *size);
-/* writeSog of a device table plus its .sog archive in one call (write-sog.ts:110-370 with the
- * ZipWriter output, index.ts's `out.sog`): the five textures complete before the SH k-means
- * (means_l, means_u, quats, scales, sh0) are WebP-encoded on a side context while it runs, so
- * the container adds only the last two textures, the CRCs and the ZIP layout.  Textures are
- * written to `tex` (device) as st_dev_sog; *out views the context's pinned archive (valid until
- * the next bundle call on this context). */
-int st_dev_sog_bundle_step(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
-                           uint64_t *used, st_sog_meta *meta, const st_sog_textures *tex, uint16_t dos_time,
-                           uint16_t dos_date, const uint8_t **out, uint64_t *size);
 /* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */
 int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                   uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);

@@ -304,13 +304,7 @@ int sog_chain(st_ctx *c, Load load, const st_action *actions, int32_t nactions, 
         uint64_t tex, cbytes;
         const st_sog_textures dt = sog_textures(c, ch.n, C, &tex, &cbytes);
         st_sog_meta meta{};
-        const uint8_t *view = nullptr;
-        uint64_t nb = 0;
-        // the .sog output: the writeSog step with its container's early textures encoded beside
-        // the SH k-means (sog_bundle_step); the textures output: the step alone
-        const uint64_t u = tex_out ? sog_tdev(c, ch.typed(), iters, draws, ndraws, &meta, &dt)
-                                   : sog_bundle_step(c, nullptr, ch.typed(), iters, draws, ndraws, &meta, dt,
-                                                     dos_time, dos_date, &view, &nb);
+        const uint64_t u = sog_tdev(c, ch.typed(), iters, draws, ndraws, &meta, &dt);
         if (tex_out) {
             std::vector<HostXfer> down;
             for (auto pr : {std::make_pair(tex_out->means_l, dt.means_l), std::make_pair(tex_out->means_u, dt.means_u),
@@ -327,6 +321,9 @@ int sog_chain(st_ctx *c, Load load, const st_action *actions, int32_t nactions, 
             staged_d2h(c, down);
             *tex_meta = meta;
         } else {
+            const uint8_t *view;
+            uint64_t nb;
+            sog_bundle_dev(c, meta, ch.n, dt, dos_time, dos_date, &view, &nb);
             uint8_t *buf = (uint8_t *)std::malloc(nb);
             ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
             std::memcpy(buf, view, nb);

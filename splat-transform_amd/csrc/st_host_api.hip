@@ -369,10 +369,10 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
             dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
         }
         st_sog_meta meta{};
+        const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, &meta, &dt);
         const uint8_t *view;
         uint64_t nb;
-        const uint64_t u = sog_bundle_step(c, &d.t, nullptr, iters, draws, ndraws, &meta, dt, dos_time, dos_date, &view,
-                                           &nb);
+        sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, &view, &nb);
         uint8_t *buf = (uint8_t *)std::malloc(nb);
         ST_REQUIRE(buf, ST_ERR_NOMEM, "sog bundle: host allocation failed");
         std::memcpy(buf, view, nb);

@@ -75,8 +75,6 @@ struct Workspace {
     void release();
 };
 
-struct EarlyWebp;  // st_webp.h
-
 struct StageTimer {
     hipEvent_t ev;
     std::string name;
@@ -143,9 +141,6 @@ struct st_ctx {
     std::vector<hipEvent_t> event_pool;
     // side context on the same device (multi-GPU writeSog: rank 0's Morton order runs there)
     st_ctx *aux = nullptr;
-    // set by sog_bundle_step around its sog call: the container's first five textures are
-    // encoded on the side context while the SH k-means runs (st_webp.h EarlyWebp)
-    st::EarlyWebp *early = nullptr;
     // st_ctx_set_verify: snapshot of the last N-D k-means (prev / final centroids, labels)
     bool verify = false;
     int vf_d = 0, vf_k = 0;

@@ -155,14 +155,8 @@ __device__ inline float norm_reach(float pn, float t) {
 //     table's residual at R instead of the palette's cm / dcm -- one outlying centroid no longer
 //     widens every point's window.
 // With R1 >= cb and R >= cm this is the palette-wide window of round 3.
-struct WinR {
-    float W;    // the window against every other tile-half
-    float eb;   // the best row's error bound
-    float sb2;  // its f64-rounding term rel (pn + |c1|)^2
-    float cr;   // the largest norm a competitor can have (<= cm)
-};
-__device__ inline WinR wbound_r(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float ntab_scale,
-                                const float *__restrict__ ntab, float m1u) {
+__device__ inline float wbound_r(const Bound &B, float pn, float dp, float cb, float dcb, float cm, float ntab_scale,
+                                 const float *__restrict__ ntab, float m1u) {
     const float e0 = err_bound(B, pn, dp, cb, dcb);
     const float c1 = fminf(norm_reach(pn, m1u + e0 * 1.0001f), cb);
     const float eb = err_bound(B, pn, dp, c1, fminf(dcb, ntab[norm_bucket(c1, ntab_scale)]));
@@ -171,17 +165,13 @@ __device__ inline WinR wbound_r(const Bound &B, float pn, float dp, float cb, fl
     const float cr = fminf(norm_reach(pn, t), cm);
     const float dcr = ntab[norm_bucket(cr, ntab_scale)];
     const float sr = pn + cr;
-    return WinR{(eb + err_bound(B, pn, dp, cr, dcr) + B.rel * (sb * sb + sr * sr)) * 1.0001f, eb, B.rel * sb * sb, cr};
+    return (eb + err_bound(B, pn, dp, cr, dcr) + B.rel * (sb * sb + sr * sr)) * 1.0001f;
 }
 
-// the window against one given tile-half (largest norm c2, residual dc2): its rows compete with
-// the norm bound of wbound_r too
-__device__ inline float wbound_half(const Bound &B, const WinR &w, float pn, float dp, float c2, float dc2,
-                                    float ntab_scale, const float *__restrict__ ntab) {
-    const float cn = fminf(w.cr, c2);
-    const float dn = fminf(dc2, ntab[norm_bucket(cn, ntab_scale)]);
-    const float s2 = pn + cn;
-    return (w.eb + err_bound(B, pn, dp, cn, dn) + w.sb2 + B.rel * s2 * s2) * 1.0001f;
+// the window between two given tile-halves (largest norms ca, cb and residuals dca, dcb)
+__device__ inline float wbound_pair(const Bound &B, float pn, float dp, float ca, float dca, float cb, float dcb) {
+    const float s = pn + fmaxf(ca, cb);
+    return (err_bound(B, pn, dp, ca, dca) + err_bound(B, pn, dp, cb, dcb) + 2.0f * B.rel * s * s) * 1.0001f;
 }
 
 // largest norm and largest rounding-residual norm (rounded up) among the 16 rows of each tile-half
@@ -586,8 +576,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float pn = pnorm[p], dp = pdn[p];
-            const WinR wr = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
-            const float W = wr.W;
+            const float W = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
                 if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
@@ -595,7 +584,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
                 // every candidate lies in the two best tile-halves.  Only the second one competes
                 // with the first, so its own largest norm bounds its rows' error instead of the
                 // palette's (chalf[code2] <= cm): often that already decides the point
-                const float W2 = wbound_half(bnd, wr, pn, dp, chalf[code2], chalf_d[code2], ntab_scale, ntab);
+                const float W2 = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], chalf[code2], chalf_d[code2]);
                 if (nm2 > nm1 + W2 + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                     labels[p] = code1;
                     if (code_hist) atomicAdd(&code_hist[code1], 1u);
@@ -1849,28 +1838,6 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
                                         chalf_d, ntab, bnd,
                                         labels, thr, amb, dstate, pair_pts, pair_codes, hist)));
-    hipStream_t ss = nullptr;      // the fused fix-up's stream (side_ev[1] marks its end)
-    State *st_fix = nullptr;       // ... its exact-tie count
-    uint32_t *ties_fix = nullptr;  // ... and list
-    // joins the fused fix-up to this stream and appends its ties to the list the walk takes;
-    // returns their count
-    auto join_fix = [&](uint32_t nties) -> uint32_t {
-        if (!ss) return 0;
-        ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
-        ss = nullptr;
-        uint32_t *hn = static_cast<uint32_t *>(pinned_slot(c, "kn.nfix", 4));
-        ST_HIP(hipMemcpyAsync(hn, &st_fix->ties, 4, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-        if (*hn) ST_HIP(hipMemcpyAsync(ties + nties, ties_fix, 4 * (size_t)*hn, hipMemcpyDeviceToDevice, c->stream));
-        return *hn;
-    };
-    struct FixJoin {  // an exception must not leave the side stream running into the next call
-        hipStream_t &ss;
-        st_ctx *c;
-        ~FixJoin() {
-            if (ss) (void)hipStreamWaitEvent(c->stream, c->side_ev[1], 0);
-        }
-    } fix_join{ss, c};
     if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
         KTimer kt(c, "kn.fixrow");
@@ -1894,30 +1861,15 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
             auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
             auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
-            // the fused fix-up runs on the side stream, beside the pair fix-up and the ambiguous
-            // points' collect / exact on this one: the three touch disjoint points (their labels
-            // were read by k_code_scatter above, before either side writes any).  Its exact ties go
-            // to their own list (kn.tiesfix, counted in its own State): the others' sum needs them
-            // apart, the walk takes both lists
-            ss = side_stream(c);
-            st_fix = wsT<State>(c, "kn.stfix", 1);
-            ties_fix = wsT<uint32_t>(c, "kn.tiesfix", n);
-            ST_HIP(hipMemsetAsync(st_fix, 0, sizeof(State), c->stream));
-            ST_HIP(hipEventRecord(c->side_ev[0], c->stream));
-            ST_HIP(hipStreamWaitEvent(ss, c->side_ev[0], 0));
             if (ld == 48)
-                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
-                                   pcnt);
+                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             else if (ld == 24)
-                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
-                                   pcnt);
+                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             else
-                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, ss, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties_fix, st_fix, psum, pabs, pemin,
-                                   pcnt);
-            ST_HIP(hipEventRecord(c->side_ev[1], ss));
+                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
+                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             fz->valid = true;
             fz->ncodes = ncodes;
         } else if (ld == 48)
@@ -1939,7 +1891,8 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ST_HIP(hipStreamSynchronize(c->stream));
     const uint32_t npair = h->pairs;
-    if (fz && fz->valid) {  // the fix-up's own ties (kn.tiesfix, counted when it joins), pairs, ambiguous
+    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
+        fz->nties_fix = h->ties;
         fz->npair = npair;
         fz->namb = h->amb;
     }
@@ -2021,21 +1974,17 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
     }
-    uint32_t nties = h->ties;
-    const uint32_t nfix = join_fix(nties);
-    if (fz && fz->valid) fz->nties_fix = nfix;
-    nties += nfix;
     if (getenv("ST_DEBUG"))
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
-                (unsigned long long)n, k, npair, namb, nties, h->overflow, sigma);
+                (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
     // exact ties from k_fixrow, k_fixpair and k_exact (and candidate overflows): the KdTree walk
-    if (!walk_ties) return nties;
-    if (nties) {
+    if (!walk_ties) return h->ties;
+    if (h->ties) {
         KTimer kt(c, "kn.ties");
-        kd_resolve_ties(c, d, k, cen, aos, caos, ld, ties, nties, labels);
+        kd_resolve_ties(c, d, k, cen, aos, caos, ld, ties, h->ties, labels);
     }
     mark(c, "kn.exact");
-    return nties;
+    return h->ties;
 }
 }  // namespace
 
@@ -2050,7 +1999,7 @@ uint32_t others_sort(st_ctx *c, uint64_t n, int k, const NdFused &fz, const uint
     if (m) {
         hipLaunchKernelGGL(k_others_keys, dim3(grid_for(m, 256, 4096)), dim3(256), 0, c->stream,
                            wsT<uint32_t>(c, "kn.pairpts", n), fz.npair, wsT<uint32_t>(c, "kn.amb", n), fz.namb,
-                           wsT<uint32_t>(c, "kn.tiesfix", n), fz.nties_fix, labels, okeys, ovals);
+                           wsT<uint32_t>(c, "kn.ties", n), fz.nties_fix, labels, okeys, ovals);
         ST_LAUNCH_CHECK();
         int bits = 1;
         while ((1ull << bits) < (uint64_t)k) ++bits;

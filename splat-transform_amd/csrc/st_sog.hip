@@ -14,7 +14,6 @@
 #include "st_jsmath.h"
 #include "st_kmeans.h"
 #include "st_typed.h"
-#include "st_webp.h"
 
 namespace st {
 namespace {
@@ -557,31 +556,6 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
                            (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
-    // sog_bundle_step: the container's first five textures are complete here; they are encoded
-    // (WebP + CRC) on the side context from its own host thread while the SH k-means runs
-    std::exception_ptr err_e;
-    std::thread early_th;
-    if (c->early) {
-        hipEvent_t ev;
-        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ST_HIP(hipEventRecord(ev, c->stream));
-        ST_HIP(hipStreamWaitEvent(aux->stream, ev, 0));
-        ST_HIP(hipEventDestroy(ev));
-        early_th = std::thread([&] {
-            try {
-                use_device(aux);
-                early_webp(aux, *meta, *out, c->early);
-            } catch (...) {
-                err_e = std::current_exception();
-            }
-        });
-    }
-    struct Joiner3 {
-        std::thread &th;
-        ~Joiner3() {
-            if (th.joinable()) th.join();
-        }
-    } joiner3{early_th};
 
     meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
     if (C > 0) {
@@ -628,8 +602,6 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
         mark(c, "sog.shn");
     }
-    if (early_th.joinable()) early_th.join();
-    if (err_e) std::rethrow_exception(err_e);
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;
 }

@@ -24,29 +24,11 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs);
 void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const uint32_t *crc_in, int cnt,
                uint32_t *crcs);
 
-// The container's first five textures (means_l, means_u, quats, scales, sh0: complete before
-// the SH k-means starts) encoded on another context while the k-means runs: sog_impl fills it
-// when c->early is set (sog_bundle_step), sog_bundle_dev takes those five from it.
-struct EarlyWebp {
-    st_ctx *ctx = nullptr;             // the context whose workspace holds the outputs
-    WebpJob jobs[5] = {};
-    uint32_t crc[5] = {};
-    const uint8_t *src[5] = {};        // the textures they encode
-    bool ready = false;
-};
-void early_webp(st_ctx *side, const st_sog_meta &meta, const st_sog_textures &tex, EarlyWebp *e);
-
 // the whole .sog archive (WebP-encoded textures + meta.json, zip-writer.ts layout) of
 // textures resident on the device, in the context's pinned archive buffer (valid until
-// the next bundle call on this context); early: the first five already encoded (same textures)
+// the next bundle call on this context)
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
-                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size,
-                    const EarlyWebp *early = nullptr);
-// writeSog + its .sog archive in one call, the container's early textures encoded beside the
-// SH k-means (float32 tables: sog_dev; typed: sog_tdev)
-uint64_t sog_bundle_step(st_ctx *c, const st_table *t, const st_ttable *tt, int iters, const double *draws,
-                         uint64_t ndraws, st_sog_meta *meta, const st_sog_textures &tex, uint16_t dos_time,
-                         uint16_t dos_date, const uint8_t **out, uint64_t *out_size);
+                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size);
 
 // ---- host: the .sog container (st_zip.cpp) ----------------------------------
 // JSON text of a JS number (Number::toString as JSON.stringify emits it; non-finite -> null)

@@ -784,31 +784,8 @@ void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const u
 
 namespace st {
 
-void early_webp(st_ctx *side, const st_sog_meta &meta, const st_sog_textures &tex, EarlyWebp *e) {
-    const uint8_t *srcs[5] = {tex.means_l, tex.means_u, tex.quats, tex.scales, tex.sh0};
-    for (int i = 0; i < 5; ++i) {
-        ST_REQUIRE(srcs[i], ST_ERR_ARG, "sog bundle: texture missing");
-        const uint64_t cap = webp_max_size(meta.width, meta.height);
-        e->jobs[i] = {srcs[i], meta.width, meta.height, meta.width * 4, wsT<uint8_t>(side, "eb.o" + std::to_string(i), cap),
-                      cap, 0};
-        e->src[i] = srcs[i];
-    }
-    webp_encode_dev(side, e->jobs, 5);
-    const uint8_t *ptrs[5];
-    uint64_t lens[5];
-    uint32_t zero[5] = {0, 0, 0, 0, 0};
-    for (int i = 0; i < 5; ++i) {
-        ptrs[i] = e->jobs[i].out;
-        lens[i] = e->jobs[i].size;
-    }
-    crc32_dev(side, ptrs, lens, zero, 5, e->crc);  // synchronises the side stream
-    e->ctx = side;
-    e->ready = true;
-}
-
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
-                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size,
-                    const EarlyWebp *early) {
+                    uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size) {
     // entries in write-sog.ts order (:186-187, :239, :251, :268, :335, :348, :364)
     struct Img {
         const char *name;
@@ -825,22 +802,14 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
         imgs.push_back({"shN_labels.webp", tex.shn_labels, meta.width, meta.height});
     }
     const int ni = (int)imgs.size();
-    // the first five may come encoded (with their CRCs) from the early pass over the same textures
-    int ne = early && early->ready ? 5 : 0;
-    for (int i = 0; i < ne; ++i)
-        if (early->src[i] != imgs[i].rgba || early->jobs[i].w != imgs[i].w || early->jobs[i].h != imgs[i].h) ne = 0;
     std::vector<WebpJob> jobs(ni);
     for (int i = 0; i < ni; ++i) {
         ST_REQUIRE(imgs[i].rgba, ST_ERR_ARG, std::string("sog bundle: texture missing for ") + imgs[i].name);
-        if (i < ne) {
-            jobs[i] = early->jobs[i];
-            continue;
-        }
         const uint64_t cap = webp_max_size(imgs[i].w, imgs[i].h);
         jobs[i] = {imgs[i].rgba, imgs[i].w, imgs[i].h, imgs[i].w * 4,
                    wsT<uint8_t>(c, "sb.o" + std::to_string(i), cap), cap, 0};
     }
-    if (ni > ne) webp_encode_dev(c, jobs.data() + ne, ni - ne);
+    webp_encode_dev(c, jobs.data(), ni);
     const std::string mj = sog_meta_json(meta, count);
     std::vector<ZipEntry> es;
     for (int i = 0; i < ni; ++i) es.push_back({imgs[i].name, jobs[i].size, 0});
@@ -859,34 +828,18 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
             ST_HIP(hipMemcpyAsync(buf + off[i], jobs[i].out, jobs[i].size, hipMemcpyDeviceToHost, c->stream));
     std::vector<const uint8_t *> ptrs;
     std::vector<uint64_t> lens;
-    for (int i = ne; i < ni; ++i) {
-        ptrs.push_back(jobs[i].out);
-        lens.push_back(jobs[i].size);
+    for (auto &j : jobs) {
+        ptrs.push_back(j.out);
+        lens.push_back(j.size);
     }
     ptrs.push_back(dmeta);
     lens.push_back(mj.size());
     std::vector<uint32_t> zero(ptrs.size(), 0), crcs(ptrs.size(), 0);
     crc32_dev(c, ptrs.data(), lens.data(), zero.data(), (int)ptrs.size(), crcs.data());  // synchronises
-    for (int i = 0; i < ne; ++i) es[i].crc = early->crc[i];
-    for (size_t i = ne; i < es.size(); ++i) es[i].crc = crcs[i - ne];
+    for (size_t i = 0; i < es.size(); ++i) es[i].crc = crcs[i];
     zip_write(es, dos_time, dos_date, buf, off.data());
     *out = buf;
     *out_size = total;
-}
-
-uint64_t sog_bundle_step(st_ctx *c, const st_table *t, const st_ttable *tt, int iters, const double *draws,
-                         uint64_t ndraws, st_sog_meta *meta, const st_sog_textures &tex, uint16_t dos_time,
-                         uint16_t dos_date, const uint8_t **out, uint64_t *out_size) {
-    EarlyWebp e;
-    struct Reset {
-        st_ctx *c;
-        ~Reset() { c->early = nullptr; }
-    } reset{c};
-    c->early = &e;
-    const uint64_t u = t ? sog_dev(c, t, iters, draws, ndraws, meta, &tex) : sog_tdev(c, tt, iters, draws, ndraws, meta, &tex);
-    c->early = nullptr;
-    sog_bundle_dev(c, *meta, t ? t->n : tt->n, tex, dos_time, dos_date, out, out_size, &e);
-    return u;
 }
 
 }  // namespace st
@@ -894,18 +847,6 @@ uint64_t sog_bundle_step(st_ctx *c, const st_table *t, const st_ttable *tt, int 
 using namespace st;
 
 extern "C" {
-
-int st_dev_sog_bundle_step(st_ctx *c, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
-                           uint64_t *used, st_sog_meta *meta, const st_sog_textures *tex, uint16_t dos_time,
-                           uint16_t dos_date, const uint8_t **out, uint64_t *size) {
-    return guard([&] {
-        ST_REQUIRE(c && table && draws && meta && tex && out && size, ST_ERR_ARG, "NULL argument");
-        use_device(c);
-        const uint64_t u = sog_bundle_step(c, table, nullptr, iters, draws, ndraws, meta, *tex, dos_time, dos_date,
-                                           out, size);
-        if (used) *used = u;
-    });
-}
 
 uint64_t st_webp_max_size(int32_t width, int32_t height) {
     if (width < 1 || height < 1 || width > 16384 || height > 16384) return 0;

@@ -9,17 +9,10 @@
 //   zip_write      serialize/zip-writer.ts:35-135 (flags 0x808: CRC and sizes in a data
 //                  descriptor after the data; method 0; DOS time/date of the writer's
 //                  construction; central directory; end record without zip64)
-#include <fcntl.h>
-#include <sys/mman.h>
-#include <unistd.h>
-
-#include <algorithm>
-#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
 
 #include "st_webp.h"
 
@@ -216,42 +209,6 @@ int st_zip_store(const char *const *names, const uint8_t *const *data, const uin
             if (sizes[i]) std::memcpy(buf + off[i], data[i], sizes[i]);
         *out = buf;
         *out_size = total;
-    });
-}
-
-// the output file in one go: write(2) of one buffer into a file takes the inode's lock and
-// copies on one core (2.5-3.5 GB/s into the page cache); here the file is sized, mapped and
-// filled by up to 8 threads (their page faults and copies run in parallel), then unmapped.
-// A file system that cannot map it gets plain writes.
-int st_file_write(const char *path, const void *data, uint64_t n) {
-    return guard([&] {
-        ST_REQUIRE(path && (data || n == 0), ST_ERR_ARG, "NULL argument");
-        const int fd = open(path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-        ST_REQUIRE(fd >= 0, ST_ERR_ARG, std::string("open ") + path + ": " + std::strerror(errno));
-        struct Closer {
-            int fd;
-            ~Closer() { close(fd); }
-        } closer{fd};
-        if (n == 0) return;
-        void *map = MAP_FAILED;
-        if (ftruncate(fd, (off_t)n) == 0) map = mmap(nullptr, n, PROT_WRITE, MAP_SHARED, fd, 0);
-        if (map == MAP_FAILED) {
-            if (ftruncate(fd, 0) != 0) {}
-            const char *p = static_cast<const char *>(data);
-            for (uint64_t done = 0; done < n;) {
-                const ssize_t w = write(fd, p + done, (size_t)std::min<uint64_t>(n - done, 1ull << 30));
-                ST_REQUIRE(w > 0 || errno == EINTR, ST_ERR_INTERNAL, std::string("write ") + path + ": " + std::strerror(errno));
-                if (w > 0) done += (uint64_t)w;
-            }
-            return;
-        }
-        const uint64_t piece = std::max<uint64_t>(8ull << 20, (n + 7) / 8);
-        std::vector<std::thread> th;
-        for (uint64_t a = 0; a < n; a += piece)
-            th.emplace_back([=] { std::memcpy(static_cast<char *>(map) + a, static_cast<const char *>(data) + a,
-                                              (size_t)std::min(piece, n - a)); });
-        for (auto &t : th) t.join();
-        ST_REQUIRE(munmap(map, n) == 0, ST_ERR_INTERNAL, std::string("munmap ") + path + ": " + std::strerror(errno));
     });
 }
 

@@ -110,7 +110,7 @@ EXPORTS = [
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
-    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_dev_sog_bundle_step', 'st_file_write', 'st_sog_bundle', 'st_free',
+    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
@@ -230,11 +230,6 @@ def get_devices():
     n = ctypes.c_int32()
     check(lib().st_get_devices(ctypes.byref(n)))
     return n.value
-
-
-def file_write(path, addr, size):
-    """st_file_write: `size` bytes at host address `addr` into the file at path"""
-    check(lib().st_file_write(os.fsencode(path), ctypes.c_void_p(addr), ctypes.c_uint64(size)))
 
 
 def comm_unique_id():
@@ -778,22 +773,6 @@ class Context:
                                            ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(out),
                                            ctypes.byref(size)))
         return out.value, size.value
-
-    def dev_sog_bundle_step(self, cols, iters, draws, tex, dos_time=0, dos_date=0):
-        """st_dev_sog_bundle_step: writeSog of device columns into tex (as dev_sog) and its .sog
-        archive, the early textures encoded beside the SH k-means: (meta, used, address, size)
-        of the context's pinned archive"""
-        t = make_table(cols)
-        out = SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
-                            ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
-        meta = SogMeta()
-        used = ctypes.c_uint64(0)
-        addr, size = ctypes.c_void_p(), ctypes.c_uint64(0)
-        check(lib().st_dev_sog_bundle_step(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws),
-                                           ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
-                                           ctypes.byref(out), ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date),
-                                           ctypes.byref(addr), ctypes.byref(size)))
-        return meta, used.value, addr.value, size.value
 
     def dev_sog_bundle(self, meta, count, tex, dos_time, dos_date):
         """the .sog archive bytes of device textures (dict as for dev_sog) and their SogMeta"""

@@ -155,33 +155,3 @@ def test_sog_bundle_device_view_matches_copy(ctx):
     assert ctypes.string_at(addr, size) == z
     host, _ = ctx.sog_bundle(g.table('b_sh1_in_'), c['iters'], draws, t, d)
     assert host == z
-    # writeSog + archive in one call (the early textures encoded beside the SH k-means)
-    tex2 = {k: torch.empty_like(v) for k, v in tex.items()}
-    meta2, used2, addr2, size2 = ctx.dev_sog_bundle_step(cols, c['iters'], draws, tex2, t, d)
-    assert used2 == used and ctypes.string_at(addr2, size2) == z
-    assert all(torch.equal(tex[k], tex2[k]) for k in tex)
-
-
-@pytest.mark.parametrize('bands', [0, 3])
-def test_sog_bundle_step_equals_separate_calls(ctx, bands):
-    """st_dev_sog_bundle_step (the five early textures WebP-encoded on a side context during the
-    SH k-means) writes the archive st_dev_sog + st_dev_sog_bundle_view write, byte for byte"""
-    import ctypes
-    n = 200_000
-    g = torch.Generator(device='cuda')
-    g.manual_seed(bands + 5)
-    names = ['x', 'y', 'z', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity', 'scale_0', 'scale_1', 'scale_2',
-             'rot_0', 'rot_1', 'rot_2', 'rot_3'] + [f'f_rest_{i}' for i in range(45 if bands == 3 else 0)]
-    cols = {k: torch.randn(n, generator=g, device='cuda') * (0.1 if k.startswith('f_rest') else 1.0) for k in names}
-    C = 15 if bands == 3 else 0
-    W, H, pal, cw, ch = sh.sog_geometry(n, C)
-    u8 = dict(device='cuda', dtype=torch.uint8)
-    tex = {k: torch.empty(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels')}
-    tex['shN_centroids'] = torch.empty(max(cw * ch, 1) * 4, **u8)
-    draws = np.random.default_rng(9).random(1 << 18)
-    meta, used = ctx.dev_sog(cols, 4, draws, tex)
-    addr, size = ctx.dev_sog_bundle_view(meta, n, tex, 7, 9)
-    want = ctypes.string_at(addr, size)
-    meta2, used2, addr2, size2 = ctx.dev_sog_bundle_step(cols, 4, draws, tex, 7, 9)
-    assert used2 == used and meta2.sh_bands == meta.sh_bands
-    assert ctypes.string_at(addr2, size2) == want
