@@ -769,7 +769,9 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
     const char *sc = getenv("ST_SIDE_CHANNEL");
     const bool side_on = !(sc && std::strcmp(sc, "0") == 0);
     Coll *bk = side_on ? co.side() : &co;
-    const bool inline_coll = !side_on || bk->enqueues();
+    // ST_SIDE_INLINE=1 (test hook): the RCCL issue order on a host transport -- the side channel's
+    // calls from this thread at the same program points, the worker only for rank 0's ordering
+    const bool inline_coll = !side_on || bk->enqueues() || getenv("ST_SIDE_INLINE");
     // the side context's stream carries the side channel's collectives and, on rank 0, the Morton
     // order and placement behind them (the context's side stream is the N-D fix-up's)
     st_ctx *mc = c;

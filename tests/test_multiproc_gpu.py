@@ -111,6 +111,12 @@ def test_small_slots_and_side_delays(tmp_path, ref):
           ref(N))
 
 
+def test_rccl_issue_order_over_shared_memory(tmp_path, ref):
+    """ST_SIDE_INLINE=1: the side channel's gathers issued from the main thread at the fixed
+    program points RCCL uses (the worker only orders and places on rank 0), across processes"""
+    check(*run_job(tmp_path, [0, N // 4, N * 2 // 3, N], env={'ST_SIDE_INLINE': '1'}), ref(N))
+
+
 def test_side_channel_off(tmp_path, ref):
     """ST_SIDE_CHANNEL=0 (the launcher's fallback): every exchange on the main channel and thread"""
     check(*run_job(tmp_path, [0, N // 2, N], env={'ST_SIDE_CHANNEL': '0'}), ref(N))
