@@ -536,7 +536,29 @@ class Context:
             pass
 
     def set_stream(self, stream_handle):
+        """run on a caller-owned hipStream_t.  Handle 0 is refused: torch's legacy default stream
+        has handle 0, which the C ABI reads as NULL = the context's own (non-blocking) stream, so
+        the library would silently stop ordering against the caller's torch work."""
+        if not stream_handle:
+            raise ValueError('set_stream(0): handle 0 selects the context\'s own stream, not the legacy '
+                             'default stream; use bind_torch_stream() or use_own_stream()')
         check(lib().st_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def use_own_stream(self):
+        check(lib().st_ctx_set_stream(self.h, None))
+
+    def bind_torch_stream(self, device):
+        """one real stream for the library and the caller's torch work on `device`: torch's
+        current stream when it is not the legacy default stream, else a new stream made
+        current, ordered after what the default stream already holds.  Returns the torch stream."""
+        import torch
+        s = torch.cuda.current_stream(device)
+        if s.cuda_stream == 0:
+            prev, s = s, torch.cuda.Stream(device)
+            s.wait_stream(prev)  # work already queued on the default stream comes first
+            torch.cuda.set_stream(s)
+        self.set_stream(s.cuda_stream)
+        return s
 
     def synchronize(self):
         check(lib().st_ctx_synchronize(self.h))

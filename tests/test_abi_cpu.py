@@ -80,6 +80,16 @@ def test_context_without_gpu_fails_loudly(L):
         sh.Context(0)
 
 
+def test_set_stream_refuses_handle_zero():
+    """torch's legacy default stream has handle 0, which the C ABI reads as NULL (the context's own
+    non-blocking stream): the wrapper refuses it rather than silently unordering the library
+    against the caller's torch work (a race found when the inputs were made on the default stream)"""
+    c = object.__new__(sh.Context)
+    for h in (0, None):
+        with pytest.raises(ValueError, match='own stream'):
+            c.set_stream(h)
+
+
 def _get_devices_with_env(value):
     """st_get_devices in a fresh process with ST_NUM_GPUS set (the switch applies once per process)"""
     import subprocess

@@ -134,13 +134,13 @@ def _single_c1d(q, n, seed, iters, cap):
         os.environ['ST_REPLAY_CAP'] = str(cap)
     import splat_hip as sh
     dev = torch.device('cuda', 0)
+    ctx = sh.Context(0)
+    ctx.bind_torch_stream(dev)  # before the inputs are made: they are ordered on the same stream
     full = _adversarial_1d(n, seed)
     cols = [torch.from_numpy(c).to(dev) for c in full]
     cb = torch.empty(256, dtype=torch.float32, device=dev)
     lab = torch.empty(3 * n, dtype=torch.uint8, device=dev)
     draws = np.random.default_rng(seed + 1).random(1 << 16)
-    ctx = sh.Context(0)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     used = ctx.dev_cluster1d(cols, iters, draws, cb, lab)
     torch.cuda.synchronize()
     q.put(dict(cb=cb.cpu().numpy(), lab=lab.cpu().numpy().reshape(3, n), used=used))
@@ -210,6 +210,8 @@ def test_multi_rank_write_sog_matches_single_device(backend, world, C, empty):
         assert p.exitcode == 0
 
     dev = torch.device('cuda', 0)
+    ctx = sh.Context(0)
+    ctx.bind_torch_stream(dev)  # before the inputs are made: they are ordered on the same stream
     full = _table(n, seed, C)
     cols = {k: torch.from_numpy(v).to(dev) for k, v in full.items()}
     W, H, pal, cw, ch = sh.sog_geometry(n, C)
@@ -219,8 +221,6 @@ def test_multi_rank_write_sog_matches_single_device(backend, world, C, empty):
     if C:
         tex['shN_centroids'] = torch.zeros(cw * ch * 4, **u8)
     draws = np.random.default_rng(seed + 1).random(1 << 20)
-    ctx = sh.Context(0)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     meta, used = ctx.dev_sog(cols, iters, draws, tex)
     torch.cuda.synchronize()
     assert res['used'] == used

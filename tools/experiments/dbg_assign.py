@@ -25,7 +25,7 @@ n = len(cols[0])
 _, want = oracle.kmeans_assign(cols, cen)
 dev = torch.device('cuda', 0)
 ctx = sh.Context(0)
-ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+ctx.bind_torch_stream(dev)
 tcols = [torch.from_numpy(c).to(dev) for c in cols]
 tcen = torch.from_numpy(cen.reshape(-1).copy()).to(dev)
 lab = torch.empty(n, dtype=torch.int32, device=dev)

@@ -23,7 +23,7 @@ if distinct:
     for c in cols:
         c.copy_(torch.floor(torch.rand(n, generator=g, device=dev) * distinct) * 0.25 - 5)
 ctx = sh.Context(0)
-ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+ctx.bind_torch_stream(dev)
 draws = np.random.default_rng(1).random(1 << 16)
 cen = torch.empty(256, device=dev)
 lab = torch.empty(3 * n, dtype=torch.int32, device=dev)

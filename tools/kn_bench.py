@@ -47,7 +47,7 @@ if a.zero_frac > 0:  # exact duplicates: identical init rows -> identical centro
     for c in cols:
         c[z] = 0.0
 ctx = sh.Context(0)
-ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+ctx.bind_torch_stream(dev)
 cen = torch.empty(a.d * a.k, device=dev)
 lab = torch.empty(a.n, dtype=torch.int32, device=dev)
 draws = np.random.default_rng(1).random(a.k * (a.iters + 2) * 2)
