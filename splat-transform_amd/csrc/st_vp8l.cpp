@@ -8,7 +8,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <queue>
 #include <stdexcept>
 
 namespace st {
@@ -32,33 +31,41 @@ std::vector<uint8_t> BitWriter::bytes() const {
     return b;
 }
 
-// Huffman over the used symbols with counts raised to at least `floor`; depths out
+// Huffman over the used symbols with counts raised to at least `floor`; depths out.  Two-queue
+// construction: the leaves sorted once by (weight, index), the merged nodes appended in
+// non-decreasing weight order; a leaf wins a weight tie (deterministic)
 static int huffman_depths(const std::vector<std::pair<uint64_t, int>> &used, uint64_t floor_,
                           std::vector<int> &depth) {
     const int m = (int)used.size();
-    // nodes 0..m-1 leaves, then internal nodes; parent links give the depths
+    std::vector<std::pair<uint64_t, int>> leaf(m);
+    for (int i = 0; i < m; ++i) leaf[i] = {std::max(used[i].first, floor_), i};
+    std::sort(leaf.begin(), leaf.end());
+    std::vector<uint64_t> iw;  // merged nodes' weights (node id m + index)
+    iw.reserve(m);
     std::vector<int> parent(2 * m, -1);
-    typedef std::pair<uint64_t, int> Item;  // (weight, node): ties by node id, deterministic
-    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
-    for (int i = 0; i < m; ++i) pq.push({std::max(used[i].first, floor_), i});
-    int next = m;
-    while (pq.size() > 1) {
-        Item a = pq.top();
-        pq.pop();
-        Item b = pq.top();
-        pq.pop();
-        parent[a.second] = next;
-        parent[b.second] = next;
-        pq.push({a.first + b.first, next});
-        ++next;
+    int li = 0, ii = 0;
+    auto take = [&]() {
+        if (li < m && (ii >= (int)iw.size() || leaf[li].first <= iw[ii])) {
+            const auto &l = leaf[li++];
+            return std::make_pair(l.first, l.second);
+        }
+        const int id = m + ii;
+        return std::make_pair(iw[ii++], id);
+    };
+    for (int k = 0; k < m - 1; ++k) {
+        const auto a = take(), b = take();
+        parent[a.second] = m + k;
+        parent[b.second] = m + k;
+        iw.push_back(a.first + b.first);
     }
+    // depths top-down: merged nodes are numbered in creation order, so a parent has a larger id
+    std::vector<int> d(2 * m, 0);
     int maxd = 0;
+    for (int v = 2 * m - 3; v >= 0; --v) d[v] = d[parent[v]] + 1;
     depth.assign(m, 0);
     for (int i = 0; i < m; ++i) {
-        int d = 0;
-        for (int p = parent[i]; p >= 0; p = parent[p]) ++d;
-        depth[i] = d;
-        maxd = std::max(maxd, d);
+        depth[i] = d[i];
+        maxd = std::max(maxd, d[i]);
     }
     return maxd;
 }
@@ -77,8 +84,12 @@ void huffman_lengths(const uint64_t *counts, int n, int limit, uint8_t *len) {
     // raising small counts flattens the tree until it fits the length limit (the
     // result is still a full binary tree, i.e. a complete code)
     std::vector<int> depth;
-    for (uint64_t floor_ = 1;; floor_ *= 2) {
-        if (huffman_depths(used, floor_, depth) <= limit) break;
+    if (huffman_depths(used, 1, depth) > limit) {
+        // a floor of total / 2^(limit - 1) always fits the limit; start a few doublings below it
+        uint64_t total = 0;
+        for (auto &u : used) total += u.first;
+        uint64_t floor_ = std::max<uint64_t>(2, total >> (limit + 2));
+        while (huffman_depths(used, floor_, depth) > limit) floor_ *= 2;
     }
     for (size_t i = 0; i < used.size(); ++i) len[used[i].second] = (uint8_t)depth[i];
 }
@@ -213,9 +224,11 @@ static void write_subimage(BitWriter &bw, const uint8_t *v, size_t n) {
 }
 
 void build_header(int width, int height, bool alpha_used, const uint32_t *hist, int ngroups, const uint8_t *groups,
-                  int group_bits, const uint8_t *modes, Header &out) {
+                  int group_bits, const uint8_t *modes, int cache_bits, Header &out) {
     if (width < 1 || height < 1 || width > 16384 || height > 16384)
         throw std::invalid_argument("vp8l: image size out of range");
+    if (cache_bits != 0 && (cache_bits < kMinCacheBits || cache_bits > kMaxCacheBits))
+        throw std::invalid_argument("vp8l: colour cache bits out of range");
     if (ngroups < 1 || ngroups > 256 || (ngroups > 1 && (group_bits < 2 || group_bits > 9)))
         throw std::invalid_argument("vp8l: prefix-code groups out of range");
     BitWriter &bw = out.bw;
@@ -233,7 +246,12 @@ void build_header(int width, int height, bool alpha_used, const uint32_t *hist, 
     write_subimage(bw, modes, (size_t)bw_ * bh_);
     bw.put(0, 1);  // no more transforms
     // main image
-    bw.put(0, 1);  // no colour cache
+    if (cache_bits) {
+        bw.put(1, 1);
+        bw.put((uint32_t)cache_bits, 4);
+    } else {
+        bw.put(0, 1);  // no colour cache
+    }
     if (ngroups > 1) {  // meta prefix codes: the entropy image (green = group)
         bw.put(1, 1);
         bw.put((uint32_t)(group_bits - 2), 3);
@@ -245,7 +263,7 @@ void build_header(int width, int height, bool alpha_used, const uint32_t *hist, 
     }
     out.tab.assign((size_t)ngroups * kTabSize, 0);
     const int off[5] = {kOffG, kOffR, kOffB, kOffA, kOffD};
-    const int size[5] = {kGreenAlphabet, 256, 256, 256, kDistAlphabet};
+    const int size[5] = {kGreenAlphabet + (cache_bits ? 1 << cache_bits : 0), 256, 256, 256, kDistAlphabet};
     for (int g = 0; g < ngroups; ++g)
         for (int ch = 0; ch < 5; ++ch) {
             std::vector<uint64_t> cnt(size[ch], 0);
@@ -266,6 +284,74 @@ double literal_bits(const uint32_t *hist) {
             if (hist[off[ch] + s]) bits -= hist[off[ch] + s] * std::log2(hist[off[ch] + s] / n);
     }
     return bits;
+}
+
+// bits of one prefix code: its description plus the symbols it codes
+static double code_bits(const std::vector<uint64_t> &c) {
+    BitWriter scratch;
+    const Code code = write_code(scratch, c.data(), (int)c.size());
+    double b = (double)scratch.nbits;
+    for (size_t s = 0; s < c.size(); ++s) b += (double)c[s] * code.len[s];
+    return b;
+}
+
+static double shannon(const uint64_t *c, int n) {
+    double t = 0, bits = 0;
+    for (int s = 0; s < n; ++s) t += (double)c[s];
+    for (int s = 0; s < n; ++s)
+        if (c[s]) bits -= (double)c[s] * std::log2((double)c[s] / t);
+    return bits;
+}
+
+int choose_cache_bits(const uint32_t *hist, const uint32_t *hitlit, const uint32_t *cidx) {
+    const int off[4] = {kOffG, kOffR, kOffB, kOffA};
+    // per candidate: the green alphabet (literals, length prefixes, cache indices) and the red,
+    // blue, alpha literals left after the hits of the sizes <= bits
+    struct Cand {
+        int bits;
+        std::vector<uint64_t> g, rba;
+        double est;
+    };
+    std::vector<Cand> cand;
+    std::vector<uint64_t> lit(4 * 256);
+    for (int ch = 0; ch < 4; ++ch)
+        for (int v = 0; v < 256; ++v) lit[ch * 256 + v] = hist[off[ch] + v];
+    for (int bits = 0; bits <= kMaxCacheBits; bits = bits ? bits + 1 : kMinCacheBits) {
+        if (bits) {
+            const uint32_t *h = hitlit + (size_t)(bits - kMinCacheBits) * 1024;
+            for (int i = 0; i < 1024; ++i) lit[i] -= h[i];
+        }
+        Cand c{bits, std::vector<uint64_t>(lit.begin(), lit.begin() + 256),
+               std::vector<uint64_t>(lit.begin() + 256, lit.end()), 0.0};
+        for (int s = 256; s < kGreenAlphabet; ++s) c.g.push_back(hist[kOffG + s]);
+        int used = 0;
+        if (bits)
+            for (int s = 0; s < (1 << bits); ++s) {
+                c.g.push_back(cidx[cache_off(bits) + s]);
+                used += cidx[cache_off(bits) + s] != 0;
+            }
+        // Shannon bits plus ~4 bits per used cache symbol's code length: the preselection
+        c.est = shannon(c.g.data(), (int)c.g.size()) + 4.0 * used;
+        for (int ch = 0; ch < 3; ++ch) c.est += shannon(c.rba.data() + ch * 256, 256);
+        cand.push_back(std::move(c));
+    }
+    // the coded size (descriptions + symbols) of no cache and the two best estimates
+    std::vector<int> order(cand.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin() + 1, order.end(), [&](int a, int b) { return cand[a].est < cand[b].est; });
+    int best = 0;
+    double bc = 0;
+    for (int k = 0; k < 3 && k < (int)order.size(); ++k) {
+        const Cand &c = cand[order[k]];
+        double b = code_bits(c.g);
+        for (int ch = 0; ch < 3; ++ch)
+            b += code_bits(std::vector<uint64_t>(c.rba.begin() + ch * 256, c.rba.begin() + ch * 256 + 256));
+        if (k == 0 || b < bc) {
+            bc = b;
+            best = c.bits;
+        }
+    }
+    return best;
 }
 
 }  // namespace vp8l

@@ -20,9 +20,17 @@ constexpr int kPredBits = 4;           // predictor blocks of 16 x 16 pixels
 constexpr int kGreenAlphabet = 280;    // 256 literals + 24 length prefixes (no colour cache)
 constexpr int kDistAlphabet = 40;
 constexpr int kMaxCodeLen = 15;
-// the device histogram / code-table layout: G (280: literals + length prefixes), R, B, A (256
-// each), distance (40)
-constexpr int kOffG = 0, kOffR = kGreenAlphabet, kOffB = kOffR + 256, kOffA = kOffB + 256, kOffD = kOffA + 256;
+// colour cache (RFC 9649 5.2.2): the candidate sizes are 2^4 .. 2^10 entries; a pixel whose colour
+// sits in the cache at (0x1e35a7bd * argb) >> (32 - bits) is coded as one green symbol 280 + index
+constexpr int kMinCacheBits = 4, kMaxCacheBits = 10;
+constexpr int kCacheLevels = kMaxCacheBits - kMinCacheBits + 1;
+constexpr int kCacheSlots = (2 << kMaxCacheBits) - (1 << kMinCacheBits);  // all levels' slots: 2,032
+constexpr int cache_off(int bits) { return (1 << bits) - (1 << kMinCacheBits); }  // level's first slot
+constexpr uint32_t kCacheMul = 0x1e35a7bdu;
+constexpr int kGreenMax = kGreenAlphabet + (1 << kMaxCacheBits);
+// the device histogram / code-table layout: G (280 + the cache symbols: literals, length
+// prefixes, cache indices), R, B, A (256 each), distance (40)
+constexpr int kOffG = 0, kOffR = kGreenMax, kOffB = kOffR + 256, kOffA = kOffB + 256, kOffD = kOffA + 256;
 constexpr int kTabSize = kOffD + kDistAlphabet;
 
 // LSB-first bit writer (the VP8L bit order)
@@ -63,11 +71,21 @@ struct Header {
     BitWriter bw;
     std::vector<uint32_t> tab;
 };
+// cache_bits: 0 (no colour cache) or kMinCacheBits..kMaxCacheBits (green alphabet 280 + 2^bits)
 void build_header(int width, int height, bool alpha_used, const uint32_t *hist, int ngroups, const uint8_t *groups,
-                  int group_bits, const uint8_t *modes, Header &out);
+                  int group_bits, const uint8_t *modes, int cache_bits, Header &out);
 // Shannon bits of the literal symbols of a kTabSize histogram (channels G, R, B, A): the
 // cost estimate that decides between predictors for a whole image
 double literal_bits(const uint32_t *hist);
+// The colour-cache size of an image, from one pass over its tokens: hist = the kTabSize
+// histogram without a cache (all prefix-code groups added); hitlit = kCacheLevels x 1,024 counts:
+// level l holds the G, R, B, A values (256 each) of the literals whose smallest hitting cache is
+// 2^(kMinCacheBits + l) (a literal that hits a cache also hits every larger one); cidx =
+// kCacheSlots counts of the hitting literals' cache indices per level (cache_off layout).
+// Returns 0 or the bits whose coded size is the smallest (prefix-code descriptions plus coded
+// symbols of the green, red, blue and alpha alphabets, as one prefix-code group would code them),
+// among no cache and the two sizes with the smallest Shannon estimates.
+int choose_cache_bits(const uint32_t *hist, const uint32_t *hitlit, const uint32_t *cidx);
 
 }  // namespace vp8l
 }  // namespace st

@@ -14,8 +14,20 @@
 //   k_vp8l_runs     per 4,096-pixel group: runs of >= 3 residuals equal to their left
 //                   neighbour become one LZ77 copy (distance code 2: the pixel to the
 //                   left; length <= 4,096), tokens: literal / copy length / covered
-//   k_vp8l_hist     symbol histograms (literal channels, length prefixes, distance;
-//                   LDS-private, one flush per group)                  read 4 + 2 B
+//   k_cc_walk       colour cache (RFC 9649 5.2.2), all candidate sizes 2^4..2^10 at once: per
+//                   4,096-pixel group one wave whose lanes 0..6 each replay one cache size over
+//                   the group's pixels in order (LDS table; reads and writes issued back to
+//                   back, the compares after), so a pixel hits when the last earlier pixel of
+//                   the group with its index has its colour; a pixel whose index is new in the
+//                   group is left to k_cc_fix.  Writes the group's final cache per size (with
+//                   written flags) and each index's first pixel            read 4 B, write 1 B
+//   k_cc_scan1/2    the cache state at each group's start: per index, the last group before it
+//                   that wrote the index (a carry scan over chunks of 64 groups, then over chunks)
+//   k_cc_fix        the first pixel of each index in each group against that state
+//   k_cc_survey     per size, the literals' hits as histograms: the host picks the size
+//                   (vp8l::choose_cache_bits) and k_vp8l_hist redoes the histograms with it
+//   k_vp8l_hist     symbol histograms (literal channels, length prefixes, cache indices,
+//                   distance; LDS-private, one flush per group)        read 4 + 2 + 1 B
 //   host            canonical length-limited prefix codes + header bits (st_vp8l.cpp)
 //   k_vp8l_bits     bits per 4,096-pixel group (table lookups in LDS)     read 4 B
 //   k_vp8l_scan     exclusive bit offsets of the groups (one workgroup) + RIFF sizes
@@ -221,10 +233,18 @@ __device__ inline uint32_t group_of(const uint8_t *gflag, uint32_t p, int w, int
 // symbol histograms per prefix-code group (CODE_GROUPS x kTabSize, the vp8l::kOff* layout) and,
 // with raw, the histogram of the pixels themselves as predictor 0 leaves them (pixel - 0xff000000):
 // the host's per-image choice between the chosen predictors and none
+// colour-cache index of an ARGB word in a 2^bits-entry cache
+__device__ inline uint32_t cc_index(uint32_t argb, int bits) { return (argb * vp8l::kCacheMul) >> (32 - bits); }
+// a literal coded as a cache index (cb: the image's cache bits, 0 = no cache)
+__device__ inline bool cc_hit(const uint8_t *hits, uint64_t p, int cb) {
+    return cb && ((hits[p] >> (cb - vp8l::kMinCacheBits)) & 1u);
+}
+
 __global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ resid,
                                                    const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
                                                    const uint8_t *__restrict__ gflag,
                                                    const uint8_t *__restrict__ rgba, int stride,
+                                                   const uint8_t *__restrict__ hits, int cb,
                                                    uint32_t *__restrict__ hist, uint32_t *__restrict__ raw) {
     __shared__ uint32_t hs[CODE_GROUPS * vp8l::kTabSize];
     __shared__ uint32_t hr[4 * 256];
@@ -253,6 +273,10 @@ __global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ 
             continue;
         }
         const uint32_t r = resid[i];
+        if (cc_hit(hits, i, cb)) {
+            atomicAdd(&H[vp8l::kOffG + vp8l::kGreenAlphabet + cc_index(r, cb)], 1u);
+            continue;
+        }
         atomicAdd(&H[vp8l::kOffG + ((r >> 8) & 0xff)], 1u);
         atomicAdd(&H[vp8l::kOffR + ((r >> 16) & 0xff)], 1u);
         atomicAdd(&H[vp8l::kOffB + (r & 0xff)], 1u);
@@ -271,10 +295,15 @@ __global__ __launch_bounds__(256) void k_vp8l_hist(const uint32_t *__restrict__ 
 
 // code of one token: (bits, length) LSB-first -- a literal's G, R, B, A codes, or a copy's
 // length prefix (green alphabet), length extra bits and distance prefix (no extra bits)
-__device__ inline uint64_t token_code(const uint32_t *tab, uint32_t r, uint32_t t, int &n) {
+__device__ inline uint64_t token_code(const uint32_t *tab, uint32_t r, uint32_t t, bool hit, int cb, int &n) {
     if (t == TOK_COVERED) {
         n = 0;
         return 0;
+    }
+    if (t == TOK_LIT && hit) {  // colour-cache index: one green symbol
+        const uint32_t e = tab[vp8l::kOffG + vp8l::kGreenAlphabet + cc_index(r, cb)];
+        n = (int)(e >> 16);
+        return e & 0xffffu;
     }
     if (t != TOK_LIT) {
         uint32_t lp, ne, ex;
@@ -298,8 +327,9 @@ __device__ inline uint64_t token_code(const uint32_t *tab, uint32_t r, uint32_t 
     return v;
 }
 
-__device__ inline int token_len(const uint32_t *tab, uint32_t r, uint32_t t) {
+__device__ inline int token_len(const uint32_t *tab, uint32_t r, uint32_t t, bool hit, int cb) {
     if (t == TOK_COVERED) return 0;
+    if (t == TOK_LIT && hit) return (int)(tab[vp8l::kOffG + vp8l::kGreenAlphabet + cc_index(r, cb)] >> 16);
     if (t != TOK_LIT) {
         uint32_t lp, ne, ex;
         prefix_of(t, lp, ne, ex);
@@ -376,6 +406,7 @@ __global__ __launch_bounds__(256) void k_vp8l_runs(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(256) void k_vp8l_bits(const uint32_t *__restrict__ resid,
                                                    const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
                                                    const uint8_t *__restrict__ gflag, int ngroups,
+                                                   const uint8_t *__restrict__ hits, int cb,
                                                    const uint32_t *__restrict__ tab_g, uint32_t *__restrict__ wg_bits) {
     __shared__ uint32_t tab[CODE_GROUPS * vp8l::kTabSize];
     __shared__ uint32_t red[4];
@@ -386,7 +417,7 @@ __global__ __launch_bounds__(256) void k_vp8l_bits(const uint32_t *__restrict__ 
     for (int j = 0; j < EMIT_PP; ++j)
         if (p0 + j < npix) {
             const uint32_t g = ngroups > 1 ? group_of(gflag, (uint32_t)(p0 + j), w, gw) : 0u;
-            bits += token_len(tab + g * vp8l::kTabSize, resid[p0 + j], tok[p0 + j]);
+            bits += token_len(tab + g * vp8l::kTabSize, resid[p0 + j], tok[p0 + j], cc_hit(hits, p0 + j, cb), cb);
         }
     for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
@@ -434,6 +465,7 @@ __global__ __launch_bounds__(1024) void k_vp8l_scan(const uint32_t *__restrict__
 __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ resid,
                                                    const uint16_t *__restrict__ tok, uint64_t npix, int w, int gw,
                                                    const uint8_t *__restrict__ gflag, int ngroups,
+                                                   const uint8_t *__restrict__ hits, int cb,
                                                    const uint32_t *__restrict__ tab_g,
                                                    const uint64_t *__restrict__ wg_off, uint32_t *__restrict__ out) {
     __shared__ uint32_t tab[CODE_GROUPS * vp8l::kTabSize];
@@ -444,13 +476,15 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
     __syncthreads();
     const uint64_t p0 = (uint64_t)blockIdx.x * EMIT_PIX + (uint64_t)threadIdx.x * EMIT_PP;
     uint32_t r[EMIT_PP], tk[EMIT_PP], gt[EMIT_PP];
+    bool hb[EMIT_PP];
     uint32_t mine = 0;
 #pragma unroll
     for (int j = 0; j < EMIT_PP; ++j) {
         r[j] = (p0 + j < npix) ? resid[p0 + j] : 0u;
         tk[j] = (p0 + j < npix) ? tok[p0 + j] : TOK_COVERED;
         gt[j] = (ngroups > 1 && p0 + j < npix) ? group_of(gflag, (uint32_t)(p0 + j), w, gw) * vp8l::kTabSize : 0u;
-        if (p0 + j < npix) mine += token_len(tab + gt[j], r[j], tk[j]);
+        hb[j] = p0 + j < npix && cc_hit(hits, p0 + j, cb);
+        if (p0 + j < npix) mine += token_len(tab + gt[j], r[j], tk[j], hb[j], cb);
     }
     // inclusive scan of the threads' bit counts
     tsum[threadIdx.x] = mine;
@@ -469,7 +503,7 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
     for (int j = 0; j < EMIT_PP; ++j) {
         if (p0 + j >= npix) break;
         int n;
-        const uint64_t v = token_code(tab + gt[j], r[j], tk[j], n);
+        const uint64_t v = token_code(tab + gt[j], r[j], tk[j], hb[j], cb, n);
         if (n) {
             const uint32_t wi = pos >> 5, s = pos & 31;
             atomicOr(&words[wi], (uint32_t)(v << s));
@@ -488,6 +522,157 @@ __global__ __launch_bounds__(256) void k_vp8l_emit(const uint32_t *__restrict__ 
         else
             dst[j] = words[j];
     }
+}
+
+// ---- colour cache ----------------------------------------------------------------
+constexpr int CC_SLOTS = vp8l::kCacheSlots;  // the slots of every candidate size, cache_off layout
+constexpr uint32_t CC_CHUNK = 64;            // groups per carry-scan chunk
+constexpr uint64_t CC_SET = 1ull << 32;      // a table entry: CC_SET | colour once written, else 0
+
+// one wave per EMIT_PIX group; lane l < kCacheLevels replays the 2^(kMinCacheBits + l)-entry cache.
+// hits[p] bit l: pixel p's colour is in that cache (the last earlier pixel of the group with the
+// same index has it); an index new in the group leaves the bit to k_cc_fix.  W: the group's last
+// colour per slot (CC_SET | colour, or 0); F: 1 + the group position of the slot's first pixel
+// (stored as it is met: at most one store per slot and group).
+__global__ __launch_bounds__(64) void k_cc_walk(const uint32_t *__restrict__ resid, uint64_t npix,
+                                                uint8_t *__restrict__ hits, uint64_t *__restrict__ W,
+                                                uint32_t *__restrict__ F) {
+    // lanes >= kCacheLevels replay nothing: they read and write a private slot past the table,
+    // so the step loop has no exec-mask branches
+    __shared__ uint64_t cache[CC_SLOTS + 64];
+    const int lane = threadIdx.x;
+    for (int j = lane; j < CC_SLOTS + 64; j += 64) cache[j] = 0;
+    __syncthreads();
+    const uint64_t g0 = (uint64_t)blockIdx.x * EMIT_PIX;
+    const uint32_t cnt = (uint32_t)min((uint64_t)EMIT_PIX, npix - g0);
+    const bool act = lane < vp8l::kCacheLevels;
+    const int bits = vp8l::kMinCacheBits + (act ? lane : 0);
+    const uint32_t base = (uint32_t)vp8l::cache_off(bits), own = (uint32_t)CC_SLOTS + lane;
+    uint32_t *Fg = F + (uint64_t)blockIdx.x * CC_SLOTS;  // zeroed by the caller
+    constexpr uint32_t LEVEL_MASK = (1u << vp8l::kCacheLevels) - 1;
+    constexpr int SUB = 16;  // steps whose LDS reads and writes are issued before their compares
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+        const uint32_t m = min(64u, cnt - i0);
+        const uint32_t pv = (uint32_t)lane < m ? resid[g0 + i0 + lane] : 0u;
+        uint32_t mine = 0;  // lane q: the hit bits of pixel i0 + q
+        if (m == 64) {
+#pragma unroll
+            for (int k0 = 0; k0 < 64; k0 += SUB) {
+                uint64_t e[SUB];
+                uint32_t slot[SUB];
+#pragma unroll
+                for (int u = 0; u < SUB; ++u) {
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
+                    slot[u] = act ? base + cc_index(c, bits) : own;
+                    e[u] = cache[slot[u]];
+                    cache[slot[u]] = CC_SET | c;
+                }
+#pragma unroll
+                for (int u = 0; u < SUB; ++u) {
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
+                    if (!e[u] && act) Fg[slot[u]] = i0 + k0 + u + 1;  // the slot's first pixel in the group
+                    const uint32_t hm = (uint32_t)__ballot(e[u] == (CC_SET | c)) & LEVEL_MASK;
+                    mine = lane == k0 + u ? hm : mine;
+                }
+            }
+        } else {  // the image's last, partial batch: one step at a time
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t c = (uint32_t)__shfl((int)pv, (int)k, 64);
+                const uint32_t slot = act ? base + cc_index(c, bits) : own;
+                const uint64_t e = cache[slot];
+                cache[slot] = CC_SET | c;
+                if (!e && act) Fg[slot] = i0 + k + 1;
+                const uint32_t hm = (uint32_t)__ballot(e == (CC_SET | c)) & LEVEL_MASK;
+                mine = (uint32_t)lane == k ? hm : mine;
+            }
+        }
+        if ((uint32_t)lane < m) hits[g0 + i0 + lane] = (uint8_t)mine;
+    }
+    __syncthreads();
+    uint64_t *Wg = W + (uint64_t)blockIdx.x * CC_SLOTS;
+    for (int j = lane; j < CC_SLOTS; j += 64) Wg[j] = cache[j];
+}
+
+// W[g][j] <- the last written entry of the groups before g in g's chunk (0: none); A[chunk][j] <-
+// the chunk's last written entry
+__global__ __launch_bounds__(256) void k_cc_scan1(uint64_t *__restrict__ W, uint32_t ngroups,
+                                                  uint64_t *__restrict__ A) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= (uint32_t)CC_SLOTS) return;
+    const uint32_t g0 = blockIdx.y * CC_CHUNK, g1 = min(ngroups, g0 + CC_CHUNK);
+    uint64_t carry = 0;
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint64_t v = W[(uint64_t)g * CC_SLOTS + j];
+        W[(uint64_t)g * CC_SLOTS + j] = carry;
+        if (v) carry = v;
+    }
+    A[(uint64_t)blockIdx.y * CC_SLOTS + j] = carry;
+}
+
+// A[chunk][j] <- the last written entry of the chunks before it (0: none)
+__global__ __launch_bounds__(256) void k_cc_scan2(uint64_t *__restrict__ A, uint32_t nchunks) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= (uint32_t)CC_SLOTS) return;
+    uint64_t carry = 0;
+    for (uint32_t q = 0; q < nchunks; ++q) {
+        const uint64_t v = A[(uint64_t)q * CC_SLOTS + j];
+        A[(uint64_t)q * CC_SLOTS + j] = carry;
+        if (v) carry = v;
+    }
+}
+
+// the first pixel of slot j in group g hits when the cache entry at the group's start (the scans)
+// holds its colour; an entry no earlier pixel wrote counts as a miss (the zero-initialised cache
+// is not relied on)
+__global__ __launch_bounds__(256) void k_cc_fix(const uint32_t *__restrict__ resid, const uint64_t *__restrict__ W,
+                                                const uint64_t *__restrict__ A, const uint32_t *__restrict__ F,
+                                                uint8_t *__restrict__ hits) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= (uint32_t)CC_SLOTS) return;
+    const uint64_t g = blockIdx.y;
+    const uint32_t f = F[g * CC_SLOTS + j];
+    if (!f) return;
+    uint64_t e = W[g * CC_SLOTS + j];
+    if (!e) e = A[(g / CC_CHUNK) * CC_SLOTS + j];
+    const uint64_t p = g * EMIT_PIX + f - 1;
+    if (e && (uint32_t)e == resid[p]) {
+        const uint32_t level = (31 - __builtin_clz(j + (1u << vp8l::kMinCacheBits))) - vp8l::kMinCacheBits;
+        atomicOr(reinterpret_cast<uint32_t *>(hits + (p & ~3ull)), (1u << level) << (8 * (p & 3)));
+    }
+}
+
+// per cache size, the literals that hit it: hitlit[l] = the G, R, B, A values of the literals
+// whose smallest hitting size is level l; cidx = their indices at every level they hit
+__global__ __launch_bounds__(256) void k_cc_survey(const uint32_t *__restrict__ resid,
+                                                   const uint16_t *__restrict__ tok, const uint8_t *__restrict__ hits,
+                                                   uint64_t npix, uint32_t *__restrict__ hitlit,
+                                                   uint32_t *__restrict__ cidx) {
+    __shared__ uint32_t hl[vp8l::kCacheLevels * 1024];
+    __shared__ uint32_t ci[CC_SLOTS];
+    for (int i = threadIdx.x; i < vp8l::kCacheLevels * 1024; i += 256) hl[i] = 0;
+    for (int i = threadIdx.x; i < CC_SLOTS; i += 256) ci[i] = 0;
+    __syncthreads();
+    const uint64_t stride_ = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += stride_) {
+        const uint32_t m = hits[i];
+        if (!m || tok[i] != TOK_LIT) continue;
+        const uint32_t r = resid[i];
+        const int l0 = __builtin_ctz(m);
+        uint32_t *h = hl + l0 * 1024;
+        atomicAdd(&h[(r >> 8) & 0xff], 1u);
+        atomicAdd(&h[256 + ((r >> 16) & 0xff)], 1u);
+        atomicAdd(&h[512 + (r & 0xff)], 1u);
+        atomicAdd(&h[768 + (r >> 24)], 1u);
+        for (int l = l0; l < vp8l::kCacheLevels; ++l) {
+            const int bits = vp8l::kMinCacheBits + l;
+            atomicAdd(&ci[vp8l::cache_off(bits) + cc_index(r, bits)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < vp8l::kCacheLevels * 1024; i += 256)
+        if (hl[i]) atomicAdd(&hitlit[i], hl[i]);
+    for (int i = threadIdx.x; i < CC_SLOTS; i += 256)
+        if (ci[i]) atomicAdd(&cidx[i], ci[i]);
 }
 
 // ---- CRC-32 (zlib polynomial, reflected) ---------------------------------------
@@ -594,9 +779,10 @@ uint64_t webp_max_size(int w, int h) {
 }
 
 void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
-    // per job in pinned staging: group histograms, the raw histogram, predictor modes, group flags
+    // per job in pinned staging: group histograms, the raw histogram, predictor modes, group
+    // flags, the colour-cache survey (hit literals per size, cache indices)
     struct Stage {
-        size_t hist, raw, modes, flags;
+        size_t hist, raw, modes, flags, hitlit, cidx;
     };
     std::vector<Stage> stage;
     size_t pin = 0;
@@ -619,9 +805,19 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         st.raw = st.hist + CODE_GROUPS * vp8l::kTabSize * 4;
         st.modes = st.raw + vp8l::kTabSize * 4;
         st.flags = st.modes + (size_t)bw * bh;
+        st.hitlit = (st.flags + (size_t)gw * gh + 15) & ~(size_t)15;
+        st.cidx = st.hitlit + (size_t)vp8l::kCacheLevels * 1024 * 4;
         stage.push_back(st);
-        pin = (st.flags + (size_t)gw * gh + 255) & ~(size_t)255;
+        pin = (st.cidx + (size_t)CC_SLOTS * 4 + 255) & ~(size_t)255;
     }
+    // colour-cache tables, shared by the jobs (one stream: each job's walk, scans and fix-up run
+    // before the next job's walk)
+    uint32_t max_groups = 1;
+    for (int j = 0; j < njobs; ++j)
+        max_groups = std::max(max_groups, (uint32_t)(((uint64_t)jobs[j].w * jobs[j].h + EMIT_PIX - 1) / EMIT_PIX));
+    uint64_t *ccW = wsT<uint64_t>(c, "wp.ccw", (size_t)max_groups * CC_SLOTS);
+    uint32_t *ccF = wsT<uint32_t>(c, "wp.ccf", (size_t)max_groups * CC_SLOTS);
+    uint64_t *ccA = wsT<uint64_t>(c, "wp.cca", (size_t)((max_groups + CC_CHUNK - 1) / CC_CHUNK) * CC_SLOTS);
     // phase A: predictors, residuals, tokens, group flags, histograms (raw = the pixels as no
     // predictor leaves them, for the choice below)
     auto phase_a = [&](int j, int force_mode) {
@@ -650,7 +846,8 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
             hipLaunchKernelGGL(k_vp8l_runs, dim3((unsigned)((npix + EMIT_PIX - 1) / EMIT_PIX)), dim3(256), 0,
                                c->stream, resid, npix, tok, jb.w, gw, gflag);
             hipLaunchKernelGGL(k_vp8l_hist, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid, tok,
-                               npix, jb.w, gw, gflag, jb.rgba, jb.stride, hist, force_mode < 0 ? raw : nullptr);
+                               npix, jb.w, gw, gflag, jb.rgba, jb.stride, (const uint8_t *)nullptr, 0, hist,
+                               force_mode < 0 ? raw : nullptr);
             ST_LAUNCH_CHECK();
         }
         uint8_t *hp = (uint8_t *)pinned(c, pin);
@@ -659,6 +856,37 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         ST_HIP(hipMemcpyAsync(hp + stage[j].raw, raw, vp8l::kTabSize * 4, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipMemcpyAsync(hp + stage[j].modes, modes, (size_t)bw * bh, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipMemcpyAsync(hp + stage[j].flags, gflag, (size_t)gw * gh, hipMemcpyDeviceToHost, c->stream));
+    };
+    // the colour cache of the final residuals: hits for every candidate size, the survey
+    auto cache_stage = [&](int j) {
+        WebpJob &jb = jobs[j];
+        const std::string tag = "wp" + std::to_string(j);
+        const uint64_t npix = (uint64_t)jb.w * jb.h;
+        const uint32_t ngrp = (uint32_t)((npix + EMIT_PIX - 1) / EMIT_PIX);
+        const uint32_t *resid = wsT<uint32_t>(c, tag + ".res", npix);
+        const uint16_t *tok = wsT<uint16_t>(c, tag + ".tok", npix);
+        uint8_t *hits = wsT<uint8_t>(c, tag + ".cch", (size_t)ngrp * EMIT_PIX);
+        uint32_t *hitlit = wsT<uint32_t>(c, tag + ".chl", (size_t)vp8l::kCacheLevels * 1024);
+        uint32_t *cidx = wsT<uint32_t>(c, tag + ".cci", (size_t)CC_SLOTS);
+        ST_HIP(hipMemsetAsync(hitlit, 0, (size_t)vp8l::kCacheLevels * 1024 * 4, c->stream));
+        ST_HIP(hipMemsetAsync(cidx, 0, (size_t)CC_SLOTS * 4, c->stream));
+        {
+            KTimer kt(c, "webp.cache");
+            const uint32_t nch = (ngrp + CC_CHUNK - 1) / CC_CHUNK;
+            const unsigned sb = (CC_SLOTS + 255) / 256;
+            ST_HIP(hipMemsetAsync(ccF, 0, (size_t)ngrp * CC_SLOTS * 4, c->stream));
+            hipLaunchKernelGGL(k_cc_walk, dim3(ngrp), dim3(64), 0, c->stream, resid, npix, hits, ccW, ccF);
+            hipLaunchKernelGGL(k_cc_scan1, dim3(sb, nch), dim3(256), 0, c->stream, ccW, ngrp, ccA);
+            hipLaunchKernelGGL(k_cc_scan2, dim3(sb), dim3(256), 0, c->stream, ccA, nch);
+            hipLaunchKernelGGL(k_cc_fix, dim3(sb, ngrp), dim3(256), 0, c->stream, resid, ccW, ccA, ccF, hits);
+            hipLaunchKernelGGL(k_cc_survey, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid, tok,
+                               hits, npix, hitlit, cidx);
+            ST_LAUNCH_CHECK();
+        }
+        uint8_t *hp = (uint8_t *)pinned(c, pin);
+        ST_HIP(hipMemcpyAsync(hp + stage[j].hitlit, hitlit, (size_t)vp8l::kCacheLevels * 1024 * 4,
+                              hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemcpyAsync(hp + stage[j].cidx, cidx, (size_t)CC_SLOTS * 4, hipMemcpyDeviceToHost, c->stream));
     };
     for (int j = 0; j < njobs; ++j) phase_a(j, -1);
     ST_HIP(hipStreamSynchronize(c->stream));
@@ -677,11 +905,42 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
             again = true;
         }
     }
-    if (again) {
+    if (again)
         for (int j = 0; j < njobs; ++j)
             if (forced[j]) phase_a(j, 0);
-        ST_HIP(hipStreamSynchronize(c->stream));
+    for (int j = 0; j < njobs; ++j) cache_stage(j);
+    ST_HIP(hipStreamSynchronize(c->stream));
+    // per image: the colour-cache size; with a cache, the histograms again (a hitting literal is
+    // one green symbol)
+    std::vector<int> cbits(njobs, 0);
+    bool rehist = false;
+    for (int j = 0; j < njobs; ++j) {
+        const uint32_t *h = (const uint32_t *)(hp + stage[j].hist);
+        std::vector<uint32_t> merged(vp8l::kTabSize);
+        for (int q = 0; q < vp8l::kTabSize; ++q) merged[q] = h[q] + h[vp8l::kTabSize + q];
+        cbits[j] = vp8l::choose_cache_bits(merged.data(), (const uint32_t *)(hp + stage[j].hitlit),
+                                           (const uint32_t *)(hp + stage[j].cidx));
+        if (!cbits[j]) continue;
+        rehist = true;
+        WebpJob &jb = jobs[j];
+        const std::string tag = "wp" + std::to_string(j);
+        int bw, bh, gw, gh;
+        geom(jb, bw, bh, gw, gh);
+        const uint64_t npix = (uint64_t)jb.w * jb.h;
+        const uint32_t ngrp = (uint32_t)((npix + EMIT_PIX - 1) / EMIT_PIX);
+        uint32_t *hist = wsT<uint32_t>(c, tag + ".hist", (size_t)CODE_GROUPS * vp8l::kTabSize);
+        ST_HIP(hipMemsetAsync(hist, 0, (size_t)CODE_GROUPS * vp8l::kTabSize * 4, c->stream));
+        KTimer kt(c, "webp.hist");
+        hipLaunchKernelGGL(k_vp8l_hist, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream,
+                           wsT<uint32_t>(c, tag + ".res", npix), wsT<uint16_t>(c, tag + ".tok", npix), npix, jb.w, gw,
+                           wsT<uint8_t>(c, tag + ".gfl", (size_t)gw * gh), jb.rgba, jb.stride,
+                           wsT<uint8_t>(c, tag + ".cch", (size_t)ngrp * EMIT_PIX), cbits[j], hist,
+                           (uint32_t *)nullptr);
+        ST_LAUNCH_CHECK();
+        ST_HIP(hipMemcpyAsync(hp + stage[j].hist, hist, (size_t)CODE_GROUPS * vp8l::kTabSize * 4,
+                              hipMemcpyDeviceToHost, c->stream));
     }
+    if (rehist) ST_HIP(hipStreamSynchronize(c->stream));
     // host: prefix codes + header bits (two groups when some block holds a literal alpha residual)
     std::vector<vp8l::Header> hdr(njobs);
     std::vector<int> ngroups(njobs, 1);
@@ -699,12 +958,14 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         for (int i = 0; i < gw * gh && ngroups[j] == 1; ++i)
             if (flags[i]) ngroups[j] = CODE_GROUPS;
         if (ngroups[j] > 1) {
-            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, hist, ngroups[j], flags, GROUP_BITS, modes, hdr[j]);
+            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, hist, ngroups[j], flags, GROUP_BITS, modes, cbits[j],
+                               hdr[j]);
         } else {  // one group: group 1's symbols (if any) join group 0
             ngroups[j] = 1;
             std::vector<uint32_t> merged(vp8l::kTabSize);
             for (int s = 0; s < vp8l::kTabSize; ++s) merged[s] = hist[s] + hist[vp8l::kTabSize + s];
-            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, merged.data(), 1, flags, GROUP_BITS, modes, hdr[j]);
+            vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, merged.data(), 1, flags, GROUP_BITS, modes, cbits[j],
+                               hdr[j]);
         }
     }
     // phase C: bit counts, offsets, emission
@@ -730,13 +991,14 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         const uint32_t *resid = wsT<uint32_t>(c, tags[j] + ".res", npix);
         const uint16_t *tok = wsT<uint16_t>(c, tags[j] + ".tok", npix);
         const uint8_t *gflag = wsT<uint8_t>(c, tags[j] + ".gfl", (size_t)gw * gh);
+        const uint8_t *hits = wsT<uint8_t>(c, tags[j] + ".cch", (size_t)nwg * EMIT_PIX);
         ST_HIP(hipMemsetAsync(jb.out, 0, webp_max_size(jb.w, jb.h), c->stream));
         ST_HIP(hipMemcpyAsync(jb.out, head[j].data(), head[j].size(), hipMemcpyHostToDevice, c->stream));
         ST_HIP(hipMemcpyAsync(tab, hdr[j].tab.data(), hdr[j].tab.size() * 4, hipMemcpyHostToDevice, c->stream));
         {
             KTimer kt(c, "webp.bits");
             hipLaunchKernelGGL(k_vp8l_bits, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, jb.w, gw, gflag,
-                               ngroups[j], tab, wg_bits);
+                               ngroups[j], hits, cbits[j], tab, wg_bits);
             ST_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(k_vp8l_scan, dim3(1), dim3(1024), 0, c->stream, wg_bits, nwg,
@@ -745,7 +1007,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         {
             KTimer kt(c, "webp.emit");
             hipLaunchKernelGGL(k_vp8l_emit, dim3(nwg), dim3(256), 0, c->stream, resid, tok, npix, jb.w, gw, gflag,
-                               ngroups[j], tab, wg_off, (uint32_t *)jb.out);
+                               ngroups[j], hits, cbits[j], tab, wg_off, (uint32_t *)jb.out);
             ST_LAUNCH_CHECK();
         }
     }

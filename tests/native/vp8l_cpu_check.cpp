@@ -4,7 +4,7 @@
 // can be checked on a machine without a GPU (tests/test_webp_cpu.py decodes the
 // output with Pillow/libwebp).  Never linked into libsplat_hip.
 //
-//   vp8l_cpu_check in.rgba W H out.webp
+//   vp8l_cpu_check in.rgba W H out.webp [cache_bits]   (cache_bits: -1 = choose, 0 = none, 4..10)
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -69,8 +69,9 @@ static uint32_t sub(uint32_t a, uint32_t b) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 5) return 2;
+    if (argc != 5 && argc != 6) return 2;
     const int w = atoi(argv[2]), h = atoi(argv[3]);
+    const int force_cb = argc == 6 ? atoi(argv[5]) : -1;
     std::vector<uint8_t> rgba((size_t)w * h * 4);
     FILE *f = fopen(argv[1], "rb");
     if (!f || fread(rgba.data(), 1, rgba.size(), f) != rgba.size()) return 3;
@@ -182,16 +183,51 @@ int main(int argc, char **argv) {
         std::fill(modes.begin(), modes.end(), 0);
         encode_pass(true);
     }
+    // colour cache (the device's k_cc_* kernels restated): bit l of hit[i] when the last earlier
+    // pixel with the same index in a 2^(4 + l)-entry cache has the same colour (none: a miss)
+    std::vector<uint8_t> hit(npix, 0);
+    for (int l = 0; l < kCacheLevels; ++l) {
+        const int bits = kMinCacheBits + l;
+        std::vector<int64_t> last((size_t)1 << bits, -1);
+        for (size_t i = 0; i < npix; ++i) {
+            const uint32_t s = (res[i] * kCacheMul) >> (32 - bits);
+            if (last[s] >= 0 && res[last[s]] == res[i]) hit[i] |= (uint8_t)(1u << l);
+            last[s] = (int64_t)i;
+        }
+    }
+    std::vector<uint32_t> hitlit(kCacheLevels * 1024, 0), cidx(kCacheSlots, 0), merged(kTabSize);
+    for (size_t i = 0; i < npix; ++i) {
+        if (tok[i] != 0 || !hit[i]) continue;
+        const int l0 = __builtin_ctz(hit[i]);
+        const uint32_t r = res[i];
+        uint32_t *hl = hitlit.data() + (size_t)l0 * 1024;
+        hl[ch(r, 1)]++, hl[256 + ch(r, 2)]++, hl[512 + ch(r, 0)]++, hl[768 + ch(r, 3)]++;
+        for (int l = l0; l < kCacheLevels; ++l) {
+            const int bits = kMinCacheBits + l;
+            cidx[cache_off(bits) + ((r * kCacheMul) >> (32 - bits))]++;
+        }
+    }
+    for (int q = 0; q < kTabSize; ++q) merged[q] = hist[q] + hist[kTabSize + q];
+    const int cb = force_cb >= 0 ? force_cb : choose_cache_bits(merged.data(), hitlit.data(), cidx.data());
+    auto cache_hit = [&](size_t i) { return cb && tok[i] == 0 && ((hit[i] >> (cb - kMinCacheBits)) & 1); };
+    if (cb) {  // the histograms again: a hitting literal is one green symbol 280 + its index
+        for (size_t i = 0; i < npix; ++i) {
+            if (!cache_hit(i)) continue;
+            const uint32_t r = res[i];
+            uint32_t *H = hist.data() + (size_t)gfl[(i / w >> GB) * gw + ((i % w) >> GB)] * kTabSize;
+            H[kOffG + ch(r, 1)]--, H[kOffR + ch(r, 2)]--, H[kOffB + ch(r, 0)]--, H[kOffA + ch(r, 3)]--;
+            H[kOffG + kGreenAlphabet + ((r * kCacheMul) >> (32 - cb))]++;
+        }
+        for (int q = 0; q < kTabSize; ++q) merged[q] = hist[q] + hist[kTabSize + q];
+    }
+    fprintf(stderr, "cache_bits %d\n", cb);
     int ngroups = 1;
     for (uint8_t f : gfl) ngroups = f ? 2 : ngroups;
     Header hd;
-    if (ngroups == 2) {
-        build_header(w, h, alpha, hist.data(), 2, gfl.data(), GB, modes.data(), hd);
-    } else {
-        std::vector<uint32_t> merged(kTabSize);
-        for (int q = 0; q < kTabSize; ++q) merged[q] = hist[q] + hist[kTabSize + q];
-        build_header(w, h, alpha, merged.data(), 1, gfl.data(), GB, modes.data(), hd);
-    }
+    if (ngroups == 2)
+        build_header(w, h, alpha, hist.data(), 2, gfl.data(), GB, modes.data(), cb, hd);
+    else
+        build_header(w, h, alpha, merged.data(), 1, gfl.data(), GB, modes.data(), cb, hd);
     BitWriter &bw_ = hd.bw;
     for (size_t i = 0; i < npix; ++i) {
         const uint32_t r = res[i];
@@ -204,6 +240,11 @@ int main(int argc, char **argv) {
             bw_.put(eg & 0xffffu, (int)(eg >> 16));
             bw_.put(ex, (int)ne);
             bw_.put(ed & 0xffffu, (int)(ed >> 16));
+            continue;
+        }
+        if (cache_hit(i)) {
+            const uint32_t e = T[kOffG + kGreenAlphabet + ((r * kCacheMul) >> (32 - cb))];
+            bw_.put(e & 0xffffu, (int)(e >> 16));
             continue;
         }
         const uint32_t e[4] = {T[kOffG + ch(r, 1)], T[kOffR + ch(r, 2)], T[kOffB + ch(r, 0)], T[kOffA + ch(r, 3)]};

@@ -122,12 +122,15 @@ def _harness():
     return HARNESS
 
 
-def _roundtrip(img, tmp_path):
+def _roundtrip(img, tmp_path, cache_bits=-1, want_bits=None):
     from PIL import Image
     h, w, _ = img.shape
     src, dst = tmp_path / 'in.rgba', tmp_path / 'out.webp'
     np.ascontiguousarray(img, np.uint8).tofile(src)
-    subprocess.check_call([_harness(), str(src), str(w), str(h), str(dst)])
+    r = subprocess.run([_harness(), str(src), str(w), str(h), str(dst), str(cache_bits)], capture_output=True,
+                       text=True, check=True)
+    if want_bits is not None:
+        assert ('cache_bits %d' % want_bits) in r.stderr, r.stderr
     return np.array(Image.open(dst).convert('RGBA'))
 
 
@@ -148,13 +151,52 @@ def _images():
         'Nx1': rng.integers(0, 256, (50, 1, 4)),
         'opaque_noise': opaque,
         'sparse_palette': rng.choice([0, 17, 200, 255], size=(33, 70, 4)),
+        'palette_noise': _palette_noise(rng),
     }
+
+
+def _palette_noise(rng):
+    """60 random opaque colours at random positions: no predictor helps, the colours repeat
+    (what a colour cache is for)"""
+    pal = rng.integers(0, 256, (60, 4))
+    pal[:, 3] = 255
+    return pal[rng.integers(0, 60, (90, 130))]
 
 
 @pytest.mark.parametrize('kind', list(_images().keys()))
 def test_vp8l_header_decodes(kind, tmp_path):
     img = _images()[kind].astype(np.uint8)
     assert np.array_equal(_roundtrip(img, tmp_path), img)
+
+
+@pytest.mark.parametrize('bits', [0, 4, 7, 10])
+@pytest.mark.parametrize('kind', ['random', 'gradient', 'sparse_palette', 'palette_noise', 'constant', '1xN'])
+def test_vp8l_colour_cache_decodes(kind, bits, tmp_path):
+    """every colour-cache size the encoder may pick (RFC 9649 5.2.2: index = (0x1e35a7bd * argb) >>
+    (32 - bits), the cache holding every decoded pixel) decodes to the input"""
+    img = _images()[kind].astype(np.uint8)
+    assert np.array_equal(_roundtrip(img, tmp_path, bits, want_bits=bits), img)
+
+
+def test_vp8l_colour_cache_chosen_for_repeated_colours(tmp_path):
+    """the size choice (st_vp8l.cpp choose_cache_bits) takes a cache where colours repeat
+    without spatial correlation, and none for noise"""
+    img = _images()['palette_noise'].astype(np.uint8)
+    from PIL import Image
+    h, w, _ = img.shape
+    src, dst = tmp_path / 'in.rgba', tmp_path / 'out.webp'
+    img.tofile(src)
+    r = subprocess.run([_harness(), str(src), str(w), str(h), str(dst)], capture_output=True, text=True, check=True)
+    assert 'cache_bits 0' not in r.stderr, r.stderr
+    assert np.array_equal(np.array(Image.open(dst).convert('RGBA')), img)
+    size_cache = os.path.getsize(dst)
+    subprocess.run([_harness(), str(src), str(w), str(h), str(dst), '0'], check=True, capture_output=True)
+    assert size_cache < os.path.getsize(dst)
+    noise = _images()['random'].astype(np.uint8)
+    h, w, _ = noise.shape
+    noise.tofile(src)
+    r = subprocess.run([_harness(), str(src), str(w), str(h), str(dst)], capture_output=True, text=True, check=True)
+    assert 'cache_bits 0' in r.stderr, r.stderr
 
 
 def test_vp8l_header_decodes_sog_textures(tmp_path):

@@ -155,3 +155,54 @@ def test_sog_bundle_device_view_matches_copy(ctx):
     assert ctypes.string_at(addr, size) == z
     host, _ = ctx.sog_bundle(g.table('b_sh1_in_'), c['iters'], draws, t, d)
     assert host == z
+
+
+def _harness_encode(img, tmp_path):
+    """the scalar emulation of the device kernels around the product's header code
+    (tests/native/vp8l_cpu_check.cpp), choosing the colour cache the same way"""
+    import subprocess
+    from test_sog_container_cpu import _harness
+    h, w = img.shape[:2]
+    src, dst = tmp_path / 'in.rgba', tmp_path / 'out.webp'
+    np.ascontiguousarray(img, np.uint8).tofile(src)
+    r = subprocess.run([_harness(), str(src), str(w), str(h), str(dst)], capture_output=True, text=True, check=True)
+    return dst.read_bytes(), int(r.stderr.split('cache_bits ')[1].split()[0])
+
+
+def _palette_scene(h, w, seed):
+    """runs of a few hundred repeating colours with smooth stretches between them: colour-cache
+    hits whose last writer lies many 4,096-pixel groups (and scan chunks) back"""
+    rng = np.random.default_rng(seed)
+    pal = rng.integers(0, 256, (300, 4)).astype(np.uint8)
+    pal[:, 3] = 255
+    img = pal[rng.integers(0, 300, (h, w))]
+    y, x = np.mgrid[0:h, 0:w]
+    band = (y // 37) % 3 == 0
+    img[band, 0] = (x[band] * 3) % 256
+    img[band, 1] = (y[band] * 2) % 256
+    rare = rng.random((h, w)) < 0.0005  # colours seen once, then again far later
+    img[rare] = pal[0]
+    return img
+
+
+def test_webp_matches_scalar_emulation_with_colour_cache(ctx, tmp_path):
+    """the device stream equals the scalar emulation byte for byte (the same predictors, copies,
+    colour-cache hits across groups and scan chunks, cache size and prefix codes), and a cache is
+    taken where colours repeat"""
+    cases = dict(_images())
+    cases['palette_scene'] = _palette_scene(700, 1000, 3)
+    g = Golden('sog')
+    for case in g.meta['cases']:
+        for f in ('means_l', 'means_u', 'scales', 'shN_labels'):
+            key = f"{case['name']}_{f}"
+            if key in g:
+                cases[key] = g[key]
+    used = 0
+    for name, img in cases.items():
+        img = np.ascontiguousarray(img, np.uint8)
+        want, bits = _harness_encode(img, tmp_path)
+        got = _dev_encode(ctx, img)
+        assert got == want, name
+        assert np.array_equal(_decode(got), img), name
+        used += bits > 0
+    assert used >= 3

@@ -48,7 +48,7 @@ def main(n=10_000_000, reps=3, pil=True):
         ctx.dev_sog_bundle_view(meta, n, tex, 0, 0)  # archive lands in pinned host memory, no copy
     wall = (time.perf_counter() - t0) / reps
     kern = {}
-    for k in ('webp.predict', 'webp.hist', 'webp.bits', 'webp.emit', 'crc32'):
+    for k in ('webp.predict', 'webp.hist', 'webp.cache', 'webp.bits', 'webp.emit', 'crc32'):
         ms, cnt = ctx.kernel_stats(k)
         kern[k] = {'ms_per_bundle': ms / reps, 'launches_per_bundle': cnt // reps}
     ctx.set_profiling(False)
