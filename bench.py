@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument('--no-e2e', action='store_true', help='skip the PLY file -> .sog file measurement (N = 1)')
     ap.add_argument('--no-paths', action='store_true', help='skip the config-3 stage table (N = 1)')
     ap.add_argument('--no-verify', action='store_true', help='skip the output verification of the last step')
+    ap.add_argument('--verify-sample', action='store_true',
+                    help='verify 4,096 sampled labels instead of every label of the last assign')
     ap.add_argument('--dist', action='store_true', help='N = 1 through the sharded code path (st_dev_sog_sharded '
                     'over a one-rank RCCL communicator) instead of st_dev_sog: its per-rank cost')
     ap.add_argument('--dist-python', action='store_true', help='the sharded path through splat_dist.py '
@@ -415,6 +417,50 @@ def check_labels(sh, prev, lab, n_labels, g):
     return bad, ties
 
 
+def check_all_labels(sh, prev, lab, tile=8192):
+    """every point: is its label the exact f64 argmin over `prev` (kd-tree.ts:26-33)?  Scores
+    |c|^2 - 2 p.c from an f64 GEMM (torch, independent of the library's kernels) decide every
+    point whose two best scores are apart by more than twice a bound on the GEMM's error; the
+    others take the reference's own distance (sequential f64 sum of (c - p)^2 over the dims)
+    against every centroid within that window.  Returns (wrong labels, exact ties unchecked,
+    points decided by the sequential distances)."""
+    import torch
+    d, k = prev.shape
+    n = lab.shape[0]
+    cd = prev.double()
+    cn = (cd * cd).sum(0)
+    cmax = float(cn.max().sqrt())
+    # |fl(s) - s| <= ~(d + 2) u (|c|^2 + 2 |p| |c|) for each score, u = 2^-53; 64x that margin
+    rel = 64 * (d + 2) * 2.0 ** -53
+    bad = ties = slow = 0
+    lab64 = lab.long()
+    for s in range(0, n, tile):
+        e = min(n, s + tile)
+        p = sh[:, s:e].double()
+        pn = (p * p).sum(0).sqrt()
+        score = torch.addmm(cn[None, :], p.t(), cd, beta=1.0, alpha=-2.0)
+        top = score.topk(2, dim=1, largest=False)
+        m1, i1, m2 = top.values[:, 0], top.indices[:, 0], top.values[:, 1]
+        w = rel * (cmax * cmax + 2 * pn * cmax)
+        clear = (m2 - m1) > 2 * w
+        bad += int(((lab64[s:e] != i1) & clear).sum().item())
+        amb = torch.nonzero(~clear).squeeze(1)
+        slow += amb.numel()
+        for a in amb.tolist():  # rare: the reference's own distances over the window's rows
+            cand = torch.nonzero(score[a] <= m1[a] + 2 * w[a]).squeeze(1)
+            dist = torch.zeros(cand.numel(), dtype=torch.float64, device=sh.device)
+            for j in range(d):
+                v = cd[j, cand] - p[j, a]
+                dist = dist + v * v
+            mn = dist.min()
+            if int((dist == mn).sum().item()) > 1:
+                ties += 1
+                continue
+            bad += int(int(cand[int(torch.argmin(dist).item())].item()) != int(lab64[s + a].item()))
+        del score, top
+    return bad, ties, slow
+
+
 def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7):
     """the sharded step's output (every rank): the library's k-means snapshot on a re-run; this
     rank's sampled labels are exact f64 argmins over the last assign's centroids, every rank holds
@@ -448,7 +494,7 @@ def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7):
                    'each rank checks sampled labels as exact f64 argmins over the last assign\'s centroids'}
 
 
-def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
+def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7, all_labels=False):
     """Re-run the step with the library's k-means snapshot on (outside the timed region) and
     check its output against the reference's definitions (k-means.ts:137-201, kd-tree.ts:22-70):
       * the textures equal those of the last timed step (the verified step IS the timed one);
@@ -457,7 +503,8 @@ def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
         decides) is counted, not checked;
       * sampled centroids are the f32-rounded sequential f64 means of their members in
         ascending point order (calcAverage, k-means.ts:41-63);
-      * every shN_labels texel holds the label of the row at its Morton position."""
+      * every shN_labels texel holds the label of the row at its Morton position.
+    all_labels: every label instead of a sample (check_all_labels, a few seconds at 10M)."""
     import numpy as np
     import torch
     dev = cols['x'].device
@@ -476,7 +523,12 @@ def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
     sh = torch.stack([cols[f'f_rest_{i}'] for i in range(d)])  # [d, n] f32
     g = torch.Generator(device='cpu')
     g.manual_seed(seed)
-    bad_labels, ties = check_labels(sh, prev, lab, n_labels, g)
+    slow = None
+    if all_labels:
+        bad_labels, ties, slow = check_all_labels(sh, prev, lab)
+        n_labels = n
+    else:
+        bad_labels, ties = check_labels(sh, prev, lab, n_labels, g)
     lab64 = lab.long()
     # centroids: sequential f64 mean of the members (numpy cumsum is a left-to-right chain)
     counts = torch.bincount(lab64, minlength=k)
@@ -498,12 +550,15 @@ def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7):
     tl = t[:, 0] | (t[:, 1] << 8)
     bad_texels = int((tl != (lab64[order.long()] & 0xffff)).sum().item())
     ok = same and bad_labels == 0 and bad_cen == 0 and bad_texels == 0
-    return {'ok': ok, 'textures_equal_timed_step': same, 'labels_checked': n_labels, 'labels_wrong': bad_labels,
-            'label_exact_ties_unchecked': ties, 'clusters_checked': len(pick), 'centroid_values_wrong': bad_cen,
-            'empty_clusters': int((counts == 0).sum().item()), 'texel_labels_checked': n,
-            'texel_labels_wrong': bad_texels,
-            'how': 'snapshot of the SH palette k-means (st_ctx_set_verify) on a re-run of the step; f64 argmin '
-                   'over the last assign\'s centroids, sequential f64 member means, Morton texel placement'}
+    out = {'ok': ok, 'textures_equal_timed_step': same, 'labels_checked': n_labels, 'labels_wrong': bad_labels,
+           'label_exact_ties_unchecked': ties, 'clusters_checked': len(pick), 'centroid_values_wrong': bad_cen,
+           'empty_clusters': int((counts == 0).sum().item()), 'texel_labels_checked': n,
+           'texel_labels_wrong': bad_texels,
+           'how': 'snapshot of the SH palette k-means (st_ctx_set_verify) on a re-run of the step; f64 argmin '
+                  'over the last assign\'s centroids, sequential f64 member means, Morton texel placement'}
+    if slow is not None:
+        out['labels_decided_by_sequential_distance'] = slow
+    return out
 
 
 def ctypes_char_array(size):
@@ -803,7 +858,7 @@ def main(args):
     progress('stage table and verification')
     if not args.no_verify:
         if not sharded:
-            verification = verify_step(ctx, tabs[0], tex, step)
+            verification = verify_step(ctx, tabs[0], tex, step, all_labels=not args.verify_sample)
         elif not args.dist_python:
             local_sh = torch.stack([torch.cat([t[f'f_rest_{i}'] for t in tabs]) for i in range(45)])
             verification = verify_sharded(ctx, local_sh, tex, step)

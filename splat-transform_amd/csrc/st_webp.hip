@@ -920,6 +920,9 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         for (int q = 0; q < vp8l::kTabSize; ++q) merged[q] = h[q] + h[vp8l::kTabSize + q];
         cbits[j] = vp8l::choose_cache_bits(merged.data(), (const uint32_t *)(hp + stage[j].hitlit),
                                            (const uint32_t *)(hp + stage[j].cidx));
+        if (getenv("ST_DEBUG"))
+            fprintf(stderr, "[st webp] image %d (%d x %d): predictor %s, colour cache bits %d\n", j, jobs[j].w,
+                    jobs[j].h, forced[j] ? "none" : "per block", cbits[j]);
         if (!cbits[j]) continue;
         rehist = true;
         WebpJob &jb = jobs[j];
