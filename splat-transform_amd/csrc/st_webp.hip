@@ -14,16 +14,14 @@
 //   k_vp8l_runs     per 4,096-pixel group: runs of >= 3 residuals equal to their left
 //                   neighbour become one LZ77 copy (distance code 2: the pixel to the
 //                   left; length <= 4,096), tokens: literal / copy length / covered
-//   k_cc_walk       colour cache (RFC 9649 5.2.2), all candidate sizes 2^4..2^10 at once: per
-//                   4,096-pixel group one wave whose lanes 0..6 each replay one cache size over
-//                   the group's pixels in order (LDS table; reads and writes issued back to
-//                   back, the compares after), so a pixel hits when the last earlier pixel of
-//                   the group with its index has its colour; a pixel whose index is new in the
-//                   group is left to k_cc_fix.  Writes the group's final cache per size (with
-//                   written flags) and each index's first pixel            read 4 B, write 1 B
-//   k_cc_scan1/2    the cache state at each group's start: per index, the last group before it
-//                   that wrote the index (a carry scan over chunks of 64 groups, then over chunks)
-//   k_cc_fix        the first pixel of each index in each group against that state
+//   k_cc_tab        colour cache (RFC 9649 5.2.2), all candidate sizes 2^4..2^10 at once: per
+//                   4,096-pixel group, the last colour written to each cache slot  read 4 B
+//   k_cc_scan1/2    the cache state at each group's start: per slot, the last group before it
+//                   that wrote the slot (a carry scan over chunks of 64 groups, then over chunks)
+//   k_cc_walk       per group one wave whose lanes 0..6 each replay one cache size over the
+//                   group's pixels in order from that state (LDS table; reads and writes issued
+//                   back to back, the compares after): a pixel hits when the last earlier pixel
+//                   with its index has its colour                      read 4 B, write 1 B
 //   k_cc_survey     per size, the literals' hits as histograms: the host picks the size
 //                   (vp8l::choose_cache_bits) and k_vp8l_hist redoes the histograms with it
 //   k_vp8l_hist     symbol histograms (literal channels, length prefixes, cache indices,
@@ -529,68 +527,30 @@ constexpr int CC_SLOTS = vp8l::kCacheSlots;  // the slots of every candidate siz
 constexpr uint32_t CC_CHUNK = 64;            // groups per carry-scan chunk
 constexpr uint64_t CC_SET = 1ull << 32;      // a table entry: CC_SET | colour once written, else 0
 
-// one wave per EMIT_PIX group; lane l < kCacheLevels replays the 2^(kMinCacheBits + l)-entry cache.
-// hits[p] bit l: pixel p's colour is in that cache (the last earlier pixel of the group with the
-// same index has it); an index new in the group leaves the bit to k_cc_fix.  W: the group's last
-// colour per slot (CC_SET | colour, or 0); F: 1 + the group position of the slot's first pixel
-// (stored as it is met: at most one store per slot and group).
-__global__ __launch_bounds__(64) void k_cc_walk(const uint32_t *__restrict__ resid, uint64_t npix,
-                                                uint8_t *__restrict__ hits, uint64_t *__restrict__ W,
-                                                uint32_t *__restrict__ F) {
-    // lanes >= kCacheLevels replay nothing: they read and write a private slot past the table,
-    // so the step loop has no exec-mask branches
-    __shared__ uint64_t cache[CC_SLOTS + 64];
-    const int lane = threadIdx.x;
-    for (int j = lane; j < CC_SLOTS + 64; j += 64) cache[j] = 0;
+// W[g][j]: the colour of the last pixel of group g with cache slot j (every candidate size at
+// once), CC_SET | colour, or 0 when no pixel of the group has that slot: the largest position per
+// slot by LDS atomicMax, then its colour
+__global__ __launch_bounds__(256) void k_cc_tab(const uint32_t *__restrict__ resid, uint64_t npix,
+                                                uint64_t *__restrict__ W) {
+    __shared__ uint32_t last[CC_SLOTS];
+    for (int j = threadIdx.x; j < CC_SLOTS; j += 256) last[j] = 0;
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * EMIT_PIX;
     const uint32_t cnt = (uint32_t)min((uint64_t)EMIT_PIX, npix - g0);
-    const bool act = lane < vp8l::kCacheLevels;
-    const int bits = vp8l::kMinCacheBits + (act ? lane : 0);
-    const uint32_t base = (uint32_t)vp8l::cache_off(bits), own = (uint32_t)CC_SLOTS + lane;
-    uint32_t *Fg = F + (uint64_t)blockIdx.x * CC_SLOTS;  // zeroed by the caller
-    constexpr uint32_t LEVEL_MASK = (1u << vp8l::kCacheLevels) - 1;
-    constexpr int SUB = 16;  // steps whose LDS reads and writes are issued before their compares
-    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-        const uint32_t m = min(64u, cnt - i0);
-        const uint32_t pv = (uint32_t)lane < m ? resid[g0 + i0 + lane] : 0u;
-        uint32_t mine = 0;  // lane q: the hit bits of pixel i0 + q
-        if (m == 64) {
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        const uint32_t h = resid[g0 + i] * vp8l::kCacheMul;
 #pragma unroll
-            for (int k0 = 0; k0 < 64; k0 += SUB) {
-                uint64_t e[SUB];
-                uint32_t slot[SUB];
-#pragma unroll
-                for (int u = 0; u < SUB; ++u) {
-                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
-                    slot[u] = act ? base + cc_index(c, bits) : own;
-                    e[u] = cache[slot[u]];
-                    cache[slot[u]] = CC_SET | c;
-                }
-#pragma unroll
-                for (int u = 0; u < SUB; ++u) {
-                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
-                    if (!e[u] && act) Fg[slot[u]] = i0 + k0 + u + 1;  // the slot's first pixel in the group
-                    const uint32_t hm = (uint32_t)__ballot(e[u] == (CC_SET | c)) & LEVEL_MASK;
-                    mine = lane == k0 + u ? hm : mine;
-                }
-            }
-        } else {  // the image's last, partial batch: one step at a time
-            for (uint32_t k = 0; k < m; ++k) {
-                const uint32_t c = (uint32_t)__shfl((int)pv, (int)k, 64);
-                const uint32_t slot = act ? base + cc_index(c, bits) : own;
-                const uint64_t e = cache[slot];
-                cache[slot] = CC_SET | c;
-                if (!e && act) Fg[slot] = i0 + k + 1;
-                const uint32_t hm = (uint32_t)__ballot(e == (CC_SET | c)) & LEVEL_MASK;
-                mine = (uint32_t)lane == k ? hm : mine;
-            }
+        for (int l = 0; l < vp8l::kCacheLevels; ++l) {
+            const int bits = vp8l::kMinCacheBits + l;
+            atomicMax(&last[vp8l::cache_off(bits) + (h >> (32 - bits))], i + 1);
         }
-        if ((uint32_t)lane < m) hits[g0 + i0 + lane] = (uint8_t)mine;
     }
     __syncthreads();
     uint64_t *Wg = W + (uint64_t)blockIdx.x * CC_SLOTS;
-    for (int j = lane; j < CC_SLOTS; j += 64) Wg[j] = cache[j];
+    for (int j = threadIdx.x; j < CC_SLOTS; j += 256) {
+        const uint32_t q = last[j];
+        Wg[j] = q ? (CC_SET | resid[g0 + q - 1]) : 0ull;
+    }
 }
 
 // W[g][j] <- the last written entry of the groups before g in g's chunk (0: none); A[chunk][j] <-
@@ -621,23 +581,69 @@ __global__ __launch_bounds__(256) void k_cc_scan2(uint64_t *__restrict__ A, uint
     }
 }
 
-// the first pixel of slot j in group g hits when the cache entry at the group's start (the scans)
-// holds its colour; an entry no earlier pixel wrote counts as a miss (the zero-initialised cache
-// is not relied on)
-__global__ __launch_bounds__(256) void k_cc_fix(const uint32_t *__restrict__ resid, const uint64_t *__restrict__ W,
-                                                const uint64_t *__restrict__ A, const uint32_t *__restrict__ F,
+// one wave per EMIT_PIX group; lane l < kCacheLevels replays the 2^(kMinCacheBits + l)-entry cache
+// over the group's pixels in order, starting from the cache as the earlier groups left it (the
+// scans).  A slot no earlier pixel wrote starts with a colour whose own index is another slot, so
+// no pixel can match it (the zero-initialised cache is not relied on): hits[p] bit l exactly when
+// the last earlier pixel with p's index has p's colour.
+__global__ __launch_bounds__(64) void k_cc_walk(const uint32_t *__restrict__ resid, uint64_t npix,
+                                                const uint64_t *__restrict__ W, const uint64_t *__restrict__ A,
                                                 uint8_t *__restrict__ hits) {
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= (uint32_t)CC_SLOTS) return;
-    const uint64_t g = blockIdx.y;
-    const uint32_t f = F[g * CC_SLOTS + j];
-    if (!f) return;
-    uint64_t e = W[g * CC_SLOTS + j];
-    if (!e) e = A[(g / CC_CHUNK) * CC_SLOTS + j];
-    const uint64_t p = g * EMIT_PIX + f - 1;
-    if (e && (uint32_t)e == resid[p]) {
-        const uint32_t level = (31 - __builtin_clz(j + (1u << vp8l::kMinCacheBits))) - vp8l::kMinCacheBits;
-        atomicOr(reinterpret_cast<uint32_t *>(hits + (p & ~3ull)), (1u << level) << (8 * (p & 3)));
+    // lanes >= kCacheLevels replay nothing: they read and write a private slot past the table,
+    // so the step loop has no exec-mask branches
+    __shared__ uint32_t cache[CC_SLOTS + 64];
+    const int lane = threadIdx.x;
+    const uint64_t g = blockIdx.x;
+    for (int j = lane; j < CC_SLOTS; j += 64) {
+        uint64_t e = W[g * CC_SLOTS + j];
+        if (!e) e = A[(g / CC_CHUNK) * CC_SLOTS + j];
+        const int bits = 31 - __builtin_clz((uint32_t)j + (1u << vp8l::kMinCacheBits));
+        const uint32_t idx = (uint32_t)j - (uint32_t)vp8l::cache_off(bits);
+        // index(0) = 0 and index(1) = 0x1e35a7bd >> (32 - bits) != 0: 1 where index 0, else 0
+        cache[j] = e ? (uint32_t)e : (idx == 0 ? 1u : 0u);
+    }
+    cache[CC_SLOTS + lane] = 0;
+    __syncthreads();
+    const uint64_t g0 = g * EMIT_PIX;
+    const uint32_t cnt = (uint32_t)min((uint64_t)EMIT_PIX, npix - g0);
+    const bool act = lane < vp8l::kCacheLevels;
+    const int bits = vp8l::kMinCacheBits + (act ? lane : 0);
+    const uint32_t base = (uint32_t)vp8l::cache_off(bits), own = (uint32_t)CC_SLOTS + lane;
+    constexpr uint32_t LEVEL_MASK = (1u << vp8l::kCacheLevels) - 1;
+    constexpr int SUB = 16;  // steps whose LDS reads and writes are issued before their compares
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+        const uint32_t m = min(64u, cnt - i0);
+        const uint32_t pv = (uint32_t)lane < m ? resid[g0 + i0 + lane] : 0u;
+        uint32_t mine = 0;  // lane q: the hit bits of pixel i0 + q
+        if (m == 64) {
+#pragma unroll
+            for (int k0 = 0; k0 < 64; k0 += SUB) {
+                uint32_t e[SUB];
+#pragma unroll
+                for (int u = 0; u < SUB; ++u) {
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
+                    const uint32_t slot = act ? base + cc_index(c, bits) : own;
+                    e[u] = cache[slot];
+                    cache[slot] = c;
+                }
+#pragma unroll
+                for (int u = 0; u < SUB; ++u) {
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pv, k0 + u);
+                    const uint32_t hm = (uint32_t)__ballot(e[u] == c) & LEVEL_MASK;
+                    mine = lane == k0 + u ? hm : mine;
+                }
+            }
+        } else {  // the image's last, partial batch: one step at a time
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t c = (uint32_t)__shfl((int)pv, (int)k, 64);
+                const uint32_t slot = act ? base + cc_index(c, bits) : own;
+                const uint32_t e = cache[slot];
+                cache[slot] = c;
+                const uint32_t hm = (uint32_t)__ballot(e == c) & LEVEL_MASK;
+                mine = (uint32_t)lane == k ? hm : mine;
+            }
+        }
+        if ((uint32_t)lane < m) hits[g0 + i0 + lane] = (uint8_t)mine;
     }
 }
 
@@ -810,13 +816,12 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         stage.push_back(st);
         pin = (st.cidx + (size_t)CC_SLOTS * 4 + 255) & ~(size_t)255;
     }
-    // colour-cache tables, shared by the jobs (one stream: each job's walk, scans and fix-up run
-    // before the next job's walk)
+    // colour-cache tables, shared by the jobs (one stream: each job's tables, scans and walk run
+    // before the next job's)
     uint32_t max_groups = 1;
     for (int j = 0; j < njobs; ++j)
         max_groups = std::max(max_groups, (uint32_t)(((uint64_t)jobs[j].w * jobs[j].h + EMIT_PIX - 1) / EMIT_PIX));
     uint64_t *ccW = wsT<uint64_t>(c, "wp.ccw", (size_t)max_groups * CC_SLOTS);
-    uint32_t *ccF = wsT<uint32_t>(c, "wp.ccf", (size_t)max_groups * CC_SLOTS);
     uint64_t *ccA = wsT<uint64_t>(c, "wp.cca", (size_t)((max_groups + CC_CHUNK - 1) / CC_CHUNK) * CC_SLOTS);
     // phase A: predictors, residuals, tokens, group flags, histograms (raw = the pixels as no
     // predictor leaves them, for the choice below)
@@ -874,11 +879,10 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
             KTimer kt(c, "webp.cache");
             const uint32_t nch = (ngrp + CC_CHUNK - 1) / CC_CHUNK;
             const unsigned sb = (CC_SLOTS + 255) / 256;
-            ST_HIP(hipMemsetAsync(ccF, 0, (size_t)ngrp * CC_SLOTS * 4, c->stream));
-            hipLaunchKernelGGL(k_cc_walk, dim3(ngrp), dim3(64), 0, c->stream, resid, npix, hits, ccW, ccF);
+            hipLaunchKernelGGL(k_cc_tab, dim3(ngrp), dim3(256), 0, c->stream, resid, npix, ccW);
             hipLaunchKernelGGL(k_cc_scan1, dim3(sb, nch), dim3(256), 0, c->stream, ccW, ngrp, ccA);
             hipLaunchKernelGGL(k_cc_scan2, dim3(sb), dim3(256), 0, c->stream, ccA, nch);
-            hipLaunchKernelGGL(k_cc_fix, dim3(sb, ngrp), dim3(256), 0, c->stream, resid, ccW, ccA, ccF, hits);
+            hipLaunchKernelGGL(k_cc_walk, dim3(ngrp), dim3(64), 0, c->stream, resid, npix, ccW, ccA, hits);
             hipLaunchKernelGGL(k_cc_survey, dim3(grid_for(npix, 256 * 16, 2048)), dim3(256), 0, c->stream, resid, tok,
                                hits, npix, hitlit, cidx);
             ST_LAUNCH_CHECK();
