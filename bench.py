@@ -461,10 +461,11 @@ def check_all_labels(sh, prev, lab, tile=8192):
     return bad, ties, slow
 
 
-def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7):
+def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7, all_labels=False):
     """the sharded step's output (every rank): the library's k-means snapshot on a re-run; this
-    rank's sampled labels are exact f64 argmins over the last assign's centroids, every rank holds
-    the same final centroids, and rank 0's textures equal the last timed step's"""
+    rank's labels (sampled, or all with all_labels) are exact f64 argmins over the last assign's
+    centroids, every rank holds the same final centroids, and rank 0's textures equal the last
+    timed step's"""
     import torch
     import torch.distributed as dist
     before = {k: v.clone() for k, v in tex.items()} if tex else None
@@ -478,20 +479,24 @@ def verify_sharded(ctx, local_sh, tex, step, n_labels=2048, seed=7):
     prev, cen, lab = ctx.verify_snapshot(local_sh.device)
     g = torch.Generator(device='cpu')
     g.manual_seed(seed + dist.get_rank())
-    bad, ties = check_labels(local_sh, prev, lab, n_labels, g)
+    if all_labels:
+        bad, ties, _ = check_all_labels(local_sh, prev, lab)
+        n_labels = lab.shape[0]
+    else:
+        bad, ties = check_labels(local_sh, prev, lab, n_labels, g)
     ref = cen.clone()
     dist.broadcast(ref, 0)
     same_cen = bool(torch.equal(ref, cen))
-    t = torch.tensor([bad, ties, 0 if same else 1, 0 if same_cen else 1], dtype=torch.float64,
+    t = torch.tensor([bad, ties, 0 if same else 1, 0 if same_cen else 1, n_labels], dtype=torch.float64,
                      device=local_sh.device)
     dist.all_reduce(t)
     same_cen = int(t[3].item()) == 0
     ok = int(t[0].item()) == 0 and int(t[2].item()) == 0 and same_cen
-    return {'ok': ok, 'labels_checked': n_labels * dist.get_world_size(), 'labels_wrong': int(t[0].item()),
+    return {'ok': ok, 'labels_checked': int(t[4].item()), 'labels_wrong': int(t[0].item()),
             'label_exact_ties_unchecked': int(t[1].item()), 'textures_equal_timed_step': int(t[2].item()) == 0,
             'centroids_identical_on_every_rank': same_cen,
             'how': 'snapshot of the sharded SH palette k-means (st_ctx_set_verify) on a re-run of the step; '
-                   'each rank checks sampled labels as exact f64 argmins over the last assign\'s centroids'}
+                   'each rank checks its labels as exact f64 argmins over the last assign\'s centroids'}
 
 
 def verify_step(ctx, cols, tex, step, n_labels=4096, n_clusters=64, seed=7, all_labels=False):
@@ -861,7 +866,7 @@ def main(args):
             verification = verify_step(ctx, tabs[0], tex, step, all_labels=not args.verify_sample)
         elif not args.dist_python:
             local_sh = torch.stack([torch.cat([t[f'f_rest_{i}'] for t in tabs]) for i in range(45)])
-            verification = verify_sharded(ctx, local_sh, tex, step)
+            verification = verify_sharded(ctx, local_sh, tex, step, all_labels=not args.verify_sample)
             del local_sh
 
     # N > 1: the weak-scaling record (10M splats per GPU) beside the strong one
