@@ -335,10 +335,14 @@ int choose_cache_bits(const uint32_t *hist, const uint32_t *hitlit, const uint32
         for (int ch = 0; ch < 3; ++ch) c.est += shannon(c.rba.data() + ch * 256, 256);
         cand.push_back(std::move(c));
     }
-    // the coded size (descriptions + symbols) of no cache and the two best estimates
+    // the coded size (descriptions + symbols) of no cache and the two best estimates, when the
+    // estimates are within 2% of each other (otherwise the estimate decides)
     std::vector<int> order(cand.size());
     for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
     std::stable_sort(order.begin() + 1, order.end(), [&](int a, int b) { return cand[a].est < cand[b].est; });
+    const double e0 = cand[0].est, e1 = cand[order[1]].est;
+    if (e1 < 0.98 * e0) return cand[order[1]].bits;
+    if (e1 > 1.02 * e0) return 0;
     int best = 0;
     double bc = 0;
     for (int k = 0; k < 3 && k < (int)order.size(); ++k) {

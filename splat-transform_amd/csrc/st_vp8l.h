@@ -84,7 +84,8 @@ double literal_bits(const uint32_t *hist);
 // kCacheSlots counts of the hitting literals' cache indices per level (cache_off layout).
 // Returns 0 or the bits whose coded size is the smallest (prefix-code descriptions plus coded
 // symbols of the green, red, blue and alpha alphabets, as one prefix-code group would code them),
-// among no cache and the two sizes with the smallest Shannon estimates.
+// among no cache and the two sizes with the smallest Shannon estimates (the estimates alone
+// decide when the best cache size and no cache are more than 2% apart).
 int choose_cache_bits(const uint32_t *hist, const uint32_t *hitlit, const uint32_t *cidx);
 
 }  // namespace vp8l

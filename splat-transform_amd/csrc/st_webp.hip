@@ -37,6 +37,8 @@
 // the XOR of all shifted CRCs is the CRC of the buffer.
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 #include "st_internal.h"
 #include "st_vp8l.h"
@@ -784,6 +786,25 @@ uint64_t webp_max_size(int w, int h) {
     return 20 + 4096 + (blocks * 15 + 7) / 8 + (npix * 60 + 7) / 8 + 16;
 }
 
+// host work of several images at once (prefix codes, headers): one thread per image, the
+// first exception rethrown after all have joined
+template <typename F>
+static void per_job(int njobs, F fn) {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(njobs);
+    for (int j = 0; j < njobs; ++j)
+        th.emplace_back([&, j] {
+            try {
+                fn(j);
+            } catch (...) {
+                err[j] = std::current_exception();
+            }
+        });
+    for (auto &t : th) t.join();
+    for (auto &e : err)
+        if (e) std::rethrow_exception(e);
+}
+
 void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     // per job in pinned staging: group histograms, the raw histogram, predictor modes, group
     // flags, the colour-cache survey (hit literals per size, cache indices)
@@ -917,13 +938,15 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     // per image: the colour-cache size; with a cache, the histograms again (a hitting literal is
     // one green symbol)
     std::vector<int> cbits(njobs, 0);
-    bool rehist = false;
-    for (int j = 0; j < njobs; ++j) {
+    per_job(njobs, [&](int j) {
         const uint32_t *h = (const uint32_t *)(hp + stage[j].hist);
         std::vector<uint32_t> merged(vp8l::kTabSize);
         for (int q = 0; q < vp8l::kTabSize; ++q) merged[q] = h[q] + h[vp8l::kTabSize + q];
         cbits[j] = vp8l::choose_cache_bits(merged.data(), (const uint32_t *)(hp + stage[j].hitlit),
                                            (const uint32_t *)(hp + stage[j].cidx));
+    });
+    bool rehist = false;
+    for (int j = 0; j < njobs; ++j) {
         if (getenv("ST_DEBUG"))
             fprintf(stderr, "[st webp] image %d (%d x %d): predictor %s, colour cache bits %d\n", j, jobs[j].w,
                     jobs[j].h, forced[j] ? "none" : "per block", cbits[j]);
@@ -951,7 +974,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     // host: prefix codes + header bits (two groups when some block holds a literal alpha residual)
     std::vector<vp8l::Header> hdr(njobs);
     std::vector<int> ngroups(njobs, 1);
-    for (int j = 0; j < njobs; ++j) {
+    per_job(njobs, [&](int j) {
         int bw, bh, gw, gh;
         geom(jobs[j], bw, bh, gw, gh);
         const uint32_t *hist = (const uint32_t *)(hp + stage[j].hist);
@@ -974,7 +997,7 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
             vp8l::build_header(jobs[j].w, jobs[j].h, alpha_used, merged.data(), 1, flags, GROUP_BITS, modes, cbits[j],
                                hdr[j]);
         }
-    }
+    });
     // phase C: bit counts, offsets, emission
     std::vector<std::vector<uint8_t>> head(njobs);
     std::vector<std::string> tags(njobs);
