@@ -439,8 +439,12 @@ def check_all_labels(sh, prev, lab, tile=8192):
         p = sh[:, s:e].double()
         pn = (p * p).sum(0).sqrt()
         score = torch.addmm(cn[None, :], p.t(), cd, beta=1.0, alpha=-2.0)
-        top = score.topk(2, dim=1, largest=False)
-        m1, i1, m2 = top.values[:, 0], top.indices[:, 0], top.values[:, 1]
+        m1, i1 = score.min(1)
+        rows = torch.arange(e - s, device=sh.device)
+        best = score[rows, i1].clone()
+        score[rows, i1] = float('inf')
+        m2 = score.min(1).values
+        score[rows, i1] = best
         w = rel * (cmax * cmax + 2 * pn * cmax)
         clear = (m2 - m1) > 2 * w
         bad += int(((lab64[s:e] != i1) & clear).sum().item())
@@ -457,7 +461,7 @@ def check_all_labels(sh, prev, lab, tile=8192):
                 ties += 1
                 continue
             bad += int(int(cand[int(torch.argmin(dist).item())].item()) != int(lab64[s + a].item()))
-        del score, top
+        del score
     return bad, ties, slow
 
 
