@@ -120,7 +120,7 @@ def test_self_launched_two_ranks_match_one_gpu(tmp_path):
     """`bench.py --gpus 2 --backend gloo` (no torchrun on the command line) rehearsed on one GPU:
     two processes running the library's st_dev_sog_sharded over its host shared-memory transport,
     and the textures of the 4M-splat table equal one GPU's"""
-    common = ['--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-e2e', '--no-paths', '--no-verify']
+    common = ['--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-e2e', '--no-paths']
     env = dict(os.environ, PYTHONUNBUFFERED='1')
     r2 = subprocess.run([sys.executable, BENCH, '--gpus', '2', '--backend', 'gloo', '--no-weak',
                          '--splats', '2000000'] + common, capture_output=True, text=True, timeout=600, env=env)
@@ -128,7 +128,10 @@ def test_self_launched_two_ranks_match_one_gpu(tmp_path):
     two = json.loads(r2.stdout.strip().splitlines()[-1])
     assert two['config']['parallelism'] == 'rowshard2-native' and two['transport'] == 'host-shm'
     assert 'fallback' not in two
-    r1 = subprocess.run([sys.executable, BENCH, '--gpus', '1', '--splats', '4000000'] + common,
+    # each rank checked every label of its shard against the reference's definitions
+    assert two['verified'] and two['verification']['labels_checked'] == 4_000_000, two['verification']
+    assert two['verification']['centroids_identical_on_every_rank']
+    r1 = subprocess.run([sys.executable, BENCH, '--gpus', '1', '--splats', '4000000'] + common + ['--no-verify'],
                         capture_output=True, text=True, timeout=600, env=env)
     assert r1.returncode == 0, r1.stderr[-4000:]
     one = json.loads(r1.stdout.strip().splitlines()[-1])
