@@ -450,17 +450,22 @@ def check_all_labels(sh, prev, lab, tile=8192):
         bad += int(((lab64[s:e] != i1) & clear).sum().item())
         amb = torch.nonzero(~clear).squeeze(1)
         slow += amb.numel()
-        for a in amb.tolist():  # rare: the reference's own distances over the window's rows
-            cand = torch.nonzero(score[a] <= m1[a] + 2 * w[a]).squeeze(1)
-            dist = torch.zeros(cand.numel(), dtype=torch.float64, device=sh.device)
-            for j in range(d):
-                v = cd[j, cand] - p[j, a]
+        for a0 in range(0, amb.numel(), 1024):  # the reference's own distances over the windows' rows
+            a = amb[a0:a0 + 1024]
+            row, col = torch.nonzero(score[a] <= (m1[a] + 2 * w[a])[:, None], as_tuple=True)
+            dist = torch.zeros(row.numel(), dtype=torch.float64, device=sh.device)
+            for j in range(d):  # dimension by dimension, as kd-tree.ts:26-33 sums
+                v = cd[j, col] - p[j, a[row]]
                 dist = dist + v * v
-            mn = dist.min()
-            if int((dist == mn).sum().item()) > 1:
-                ties += 1
-                continue
-            bad += int(int(cand[int(torch.argmin(dist).item())].item()) != int(lab64[s + a].item()))
+            mn = torch.full((a.numel(),), float('inf'), dtype=torch.float64, device=sh.device)
+            mn = mn.scatter_reduce(0, row, dist, reduce='amin')
+            at_min = dist == mn[row]
+            nmin = torch.zeros(a.numel(), dtype=torch.long, device=sh.device).scatter_add(0, row, at_min.long())
+            # the unique minimum's column per row (rows with a tie are counted, not checked)
+            win = torch.full((a.numel(),), -1, dtype=torch.long, device=sh.device)
+            win = win.scatter_reduce(0, row[at_min], col[at_min], reduce='amax')
+            ties += int((nmin > 1).sum().item())
+            bad += int(((nmin == 1) & (win != lab64[s + a])).sum().item())
         del score
     return bad, ties, slow
 

@@ -36,3 +36,24 @@ def test_check_all_labels_exact_wrong_and_ties():
     lab[100] = (lab[100] + 1) % k
     bad, _, _ = bench.check_all_labels(sh, cen, lab, tile=512)
     assert bad == 1
+
+
+def test_check_all_labels_many_exact_ties_vectorised():
+    """30% of the points sit on a centroid that has a duplicate (what the reference's KdTree
+    order decides): every one is counted as a tie, in one pass"""
+    import time
+    rng = np.random.default_rng(4)
+    d, k, n = 9, 64, 20000
+    cen = torch.from_numpy(rng.normal(size=(d, k)).astype(np.float32))
+    cen[:, 20] = cen[:, 5]
+    sh = torch.from_numpy(rng.normal(size=(d, n)).astype(np.float32))
+    dup = rng.random(n) < 0.3
+    sh[:, torch.from_numpy(dup)] = cen[:, 5:6]
+    dist = _exact(sh, cen)
+    lab = torch.from_numpy(dist.argmin(1).astype(np.int32))
+    want_ties = int(((dist == dist.min(1, keepdims=True)).sum(1) > 1).sum())  # also points nearest to 5 anyway
+    assert want_ties >= int(dup.sum())
+    t0 = time.time()
+    bad, ties, slow = bench.check_all_labels(sh, cen, lab, tile=4096)
+    assert bad == 0 and ties == want_ties and slow >= ties
+    assert time.time() - t0 < 60
