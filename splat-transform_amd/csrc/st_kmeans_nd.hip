@@ -1345,7 +1345,18 @@ __global__ __launch_bounds__(256) void k_nd_seq(const float *__restrict__ aos, i
     if (lane < d && cnt) {
         const int ld = aos_ld(d);
         double sum = 0;
-        for (uint32_t i = 0; i < cnt; ++i) sum += (double)aos[(uint64_t)m[i] * ld + lane];
+        // the member values move 8 at a time (independent loads in flight), the adds stay in
+        // point order
+        constexpr uint32_t U = 8;
+        uint32_t i = 0;
+        for (; i + U <= cnt; i += U) {
+            float v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = aos[(uint64_t)m[i + u] * ld + lane];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) sum += (double)v[u];
+        }
+        for (; i < cnt; ++i) sum += (double)aos[(uint64_t)m[i] * ld + lane];
         cen[(uint64_t)lane * k + cl] = (float)(sum / (double)cnt);
     }
     __syncthreads();  // m and cnt_s are reused by the next flagged cluster
