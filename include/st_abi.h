@@ -462,6 +462,15 @@ int st_dev_sog_bundle(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, cons
  * until the next bundle call on ctx; no copy) -- what a writer hands to write(2) */
 int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count, const st_sog_textures *tex,
                            uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *size);
+/* writeSog into a file (write-sog.ts:110-370 and the CLI's write of the .sog, index.ts:101-154):
+ * st_dev_sog with its archive streamed to the open file descriptor fd (written from offset 0) --
+ * the five textures that are final before the SH palette k-means (means_l/u, quats, scales,
+ * sh0) are WebP-encoded on a side context and written while the k-means runs, the shN
+ * textures, meta.json and the central directory after it.  The file holds the same bytes as
+ * st_dev_sog_bundle's archive; *size = its length.  The caller opens and closes fd. */
+int st_dev_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
+                    uint64_t *used, st_sog_meta *meta, const st_sog_textures *out, int32_t fd, uint16_t dos_time,
+                    uint16_t dos_date, uint64_t *size);
 /* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */
 int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                   uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);

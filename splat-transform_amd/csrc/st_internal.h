@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <functional>
 
 #include <cstdint>
 #include <map>
@@ -141,6 +142,9 @@ struct st_ctx {
     std::vector<hipEvent_t> event_pool;
     // side context on the same device (multi-GPU writeSog: rank 0's Morton order runs there)
     st_ctx *aux = nullptr;
+    // called by the SOG step once the five textures that precede the SH k-means are queued on
+    // the stream (sog_file_dev streams them to the file meanwhile); empty otherwise
+    std::function<void(st_ctx *)> sog_early;
     // st_ctx_set_verify: snapshot of the last N-D k-means (prev / final centroids, labels)
     bool verify = false;
     int vf_d = 0, vf_k = 0;

@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "st_internal.h"
+#include "st_webp.h"
 
 namespace st {
 
@@ -713,6 +714,19 @@ int st_dev_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws,
     });
 }
 
+int st_dev_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                    st_sog_meta *meta, const st_sog_textures *out, int32_t fd, uint16_t dos_time, uint16_t dos_date,
+                    uint64_t *size) {
+    return guarded([&] {
+        ST_ARG(c && meta && out && size && fd >= 0, "bad argument");
+        check_table(t);
+        use_device(c);
+        begin_timing(c);
+        uint64_t u = sog_file_dev(c, t, iters, draws, ndraws, meta, out, fd, dos_time, dos_date, size);
+        end_timing(c);
+        if (used) *used = u;
+    });
+}
 
 // ---- multi-GPU building blocks ------------------------------------------------------
 int st_dev_minmax(st_ctx *c, const float *const *cols, int32_t ncols, uint64_t n, double *lo, double *hi) {

@@ -556,6 +556,7 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
                            (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
     ST_LAUNCH_CHECK();
     mark(c, "sog.sh0");
+    if (c->sog_early) c->sog_early(c);  // means_l/u, quats, scales, sh0 are final on c->stream
 
     meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
     if (C > 0) {

@@ -29,6 +29,12 @@ void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const u
 // the next bundle call on this context)
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
                     uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size);
+// writeSog into an open file: the step (sog_dev) with the archive streamed to fd -- the five
+// textures final before the SH k-means encoded on the side context and written by a host thread
+// while the k-means runs; the same bytes as sog_bundle_dev's archive.  Returns the draws used.
+uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws,
+                      st_sog_meta *meta, const st_sog_textures *out, int fd, uint16_t dos_time, uint16_t dos_date,
+                      uint64_t *file_size);
 
 // ---- host: the .sog container (st_zip.cpp) ----------------------------------
 // JSON text of a JS number (Number::toString as JSON.stringify emits it; non-finite -> null)
@@ -48,5 +54,12 @@ uint64_t zip_size(const std::vector<ZipEntry> &entries);
 // entry i's bytes go
 void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf,
                uint64_t *data_off);
+// the pieces zip_write lays out, for a writer that streams the entries: one entry's local header
+// (returns its 30 + name bytes; independent of the entry's size and CRC), its 16-byte data
+// descriptor, and the central directory + end record of entries laid out in order from offset 0
+size_t zip_local(const ZipEntry &e, uint16_t dos_time, uint16_t dos_date, uint8_t *h);
+void zip_descriptor(const ZipEntry &e, uint8_t *d);
+uint64_t zip_central_size(const std::vector<ZipEntry> &entries);
+void zip_central(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf);
 
 }  // namespace st

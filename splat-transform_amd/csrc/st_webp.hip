@@ -35,6 +35,10 @@
 // CRC-32: each thread takes the zlib CRC of a 2 KiB span (slicing-by-8) and shifts it to the end
 // of the buffer (multiplication by x^(8m) mod P, zlib's crc32_combine identity);
 // the XOR of all shifted CRCs is the CRC of the buffer.
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -1132,6 +1136,151 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
     zip_write(es, dos_time, dos_date, buf, off.data());
     *out = buf;
     *out_size = total;
+}
+
+// ---- writeSog into a file, the archive streamed ------------------------------------------
+namespace {
+void write_at(int fd, const uint8_t *p, uint64_t n, uint64_t off) {
+    while (n) {
+        const ssize_t w = pwrite(fd, p, n, (off_t)off);
+        if (w < 0 && errno == EINTR) continue;
+        ST_REQUIRE(w > 0, ST_ERR_ARG, std::string("sog file: write failed: ") + std::strerror(errno));
+        p += w;
+        n -= (uint64_t)w;
+        off += (uint64_t)w;
+    }
+}
+
+struct Img {
+    const char *name;
+    const uint8_t *rgba;
+    int w, h;
+};
+
+// entries in order into one pinned block [local header, data, descriptor]...: the images' WebP
+// streams and `extra` host entries (meta.json), CRCs on the device; returns the block's bytes
+uint64_t stage_entries(st_ctx *c, const std::vector<Img> &imgs, const std::vector<std::string> &extra,
+                       const char *const *extra_names, uint16_t dos_time, uint16_t dos_date, const std::string &tag,
+                       std::vector<ZipEntry> &es, uint8_t **block) {
+    const int ni = (int)imgs.size(), ne = (int)extra.size();
+    std::vector<WebpJob> jobs(ni);
+    for (int i = 0; i < ni; ++i) {
+        ST_REQUIRE(imgs[i].rgba, ST_ERR_ARG, std::string("sog file: texture missing for ") + imgs[i].name);
+        const uint64_t cap = webp_max_size(imgs[i].w, imgs[i].h);
+        jobs[i] = {imgs[i].rgba, imgs[i].w, imgs[i].h, imgs[i].w * 4, wsT<uint8_t>(c, tag + std::to_string(i), cap),
+                   cap, 0};
+    }
+    if (ni) webp_encode_dev(c, jobs.data(), ni);
+    es.clear();
+    for (int i = 0; i < ni; ++i) es.push_back({imgs[i].name, jobs[i].size, 0});
+    for (int i = 0; i < ne; ++i) es.push_back({extra_names[i], extra[i].size(), 0});
+    uint64_t total = 0;
+    for (auto &e : es) total += 30 + e.name.size() + e.size + 16;
+    uint8_t *buf = (uint8_t *)pinned_slot(c, tag + "blk", total);
+    std::vector<uint64_t> off(es.size());
+    uint64_t o = 0;
+    for (size_t i = 0; i < es.size(); ++i) {
+        o += zip_local(es[i], dos_time, dos_date, buf + o);
+        off[i] = o;
+        o += es[i].size + 16;
+    }
+    std::vector<const uint8_t *> ptrs;
+    std::vector<uint64_t> lens;
+    for (int i = 0; i < ni; ++i) {
+        if (jobs[i].size)
+            ST_HIP(hipMemcpyAsync(buf + off[i], jobs[i].out, jobs[i].size, hipMemcpyDeviceToHost, c->stream));
+        ptrs.push_back(jobs[i].out);
+        lens.push_back(jobs[i].size);
+    }
+    for (int i = 0; i < ne; ++i) {
+        std::memcpy(buf + off[ni + i], extra[i].data(), extra[i].size());
+        uint8_t *d = wsT<uint8_t>(c, tag + "x" + std::to_string(i), extra[i].size());
+        ST_HIP(hipMemcpyAsync(d, buf + off[ni + i], extra[i].size(), hipMemcpyHostToDevice, c->stream));
+        ptrs.push_back(d);
+        lens.push_back(extra[i].size());
+    }
+    std::vector<uint32_t> zero(ptrs.size(), 0), crcs(ptrs.size(), 0);
+    if (!ptrs.empty()) crc32_dev(c, ptrs.data(), lens.data(), zero.data(), (int)ptrs.size(), crcs.data());  // syncs
+    for (size_t i = 0; i < es.size(); ++i) {
+        es[i].crc = crcs[i];
+        zip_descriptor(es[i], buf + off[i] + es[i].size);
+    }
+    *block = buf;
+    return total;
+}
+}  // namespace
+
+uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws,
+                      st_sog_meta *meta, const st_sog_textures *out, int fd, uint16_t dos_time, uint16_t dos_date,
+                      uint64_t *file_size) {
+    // the five textures final before the SH k-means: their entries go to the file from a host
+    // thread on the side context (the step's colour k-means, which used it, has joined by then)
+    struct Early {
+        std::vector<ZipEntry> es;
+        uint64_t bytes = 0;
+        std::exception_ptr err;
+        std::thread th;
+    } early;
+    struct Join {
+        Early &e;
+        ~Join() {
+            if (e.th.joinable()) e.th.join();
+        }
+    } join{early};
+    struct Hook {
+        st_ctx *c;
+        ~Hook() { c->sog_early = nullptr; }
+    } hook{c};
+    c->sog_early = [&](st_ctx *cc) {
+        st_ctx *aux = cc->aux;
+        ST_REQUIRE(aux, ST_ERR_INTERNAL, "sog file: no side context");
+        hipEvent_t ev;
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, cc->stream));
+        ST_HIP(hipStreamWaitEvent(aux->stream, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+        const std::vector<Img> imgs = {{"means_l.webp", out->means_l, meta->width, meta->height},
+                                       {"means_u.webp", out->means_u, meta->width, meta->height},
+                                       {"quats.webp", out->quats, meta->width, meta->height},
+                                       {"scales.webp", out->scales, meta->width, meta->height},
+                                       {"sh0.webp", out->sh0, meta->width, meta->height}};
+        early.th = std::thread([&early, aux, imgs, fd, dos_time, dos_date] {
+            try {
+                use_device(aux);
+                uint8_t *blk = nullptr;
+                early.bytes = stage_entries(aux, imgs, {}, nullptr, dos_time, dos_date, "sf.e", early.es, &blk);
+                write_at(fd, blk, early.bytes, 0);
+            } catch (...) {
+                early.err = std::current_exception();
+            }
+        });
+    };
+    const uint64_t used = sog_dev(c, t, iters, draws, ndraws, meta, out);
+    c->sog_early = nullptr;
+    ST_REQUIRE(early.th.joinable(), ST_ERR_INTERNAL, "sog file: the early entries never started");
+    // shN textures and meta.json on this context while the early entries are written
+    std::vector<Img> late;
+    if (meta->sh_bands > 0) {
+        late.push_back({"shN_centroids.webp", out->shn_centroids, meta->shn_width, meta->shn_height});
+        late.push_back({"shN_labels.webp", out->shn_labels, meta->width, meta->height});
+    }
+    const uint64_t count = t->n;
+    const std::vector<std::string> extra = {sog_meta_json(*meta, count)};
+    const char *const extra_names[1] = {"meta.json"};
+    std::vector<ZipEntry> les;
+    uint8_t *lblk = nullptr;
+    const uint64_t lbytes = stage_entries(c, late, extra, extra_names, dos_time, dos_date, "sf.l", les, &lblk);
+    early.th.join();
+    if (early.err) std::rethrow_exception(early.err);
+    std::vector<ZipEntry> all = early.es;
+    all.insert(all.end(), les.begin(), les.end());
+    ST_REQUIRE(zip_size(all) < (1ull << 32), ST_ERR_ARG, "sog file: archive exceeds 4 GiB (no zip64, as the reference)");
+    write_at(fd, lblk, lbytes, early.bytes);
+    std::vector<uint8_t> cd(zip_central_size(all));
+    zip_central(all, dos_time, dos_date, cd.data());
+    write_at(fd, cd.data(), cd.size(), early.bytes + lbytes);
+    *file_size = early.bytes + lbytes + cd.size();
+    return used;
 }
 
 }  // namespace st

@@ -122,36 +122,35 @@ uint64_t zip_size(const std::vector<ZipEntry> &entries) {
     return s;
 }
 
-void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf,
-               uint64_t *data_off) {
-    uint64_t o = 0;
-    std::vector<uint64_t> hdr_off;
-    for (size_t i = 0; i < entries.size(); ++i) {
-        const ZipEntry &e = entries[i];
-        const uint32_t nl = (uint32_t)e.name.size();
-        uint8_t *h = buf + o;
-        std::memset(h, 0, 30);
-        hdr_off.push_back(o);
-        le32(h + 0, 0x04034b50u);
-        le16(h + 4, 20);            // version needed: 2.0
-        le16(h + 6, 0x8 | 0x800);   // CRC/sizes in the descriptor, UTF-8 names
-        le16(h + 8, 0);             // stored
-        le16(h + 10, dos_time);
-        le16(h + 12, dos_date);
-        le16(h + 26, nl);
-        std::memcpy(h + 30, e.name.data(), nl);
-        o += 30 + nl;
-        data_off[i] = o;
-        o += e.size;
-        uint8_t *d = buf + o;
-        le32(d + 0, 0x08074b50u);
-        le32(d + 4, e.crc);
-        le32(d + 8, (uint32_t)e.size);
-        le32(d + 12, (uint32_t)e.size);
-        o += 16;
-    }
-    const uint64_t cd_start = o;
-    uint64_t names = 0, data = 0;
+size_t zip_local(const ZipEntry &e, uint16_t dos_time, uint16_t dos_date, uint8_t *h) {
+    const uint32_t nl = (uint32_t)e.name.size();
+    std::memset(h, 0, 30);
+    le32(h + 0, 0x04034b50u);
+    le16(h + 4, 20);            // version needed: 2.0
+    le16(h + 6, 0x8 | 0x800);   // CRC/sizes in the descriptor, UTF-8 names
+    le16(h + 8, 0);             // stored
+    le16(h + 10, dos_time);
+    le16(h + 12, dos_date);
+    le16(h + 26, nl);
+    std::memcpy(h + 30, e.name.data(), nl);
+    return 30 + nl;
+}
+
+void zip_descriptor(const ZipEntry &e, uint8_t *d) {
+    le32(d + 0, 0x08074b50u);
+    le32(d + 4, e.crc);
+    le32(d + 8, (uint32_t)e.size);
+    le32(d + 12, (uint32_t)e.size);
+}
+
+uint64_t zip_central_size(const std::vector<ZipEntry> &entries) {
+    uint64_t s = 22;
+    for (auto &e : entries) s += 46 + e.name.size();
+    return s;
+}
+
+void zip_central(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf) {
+    uint64_t o = 0, hdr = 0, names = 0, data = 0;
     for (size_t i = 0; i < entries.size(); ++i) {
         const ZipEntry &e = entries[i];
         const uint32_t nl = (uint32_t)e.name.size();
@@ -168,9 +167,10 @@ void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t
         le32(c + 20, (uint32_t)e.size);
         le32(c + 24, (uint32_t)e.size);
         le16(c + 28, nl);
-        le32(c + 42, (uint32_t)hdr_off[i]);
+        le32(c + 42, (uint32_t)hdr);  // the entry's local header: entries are laid out in order
         std::memcpy(c + 46, e.name.data(), nl);
         o += 46 + nl;
+        hdr += 30 + nl + e.size + 16;
         names += nl;
         data += e.size;
     }
@@ -182,7 +182,20 @@ void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t
     le16(z + 10, n);
     le32(z + 12, (uint32_t)(names + n * 46));
     le32(z + 16, (uint32_t)(names + n * (30 + 16) + data));
-    (void)cd_start;
+}
+
+void zip_write(const std::vector<ZipEntry> &entries, uint16_t dos_time, uint16_t dos_date, uint8_t *buf,
+               uint64_t *data_off) {
+    uint64_t o = 0;
+    for (size_t i = 0; i < entries.size(); ++i) {
+        const ZipEntry &e = entries[i];
+        o += zip_local(e, dos_time, dos_date, buf + o);
+        data_off[i] = o;
+        o += e.size;
+        zip_descriptor(e, buf + o);
+        o += 16;
+    }
+    zip_central(entries, dos_time, dos_date, buf + o);
 }
 
 }  // namespace st

@@ -110,7 +110,7 @@ EXPORTS = [
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
-    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_sog_bundle', 'st_free',
+    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_dev_sog_file', 'st_sog_bundle', 'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
@@ -1022,6 +1022,24 @@ class Context:
                                ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
                                ctypes.byref(out)))
         return meta, used.value
+
+    def dev_sog_file(self, cols, iters, draws, tex, path, dos_time=0, dos_date=0):
+        """writeSog into the file at `path` (st_dev_sog_file: the step, the archive streamed to the
+        file while the SH k-means runs): (meta, draws used, file bytes)"""
+        t = make_table(cols)
+        out = SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                            ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        meta = SogMeta()
+        used, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            check(lib().st_dev_sog_file(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws),
+                                        ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                                        ctypes.byref(out), ctypes.c_int32(fd), ctypes.c_uint16(dos_time),
+                                        ctypes.c_uint16(dos_date), ctypes.byref(size)))
+        finally:
+            os.close(fd)
+        return meta, used.value, size.value
 
     # ---- multi-GPU building blocks (device tensors; see splat_dist.py) ----------------
     def dev_minmax(self, cols):

@@ -1,0 +1,88 @@
+"""writeSog into a file with the archive streamed (st_dev_sog_file; write-sog.ts:110-370 and the
+CLI's write of the .sog): the file holds exactly the archive st_dev_sog_bundle builds from the
+same step's textures, the textures equal st_dev_sog's, for SH-3 and SH-0 tables; a failing write
+(a descriptor opened read-only) is reported, not hung on."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    import torch
+
+    import splat_hip as sh
+    c = sh.Context(0)
+    c.bind_torch_stream(torch.device('cuda', 0))
+    yield c
+    c.close()
+
+
+def _textures(sh, n, C, dev):
+    import torch
+    W, H, pal, cw, ch = sh.sog_geometry(n, C)
+    u8 = dict(device=dev, dtype=torch.uint8)
+    tex = {k: torch.zeros(W * H * 4, **u8) for k in ('means_l', 'means_u', 'quats', 'scales', 'sh0')}
+    if C:
+        tex['shN_labels'] = torch.zeros(W * H * 4, **u8)
+        tex['shN_centroids'] = torch.zeros(cw * ch * 4, **u8)
+    return tex
+
+
+@pytest.mark.parametrize('n,C', [(300_000, 15), (70_000, 0)])
+def test_sog_file_equals_the_bundle(ctx, tmp_path, n, C):
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    cols = bench.synth_table(n, 31 + C, dev)
+    if not C:
+        cols = {k: v for k, v in cols.items() if not k.startswith('f_rest')}
+    draws = np.random.default_rng(3).random(2 * 65536 * 8)
+    tex = _textures(sh, n, C, dev)
+    path = str(tmp_path / 'out.sog')
+    meta, used, size = ctx.dev_sog_file(cols, 5, draws, tex, path, 0x6a2b, 0x58b1)
+    data = open(path, 'rb').read()
+    assert len(data) == size
+    assert ctx.dev_sog_bundle(meta, n, tex, 0x6a2b, 0x58b1) == data
+    ref = _textures(sh, n, C, dev)
+    meta2, used2 = ctx.dev_sog(cols, 5, draws, ref)
+    assert used2 == used and meta2.palette_size == meta.palette_size
+    for k in tex:
+        assert torch.equal(tex[k], ref[k]), k
+
+
+def test_sog_file_write_error_is_reported(ctx, tmp_path):
+    import ctypes
+
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    n = 70_000
+    cols = bench.synth_table(n, 5, dev)
+    tex = _textures(sh, n, 15, dev)
+    draws = np.random.default_rng(3).random(2 * 65536 * 8)
+    path = str(tmp_path / 'ro.sog')
+    open(path, 'wb').close()
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        t = sh.make_table(cols)
+        out = sh.SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                               ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+        meta, used, size = sh.SogMeta(), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = sh.lib().st_dev_sog_file(ctx.h, ctypes.byref(t), ctypes.c_int32(2), sh._vp(draws),
+                                      ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                                      ctypes.byref(out), ctypes.c_int32(fd), ctypes.c_uint16(0), ctypes.c_uint16(0),
+                                      ctypes.byref(size))
+    finally:
+        os.close(fd)
+    assert rc == sh.ST_ERR_ARG and b'write failed' in sh.lib().st_last_error()
+    # the context still works afterwards
+    meta, used, size = ctx.dev_sog_file(cols, 2, draws, tex, str(tmp_path / 'ok.sog'))
+    assert size == os.path.getsize(str(tmp_path / 'ok.sog'))
