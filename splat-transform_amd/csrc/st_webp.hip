@@ -39,6 +39,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -1220,6 +1221,7 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
         uint64_t bytes = 0;
         std::exception_ptr err;
         std::thread th;
+        std::chrono::steady_clock::time_point t0, t1, t2;  // hook, early entries staged, written
     } early;
     struct Join {
         Early &e;
@@ -1244,12 +1246,15 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
                                        {"quats.webp", out->quats, meta->width, meta->height},
                                        {"scales.webp", out->scales, meta->width, meta->height},
                                        {"sh0.webp", out->sh0, meta->width, meta->height}};
+        early.t0 = std::chrono::steady_clock::now();
         early.th = std::thread([&early, aux, imgs, fd, dos_time, dos_date] {
             try {
                 use_device(aux);
                 uint8_t *blk = nullptr;
                 early.bytes = stage_entries(aux, imgs, {}, nullptr, dos_time, dos_date, "sf.e", early.es, &blk);
+                early.t1 = std::chrono::steady_clock::now();
                 write_at(fd, blk, early.bytes, 0);
+                early.t2 = std::chrono::steady_clock::now();
             } catch (...) {
                 early.err = std::current_exception();
             }
@@ -1270,7 +1275,16 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
     std::vector<ZipEntry> les;
     uint8_t *lblk = nullptr;
     const uint64_t lbytes = stage_entries(c, late, extra, extra_names, dos_time, dos_date, "sf.l", les, &lblk);
+    const auto t3 = std::chrono::steady_clock::now();
     early.th.join();
+    if (getenv("ST_DEBUG")) {
+        const auto ms = [&](std::chrono::steady_clock::time_point a) {
+            return std::chrono::duration<double, std::milli>(a - early.t0).count();
+        };
+        fprintf(stderr, "[st sog file] after the hook: early entries staged %.1f ms, written %.1f ms; late entries "
+                "staged %.1f ms, early thread joined %.1f ms\n", ms(early.t1), ms(early.t2), ms(t3),
+                ms(std::chrono::steady_clock::now()));
+    }
     if (early.err) std::rethrow_exception(early.err);
     std::vector<ZipEntry> all = early.es;
     all.insert(all.end(), les.begin(), les.end());
