@@ -1262,6 +1262,9 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
     };
     const uint64_t used = sog_dev(c, t, iters, draws, ndraws, meta, out);
     c->sog_early = nullptr;
+    const auto t_ret = std::chrono::steady_clock::now();
+    if (getenv("ST_DEBUG")) ST_HIP(hipStreamSynchronize(c->stream));
+    const auto t_gpu = std::chrono::steady_clock::now();
     ST_REQUIRE(early.th.joinable(), ST_ERR_INTERNAL, "sog file: the early entries never started");
     // shN textures and meta.json on this context while the early entries are written
     std::vector<Img> late;
@@ -1281,9 +1284,9 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
         const auto ms = [&](std::chrono::steady_clock::time_point a) {
             return std::chrono::duration<double, std::milli>(a - early.t0).count();
         };
-        fprintf(stderr, "[st sog file] after the hook: early entries staged %.1f ms, written %.1f ms; late entries "
-                "staged %.1f ms, early thread joined %.1f ms\n", ms(early.t1), ms(early.t2), ms(t3),
-                ms(std::chrono::steady_clock::now()));
+        fprintf(stderr, "[st sog file] after the hook: early entries staged %.1f ms, written %.1f ms; the step "
+                "returned %.1f ms, its work done %.1f ms; late entries staged %.1f ms, early thread joined %.1f ms\n",
+                ms(early.t1), ms(early.t2), ms(t_ret), ms(t_gpu), ms(t3), ms(std::chrono::steady_clock::now()));
     }
     if (early.err) std::rethrow_exception(early.err);
     std::vector<ZipEntry> all = early.es;
