@@ -446,7 +446,9 @@ def check_all_labels(sh, prev, lab, tile=8192):
     cd = prev.double()
     cn = (cd * cd).sum(0)
     cmax = float(cn.max().sqrt())
-    # |fl(s) - s| <= ~(d + 2) u (|c|^2 + 2 |p| |c|) for each score, u = 2^-53; 64x that margin
+    # each score's GEMM error is <= ~(d + 2) u (|c|^2 + 2 |p| |c|) and the reference's sequential
+    # f64 distance is within ~(d + 2) u |p - c|^2 <= (d + 2) u (|p| + |c|)^2 of the exact one
+    # (u = 2^-53): scores apart by more than twice 64 x (d + 2) u 2 (|p| + max|c|)^2 keep their order
     rel = 64 * (d + 2) * 2.0 ** -53
     bad = ties = slow = 0
     lab64 = lab.long()
@@ -461,7 +463,7 @@ def check_all_labels(sh, prev, lab, tile=8192):
         score[rows, i1] = float('inf')
         m2 = score.min(1).values
         score[rows, i1] = best
-        w = rel * (cmax * cmax + 2 * pn * cmax)
+        w = rel * 2 * (pn + cmax) ** 2
         clear = (m2 - m1) > 2 * w
         bad += int(((lab64[s:e] != i1) & clear).sum().item())
         amb = torch.nonzero(~clear).squeeze(1)
