@@ -471,6 +471,9 @@ int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count,
 int st_dev_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                     uint64_t *used, st_sog_meta *meta, const st_sog_textures *out, int32_t fd, uint16_t dos_time,
                     uint16_t dos_date, uint64_t *size);
+/* the same from a host table (uploaded; st_set_devices > 1: the group's archive written whole) */
+int st_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
+                uint64_t *used, int32_t fd, uint16_t dos_time, uint16_t dos_date, uint64_t *size);
 /* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */
 int st_sog_bundle(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                   uint64_t *used, uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *size);

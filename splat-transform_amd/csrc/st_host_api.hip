@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <unistd.h>
+#include <cerrno>
 #include "st_internal.h"
 #include "st_webp.h"
 
@@ -378,6 +380,53 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
         std::memcpy(buf, view, nb);
         *out = buf;
         *out_size = nb;
+        if (used) *used = u;
+    });
+}
+
+int st_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
+                int32_t fd, uint16_t dos_time, uint16_t dos_date, uint64_t *size) {
+    if (int rc = apply_env_devices()) return rc;
+    if (auto g = default_group()) {  // rows sharded over GPUs: the group's archive, then one write
+        uint8_t *zip = nullptr;
+        uint64_t nb = 0;
+        if (int rc = st_group_sog_bundle(g.get(), &t, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, &zip,
+                                         &nb))
+            return rc;
+        const int rc = guarded_h([&] {
+            ST_ARGH(fd >= 0 && size, "bad argument");
+            uint64_t o = 0;
+            while (o < nb) {
+                const ssize_t w = pwrite(fd, zip + o, nb - o, (off_t)o);
+                if (w < 0 && errno == EINTR) continue;
+                ST_REQUIRE(w > 0, ST_ERR_ARG, std::string("sog file: write failed: ") + std::strerror(errno));
+                o += (uint64_t)w;
+            }
+            *size = nb;
+        });
+        std::free(zip);
+        return rc;
+    }
+    return guarded_h([&] {
+        ST_ARGH(c && t && size && fd >= 0, "bad argument");
+        use_device(c);
+        DevTable d = upload(c, t, {}, "h.s");
+        const int C = sh_coeffs_of(t);
+        int32_t W, H, pal, cw, chh;
+        ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
+        const uint64_t tex = (uint64_t)W * H * 4;
+        st_sog_textures dt{};
+        dt.means_l = wsT<uint8_t>(c, "h.s.ml", tex);
+        dt.means_u = wsT<uint8_t>(c, "h.s.mu", tex);
+        dt.quats = wsT<uint8_t>(c, "h.s.q", tex);
+        dt.scales = wsT<uint8_t>(c, "h.s.sc", tex);
+        dt.sh0 = wsT<uint8_t>(c, "h.s.sh0", tex);
+        if (C) {
+            dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
+            dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
+        }
+        st_sog_meta meta{};
+        const uint64_t u = sog_file_dev(c, &d.t, iters, draws, ndraws, &meta, &dt, fd, dos_time, dos_date, size);
         if (used) *used = u;
     });
 }

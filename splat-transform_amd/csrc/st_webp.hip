@@ -36,6 +36,7 @@
 // of the buffer (multiplication by x^(8m) mod P, zlib's crc32_combine identity);
 // the XOR of all shifted CRCs is the CRC of the buffer.
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -1297,6 +1298,11 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
     zip_central(all, dos_time, dos_date, cd.data());
     write_at(fd, cd.data(), cd.size(), early.bytes + lbytes);
     *file_size = early.bytes + lbytes + cd.size();
+    // a file longer than the archive (an earlier, longer content) ends at the archive
+    struct stat stt;
+    if (fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && (uint64_t)stt.st_size > *file_size)
+        ST_REQUIRE(ftruncate(fd, (off_t)*file_size) == 0, ST_ERR_ARG,
+                   std::string("sog file: truncate failed: ") + std::strerror(errno));
     return used;
 }
 

@@ -391,6 +391,20 @@ const writeSogBundle = (dataTable, iterations, processActions) => {
     return Promise.resolve(res.archive);
 };
 
+// writeSog into an open FileHandle (write-sog.ts:110-370 and the CLI's write of the .sog): the
+// archive is streamed into the file while the SH palette k-means runs (st_sog_file); the file
+// holds writeSogBundle's bytes.  Float32 columns.
+const writeSogFile = (fileHandle, dataTable, iterations) => {
+    const k = 65536;
+    const date = new Date();
+    const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
+    const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
+    const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
+        draws => addon.sogFile(fileHandle.fd, dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+            iterations, draws, dosTime, dosDate));
+    return Promise.resolve(res.size);
+};
+
 // readers/read-ply.ts:111-191: {comments, elements: [{name, dataTable}]} from an open FileHandle
 // (rows stream through pinned memory into HBM and are transposed to columns there)
 const readPly = (fileHandle) => {
@@ -475,6 +489,7 @@ module.exports = {
     sogTextures,
     WebpEncoder,
     writeSogBundle,
+    writeSogFile,
     readPly,
     isCompressedPly,
     decompressPly

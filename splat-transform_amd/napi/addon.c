@@ -24,6 +24,8 @@
  *   webpLossless(rgba, w, h, stride) -> Buffer WebpEncoder.encodeLosslessRGBA (utils/webp.ts:19-41,
  *                                             lib/webp_encode.c:19-29)
  *   sogBundle(cols, names, iters, draws, dosTime, dosDate)
+ *   sogFile(fd, cols, names, iters,        writeSog into an open file (st_sog_file): the .sog streamed
+ *           draws, dosTime, dosDate)        while the SH k-means runs; {used, size}
  *        -> {archive: Buffer, used}           writeSog to a .sog (write-sog.ts:110-370 +
  *                                             serialize/zip-writer.ts)
  *   readPly(fd) -> {comments, elements:       readPly (readers/read-ply.ts:111-191)
@@ -1286,6 +1288,41 @@ fail:
     return NULL;
 }
 
+/* sogFile(fd, cols, names, iters, draws: Float64Array, dosTime, dosDate) -> {used, size}: writeSog
+ * into the open file fd (st_sog_file: the archive streamed while the SH k-means runs) */
+static napi_value js_sog_file(napi_env env, napi_callback_info info) {
+    size_t argc = 7, nd = 0;
+    napi_value argv[7], out;
+    uint32_t m = 0;
+    uint64_t n = 0, used = 0, size = 0;
+    float **cols = NULL;
+    char **names = NULL;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (!(cols = f32_list(env, argv[1], &m, &n))) return NULL;
+    if (!(names = str_list(env, argv[2], m))) goto fail;
+    {
+        const int32_t fd = (int32_t)num(env, argv[0]), iters = (int32_t)num(env, argv[3]);
+        double *draws = (double *)ta_data(env, argv[4], napi_float64_array, &nd);
+        const uint16_t dos_time = (uint16_t)num(env, argv[5]), dos_date = (uint16_t)num(env, argv[6]);
+        if (!draws) goto fail;
+        if (!get_ctx(env, &ctx)) goto fail;
+        st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+        int rc = st_sog_file(ctx, &tab, iters, draws, nd, &used, fd, dos_time, dos_date, &size);
+        free(cols);
+        free_strs(names, m);
+        if (rc != ST_OK) return throw_st(env, rc);
+        NAPI_OK(napi_create_object(env, &out));
+        set_named(env, out, "used", make_num(env, (double)used));
+        set_named(env, out, "size", make_num(env, (double)size));
+        return out;
+    }
+fail:
+    free(cols);
+    free_strs(names, m);
+    return NULL;
+}
+
 static napi_value js_read_ply(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1], out, els, comments;
@@ -1449,6 +1486,7 @@ static napi_value init(napi_env env, napi_value exports) {
                {"sog", js_sog},
                {"webpLossless", js_webp_lossless},
                {"sogBundle", js_sog_bundle},
+               {"sogFile", js_sog_file},
                {"readPly", js_read_ply},
                {"decompressPly", js_decompress_ply},
                {"compressedPly", js_compressed_ply},

@@ -110,7 +110,8 @@ EXPORTS = [
     'st_dev_kmeans_seqsum', 'st_dev_kmeans_finish', 'st_dev_kmeans_average', 'st_dev_cluster1d_codebook',
     'st_dev_sog_scatter', 'st_dev_sog_shn_centroids',
     'st_webp_max_size', 'st_dev_webp_lossless', 'st_webp_lossless', 'st_dev_crc32', 'st_zip_store',
-    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_dev_sog_file', 'st_sog_bundle', 'st_free',
+    'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_dev_sog_file', 'st_sog_file', 'st_sog_bundle',
+    'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
     'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',

@@ -41,7 +41,8 @@ def test_addon_exports(addon_built):
                                        'filterNaN', 'combineLayout', 'setDevices', 'getDevices', 'mortonOrder', 'packCompressed', 'kmeans', 'cluster1d', 'sog',
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
                                        'process', 'compressedPlyFromFile', 'sogBundleFromFile',
-                                       'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped'])
+                                       'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped',
+                                       'sogFile'])
     assert ver == '1'
 
 
@@ -223,3 +224,22 @@ def test_js_read_ply_and_decompress_match_reference(addon_built, tmp_path):
         ref = g[f'sh3_dec_{k}']
         got = np.fromfile(tmp_path / f'comp_dec_{k}.bin', np.float32)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+
+
+@pytest.mark.gpu
+def test_js_sog_file_equals_bundle(addon_built, tmp_path):
+    """writeSogFile (st_sog_file: the .sog streamed into an open FileHandle while the SH k-means
+    runs) writes exactly writeSogBundle's archive for the same table, draws and clock"""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from golden_io import Golden
+    g = Golden('sog_bundle')
+    c = next(c for c in g.meta['cases'] if c['name'] == 'b_sh1')
+    cols = g.table('b_sh1_in_')
+    for k, v in cols.items():
+        v.astype(np.float32).tofile(tmp_path / f'{k}.f32')
+    (tmp_path / 'manifest.json').write_text(json.dumps(
+        {'columns': list(cols), 'seed': c['seed'], 'iters': c['iters'], 'clock': c['clock']}))
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'sog_file.js'), str(tmp_path)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert 'sog file ok' in r.stdout
