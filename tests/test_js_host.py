@@ -239,7 +239,9 @@ def test_js_sog_file_equals_bundle(addon_built, tmp_path):
         v.astype(np.float32).tofile(tmp_path / f'{k}.f32')
     (tmp_path / 'manifest.json').write_text(json.dumps(
         {'columns': list(cols), 'seed': c['seed'], 'iters': c['iters'], 'clock': c['clock']}))
-    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'sog_file.js'), str(tmp_path)],
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert 'sog file ok' in r.stdout
+    for mode in ('file', 'bundle'):
+        r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'sog_file.js'), str(tmp_path), mode],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert f'sog {mode} ok' in r.stdout
+    assert (tmp_path / 'out_file.sog').read_bytes() == (tmp_path / 'out_bundle.sog').read_bytes()
