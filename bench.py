@@ -12,13 +12,18 @@ textures and reported in "container" with the end-to-end rate.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--splats S] [--total-splats T] [--merge F]
 
 Workloads (BASELINE.json configs):
-  N = 1 (default)       10M splats on one GPU, st_dev_sog (the metric's 1-GPU point)
-  N > 1 (default)       config 4: one 50M-splat table split N ways (strong scaling), each rank
-                        runs st_dev_sog_sharded (the library's RCCL exchange, st_multi.hip); a
-                        second record times 10M splats per GPU (weak scaling)
+  default (every N)     north_star's workload: ONE 10M-splat SH-3 table (seed 1002), strong-scaled
+                        -- at N = 1 through st_dev_sog, at N > 1 split N ways by rows, each rank
+                        running st_dev_sog_sharded (the library's RCCL exchange, st_multi.hip).
+                        `config.workload` is the same string at every N.  Extra records beside
+                        it: N = 1 `sharded_world1` (the same table through st_dev_sog_sharded
+                        over a one-rank RCCL communicator: the sharded path's own denominator),
+                        every N `config4_50M` (one 50M-splat table, strong) and, N > 1,
+                        `weak_10M_per_gpu` (10M splats per GPU)
   --merge F             config 5: F input tables of 10M splats (--file-splats) concatenated
                         (combine, index.ts:158-210) + Morton + SOG, the rows split over the ranks
-  --total-splats T      one T-splat table split over the ranks
+  --total-splats T      one T-splat table split over the ranks (strong)
+  --splats S            S splats per GPU (weak)
 N > 1 runs one process per GPU.  `python bench.py --gpus N` with no launcher around it starts
 the N-rank job itself (a child `python -m torch.distributed.run --nproc-per-node N ...`, spawned
 before this process touches torch or the GPU), relays rank 0's JSON line and fails unless the
@@ -56,7 +61,9 @@ def parse(argv=None):
                     help='one table of this many splats split over the ranks (default 50M at N > 1: config 4)')
     ap.add_argument('--merge', type=int, default=0, help='config 5: this many input tables concatenated')
     ap.add_argument('--file-splats', type=int, default=10_000_000, help='rows per --merge input')
-    ap.add_argument('--no-weak', action='store_true', help='N > 1: skip the 10M-per-GPU weak-scaling record')
+    ap.add_argument('--no-weak', '--no-extra', dest='no_extra', action='store_true',
+                    help='skip the extra records (sharded_world1, config4_50M, weak_10M_per_gpu)')
+    ap.add_argument('--extra-steps', type=int, default=3, help='timed steps of each extra record (1 warmup)')
     ap.add_argument('--iters', type=int, default=10, help='k-means iterations (reference default 10)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo with '
@@ -670,11 +677,31 @@ def table_rows(T, lo, hi, dev, seed=SEED, block=BLOCK):
     return out
 
 
-def rank_tables(args, world, rank, dev):
-    """this rank's input tables (device columns) and the workload's description"""
+NORTH_STAR_SPLATS = 10_000_000  # BASELINE.json north_star: "a synthetic 10M-splat input at 1 GPU and its 2/4/8-GPU
+CONFIG4_SPLATS = 50_000_000     # scaling curve"; BASELINE config 4: one 50M-splat table
+
+
+def workload(args, world):
+    """(description, splats in the job, scaling) of the run's main record: a function of the flags
+    only, so the same workload prints the same `config.workload` at every N (the split goes into
+    `config.parallelism`)"""
+    it = f'{args.iters} k-means iters'
     if args.merge:
         F, S = args.merge, args.file_splats
-        total = F * S
+        return (f'config 5: merge {F} x {S / 1e6:g}M-splat inputs (combine, seeds 5001..) + Morton -> writeSog SH3, '
+                f'{it}'), F * S, 'strong'
+    if args.splats is not None:
+        return f'writeSog SH3, {args.splats} splats per GPU (fixed-seed 10M blocks), {it}', args.splats * world, 'weak'
+    T = args.total_splats if args.total_splats is not None else NORTH_STAR_SPLATS
+    what = ('north_star: ' if T == NORTH_STAR_SPLATS else 'config 4: ' if T == CONFIG4_SPLATS else '')
+    return f'{what}writeSog SH3 of one {T / 1e6:g}M-splat table (fixed-seed 10M blocks, seed 1002), {it}', T, 'strong'
+
+
+def rank_tables(args, world, rank, dev):
+    """this rank's input tables (device columns) and the workload's description"""
+    desc, total, scaling = workload(args, world)
+    if args.merge:
+        F, S = args.merge, args.file_splats
         lo, hi = total * rank // world, total * (rank + 1) // world
         tabs = []
         for f in range(F):
@@ -683,17 +710,12 @@ def rank_tables(args, world, rank, dev):
                 full = synth_table(S, 5001 + f, dev)  # merge inputs use seeds 5001..
                 tabs.append({k: v[a - f * S:max(a, b) - f * S].contiguous() for k, v in full.items()})
                 del full
-        return tabs, total, (f'config 5: merge {F} x {S // 1_000_000}M-splat inputs (combine) + Morton -> writeSog '
-                             f'SH3, {args.iters} k-means iters, {total} splats over {world} GPU(s)'), 'strong'
-    if args.total_splats:
-        T = args.total_splats
-        lo, hi = T * rank // world, T * (rank + 1) // world
-        return [table_rows(T, lo, hi, dev)], T, (
-            f'config 4: writeSog SH3 of one {T / 1e6:g}M-splat table (fixed-seed 10M blocks) split {world} way(s), '
-            f'{args.iters} k-means iters'), 'strong'
-    n = args.splats
-    return [table_rows(n * world, n * rank, n * (rank + 1), dev)], n * world, (
-        f'writeSog SH3 {n * world} splats ({n}/GPU), {args.iters} k-means iters'), 'weak'
+        return tabs, total, desc, scaling
+    if scaling == 'weak':
+        n = args.splats
+        return [table_rows(total, n * rank, n * (rank + 1), dev)], total, desc, scaling
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    return [table_rows(total, lo, hi, dev)], total, desc, scaling
 
 
 TEX_ORDER = ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_labels', 'shN_centroids')
@@ -753,14 +775,9 @@ def main(args):
     if world > 1:
         rank_watchdog(args.rank_watchdog)
     torch.cuda.set_device(local)  # before the process group: RCCL binds the rank to this device
-    if args.splats is None and args.total_splats is None and not args.merge:
-        if world == 1:
-            args.splats = 10_000_000
-        else:
-            args.total_splats = 50_000_000  # BASELINE config 4
-    if args.splats is None:
-        args.splats = 10_000_000
-    sharded = world > 1 or args.dist or args.dist_python or bool(args.merge) or bool(args.total_splats)
+    # N = 1 runs st_dev_sog unless asked for the sharded path (--dist / --dist-python) or given several
+    # input tables (--merge: combine inside st_dev_sog_sharded)
+    sharded = world > 1 or args.dist or args.dist_python or bool(args.merge)
     if sharded:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29533')
@@ -855,7 +872,7 @@ def main(args):
         dist.all_gather_object(devs, (os.uname().nodename, local))
         devices = len(set(str(d) for d in devs))
     progress('building the tables')
-    tabs, total, workload, scaling = rank_tables(args, world, rank, dev)
+    tabs, total, wl_desc, scaling = rank_tables(args, world, rank, dev)
     step, tex, pal = make_step(tabs, total)
     torch.cuda.synchronize()
     progress('warmup steps')
@@ -896,18 +913,55 @@ def main(args):
             verification = verify_sharded(ctx, local_sh, tex, step, all_labels=not args.verify_sample)
             del local_sh
 
-    # N > 1: the weak-scaling record (10M splats per GPU) beside the strong one
-    weak = None
-    if world > 1 and not args.no_weak and not args.merge and not args.dist_python:
-        del step, tabs
+    # extra records beside the main one (fewer steps; outside the main timed region)
+    extras = {}
+    main_default = not args.merge and args.splats is None and args.total_splats is None and not args.dist_python
+    if main_default and not args.no_extra:
+        ks, kw = max(1, args.extra_steps), 1
+        main_sha = textures_digest(tex, meta) if rank == 0 else None
+
+        def record(what, T, el, scal, sha=None):
+            r = {'workload': what, 'splats_total': T, 'value': T * ks / el / 1e6, 'unit': 'Msplats/s',
+                 'ms_per_step': el / ks * 1e3, 'steps': ks, 'warmup': kw, 'scaling': scal}
+            if sha is not None:
+                r['textures_sha256'] = sha
+            return r
+        if not sharded:
+            # the same table through the sharded code path at world 1 (one-rank RCCL communicator): the
+            # denominator of a scaling curve taken over st_dev_sog_sharded alone
+            progress('extra record: sharded path at world 1')
+            comm1 = sh.Comm(ctx, 1, 0, sh.comm_unique_id())
+            W1, H1, _, cw1, ch1 = sh.sog_geometry(total, 15)
+            u8 = dict(device=dev, dtype=torch.uint8)
+            tex1 = {k: torch.empty(W1 * H1 * 4, **u8) for k in TEX_ORDER[:6]}
+            tex1['shN_centroids'] = torch.empty(cw1 * ch1 * 4, **u8)
+            el1, meta1, _ = timed(lambda: ctx.dev_sog_sharded(comm1, tabs, args.iters, draws, tex1), ks, kw)
+            sha1 = textures_digest(tex1, meta1)
+            extras['sharded_world1'] = dict(record(workload(args, 1)[0] + ' through st_dev_sog_sharded (1-rank RCCL)',
+                                                   total, el1, 'strong', sha1),
+                                            textures_equal_main=sha1 == main_sha, parallelism='rowshard1-native')
+            comm1.close()
+            del tex1
+        # BASELINE config 4: one 50M-splat table, split over the ranks like the main table
+        progress('extra record: config 4 (50M)')
+        lo4, hi4 = CONFIG4_SPLATS * rank // world, CONFIG4_SPLATS * (rank + 1) // world
+        t4 = [table_rows(CONFIG4_SPLATS, lo4, hi4, dev)]
+        s4, tex4, _ = make_step(t4, CONFIG4_SPLATS)
+        el4, meta4, _ = timed(s4, ks, kw)
+        a4 = argparse.Namespace(**dict(vars(args), total_splats=CONFIG4_SPLATS))
+        extras['config4_50M'] = record(workload(a4, world)[0], CONFIG4_SPLATS, el4, 'strong',
+                                       textures_digest(tex4, meta4) if rank == 0 else None)
+        del t4, s4, tex4
         torch.cuda.empty_cache()
-        wt = [synth_table(10_000_000, 1002 + rank, dev)]
-        wstep, _, _ = make_step(wt, 10_000_000 * world)
-        wel, _, _ = timed(wstep, args.steps, args.warmup)
-        weak = {'workload': f'writeSog SH3 10M splats per GPU ({10_000_000 * world} total), {args.iters} iters',
-                'value': 10_000_000 * world * args.steps / wel / 1e6, 'unit': 'Msplats/s',
-                'ms_per_step': wel / args.steps * 1e3, 'scaling': 'weak'}
-        del wt, wstep
+        if world > 1:  # 10M splats per GPU (block `rank`): weak scaling
+            progress('extra record: 10M splats per GPU')
+            wt = [synth_table(10_000_000, SEED + rank, dev)]
+            wstep, _, _ = make_step(wt, 10_000_000 * world)
+            wel, _, _ = timed(wstep, ks, kw)
+            aw = argparse.Namespace(**dict(vars(args), splats=10_000_000))
+            extras['weak_10M_per_gpu'] = record(workload(aw, world)[0], 10_000_000 * world, wel, 'weak')
+            del wt, wstep
+            torch.cuda.empty_cache()
 
     if rank != 0:
         if comm:
@@ -989,7 +1043,7 @@ def main(args):
         'vs_baseline': None,
         'dtype': 'f64+f32 (bit-exact JS semantics); fp16 MFMA (f32 accumulate) for the assign prefilter',
         'data': 'synthetic (SURVEY.md 8d distributions, torch Generator seeds 1002+rank / 5001+file), resident in HBM',
-        'config': {'workload': workload, 'splats_total': total, 'splats_rank0': n_local, 'sh_bands': 3,
+        'config': {'workload': wl_desc, 'splats_total': total, 'splats_rank0': n_local, 'sh_bands': 3,
                    'palette_size': pal, 'iterations': args.iters,
                    'parallelism': (f'rowshard{world}' + ('-pytorch' if args.dist_python else '-native'))
                    if sharded else 'single'},
@@ -1030,7 +1084,7 @@ def main(args):
         'side_channel': (os.environ.get('ST_SIDE_CHANNEL') != '0') if comm else None,
         'distinct_devices': devices if sharded else 1,
         'textures_sha256': tex_sha,
-        'weak_10M_per_gpu': weak,
+        'extra_records': extras or None,
         'verified': verification['ok'] if verification else None,
         'verification': verification,
     }

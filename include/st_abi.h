@@ -467,11 +467,15 @@ int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count,
  * the five textures that are final before the SH palette k-means (means_l/u, quats, scales,
  * sh0) are WebP-encoded on a side context and written while the k-means runs, the shN
  * textures, meta.json and the central directory after it.  The file holds the same bytes as
- * st_dev_sog_bundle's archive; *size = its length.  The caller opens and closes fd. */
+ * st_dev_sog_bundle's archive and is cut to its length; *size = that length.  fd must be
+ * seekable (a regular file opened for writing; the archive goes out with pwrite at absolute
+ * offsets): a pipe or socket fails with ST_ERR_ARG before any work.  The caller opens and
+ * closes fd. */
 int st_dev_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                     uint64_t *used, st_sog_meta *meta, const st_sog_textures *out, int32_t fd, uint16_t dos_time,
                     uint16_t dos_date, uint64_t *size);
-/* the same from a host table (uploaded; st_set_devices > 1: the group's archive written whole) */
+/* the same from a host table (uploaded; st_set_devices > 1: the group's archive written whole,
+ * from offset 0, the file cut to its length; the same fd requirement) */
 int st_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                 uint64_t *used, int32_t fd, uint16_t dos_time, uint16_t dos_date, uint64_t *size);
 /* the whole writeSog(.sog) from a host table: st_sog + st_dev_sog_bundle */

@@ -388,20 +388,19 @@ int st_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws
                 int32_t fd, uint16_t dos_time, uint16_t dos_date, uint64_t *size) {
     if (int rc = apply_env_devices()) return rc;
     if (auto g = default_group()) {  // rows sharded over GPUs: the group's archive, then one write
+        if (int rc = guarded_h([&] {
+                ST_ARGH(size, "bad argument");
+                sog_file_check(fd);
+            }))
+            return rc;
         uint8_t *zip = nullptr;
         uint64_t nb = 0;
         if (int rc = st_group_sog_bundle(g.get(), &t, 1, nullptr, iters, draws, ndraws, used, dos_time, dos_date, &zip,
                                          &nb))
             return rc;
-        const int rc = guarded_h([&] {
-            ST_ARGH(fd >= 0 && size, "bad argument");
-            uint64_t o = 0;
-            while (o < nb) {
-                const ssize_t w = pwrite(fd, zip + o, nb - o, (off_t)o);
-                if (w < 0 && errno == EINTR) continue;
-                ST_REQUIRE(w > 0, ST_ERR_ARG, std::string("sog file: write failed: ") + std::strerror(errno));
-                o += (uint64_t)w;
-            }
+        const int rc = guarded_h([&] {  // the same writer as the one-GPU path: from offset 0, then truncated
+            write_at(fd, zip, nb, 0);
+            sog_file_truncate(fd, nb);
             *size = nb;
         });
         std::free(zip);

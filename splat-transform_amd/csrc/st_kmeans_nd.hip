@@ -59,7 +59,7 @@ constexpr int WG = 64 * NW;    // threads per workgroup
 constexpr int CT_STAGE = 8;    // centroid tiles per LDS stage
 constexpr int CAND_CAP = 64;   // candidate slots per ambiguous point
 constexpr int CAND_CAP2 = 2048;  // ... per point whose list overflowed (a second collect)
-constexpr int OVF_BATCH = 32768;  // overflowed points per second collect (256 MiB of lists)
+constexpr int OVF_BATCH = 4096;  // overflowed points per second collect (32 MiB of lists, kept by the workspace)
 // members above which a cluster's sum is split over many workgroups (k_big_*); ST_SUMND_BIG
 // lowers it so that tests drive that path with small inputs
 uint32_t sumnd_big() {

@@ -39,6 +39,7 @@ namespace {
 
 constexpr uint64_t kMagic = 0x31304d48535f5453ull;  // "ST_SHM01"
 constexpr int kMaxRanks = 256;
+constexpr double kAttachLimitS = 120;  // longest wait for every rank to attach
 constexpr int kChannels = 2;
 
 struct alignas(64) Chan {
@@ -96,7 +97,8 @@ struct Seg {
     }
     // spin, then yield, then sleep until done(); abort / dead peer / timeout throw
     template <typename F>
-    void wait(F &&done, const char *what) {
+    void wait(F &&done, const char *what, double limit_s = 0) {
+        if (limit_s <= 0) limit_s = timeout_s;
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
         auto checked = t0;
@@ -117,10 +119,10 @@ struct Seg {
                     throw Error(ST_ERR_INTERNAL, "shared-memory transport: rank " + std::to_string(d) +
                                                      " exited during " + what);
                 }
-                if (std::chrono::duration<double>(now - t0).count() > timeout_s) {
+                if (std::chrono::duration<double>(now - t0).count() > limit_s) {
                     abort_job();
                     throw Error(ST_ERR_INTERNAL, std::string("shared-memory transport: no progress for ") +
-                                                     std::to_string((int)timeout_s) + " s during " + what);
+                                                     std::to_string((int)limit_s) + " s during " + what);
                 }
             }
             if (i < 8192) {
@@ -299,8 +301,12 @@ std::unique_ptr<Coll> make_shm_coll(int world, int rank, const char *name, size_
     seg->rank = rank;
     seg->timeout_s = timeout_s > 0 ? timeout_s : 600;
     seg->size = header_bytes() + (size_t)kChannels * world * slot_bytes;
+    // the ranks meet within kAttachLimitS (or the job's timeout if shorter): a rank that died before
+    // attaching ends rank 0's wait, and rank 0 unlinks the name, well before a launcher's first-stall
+    // kill (bench.py: 600 s) could stop rank 0 with no destructor run and leave the segment in tmpfs
+    const double attach_s = std::min(seg->timeout_s, kAttachLimitS);
     using clk = std::chrono::steady_clock;
-    const auto deadline = clk::now() + std::chrono::duration<double>(seg->timeout_s);
+    const auto deadline = clk::now() + std::chrono::duration<double>(attach_s);
     if (rank == 0) {
         const int fd = shm_open(seg->name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
         if (fd < 0) {
@@ -355,7 +361,8 @@ std::unique_ptr<Coll> make_shm_coll(int world, int rank, const char *name, size_
     seg->slots = static_cast<char *>(seg->base) + header_bytes();
     seg->h->pid[rank].store((int32_t)getpid(), std::memory_order_release);
     seg->h->attached.fetch_add(1, std::memory_order_acq_rel);
-    seg->wait([&] { return seg->h->attached.load(std::memory_order_acquire) == (uint32_t)world; }, "attach");
+    seg->wait([&] { return seg->h->attached.load(std::memory_order_acquire) == (uint32_t)world; }, "attach",
+              attach_s);
     if (rank == 0) {  // every rank has it mapped: the name can go
         shm_unlink(seg->name.c_str());
         seg->unlinked = true;

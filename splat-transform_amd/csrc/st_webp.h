@@ -35,6 +35,11 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
 uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws,
                       st_sog_meta *meta, const st_sog_textures *out, int fd, uint16_t dos_time, uint16_t dos_date,
                       uint64_t *file_size);
+// the descriptor checks of the file writers: fd must be a seekable file (ST_ERR_ARG otherwise);
+// write n bytes at offset off; cut a longer file to `size` bytes
+void sog_file_check(int fd);
+void write_at(int fd, const uint8_t *p, uint64_t n, uint64_t off);
+void sog_file_truncate(int fd, uint64_t size);
 
 // ---- host: the .sog container (st_zip.cpp) ----------------------------------
 // JSON text of a JS number (Number::toString as JSON.stringify emits it; non-finite -> null)

@@ -1141,7 +1141,16 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
 }
 
 // ---- writeSog into a file, the archive streamed ------------------------------------------
-namespace {
+void sog_file_check(int fd) {
+    // the archive is written at absolute offsets (pwrite), so the descriptor must be seekable: a
+    // pipe fails here, before any work, instead of with ESPIPE after the step
+    ST_REQUIRE(fd >= 0, ST_ERR_ARG, "sog file: bad file descriptor");
+    struct stat stt;
+    ST_REQUIRE(fstat(fd, &stt) == 0, ST_ERR_ARG, std::string("sog file: fstat failed: ") + std::strerror(errno));
+    ST_REQUIRE(S_ISREG(stt.st_mode) || lseek(fd, 0, SEEK_CUR) != (off_t)-1, ST_ERR_ARG,
+               "sog file: fd must be a seekable file (a regular file opened for writing)");
+}
+
 void write_at(int fd, const uint8_t *p, uint64_t n, uint64_t off) {
     while (n) {
         const ssize_t w = pwrite(fd, p, n, (off_t)off);
@@ -1152,6 +1161,17 @@ void write_at(int fd, const uint8_t *p, uint64_t n, uint64_t off) {
         off += (uint64_t)w;
     }
 }
+
+void sog_file_truncate(int fd, uint64_t size) {
+    // a file longer than the archive (an earlier, longer content) ends at the archive: zip readers
+    // look for the end record from the end of the file
+    struct stat stt;
+    if (fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && (uint64_t)stt.st_size > size)
+        ST_REQUIRE(ftruncate(fd, (off_t)size) == 0, ST_ERR_ARG,
+                   std::string("sog file: truncate failed: ") + std::strerror(errno));
+}
+
+namespace {
 
 struct Img {
     const char *name;
@@ -1215,6 +1235,7 @@ uint64_t stage_entries(st_ctx *c, const std::vector<Img> &imgs, const std::vecto
 uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws,
                       st_sog_meta *meta, const st_sog_textures *out, int fd, uint16_t dos_time, uint16_t dos_date,
                       uint64_t *file_size) {
+    sog_file_check(fd);
     // the five textures final before the SH k-means: their entries go to the file from a host
     // thread on the side context (the step's colour k-means, which used it, has joined by then)
     struct Early {
@@ -1298,11 +1319,7 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
     zip_central(all, dos_time, dos_date, cd.data());
     write_at(fd, cd.data(), cd.size(), early.bytes + lbytes);
     *file_size = early.bytes + lbytes + cd.size();
-    // a file longer than the archive (an earlier, longer content) ends at the archive
-    struct stat stt;
-    if (fstat(fd, &stt) == 0 && S_ISREG(stt.st_mode) && (uint64_t)stt.st_size > *file_size)
-        ST_REQUIRE(ftruncate(fd, (off_t)*file_size) == 0, ST_ERR_ARG,
-                   std::string("sog file: truncate failed: ") + std::strerror(errno));
+    sog_file_truncate(fd, *file_size);
     return used;
 }
 

@@ -393,7 +393,9 @@ const writeSogBundle = (dataTable, iterations, processActions) => {
 
 // writeSog into an open FileHandle (write-sog.ts:110-370 and the CLI's write of the .sog): the
 // archive is streamed into the file while the SH palette k-means runs (st_sog_file); the file
-// holds writeSogBundle's bytes.  Float32 columns.
+// holds writeSogBundle's bytes and is cut to their length.  The handle must be a seekable file
+// (the archive is written at absolute offsets): a pipe's handle throws before any work.  Float32
+// columns.
 const writeSogFile = (fileHandle, dataTable, iterations) => {
     const k = 65536;
     const date = new Date();

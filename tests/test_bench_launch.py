@@ -97,6 +97,26 @@ def test_launch_budget_and_a_failing_fallback(tmp_path):
     assert r.stderr.count('killing the job') == 2 and 'budget' in r.stderr
 
 
+def test_workload_is_the_same_at_every_n():
+    """the default run is north_star's workload -- one 10M-splat table, strong-scaled -- at every N,
+    so the driver's 1/2/4/8-GPU values divide the same job; config 4 and config 5 likewise"""
+    import bench
+    for extra in ([], ['--total-splats', '50000000'], ['--merge', '4']):
+        rec = {}
+        for n, backend in ((1, 'nccl'), (2, 'gloo'), (2, 'nccl'), (4, 'nccl'), (8, 'nccl')):
+            a = bench.parse(['--gpus', str(n), '--backend', backend] + extra)
+            rec[(n, backend)] = bench.workload(a, n)
+        assert len(set(rec.values())) == 1, rec
+        desc, total, scaling = rec[(1, 'nccl')]
+        assert scaling == 'strong'
+        if not extra:
+            assert total == 10_000_000 and desc.startswith('north_star: ')
+    # weak scaling (--splats S per GPU): same description, S x N splats
+    w1 = bench.workload(bench.parse(['--splats', '10000000']), 1)
+    w8 = bench.workload(bench.parse(['--gpus', '8', '--splats', '10000000']), 8)
+    assert w1[0] == w8[0] and (w1[1], w8[1]) == (10_000_000, 80_000_000) and w8[2] == 'weak'
+
+
 def test_table_rows_independent_of_the_split():
     """rows [lo, hi) of a T-row table built from fixed-seed blocks: any split concatenates to the
     same table (small blocks here; the bench uses 10M-row blocks)"""

@@ -1,0 +1,195 @@
+"""BASELINE configs 3, 4 and 5 at their full sizes on the GPU.
+
+* config 4 (write-sog.ts:110-370): ONE 50M-splat SH-3 table -> .sog with its rows sharded over 4
+  rank processes -- `bench.py --gpus 4 --backend gloo`, i.e. the launcher, one process per rank and
+  st_dev_sog_sharded over the library's host shared-memory transport (the calls of the 8-GPU job,
+  with host memory carrying the bytes RCCL would) -- against st_dev_sog of the whole table on one
+  device in this process;
+* config 5 (index.ts:158-210 + write-sog.ts): four 10M-splat inputs (seeds 5001..5004) combined
+  in file order, Morton-ordered and written as one .sog, its 40M rows split over 3 rank processes
+  so that ranks cut across the input files -- against combine (st_dev_combine) + st_dev_sog on
+  one device;
+* config 3 (process.ts:64-145, write-compressed-ply.ts:56-114): 10M SH-3 splats, -r 0,45,0 then
+  filterNaN (0.1% of the rows non-finite), Morton order and chunk pack through
+  st_dev_compressed_ply, bit-exact against the oracle's chain (oracle/st_oracle.c).
+
+The multi-process runs check every label of every shard as the exact f64 argmin over the last
+assign's centroids, and that every rank ends with the same centroids; the one-device run checks
+every shN_labels texel's placement (the Morton position of its row), sampled labels and member
+means; the two must give the same seven textures and meta fields (textures_sha256)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+BENCH = os.path.join(ROOT, 'bench.py')
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'splat-transform_amd', 'py'))
+sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+
+pytestmark = pytest.mark.gpu
+
+COMMON = ['--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-e2e', '--no-paths', '--no-extra']
+ITERS = 10
+
+
+def _bench(args, timeout=840):
+    env = dict(os.environ, PYTHONUNBUFFERED='1')
+    r = subprocess.run([sys.executable, BENCH] + args + COMMON, capture_output=True, text=True, timeout=timeout,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-6000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _check_sharded(res, world, total):
+    assert res['n_gpus'] == world and res['config']['parallelism'] == f'rowshard{world}-native'
+    assert res['transport'] == 'host-shm' and 'fallback' not in res
+    assert res['config']['splats_total'] == total
+    v = res['verification']
+    assert v['ok'] and v['labels_wrong'] == 0 and v['labels_checked'] == total, v
+    assert v['centroids_identical_on_every_rank'] and v['textures_equal_timed_step'], v
+
+
+def _one_device(table):
+    """st_dev_sog of the whole table in this process: (textures_sha256, verification)"""
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    ctx = sh.Context(0)
+    try:
+        ctx.bind_torch_stream(dev)
+        total = table['x'].shape[0]
+        W, H, _, cw, ch = sh.sog_geometry(total, 15)
+        u8 = dict(device=dev, dtype=torch.uint8)
+        tex = {k: torch.empty(W * H * 4, **u8) for k in bench.TEX_ORDER[:6]}
+        tex['shN_centroids'] = torch.empty(cw * ch * 4, **u8)
+        draws = np.random.default_rng(42).random(2 * 65536 * (ITERS + 2))  # bench.py's Math.random stream
+
+        def step():
+            return ctx.dev_sog(table, ITERS, draws, tex)
+        meta, _ = step()
+        torch.cuda.synchronize()
+        sha = bench.textures_digest(tex, meta)
+        ver = bench.verify_step(ctx, table, tex, step)
+        del tex
+        return sha, ver
+    finally:
+        ctx.close()
+        torch.cuda.empty_cache()
+
+
+def _check_one_device(ver, total):
+    assert ver['ok'] and ver['textures_equal_timed_step'], ver
+    assert ver['texel_labels_checked'] == total and ver['texel_labels_wrong'] == 0, ver
+    assert ver['labels_wrong'] == 0 and ver['centroid_values_wrong'] == 0, ver
+
+
+def test_config4_50m_in_four_processes_matches_one_gpu():
+    T = 50_000_000
+    four = _bench(['--gpus', '4', '--backend', 'gloo', '--total-splats', str(T)])
+    _check_sharded(four, 4, T)
+    import torch
+
+    import bench
+    table = bench.table_rows(T, 0, T, torch.device('cuda', 0))
+    sha, ver = _one_device(table)
+    del table
+    _check_one_device(ver, T)
+    assert sha == four['textures_sha256']
+
+
+def test_config5_merge_4x10m_in_three_processes_matches_one_gpu():
+    F, S = 4, 10_000_000
+    three = _bench(['--gpus', '3', '--backend', 'gloo', '--merge', str(F)])
+    _check_sharded(three, 3, F * S)
+    # rank r holds rows [40M r / 3, 40M (r + 1) / 3): ranks 0 and 1 each end inside an input file
+    assert three['config']['splats_rank0'] == F * S // 3
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    inputs = [list(bench.synth_table(S, 5001 + f, dev).items()) for f in range(F)]
+    lay = sh.combine_layout([[(k, np.zeros(1, np.float32)) for k, _ in t] for t in inputs])
+    names = [inputs[ti][ci][0] for ti, ci in lay]
+    dst = [(k, torch.empty(F * S, dtype=torch.float32, device=dev)) for k in names]
+    ctx = sh.Context(0)
+    try:
+        ctx.bind_torch_stream(dev)
+        ctx.dev_combine(inputs, dst)  # combine (index.ts:158-210): the inputs' rows in file order
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    del inputs
+    sha, ver = _one_device(dict(dst))
+    del dst
+    _check_one_device(ver, F * S)
+    assert sha == three['textures_sha256']
+
+
+def test_config3_10m_compressed_ply_vs_oracle():
+    """-r 0,45,0 --filterNaN -> .compressed.ply at 10M SH-3 splats (BASELINE config 3): the device
+    chain (st_dev_compressed_ply) against the oracle's, byte for byte; 0.1% of the rows hold a
+    NaN / +-Inf in some column, 5% sit in a 1e-3 cube (Morton runs longer than 256)"""
+    import torch
+
+    import oracle
+    import splat_hip as sh
+    n = 10_000_000
+    rng = np.random.default_rng(1003)  # config i uses seed 1000 + i
+    names = ['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] + \
+        ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3']
+    cols = {}
+    cube = rng.random(n) < 0.05
+    for a, off in zip('xyz', (1.0, -2.0, 3.0)):
+        cols[a] = np.where(cube, off + rng.random(n) * 1e-3, rng.normal(0, 10, n)).astype(np.float32)
+    for k in ('nx', 'ny', 'nz'):
+        cols[k] = np.zeros(n, np.float32)
+    for i in range(3):
+        cols[f'f_dc_{i}'] = rng.normal(0, 1, n).astype(np.float32)
+    for i in range(45):
+        cols[f'f_rest_{i}'] = (rng.normal(0, 0.1, n)).astype(np.float32)
+    cols['opacity'] = rng.normal(0, 2, n).astype(np.float32)
+    for i in range(3):
+        cols[f'scale_{i}'] = (rng.random(n) * 5 - 7).astype(np.float32)
+    for i in range(4):
+        cols[f'rot_{i}'] = rng.normal(0, 1, n).astype(np.float32)
+    bad = rng.choice(n, n // 1000, replace=False)
+    which = rng.integers(0, len(names), bad.size)
+    for j, (r, c) in enumerate(zip(bad, which)):
+        cols[names[c]][r] = (np.nan, np.inf, -np.inf)[j % 3]
+    src = [(k, cols[k]) for k in names]
+    acts = [{'kind': 'rotate', 'value': [0, 45, 0]}, {'kind': 'filterNaN'}]
+
+    dev = torch.device('cuda', 0)
+    d = [(k, torch.from_numpy(a).to(dev)) for k, a in src]
+    chunk = torch.empty((n + 255) // 256 * 18, dtype=torch.float32, device=dev)
+    vertex = torch.empty(n * 4, dtype=torch.int32, device=dev)
+    shb = torch.empty(n * 45, dtype=torch.uint8, device=dev)
+    ctx = sh.Context(0)
+    try:
+        ctx.bind_torch_stream(dev)
+        m, C = ctx.dev_compressed_ply(d, acts, chunk, vertex, shb)
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    del d
+    got = (chunk[:(m + 255) // 256 * 18].cpu().numpy(), vertex[:m * 4].cpu().numpy().view(np.uint32),
+           shb[:m * 3 * C].cpu().numpy())
+    del chunk, vertex, shb
+    torch.cuda.empty_cache()
+
+    out, ochunk, overtex, osh = oracle.compressed_ply(src, acts)
+    assert C == 15 and m == len(out[0][1]) and n - bad.size <= m < n
+    for nm, a, b in (('chunk', got[0], ochunk), ('vertex', got[1], overtex), ('sh', got[2], osh)):
+        a, b = np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8)
+        assert a.size == b.size, nm
+        diff = np.flatnonzero(a != b)
+        assert diff.size == 0, f'{nm}: {diff.size} bytes differ, first at {diff[:8]}'
