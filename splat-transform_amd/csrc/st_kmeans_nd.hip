@@ -576,7 +576,12 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float pn = pnorm[p], dp = pdn[p];
+#ifdef ST_WINDOW_R3
+            const float dcm = __builtin_bit_cast(float, cmax_bits[1]);
+            const float W = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, dcm);
+#else
             const float W = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
+#endif
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
                 if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
@@ -1149,6 +1154,300 @@ __global__ __launch_bounds__(256) void k_fixrow_acc(const float *__restrict__ ao
         pemin[(uint64_t)sl * 16 * LD + e] = E[e];
     }
     if (threadIdx.x < 16) pcnt[(uint64_t)sl * 16 + threadIdx.x] = C[threadIdx.x];
+}
+
+// ---- the fused fix-up, one lane per point ---------------------------------------------------
+// The same job as k_fixrow_acc -- one slice of one tile-half's decided points: the exact argmin
+// among the half's 16 rows (kd-tree.ts:26-35) and the certified per-cluster sums of calcAverage
+// (k-means.ts:41-63) -- laid out for the vector unit instead of for the gather:
+//   * a lane holds ONE point's row (12 dwordx4 loads; a wave's loads cover 64 rows, the next
+//     batch's in flight while this one is scored);
+//   * the 16 centroid rows are wave-uniform: scalar loads, and the screen is one packed FMA per
+//     two dimensions with the centroid in SGPRs (p.c, not (p - c)^2: half the VALU work);
+//   * the decision is lane-local; the point's row then goes through LDS to the "lane = dimension"
+//     layout, where each cluster's members of the batch are summed in registers (their lanes
+//     found by one ballot per cluster) and added to the slice's LDS sums once per cluster.
+// Screen: s_r = fl(|c_r|^2) - 2 fl(p.c_r) estimates T_r = |c_r|^2 - 2 p.c_r = D_r - |p|^2; the
+// f32 evaluation is within e1 |p||c_r| + e2 |c_r|^2 (+ underflow) of T_r and the reference's f64
+// distance within rel (|p| + |c_r|)^2 of D_r, so [s_r - err_r, s_r + err_r] holds ref_r - |p|^2
+// and the row with the reference's minimum reaches the lowest upper end: one such row decides,
+// otherwise the candidates' exact f64 distances do (an exact tie goes to the KdTree walk).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// a 16-byte load issued where it stands (the compiler would sink it to its use), at an immediate offset
+template <int OFF>
+__device__ inline void load16_at(f32x4 &dst, const void *src) {
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst) : "v"(src), "i"(OFF) : "memory");
+}
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// lane R's value of v, into an SGPR (volatile: read where it stands, not hoisted out of the loop)
+template <int R>
+__device__ inline float readlane_f(float v) {
+    float x;
+    asm volatile("v_readlane_b32 %0, %1, %2" : "=s"(x) : "v"(v), "i"(R));
+    return x;
+}
+// one centroid row of LD floats at base + OFF bytes into SGPRs: scalar loads issued and waited for
+// where they stand (the compiler would hoist all 16 rows' loads and spill them)
+template <int LD, int OFF>
+__device__ inline void srow(float (&v)[LD], const float *base) {
+    if constexpr (LD == 48) {
+        f32x16 t0, t1, t2;
+        asm volatile("s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %5\n\ts_load_dwordx16 %2, %3, %6\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=s"(t0), "=s"(t1), "=s"(t2) : "s"(base), "i"(OFF), "i"(OFF + 64), "i"(OFF + 128));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            v[i] = t0[i];
+            v[16 + i] = t1[i];
+            v[32 + i] = t2[i];
+        }
+    } else if constexpr (LD == 24) {
+        f32x16 t0;
+        f32x8 t1;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(t0), "=s"(t1) : "s"(base), "i"(OFF), "i"(OFF + 64));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = t0[i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[16 + i] = t1[i];
+    } else {
+        static_assert(LD == 12, "rows of 12, 24 or 48 floats");
+        f32x8 t0;
+        f32x4 t1;
+        asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(t0), "=s"(t1) : "s"(base), "i"(OFF), "i"(OFF + 32));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = t0[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[8 + i] = t1[i];
+    }
+}
+constexpr int FL_WAVES = 4;     // waves per workgroup (one slice's batches shared out)
+constexpr int FL_TS = 65;       // LDS transpose stride (floats): conflict-free both ways
+template <int LD>
+__global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
+    const float *__restrict__ aos, int d, const float *__restrict__ caos, int k, const uint2 *__restrict__ grouped,
+    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ cend, const uint32_t *__restrict__ soff,
+    uint32_t ncodes, uint32_t *__restrict__ labels, uint32_t *__restrict__ ties, State *st,
+    double *__restrict__ psum, double *__restrict__ pabs, int *__restrict__ pemin, uint32_t *__restrict__ pcnt) {
+    constexpr int NQ = LD / 4;
+    __shared__ double S[16 * LD], A[16 * LD];
+    __shared__ int E[16 * LD];
+    __shared__ uint32_t C[16];
+    __shared__ float tr[FL_WAVES][LD * FL_TS];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: the batch loop is a wave loop
+    const uint32_t nsl = soff[ncodes];
+    // f32 screen error constants (u = 2^-24): 4 FMA chains of NQ terms + 3 adds for p.c
+    // (gamma_{NQ+2} per side, x2 for the factor 2), the subtraction's and |c|^2's roundings; rel:
+    // the reference's f64 distance (kd-tree.ts:26-35) against the exact one
+    constexpr float u = 0x1p-24f;
+    constexpr float e1 = (2.0f * (NQ + 2) + 3.0f) * u * 1.01f, e2 = 2.01f * u, rel = 1.0e-13f;
+    const float ab = 64.0f * 0x1p-126f;
+    for (uint32_t sl = blockIdx.x; sl < nsl; sl += gridDim.x) {
+        uint32_t lo = 0, hi = ncodes;  // the code whose slices hold sl
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (soff[mid] <= sl) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t code = __builtin_amdgcn_readfirstlane(lo);
+        const uint32_t b0 = cend[code] - hist[code] + (sl - soff[code]) * FA_SL;
+        const uint32_t b1 = min(cend[code], b0 + FA_SL);
+        for (int e = threadIdx.x; e < 16 * LD; e += 64 * FL_WAVES) {
+            S[e] = 0.0;
+            A[e] = 0.0;
+            E[e] = 1 << 20;
+        }
+        if (threadIdx.x < 16) C[threadIdx.x] = 0u;
+        // per row: |c|^2 (f32, nearest) and the bound's coefficients, from the f64 norm (lanes 0..15);
+        // a row past k (padding of the last tile) reads the tile's first row and scores 3e38 (finite:
+        // no inf - inf in the bound), never a candidate
+        float rnc = 3.0e38f, rbeta = 0.f, rgam = 0.f;
+        {
+            const uint32_t c = code_row(code, lane & 15);
+            if (lane < 16 && c < (uint32_t)k) {
+                const float4 *cr = reinterpret_cast<const float4 *>(caos + (uint64_t)c * LD);
+                double nn = 0;
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 v = cr[q];
+                    nn += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+                }
+                const float cn = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+                rnc = (float)nn;
+                rbeta = (e1 + 2.0f * rel) * cn;
+                rgam = (e2 + rel) * cn * cn + ab;
+            }
+        }
+        __syncthreads();
+        // batches of 64 grouped points per wave: wave wv takes batches wv, wv + FL_WAVES, ...
+        const uint32_t nb = (b1 - b0 + 63) / 64;
+        auto row_src = [&](uint32_t pt) { return reinterpret_cast<const f32x4 *>(aos + (uint64_t)pt * LD); };
+        uint32_t bi = wv;
+        uint32_t pcur = 0, pnx = 0;
+        f32x4 cur[NQ], nxt[NQ];  // native vectors: the wait below ties them in place
+        if (bi < nb) {
+            const uint32_t j = min(b0 + bi * 64 + lane, b1 - 1);
+            pcur = grouped[j].x;
+            const uint32_t j2 = min(b0 + (bi + FL_WAVES) * 64 + lane, b1 - 1);
+            pnx = grouped[j2].x;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) cur[q] = row_src(pcur)[q];
+        }
+        for (; bi < nb; bi += FL_WAVES) {  // uniform per wave
+            const bool have = b0 + bi * 64 + lane < b1;
+            // the next batch's rows and the one after's point indices, in flight while this batch
+            // is scored (by hand: the compiler would sink them to their use)
+            uint32_t pnn;
+            {
+                const f32x4 *src = row_src(pnx);
+                static_for<NQ>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    load16_at<16 * q>(nxt[q], src);
+                });
+                const uint2 *gsrc = grouped + min(b0 + (bi + 2 * FL_WAVES) * 64 + lane, b1 - 1);
+                asm volatile("global_load_dword %0, %1, off" : "=v"(pnn) : "v"(gsrc) : "memory");
+            }
+            // |p|^2 and the 16 screens
+            f32x2 pa = {0.f, 0.f}, pb = {0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const f32x2 x01 = {cur[q].x, cur[q].y}, x23 = {cur[q].z, cur[q].w};
+                pa = __builtin_elementwise_fma(x01, x01, pa);
+                pb = __builtin_elementwise_fma(x23, x23, pb);
+            }
+            const float pn = __builtin_sqrtf(((pa.x + pa.y) + (pb.x + pb.y)) * (1.0f + 16.0f * u)) * (1.0f + 4.0f * u);
+            const float apn = rel * pn * pn;
+            float s[16];
+            float mh = __builtin_inff();
+            // the tile-half's rows: row r at tile row (r & 3) + 8 (r >> 2) (code_row), constant offsets
+            // from one base, loaded into SGPRs one row at a time (srow) right before its 2 x NQ packed
+            // FMAs; the per-row constants are read from lanes 0..15 at their use
+            const float *cbase = caos + (uint64_t)code_row(code, 0) * LD;
+            const bool allvalid = (code >> 1) * 32 + 32 <= (uint32_t)k;  // every row of the tile below k
+            static_for<16>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const float nc = readlane_f<r>(rnc), be = readlane_f<r>(rbeta), ga = readlane_f<r>(rgam);
+                float lo_r = 3.0e38f;
+                if (allvalid || code_row(code, r) < (uint32_t)k) {  // uniform
+                    float cv[LD];
+                    srow<LD, ((r & 3) + 8 * (r >> 2)) * LD * 4>(cv, cbase);
+                    f32x2 a = {0.f, 0.f}, b = {0.f, 0.f};
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        a = __builtin_elementwise_fma((f32x2){cur[q].x, cur[q].y}, (f32x2){cv[4 * q], cv[4 * q + 1]}, a);
+                        b = __builtin_elementwise_fma((f32x2){cur[q].z, cur[q].w}, (f32x2){cv[4 * q + 2], cv[4 * q + 3]}, b);
+                    }
+                    const float sr = nc - 2.0f * ((a.x + a.y) + (b.x + b.y));
+                    const float err = __builtin_fmaf(pn, be, ga + apn) * 1.001f + __builtin_fabsf(sr) * 0x1p-22f;
+                    mh = fminf(mh, sr + err);
+                    lo_r = sr - err;  // the interval's lower end is all the decision needs from here on
+                }
+                s[r] = lo_r;
+                __builtin_amdgcn_sched_barrier(0);  // one row's SGPRs at a time
+            });
+            // the batch's rows into the lane = dimension layout (the sums below; the exact path reads
+            // its point back from here)
+            float *t = tr[wv];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                t[(4 * q + 0) * FL_TS + lane] = cur[q].x;
+                t[(4 * q + 1) * FL_TS + lane] = cur[q].y;
+                t[(4 * q + 2) * FL_TS + lane] = cur[q].z;
+                t[(4 * q + 3) * FL_TS + lane] = cur[q].w;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t cand = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cand |= (s[r] <= mh ? 1u : 0u) << r;
+            uint32_t wl = 16;  // local winner (16: none -- not this lane's point, or an exact tie)
+            if (have) {
+                uint32_t wc;
+                bool tie = false;
+                if (__builtin_popcount(cand) == 1 && allvalid) {
+                    wl = __builtin_ctz(cand);
+                    wc = code_row(code, (int)wl);
+                } else {
+                    // the exact reference distances of the candidates (every valid row if none)
+                    uint32_t valid = 0;
+                    for (int r = 0; r < 16; ++r) valid |= (code_row(code, r) < (uint32_t)k ? 1u : 0u) << r;
+                    uint32_t cm = cand & valid;
+                    if (!cm) cm = valid;
+                    double best = __builtin_inf();
+                    uint32_t bl = 16, cnt = 0;
+                    for (uint32_t m = cm; m; m &= m - 1) {  // ascending rows = ascending centroid index
+                        asm volatile("" ::: "memory");  // re-read per row: nothing hoisted into registers
+                        const int r = __builtin_ctz(m);
+                        const float *cr = caos + (uint64_t)code_row(code, r) * LD;
+                        double l = 0;
+                        for (int jd = 0; jd < LD; ++jd) {  // kd-tree.ts:26-35: sequential f64 sum of (c - p)^2
+                            const double v = (double)cr[jd] - (double)t[jd * FL_TS + lane];
+                            l += v * v;
+                        }
+                        if (l < best) {
+                            best = l;
+                            bl = (uint32_t)r;
+                            cnt = 1;
+                        } else if (l == best) {
+                            ++cnt;
+                        }
+                    }
+                    wc = code_row(code, (int)bl);
+                    tie = cnt > 1;
+                    wl = tie ? 16u : bl;
+                }
+                labels[pcur] = wc;  // provisional on a tie; the KdTree pass decides
+                if (tie) ties[atomicAdd(&st->ties, 1u)] = pcur;
+            }
+            // per cluster: its members' values in this lane's dimension, summed in registers
+            const int jd = lane < LD ? lane : LD - 1;
+            static_for<16>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                uint64_t m = __ballot(wl == (uint32_t)c);
+                if (m) {  // uniform
+                    const uint32_t cnt = (uint32_t)__popcll(m);
+                    double sm = 0.0, sa = 0.0;
+                    float mn = __builtin_inff();
+                    while (m) {
+                        const int i = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const float x = t[jd * FL_TS + i];
+                        sm += (double)x;
+                        sa += (double)__builtin_fabsf(x);
+                        mn = fminf(mn, x != 0.0f ? __builtin_fabsf(x) : __builtin_inff());
+                    }
+                    if (lane < LD) {  // padding dimensions add 0 (and no exponent)
+                        const int e = c * LD + fa_slot<LD>(lane);
+                        atomicAdd(&S[e], sm);
+                        atomicAdd(&A[e], sa);
+                        if (mn != __builtin_inff()) atomicMin(&E[e], ulp_exp(mn));
+                    }
+                    if (lane == 0) atomicAdd(&C[c], cnt);
+                }
+            });
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(pnn) : : "memory");
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                // tied to the wait (volatile asm keeps program order): nothing reads the new rows
+                // before the loads have landed
+                asm volatile("" : "+v"(nxt[q]));
+                cur[q] = nxt[q];
+            }
+            pcur = pnx;
+            pnx = pnn;
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < 16 * LD; e += 64 * FL_WAVES) {
+            psum[(uint64_t)sl * 16 * LD + e] = S[e];
+            pabs[(uint64_t)sl * 16 * LD + e] = A[e];
+            pemin[(uint64_t)sl * 16 * LD + e] = E[e];
+        }
+        if (threadIdx.x < 16) pcnt[(uint64_t)sl * 16 + threadIdx.x] = C[threadIdx.x];
+        __syncthreads();
+    }
 }
 
 // the points the fused fix-up did not sum (pairs, ambiguous, its own exact ties), keyed by
@@ -1872,6 +2171,7 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
             auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
             auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
+#ifdef ST_FIX_GROUP16
             if (ld == 48)
                 hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
                                    grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
@@ -1881,6 +2181,19 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             else
                 hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
                                    grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+#else
+            // the slices (their count is on the device) shared out over a grid of resident workgroups
+            const dim3 gl((unsigned)std::min<uint64_t>(slices, 2048));
+            if (ld == 48)
+                hipLaunchKernelGGL(k_fixrow_lp<48>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                                   cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+            else if (ld == 24)
+                hipLaunchKernelGGL(k_fixrow_lp<24>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                                   cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+            else
+                hipLaunchKernelGGL(k_fixrow_lp<12>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                                   cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
+#endif
             fz->valid = true;
             fz->ncodes = ncodes;
         } else if (ld == 48)

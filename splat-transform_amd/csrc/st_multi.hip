@@ -924,12 +924,85 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
     return cursor;
 }
 
+// ST_COLL_TRACE=<dir> (diagnostics): every collective this rank issues, in the order its host
+// threads issue them, one line per call appended to <dir>/coll_rank<r>.txt --
+// "<channel> <op> <type/bytes> <root | from to>", the byte counts the ones every rank passes
+// alike (a gatherv logs the total).  With RCCL (and ST_SIDE_INLINE=1 on a host transport) both
+// channels are issued from the rank's main thread, so the files of all ranks must be identical:
+// the issue-order argument of DESIGN.md (e) that a first RCCL run depends on.
+struct TraceLog {
+    std::mutex mu;
+    FILE *f = nullptr;
+    ~TraceLog() {
+        if (f) fclose(f);
+    }
+    void put(int ch, const char *op, unsigned long long a, long long b = -1, long long c = -1) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!f) return;
+        fprintf(f, "%d %s %llu", ch, op, a);
+        if (b >= 0) fprintf(f, " %lld", b);
+        if (c >= 0) fprintf(f, " %lld", c);
+        fputc('\n', f);
+        fflush(f);
+    }
+};
+struct TraceColl : Coll {
+    Coll *in;
+    int ch;
+    std::shared_ptr<TraceLog> log;
+    std::unique_ptr<TraceColl> side_;
+    TraceColl(Coll *inner, int channel, std::shared_ptr<TraceLog> l) : in(inner), ch(channel), log(std::move(l)) {
+        rank = in->rank;
+        world = in->world;
+    }
+    void allreduce(void *buf, size_t count, Dt dt, Op op, hipStream_t s) override {
+        log->put(ch, op == Op::Sum ? (dt == Dt::F64 ? "allreduce_sum_f64" : "allreduce_sum_i32")
+                                   : (dt == Dt::F64 ? "allreduce_min_f64" : "allreduce_min_i32"),
+                 count);
+        in->allreduce(buf, count, dt, op, s);
+    }
+    void broadcast(void *buf, size_t bytes, int root, hipStream_t s) override {
+        log->put(ch, "broadcast", bytes, root);
+        in->broadcast(buf, bytes, root, s);
+    }
+    void allgather(const void *send, void *recv, size_t bytes, hipStream_t s) override {
+        log->put(ch, "allgather", bytes);
+        in->allgather(send, recv, bytes, s);
+    }
+    void gatherv(const void *send, size_t mybytes, void *recv, const std::vector<size_t> &bytes,
+                 const std::vector<size_t> &displ, int root, hipStream_t s) override {
+        unsigned long long tot = 0;
+        for (size_t b : bytes) tot += b;
+        log->put(ch, "gatherv", tot, root);
+        in->gatherv(send, mybytes, recv, bytes, displ, root, s);
+    }
+    void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
+        log->put(ch, "sendrecv", bytes, from, to);
+        in->sendrecv(buf, bytes, from, to, s);
+    }
+    void abort() override { in->abort(); }
+    Coll *side() override {
+        if (!side_) side_ = std::make_unique<TraceColl>(in->side(), ch + 1, log);
+        return side_.get();
+    }
+    bool enqueues() const override { return in->enqueues(); }
+};
+
 // a failure on this rank aborts the job's channels: the peers' collectives fail instead of
 // waiting for this rank (the communicator is not usable afterwards)
 uint64_t sog_sharded(st_ctx *c, Coll &co, const st_table *const *tabs, int ntab, int iters, const double *draws,
                      uint64_t ndraws, st_sog_meta *meta, const st_sog_textures *out, uint64_t *n_global = nullptr) {
+    std::unique_ptr<TraceColl> tc;
+    if (const char *dir = getenv("ST_COLL_TRACE")) {
+        auto log = std::make_shared<TraceLog>();
+        const std::string path = std::string(dir) + "/coll_rank" + std::to_string(co.rank) + ".txt";
+        log->f = fopen(path.c_str(), "a");
+        ST_REQUIRE(log->f, ST_ERR_ARG, "ST_COLL_TRACE: cannot open " + path);
+        tc = std::make_unique<TraceColl>(&co, 0, log);
+    }
+    Coll &cc = tc ? *tc : co;
     try {
-        return sog_sharded_rank(c, co, tabs, ntab, iters, draws, ndraws, meta, out, n_global);
+        return sog_sharded_rank(c, cc, tabs, ntab, iters, draws, ndraws, meta, out, n_global);
     } catch (...) {
         co.abort();
         throw;

@@ -111,10 +111,38 @@ def test_small_slots_and_side_delays(tmp_path, ref):
           ref(N))
 
 
+def _traces(d, world):
+    return [open(d / f'coll_rank{r}.txt').read().splitlines() for r in range(world)]
+
+
 def test_rccl_issue_order_over_shared_memory(tmp_path, ref):
     """ST_SIDE_INLINE=1: the side channel's gathers issued from the main thread at the fixed
-    program points RCCL uses (the worker only orders and places on rank 0), across processes"""
-    check(*run_job(tmp_path, [0, N // 4, N * 2 // 3, N], env={'ST_SIDE_INLINE': '1'}), ref(N))
+    program points RCCL uses (the worker only orders and places on rank 0), across processes.
+    ST_COLL_TRACE records every collective each rank issues, in issue order: the sequences over
+    both channels are identical on every rank -- what keeps two ranks from enqueueing blocking
+    collectives of the two communicators in opposite orders on a shared hardware queue"""
+    d = tmp_path / 'trace'
+    d.mkdir()
+    check(*run_job(tmp_path, [0, N // 4, N * 2 // 3, N], env={'ST_SIDE_INLINE': '1', 'ST_COLL_TRACE': str(d)}), ref(N))
+    tr = _traces(d, 3)
+    assert tr[0] and all(t == tr[0] for t in tr), [len(t) for t in tr]
+    chans = {ln.split()[0] for ln in tr[0]}
+    ops = {ln.split()[1] for ln in tr[0]}
+    assert chans == {'0', '1'}, chans  # the main and the side channel
+    assert {'allreduce_sum_f64', 'allreduce_sum_i32', 'gatherv'} <= ops, ops
+
+
+def test_issue_order_per_channel_with_side_worker(tmp_path, ref):
+    """the host transports' default: the side channel's calls from the worker thread.  The
+    interleaving of the two channels then varies, but each channel's own sequence is the same on
+    every rank"""
+    d = tmp_path / 'trace'
+    d.mkdir()
+    check(*run_job(tmp_path, [0, N // 2, N], env={'ST_COLL_TRACE': str(d)}), ref(N))
+    tr = _traces(d, 2)
+    for ch in ('0', '1'):
+        seq = [[ln for ln in t if ln.split()[0] == ch] for t in tr]
+        assert seq[0] and seq[0] == seq[1], ch
 
 
 def test_side_channel_off(tmp_path, ref):
