@@ -405,12 +405,38 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
                 'Msplats_per_s': one['Msplats_per_s'], 'split_ms': one['split_ms'], 'reps': reps,
                 'archive_equals_in_memory_step': one['archive_equals_in_memory_step'] and
                 sep['archive_equals_in_memory_step'],
-                'separate_calls': dict(sep, what='st_dev_sog, st_dev_sog_bundle_view, one write(2)')}
+                'separate_calls': dict(sep, what='st_dev_sog, st_dev_sog_bundle_view, one write(2)'),
+                'node_host': node_end_to_end(src, dst, n, iters, reps)}
     finally:
         for f in (src, dst):
             if os.path.exists(f):
                 os.remove(f)
         os.rmdir(d)
+
+
+def node_end_to_end(src, dst, n, iters, reps):
+    """The same job through the Node drop-in host (tools/bench_node.js: js/index.js readPly ->
+    writeSogFile over the N-API addon, as the reference's index.ts:433-510 drives its reader and
+    writer): the PLY read into a host DataTable, then uploaded and written as .sog.  A separate
+    process on the same GPU; None when node or the addon is absent."""
+    import shutil
+    import subprocess
+    node = shutil.which('node')
+    addon = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
+    if not node or not os.path.exists(addon):
+        return None
+    r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(reps), str(iters)],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {'error': r.stderr[-2000:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    runs = sorted(out['runs'], key=lambda x: x['total'])
+    med = runs[len(runs) // 2]
+    return {'what': 'node tools/bench_node.js: readPly(FileHandle) -> host DataTable -> writeSogFile(FileHandle) '
+                    '(js/index.js over napi/addon.node: st_ply_read + st_sog_file), median of the timed reps',
+            'ms': med['total'], 'Msplats_per_s': n / med['total'] / 1e3,
+            'split_ms': {'readPly': med['readPly'], 'writeSogFile': med['writeSogFile']},
+            'rows': out['rows'], 'sog_bytes': out['sog_bytes'], 'reps': len(runs)}
 
 
 def check_labels(sh, prev, lab, n_labels, g):

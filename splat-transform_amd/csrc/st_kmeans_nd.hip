@@ -1224,18 +1224,19 @@ __device__ inline void srow(float (&v)[LD], const float *base) {
     }
 }
 constexpr int FL_WAVES = 4;     // waves per workgroup (one slice's batches shared out)
-constexpr int FL_TS = 65;       // LDS transpose stride (floats): conflict-free both ways
+constexpr int FL_TS = 33;       // LDS transpose stride (floats) of a half batch: conflict-free both ways
 template <int LD>
-__global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
+__global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fixrow_lp(
     const float *__restrict__ aos, int d, const float *__restrict__ caos, int k, const uint2 *__restrict__ grouped,
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ cend, const uint32_t *__restrict__ soff,
     uint32_t ncodes, uint32_t *__restrict__ labels, uint32_t *__restrict__ ties, State *st,
     double *__restrict__ psum, double *__restrict__ pabs, int *__restrict__ pemin, uint32_t *__restrict__ pcnt) {
     constexpr int NQ = LD / 4;
+    constexpr int DT = LD == 48 ? 45 : LD == 24 ? 24 : 9;  // dimensions that can be non-zero (3C, C = 15 / 8 / 3)
     __shared__ double S[16 * LD], A[16 * LD];
     __shared__ int E[16 * LD];
     __shared__ uint32_t C[16];
-    __shared__ float tr[FL_WAVES][LD * FL_TS];
+    __shared__ float tr[FL_WAVES][DT * FL_TS];  // a half batch (32 points) in the lane = dimension layout
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: the batch loop is a wave loop
     const uint32_t nsl = soff[ncodes];
     // f32 screen error constants (u = 2^-24): 4 FMA chains of NQ terms + 3 adds for p.c
@@ -1267,12 +1268,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
         {
             const uint32_t c = code_row(code, lane & 15);
             if (lane < 16 && c < (uint32_t)k) {
-                const float4 *cr = reinterpret_cast<const float4 *>(caos + (uint64_t)c * LD);
+                const float *cr = caos + (uint64_t)c * LD;
                 double nn = 0;
-                for (int q = 0; q < NQ; ++q) {
-                    const float4 v = cr[q];
-                    nn += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-                }
+                for (int q = 0; q < LD; ++q) nn += (double)cr[q] * cr[q];
                 const float cn = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
                 rnc = (float)nn;
                 rbeta = (e1 + 2.0f * rel) * cn;
@@ -1280,34 +1278,23 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
             }
         }
         __syncthreads();
-        // batches of 64 grouped points per wave: wave wv takes batches wv, wv + FL_WAVES, ...
+        const float *cbase = caos + (uint64_t)code_row(code, 0) * LD;
+        const bool allvalid = (code >> 1) * 32 + 32 <= (uint32_t)k;  // every row of the tile below k
+        // batches of 64 grouped points per wave: wave wv takes batches wv, wv + FL_WAVES, ...  No
+        // software pipeline: four workgroups per CU (16 waves) hide each other's gathers
         const uint32_t nb = (b1 - b0 + 63) / 64;
-        auto row_src = [&](uint32_t pt) { return reinterpret_cast<const f32x4 *>(aos + (uint64_t)pt * LD); };
         uint32_t bi = wv;
-        uint32_t pcur = 0, pnx = 0;
-        f32x4 cur[NQ], nxt[NQ];  // native vectors: the wait below ties them in place
-        if (bi < nb) {
-            const uint32_t j = min(b0 + bi * 64 + lane, b1 - 1);
-            pcur = grouped[j].x;
-            const uint32_t j2 = min(b0 + (bi + FL_WAVES) * 64 + lane, b1 - 1);
-            pnx = grouped[j2].x;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) cur[q] = row_src(pcur)[q];
-        }
+        uint32_t pnx = bi < nb ? grouped[min(b0 + bi * 64 + lane, b1 - 1)].x : 0u;
         for (; bi < nb; bi += FL_WAVES) {  // uniform per wave
             const bool have = b0 + bi * 64 + lane < b1;
-            // the next batch's rows and the one after's point indices, in flight while this batch
-            // is scored (by hand: the compiler would sink them to their use)
-            uint32_t pnn;
+            const uint32_t pcur = pnx;
+            f32x4 cur[NQ];
             {
-                const f32x4 *src = row_src(pnx);
-                static_for<NQ>([&](auto qc) {
-                    constexpr int q = decltype(qc)::value;
-                    load16_at<16 * q>(nxt[q], src);
-                });
-                const uint2 *gsrc = grouped + min(b0 + (bi + 2 * FL_WAVES) * 64 + lane, b1 - 1);
-                asm volatile("global_load_dword %0, %1, off" : "=v"(pnn) : "v"(gsrc) : "memory");
+                const f32x4 *src = reinterpret_cast<const f32x4 *>(aos + (uint64_t)pcur * LD);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) cur[q] = src[q];
             }
+            if (bi + FL_WAVES < nb) pnx = grouped[min(b0 + (bi + FL_WAVES) * 64 + lane, b1 - 1)].x;  // the next index
             // |p|^2 and the 16 screens
             f32x2 pa = {0.f, 0.f}, pb = {0.f, 0.f};
 #pragma unroll
@@ -1323,8 +1310,6 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
             // the tile-half's rows: row r at tile row (r & 3) + 8 (r >> 2) (code_row), constant offsets
             // from one base, loaded into SGPRs one row at a time (srow) right before its 2 x NQ packed
             // FMAs; the per-row constants are read from lanes 0..15 at their use
-            const float *cbase = caos + (uint64_t)code_row(code, 0) * LD;
-            const bool allvalid = (code >> 1) * 32 + 32 <= (uint32_t)k;  // every row of the tile below k
             static_for<16>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
                 const float nc = readlane_f<r>(rnc), be = readlane_f<r>(rbeta), ga = readlane_f<r>(rgam);
@@ -1346,19 +1331,6 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
                 s[r] = lo_r;
                 __builtin_amdgcn_sched_barrier(0);  // one row's SGPRs at a time
             });
-            // the batch's rows into the lane = dimension layout (the sums below; the exact path reads
-            // its point back from here)
-            float *t = tr[wv];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                t[(4 * q + 0) * FL_TS + lane] = cur[q].x;
-                t[(4 * q + 1) * FL_TS + lane] = cur[q].y;
-                t[(4 * q + 2) * FL_TS + lane] = cur[q].z;
-                t[(4 * q + 3) * FL_TS + lane] = cur[q].w;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             uint32_t cand = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) cand |= (s[r] <= mh ? 1u : 0u) << r;
@@ -1375,15 +1347,16 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
                     for (int r = 0; r < 16; ++r) valid |= (code_row(code, r) < (uint32_t)k ? 1u : 0u) << r;
                     uint32_t cm = cand & valid;
                     if (!cm) cm = valid;
+                    const float *prow = aos + (uint64_t)pcur * LD;  // re-read: nothing hoisted into registers
                     double best = __builtin_inf();
                     uint32_t bl = 16, cnt = 0;
                     for (uint32_t m = cm; m; m &= m - 1) {  // ascending rows = ascending centroid index
-                        asm volatile("" ::: "memory");  // re-read per row: nothing hoisted into registers
+                        asm volatile("" ::: "memory");
                         const int r = __builtin_ctz(m);
                         const float *cr = caos + (uint64_t)code_row(code, r) * LD;
                         double l = 0;
                         for (int jd = 0; jd < LD; ++jd) {  // kd-tree.ts:26-35: sequential f64 sum of (c - p)^2
-                            const double v = (double)cr[jd] - (double)t[jd * FL_TS + lane];
+                            const double v = (double)cr[jd] - (double)prow[jd];
                             l += v * v;
                         }
                         if (l < best) {
@@ -1401,43 +1374,55 @@ __global__ __launch_bounds__(64 * FL_WAVES) void k_fixrow_lp(
                 labels[pcur] = wc;  // provisional on a tie; the KdTree pass decides
                 if (tie) ties[atomicAdd(&st->ties, 1u)] = pcur;
             }
-            // per cluster: its members' values in this lane's dimension, summed in registers
-            const int jd = lane < LD ? lane : LD - 1;
-            static_for<16>([&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                uint64_t m = __ballot(wl == (uint32_t)c);
-                if (m) {  // uniform
-                    const uint32_t cnt = (uint32_t)__popcll(m);
-                    double sm = 0.0, sa = 0.0;
-                    float mn = __builtin_inff();
-                    while (m) {
-                        const int i = __builtin_ctzll(m);
-                        m &= m - 1;
-                        const float x = t[jd * FL_TS + i];
-                        sm += (double)x;
-                        sa += (double)__builtin_fabsf(x);
-                        mn = fminf(mn, x != 0.0f ? __builtin_fabsf(x) : __builtin_inff());
-                    }
-                    if (lane < LD) {  // padding dimensions add 0 (and no exponent)
-                        const int e = c * LD + fa_slot<LD>(lane);
-                        atomicAdd(&S[e], sm);
-                        atomicAdd(&A[e], sa);
-                        if (mn != __builtin_inff()) atomicMin(&E[e], ulp_exp(mn));
-                    }
-                    if (lane == 0) atomicAdd(&C[c], cnt);
+            // the sums: each half batch's rows through LDS into the lane = dimension layout; per
+            // cluster, its members' values in this lane's dimension summed in registers (their lanes
+            // from one ballot), then added to the slice's LDS sums once
+            float *t = tr[wv];
+            const int jd = lane < DT ? lane : DT - 1;
+            static_for<2>([&](auto hc) {
+                constexpr int hf = decltype(hc)::value;
+                if ((lane >> 5) == hf) {
+                    const int i = lane & 31;
+                    static_for<NQ>([&](auto qc) {
+                        constexpr int q = decltype(qc)::value;
+                        if (4 * q + 0 < DT) t[(4 * q + 0) * FL_TS + i] = cur[q].x;
+                        if (4 * q + 1 < DT) t[(4 * q + 1) * FL_TS + i] = cur[q].y;
+                        if (4 * q + 2 < DT) t[(4 * q + 2) * FL_TS + i] = cur[q].z;
+                        if (4 * q + 3 < DT) t[(4 * q + 3) * FL_TS + i] = cur[q].w;
+                    });
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                static_for<16>([&](auto cc) {
+                    constexpr int c = decltype(cc)::value;
+                    uint64_t m = __ballot(wl == (uint32_t)c);
+                    m = hf ? (m >> 32) : (m & 0xffffffffull);
+                    if (m) {  // uniform
+                        const uint32_t cnt = (uint32_t)__popcll(m);
+                        double sm = 0.0, sa = 0.0;
+                        float mn = __builtin_inff();
+                        while (m) {
+                            const int i = __builtin_ctzll(m);
+                            m &= m - 1;
+                            const float x = t[jd * FL_TS + i];
+                            sm += (double)x;
+                            sa += (double)__builtin_fabsf(x);
+                            mn = fminf(mn, x != 0.0f ? __builtin_fabsf(x) : __builtin_inff());
+                        }
+                        if (lane < DT) {  // the padding dimensions add 0 (and no exponent)
+                            const int e = c * LD + fa_slot<LD>(lane);
+                            atomicAdd(&S[e], sm);
+                            atomicAdd(&A[e], sa);
+                            if (mn != __builtin_inff()) atomicMin(&E[e], ulp_exp(mn));
+                        }
+                        if (lane == 0) atomicAdd(&C[c], cnt);
+                    }
+                });
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             });
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(pnn) : : "memory");
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                // tied to the wait (volatile asm keeps program order): nothing reads the new rows
-                // before the loads have landed
-                asm volatile("" : "+v"(nxt[q]));
-                cur[q] = nxt[q];
-            }
-            pcur = pnx;
-            pnx = pnn;
         }
         __syncthreads();
         for (int e = threadIdx.x; e < 16 * LD; e += 64 * FL_WAVES) {

@@ -1,0 +1,39 @@
+'use strict';
+// The reference CLI's job for `splat-transform in.ply out.sog` through the Node drop-in host
+// (splat-transform_amd/js: readPly -> writeSogFile over the N-API addon), the way the reference's
+// index.ts:433-510 drives it: the PLY is read into a host DataTable (readers/read-ply.ts:111-191),
+// then writeSog writes the .sog into an open FileHandle (writers/write-sog.ts:110-370).
+//   node tools/bench_node.js <in.ply> <out.sog> <reps> <iters>
+// Rep 0 warms the addon, the device buffers and the page cache; reps 1.. are timed.  Prints one
+// JSON line: per-rep milliseconds of readPly, writeSogFile and the whole job, and the .sog size.
+const fs = require('fs');
+const path = require('path');
+
+const host = require(path.join(__dirname, '..', 'splat-transform_amd', 'js'));
+
+const ms = (a, b) => Number(b - a) / 1e6;
+
+(async () => {
+    const [src, dst] = process.argv.slice(2, 4);
+    const reps = parseInt(process.argv[4] || '2', 10);
+    const iters = parseInt(process.argv[5] || '10', 10);
+    const runs = [];
+    let size = 0;
+    let rows = 0;
+    for (let r = 0; r <= reps; ++r) {
+        const t0 = process.hrtime.bigint();
+        const inH = await fs.promises.open(src, 'r');
+        const ply = await host.readPly(inH);
+        await inH.close();
+        const t1 = process.hrtime.bigint();
+        const table = ply.elements.find(e => e.name === 'vertex').dataTable;
+        rows = table.numRows;
+        const outH = await fs.promises.open(dst, 'w');
+        size = await host.writeSogFile(outH, table, iters);
+        await outH.close();
+        const t2 = process.hrtime.bigint();
+        if (r) runs.push({ readPly: ms(t0, t1), writeSogFile: ms(t1, t2), total: ms(t0, t2) });
+    }
+    if (size !== fs.statSync(dst).size) throw new Error('writeSogFile size mismatch');
+    console.log(JSON.stringify({ rows, sog_bytes: size, runs }));
+})().catch((e) => { console.error(e); process.exit(1); });

@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 L=splat-transform_amd/lib
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_sog65k.py tests/test_config2_gpu.py \
-  tests/test_full_verify_gpu.py tests/test_multiproc_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_fix_tests.log 2>&1 \
+  tests/test_full_verify_gpu.py tests/test_multiproc_gpu.py tests/test_process_chain.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_fix_tests.log 2>&1 \
   || { tail -40 gpurun_out/r05_fix_tests.log; exit 1; }
 tail -3 gpurun_out/r05_fix_tests.log
 for rep in 1 2 3; do
@@ -26,4 +26,13 @@ for m in "--dist" ""; do
     > gpurun_out/r05_rank8$m.json 2> gpurun_out/r05_rank8$m.err || { tail -30 gpurun_out/r05_rank8$m.err; exit 1; }
   python3 -c "
 import json; r=json.load(open('gpurun_out/r05_rank8$m.json')); print('1.25M $m', r['config']['parallelism'], round(r['ms_per_step'],2), r['verified'], r['kernels']['kn.sweep'], r['kernels']['kn.fixrow'])"
+done
+# chunk pack: SH bytes staged through LDS (libsplat_hip.so) against direct lane stores (libsplat_hip_cp0.so)
+for rep in 1 2; do
+  for v in cp0 new; do
+    lib=$L/libsplat_hip.so; [ $v = cp0 ] && lib=$L/libsplat_hip_cp0.so
+    ST_LIB=$lib timeout -k 10 200 python3 tools/bench_paths.py > gpurun_out/cp_${v}_$rep.log 2>&1 || { tail -20 gpurun_out/cp_${v}_$rep.log; exit 1; }
+    python3 -c "
+import json; r=json.loads(open('gpurun_out/cp_${v}_$rep.log').read().strip().splitlines()[-1]); print('$v $rep', {k: (round(v['ms'], 3), round(v.get('frac_hbm', 0), 3)) for k, v in r['stages'].items()})"
+  done
 done
