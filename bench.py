@@ -425,7 +425,7 @@ def node_end_to_end(src, dst, n, iters, reps):
     addon = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
     if not node or not os.path.exists(addon):
         return None
-    r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(reps), str(iters)],
+    r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(max(3, reps)), str(iters)],
                        capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         return {'error': r.stderr[-2000:]}

@@ -15,7 +15,11 @@ struct WebpJob {
     uint8_t *out;         // device, >= webp_max_size(w, h) bytes, 4-byte aligned
     uint64_t cap;
     uint64_t size;        // out: bytes of the .webp file
+    bool cache = true;    // try a colour cache (the hit search costs ~0.6 ms per 10 MPix image)
 };
+// the .sog textures a colour cache pays for: measured at 10M SH-3 (profiles/r05/colour_cache.json),
+// only the means textures gain (means_l -0.36%, means_u -2.3%); the others gain bytes, not percents
+bool sog_texture_cache(const char *name);
 
 uint64_t webp_max_size(int w, int h);
 // encodes every job (three stream synchronisations for the whole batch)

@@ -939,8 +939,13 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
     if (again)
         for (int j = 0; j < njobs; ++j)
             if (forced[j]) phase_a(j, 0);
-    for (int j = 0; j < njobs; ++j) cache_stage(j);
-    ST_HIP(hipStreamSynchronize(c->stream));
+    bool any_cache = false;
+    for (int j = 0; j < njobs; ++j)
+        if (jobs[j].cache) {
+            cache_stage(j);
+            any_cache = true;
+        }
+    if (any_cache) ST_HIP(hipStreamSynchronize(c->stream));
     // per image: the colour-cache size; with a cache, the histograms again (a hitting literal is
     // one green symbol)
     std::vector<int> cbits(njobs, 0);
@@ -948,8 +953,9 @@ void webp_encode_dev(st_ctx *c, WebpJob *jobs, int njobs) {
         const uint32_t *h = (const uint32_t *)(hp + stage[j].hist);
         std::vector<uint32_t> merged(vp8l::kTabSize);
         for (int q = 0; q < vp8l::kTabSize; ++q) merged[q] = h[q] + h[vp8l::kTabSize + q];
-        cbits[j] = vp8l::choose_cache_bits(merged.data(), (const uint32_t *)(hp + stage[j].hitlit),
-                                           (const uint32_t *)(hp + stage[j].cidx));
+        if (jobs[j].cache)
+            cbits[j] = vp8l::choose_cache_bits(merged.data(), (const uint32_t *)(hp + stage[j].hitlit),
+                                               (const uint32_t *)(hp + stage[j].cidx));
     });
     bool rehist = false;
     for (int j = 0; j < njobs; ++j) {
@@ -1082,6 +1088,10 @@ void crc32_dev(st_ctx *c, const uint8_t *const *data, const uint64_t *n, const u
 
 namespace st {
 
+bool sog_texture_cache(const char *name) {
+    return !std::strcmp(name, "means_l.webp") || !std::strcmp(name, "means_u.webp");
+}
+
 void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st_sog_textures &tex,
                     uint16_t dos_time, uint16_t dos_date, const uint8_t **out, uint64_t *out_size) {
     // entries in write-sog.ts order (:186-187, :239, :251, :268, :335, :348, :364)
@@ -1106,6 +1116,7 @@ void sog_bundle_dev(st_ctx *c, const st_sog_meta &meta, uint64_t count, const st
         const uint64_t cap = webp_max_size(imgs[i].w, imgs[i].h);
         jobs[i] = {imgs[i].rgba, imgs[i].w, imgs[i].h, imgs[i].w * 4,
                    wsT<uint8_t>(c, "sb.o" + std::to_string(i), cap), cap, 0};
+        jobs[i].cache = sog_texture_cache(imgs[i].name);
     }
     webp_encode_dev(c, jobs.data(), ni);
     const std::string mj = sog_meta_json(meta, count);
@@ -1191,6 +1202,7 @@ uint64_t stage_entries(st_ctx *c, const std::vector<Img> &imgs, const std::vecto
         const uint64_t cap = webp_max_size(imgs[i].w, imgs[i].h);
         jobs[i] = {imgs[i].rgba, imgs[i].w, imgs[i].h, imgs[i].w * 4, wsT<uint8_t>(c, tag + std::to_string(i), cap),
                    cap, 0};
+        jobs[i].cache = sog_texture_cache(imgs[i].name);
     }
     if (ni) webp_encode_dev(c, jobs.data(), ni);
     es.clear();

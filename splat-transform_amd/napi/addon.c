@@ -44,10 +44,13 @@
  *        draws, dosTime, dosDate)             resident
  *        -> {archive, used}
  */
+#define _GNU_SOURCE /* clock_gettime, madvise */
 #include <node_api.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <time.h>
 
 #include "st_abi.h"
 
@@ -60,6 +63,13 @@ static st_ctx *g_ctx = NULL;
             goto fail;                                                  \
         }                                                               \
     } while (0)
+
+/* ST_DEBUG=1: where a long call's time goes, on stderr */
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
 
 static napi_value throw_st(napi_env env, int rc) {
     char buf[600];
@@ -183,6 +193,38 @@ static napi_value new_typed(napi_env env, napi_typedarray_type type, size_t elem
 
 static void set_named(napi_env env, napi_value obj, const char *k, napi_value v) {
     napi_set_named_property(env, obj, k, v);
+}
+
+/* a large output column: its own 2 MiB-aligned allocation with transparent huge pages, handed to
+ * JS as an external ArrayBuffer (freed by its finalizer).  V8's own ArrayBuffers are zero-filled
+ * 4 KiB pages; the reader overwrites every byte anyway, and first-touch faults on 2.5 GB of 4 KiB
+ * pages halved the rate of readPly's device-to-host copies. */
+static void free_column(napi_env env, void *data, void *hint) {
+    int64_t adj;
+    napi_adjust_external_memory(env, -(int64_t)(size_t)hint, &adj);
+    free(data);
+}
+
+static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t elems, size_t esize, void **data) {
+    const size_t bytes = elems * esize, huge = (size_t)2 << 20;
+    if (bytes < ((size_t)8 << 20)) return new_typed(env, type, elems, esize, data);
+    void *p = NULL;
+    const size_t len = (bytes + huge - 1) / huge * huge;
+    if (posix_memalign(&p, huge, len) != 0) {
+        napi_throw_error(env, NULL, "splat-hip: out of host memory for a column");
+        return NULL;
+    }
+    madvise(p, len, MADV_HUGEPAGE);  /* best effort */
+    napi_value ab, ta;
+    if (napi_create_external_arraybuffer(env, p, bytes, free_column, (void *)bytes, &ab) != napi_ok) {
+        free(p);
+        return NULL;
+    }
+    int64_t adj;
+    napi_adjust_external_memory(env, (int64_t)bytes, &adj);
+    if (napi_create_typedarray(env, type, elems, ab, 0, &ta) != napi_ok) return NULL;
+    *data = p;
+    return ta;
 }
 
 static napi_value make_num(napi_env env, double d) {
@@ -1308,7 +1350,9 @@ static napi_value js_sog_file(napi_env env, napi_callback_info info) {
         if (!draws) goto fail;
         if (!get_ctx(env, &ctx)) goto fail;
         st_table tab = {n, (int32_t)m, (const char *const *)names, cols};
+        const double t0 = now_ms();
         int rc = st_sog_file(ctx, &tab, iters, draws, nd, &used, fd, dos_time, dos_date, &size);
+        if (getenv("ST_DEBUG")) fprintf(stderr, "[addon] sogFile: st_sog_file %.1f ms\n", now_ms() - t0);
         free(cols);
         free_strs(names, m);
         if (rc != ST_OK) return throw_st(env, rc);
@@ -1357,7 +1401,9 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
             }
         }
         NAPI_OK(napi_create_array_with_length(env, (size_t)h->nelements, &els));
+        double t_alloc = 0, t_read = 0;
         for (int32_t ei = 0; ei < h->nelements; ++ei) {
+            const double t0 = now_ms();
             const st_ply_element *el = &h->elements[ei];
             napi_value eo, cols, nm;
             void *ptrs[ST_PLY_MAX_PROPS];
@@ -1366,8 +1412,8 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
             set_named(env, eo, "name", nm);
             napi_create_array_with_length(env, (size_t)el->nprops, &cols);
             for (int32_t p = 0; p < el->nprops; ++p) {
-                napi_value co, pn, ta = new_typed(env, tt[el->props[p].type], (size_t)el->count,
-                                                  ts[el->props[p].type], &ptrs[p]);
+                napi_value co, pn, ta = new_typed_big(env, tt[el->props[p].type], (size_t)el->count,
+                                                      ts[el->props[p].type], &ptrs[p]);
                 if (!ta) goto fail;
                 napi_create_object(env, &co);
                 napi_create_string_utf8(env, el->props[p].name, NAPI_AUTO_LENGTH, &pn);
@@ -1375,7 +1421,10 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
                 set_named(env, co, "data", ta);
                 napi_set_element(env, cols, (uint32_t)p, co);
             }
+            const double t1 = now_ms();
             rc = st_ply_read(ctx, fd, h, ei, ptrs);
+            t_alloc += t1 - t0;
+            t_read += now_ms() - t1;
             if (rc != ST_OK) {
                 free(h);
                 return throw_st(env, rc);
@@ -1383,6 +1432,8 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
             set_named(env, eo, "columns", cols);
             napi_set_element(env, els, (uint32_t)ei, eo);
         }
+        if (getenv("ST_DEBUG"))
+            fprintf(stderr, "[addon] readPly: column arrays %.1f ms, st_ply_read %.1f ms\n", t_alloc, t_read);
         set_named(env, out, "comments", comments);
         set_named(env, out, "elements", els);
     }

@@ -29,10 +29,15 @@ const ms = (a, b) => Number(b - a) / 1e6;
         const table = ply.elements.find(e => e.name === 'vertex').dataTable;
         rows = table.numRows;
         const outH = await fs.promises.open(dst, 'w');
+        const t1b = process.hrtime.bigint();
         size = await host.writeSogFile(outH, table, iters);
+        const t1c = process.hrtime.bigint();
         await outH.close();
         const t2 = process.hrtime.bigint();
-        if (r) runs.push({ readPly: ms(t0, t1), writeSogFile: ms(t1, t2), total: ms(t0, t2) });
+        if (r) {
+            runs.push({ readPly: ms(t0, t1), writeSogFile: ms(t1, t2), total: ms(t0, t2),
+                open: ms(t1, t1b), write: ms(t1b, t1c), close: ms(t1c, t2) });
+        }
     }
     if (size !== fs.statSync(dst).size) throw new Error('writeSogFile size mismatch');
     console.log(JSON.stringify({ rows, sog_bytes: size, runs }));
