@@ -335,7 +335,7 @@ PLY_ORDER = (['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [
              ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3'])
 
 
-def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=2):
+def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=3):
     """The CLI's work for `splat-transform in.ply out.sog` on this table: the step's table is
     written once as a binary little-endian 3DGS PLY (62 float properties, 248 B per splat,
     normals 0; untimed), then each timed rep reads the file into device columns

@@ -576,12 +576,7 @@ __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, u
             const float kr = __builtin_ldexpf(1.0f, (int)kbits - 23) * 1.01f + 0x1p-20f, ka = 0x1p-126f;
             const float e1 = __builtin_fabsf(nm1) * kr + ka;
             const float pn = pnorm[p], dp = pdn[p];
-#ifdef ST_WINDOW_R3
-            const float dcm = __builtin_bit_cast(float, cmax_bits[1]);
-            const float W = wbound_pair(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, dcm);
-#else
             const float W = wbound_r(bnd, pn, dp, chalf[code1], chalf_d[code1], cm, ntab_scale, ntab, nm1 + e1);
-#endif
             if (nm2 > nm1 + W + e1 + (__builtin_fabsf(nm2) * kr + ka)) {
                 labels[p] = code1;  // k_fixrow turns the code into the centroid index
                 if (code_hist) atomicAdd(&code_hist[code1], 1u);  // the decided points' grouping counts
@@ -886,6 +881,12 @@ __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict
     }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// a 16-byte load issued where it stands (the compiler would sink it to its use), at an immediate offset
+template <int OFF>
+__device__ inline void load16_at(f32x4 &dst, const void *src) {
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst) : "v"(src), "i"(OFF) : "memory");
+}
 // lane q of a 16-lane DPP row reads x from lane Q of its row (row_newbcast); folded into
 // the consuming VALU op (v_sub_f32_dpp)
 template <int Q>
@@ -924,12 +925,12 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
     // every lane loads (lanes past LD / 4 repeat a slice nobody broadcasts): no branch around
     // the load, so the wait before the scoring covers only the older loads
     const int sq = rr % (LD / 4);
-    auto slice = [&](uint32_t pt) { return reinterpret_cast<const float4 *>(aos + (uint64_t)pt * LD)[sq]; };
+    auto slice = [&](uint32_t pt) { return reinterpret_cast<const f32x4 *>(aos + (uint64_t)pt * LD)[sq]; };
     float4 row[LD / 4];
     uint32_t have = 0xffffffffu, c = 0;
     bool valid = false;
     uint32_t p = point_of(0);
-    float4 cur = slice(p);
+    f32x4 cur = slice(p);  // native vectors: the wait below ties the next row in place
     for (int i = 0; i < cnt; ++i) {
         const uint32_t code = code_of(i);
         const uint32_t pn = point_of(i + 1 < cnt ? i + 1 : i);
@@ -944,11 +945,8 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
         // the next point's slice is loaded by hand so the compiler cannot sink the load below
         // the scoring (it would wait for it at the top of the next iteration); the wait
         // before `cur = nxt` covers it
-        float4 nxt;
-        {
-            const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn * LD) + sq;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt) : "v"(src) : "memory");
-        }
+        f32x4 nxt;
+        load16_at<0>(nxt, reinterpret_cast<const f32x4 *>(aos + (uint64_t)pn * LD) + sq);
         // differences by DPP-broadcast subtracts (v_sub_f32_dpp), squares accumulated in pairs
         // (v_pk_fma_f32): four chains, the screen bound holds for any summation order
         f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
@@ -962,6 +960,7 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
         fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos, aos + (uint64_t)p * LD, p, rr, labels,
                        ties, st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(nxt));  // tied to the wait: nothing reads the row before it landed
         cur = nxt;
         p = pn;
     }
@@ -976,10 +975,8 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
 // (that tile-half's 16 clusters: no atomics outside LDS).  The other points (pairs, ambiguous,
 // exact ties) are summed by k_nd_combine from a short label sort; clusters failing the
 // certificate take the sequential sum over their members in point order (k_nd_seq).
-constexpr uint32_t FA_SL = 4096;  // decided points per slice (one workgroup; 8,192: 2% slower at 10M)
-constexpr int FA_B = 4;           // point rows per prefetch batch of a 16-lane group
-// accumulator slot of dimension j inside a cluster's LD slots: lane q adds dimensions 4q..4q+3,
-// stored q-consecutive so that one atomic instruction's lanes hit consecutive doubles
+constexpr uint32_t FA_SL = 4096;  // decided points per slice (a workgroup's unit of work)
+// accumulator slot of dimension j inside a cluster's LD slots (the layout k_nd_combine reads)
 template <int LD>
 __host__ __device__ inline int fa_slot(int j) { return (j & 3) * (LD / 4) + (j >> 2); }
 constexpr uint32_t OTHER_TIE = 0x80000000u;  // others' value bit: a fix-up tie (also in the slices' range)
@@ -1047,137 +1044,6 @@ __global__ __launch_bounds__(FS_T) void k_fa_slices(const uint32_t *__restrict__
     }
 }
 
-template <int LD>
-__global__ __launch_bounds__(256) void k_fixrow_acc(const float *__restrict__ aos, int d, const float *__restrict__ caos,
-                                                    int k, const uint2 *__restrict__ grouped,
-                                                    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ cend,
-                                                    const uint32_t *__restrict__ soff, uint32_t ncodes,
-                                                    uint32_t *__restrict__ labels, uint32_t *__restrict__ ties,
-                                                    State *st, double *__restrict__ psum, double *__restrict__ pabs,
-                                                    int *__restrict__ pemin, uint32_t *__restrict__ pcnt) {
-    static_assert(FB_RUN == 32, "two run slots per lane");
-    __shared__ double S[16 * LD], A[16 * LD];
-    __shared__ int E[16 * LD];
-    __shared__ uint32_t C[16];
-    const uint32_t sl = blockIdx.x;
-    if (sl >= soff[ncodes]) return;  // uniform
-    uint32_t lo = 0, hi = ncodes;  // the code whose slices hold sl
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (soff[mid] <= sl) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t code = lo;
-    const uint32_t b0 = cend[code] - hist[code] + (sl - soff[code]) * FA_SL;
-    const uint32_t b1 = min(cend[code], b0 + FA_SL);
-    for (int e = threadIdx.x; e < 16 * LD; e += 256) {
-        S[e] = 0.0;
-        A[e] = 0.0;
-        E[e] = 1 << 20;
-    }
-    if (threadIdx.x < 16) C[threadIdx.x] = 0u;
-    __syncthreads();
-    const int rr = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const int gl = (threadIdx.x & 63) & ~15;
-    const uint32_t c = code_row(code, rr);
-    const bool valid = c < (uint32_t)k;
-    float4 row[LD / 4];
-    {
-        const float4 *src = reinterpret_cast<const float4 *>(caos + (uint64_t)(valid ? c : 0) * LD);
-#pragma unroll
-        for (int q = 0; q < LD / 4; ++q) row[q] = src[q];
-    }
-    const int sq = rr % (LD / 4);
-    // the point rows move in batches of FA_B: the next batch's rows are in flight while this
-    // batch is scored and summed (one row in flight per group left the kernel bound by the
-    // gather latency: ~2 TB/s of random 192-B rows)
-    for (uint32_t j0 = b0 + grp * FB_RUN; j0 < b1; j0 += 16 * FB_RUN) {  // uniform per 16-lane group
-        const int cnt = (int)min(b1 - j0, (uint32_t)FB_RUN);
-        const uint32_t pa = rr < cnt ? grouped[j0 + rr].x : 0u;
-        const uint32_t pb = 16 + rr < cnt ? grouped[j0 + 16 + rr].x : 0u;
-        auto point_of = [&](int i) { return (uint32_t)__shfl(i < 16 ? pa : pb, gl + (i & 15), 64); };
-        float4 cur[FA_B], nxt[FA_B];
-        uint32_t pc[FA_B];
-#pragma unroll
-        for (int u = 0; u < FA_B; ++u) {
-            pc[u] = point_of(u < cnt ? u : cnt - 1);
-            cur[u] = reinterpret_cast<const float4 *>(aos + (uint64_t)pc[u] * LD)[sq];
-        }
-        for (int i0 = 0; i0 < cnt; i0 += FA_B) {
-            uint32_t pn[FA_B];
-#pragma unroll
-            for (int u = 0; u < FA_B; ++u) {
-                const int i = i0 + FA_B + u;
-                pn[u] = point_of(i < cnt ? i : cnt - 1);
-                // by hand, so the compiler cannot sink the loads below the scoring; the wait at
-                // the end of the batch covers them
-                const float4 *src = reinterpret_cast<const float4 *>(aos + (uint64_t)pn[u] * LD) + sq;
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(nxt[u]) : "v"(src) : "memory");
-            }
-#pragma unroll
-            for (int u = 0; u < FA_B; ++u) {
-                if (i0 + u >= cnt) break;  // uniform per group
-                f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
-                static_for<LD / 4>([&](auto qc) {
-                    constexpr int q = decltype(qc)::value;
-                    const f32x2 t01 = {row_bcast<q>(cur[u].x) - row[q].x, row_bcast<q>(cur[u].y) - row[q].y};
-                    const f32x2 t23 = {row_bcast<q>(cur[u].z) - row[q].z, row_bcast<q>(cur[u].w) - row[q].w};
-                    a01 = __builtin_elementwise_fma(t01, t01, a01);
-                    a23 = __builtin_elementwise_fma(t23, t23, a23);
-                });
-                const FixOut fo = fix_decide<16>((a01.x + a01.y) + (a23.x + a23.y), valid, c, d, caos,
-                                                 aos + (uint64_t)pc[u] * LD, pc[u], rr, labels, ties, st);
-                if (!fo.tie && rr < LD / 4) {  // lane rr adds dimensions 4 rr .. 4 rr + 3 (padding adds 0)
-                    const uint32_t base = code_local(fo.label) * LD + rr;
-                    const float v[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        atomicAdd(&S[base + w * (LD / 4)], (double)v[w]);
-                        atomicAdd(&A[base + w * (LD / 4)], (double)__builtin_fabsf(v[w]));
-                        if (v[w] != 0.0f) atomicMin(&E[base + w * (LD / 4)], ulp_exp(v[w]));
-                    }
-                    if (rr == 0) atomicAdd(&C[code_local(fo.label)], 1u);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < FA_B; ++u) {
-                cur[u] = nxt[u];
-                pc[u] = pn[u];
-            }
-        }
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 16 * LD; e += 256) {
-        psum[(uint64_t)sl * 16 * LD + e] = S[e];
-        pabs[(uint64_t)sl * 16 * LD + e] = A[e];
-        pemin[(uint64_t)sl * 16 * LD + e] = E[e];
-    }
-    if (threadIdx.x < 16) pcnt[(uint64_t)sl * 16 + threadIdx.x] = C[threadIdx.x];
-}
-
-// ---- the fused fix-up, one lane per point ---------------------------------------------------
-// The same job as k_fixrow_acc -- one slice of one tile-half's decided points: the exact argmin
-// among the half's 16 rows (kd-tree.ts:26-35) and the certified per-cluster sums of calcAverage
-// (k-means.ts:41-63) -- laid out for the vector unit instead of for the gather:
-//   * a lane holds ONE point's row (12 dwordx4 loads; a wave's loads cover 64 rows, the next
-//     batch's in flight while this one is scored);
-//   * the 16 centroid rows are wave-uniform: scalar loads, and the screen is one packed FMA per
-//     two dimensions with the centroid in SGPRs (p.c, not (p - c)^2: half the VALU work);
-//   * the decision is lane-local; the point's row then goes through LDS to the "lane = dimension"
-//     layout, where each cluster's members of the batch are summed in registers (their lanes
-//     found by one ballot per cluster) and added to the slice's LDS sums once per cluster.
-// Screen: s_r = fl(|c_r|^2) - 2 fl(p.c_r) estimates T_r = |c_r|^2 - 2 p.c_r = D_r - |p|^2; the
-// f32 evaluation is within e1 |p||c_r| + e2 |c_r|^2 (+ underflow) of T_r and the reference's f64
-// distance within rel (|p| + |c_r|)^2 of D_r, so [s_r - err_r, s_r + err_r] holds ref_r - |p|^2
-// and the row with the reference's minimum reaches the lowest upper end: one such row decides,
-// otherwise the candidates' exact f64 distances do (an exact tie goes to the KdTree walk).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-// a 16-byte load issued where it stands (the compiler would sink it to its use), at an immediate offset
-template <int OFF>
-__device__ inline void load16_at(f32x4 &dst, const void *src) {
-    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst) : "v"(src), "i"(OFF) : "memory");
-}
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // lane R's value of v, into an SGPR (volatile: read where it stands, not hoisted out of the loop)
@@ -2150,23 +2016,12 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         ST_LAUNCH_CHECK();
         const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
         if (fused) {
-            // the fix-up with the decided points' sums (k_fixrow_acc), one slice per workgroup
+            // the fix-up with the decided points' sums (k_fixrow_lp), slices shared out over the workgroups
             const uint64_t slices = ncodes + n / FA_SL + 1;
             auto *psum = wsT<double>(c, "kn.fasum", slices * 16 * ld);
             auto *pabs = wsT<double>(c, "kn.faabs", slices * 16 * ld);
             auto *pemin = wsT<int>(c, "kn.faemin", slices * 16 * ld);
             auto *pcnt = wsT<uint32_t>(c, "kn.facnt", slices * 16);
-#ifdef ST_FIX_GROUP16
-            if (ld == 48)
-                hipLaunchKernelGGL(k_fixrow_acc<48>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
-            else if (ld == 24)
-                hipLaunchKernelGGL(k_fixrow_acc<24>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
-            else
-                hipLaunchKernelGGL(k_fixrow_acc<12>, dim3((unsigned)slices), dim3(256), 0, c->stream, aos, d, caos, k,
-                                   grouped, hist, cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
-#else
             // the slices (their count is on the device) shared out over a grid of resident workgroups
             const dim3 gl((unsigned)std::min<uint64_t>(slices, 2048));
             if (ld == 48)
@@ -2178,7 +2033,6 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             else
                 hipLaunchKernelGGL(k_fixrow_lp<12>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
                                    cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
-#endif
             fz->valid = true;
             fz->ncodes = ncodes;
         } else if (ld == 48)
