@@ -10,7 +10,7 @@ import re
 import sys
 from collections import defaultdict
 
-KEYS = ('k_fixrow_acc', 'k_code_scatter', 'k_fixpair_b', 'k_sweep<3, 0>', 'k_sweep<3, 1>', 'k_nd_seq', 'k_nd_combine')
+KEYS = ('k_fixrow_lp', 'k_code_scatter', 'k_fixpair_b', 'k_sweep<3, 0>', 'k_sweep<3, 1>', 'k_nd_seq', 'k_nd_combine')
 
 
 def main():

@@ -1,5 +1,5 @@
 #!/bin/bash
-# What bounds the fused fix-up (k_fixrow_acc) and the grouping (k_code_scatter): wave-state and
+# What bounds the fused fix-up (k_fixrow_lp) and the grouping (k_code_scatter): wave-state and
 # LDS counters, then FETCH_SIZE / WRITE_SIZE, each in its own --pmc pass over kn_bench at 10M
 # (kernel trace only).  Summarise with tools/pmc_fix.py.
 set -o pipefail
