@@ -856,8 +856,11 @@ constexpr int FB_RUN = 32;           // consecutive grouped points per 16-lane g
 
 // cursor = exclusive scan of the histogram; each round ranks its points per code in LDS,
 // reserves one range per code with a global atomic, and writes the point indices
+// G = uint2: (point, code) pairs (k_fixrow_b); G = uint32_t: the point alone (the fused fix-up's
+// slices know their code): half the scattered bytes
+template <typename G>
 __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict__ labels, uint32_t n, uint32_t ncodes,
-                                                      uint32_t *__restrict__ cursor, uint2 *__restrict__ grouped) {
+                                                      uint32_t *__restrict__ cursor, G *__restrict__ grouped) {
     __shared__ uint32_t h[FB_MAX_CODES];
     constexpr int PER = FB_TILE / 256;
     for (uint32_t base = blockIdx.x * FB_TILE; base < n; base += gridDim.x * FB_TILE) {
@@ -876,7 +879,12 @@ __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PER; ++j)
-            if (code[j] < ncodes) grouped[h[code[j]] + rank[j]] = make_uint2(base + j * 256 + threadIdx.x, code[j]);
+            if (code[j] < ncodes) {
+                if constexpr (sizeof(G) == 8)
+                    grouped[h[code[j]] + rank[j]] = make_uint2(base + j * 256 + threadIdx.x, code[j]);
+                else
+                    grouped[h[code[j]] + rank[j]] = base + j * 256 + threadIdx.x;
+            }
         __syncthreads();
     }
 }
@@ -1093,7 +1101,7 @@ constexpr int FL_WAVES = 4;     // waves per workgroup (one slice's batches shar
 constexpr int FL_TS = 33;       // LDS transpose stride (floats) of a half batch: conflict-free both ways
 template <int LD>
 __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fixrow_lp(
-    const float *__restrict__ aos, int d, const float *__restrict__ caos, int k, const uint2 *__restrict__ grouped,
+    const float *__restrict__ aos, int d, const float *__restrict__ caos, int k, const uint32_t *__restrict__ grouped,
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ cend, const uint32_t *__restrict__ soff,
     uint32_t ncodes, uint32_t *__restrict__ labels, uint32_t *__restrict__ ties, State *st,
     double *__restrict__ psum, double *__restrict__ pabs, int *__restrict__ pemin, uint32_t *__restrict__ pcnt) {
@@ -1150,7 +1158,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(4
         // software pipeline: four workgroups per CU (16 waves) hide each other's gathers
         const uint32_t nb = (b1 - b0 + 63) / 64;
         uint32_t bi = wv;
-        uint32_t pnx = bi < nb ? grouped[min(b0 + bi * 64 + lane, b1 - 1)].x : 0u;
+        uint32_t pnx = bi < nb ? grouped[min(b0 + bi * 64 + lane, b1 - 1)] : 0u;
         for (; bi < nb; bi += FL_WAVES) {  // uniform per wave
             const bool have = b0 + bi * 64 + lane < b1;
             const uint32_t pcur = pnx;
@@ -1160,7 +1168,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) cur[q] = src[q];
             }
-            if (bi + FL_WAVES < nb) pnx = grouped[min(b0 + (bi + FL_WAVES) * 64 + lane, b1 - 1)].x;  // the next index
+            if (bi + FL_WAVES < nb) pnx = grouped[min(b0 + (bi + FL_WAVES) * 64 + lane, b1 - 1)];  // the next index
             // |p|^2 and the 16 screens
             f32x2 pa = {0.f, 0.f}, pb = {0.f, 0.f};
 #pragma unroll
@@ -1441,7 +1449,7 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
 constexpr uint32_t NS_CAP = 4096;
 __global__ __launch_bounds__(256) void k_nd_seq(const float *__restrict__ aos, int d, int k,
                                                 const uint32_t *__restrict__ flagged, const uint32_t *__restrict__ nflagged,
-                                                const uint2 *__restrict__ grouped, const uint32_t *__restrict__ hist,
+                                                const uint32_t *__restrict__ grouped, const uint32_t *__restrict__ hist,
                                                 const uint32_t *__restrict__ cend, const uint32_t *__restrict__ labels,
                                                 const uint32_t *__restrict__ ostart,
                                                 const uint32_t *__restrict__ ovals, float *__restrict__ cen,
@@ -1458,7 +1466,7 @@ __global__ __launch_bounds__(256) void k_nd_seq(const float *__restrict__ aos, i
         if (i < NS_CAP) m[i] = p;
     };
     for (uint32_t i = cend[code] - hist[code] + threadIdx.x; i < cend[code]; i += 256) {
-        const uint32_t p = grouped[i].x;
+        const uint32_t p = grouped[i];
         if (labels[p] == cl) put(p);
     }
     for (uint32_t j = ostart[cl] + threadIdx.x; j < ostart[cl + 1]; j += 256) {
@@ -2004,15 +2012,20 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         KTimer kt(c, "kn.fixrow");
         auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
         auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
-        auto *grouped = wsT<uint2>(c, "kn.fbpts2", n);
         const bool fused = fz && fz->want && walk_ties;
+        // fused: the grouped points alone (a slice knows its code); otherwise (point, code) pairs
+        auto *grouped = fused ? nullptr : wsT<uint2>(c, "kn.fbpts2", n);
+        auto *grouped1 = fused ? wsT<uint32_t>(c, "kn.fbpts1", n) : nullptr;
         auto *soff = fused ? wsT<uint32_t>(c, "kn.fasoff", (size_t)ncodes + 1) : nullptr;
-        if (fused)  // slice offsets and the codes' starts in one workgroup
+        if (fused) {  // slice offsets and the codes' starts in one workgroup
             hipLaunchKernelGGL(k_fa_slices, dim3(1), dim3(FS_T), 0, c->stream, hist, ncodes, soff, cursor, ndec);
-        else
+            hipLaunchKernelGGL(k_code_scatter<uint32_t>, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream,
+                               labels, (uint32_t)n, ncodes, cursor, grouped1);
+        } else {
             scan_u32(c, hist, cursor, ncodes, ndec);
-        hipLaunchKernelGGL(k_code_scatter, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream, labels,
-                           (uint32_t)n, ncodes, cursor, grouped);
+            hipLaunchKernelGGL(k_code_scatter<uint2>, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream,
+                               labels, (uint32_t)n, ncodes, cursor, grouped);
+        }
         ST_LAUNCH_CHECK();
         const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
         if (fused) {
@@ -2025,13 +2038,13 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             // the slices (their count is on the device) shared out over a grid of resident workgroups
             const dim3 gl((unsigned)std::min<uint64_t>(slices, 2048));
             if (ld == 48)
-                hipLaunchKernelGGL(k_fixrow_lp<48>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                hipLaunchKernelGGL(k_fixrow_lp<48>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped1, hist,
                                    cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             else if (ld == 24)
-                hipLaunchKernelGGL(k_fixrow_lp<24>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                hipLaunchKernelGGL(k_fixrow_lp<24>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped1, hist,
                                    cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             else
-                hipLaunchKernelGGL(k_fixrow_lp<12>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped, hist,
+                hipLaunchKernelGGL(k_fixrow_lp<12>, gl, dim3(64 * FL_WAVES), 0, c->stream, aos, d, caos, k, grouped1, hist,
                                    cursor, soff, ncodes, labels, ties, dstate, psum, pabs, pemin, pcnt);
             fz->valid = true;
             fz->ncodes = ncodes;
@@ -2209,7 +2222,7 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
     // (grid-stride over the flagged list; none: every workgroup returns at once)
     auto *big = wsT<uint32_t>(c, "kn.big", (size_t)k);
     hipLaunchKernelGGL(k_nd_seq, dim3(256), dim3(256), 0, c->stream, aos, d, k, flagged, nflag,
-                       wsT<uint2>(c, "kn.fbpts2", n), wsT<uint32_t>(c, "kn.fbhist", fz.ncodes),
+                       wsT<uint32_t>(c, "kn.fbpts1", n), wsT<uint32_t>(c, "kn.fbhist", fz.ncodes),
                        wsT<uint32_t>(c, "kn.fbcur", fz.ncodes), labels, ostart, ovals, cen, big, nflag + 1);
     ST_LAUNCH_CHECK();
     auto *h = static_cast<uint32_t *>(pinned_slot(c, "kn.hflag", 8));
