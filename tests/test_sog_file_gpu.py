@@ -86,3 +86,69 @@ def test_sog_file_write_error_is_reported(ctx, tmp_path):
     # the context still works afterwards
     meta, used, size = ctx.dev_sog_file(cols, 2, draws, tex, str(tmp_path / 'ok.sog'))
     assert size == os.path.getsize(str(tmp_path / 'ok.sog'))
+
+
+def _sog_file_fd(ctx, cols, tex, draws, fd, iters=2):
+    import ctypes
+
+    import splat_hip as sh
+    t = sh.make_table(cols)
+    out = sh.SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
+                           ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
+    meta, used, size = sh.SogMeta(), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = sh.lib().st_dev_sog_file(ctx.h, ctypes.byref(t), ctypes.c_int32(iters), sh._vp(draws),
+                                  ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
+                                  ctypes.byref(out), ctypes.c_int32(fd), ctypes.c_uint16(0), ctypes.c_uint16(0),
+                                  ctypes.byref(size))
+    return rc, size.value
+
+
+def test_sog_file_needs_a_seekable_descriptor(ctx, tmp_path):
+    """the archive goes out at absolute offsets: a pipe is refused before any work (ST_ERR_ARG,
+    'seekable'), as a negative descriptor is"""
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    n = 70_000
+    cols = bench.synth_table(n, 5, dev)
+    tex = _textures(sh, n, 15, dev)
+    draws = np.random.default_rng(3).random(2 * 65536 * 8)
+    r, w = os.pipe()
+    try:
+        rc, _ = _sog_file_fd(ctx, cols, tex, draws, w)
+    finally:
+        os.close(r)
+        os.close(w)
+    assert rc == sh.ST_ERR_ARG and b'seekable' in sh.lib().st_last_error()
+    rc, _ = _sog_file_fd(ctx, cols, tex, draws, -1)
+    assert rc == sh.ST_ERR_ARG
+
+
+def test_sog_file_over_a_longer_file_is_cut_to_the_archive(ctx, tmp_path):
+    """a descriptor opened without O_TRUNC on a longer file: the file ends where the archive does
+    (a zip reader looks for the end record from the end of the file)"""
+    import io
+    import zipfile
+
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    n = 70_000
+    cols = bench.synth_table(n, 5, dev)
+    tex = _textures(sh, n, 15, dev)
+    draws = np.random.default_rng(3).random(2 * 65536 * 8)
+    path = str(tmp_path / 'old.sog')
+    with open(path, 'wb') as f:
+        f.write(b'\xab' * (8 << 20))  # longer than the archive
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        rc, size = _sog_file_fd(ctx, cols, tex, draws, fd)
+    finally:
+        os.close(fd)
+    assert rc == 0 and os.path.getsize(path) == size < (8 << 20)
+    data = open(path, 'rb').read()
+    assert len(zipfile.ZipFile(io.BytesIO(data)).namelist()) == 8
