@@ -83,8 +83,10 @@ struct NdFused {
     bool want = false, valid = false;
     uint32_t npair = 0, namb = 0, nties_fix = 0, ncodes = 0;
 };
+// (settle: called once the centroids' duplicate-row check has synchronised the stream; true when
+// it changed centroids, and the check runs again -- kmeansnd_loop's pending large-cluster sums)
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
-               km::State *dstate, NdFused *fz = nullptr);
+               km::State *dstate, NdFused *fz = nullptr, const std::function<bool()> &settle = {});
 // after a fused nd_assign (fz.valid): the (dimension, cluster) partials of the shard -- f64 sum,
 // sum|x|, smallest ulp exponent ([dim][k]) and counts -- from the fix-up's slices and the other
 // points, without the member sort (the sharded writer's N-D update)

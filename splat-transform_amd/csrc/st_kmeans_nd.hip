@@ -889,6 +889,66 @@ __global__ __launch_bounds__(256) void k_code_scatter(const uint32_t *__restrict
     }
 }
 
+// the same grouping with one reservation per code per workgroup: each workgroup takes a
+// contiguous run of ~n / gridDim.x points, counts it per code in LDS, reserves each code's range
+// with one global atomic (device-scope atomics cross the XCDs: their number, workgroups x codes
+// met, is what k_code_scatter pays per 4,096-point round), then reads the run's codes again and
+// places each point at the LDS cursor of its code
+template <typename G>
+__global__ __launch_bounds__(256) void k_code_scatter_run(const uint32_t *__restrict__ labels, uint32_t n,
+                                                          uint32_t ncodes, uint32_t *__restrict__ cursor,
+                                                          G *__restrict__ grouped) {
+    __shared__ uint32_t h[FB_MAX_CODES];
+    // runs of a multiple of 4 points: 16-byte label loads, 4 x U per thread in flight
+    const uint32_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~3u;
+    const uint32_t lo = min(n, blockIdx.x * per), hi = min(n, lo + per);
+    for (uint32_t i = threadIdx.x; i < ncodes; i += 256) h[i] = 0;
+    __syncthreads();
+    constexpr int U = 4;
+    const uint4 *l4 = reinterpret_cast<const uint4 *>(labels);
+    uint32_t p = lo + 4 * threadIdx.x;
+    for (; p + (U - 1) * 1024 + 3 < hi; p += U * 1024) {
+        uint4 c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = l4[(p >> 2) + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            for (uint32_t v : {c[u].x, c[u].y, c[u].z, c[u].w})
+                if (v < ncodes) atomicAdd(&h[v], 1u);
+    }
+    for (; p < hi; p += 1024)
+        for (uint32_t q = p; q < min(hi, p + 4); ++q) {
+            const uint32_t v = labels[q];
+            if (v < ncodes) atomicAdd(&h[v], 1u);
+        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ncodes; i += 256)
+        if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);
+    __syncthreads();
+    auto put = [&](uint32_t q, uint32_t c) {
+        if (c >= ncodes) return;
+        const uint32_t at = atomicAdd(&h[c], 1u);
+        if constexpr (sizeof(G) == 8) grouped[at] = make_uint2(q, c);
+        else grouped[at] = q;
+    };
+    p = lo + 4 * threadIdx.x;
+    for (; p + (U - 1) * 1024 + 3 < hi; p += U * 1024) {
+        uint4 c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = l4[(p >> 2) + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t q = p + u * 1024;
+            put(q, c[u].x);
+            put(q + 1, c[u].y);
+            put(q + 2, c[u].z);
+            put(q + 3, c[u].w);
+        }
+    }
+    for (; p < hi; p += 1024)
+        for (uint32_t q = p; q < min(hi, p + 4); ++q) put(q, labels[q]);
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // a 16-byte load issued where it stands (the compiler would sink it to its use), at an immediate offset
 template <int OFF>
@@ -1931,10 +1991,13 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
 // meets first (kd_group_labels, a descent of the tree); exact ties between distinct rows go to
 // the walk over the whole tree.  Without shared rows this is the plain assign.
 void nd_assign(st_ctx *c, const float *const *dcols, int d, uint64_t n, int k, const float *cen, uint32_t *labels,
-               km::State *dstate, NdFused *fz) {
+               km::State *dstate, NdFused *fz, const std::function<bool()> &settle) {
     if (fz) fz->valid = false;
     CenGroups g;
-    if (k > 1 && !getenv("ST_NO_CEN_GROUPS") && cen_groups(c, d, k, cen, &g)) {
+    const bool try_groups = k > 1 && !getenv("ST_NO_CEN_GROUPS");
+    bool grouped = try_groups && cen_groups(c, d, k, cen, &g);
+    if (settle && settle()) grouped = try_groups && cen_groups(c, d, k, cen, &g);
+    if (grouped) {
         const uint32_t nties = nd_assign_core(c, dcols, d, n, (int)g.kr, g.cen_r, labels, dstate, false);
         const int ld = aos_ld(d);
         auto *aos = wsT<float>(c, "kn.aos", n * (size_t)ld);
@@ -2017,14 +2080,25 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         auto *grouped = fused ? nullptr : wsT<uint2>(c, "kn.fbpts2", n);
         auto *grouped1 = fused ? wsT<uint32_t>(c, "kn.fbpts1", n) : nullptr;
         auto *soff = fused ? wsT<uint32_t>(c, "kn.fasoff", (size_t)ncodes + 1) : nullptr;
+        // workgroups of the one-reservation grouping (0: k_code_scatter's 4,096-point rounds)
+        static const int cs_wg = getenv("ST_CS_WG") ? atoi(getenv("ST_CS_WG")) : 256;
+        const unsigned gcs = cs_wg > 0 ? grid_for(n, 256, (unsigned)cs_wg) : grid_for(n, FB_TILE, 2048);
         if (fused) {  // slice offsets and the codes' starts in one workgroup
             hipLaunchKernelGGL(k_fa_slices, dim3(1), dim3(FS_T), 0, c->stream, hist, ncodes, soff, cursor, ndec);
-            hipLaunchKernelGGL(k_code_scatter<uint32_t>, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream,
-                               labels, (uint32_t)n, ncodes, cursor, grouped1);
+            if (cs_wg > 0)
+                hipLaunchKernelGGL(k_code_scatter_run<uint32_t>, dim3(gcs), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                                   ncodes, cursor, grouped1);
+            else
+                hipLaunchKernelGGL(k_code_scatter<uint32_t>, dim3(gcs), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                                   ncodes, cursor, grouped1);
         } else {
             scan_u32(c, hist, cursor, ncodes, ndec);
-            hipLaunchKernelGGL(k_code_scatter<uint2>, dim3(grid_for(n, FB_TILE, 2048)), dim3(256), 0, c->stream,
-                               labels, (uint32_t)n, ncodes, cursor, grouped);
+            if (cs_wg > 0)
+                hipLaunchKernelGGL(k_code_scatter_run<uint2>, dim3(gcs), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                                   ncodes, cursor, grouped);
+            else
+                hipLaunchKernelGGL(k_code_scatter<uint2>, dim3(gcs), dim3(256), 0, c->stream, labels, (uint32_t)n,
+                                   ncodes, cursor, grouped);
         }
         ST_LAUNCH_CHECK();
         const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
@@ -2225,21 +2299,34 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
                        wsT<uint32_t>(c, "kn.fbpts1", n), wsT<uint32_t>(c, "kn.fbhist", fz.ncodes),
                        wsT<uint32_t>(c, "kn.fbcur", fz.ncodes), labels, ostart, ovals, cen, big, nflag + 1);
     ST_LAUNCH_CHECK();
+    // the count of uncertified clusters too large for k_nd_seq is read at the next host sync
+    // (nd_big_sums, before anything reads these centroids): no sync of its own
     auto *h = static_cast<uint32_t *>(pinned_slot(c, "kn.hflag", 8));
     ST_HIP(hipMemcpyAsync(h, nflag, 8, hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
-    if (getenv("ST_DEBUG"))
+    if (getenv("ST_DEBUG")) {
+        ST_HIP(hipStreamSynchronize(c->stream));
         fprintf(stderr, "[st kmeans] fused update: others=%u uncertified clusters=%u over %u members=%u\n", m, h[0],
                 NS_CAP, h[1]);
-    if (h[1]) {  // uncertified clusters too large for k_nd_seq: the member sort, then their sums
-        auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
-        auto *members = wsT<uint32_t>(c, "kn.members", n);
-        auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
-        member_sort(c, labels, n, k, sorted_labels, members, start);
-        hipLaunchKernelGGL(k_sumnd<float>, dim3((h[1] + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k,
-                           cen, 0xffffffffu, 0u, (uint32_t *)nullptr, (uint32_t *)nullptr, big, nflag + 1);
-        ST_LAUNCH_CHECK();
     }
+    return true;
+}
+
+// the fused update's pending count (kn.hflag, copied behind its kernels): the clusters k_nd_seq
+// left to the member sort get their sequential sums now.  Their rows are disjoint from the
+// re-seeded (empty) ones queued in between.  Returns true when centroids changed.
+bool nd_big_sums(st_ctx *c, int d, uint64_t n, int k, const uint32_t *labels, float *cen) {
+    ST_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t nbig = static_cast<uint32_t *>(pinned_slot(c, "kn.hflag", 8))[1];
+    if (!nbig) return false;
+    auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
+    auto *sorted_labels = wsT<uint32_t>(c, "kn.slab", n);
+    auto *members = wsT<uint32_t>(c, "kn.members", n);
+    auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
+    member_sort(c, labels, n, k, sorted_labels, members, start);
+    hipLaunchKernelGGL(k_sumnd<float>, dim3((nbig + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen,
+                       0xffffffffu, 0u, (uint32_t *)nullptr, (uint32_t *)nullptr, wsT<uint32_t>(c, "kn.big", (size_t)k),
+                       wsT<uint32_t>(c, "kn.nflag", 2) + 1);
+    ST_LAUNCH_CHECK();
     return true;
 }
 }  // namespace
@@ -2291,15 +2378,23 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
     auto *counts = wsT<uint32_t>(c, "kn.counts", (size_t)k);
     nd_prepare(c, dcols, d, n);
     const size_t cbytes = (size_t)k * d * sizeof(float);
+    // a fused update's large uncertified clusters are summed at the next assign's first sync
+    bool pending = false;
+    const std::function<bool()> settle = [&]() {
+        pending = false;
+        return nd_big_sums(c, d, n, k, labels, cen);
+    };
     for (int it = 0; it < iters; ++it) {
+        if (pending && c->verify && it == iters - 1) settle();
         if (c->verify && it == iters - 1)
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         NdFused fz;
         fz.want = !aos64 && !getenv("ST_ND_SORT");
-        nd_assign(c, dcols, d, n, k, cen, labels, dstate, &fz);
+        nd_assign(c, dcols, d, n, k, cen, labels, dstate, &fz, pending ? settle : std::function<bool()>());
         // update
         if (fz.valid && nd_fused_update(c, d, n, k, fz, labels, cen, counts, dstate)) {
             reseed_empty_counts(c, dcols, d, n, k, counts, ddraws, ndraws, dstate, cen);
+            pending = true;
         } else {
             member_sort(c, labels, n, k, sorted_labels, members, start);
             {
@@ -2311,6 +2406,7 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         }
         mark(c, "kn.update");
     }
+    if (pending) settle();
     if (c->verify && iters > 0) {
         ST_HIP(hipMemcpyAsync(ws(c, "verify.cen", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         ST_HIP(hipMemcpyAsync(ws(c, "verify.labels", n * 4), labels, n * 4, hipMemcpyDeviceToDevice, c->stream));

@@ -60,3 +60,6 @@ print(f'kmeans total {(time.perf_counter() - t0) * 1e3:.1f} ms ({a.iters} iters,
 for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'kn.groups', 'kn.ties', 'kn.sumnd'):
     ms, cnt = ctx.kernel_stats(name)
     print(f'{name}: {ms / max(cnt, 1):.3f} ms x {cnt}')
+import hashlib
+print('result sha256', hashlib.sha256(cen.cpu().numpy().tobytes() + lab.cpu().numpy().tobytes()).hexdigest()[:16],
+      'draws used', used)
