@@ -287,6 +287,13 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
                      const uint8_t *scale_lab, const uint8_t *color_lab, const uint32_t *shn_lab, st_sog_meta *meta,
                      const st_sog_textures *out);
 void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *out);
+// the scales / sh0 texels of n rows in row order (byte labels: three planes of n; opacity nullable)
+void sog_table_rows(st_ctx *c, uint64_t n, const uint8_t *lab, const float *opacity, uint8_t *out);
+// cluster1d of the scales (a) and the colours (b) as the single-device writer runs them (b beside a
+// on the context `side`, speculatively from draw 0); returns the draws both took
+uint64_t cluster1d_pair_dev(st_ctx *c, st_ctx *side, const float *const *a, const float *const *b, uint64_t n,
+                            int iters, const double *draws, uint64_t ndraws, float *cb_a, uint8_t *lab_a, float *cb_b,
+                            uint8_t *lab_b);
 
 // PLY ingest / compressed-PLY reader (st_ply.hip)
 void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols);

@@ -12,7 +12,10 @@
 //     sum is that sum (every partial sum is exact); the remaining (cluster, dim) pairs replay the
 //     sequential sum, the running value handed from segment to segment in global order.
 //     Math.random: every rank holds the same draws and consumes them identically; a drawn row
-//     is supplied by its owner (bit patterns, integer SUM all-reduce).
+//     is supplied by its owner (bit patterns, integer SUM all-reduce).  That is the SH palette's
+//     k-means; the two cluster1d (scales, colours: 28 B of columns per row, 20 latency-bound
+//     iterations) run on rank 0 over the gathered columns as on one device, and every rank
+//     takes the draws they consumed from rank 0.
 //   * Morton order (ordering.ts:4-110) is global: rank 0 gathers x/y/z and orders the whole
 //     table; every rank writes the texels of its rows in row order and rank 0 places them at
 //     their Morton positions.  Both run beside the k-means: a side host thread per rank moves
@@ -537,22 +540,6 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     return cursor;
 }
 
-// cluster1d (write-sog.ts:56-99) over the global table: codebook + byte labels of the local rows
-uint64_t cluster1d_sharded(st_ctx *c, Coll &co, const Shard &sh, const float *const *cols, int ncols, int iters,
-                           const double *draws, uint64_t ndraws, float *cb256, uint8_t *lab8) {
-    ST_REQUIRE(sh.N * ncols >= 256, ST_ERR_ARG,
-               "cluster1d: fewer than 256 values (the reference's kmeans returns a plain Array and .subarray throws)");
-    auto *data = wsT<float>(c, "mg.c1data", sh.n * ncols);
-    for (int i = 0; i < ncols; ++i)
-        if (sh.n) ST_HIP(hipMemcpyAsync(data + i * sh.n, cols[i], 4 * sh.n, hipMemcpyDeviceToDevice, c->stream));
-    Points P{&sh, true, 1, ncols, sh.n * ncols, sh.N * ncols, {data}};
-    auto *cen = wsT<float>(c, "mg.c1cen", 256);
-    auto *lab = wsT<uint32_t>(c, "mg.c1lab", P.n);
-    const uint64_t used = kmeans_sharded(c, co, P, 256, iters, draws, ndraws, cen, lab, "mg.k1");
-    codebook_dev(c, cen, lab, P.n, cb256, lab8);
-    return used;
-}
-
 // the rank's rows of the member columns (the combine of its local tables: every column of the
 // union, absent ones zero-filled, index.ts:158-210); band from the union over every rank
 struct LocalTable {
@@ -790,7 +777,8 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
         gath = wsT<uint32_t>(c, "mg.gath", N * 5);
     }
     uint8_t *loc[6];
-    for (int i = 0; i < ntex; ++i) loc[i] = wsT<uint8_t>(c, std::string("mg.loc.") + texn[i], sh.n * 4 + 4);
+    for (int i = 0; i < ntex; ++i)  // (the scales / sh0 texels are rank 0's, in global row order)
+        loc[i] = (i == 3 || i == 4) ? nullptr : wsT<uint8_t>(c, std::string("mg.loc.") + texn[i], sh.n * 4 + 4);
     uint8_t *dst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (root) {
         uint8_t *o[6] = {out->means_l, out->means_u, out->quats, out->scales, out->sh0, out->shn_labels};
@@ -840,22 +828,45 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
             hi[a] = -h6[3 + a];
         }
     }
+    // cluster1d of the scales and the colours (write-sog.ts:245-268) on rank 0 over the gathered
+    // global columns: the single-device block (cluster1d_pair_dev, the colours beside the scales),
+    // not a sharded k-means -- 2 x 10 latency-bound iterations whose all-reduces, read-backs and
+    // sequential hand-offs cost every rank more than moving 7 columns (28 B per row) into rank 0.
+    // Rank 0 writes the scales / sh0 texels in global row order straight into the gather buffer
+    // the placement reads; every rank learns the draws they took from rank 0.
     uint64_t cursor = 0;
-    auto *slab = wsT<uint8_t>(c, "mg.slab", sh.n * 3 + 1);
-    auto *clab = wsT<uint8_t>(c, "mg.clab", sh.n * 3 + 1);
     auto *cb = wsT<float>(c, "mg.cb", 256);
     st_sog_meta lm{};
-    cursor += cluster1d_sharded(c, co, sh, m + 3, 3, iters, draws + cursor, ndraws - cursor, cb, slab);
-    if (root) ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 1024, hipMemcpyDeviceToHost, c->stream));
-    cursor += cluster1d_sharded(c, co, sh, m + 6, 3, iters, draws + cursor, ndraws - cursor, cb, clab);
-    if (root) ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb, 1024, hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
+    {
+        float *g7 = root ? wsT<float>(c, "mg.g1d", N * 7) : nullptr;  // scale_0..2, f_dc_0..2, opacity
+        for (int i = 0; i < 7; ++i) co.gatherv(m[3 + i], 4 * sh.n, g7 ? g7 + N * i : nullptr, bytes, displ, 0, c->stream);
+        auto *dused = wsT<unsigned long long>(c, "mg.used1d", 1);
+        auto *hused = static_cast<unsigned long long *>(pinned_slot(c, "mg.used1d", 8));
+        if (root) {
+            if (!mc->aux) ST_REQUIRE(st_ctx_create(c->device, &mc->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+            const float *sc3[3] = {g7, g7 + N, g7 + 2 * N}, *co3[3] = {g7 + 3 * N, g7 + 4 * N, g7 + 5 * N};
+            auto *slab = wsT<uint8_t>(c, "mg.slab", N * 3);
+            auto *clab = wsT<uint8_t>(c, "mg.clab", N * 3);
+            auto *cb_c = wsT<float>(c, "mg.cb_c", 256);
+            const uint64_t used = cluster1d_pair_dev(c, mc->aux, sc3, co3, N, iters, draws, ndraws, cb, slab, cb_c, clab);
+            ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 1024, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb_c, 1024, hipMemcpyDeviceToHost, c->stream));
+            sog_table_rows(c, N, slab, nullptr, (uint8_t *)(gath + N * 3));
+            sog_table_rows(c, N, clab, g7 + N * 6, (uint8_t *)(gath + N * 4));
+            *hused = used;
+            ST_HIP(hipMemcpyAsync(dused, hused, 8, hipMemcpyHostToDevice, c->stream));
+        }
+        co.broadcast(dused, 8, 0, c->stream);
+        ST_HIP(hipMemcpyAsync(hused, dused, 8, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipStreamSynchronize(c->stream));
+        cursor += *hused;
+    }
 
-    // this rank's texels in local row order (4 bytes per row and texture)
+    // this rank's means / quats texels in local row order (4 bytes per row and texture)
     auto *rows = wsT<uint32_t>(c, "mg.iota", sh.n + 1);
     if (sh.n) iota_u32(c, rows, sh.n);
-    st_sog_textures lt{loc[0], loc[1], loc[2], loc[3], loc[4], nullptr, nullptr};
-    sog_scatter_dev(c, t, rows, lo, hi, slab, clab, nullptr, &lm, &lt);
+    st_sog_textures lt{loc[0], loc[1], loc[2], nullptr, nullptr, nullptr, nullptr};
+    sog_scatter_dev(c, t, rows, lo, hi, nullptr, nullptr, nullptr, &lm, &lt);
     if (root) {
         for (int a = 0; a < 3; ++a) {
             meta->means_min[a] = lm.means_min[a];
@@ -865,7 +876,7 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
     ST_HIP(hipEventRecord(ev[2], c->stream));
     side_coll([&] {
         ST_HIP(hipStreamWaitEvent(cs, ev[2], 0));
-        for (int i = 0; i < 5; ++i) bk->gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0, cs);
+        for (int i = 0; i < 3; ++i) bk->gatherv(loc[i], 4 * sh.n, gath ? gath + N * i : nullptr, bytes, displ, 0, cs);
         ST_HIP(hipEventRecord(ev[3], cs));
     });
     if (root)

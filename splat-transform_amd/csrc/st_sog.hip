@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_invert(const uint32_t *__restrict__ idx
 // Texture kernels run in two forms: gather (texel i <- row idx[i], the single-device
 // writeSog) or scatter (local row i -> texel pos[i], one shard of a multi-GPU writeSog)
 __device__ inline void tex_slot(const uint32_t *idx, const uint32_t *pos, uint64_t i, uint32_t &row, uint64_t &o) {
-    row = pos ? (uint32_t)i : idx[i];
+    row = pos ? (uint32_t)i : idx ? idx[i] : (uint32_t)i;  // neither: row order
     o = pos ? (uint64_t)pos[i] : i;
 }
 
@@ -288,6 +288,55 @@ void sog_scatter_dev(st_ctx *c, const st_table *t, const uint32_t *pos, const do
         hipLaunchKernelGGL(k_shn_labels_tex, dim3(g), dim3(256), 0, c->stream, shn_lab, (const uint32_t *)nullptr,
                            pos, n, (uint32_t *)out->shn_labels);
     ST_LAUNCH_CHECK();
+}
+
+// the scales / sh0 texels (write-sog.ts:245-268) of n rows in row order: out[r] from the byte labels
+// lab[0..3n) (three planes) and the opacity (nullable: alpha 255)
+void sog_table_rows(st_ctx *c, uint64_t n, const uint8_t *lab, const float *opacity, uint8_t *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_table_tex<float>, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c->stream, lab, lab + n,
+                       lab + 2 * n, opacity, (const uint32_t *)nullptr, (const uint32_t *)nullptr, n, (uint32_t *)out);
+    ST_LAUNCH_CHECK();
+}
+
+// cluster1d of the scales (a) then of the colours (b), write-sog.ts:245-268, as sog_impl runs
+// them: b on the context `side` from its own host thread, from draw 0 (re-seeds of empty
+// clusters are the only draws a 1-D k-means takes, and b's come after a's), kept when a took no
+// draw and otherwise rerun here at a's cursor.  Returns the draws both took.
+uint64_t cluster1d_pair_dev(st_ctx *c, st_ctx *side, const float *const *a, const float *const *b, uint64_t n,
+                            int iters, const double *draws, uint64_t ndraws, float *cb_a, uint8_t *lab_a, float *cb_b,
+                            uint8_t *lab_b) {
+    {
+        hipEvent_t ev;  // the columns: whatever the caller queued on c->stream first
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, c->stream));
+        ST_HIP(hipStreamWaitEvent(side->stream, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+    }
+    uint64_t used_b = 0;
+    std::exception_ptr err_b;
+    std::thread th([&] {
+        try {
+            use_device(side);
+            used_b = cluster1d_dev(side, b, 3, n, iters, draws, ndraws, cb_b, lab_b);
+            ST_HIP(hipStreamSynchronize(side->stream));
+        } catch (...) {
+            err_b = std::current_exception();
+        }
+    });
+    struct Join {
+        std::thread &t;
+        ~Join() {
+            if (t.joinable()) t.join();
+        }
+    } join{th};
+    const uint64_t used_a = cluster1d_dev(c, a, 3, n, iters, draws, ndraws, cb_a, lab_a);
+    th.join();
+    if (used_a == 0) {
+        if (err_b) std::rethrow_exception(err_b);
+        return used_b;
+    }
+    return used_a + cluster1d_dev(c, b, 3, n, iters, draws + used_a, ndraws - used_a, cb_b, lab_b);
 }
 
 void shn_centroids_dev(st_ctx *c, const uint8_t *cl, int C, int pal, uint8_t *out) {

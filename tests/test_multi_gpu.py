@@ -86,6 +86,28 @@ def test_group_duplicated_rows_and_clumps_equal_single_device(ctx):
         g.close()
 
 
+@pytest.mark.parametrize('who', ['scales', 'colours', 'neither'])
+def test_group_cluster1d_reseeds_equal_single_device(ctx, who):
+    """The two cluster1d run on rank 0 over the gathered columns, the colours beside the scales
+    from draw 0 (kept only when the scales took no draw, rerun after them otherwise; re-seeds of
+    empty clusters, k-means.ts:174-178).  A far outlier in a column leaves most linspace centroids
+    (k-means.ts:23-39) without members, so that cluster1d takes draws; shards of 3 ranks, one
+    empty, and every rank must continue from the draws rank 0 reports."""
+    n = 20_011
+    cols = _table(n, 91, C=3)
+    rng = np.random.default_rng(92)
+    for k in {'scales': ['scale_0', 'scale_2'], 'colours': ['f_dc_1'], 'neither': []}[who]:
+        cols[k] = (rng.integers(0, 4, n) * 0.25 - 5).astype(np.float32)
+        cols[k][17] = 40.0
+    draws = np.random.default_rng(93).random(1 << 17)
+    want = ctx.sog(cols, 2, draws)
+    g = sh.Group([0] * 3, host_staged=True)
+    try:
+        _same(g.sog([cols], 2, draws, [0, 0, 7000, n]), want)
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize('world,splits,adv', [(2, None, False), (3, 'empty0', False), (4, 'ragged', True)])
 def test_group_host_staged_equals_single_device(ctx, world, splits, adv):
     n = 30_011
