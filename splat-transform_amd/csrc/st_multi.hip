@@ -14,8 +14,8 @@
 //     Math.random: every rank holds the same draws and consumes them identically; a drawn row
 //     is supplied by its owner (bit patterns, integer SUM all-reduce).  That is the SH palette's
 //     k-means; the two cluster1d (scales, colours: 28 B of columns per row, 20 latency-bound
-//     iterations) run on rank 0 over the gathered columns as on one device, and every rank
-//     takes the draws they consumed from rank 0.
+//     iterations) run over the gathered columns as on one device, the scales on rank 0 and the
+//     colours on rank 1, and every rank takes the draws they consumed from those two.
 //   * Morton order (ordering.ts:4-110) is global: rank 0 gathers x/y/z and orders the whole
 //     table; every rank writes the texels of its rows in row order and rank 0 places them at
 //     their Morton positions.  Both run beside the k-means: a side host thread per rank moves
@@ -828,38 +828,66 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
             hi[a] = -h6[3 + a];
         }
     }
-    // cluster1d of the scales and the colours (write-sog.ts:245-268) on rank 0 over the gathered
-    // global columns: the single-device block (cluster1d_pair_dev, the colours beside the scales),
-    // not a sharded k-means -- 2 x 10 latency-bound iterations whose all-reduces, read-backs and
-    // sequential hand-offs cost every rank more than moving 7 columns (28 B per row) into rank 0.
-    // Rank 0 writes the scales / sh0 texels in global row order straight into the gather buffer
-    // the placement reads; every rank learns the draws they took from rank 0.
+    // cluster1d of the scales and of the colours (write-sog.ts:245-268) over the gathered global
+    // columns, as on one device: not a sharded k-means -- 2 x 10 latency-bound iterations whose
+    // all-reduces, read-backs and sequential hand-offs cost every rank more than moving the
+    // columns (28 B per row).  The scales on rank 0, the colours on rank 1 from draw 0 (its
+    // re-seed draws follow the scales': kept when the scales took none, rerun after them
+    // otherwise); with one rank both on rank 0, the colours on a side context
+    // (cluster1d_pair_dev).  The scales / sh0 texels go in global row order into the gather
+    // buffer rank 0 places from; every rank takes the draws both consumed.
     uint64_t cursor = 0;
     auto *cb = wsT<float>(c, "mg.cb", 256);
     st_sog_meta lm{};
     {
-        float *g7 = root ? wsT<float>(c, "mg.g1d", N * 7) : nullptr;  // scale_0..2, f_dc_0..2, opacity
-        for (int i = 0; i < 7; ++i) co.gatherv(m[3 + i], 4 * sh.n, g7 ? g7 + N * i : nullptr, bytes, displ, 0, c->stream);
+        const int cr = co.world > 1 ? 1 : 0;  // the colours' rank
+        const bool mine_c = co.rank == cr;
+        float *gs = root ? wsT<float>(c, "mg.g1s", N * 3) : nullptr;    // scale_0..2
+        float *gc = mine_c ? wsT<float>(c, "mg.g1c", N * 4) : nullptr;  // f_dc_0..2, opacity
+        for (int i = 0; i < 3; ++i) co.gatherv(m[3 + i], 4 * sh.n, gs ? gs + N * i : nullptr, bytes, displ, 0, c->stream);
+        for (int i = 0; i < 4; ++i) co.gatherv(m[6 + i], 4 * sh.n, gc ? gc + N * i : nullptr, bytes, displ, cr, c->stream);
+        const float *sc3[3] = {gs, gs + N, gs + 2 * N};
+        const float *co3[3] = {gc, gc + N, gc + 2 * N};
+        auto *slab = root ? wsT<uint8_t>(c, "mg.slab", N * 3) : nullptr;
+        auto *clab = mine_c ? wsT<uint8_t>(c, "mg.clab", N * 3) : nullptr;
+        auto *cb_c = wsT<float>(c, "mg.cb_c", 256);
         auto *dused = wsT<unsigned long long>(c, "mg.used1d", 1);
         auto *hused = static_cast<unsigned long long *>(pinned_slot(c, "mg.used1d", 8));
-        if (root) {
+        // rank `from`'s count of draws, on every rank
+        auto share = [&](uint64_t v, int from) -> uint64_t {
+            if (co.rank == from) {
+                *hused = v;
+                ST_HIP(hipMemcpyAsync(dused, hused, 8, hipMemcpyHostToDevice, c->stream));
+            }
+            co.broadcast(dused, 8, from, c->stream);
+            ST_HIP(hipMemcpyAsync(hused, dused, 8, hipMemcpyDeviceToHost, c->stream));
+            ST_HIP(hipStreamSynchronize(c->stream));
+            return *hused;
+        };
+        if (cr == 0) {
             if (!mc->aux) ST_REQUIRE(st_ctx_create(c->device, &mc->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
-            const float *sc3[3] = {g7, g7 + N, g7 + 2 * N}, *co3[3] = {g7 + 3 * N, g7 + 4 * N, g7 + 5 * N};
-            auto *slab = wsT<uint8_t>(c, "mg.slab", N * 3);
-            auto *clab = wsT<uint8_t>(c, "mg.clab", N * 3);
-            auto *cb_c = wsT<float>(c, "mg.cb_c", 256);
-            const uint64_t used = cluster1d_pair_dev(c, mc->aux, sc3, co3, N, iters, draws, ndraws, cb, slab, cb_c, clab);
+            cursor += cluster1d_pair_dev(c, mc->aux, sc3, co3, N, iters, draws, ndraws, cb, slab, cb_c, clab);
+        } else {
+            uint64_t used_s = 0, used_c = 0;
+            if (root) used_s = cluster1d_dev(c, sc3, 3, N, iters, draws, ndraws, cb, slab);
+            if (mine_c) used_c = cluster1d_dev(c, co3, 3, N, iters, draws, ndraws, cb_c, clab);
+            used_s = share(used_s, 0);
+            if (mine_c && used_s)  // the scales took draws: the colours' k-means starts after them
+                used_c = cluster1d_dev(c, co3, 3, N, iters, draws + used_s, ndraws - used_s, cb_c, clab);
+            used_c = share(used_c, cr);
+            cursor += used_s + used_c;
+            // the colours' texels (global row order) and codebook to rank 0
+            uint8_t *ctex = root ? (uint8_t *)(gath + N * 4) : mine_c ? wsT<uint8_t>(c, "mg.ctex", N * 4) : nullptr;
+            if (mine_c) sog_table_rows(c, N, clab, gc + N * 3, ctex);
+            co.sendrecv(ctex, 4 * N, cr, 0, c->stream);
+            co.sendrecv(cb_c, 1024, cr, 0, c->stream);
+        }
+        if (root) {
             ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 1024, hipMemcpyDeviceToHost, c->stream));
             ST_HIP(hipMemcpyAsync(meta->sh0_codebook, cb_c, 1024, hipMemcpyDeviceToHost, c->stream));
             sog_table_rows(c, N, slab, nullptr, (uint8_t *)(gath + N * 3));
-            sog_table_rows(c, N, clab, g7 + N * 6, (uint8_t *)(gath + N * 4));
-            *hused = used;
-            ST_HIP(hipMemcpyAsync(dused, hused, 8, hipMemcpyHostToDevice, c->stream));
+            if (cr == 0) sog_table_rows(c, N, clab, gc + N * 3, (uint8_t *)(gath + N * 4));
         }
-        co.broadcast(dused, 8, 0, c->stream);
-        ST_HIP(hipMemcpyAsync(hused, dused, 8, hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-        cursor += *hused;
     }
 
     // this rank's means / quats texels in local row order (4 bytes per row and texture)

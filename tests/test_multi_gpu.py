@@ -88,11 +88,12 @@ def test_group_duplicated_rows_and_clumps_equal_single_device(ctx):
 
 @pytest.mark.parametrize('who', ['scales', 'colours', 'neither'])
 def test_group_cluster1d_reseeds_equal_single_device(ctx, who):
-    """The two cluster1d run on rank 0 over the gathered columns, the colours beside the scales
-    from draw 0 (kept only when the scales took no draw, rerun after them otherwise; re-seeds of
-    empty clusters, k-means.ts:174-178).  A far outlier in a column leaves most linspace centroids
-    (k-means.ts:23-39) without members, so that cluster1d takes draws; shards of 3 ranks, one
-    empty, and every rank must continue from the draws rank 0 reports."""
+    """The two cluster1d run over the gathered columns, the scales on rank 0 and the colours on
+    rank 1 from draw 0 (kept only when the scales took no draw, rerun after them otherwise;
+    re-seeds of empty clusters, k-means.ts:174-178).  A far outlier in a column leaves most
+    linspace centroids (k-means.ts:23-39) without members, so that cluster1d takes draws; shards
+    of 3 ranks (rank 1's empty: it still runs the colours), and every rank must continue from the
+    draws ranks 0 and 1 report."""
     n = 20_011
     cols = _table(n, 91, C=3)
     rng = np.random.default_rng(92)
@@ -103,7 +104,7 @@ def test_group_cluster1d_reseeds_equal_single_device(ctx, who):
     want = ctx.sog(cols, 2, draws)
     g = sh.Group([0] * 3, host_staged=True)
     try:
-        _same(g.sog([cols], 2, draws, [0, 0, 7000, n]), want)
+        _same(g.sog([cols], 2, draws, [0, 7000, 7000, n]), want)
     finally:
         g.close()
 
