@@ -381,8 +381,14 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=3):
                     t2 = time.perf_counter()
                     addr, size = ctx.dev_sog_bundle_view(meta, n, tex, 0, 0)
                     t3 = time.perf_counter()
-                    with open(dst, 'wb') as f:
-                        f.write((ctypes_char_array(size)).from_address(addr))
+                    fd = os.open(dst, os.O_WRONLY | os.O_CREAT, 0o644)  # as dev_sog_file: no O_TRUNC
+                    try:
+                        mv, o = memoryview((ctypes_char_array(size)).from_address(addr)).cast('B'), 0
+                        while o < size:
+                            o += os.write(fd, mv[o:])
+                        os.ftruncate(fd, size)
+                    finally:
+                        os.close(fd)
                     t4 = time.perf_counter()
                 if r:
                     times.append(t4 - t0)

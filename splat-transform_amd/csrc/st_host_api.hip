@@ -78,6 +78,15 @@ void download(st_ctx *c, const DevTable &d, const st_table *h) {
     down.d2h();
 }
 
+// the columns writeSog reads (write-sog.ts:110-370): the other columns of a PLY (normals, extra
+// properties) are not uploaded
+std::vector<std::string> sog_columns() {
+    std::vector<std::string> v = {"x", "y", "z", "scale_0", "scale_1", "scale_2", "f_dc_0",
+                                  "f_dc_1", "f_dc_2", "opacity", "rot_0", "rot_1", "rot_2", "rot_3"};
+    for (int i = 0; i < 45; ++i) v.push_back("f_rest_" + std::to_string(i));
+    return v;
+}
+
 std::vector<std::string> transform_columns() {
     std::vector<std::string> v = {"x", "y", "z", "rot_0", "rot_1", "rot_2", "rot_3", "scale_0", "scale_1", "scale_2"};
     for (int i = 0; i < 45; ++i) v.push_back("f_rest_" + std::to_string(i));
@@ -313,7 +322,7 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
     return guarded_h([&] {
         ST_ARGH(c && t && meta && out, "NULL argument");
         use_device(c);
-        DevTable d = upload(c, t, {}, "h.s");
+        DevTable d = upload(c, t, sog_columns(), "h.s");
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
@@ -355,7 +364,7 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
     return guarded_h([&] {
         ST_ARGH(c && t && out && out_size, "NULL argument");
         use_device(c);
-        DevTable d = upload(c, t, {}, "h.s");
+        DevTable d = upload(c, t, sog_columns(), "h.s");
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
@@ -409,7 +418,7 @@ int st_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws
     return guarded_h([&] {
         ST_ARGH(c && t && size && fd >= 0, "bad argument");
         use_device(c);
-        DevTable d = upload(c, t, {}, "h.s");
+        DevTable d = upload(c, t, sog_columns(), "h.s");
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");

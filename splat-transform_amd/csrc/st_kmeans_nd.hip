@@ -2081,7 +2081,10 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         auto *grouped1 = fused ? wsT<uint32_t>(c, "kn.fbpts1", n) : nullptr;
         auto *soff = fused ? wsT<uint32_t>(c, "kn.fasoff", (size_t)ncodes + 1) : nullptr;
         // workgroups of the one-reservation grouping (0: k_code_scatter's 4,096-point rounds)
-        static const int cs_wg = getenv("ST_CS_WG") ? atoi(getenv("ST_CS_WG")) : 256;
+        // (k_code_scatter_run reads the labels 16 bytes at a time: a caller's unaligned labels take
+        // the rounds)
+        static const int cs_env = getenv("ST_CS_WG") ? atoi(getenv("ST_CS_WG")) : 256;
+        const int cs_wg = ((uintptr_t)labels & 15u) ? 0 : cs_env;
         const unsigned gcs = cs_wg > 0 ? grid_for(n, 256, (unsigned)cs_wg) : grid_for(n, FB_TILE, 2048);
         if (fused) {  // slice offsets and the codes' starts in one workgroup
             hipLaunchKernelGGL(k_fa_slices, dim3(1), dim3(FS_T), 0, c->stream, hist, ncodes, soff, cursor, ndec);

@@ -1247,6 +1247,7 @@ uint64_t stage_entries(st_ctx *c, const std::vector<Img> &imgs, const std::vecto
 uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws,
                       st_sog_meta *meta, const st_sog_textures *out, int fd, uint16_t dos_time, uint16_t dos_date,
                       uint64_t *file_size) {
+    const auto t_call = std::chrono::steady_clock::now();
     sog_file_check(fd);
     // the five textures final before the SH k-means: their entries go to the file from a host
     // thread on the side context (the step's colour k-means, which used it, has joined by then)
@@ -1326,12 +1327,22 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
     std::vector<ZipEntry> all = early.es;
     all.insert(all.end(), les.begin(), les.end());
     ST_REQUIRE(zip_size(all) < (1ull << 32), ST_ERR_ARG, "sog file: archive exceeds 4 GiB (no zip64, as the reference)");
+    const auto t4 = std::chrono::steady_clock::now();
     write_at(fd, lblk, lbytes, early.bytes);
+    const auto t5 = std::chrono::steady_clock::now();
     std::vector<uint8_t> cd(zip_central_size(all));
     zip_central(all, dos_time, dos_date, cd.data());
     write_at(fd, cd.data(), cd.size(), early.bytes + lbytes);
     *file_size = early.bytes + lbytes + cd.size();
     sog_file_truncate(fd, *file_size);
+    if (getenv("ST_DEBUG")) {
+        const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "[st sog file] hook %.1f ms after the call; late entries %.1f MB written in %.1f ms; "
+                "directory + truncate %.1f ms; the call %.1f ms\n", ms(t_call, early.t0), lbytes / 1e6, ms(t4, t5),
+                ms(t5, std::chrono::steady_clock::now()), ms(t_call, std::chrono::steady_clock::now()));
+    }
     return used;
 }
 

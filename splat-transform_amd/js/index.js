@@ -61,24 +61,30 @@ class DataTable {
 }
 
 // ---- Math.random stream --------------------------------------------------------
-let pending = [];
+// draws taken from Math.random but not consumed yet, oldest first (a typed array: a call hands
+// back ~10^6 unconsumed draws, copied as memory rather than element by element)
+let pending = new Float64Array(0);
 
 const takeDraws = (count) => {
     const out = new Float64Array(count);
-    let i = 0;
-    for (; i < count && i < pending.length; ++i) out[i] = pending[i];
-    for (; i < count; ++i) out[i] = Math.random();
-    pending = pending.slice(Math.min(count, pending.length));
+    const m = Math.min(count, pending.length);
+    out.set(pending.subarray(0, m));
+    for (let i = m; i < count; ++i) out[i] = Math.random();
+    pending = pending.subarray(m);
     return out;
 };
 
 const giveBack = (draws, used) => {
-    pending = Array.from(draws.subarray(used)).concat(pending);
+    const back = draws.subarray(used);
+    const merged = new Float64Array(back.length + pending.length);
+    merged.set(back);
+    merged.set(pending, back.length);
+    pending = merged;
 };
 
 // drop the draws taken from Math.random but not consumed yet (call after re-seeding Math.random:
 // the next call then starts on the new stream)
-const resetRandomStream = () => { pending = []; };
+const resetRandomStream = () => { pending = new Float64Array(0); };
 
 // error.code of a call that ran out of draws (ST_ERR_DRAWS = -4, st_abi.h; the addon's throw_st)
 const ST_ERR_DRAWS_CODE = 'ST_STATUS_4';

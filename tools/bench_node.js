@@ -28,7 +28,9 @@ const ms = (a, b) => Number(b - a) / 1e6;
         const t1 = process.hrtime.bigint();
         const table = ply.elements.find(e => e.name === 'vertex').dataTable;
         rows = table.numRows;
-        const outH = await fs.promises.open(dst, 'w');
+        // no O_TRUNC: writeSogFile cuts the file to the archive's length (a file truncated to zero and
+        // rewritten is flushed at close on ext4, and frees its old pages first)
+        const outH = await fs.promises.open(dst, fs.constants.O_WRONLY | fs.constants.O_CREAT, 0o644);
         const t1b = process.hrtime.bigint();
         size = await host.writeSogFile(outH, table, iters);
         const t1c = process.hrtime.bigint();

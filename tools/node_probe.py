@@ -28,7 +28,7 @@ env = dict(os.environ, ST_XFER_PRINT='1', ST_DEBUG='1')
 r = subprocess.run(['node', os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, '2', '10'], capture_output=True,
                    text=True, env=env, timeout=600)
 print(r.stdout)
-print('\n'.join(ln for ln in r.stderr.splitlines() if ln.startswith('[st xfer]') or ln.startswith('[st sog file]')))
+print('\n'.join(ln for ln in r.stderr.splitlines() if ln.startswith(('[st xfer]', '[st sog file]', '[addon]'))))
 for p in (src, dst):
     if os.path.exists(p):
         os.remove(p)
