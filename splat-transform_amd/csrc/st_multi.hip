@@ -1495,6 +1495,20 @@ int apply_env_devices() {
                 msg = std::string("ST_NUM_GPUS: ") + st_last_error();
             }
         }
+        // test hook: the default group as n host-staged ranks on device 0, so that the one-call
+        // writers' multi-GPU branches run on a one-GPU box
+        const char *gr = getenv("ST_DEFAULT_GROUP_RANKS");
+        if (rc == ST_OK && gr && atoi(gr) > 1) {
+            rc = guarded_m([&] {
+                const int n = std::min(atoi(gr), 16);
+                std::vector<int32_t> devs(n, 0);
+                std::shared_ptr<st_group> fresh(group_new(devs.data(), n, true));
+                std::lock_guard<std::mutex> lk(g_group_mu);
+                g_group = std::move(fresh);
+                g_ndev = n;
+            });
+            if (rc != ST_OK) msg = std::string("ST_DEFAULT_GROUP_RANKS: ") + st_last_error();
+        }
     }
     if (rc != ST_OK) set_last_error(msg);
     return rc;

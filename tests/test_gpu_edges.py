@@ -490,3 +490,28 @@ def test_sync_check_mode_vs_oracle(monkeypatch):
     assert rc == 0 and used == oused
     for k in tex:
         same_bits(tex[k], otex[k])
+
+
+def test_kmeans_labels_buffer_unaligned(ctx):
+    """The decided points' grouping reads the labels 16 bytes at a time (k_code_scatter_run); a
+    caller's labels buffer that is not 16-byte aligned takes the 4,096-point rounds instead
+    (k_code_scatter).  Both give the reference's labels and centroids."""
+    import torch
+    n, d, k, iters = 40_000, 9, 256, 2
+    rng = np.random.default_rng(61)
+    cols = [rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)]
+    draws = oracle.mulberry32(n + k + 3, 4 * k * (iters + 1) + 64)
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, iters, draws)
+    assert rc == 0
+    dev = torch.device('cuda', 0)
+    tcols = [torch.from_numpy(c).to(dev) for c in cols]
+    for off in (0, 1):
+        cen = torch.empty(d * k, device=dev)
+        lab_buf = torch.empty(n + 4, dtype=torch.int32, device=dev)
+        lab = lab_buf[off:off + n]
+        assert (lab.data_ptr() % 16 == 0) == (off == 0)
+        used = ctx.dev_kmeans(tcols, k, iters, draws, cen, lab)
+        torch.cuda.synchronize()
+        assert used == oused
+        same_bits(lab.cpu().numpy().astype(np.uint32), np.asarray(olabels, dtype=np.uint32))
+        same_bits(cen.cpu().numpy(), np.asarray(ocent, dtype=np.float32).reshape(-1))

@@ -152,3 +152,55 @@ def test_sog_file_over_a_longer_file_is_cut_to_the_archive(ctx, tmp_path):
     assert rc == 0 and os.path.getsize(path) == size < (8 << 20)
     data = open(path, 'rb').read()
     assert len(zipfile.ZipFile(io.BytesIO(data)).namelist()) == 8
+
+
+_GROUP_FILE = r'''
+import ctypes, io, os, sys, zipfile
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import splat_hip as sh
+n = 30_011
+rng = np.random.default_rng(8)
+cols = {k: rng.normal(0, 1, n).astype(np.float32) for k in
+        ['x', 'y', 'z', 'scale_0', 'scale_1', 'scale_2', 'f_dc_0', 'f_dc_1', 'f_dc_2', 'opacity',
+         'rot_0', 'rot_1', 'rot_2', 'rot_3'] + ['f_rest_%d' % i for i in range(9)]}
+draws = np.random.default_rng(9).random(1 << 18)
+ctx = sh.Context(0)
+path = sys.argv[2]
+with open(path, 'wb') as f:
+    f.write(b'\xee' * (8 << 20))  # a longer earlier file: no O_TRUNC below
+fd = os.open(path, os.O_WRONLY)
+t = sh.make_table(cols)
+used, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+try:
+    sh.check(sh.lib().st_sog_file(ctx.h, ctypes.byref(t), ctypes.c_int32(2), sh._vp(draws), ctypes.c_uint64(len(draws)),
+                                  ctypes.byref(used), ctypes.c_int32(fd), ctypes.c_uint16(0), ctypes.c_uint16(0),
+                                  ctypes.byref(size)))
+finally:
+    os.close(fd)
+got = open(path, 'rb').read()
+assert len(got) == size.value, (len(got), size.value)
+assert len(zipfile.ZipFile(io.BytesIO(got)).namelist()) == 8
+n_dev = ctypes.c_int32(0)
+sh.check(sh.lib().st_get_devices(ctypes.byref(n_dev)))
+print('ranks', n_dev.value, 'bytes', size.value, 'used', used.value, 'digest', __import__('hashlib').sha256(got).hexdigest())
+'''
+
+
+def test_sog_file_group_branch_cuts_a_longer_file(tmp_path):
+    """st_sog_file's multi-GPU branch (the default group; ST_DEFAULT_GROUP_RANKS=2 makes it two
+    host-staged ranks on this one GPU): the group's archive written over a longer existing file
+    opened without O_TRUNC is cut to its length, a valid 8-entry zip, the same bytes as the one-GPU
+    branch writes"""
+    import subprocess
+    import sys
+    py = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'splat-transform_amd', 'py')
+    out = {}
+    for ranks in ('2', ''):
+        env = dict(os.environ, ST_DEFAULT_GROUP_RANKS=ranks)
+        r = subprocess.run([sys.executable, '-c', _GROUP_FILE, py, str(tmp_path / f'g{ranks}.sog')],
+                           capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[ranks] = r.stdout.split()
+    assert out['2'][1] == '2' and out[''][1] == '1'
+    assert out['2'][3:] == out[''][3:]  # bytes, draws used and digest

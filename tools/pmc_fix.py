@@ -11,6 +11,8 @@ import sys
 from collections import defaultdict
 
 KEYS = ('k_fixrow_lp', 'k_code_scatter', 'k_fixpair_b', 'k_sweep<3, 0>', 'k_sweep<3, 1>', 'k_nd_seq', 'k_nd_combine')
+if len(sys.argv) > 3:  # other kernels: comma-separated name prefixes
+    KEYS = tuple(sys.argv[3].split(','))
 
 
 def main():
