@@ -27,6 +27,18 @@ struct Coll {
     // root: recv[r] (at offset displ[r]) = rank r's send of bytes[r]; recv ignored elsewhere
     virtual void gatherv(const void *send, size_t mybytes, void *recv, const std::vector<size_t> &bytes,
                          const std::vector<size_t> &displ, int root, hipStream_t s) = 0;
+    // several gathervs over the same shard layout, each to its own root (recv ignored off the
+    // root): RCCL issues them as one group, so gathers into different roots move at once
+    struct Gather {
+        const void *send;
+        size_t mybytes;
+        void *recv;
+        int root;
+    };
+    virtual void gatherv_many(const std::vector<Gather> &gs, const std::vector<size_t> &bytes,
+                              const std::vector<size_t> &displ, hipStream_t s) {
+        for (const Gather &g : gs) gatherv(g.send, g.mybytes, g.recv, bytes, displ, g.root, s);
+    }
     // rank `to` receives rank `from`'s buf (every rank makes the call; the others pass through)
     virtual void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) = 0;
     // after abort() every call of every rank on this channel (and its side channel) throws

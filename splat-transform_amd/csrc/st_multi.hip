@@ -117,6 +117,26 @@ struct RcclColl : Coll {
         }
         ST_NCCL(ncclGroupEnd());
     }
+    void gatherv_many(const std::vector<Gather> &gs, const std::vector<size_t> &bytes,
+                      const std::vector<size_t> &displ, hipStream_t s) override {
+        live();
+        for (const Gather &g : gs)
+            if (rank == g.root && g.mybytes)
+                ST_HIP(hipMemcpyAsync(static_cast<char *>(g.recv) + displ[rank], g.send, g.mybytes,
+                                      hipMemcpyDeviceToDevice, s));
+        if (world == 1) return;
+        ST_NCCL(ncclGroupStart());
+        for (const Gather &g : gs) {
+            if (rank == g.root) {
+                for (int r = 0; r < world; ++r)
+                    if (r != g.root && bytes[r])
+                        ST_NCCL(ncclRecv(static_cast<char *>(g.recv) + displ[r], bytes[r], ncclUint8, r, comm, s));
+            } else if (g.mybytes) {
+                ST_NCCL(ncclSend(g.send, g.mybytes, ncclUint8, g.root, comm, s));
+            }
+        }
+        ST_NCCL(ncclGroupEnd());
+    }
     void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
         live();
         if (world == 1 || from == to || !bytes || (rank != from && rank != to)) return;
@@ -844,8 +864,10 @@ static uint64_t sog_sharded_rank(st_ctx *c, Coll &co, const st_table *const *tab
         const bool mine_c = co.rank == cr;
         float *gs = root ? wsT<float>(c, "mg.g1s", N * 3) : nullptr;    // scale_0..2
         float *gc = mine_c ? wsT<float>(c, "mg.g1c", N * 4) : nullptr;  // f_dc_0..2, opacity
-        for (int i = 0; i < 3; ++i) co.gatherv(m[3 + i], 4 * sh.n, gs ? gs + N * i : nullptr, bytes, displ, 0, c->stream);
-        for (int i = 0; i < 4; ++i) co.gatherv(m[6 + i], 4 * sh.n, gc ? gc + N * i : nullptr, bytes, displ, cr, c->stream);
+        std::vector<Coll::Gather> g7;  // one group: rank 0's and rank 1's gathers move at once
+        for (int i = 0; i < 3; ++i) g7.push_back({m[3 + i], 4 * sh.n, gs ? gs + N * i : nullptr, 0});
+        for (int i = 0; i < 4; ++i) g7.push_back({m[6 + i], 4 * sh.n, gc ? gc + N * i : nullptr, cr});
+        co.gatherv_many(g7, bytes, displ, c->stream);
         const float *sc3[3] = {gs, gs + N, gs + 2 * N};
         const float *co3[3] = {gc, gc + N, gc + 2 * N};
         auto *slab = root ? wsT<uint8_t>(c, "mg.slab", N * 3) : nullptr;
@@ -1014,6 +1036,13 @@ struct TraceColl : Coll {
         for (size_t b : bytes) tot += b;
         log->put(ch, "gatherv", tot, root);
         in->gatherv(send, mybytes, recv, bytes, displ, root, s);
+    }
+    void gatherv_many(const std::vector<Gather> &gs, const std::vector<size_t> &bytes,
+                      const std::vector<size_t> &displ, hipStream_t s) override {
+        unsigned long long tot = 0;
+        for (size_t b : bytes) tot += b;
+        for (const Gather &g : gs) log->put(ch, "gatherv", tot, g.root);
+        in->gatherv_many(gs, bytes, displ, s);
     }
     void sendrecv(void *buf, size_t bytes, int from, int to, hipStream_t s) override {
         log->put(ch, "sendrecv", bytes, from, to);
