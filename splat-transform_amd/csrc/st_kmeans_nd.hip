@@ -295,32 +295,55 @@ __global__ __launch_bounds__(PF_PTS) void k_point_frags(const float *const *cols
 
 // centroid A fragments + cmax + the AoS f32 copy of the centroids (exact distances);
 // one thread per centroid row; rows >= k can never win
-__global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
-                                                        float sigma, uint4 *cfrag, uint32_t *cmax_bits, float *caos,
-                                                        float2 *cfix, float *cnorm, float *cdn) {
+// 64 centroid rows per workgroup, one per lane; wave w of the four owns dimensions
+// [per w, per (w + 1)) of those rows' caos / cfix entries and its share of their squared norms
+// (f64, summed over the waves through LDS in a fixed order), and waves 0..ks-1 their fp16
+// fragments (fragment s: dimensions 16s .. 16s + 15; the norm columns d, d + 1, d + 2 in the
+// last).  Every column read is 64 consecutive rows; one row per lane over all dimensions left a
+// single wave per SIMD to hide those reads' latency.
+constexpr int CF_W = 4;
+__global__ __launch_bounds__(64 * CF_W) void k_centroid_frags(const float *cen, int d, int k, uint32_t ctiles, int ks,
+                                                              float sigma, uint4 *cfrag, uint32_t *cmax_bits,
+                                                              float *caos, float2 *cfix, float *cnorm, float *cdn) {
+    __shared__ double pn[CF_W][64], pd[CF_W][64];
     const uint32_t total = ctiles * 32;
     const int ld = aos_ld(d);
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int per = (ld / 2 + CF_W - 1) / CF_W * 2;  // dimensions per wave: whole cfix pairs
+    const int c0 = w * per, c1 = min(ld, c0 + per);
     float mymax = 0.f, mydmax = 0.f;
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < total; r += gridDim.x * blockDim.x) {
-        const bool valid = r < (uint32_t)k;
+    for (uint32_t rb = blockIdx.x; rb * 64 < total; rb += gridDim.x) {
+        const uint32_t r = rb * 64 + lane;
+        const bool live = r < total;
+        const bool valid = live && r < (uint32_t)k;
+        double nn = 0, dd = 0;
         if (valid) {
-            for (int c = 0; c < ld; ++c) caos[(uint64_t)r * ld + c] = c < d ? cen[(uint64_t)c * k + r] : 0.0f;
             // k_fixrow layout: [tile][lane-half][dim pair][16 rows] float2, so the 16 lanes of a
             // point read one whole 128-byte line per dimension pair
             const uint32_t row = r & 31, hh = (row >> 2) & 1, r16 = (row & 3) | ((row >> 3) << 2);
-            for (int q = 0; q < ld / 2; ++q) {
-                const float a = 2 * q < d ? cen[(uint64_t)(2 * q) * k + r] : 0.0f;
-                const float b = 2 * q + 1 < d ? cen[(uint64_t)(2 * q + 1) * k + r] : 0.0f;
-                cfix[(((uint64_t)(r >> 5) * 2 + hh) * (ld / 2) + q) * 16 + r16] = make_float2(a, b);
+            for (int c = c0; c < c1; c += 2) {
+                const float a = c < d ? cen[(uint64_t)c * k + r] : 0.0f;
+                const float b = c + 1 < d ? cen[(uint64_t)(c + 1) * k + r] : 0.0f;
+                caos[(uint64_t)r * ld + c] = a;
+                caos[(uint64_t)r * ld + c + 1] = b;
+                cfix[(((uint64_t)(r >> 5) * 2 + hh) * (ld / 2) + c / 2) * 16 + r16] = make_float2(a, b);
+            }
+            for (int c = c0; c < min(c1, d); ++c) {
+                const float f = cen[(uint64_t)c * k + r] * sigma;
+                const double x = (double)f, e = x - (double)h_val(h_bits(f));
+                nn += x * x;
+                dd += e * e;
             }
         }
-        double nn = 0, dd = 0;
-        for (int c = 0; c < d; ++c) {
-            const float f = valid ? cen[(uint64_t)c * k + r] * sigma : 0.0f;
-            const double x = (double)f, e = x - (double)h_val(h_bits(f));
-            nn += x * x;
-            dd += e * e;
-        }
+        pn[w][lane] = nn;
+        pd[w][lane] = dd;
+        __syncthreads();
+        nn = ((pn[0][lane] + pn[1][lane]) + pn[2][lane]) + pn[3][lane];
+        dd = ((pd[0][lane] + pd[1][lane]) + pd[2][lane]) + pd[3][lane];
+        __syncthreads();  // the next row block's partials overwrite these
+        static_assert(CF_W == 4, "the fixed-order sum above");
+        if (!live || w >= ks) continue;
         uint16_t n1, n2, n3;
         if (valid) {
             n1 = h_bits((float)nn);
@@ -328,45 +351,49 @@ __global__ __launch_bounds__(256) void k_centroid_frags(const float *cen, int d,
             n2 = h_bits((float)r1);
             const double r2 = r1 - (double)h_val(n2);
             n3 = h_bits((float)r2);
-            const float nr = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
-            const float dr = (float)(__builtin_sqrt(dd) * (1.0 + 1e-6));
-            mymax = fmaxf(mymax, nr);
-            mydmax = fmaxf(mydmax, dr);
-            cnorm[r] = nr;
-            cdn[r] = dr;
+            if (w == 0) {
+                const float nr = (float)(__builtin_sqrt(nn) * (1.0 + 1e-6));
+                const float dr = (float)(__builtin_sqrt(dd) * (1.0 + 1e-6));
+                mymax = fmaxf(mymax, nr);
+                mydmax = fmaxf(mydmax, dr);
+                cnorm[r] = nr;
+                cdn[r] = dr;
+            }
         } else {
-            cnorm[r] = 0.0f;  // padding row: never the best
-            cdn[r] = 0.0f;
+            if (w == 0) {
+                cnorm[r] = 0.0f;  // padding row: never the best
+                cdn[r] = 0.0f;
+            }
             n1 = h_bits(60000.0f);  // padding: score ~6e4 >> any real score (< 200)
             n2 = n3 = 0;
         }
+        const int s = w;
         const uint32_t t = r >> 5, row = r & 31;
-        for (int s = 0; s < ks; ++s)
-            for (int h = 0; h < 2; ++h) {
-                uint16_t e[8];
+        for (int h = 0; h < 2; ++h) {
+            uint16_t e[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int kk = 16 * s + 8 * h + j;
-                    uint16_t bits = 0;
-                    if (kk < d) bits = valid ? h_bits(cen[(uint64_t)kk * k + r] * sigma) : (uint16_t)0;
-                    else if (kk == d) bits = n1;
-                    else if (kk == d + 1) bits = n2;
-                    else if (kk == d + 2) bits = n3;
-                    e[j] = bits;
-                }
-                uint4 v;
-                v.x = e[0] | ((uint32_t)e[1] << 16);
-                v.y = e[2] | ((uint32_t)e[3] << 16);
-                v.z = e[4] | ((uint32_t)e[5] << 16);
-                v.w = e[6] | ((uint32_t)e[7] << 16);
-                cfrag[((uint64_t)t * ks + s) * 64 + h * 32 + row] = v;
+            for (int j = 0; j < 8; ++j) {
+                const int kk = 16 * s + 8 * h + j;
+                uint16_t bits = 0;
+                if (kk < d) bits = valid ? h_bits(cen[(uint64_t)kk * k + r] * sigma) : (uint16_t)0;
+                else if (kk == d) bits = n1;
+                else if (kk == d + 1) bits = n2;
+                else if (kk == d + 2) bits = n3;
+                e[j] = bits;
             }
+            uint4 v;
+            v.x = e[0] | ((uint32_t)e[1] << 16);
+            v.y = e[2] | ((uint32_t)e[3] << 16);
+            v.z = e[4] | ((uint32_t)e[5] << 16);
+            v.w = e[6] | ((uint32_t)e[7] << 16);
+            cfrag[((uint64_t)t * ks + s) * 64 + h * 32 + row] = v;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         mymax = fmaxf(mymax, __shfl_xor(mymax, o, 64));
         mydmax = fmaxf(mydmax, __shfl_xor(mydmax, o, 64));
     }
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0 && w == 0) {
         atomicMax(cmax_bits, __builtin_bit_cast(uint32_t, mymax));  // non-negative floats: bit order
         atomicMax(cmax_bits + 1, __builtin_bit_cast(uint32_t, mydmax));
     }
@@ -1384,6 +1411,36 @@ __global__ __launch_bounds__(256) void k_others_keys(const uint32_t *__restrict_
     }
 }
 
+// a cluster's other members (ovals[o0 .. o1), label-sorted; lane = dimension) added in list
+// order: the wave loads 64 list entries at once (one per lane) and then up to U member rows in
+// flight, each row's index broadcast from its lane -- a cluster holds a handful of others, and
+// loading them one list entry, then one row, at a time made each a chain of dependent reads
+template <int LD>
+__device__ inline void others_sum(const float *__restrict__ aos, const uint32_t *__restrict__ ovals, uint32_t o0,
+                                  uint32_t o1, int lane, double &sum, double &sabs, int &emin) {
+    constexpr int U = 8;  // member rows in flight
+    for (uint32_t b = o0; b < o1; b += 64) {
+        const uint32_t m = min(64u, o1 - b);
+        const uint32_t mine = (uint32_t)lane < m ? (ovals[b + lane] & ~OTHER_TIE) : 0u;
+        for (uint32_t u0 = 0; u0 < m; u0 += U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t row = __shfl(mine, (int)(u0 + u) & 63, 64);
+                v[u] = (u0 + u < m && lane < LD) ? aos[(uint64_t)row * LD + lane] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u0 + u < m) {  // uniform
+                    sum += (double)v[u];
+                    sabs += (double)__builtin_fabsf(v[u]);
+                    if (v[u] != 0.0f) emin = min(emin, ulp_exp(v[u]));
+                }
+            }
+        }
+    }
+}
+
 // one wave per cluster, lane = dimension: the slices' partials of its tile-half plus its other
 // members (ostart / ovals: the label-sorted others); the centroid where every dimension is
 // certified, otherwise the cluster is listed for k_nd_seq.  counts[cl] = its members.
@@ -1413,25 +1470,7 @@ __global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ ao
         cnt += pcnt[(uint64_t)sl * 16 + loc];
     }
     const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
-    constexpr int U = 8;  // member rows in flight
-    uint32_t j = o0;
-    for (; j + U <= o1; j += U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = lane < LD ? aos[(uint64_t)(ovals[j + u] & ~OTHER_TIE) * LD + lane] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            sum += (double)v[u];
-            sabs += (double)__builtin_fabsf(v[u]);
-            if (v[u] != 0.0f) emin = min(emin, ulp_exp(v[u]));
-        }
-    }
-    for (; j < o1; ++j) {
-        const float v = lane < LD ? aos[(uint64_t)(ovals[j] & ~OTHER_TIE) * LD + lane] : 0.0f;
-        sum += (double)v;
-        sabs += (double)__builtin_fabsf(v);
-        if (v != 0.0f) emin = min(emin, ulp_exp(v));
-    }
+    others_sum<LD>(aos, ovals, o0, o1, lane, sum, sabs, emin);
     cnt += o1 - o0;
     if (lane == 0) counts[cl] = cnt;
     if (cnt == 0) return;  // empty: re-seeded
@@ -1472,25 +1511,7 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
         cnt += pcnt[(uint64_t)sl * 16 + loc];
     }
     const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
-    constexpr int U = 8;  // member rows in flight
-    uint32_t j = o0;
-    for (; j + U <= o1; j += U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = lane < LD ? aos[(uint64_t)(ovals[j + u] & ~OTHER_TIE) * LD + lane] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            sum += (double)v[u];
-            sabs += (double)__builtin_fabsf(v[u]);
-            if (v[u] != 0.0f) emin = min(emin, ulp_exp(v[u]));
-        }
-    }
-    for (; j < o1; ++j) {
-        const float v = lane < LD ? aos[(uint64_t)(ovals[j] & ~OTHER_TIE) * LD + lane] : 0.0f;
-        sum += (double)v;
-        sabs += (double)__builtin_fabsf(v);
-        if (v != 0.0f) emin = min(emin, ulp_exp(v));
-    }
+    others_sum<LD>(aos, ovals, o0, o1, lane, sum, sabs, emin);
     cnt += o1 - o0;
     if (lane == 0) counts[cl] = cnt;
     if (lane < d) {
@@ -2050,7 +2071,8 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     auto *chalf = wsT<float>(c, "kn.chalf", (size_t)ctiles * 2);
     auto *cdn = wsT<float>(c, "kn.cdn", (size_t)ctiles * 32);
     auto *chalf_d = wsT<float>(c, "kn.chalfd", (size_t)ctiles * 2);
-    hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 256, 1024)), dim3(256), 0, c->stream,
+    ST_REQUIRE(ks <= CF_W, ST_ERR_INTERNAL, "kmeans: more fragments per row than centroid waves");
+    hipLaunchKernelGGL(k_centroid_frags, dim3(grid_for((uint64_t)ctiles * 32, 64, 4096)), dim3(64 * CF_W), 0, c->stream,
                        cen, d, k, ctiles, ks, sigma, cfrag, scal + 1, caos, cfix, cnorm, cdn);
     hipLaunchKernelGGL(k_half_max, dim3(grid_for((uint64_t)ctiles * 2, 256, 1024)), dim3(256), 0, c->stream, cnorm,
                        cdn, ctiles * 2, chalf, chalf_d);

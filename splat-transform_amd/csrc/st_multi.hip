@@ -320,6 +320,10 @@ __global__ __launch_bounds__(256) void k_put_rows(const float *vals, int d, int 
 
 // fold the per-segment partials [nseg][d][k] into SAC = [sum (d*k) | sum|x| (d*k) | count (k)]
 // (f64: counts are exact below 2^53) and E = min emin [d*k]
+__global__ __launch_bounds__(256) void k_counts_f64(const uint32_t *counts, int k, double *out) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) out[i] = (double)counts[i];
+}
+
 __global__ __launch_bounds__(256) void k_fold_partials(const double *sums, const double *sabs, const int32_t *emin,
                                                        const uint32_t *counts, int nseg, int d, int k, double *sac,
                                                        int32_t *e) {
@@ -493,14 +497,16 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
     if (P.n && d > 1)
         ST_HIP(hipMemcpyAsync(dpts, P.pts.data(), sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
     for (int it = 0; it < iters; ++it) {
+        bool folded = false;  // the partials are already in sac / E
         if (c->verify && d > 1 && it == iters - 1)  // st_ctx_set_verify: the last assign's centroids
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));
         if (P.n && d == 1 && k <= 256 && !getenv("ST_K1_SORT")) {
             dist_assign_partials1d(c, P.pts[0], P.n, P.nseg, k, cen, labels, sums, sabs, emin, counts);
         } else if (P.n && d > 1 && P.nseg == 1 && !getenv("ST_ND_SORT")) {
-            // the fused fix-up's partials (ST_ND_SORT=1: the member sort)
-            if (!dist_assign_partials_nd(c, dpts, d, P.n, k, cen, labels, sums, sabs, emin, counts))
-                dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
+            // the fused fix-up's partials (ST_ND_SORT=1: the member sort), written straight into
+            // the all-reduce's layout (one segment: nothing to fold but the counts)
+            folded = dist_assign_partials_nd(c, dpts, d, P.n, k, cen, labels, sac, sac + dk, E, counts);
+            if (!folded) dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
         } else if (P.n) {
             dist_assign(c, P.pts.data(), d, P.n, k, cen, labels);
             dist_partials(c, P.pts.data(), d, P.n, P.nseg, k, labels, sums, sabs, emin, counts);
@@ -510,8 +516,12 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
             ST_HIP(hipMemsetD32Async(emin, 1 << 20, P.nseg * dk, c->stream));
             ST_HIP(hipMemsetAsync(counts, 0, 4 * (size_t)P.nseg * k, c->stream));
         }
-        hipLaunchKernelGGL(k_fold_partials, dim3(grid_for(dk + k, 256, 4096)), dim3(256), 0, c->stream, sums, sabs,
-                           emin, counts, P.nseg, d, k, sac, E);
+        if (folded)
+            hipLaunchKernelGGL(k_counts_f64, dim3(grid_for(k, 256, 1024)), dim3(256), 0, c->stream, counts, k,
+                               sac + 2 * dk);
+        else
+            hipLaunchKernelGGL(k_fold_partials, dim3(grid_for(dk + k, 256, 4096)), dim3(256), 0, c->stream, sums,
+                               sabs, emin, counts, P.nseg, d, k, sac, E);
         ST_LAUNCH_CHECK();
         co.allreduce(sac, 2 * dk + k, Dt::F64, Op::Sum, c->stream);
         co.allreduce(E, dk, Dt::I32, Op::Min, c->stream);
