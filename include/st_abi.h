@@ -470,7 +470,8 @@ int st_dev_sog_bundle_view(st_ctx *ctx, const st_sog_meta *meta, uint64_t count,
  * st_dev_sog_bundle's archive and is cut to its length; *size = that length.  fd must be
  * seekable (a regular file opened for writing; the archive goes out with pwrite at absolute
  * offsets): a pipe or socket fails with ST_ERR_ARG before any work.  The caller opens and
- * closes fd. */
+ * closes fd; open it without O_TRUNC (the call cuts the file itself: on ext4 a file truncated to
+ * zero and rewritten is flushed at close, and its old pages are freed at the open). */
 int st_dev_sog_file(st_ctx *ctx, const st_table *table, int32_t iters, const double *draws, uint64_t ndraws,
                     uint64_t *used, st_sog_meta *meta, const st_sog_textures *out, int32_t fd, uint16_t dos_time,
                     uint16_t dos_date, uint64_t *size);
