@@ -199,9 +199,38 @@ static void set_named(napi_env env, napi_value obj, const char *k, napi_value v)
  * JS as an external ArrayBuffer (freed by its finalizer).  V8's own ArrayBuffers are zero-filled
  * 4 KiB pages; the reader overwrites every byte anyway, and first-touch faults on 2.5 GB of 4 KiB
  * pages halved the rate of readPly's device-to-host copies. */
+/* Freed columns' blocks are kept (up to ST_NAPI_POOL_MB, default 4096 MiB) and handed to the
+ * next column of the same rounded length: a reused block is already faulted in, while a fresh
+ * one is zeroed by the kernel on first touch inside the device-to-host copy (1,240 huge pages
+ * for a 10M-splat table).  Finalizers and allocations both run on the JS thread. */
+#define POOL_MAX 512
+static struct {
+    void *p;
+    size_t len;
+} g_pool[POOL_MAX];
+static int g_pool_n = 0;
+static size_t g_pool_bytes = 0;
+
+static size_t pool_cap(void) {
+    static size_t cap = (size_t)-1;
+    if (cap == (size_t)-1) {
+        const char *e = getenv("ST_NAPI_POOL_MB");
+        cap = (size_t)(e ? strtoull(e, NULL, 10) : 4096) << 20;
+    }
+    return cap;
+}
+
 static void free_column(napi_env env, void *data, void *hint) {
     int64_t adj;
-    napi_adjust_external_memory(env, -(int64_t)(size_t)hint, &adj);
+    const size_t bytes = (size_t)hint, huge = (size_t)2 << 20, len = (bytes + huge - 1) / huge * huge;
+    napi_adjust_external_memory(env, -(int64_t)bytes, &adj);
+    if (g_pool_n < POOL_MAX && g_pool_bytes + len <= pool_cap()) {
+        g_pool[g_pool_n].p = data;
+        g_pool[g_pool_n].len = len;
+        ++g_pool_n;
+        g_pool_bytes += len;
+        return;
+    }
     free(data);
 }
 
@@ -210,11 +239,19 @@ static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t 
     if (bytes < ((size_t)8 << 20)) return new_typed(env, type, elems, esize, data);
     void *p = NULL;
     const size_t len = (bytes + huge - 1) / huge * huge;
-    if (posix_memalign(&p, huge, len) != 0) {
-        napi_throw_error(env, NULL, "splat-hip: out of host memory for a column");
-        return NULL;
+    for (int i = g_pool_n - 1; i >= 0 && !p; --i)
+        if (g_pool[i].len == len) {
+            p = g_pool[i].p;
+            g_pool[i] = g_pool[--g_pool_n];
+            g_pool_bytes -= len;
+        }
+    if (!p) {
+        if (posix_memalign(&p, huge, len) != 0) {
+            napi_throw_error(env, NULL, "splat-hip: out of host memory for a column");
+            return NULL;
+        }
+        madvise(p, len, MADV_HUGEPAGE);  /* best effort */
     }
-    madvise(p, len, MADV_HUGEPAGE);  /* best effort */
     napi_value ab, ta;
     if (napi_create_external_arraybuffer(env, p, bytes, free_column, (void *)bytes, &ab) != napi_ok) {
         free(p);
