@@ -916,6 +916,9 @@ def main(args):
     ctx.reset_kernel_stats()
     os.environ.pop('ST_TIMING', None)
     elapsed, meta, used = timed(step, args.steps, 0)
+    # the last timed step's SH palette k-means: how its points were decided (summed over its 10
+    # assigns; the python harness path runs its own k-means and leaves this empty)
+    sh_assign = ctx.kmeans_stats() or None
     sweep_ms, sweep_launches = ctx.kernel_stats('kn.sweep')
     kstats = {}
     for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum',
@@ -1111,6 +1114,7 @@ def main(args):
         'sog_stages': sog_stage_table(stages, n_local, args.iters),
         'kernels': kstats,
         'draws_used_per_step': used,
+        'sh_kmeans_assign': sh_assign,
         'rccl_ranks': rccl_ranks,
         'transport': transport,
         'side_channel': (os.environ.get('ST_SIDE_CHANNEL') != '0') if comm else None,

@@ -172,6 +172,13 @@ int st_ctx_set_stream(st_ctx *ctx, void *hip_stream);
 int st_ctx_synchronize(st_ctx *ctx);
 /* Per-stage device timing (hipEvents) of the last st_*sog / st_*kmeans call, JSON text. */
 const char *st_ctx_last_timings(st_ctx *ctx);
+/* the last N-D k-means' assign classification on ctx, summed over its iterations, as JSON:
+ * {"assigns", "points", "pairs" (two tile-halves settled by the exact fix-up), "ambiguous"
+ * (the second sweep's candidate lists), "overflow" (first lists past 64 rows, collected again),
+ * "walked_overflow" (past 2,048 rows too: the KdTree walk), "ties" (exact ties walked)}; "{}"
+ * before the first.  Owned by ctx, valid until its next N-D k-means.  (No reference counterpart:
+ * diagnostics of this build's exact assign.) */
+const char *st_ctx_last_kmeans_stats(st_ctx *ctx);
 /* Kernel profiling: when enabled, the library brackets its named hot kernels
  * ("kn.sweep", "mo.sort", ...) with hipEvents on the context stream; stats
  * accumulate until st_ctx_reset_kernel_stats.  Query after a synchronize. */

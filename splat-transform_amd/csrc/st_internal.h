@@ -132,6 +132,14 @@ struct st_ctx {
     std::vector<st::StageTimer> marks;
     bool timing = false;
     std::string last_timings = "{}";
+    // the N-D assign's classification summed over the last N-D kmeans_dev call's iterations
+    // (st_ctx_last_kmeans_stats): points the sweep decided, pair points, ambiguous points, those
+    // whose first candidate list overflowed, those the second list did not hold either (the
+    // KdTree walk), and the exact ties walked
+    struct KnStats {
+        uint64_t assigns = 0, points = 0, pairs = 0, ambiguous = 0, overflow = 0, walked_overflow = 0, ties = 0;
+    } kn_stats;
+    std::string last_kn_stats = "{}";
     // kernel profiling (st_ctx_set_profiling)
     bool profiling = false;
     struct KEv {
@@ -273,6 +281,8 @@ void gather_owned_rows(st_ctx *c, const float *const *cols, int d, uint64_t n_lo
 uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int k, int iters, const double *draws,
                     uint64_t ndraws, float *centroids, uint32_t *labels, bool host_init = false,
                     const double *const *sum64 = nullptr);
+// st_ctx_last_kmeans_stats' JSON from c->kn_stats (the N-D k-means writers call it at their end)
+void kn_stats_publish(st_ctx *c);
 uint64_t cluster1d_dev(st_ctx *c, const float *const *cols, int ncols, uint64_t n, int iters, const double *draws,
                        uint64_t ndraws, float *centroids256, uint8_t *labels);
 uint64_t sog_dev(st_ctx *c, const st_table *t, int iters, const double *draws, uint64_t ndraws, st_sog_meta *meta,

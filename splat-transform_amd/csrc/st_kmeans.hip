@@ -477,6 +477,7 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     }
     auto **dcols = wsT<const float *>(c, "km.cols", (size_t)d);
     ST_HIP(hipMemcpyAsync(dcols, cols, sizeof(float *) * d, hipMemcpyHostToDevice, c->stream));
+    if (d > 1) c->kn_stats = st_ctx::KnStats{};
     const bool finite_known = c->km_finite_known && d == 1;
     c->km_finite_known = false;
     if (!finite_known) check_finite(c, cols, dcols, d, n);
@@ -547,7 +548,20 @@ uint64_t kmeans_dev(st_ctx *c, const float *const *cols, int d, uint64_t n, int 
     ST_REQUIRE(!(hs.err & ERR_DRAWS), ST_ERR_DRAWS, "kmeans: Math.random draws exhausted while re-seeding");
     ST_REQUIRE(!(hs.err & ERR_DRAW_RANGE), ST_ERR_ARG, "kmeans: a re-seed draw outside [0, 1)");
     ST_REQUIRE(!(hs.err & ERR_INTERNAL), ST_ERR_INTERNAL, "kmeans: internal consistency check failed");
+    if (d > 1) kn_stats_publish(c);
     return hs.cursor;
+}
+
+void kn_stats_publish(st_ctx *c) {
+    const auto &k_ = c->kn_stats;
+    char buf[320];
+    snprintf(buf, sizeof buf,
+             "{\"assigns\": %llu, \"points\": %llu, \"pairs\": %llu, \"ambiguous\": %llu, \"overflow\": %llu, "
+             "\"walked_overflow\": %llu, \"ties\": %llu}",
+             (unsigned long long)k_.assigns, (unsigned long long)k_.points, (unsigned long long)k_.pairs,
+             (unsigned long long)k_.ambiguous, (unsigned long long)k_.overflow, (unsigned long long)k_.walked_overflow,
+             (unsigned long long)k_.ties);
+    c->last_kn_stats = buf;
 }
 
 }  // namespace st

@@ -2190,6 +2190,7 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     }
     mark(c, "kn.assign");
     const uint32_t namb = h->amb;
+    uint32_t ovf1 = 0;  // first lists that overflowed (collected again with CAND_CAP2)
     if (namb) {
         const uint32_t atiles = (namb + 31) / 32;
         auto *afrag = wsT<uint4>(c, "kn.afrag", (size_t)atiles * ks * 64);
@@ -2210,6 +2211,7 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         }
         ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipStreamSynchronize(c->stream));
+        ovf1 = h->overflow;
         if (h->overflow) {
             // points whose window holds more than CAND_CAP rows (wide windows: outlying points of
             // heavy-tailed data): collected again with lists of CAND_CAP2, in batches; only those
@@ -2252,6 +2254,16 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     if (getenv("ST_DEBUG"))
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
                 (unsigned long long)n, k, npair, namb, h->ties, h->overflow, sigma);
+    {
+        auto &ks_ = c->kn_stats;
+        ++ks_.assigns;
+        ks_.points += n;
+        ks_.pairs += npair;
+        ks_.ambiguous += namb;
+        ks_.overflow += ovf1;
+        ks_.walked_overflow += h->overflow - ovf1;  // the second lists' overflows go to the walk
+        ks_.ties += h->ties;
+    }
     // exact ties from k_fixrow, k_fixpair and k_exact (and candidate overflows): the KdTree walk
     if (!walk_ties) return h->ties;
     if (h->ties) {

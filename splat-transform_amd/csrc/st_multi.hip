@@ -480,6 +480,7 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
         co.allreduce(cen, dk, Dt::I32, Op::Sum, c->stream);
     }
     const std::string t(tag);
+    if (d > 1) c->kn_stats = st_ctx::KnStats{};
     auto *sac = wsT<double>(c, t + ".sac", 2 * dk + k);
     auto *E = wsT<int32_t>(c, t + ".e", dk);
     auto *C = wsT<uint32_t>(c, t + ".c", (size_t)k);
@@ -567,6 +568,7 @@ uint64_t kmeans_sharded(st_ctx *c, Coll &co, const Points &P, int k, int iters, 
         c->vf_k = k;
         c->vf_n = P.n;
     }
+    if (d > 1) kn_stats_publish(c);  // this rank's points
     return cursor;
 }
 

@@ -479,6 +479,7 @@ int st_ctx_synchronize(st_ctx *c) {
 }
 
 const char *st_ctx_last_timings(st_ctx *c) { return c ? c->last_timings.c_str() : "{}"; }
+const char *st_ctx_last_kmeans_stats(st_ctx *c) { return c ? c->last_kn_stats.c_str() : "{}"; }
 
 int st_ctx_set_profiling(st_ctx *c, int32_t enable) {
     return guarded([&] {

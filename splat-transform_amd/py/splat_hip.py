@@ -96,7 +96,7 @@ class PlyHeader(ctypes.Structure):
 
 EXPORTS = [
     'st_abi_version', 'st_last_error', 'st_device_count', 'st_ctx_create', 'st_ctx_destroy', 'st_ctx_set_stream',
-    'st_ctx_synchronize', 'st_ctx_last_timings', 'st_ctx_set_profiling', 'st_ctx_reset_kernel_stats',
+    'st_ctx_synchronize', 'st_ctx_last_timings', 'st_ctx_last_kmeans_stats', 'st_ctx_set_profiling', 'st_ctx_reset_kernel_stats',
     'st_ctx_kernel_stats', 'st_ctx_set_verify', 'st_ctx_verify_snapshot', 'st_quat_from_euler', 'st_transform_params_make', 'st_sog_geometry',
     'st_transform', 'st_filter_finite', 'st_morton_order', 'st_pack_compressed', 'st_kmeans', 'st_cluster1d', 'st_sog',
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
@@ -136,6 +136,7 @@ def lib():
             getattr(L, name)
         L.st_last_error.restype = ctypes.c_char_p
         L.st_ctx_last_timings.restype = ctypes.c_char_p
+        L.st_ctx_last_kmeans_stats.restype = ctypes.c_char_p
         L.st_ctx_destroy.restype = None
         L.st_comm_destroy.restype = None
         L.st_group_destroy.restype = None
@@ -143,7 +144,7 @@ def lib():
         L.st_webp_max_size.restype = ctypes.c_uint64
         L.st_ply_row_bytes.restype = ctypes.c_uint64
         for name in EXPORTS:
-            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_destroy', 'st_free', 'st_webp_max_size',
+            if name not in ('st_last_error', 'st_ctx_last_timings', 'st_ctx_last_kmeans_stats', 'st_ctx_destroy', 'st_free', 'st_webp_max_size',
                             'st_ply_row_bytes', 'st_comm_destroy', 'st_group_destroy'):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -566,6 +567,11 @@ class Context:
 
     def timings(self):
         return lib().st_ctx_last_timings(self.h).decode()
+
+    def kmeans_stats(self):
+        """the last N-D k-means' assign classification (st_ctx_last_kmeans_stats) as a dict"""
+        import json
+        return json.loads(lib().st_ctx_last_kmeans_stats(self.h).decode())
 
     def set_profiling(self, on=True):
         check(lib().st_ctx_set_profiling(self.h, ctypes.c_int32(1 if on else 0)))

@@ -172,6 +172,11 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
     assert rc == 0 and used == oused
     same_bits(labels, olabels)
     same_bits(cent, ocent)
+    if d > 1:  # how the assigns decided the points (st_ctx_last_kmeans_stats), summed over iterations
+        st = ctx.kmeans_stats()
+        assert st['assigns'] == iters and st['points'] == n * iters
+        assert st['ambiguous'] >= st['overflow'] >= st['walked_overflow'] >= 0
+        assert st['pairs'] + st['ambiguous'] <= st['points']
 
 
 K1_MODES = ['', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX=0', 'ST_REPLAY_CAP=0',

@@ -63,3 +63,4 @@ for name in ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'k
 import hashlib
 print('result sha256', hashlib.sha256(cen.cpu().numpy().tobytes() + lab.cpu().numpy().tobytes()).hexdigest()[:16],
       'draws used', used)
+print('assign classification', ctx.kmeans_stats())
