@@ -645,28 +645,14 @@ def sog_stage_table(stages, n, iters, K=65536, D=45):
         return None
     cb = K * D  # values of the codebook cluster1d (the palette's centroid coordinates)
     spec = {
-        'sog.morton': ('hbm', 92 * n, 'generateOrdering: extents 12 + keys 16 + 4 LSD passes on 8-B pairs 64 B/splat'),
-        'sog.means_quats': ('hbm', 40 * n, 'x, y, z, rot_0..3 read (28 B) + means_l/u, quats texels (12 B) per splat'),
-        'sog.scales': ('hbm', 15 * iters * n + 7 * n, 'cluster1d over 3 columns: 5 B per value-iteration '
-                       '(4 B read + 1 B label) x 3 values + the scales texels'),
-        'sog.sh0': ('hbm', 15 * iters * n + 11 * n, 'cluster1d of f_dc as sog.scales + opacity read + sh0 texels'),
+        'sog.cluster1d': ('hbm', 30 * iters * n + 4 * n,
+                          'the scales and the colours cluster1d side by side (st_sog.hip): 5 B per '
+                          'value-iteration (4 B read + 1 B label) x 6 values + the opacity read'),
         'sog.shkmeans': ('mfma', 2.0 * n * K * D * iters, 'SH palette k-means: 2 n K D flop per iteration '
-                         '(the sweep); 184 B/splat/iter of HBM besides'),
+                         '(the sweep); 184 B/splat/iter of HBM besides; the Morton order (92 B/splat) and '
+                         'the five textures (40 + 14 B/splat) run beside it on a side context'),
         'sog.shn': ('hbm', 5 * iters * cb + 8 * n, 'codebook cluster1d over K x D values + shN labels texels'),
     }
-    # the colours' cluster1d and the Morton order + means/quats run on side contexts beside the
-    # scales' cluster1d (st_sog.hip): the marks up to sog.sh0 time one overlapped block, priced
-    # as one
-    block = tuple(k for k in ('sog.morton', 'sog.means_quats', 'sog.scales', 'sog.sh0') if k in stages)
-    if stages.get('sog.scales') and stages.get('sog.sh0'):
-        stages = dict(stages)
-        spec = dict(spec)
-        ms_b = sum(stages.pop(k) for k in block)
-        work_b = sum(spec.pop(k)[1] for k in ('sog.morton', 'sog.means_quats', 'sog.scales', 'sog.sh0'))
-        stages['sog.morton..sh0'] = ms_b
-        spec['sog.morton..sh0'] = ('hbm', work_b, 'scales cluster1d on the main stream, the colours cluster1d and '
-                                   'Morton + means/quats beside it on side contexts (one overlapped block): '
-                                   '92 + 40 + (15 iters + 7) + (15 iters + 11) B per splat')
     out = {}
     for k, (bound, work, what) in spec.items():
         ms = stages.get(k)

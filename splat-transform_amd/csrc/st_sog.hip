@@ -476,15 +476,17 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         }
     } joiner{colours};
 
-    // Morton order, extents and the means / quats textures on a third context from their own
-    // host thread (c->aux->aux), beside the scales' cluster1d here: only the texture writes
-    // after the k-means wait for the texel positions
+    // Morton order, extents and the five textures on a third context from their own host
+    // thread (c->aux->aux), started once both cluster1d are done so that the 1-D block runs
+    // alone and the Morton passes overlap the SH k-means' sweep instead: only the shN texture
+    // writes wait for the texel positions
     auto *pos = wsT<uint32_t>(c, "sog.pos", n);
     const unsigned g = grid_for(n, 256, 8192);
     if (!aux->aux) ST_REQUIRE(st_ctx_create(c->device, &aux->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
     st_ctx *mc = aux->aux;
-    hipEvent_t ev_pos;
+    hipEvent_t ev_pos, ev_lab;
     ST_HIP(hipEventCreateWithFlags(&ev_pos, hipEventDisableTiming));
+    ST_HIP(hipEventCreateWithFlags(&ev_lab, hipEventDisableTiming));
     {
         hipEvent_t ev;  // the textures' clears above and the caller's columns
         ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -493,7 +495,8 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         ST_HIP(hipEventDestroy(ev));
     }
     std::exception_ptr err_m;
-    std::thread order_th([&] {
+    const uint8_t *lab_s_ = nullptr, *clab_ = nullptr;  // the labels the texture writes read
+    auto order_fn = [&] {
         try {
             use_device(mc);
             // Morton order (write-sog.ts:42-49)
@@ -555,20 +558,35 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
                 hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, mc->stream, m[10], m[11], m[12], m[13],
                                    (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
             ST_LAUNCH_CHECK();
+            {  // the scales / sh0 texels, once the labels are in place
+                ST_HIP(hipStreamWaitEvent(mc->stream, ev_lab, 0));
+                hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, lab_s_, lab_s_ + n, lab_s_ + 2 * n,
+                                   (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
+                if (src.op64)
+                    hipLaunchKernelGGL(k_table_tex<double>, dim3(g), dim3(256), 0, mc->stream, clab_, clab_ + n,
+                                       clab_ + 2 * n, src.op64, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+                else
+                    hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, clab_, clab_ + n,
+                                       clab_ + 2 * n, m[9], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+                ST_LAUNCH_CHECK();
+            }
             ST_HIP(hipEventRecord(ev_pos, mc->stream));
+            if (c->sog_early) c->sog_early(mc);  // the five textures are final on mc->stream
             ST_HIP(hipStreamSynchronize(mc->stream));
         } catch (...) {
             err_m = std::current_exception();
         }
-    });
+    };
+    std::thread order_th;
     struct Joiner2 {
         std::thread &th;
-        hipEvent_t ev;
+        hipEvent_t ev, ev2;
         ~Joiner2() {
             if (th.joinable()) th.join();
             (void)hipEventDestroy(ev);
+            (void)hipEventDestroy(ev2);
         }
-    } joiner2{order_th, ev_pos};
+    } joiner2{order_th, ev_pos, ev_lab};
 
     uint64_t cursor = 0;
     auto *lab = wsT<uint8_t>(c, "sog.lab", n * 3);
@@ -576,36 +594,37 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
     // scales (write-sog.ts:245-251)
     cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
     ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    order_th.join();
-    if (err_m) std::rethrow_exception(err_m);
-    ST_HIP(hipStreamWaitEvent(c->stream, ev_pos, 0));
-    mark(c, "sog.morton");
-    hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, lab, lab + n, lab + 2 * n,
-                       (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
-    ST_LAUNCH_CHECK();
-    mark(c, "sog.scales");
     // colour + opacity (write-sog.ts:253-268)
     colours.join();
     const uint8_t *clab = lab_c;
     const float *ccb = cb_c;
+    uint8_t *lab_s = lab;
     if (cursor == 0) {
         if (err_c) std::rethrow_exception(err_c);
         cursor += used_c;
     } else {  // the scales took draws: the colours' k-means starts after them
+        lab_s = wsT<uint8_t>(c, "sog.lab_s", n * 3);
+        ST_HIP(hipMemcpyAsync(lab_s, lab, n * 3, hipMemcpyDeviceToDevice, c->stream));
         cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
         clab = lab;
         ccb = cb;
     }
     ST_HIP(hipMemcpyAsync(meta->sh0_codebook, ccb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    if (src.op64)
-        hipLaunchKernelGGL(k_table_tex<double>, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n,
-                           src.op64, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
-    else
-        hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, c->stream, clab, clab + n, clab + 2 * n, m[9],
-                           (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
-    ST_LAUNCH_CHECK();
-    mark(c, "sog.sh0");
-    if (c->sog_early) c->sog_early(c);  // means_l/u, quats, scales, sh0 are final on c->stream
+    mark(c, "sog.cluster1d");
+    // the Morton order and the five textures beside the SH k-means (order_fn)
+    lab_s_ = lab_s;
+    clab_ = clab;
+    ST_HIP(hipEventRecord(ev_lab, c->stream));
+    if (c->sog_early && !mc->aux)
+        ST_REQUIRE(st_ctx_create(c->device, &mc->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    order_th = std::thread(order_fn);
+    // the texture thread ends before anything reads the texel positions on this stream
+    auto join_late = [&] {
+        if (!order_th.joinable()) return;
+        order_th.join();
+        if (err_m) std::rethrow_exception(err_m);
+        ST_HIP(hipStreamWaitEvent(c->stream, ev_pos, 0));
+    };
 
     meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
     if (C > 0) {
@@ -619,6 +638,7 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         cursor += kmeans_dev(c, src.sh, D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels, false,
                              src.sh64[0] ? src.sh64 : nullptr);
         mark(c, "sog.shkmeans");
+        join_late();
         // the shN labels texels (random 4-byte stores at the Morton positions) do not wait for
         // the codebook: they run on the side stream beside its latency-bound 1-D iterations,
         // on few workgroups so that those kernels still find free CUs
@@ -652,6 +672,7 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
         mark(c, "sog.shn");
     }
+    join_late();
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;
 }
