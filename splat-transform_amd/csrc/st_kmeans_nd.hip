@@ -220,24 +220,37 @@ __global__ __launch_bounds__(256) void k_absmax(const float *const *cols, int d,
 constexpr int PF_PTS = 128;            // points (= threads) per workgroup (4 tiles): 31.5 KiB of LDS,
                                        // five workgroups per CU
 constexpr int PF_LDS_LD = PF_PTS + 1;  // LDS column stride: row-wise reads hit distinct banks
-__global__ __launch_bounds__(PF_PTS) void k_point_frags(const float *const *cols, int d, uint64_t n, uint32_t ntiles,
-                                                     int ks, float sigma, uint4 *pfrag, float *pnorm, float *pdn,
+// DT > 0: the dimension count known at compile time (the SH palettes: 45, 24, 9) -- every column
+// load in flight at once and the row / fragment index arithmetic by constants; DT = 0: any d <= 61
+template <int DT>
+__global__ __launch_bounds__(PF_PTS) void k_point_frags(const float *const *cols, int d_rt, uint64_t n, uint32_t ntiles,
+                                                     int ks_rt, float sigma, uint4 *pfrag, float *pnorm, float *pdn,
                                                      float *aos) {
-    __shared__ float x[61 * PF_LDS_LD];  // d <= 61
+    __shared__ float x[(DT ? DT : 61) * PF_LDS_LD];  // d <= 61
+    const int d = DT ? DT : d_rt;
+    const int ks = DT ? kp_of(DT) / 16 : ks_rt;
     const uint64_t p0 = (uint64_t)blockIdx.x * PF_PTS;
     const int j = threadIdx.x;
     const bool valid = p0 + j < n;
     const uint64_t pj = valid ? p0 + j : n - 1;  // loads stay in bounds without a branch
-    // batches of 8 columns: the loads of a batch are in flight together
-    int k0 = 0;
-    for (; k0 + 8 <= d; k0 += 8) {
-        float v[8];
+    if constexpr (DT > 0) {
+        float v[DT];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = cols[k0 + u][pj];
+        for (int u = 0; u < DT; ++u) v[u] = cols[u][pj];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[(k0 + u) * PF_LDS_LD + j] = valid ? v[u] : 0.0f;
+        for (int u = 0; u < DT; ++u) x[u * PF_LDS_LD + j] = valid ? v[u] : 0.0f;
+    } else {
+        // batches of 8 columns: the loads of a batch are in flight together
+        int k0 = 0;
+        for (; k0 + 8 <= d; k0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = cols[k0 + u][pj];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[(k0 + u) * PF_LDS_LD + j] = valid ? v[u] : 0.0f;
+        }
+        for (; k0 < d; ++k0) x[k0 * PF_LDS_LD + j] = valid ? cols[k0][pj] : 0.0f;
     }
-    for (; k0 < d; ++k0) x[k0 * PF_LDS_LD + j] = valid ? cols[k0][pj] : 0.0f;
     __syncthreads();
     if (valid) {
         // |sigma p| and the norm of its fp16 rounding residual p - p~ (exact in f64), rounded up
@@ -1983,8 +1996,19 @@ void nd_prepare(st_ctx *c, const float *const *dcols, int d, uint64_t n) {
     }
     float sigma = 1.0f;
     if (amax > 0) sigma = std::ldexp(1.0f, -std::ilogb(amax));
-    hipLaunchKernelGGL(k_point_frags, dim3((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS)), dim3(PF_PTS), 0,
-                       c->stream, dcols, d, n, ntiles, ks, sigma, pfrag, pnorm, pdn, aos);
+    const dim3 gpf((unsigned)(((uint64_t)ntiles * 32 + PF_PTS - 1) / PF_PTS));
+    if (d == 45)
+        hipLaunchKernelGGL(k_point_frags<45>, gpf, dim3(PF_PTS), 0, c->stream, dcols, d, n, ntiles, ks, sigma, pfrag,
+                           pnorm, pdn, aos);
+    else if (d == 24)
+        hipLaunchKernelGGL(k_point_frags<24>, gpf, dim3(PF_PTS), 0, c->stream, dcols, d, n, ntiles, ks, sigma, pfrag,
+                           pnorm, pdn, aos);
+    else if (d == 9)
+        hipLaunchKernelGGL(k_point_frags<9>, gpf, dim3(PF_PTS), 0, c->stream, dcols, d, n, ntiles, ks, sigma, pfrag,
+                           pnorm, pdn, aos);
+    else
+        hipLaunchKernelGGL(k_point_frags<0>, gpf, dim3(PF_PTS), 0, c->stream, dcols, d, n, ntiles, ks, sigma, pfrag,
+                           pnorm, pdn, aos);
     ST_LAUNCH_CHECK();
     c->kn_sigma = sigma;
     c->kn_n = n;
