@@ -419,8 +419,8 @@ __global__ __launch_bounds__(64 * CF_W) void k_centroid_frags(const float *cen, 
 // Software pipeline over "slots" (one centroid tile x one point tile = KS MFMAs): the
 // epilogue of the previous slot is cut into KS slices, slice s issued right behind
 // MFMA s of this slot and fenced with sched_barrier, so each MFMA's 32 cycles on the
-// matrix pipe cover ~10 VALU ops of the same wave.  Occupancy is 2 waves per SIMD
-// (~190 VGPRs: B fragments 48, score buffers 64, A ping-pong 24, top-3 state 20).
+// matrix pipe cover ~10 VALU ops of the same wave.  Occupancy is 3 waves per SIMD (160 VGPRs:
+// B fragments 48, score buffers 64, A ping-pong 24, top-3 state; 48 KiB of LDS per workgroup).
 template <int KS, int MODE>
 __global__ __launch_bounds__(WG) void k_sweep(const uint4 *__restrict__ pfrag, uint32_t ntiles, uint32_t npts,
                                                const uint4 *__restrict__ cfrag, uint32_t ctiles,
