@@ -112,6 +112,8 @@ struct st_ctx {
     // overlaps latency-bound chains on `stream`, joined by the two events
     hipStream_t side = nullptr;
     hipEvent_t side_ev[2] = {nullptr, nullptr};
+    // the N-D assign's read-backs: behind the sweep, behind the fix-up (created on first use)
+    hipEvent_t kn_ev[2] = {nullptr, nullptr};
     st::Workspace ws;
     // pinned host staging for small readbacks
     void *pinned = nullptr;

@@ -2116,6 +2116,16 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_KS_DISPATCH(ks, (Sweep<KS>::main(c, pfrag, ntiles, (uint32_t)n, cfrag, ctiles, pnorm, pdn, scal + 1, chalf,
                                         chalf_d, ntab, bnd,
                                         labels, thr, amb, dstate, pair_pts, pair_codes, hist)));
+    // the sweep's pair / ambiguous counts are final here (the fix-up only adds ties): read back
+    // behind the sweep, waited for while the fix-up runs, so that the pairs' and the ambiguous
+    // points' kernels queue up behind it with no idle gap; the fix-up's own tie count (h_fix)
+    // is read behind it and waited for only where it is needed
+    auto *h_fix = static_cast<State *>(pinned_slot(c, "kn.hfix", sizeof(State)));
+    ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    for (auto &e : c->kn_ev)
+        if (!e) ST_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipEvent_t ev_sw = c->kn_ev[0], ev_fix = c->kn_ev[1];
+    ST_HIP(hipEventRecord(ev_sw, c->stream));
     if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
         KTimer kt(c, "kn.fixrow");
@@ -2189,14 +2199,10 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
                            caos, k, (uint32_t)n, labels, ties, dstate);
         ST_LAUNCH_CHECK();
     }
-    ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-    ST_HIP(hipStreamSynchronize(c->stream));
+    ST_HIP(hipMemcpyAsync(h_fix, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    ST_HIP(hipEventRecord(ev_fix, c->stream));
+    ST_HIP(hipEventSynchronize(ev_sw));
     const uint32_t npair = h->pairs;
-    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
-        fz->nties_fix = h->ties;
-        fz->npair = npair;
-        fz->namb = h->amb;
-    }
     if (npair) {
         KTimer kt(c, "kn.fixpair");
         const dim3 g((npair * 32 + 255) / 256);
@@ -2216,6 +2222,14 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     }
     mark(c, "kn.assign");
     const uint32_t namb = h->amb;
+    // the fix-up's read-back (the pairs' kernel already queued behind it); h is the latest from here
+    ST_HIP(hipEventSynchronize(ev_fix));
+    *h = *h_fix;
+    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
+        fz->nties_fix = h->ties;
+        fz->npair = npair;
+        fz->namb = namb;
+    }
     uint32_t ovf1 = 0;  // first lists that overflowed (collected again with CAND_CAP2)
     if (namb) {
         const uint32_t atiles = (namb + 31) / 32;

@@ -446,6 +446,8 @@ void st_ctx_destroy(st_ctx *c) {
     }
     for (auto e : c->side_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto e : c->kn_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
