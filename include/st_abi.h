@@ -403,8 +403,10 @@ int st_comm_init_rank(st_ctx *ctx, int32_t world, int32_t rank, const uint8_t id
  * N-GPU job rehearsed on one card).  Every rank passes the same `name` ([A-Za-z0-9_.-], unique
  * per job; rank 0 creates /dev/shm/st_<name>, which is unlinked once every rank has attached),
  * slot_bytes (per-rank staging slot, multiple of 4096; 0 = 32 MiB) and timeout_s (longest wait
- * for a peer before the job is aborted; <= 0 = 600 s).  A peer process that exits, or a rank
- * that fails, makes every rank's next exchange fail. */
+ * for a peer before the job is aborted; <= 0 = 600 s).  The ranks must all attach within
+ * timeout_s when it is set (> 0), within 120 s when it is not; the environment variable
+ * ST_SHM_ATTACH_S overrides the attach wait.  A peer process that exits, or a rank that fails,
+ * makes every rank's next exchange fail. */
 int st_comm_init_host(st_ctx *ctx, int32_t world, int32_t rank, const char *name, uint64_t slot_bytes,
                       double timeout_s, st_comm **out);
 void st_comm_destroy(st_comm *comm);

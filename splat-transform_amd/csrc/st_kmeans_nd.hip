@@ -2131,7 +2131,9 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         KTimer kt(c, "kn.fixrow");
         auto *cursor = wsT<uint32_t>(c, "kn.fbcur", ncodes);
         auto *ndec = wsT<uint32_t>(c, "kn.fbnd", 1);
-        const bool fused = fz && fz->want && walk_ties;
+        // k_fixrow_lp sums DT = 45 / 24 / 9 dimensions of its LD-wide rows (the SH palettes' d):
+        // any other d in the same row width (10-12, 21-23, 46-48) takes the member-sort update
+        const bool fused = fz && fz->want && walk_ties && d == (ld == 48 ? 45 : ld == 24 ? 24 : 9);
         // fused: the grouped points alone (a slice knows its code); otherwise (point, code) pairs
         auto *grouped = fused ? nullptr : wsT<uint2>(c, "kn.fbpts2", n);
         auto *grouped1 = fused ? wsT<uint32_t>(c, "kn.fbpts1", n) : nullptr;

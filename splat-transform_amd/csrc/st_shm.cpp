@@ -301,10 +301,14 @@ std::unique_ptr<Coll> make_shm_coll(int world, int rank, const char *name, size_
     seg->rank = rank;
     seg->timeout_s = timeout_s > 0 ? timeout_s : 600;
     seg->size = header_bytes() + (size_t)kChannels * world * slot_bytes;
-    // the ranks meet within kAttachLimitS (or the job's timeout if shorter): a rank that died before
-    // attaching ends rank 0's wait, and rank 0 unlinks the name, well before a launcher's first-stall
-    // kill (bench.py: 600 s) could stop rank 0 with no destructor run and leave the segment in tmpfs
-    const double attach_s = std::min(seg->timeout_s, kAttachLimitS);
+    // the ranks meet within kAttachLimitS by default: a rank that died before attaching ends rank
+    // 0's wait, and rank 0 unlinks the name, well before a launcher's first-stall kill (bench.py:
+    // 600 s) could stop rank 0 with no destructor run and leave the segment in tmpfs.  A job that
+    // sets its timeout explicitly (timeout_s > 0) waits that long instead -- ranks that start far
+    // apart on purpose -- and ST_SHM_ATTACH_S overrides both
+    double attach_s = timeout_s > 0 ? timeout_s : std::min(seg->timeout_s, kAttachLimitS);
+    if (const char *e = getenv("ST_SHM_ATTACH_S"))
+        if (atof(e) > 0) attach_s = atof(e);
     using clk = std::chrono::steady_clock;
     const auto deadline = clk::now() + std::chrono::duration<double>(attach_s);
     if (rank == 0) {

@@ -1160,6 +1160,13 @@ void sog_file_check(int fd) {
     ST_REQUIRE(fstat(fd, &stt) == 0, ST_ERR_ARG, std::string("sog file: fstat failed: ") + std::strerror(errno));
     ST_REQUIRE(S_ISREG(stt.st_mode) || lseek(fd, 0, SEEK_CUR) != (off_t)-1, ST_ERR_ARG,
                "sog file: fd must be a seekable file (a regular file opened for writing)");
+    // pwrite on an O_APPEND descriptor ignores the offset (Linux) and a read-only one fails only
+    // after the step: both are refused here
+    const int fl = fcntl(fd, F_GETFL);
+    ST_REQUIRE(fl != -1, ST_ERR_ARG, std::string("sog file: fcntl failed: ") + std::strerror(errno));
+    ST_REQUIRE((fl & O_ACCMODE) == O_WRONLY || (fl & O_ACCMODE) == O_RDWR, ST_ERR_ARG,
+               "sog file: fd must be open for writing");
+    ST_REQUIRE(!(fl & O_APPEND), ST_ERR_ARG, "sog file: fd must not be opened with O_APPEND (writes go at offsets)");
 }
 
 void write_at(int fd, const uint8_t *p, uint64_t n, uint64_t off) {

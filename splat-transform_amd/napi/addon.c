@@ -49,6 +49,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include <sys/mman.h>
 #include <time.h>
 
@@ -202,7 +203,8 @@ static void set_named(napi_env env, napi_value obj, const char *k, napi_value v)
 /* Freed columns' blocks are kept (up to ST_NAPI_POOL_MB, default 4096 MiB) and handed to the
  * next column of the same rounded length: a reused block is already faulted in, while a fresh
  * one is zeroed by the kernel on first touch inside the device-to-host copy (1,240 huge pages
- * for a 10M-splat table).  Finalizers and allocations both run on the JS thread. */
+ * for a 10M-splat table).  The pool is process-wide: with the addon loaded in worker_threads
+ * each env's finalizers and allocations run on that env's own thread, so g_pool_mu guards it. */
 #define POOL_MAX 512
 static struct {
     void *p;
@@ -210,6 +212,7 @@ static struct {
 } g_pool[POOL_MAX];
 static int g_pool_n = 0;
 static size_t g_pool_bytes = 0;
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static size_t pool_cap(void) {
     static size_t cap = (size_t)-1;
@@ -224,13 +227,16 @@ static void free_column(napi_env env, void *data, void *hint) {
     int64_t adj;
     const size_t bytes = (size_t)hint, huge = (size_t)2 << 20, len = (bytes + huge - 1) / huge * huge;
     napi_adjust_external_memory(env, -(int64_t)bytes, &adj);
+    pthread_mutex_lock(&g_pool_mu);
     if (g_pool_n < POOL_MAX && g_pool_bytes + len <= pool_cap()) {
         g_pool[g_pool_n].p = data;
         g_pool[g_pool_n].len = len;
         ++g_pool_n;
         g_pool_bytes += len;
+        pthread_mutex_unlock(&g_pool_mu);
         return;
     }
+    pthread_mutex_unlock(&g_pool_mu);
     free(data);
 }
 
@@ -239,12 +245,14 @@ static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t 
     if (bytes < ((size_t)8 << 20)) return new_typed(env, type, elems, esize, data);
     void *p = NULL;
     const size_t len = (bytes + huge - 1) / huge * huge;
+    pthread_mutex_lock(&g_pool_mu);
     for (int i = g_pool_n - 1; i >= 0 && !p; --i)
         if (g_pool[i].len == len) {
             p = g_pool[i].p;
             g_pool[i] = g_pool[--g_pool_n];
             g_pool_bytes -= len;
         }
+    pthread_mutex_unlock(&g_pool_mu);
     if (!p) {
         if (posix_memalign(&p, huge, len) != 0) {
             napi_throw_error(env, NULL, "splat-hip: out of host memory for a column");

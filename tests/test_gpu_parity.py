@@ -161,7 +161,11 @@ def heavy_tailed(rng, n, d, scale=0.1):
 
 
 @pytest.mark.parametrize('n,d,k,iters,dist', [(20_000, 45, 1024, 2, 'gauss'), (30_000, 9, 2048, 2, 'gauss'),
-                                              (60_000, 1, 256, 4, 'gauss'), (20_000, 45, 1024, 3, 't3')])
+                                              (60_000, 1, 256, 4, 'gauss'), (20_000, 45, 1024, 3, 't3'),
+                                              # row widths the SH palettes share (12, 48) at other d:
+                                              # the fused fix-up is for d = 9 / 24 / 45 only
+                                              (20_000, 12, 1024, 2, 'gauss'), (20_000, 48, 1024, 2, 'gauss'),
+                                              (20_000, 10, 1024, 2, 'gauss'), (20_000, 22, 1024, 2, 'gauss')])
 def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
     rng = np.random.default_rng(n + d)
     cols = ([rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)] if dist == 'gauss'
