@@ -167,7 +167,8 @@ def launch(args, argv):
     """parent of a self-launched N-rank job: never imports torch (nothing here touches the GPU);
     the ranks' stdout is read here, rank 0's JSON line relayed, everything else goes to stderr.
     A job that stalls or fails is rerun once with the side channel off (ST_SIDE_CHANNEL=0: every
-    exchange on the main communicator, in one host thread's program order), and the line says so."""
+    exchange on the main communicator, in one host thread's program order) and the library's
+    collectives on torch's RCCL (ST_RCCL=process), and the line says so."""
     cmd = launcher_cmd(argv, args.gpus, free_port())
     if args.launch_dry_run:
         _RESULT.write(json.dumps({'cmd': cmd, 'torch_imported': 'torch' in sys.modules}) + '\n')
@@ -185,9 +186,12 @@ def launch(args, argv):
         print(f'bench.py: the {args.gpus}-rank job ended without a result ({first}); rerunning it once with the '
               'side channel off (ST_SIDE_CHANNEL=0)', file=sys.stderr, flush=True)
         env['ST_SIDE_CHANNEL'] = '0'
+        # and the collectives on the RCCL torch already loaded (st_rccl.h: ST_RCCL=process) instead
+        # of a second copy beside it
+        env.setdefault('ST_RCCL', 'process')
         cmd = launcher_cmd(argv, args.gpus, free_port())
         rc, line, why = run_job(cmd, env, args.launch_budget, args.launch_stall)
-        fallback = {'side_channel': 'off', 'first_job': first}
+        fallback = {'side_channel': 'off', 'rccl': env['ST_RCCL'], 'first_job': first}
     if line is None:
         print(f'bench.py: the {args.gpus}-rank job exited with {rc}' + (f' ({why})' if why else ''), file=sys.stderr)
         return rc or 3
@@ -335,7 +339,7 @@ PLY_ORDER = (['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [
              ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3'])
 
 
-def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=3):
+def end_to_end(ctx, cols, iters, draws, tex, ref_archive, meta, reps=3):
     """The CLI's work for `splat-transform in.ply out.sog` on this table: the step's table is
     written once as a binary little-endian 3DGS PLY (62 float properties, 248 B per splat,
     normals 0; untimed), then each timed rep reads the file into device columns
@@ -412,7 +416,7 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=3):
                 'archive_equals_in_memory_step': one['archive_equals_in_memory_step'] and
                 sep['archive_equals_in_memory_step'],
                 'separate_calls': dict(sep, what='st_dev_sog, st_dev_sog_bundle_view, one write(2)'),
-                'node_host': node_end_to_end(src, dst, n, iters, reps)}
+                'node_host': node_end_to_end(ctx, src, dst, n, iters, reps, draws, tex, meta)}
     finally:
         for f in (src, dst):
             if os.path.exists(f):
@@ -420,29 +424,53 @@ def end_to_end(ctx, cols, iters, draws, tex, ref_archive, reps=3):
         os.rmdir(d)
 
 
-def node_end_to_end(src, dst, n, iters, reps):
+NODE_CLOCK = [2024, 0, 1, 0, 0, 0]  # the Node job's pinned Date: 2024-01-01 00:00:00
+NODE_DOS_TIME, NODE_DOS_DATE = 0, ((2024 - 1980) << 9) | (1 << 5) | 1  # zip-writer.ts:39-41 of that clock
+
+
+def node_end_to_end(ctx, src, dst, n, iters, reps, draws, tex, meta):
     """The same job through the Node drop-in host (tools/bench_node.js: js/index.js readPly ->
     writeSogFile over the N-API addon, as the reference's index.ts:433-510 drives its reader and
     writer): the PLY read into a host DataTable, then uploaded and written as .sog.  A separate
-    process on the same GPU; None when node or the addon is absent."""
+    process on the same GPU; None when node or the addon is absent.  Math.random is the bench's
+    draw stream and Date a pinned clock in every rep, so each timed rep's file must equal the
+    library's archive of the main step's textures with that clock (archive_equals_library)."""
+    import hashlib
     import shutil
     import subprocess
+
+    import numpy as np
     node = shutil.which('node')
     addon = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
     if not node or not os.path.exists(addon):
         return None
-    r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(max(3, reps)), str(iters)],
-                       capture_output=True, text=True, timeout=600)
+    dfile = dst + '.draws.f64'
+    np.asarray(draws, '<f8').tofile(dfile)
+    try:
+        r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(max(3, reps)), str(iters),
+                            dfile, json.dumps(NODE_CLOCK)], capture_output=True, text=True, timeout=600)
+    finally:
+        os.remove(dfile)
     if r.returncode != 0:
         return {'error': r.stderr[-2000:]}
     out = json.loads(r.stdout.strip().splitlines()[-1])
+    want = None
+    if meta is not None:
+        addr, size = ctx.dev_sog_bundle_view(meta, n, tex, NODE_DOS_TIME, NODE_DOS_DATE)
+        want = hashlib.sha256(bytes((ctypes_char_array(size)).from_address(addr))).hexdigest()
     runs = sorted(out['runs'], key=lambda x: x['total'])
     med = runs[len(runs) // 2]
     return {'what': 'node tools/bench_node.js: readPly(FileHandle) -> host DataTable -> writeSogFile(FileHandle) '
-                    '(js/index.js over napi/addon.node: st_ply_read + st_sog_file), median of the timed reps',
+                    '(js/index.js over napi/addon.node: st_ply_read + st_sog_file), median of the timed reps; '
+                    'Math.random = the bench\'s draw stream, Date pinned',
             'ms': med['total'], 'Msplats_per_s': n / med['total'] / 1e3,
             'split_ms': {'readPly': med['readPly'], 'writeSogFile': med['writeSogFile']},
-            'rows': out['rows'], 'sog_bytes': out['sog_bytes'], 'reps': len(runs)}
+            'rows': out['rows'], 'sog_bytes': out['sog_bytes'], 'reps': len(runs),
+            'resident_columns_reused': med.get('reusedColumns'),
+            'archive_sha256': out['sha256'][-1],
+            'archive_equals_library': (want is not None and all(h == want for h in out['sha256'])),
+            'how_checked': 'sha256 of the file after every rep (warm-up included) against st_dev_sog_bundle_view of '
+                           'the main step\'s textures and meta with the same DOS clock'}
 
 
 def check_labels(sh, prev, lab, n_labels, g):
@@ -993,6 +1021,17 @@ def main(args):
             sys.exit(1)
         return
     tex_sha = textures_digest(tex, meta)
+    # the RCCL the library's collectives run on (st_rccl_info; the same file under the Node host)
+    # and torch.distributed's own copy
+    rccl_version = rccl_path = rccl_torch = None
+    try:
+        rccl_version, rccl_path = sh.rccl_info()
+    except sh.StError as e:
+        rccl_path = f'not loadable: {e}'
+    try:
+        rccl_torch = '.'.join(map(str, torch.cuda.nccl.version()))
+    except Exception:
+        pass
     # the .sog container of this step's textures on rank 0 (outside the headline's timed region)
     addr0, size0 = ctx.dev_sog_bundle_view(meta, total, tex, 0, 0)  # warm: workspace + pinned archive
     ref_archive = bytes((ctypes_char_array(size0)).from_address(addr0))
@@ -1016,7 +1055,7 @@ def main(args):
     e2e = None
     progress('end-to-end file run')
     if not sharded and not args.no_e2e:
-        e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive)
+        e2e = end_to_end(ctx, tabs[0], args.iters, draws, tex, ref_archive, meta)
     paths = None
     progress('config-3 stage table')
     if not sharded and not args.no_paths:
@@ -1053,6 +1092,8 @@ def main(args):
                  'source': os.path.relpath(ufile, ROOT)}
     out = {
         'metric': 'Msplats/sec PLY->SOG (SH-3, 10 k-means iters)',
+        'headline': ('device pipeline, resident table (PLY ingest and WebP/ZIP excluded; see end_to_end_file '
+                     'for the PLY file -> .sog file job, end_to_end_file.node_host for the Node drop-in)'),
         'value': value,
         'unit': 'Msplats/s',
         'n_gpus': world,
@@ -1102,6 +1143,9 @@ def main(args):
         'draws_used_per_step': used,
         'sh_kmeans_assign': sh_assign,
         'rccl_ranks': rccl_ranks,
+        'rccl_version': rccl_version,
+        'rccl_path': rccl_path,
+        'rccl_torch_version': rccl_torch,
         'transport': transport,
         'side_channel': (os.environ.get('ST_SIDE_CHANNEL') != '0') if comm else None,
         'distinct_devices': devices if sharded else 1,

@@ -179,6 +179,15 @@ const char *st_ctx_last_timings(st_ctx *ctx);
  * before the first.  Owned by ctx, valid until its next N-D k-means.  (No reference counterpart:
  * diagnostics of this build's exact assign.) */
 const char *st_ctx_last_kmeans_stats(st_ctx *ctx);
+/* The writeSog host forms (st_sog, st_sog_bundle, st_sog_file) run on the device columns the
+ * last st_ply_read left resident when the caller's table is that read's host columns, unchanged:
+ * the step starts at once on them while host threads compare every byte of the host columns
+ * with the read's pinned copy; the first changed byte abandons the run (nothing has left the
+ * device), and the call uploads the columns and runs again.  This reports, for the last such
+ * call on ctx, how many columns / bytes ran from the resident copy (0 / 0: uploaded).
+ * ST_HOST_MIRROR=0 disables the reuse.  (No reference counterpart: the reference's readPly ->
+ * writeSog keeps the table in JS memory, index.ts:433-510.) */
+int st_ctx_last_host_reuse(st_ctx *ctx, uint64_t *columns, uint64_t *bytes);
 /* Kernel profiling: when enabled, the library brackets its named hot kernels
  * ("kn.sweep", "mo.sort", ...) with hipEvents on the context stream; stats
  * accumulate until st_ctx_reset_kernel_stats.  Query after a synchronize. */
@@ -412,6 +421,12 @@ int st_comm_init_host(st_ctx *ctx, int32_t world, int32_t rank, const char *name
 void st_comm_destroy(st_comm *comm);
 /* ranks in the communicator (ncclCommCount for RCCL): the bench reports it as `rccl_ranks` */
 int st_comm_count(const st_comm *comm, int32_t *count);
+/* the RCCL the library's collectives run on (loaded on first use, no GPU needed): its
+ * ncclGetVersion (e.g. 22707 = 2.27.7) and the real path of the file.  Both hosts load the same
+ * file by path -- /opt/rocm/lib/librccl.so.1 unless ST_RCCL names another, or ST_RCCL=process
+ * (the copy of soname librccl.so.1 already in the process: torch's under Python) -- under a
+ * handle of its own (RTLD_LOCAL).  path may be NULL.  ST_ERR_INTERNAL if it cannot be loaded. */
+int st_rccl_info(int32_t *version, char *path, uint64_t path_len);
 /* one rank's part of a sharded writeSog: `locals` are this rank's tables (device columns; its
  * files or file parts, in global order); every rank calls it with the same iters and draws.
  * meta / out (device textures) are written on rank 0 only. */

@@ -4,6 +4,9 @@
 // N-API addon, ctypes); callers that keep tables resident use st_dev_*.
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
 
 #include <unistd.h>
 #include <cerrno>
@@ -91,6 +94,127 @@ std::vector<std::string> transform_columns() {
     std::vector<std::string> v = {"x", "y", "z", "rot_0", "rot_1", "rot_2", "rot_3", "scale_0", "scale_1", "scale_2"};
     for (int i = 0; i < 45; ++i) v.push_back("f_rest_" + std::to_string(i));
     return v;
+}
+
+// ---- writeSog host forms on st_ply_read's mirrors --------------------------------------------
+// A host table whose every column writeSog reads is one st_ply_read filled (st_ctx::HostMirror)
+// is not uploaded: the step runs on the resident device columns at once, while host threads
+// compare the caller's columns with their pinned twins byte for byte (memcmp, ~4.7 GB read at
+// 10M splats, beside the step).  Nothing leaves the device (no file write, no host output) until
+// the compare has said "equal"; a changed byte raises spec_abort (the SH k-means stops at its
+// next iteration), the call waits for its queued work, uploads the columns and runs again.
+struct Spec {
+    st_ctx *c;
+    std::atomic<bool> abort{false};
+    std::vector<std::thread> th;
+    std::mutex mu;  // verdict() is called from the call's thread and from sog_file_dev's writer
+    bool joined = false;
+    explicit Spec(st_ctx *ctx) : c(ctx) {}
+    bool verdict() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!joined) {
+            for (auto &t : th) t.join();
+            joined = true;
+        }
+        return !abort.load();
+    }
+    ~Spec() {
+        verdict();
+        c->spec_abort = nullptr;
+        c->spec_verdict = nullptr;
+    }
+};
+
+const st_ctx::HostMirror *find_mirror(st_ctx *c, const void *host, uint64_t bytes) {
+    for (const auto &m : c->mirrors)
+        if (m.host == host && m.bytes == bytes) return &m;
+    return nullptr;
+}
+
+// the wanted float columns of h, all mirrored: d holds their device twins and the compare runs
+// on sp's threads; false (nothing started) when any one is not a mirror
+bool mirror_table(st_ctx *c, const st_table *h, const std::vector<std::string> &want, DevTable &d, Spec &sp) {
+    const char *mo = getenv("ST_HOST_MIRROR");
+    if ((mo && std::strcmp(mo, "0") == 0) || c->mirrors.empty() || !h->n) return false;
+    std::vector<const st_ctx::HostMirror *> ms;
+    for (int i = 0; i < h->ncol; ++i) {
+        bool hit = want.empty();
+        for (auto &w : want) hit = hit || (w == h->names[i]);
+        if (!hit) continue;
+        const auto *m = find_mirror(c, h->cols[i], h->n * sizeof(float));
+        if (!m) return false;
+        d.names.push_back(h->names[i]);
+        d.cols.push_back(static_cast<float *>(const_cast<void *>(m->dev)));
+        ms.push_back(m);
+    }
+    for (auto &s : d.names) d.cnames.push_back(s.c_str());
+    d.t.n = h->n;
+    d.t.ncol = (int32_t)d.names.size();
+    d.t.names = d.cnames.data();
+    d.t.cols = d.cols.data();
+    // the compare: the columns' bytes cut into 1 MiB blocks dealt round-robin to the threads
+    constexpr uint64_t BLK = 1ull << 20;
+    std::vector<std::pair<const char *, const char *>> blocks;
+    std::vector<uint64_t> lens;
+    for (const auto *m : ms)
+        for (uint64_t o = 0; o < m->bytes; o += BLK) {
+            blocks.emplace_back(static_cast<const char *>(m->host) + o, static_cast<const char *>(m->shadow) + o);
+            lens.push_back(std::min(BLK, m->bytes - o));
+        }
+    const int nt = std::max(1, std::min(16, getenv("ST_MIRROR_THREADS") ? atoi(getenv("ST_MIRROR_THREADS")) : 8));
+    auto shared = std::make_shared<std::pair<decltype(blocks), decltype(lens)>>(std::move(blocks), std::move(lens));
+    for (int t = 0; t < nt; ++t)
+        sp.th.emplace_back([&sp, shared, t, nt] {
+            const auto &bl = shared->first;
+            const auto &ln = shared->second;
+            for (size_t b = (size_t)t; b < bl.size(); b += (size_t)nt) {
+                if (sp.abort.load(std::memory_order_relaxed)) return;
+                if (std::memcmp(bl[b].first, bl[b].second, ln[b]) != 0) {
+                    sp.abort.store(true);
+                    return;
+                }
+            }
+        });
+    c->spec_abort = &sp.abort;
+    c->spec_verdict = [&sp] { return sp.verdict(); };
+    return true;
+}
+
+// waits for everything queued on the context's streams (an abandoned speculative run's work)
+void drain_ctx(st_ctx *c) {
+    for (st_ctx *x : {c, c->aux}) {
+        if (!x) continue;
+        (void)hipStreamSynchronize(x->stream);
+        if (x->side) (void)hipStreamSynchronize(x->side);
+    }
+}
+
+// body(dev_table) on the mirrors when possible (spec_gate inside body before any output leaves
+// the device), else -- or when the host columns changed -- on an upload
+template <typename F>
+void run_host_sog(st_ctx *c, const st_table *t, const std::vector<std::string> &want, const std::string &tag, F &&body) {
+    c->last_reuse_cols = c->last_reuse_bytes = 0;
+    {
+        DevTable d;
+        Spec sp(c);
+        if (mirror_table(c, t, want, d, sp)) {
+            std::exception_ptr err;
+            try {
+                body(&d.t);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            if (sp.verdict()) {
+                if (err) std::rethrow_exception(err);
+                c->last_reuse_cols = d.cols.size();
+                c->last_reuse_bytes = d.cols.size() * t->n * sizeof(float);
+                return;
+            }
+            drain_ctx(c);
+        }
+    }
+    DevTable d = upload(c, t, want, tag);
+    body(&d.t);
 }
 
 // a workspace slot that receives `count` host elements with the batch's next h2d()
@@ -322,7 +446,6 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
     return guarded_h([&] {
         ST_ARGH(c && t && meta && out, "NULL argument");
         use_device(c);
-        DevTable d = upload(c, t, sog_columns(), "h.s");
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
@@ -337,7 +460,11 @@ int st_sog(st_ctx *c, const st_table *t, int32_t iters, const double *draws, uin
             dt.shn_labels = wsT<uint8_t>(c, "h.s.shl", tex);
             dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
         }
-        const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, meta, &dt);
+        uint64_t u = 0;
+        run_host_sog(c, t, sog_columns(), "h.s", [&](const st_table *dtab) {
+            u = sog_dev(c, dtab, iters, draws, ndraws, meta, &dt);
+            spec_gate(c);
+        });
         Batch b{c};
         b.add_d2h(out->means_l, dt.means_l, tex);
         b.add_d2h(out->means_u, dt.means_u, tex);
@@ -364,7 +491,6 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
     return guarded_h([&] {
         ST_ARGH(c && t && out && out_size, "NULL argument");
         use_device(c);
-        DevTable d = upload(c, t, sog_columns(), "h.s");
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
@@ -380,7 +506,11 @@ int st_sog_bundle(st_ctx *c, const st_table *t, int32_t iters, const double *dra
             dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
         }
         st_sog_meta meta{};
-        const uint64_t u = sog_dev(c, &d.t, iters, draws, ndraws, &meta, &dt);
+        uint64_t u = 0;
+        run_host_sog(c, t, sog_columns(), "h.s", [&](const st_table *dtab) {
+            u = sog_dev(c, dtab, iters, draws, ndraws, &meta, &dt);
+            spec_gate(c);
+        });
         const uint8_t *view;
         uint64_t nb;
         sog_bundle_dev(c, meta, t->n, dt, dos_time, dos_date, &view, &nb);
@@ -418,7 +548,7 @@ int st_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws
     return guarded_h([&] {
         ST_ARGH(c && t && size && fd >= 0, "bad argument");
         use_device(c);
-        DevTable d = upload(c, t, sog_columns(), "h.s");
+        sog_file_check(fd);
         const int C = sh_coeffs_of(t);
         int32_t W, H, pal, cw, chh;
         ST_REQUIRE(st_sog_geometry(t->n, C, &W, &H, &pal, &cw, &chh) == ST_OK, ST_ERR_ARG, "sog: empty table");
@@ -434,7 +564,10 @@ int st_sog_file(st_ctx *c, const st_table *t, int32_t iters, const double *draws
             dt.shn_centroids = wsT<uint8_t>(c, "h.s.shc", (uint64_t)cw * chh * 4);
         }
         st_sog_meta meta{};
-        const uint64_t u = sog_file_dev(c, &d.t, iters, draws, ndraws, &meta, &dt, fd, dos_time, dos_date, size);
+        uint64_t u = 0;
+        run_host_sog(c, t, sog_columns(), "h.s", [&](const st_table *dtab) {
+            u = sog_file_dev(c, dtab, iters, draws, ndraws, &meta, &dt, fd, dos_time, dos_date, size);
+        });
         if (used) *used = u;
     });
 }

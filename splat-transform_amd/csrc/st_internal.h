@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
 #include <functional>
 
 #include <cstdint>
@@ -24,6 +25,13 @@ struct Error : std::runtime_error {
 };
 
 void set_last_error(const std::string &msg);
+
+// a host form that ran on st_ply_read's device twins of the caller's columns while the columns
+// were compared with their pinned twins (st_host_api.hip: run_host_sog) stops with this when the
+// compare finds a changed byte; the call then uploads the columns and runs again
+struct SpecAbort : Error {
+    SpecAbort() : Error(ST_ERR_INTERNAL, "speculative run abandoned: the host columns changed since st_ply_read") {}
+};
 
 #define ST_HIP(expr)                                                                          \
     do {                                                                                      \
@@ -159,6 +167,23 @@ struct st_ctx {
     bool verify = false;
     int vf_d = 0, vf_k = 0;
     uint64_t vf_n = 0;
+    // the host columns the last st_ply_read filled, with their device columns (workspace slots
+    // "plyh.c<p>", still resident) and pinned host twins (every byte as the device copy has it).
+    // The writeSog host forms run on `dev` when every column they read is here, while other
+    // threads compare `host` with `shadow` (exact: memcmp); a changed byte sends the call back to
+    // an upload (st_host_api.hip).  Dropped by the next st_ply_read.  ST_HOST_MIRROR=0: off.
+    struct HostMirror {
+        const void *host;
+        uint64_t bytes;
+        const void *shadow;
+        const void *dev;
+    };
+    std::vector<HostMirror> mirrors;
+    // set while a host form runs on mirrors: the compare raises *spec_abort on a mismatch (the
+    // N-D k-means checks it every iteration), spec_verdict waits for the compare (true = equal)
+    std::atomic<bool> *spec_abort = nullptr;
+    std::function<bool()> spec_verdict;
+    uint64_t last_reuse_cols = 0, last_reuse_bytes = 0;  // st_ctx_last_host_reuse
 };
 
 namespace st {
@@ -184,6 +209,13 @@ struct HostXfer {
 };
 void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs);
 void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs);
+// host-side copy over the context's copy threads (large copies split; small ones inline)
+void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes);
+// a speculative host form's gate before it writes anything outside the device: throws SpecAbort
+// when the compare found the host columns changed (waits for the compare)
+inline void spec_gate(st_ctx *c) {
+    if (c->spec_verdict && !c->spec_verdict()) throw SpecAbort();
+}
 void use_device(st_ctx *c);
 void mark(st_ctx *c, const char *name);  // records a hipEvent when timing is on
 
@@ -308,7 +340,11 @@ uint64_t cluster1d_pair_dev(st_ctx *c, st_ctx *side, const float *const *a, cons
                             uint8_t *lab_b);
 
 // PLY ingest / compressed-PLY reader (st_ply.hip)
-void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols);
+// (after_chunk: called once each chunk's transpose is queued on c->stream, with its rows)
+void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols,
+                  const std::function<void(uint64_t row, uint64_t nrows)> &after_chunk = {});
+// st_ply_read: into the caller's host columns, and the element's mirrors (st_ctx::HostMirror)
+void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols);
 void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
                         const uint8_t *const *sh, int nsh, float *const *out);
 

@@ -2464,6 +2464,8 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
         return nd_big_sums(c, d, n, k, labels, cen);
     };
     for (int it = 0; it < iters; ++it) {
+        // a speculative host form whose compare found the host columns changed stops here
+        if (c->spec_abort && c->spec_abort->load(std::memory_order_relaxed)) throw SpecAbort();
         if (pending && c->verify && it == iters - 1) settle();
         if (c->verify && it == iters - 1)
             ST_HIP(hipMemcpyAsync(ws(c, "verify.prev", cbytes), cen, cbytes, hipMemcpyDeviceToDevice, c->stream));

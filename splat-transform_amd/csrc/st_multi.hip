@@ -43,6 +43,24 @@
 #include "st_internal.h"
 #include "st_kmeans.h"
 #include "st_webp.h"
+#include "st_rccl.h"
+
+// every RCCL entry point through the run-time binding (st_rccl.h: one RCCL file for both hosts)
+#define ncclGetErrorString (::st::rccl().GetErrorString)
+#define ncclGetUniqueId (::st::rccl().GetUniqueId)
+#define ncclCommInitRank (::st::rccl().CommInitRank)
+#define ncclCommInitAll (::st::rccl().CommInitAll)
+#define ncclCommSplit (::st::rccl().CommSplit)
+#define ncclCommDestroy (::st::rccl().CommDestroy)
+#define ncclCommAbort (::st::rccl().CommAbort)
+#define ncclCommCount (::st::rccl().CommCount)
+#define ncclAllReduce (::st::rccl().AllReduce)
+#define ncclBroadcast (::st::rccl().Broadcast)
+#define ncclAllGather (::st::rccl().AllGather)
+#define ncclSend (::st::rccl().Send)
+#define ncclRecv (::st::rccl().Recv)
+#define ncclGroupStart (::st::rccl().GroupStart)
+#define ncclGroupEnd (::st::rccl().GroupEnd)
 
 namespace st {
 

@@ -17,8 +17,11 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -301,8 +304,10 @@ void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const 
     }
 }
 
-// one element of a PLY file (fd) into device columns, streamed through pinned chunks
-void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols) {
+// one element of a PLY file (fd) into device columns, streamed through pinned chunks; after_chunk
+// (if set) is called on this thread once each chunk's transpose is queued on c->stream
+void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols,
+                  const std::function<void(uint64_t row, uint64_t nrows)> &after_chunk) {
     ST_REQUIRE(element >= 0 && element < h.nelements, ST_ERR_ARG, "ply: element index out of range");
     uint64_t off = h.header_bytes;
     for (int e = 0; e < element; ++e) off += h.elements[e].count * row_bytes(h.elements[e]);
@@ -360,6 +365,7 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
             ST_HIP(hipEventRecord(ev[b], c->stream));
             pending[b] = true;
             tp.run(stage[b], nr, row);
+            if (after_chunk) after_chunk(row, nr);
             row += nr;
         }
         ST_HIP(hipStreamSynchronize(c->stream));
@@ -371,6 +377,134 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
     }
     (void)hipEventDestroy(ev[0]);
     (void)hipEventDestroy(ev[1]);
+}
+
+// st_ply_read: the element into device columns (ply_read_dev), and their bytes out to the
+// caller's host columns while later chunks are still read: every ~256 MiB of rows, once their
+// transpose is done, a second stream copies the columns' new rows into one pinned block (the
+// element's pinned twin, column after column) and a host thread copies them on into the caller's
+// columns -- host-to-device reads and device-to-host writes on the link at once, instead of the
+// whole element up and then the whole element down.  The device columns and the pinned twin
+// stay: they are the mirrors the writeSog host forms run on while the host columns are
+// unchanged (st_ctx::HostMirror).
+void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols) {
+    c->mirrors.clear();  // their device slots and pinned twin are overwritten below
+    const st_ply_element &el = h.elements[element];
+    const int np = el.nprops;
+    std::vector<void *> dcols(np);
+    std::vector<uint64_t> sz(np), off(np);
+    uint64_t total = 0;
+    for (int p = 0; p < np; ++p) {
+        sz[p] = (uint64_t)type_size(el.props[p].type);
+        dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * sz[p] + 8);
+        off[p] = total;
+        total += (el.count * sz[p] + 63) / 64 * 64;
+    }
+    if (!el.count || !np) {
+        ply_read_dev(c, fd, h, element, dcols.data(), {});
+        return;
+    }
+    auto *shadow = static_cast<uint8_t *>(pinned_slot(c, "plyh.shadow", total));
+    hipStream_t s2 = side_stream(c);
+    struct Group {
+        uint64_t row, nr;
+        hipEvent_t ev;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Group> q;
+    bool fin = false;
+    std::exception_ptr err;
+    // the drain thread: waits for a group's device-to-host copy, then copies it on
+    std::thread drain([&] {
+        try {
+            use_device(c);
+            for (;;) {
+                Group g;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return fin || !q.empty(); });
+                    if (q.empty()) return;
+                    g = q.front();
+                    q.pop_front();
+                }
+                const hipError_t e = hipEventSynchronize(g.ev);
+                (void)hipEventDestroy(g.ev);
+                ST_HIP(e);
+                for (int p = 0; p < np; ++p)
+                    host_copy(c, static_cast<char *>(host_cols[p]) + g.row * sz[p],
+                              reinterpret_cast<const char *>(shadow + off[p] + g.row * sz[p]), g.nr * sz[p]);
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            err = std::current_exception();
+            // drop the queued groups' events (their copies are never waited for)
+            for (auto &g : q) (void)hipEventDestroy(g.ev);
+            q.clear();
+        }
+    });
+    uint64_t row_bytes_all = 0;
+    for (int p = 0; p < np; ++p) row_bytes_all += sz[p];
+    uint64_t group_rows = std::max<uint64_t>(1, (256ull << 20) / row_bytes_all);
+    if (const char *e = std::getenv("ST_PLY_D2H_ROWS")) group_rows = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    uint64_t g0 = 0;  // first row not yet sent down
+    auto send = [&](uint64_t upto) {
+        if (upto <= g0) return;
+        hipEvent_t ev;
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, c->stream));
+        ST_HIP(hipStreamWaitEvent(s2, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+        const uint64_t nr = upto - g0;
+        for (int p = 0; p < np; ++p)
+            ST_HIP(hipMemcpyAsync(shadow + off[p] + g0 * sz[p], static_cast<char *>(dcols[p]) + g0 * sz[p], nr * sz[p],
+                                  hipMemcpyDeviceToHost, s2));
+        hipEvent_t done;
+        ST_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(done, s2));
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (err) {
+                (void)hipEventDestroy(done);
+            } else {
+                q.push_back({g0, nr, done});
+            }
+        }
+        cv.notify_one();
+        g0 = upto;
+    };
+    struct Finish {  // the drain thread ends on every path out of here
+        std::mutex &mu;
+        std::condition_variable &cv;
+        bool &fin;
+        std::thread &th;
+        hipStream_t s2;
+        ~Finish() {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                fin = true;
+            }
+            cv.notify_one();
+            if (th.joinable()) th.join();
+            (void)hipStreamSynchronize(s2);
+        }
+    } finish{mu, cv, fin, drain, s2};
+    ply_read_dev(c, fd, h, element, dcols.data(), [&](uint64_t row, uint64_t nr) {
+        if (row + nr - g0 >= group_rows) send(row + nr);
+    });
+    send(el.count);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        fin = true;
+    }
+    cv.notify_one();
+    drain.join();
+    ST_HIP(hipStreamSynchronize(s2));
+    if (err) std::rethrow_exception(err);
+    const char *mo = std::getenv("ST_HOST_MIRROR");
+    if (!(mo && std::strcmp(mo, "0") == 0))
+        for (int p = 0; p < np; ++p)
+            c->mirrors.push_back({host_cols[p], el.count * sz[p], shadow + off[p], dcols[p]});
 }
 
 }  // namespace st
@@ -421,7 +555,7 @@ int st_dev_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t eleme
     return guard([&] {
         ST_REQUIRE(c && h && cols && fd >= 0, ST_ERR_ARG, "bad argument");
         use_device(c);
-        ply_read_dev(c, fd, *h, element, cols);
+        ply_read_dev(c, fd, *h, element, cols, {});
     });
 }
 
@@ -430,15 +564,7 @@ int st_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, 
         ST_REQUIRE(c && h && host_cols && fd >= 0 && element >= 0 && element < h->nelements, ST_ERR_ARG,
                    "bad argument");
         use_device(c);
-        const st_ply_element &el = h->elements[element];
-        std::vector<void *> dcols(el.nprops);
-        for (int p = 0; p < el.nprops; ++p)
-            dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * type_size(el.props[p].type) + 8);
-        ply_read_dev(c, fd, *h, element, dcols.data());
-        std::vector<HostXfer> down;
-        for (int p = 0; p < el.nprops; ++p)
-            down.push_back(HostXfer{host_cols[p], dcols[p], el.count * type_size(el.props[p].type)});
-        staged_d2h(c, down);
+        ply_read_host(c, fd, *h, element, host_cols);
     });
 }
 

@@ -167,17 +167,6 @@ void xfer_setup(st_ctx *c) {
     if (!c->xfer_pool) c->xfer_pool = new CopyPool(XF_THREADS);
 }
 
-// host-side copy of one piece: split over the pool when it is large
-void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes) {
-    if (bytes < (2ull << 20)) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    static_cast<CopyPool *>(c->xfer_pool)->run([=](int t) {
-        const size_t a0 = bytes * t / XF_THREADS, a1 = bytes * (t + 1) / XF_THREADS;
-        std::memcpy(dst + a0, src + a0, a1 - a0);
-    });
-}
 
 // the staged transfers cut into slot-sized pieces; small ones are issued directly
 std::vector<Piece> pieces_of(st_ctx *c, const std::vector<HostXfer> &xs, bool h2d) {
@@ -196,6 +185,19 @@ std::vector<Piece> pieces_of(st_ctx *c, const std::vector<HostXfer> &xs, bool h2
     return ps;
 }
 }  // namespace
+
+// host-side copy of one piece: split over the pool when it is large
+void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes) {
+    if (bytes < (2ull << 20)) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    if (!c->xfer_pool) c->xfer_pool = new CopyPool(XF_THREADS);
+    static_cast<CopyPool *>(c->xfer_pool)->run([=](int t) {
+        const size_t a0 = bytes * t / XF_THREADS, a1 = bytes * (t + 1) / XF_THREADS;
+        std::memcpy(dst + a0, src + a0, a1 - a0);
+    });
+}
 
 // ST_XFER_PRINT=1: bytes and rate of every staged copy on stderr
 struct XferLog {
@@ -482,6 +484,14 @@ int st_ctx_synchronize(st_ctx *c) {
 
 const char *st_ctx_last_timings(st_ctx *c) { return c ? c->last_timings.c_str() : "{}"; }
 const char *st_ctx_last_kmeans_stats(st_ctx *c) { return c ? c->last_kn_stats.c_str() : "{}"; }
+
+int st_ctx_last_host_reuse(st_ctx *c, uint64_t *columns, uint64_t *bytes) {
+    return guarded([&] {
+        ST_ARG(c && columns && bytes, "NULL argument");
+        *columns = c->last_reuse_cols;
+        *bytes = c->last_reuse_bytes;
+    });
+}
 
 int st_ctx_set_profiling(st_ctx *c, int32_t enable) {
     return guarded([&] {

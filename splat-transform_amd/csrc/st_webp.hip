@@ -1289,12 +1289,16 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
                                        {"scales.webp", out->scales, meta->width, meta->height},
                                        {"sh0.webp", out->sh0, meta->width, meta->height}};
         early.t0 = std::chrono::steady_clock::now();
-        early.th = std::thread([&early, aux, imgs, fd, dos_time, dos_date] {
+        // a speculative host form (st_host_api: run_host_sog) writes nothing before its compare says
+        // the host columns are unchanged
+        std::function<bool()> verdict = cc->spec_verdict;
+        early.th = std::thread([&early, aux, imgs, fd, dos_time, dos_date, verdict] {
             try {
                 use_device(aux);
                 uint8_t *blk = nullptr;
                 early.bytes = stage_entries(aux, imgs, {}, nullptr, dos_time, dos_date, "sf.e", early.es, &blk);
                 early.t1 = std::chrono::steady_clock::now();
+                if (verdict && !verdict()) throw SpecAbort();
                 write_at(fd, blk, early.bytes, 0);
                 early.t2 = std::chrono::steady_clock::now();
             } catch (...) {
@@ -1331,6 +1335,7 @@ uint64_t sog_file_dev(st_ctx *c, const st_table *t, int iters, const double *dra
                 ms(early.t1), ms(early.t2), ms(t_ret), ms(t_gpu), ms(t3), ms(std::chrono::steady_clock::now()));
     }
     if (early.err) std::rethrow_exception(early.err);
+    spec_gate(c);
     std::vector<ZipEntry> all = early.es;
     all.insert(all.end(), les.begin(), les.end());
     ST_REQUIRE(zip_size(all) < (1ull << 32), ST_ERR_ARG, "sog file: archive exceeds 4 GiB (no zip64, as the reference)");

@@ -474,11 +474,14 @@ const decompressPly = (ply) => {
 // write-sog.ts:241-243): 1 (default) = one device
 const setDevices = (n) => addon.setDevices(n);
 const getDevices = () => addon.getDevices();
+// {version, path} of the RCCL the library's collectives run on (the same file under every host)
+const rcclInfo = () => addon.rcclInfo();
 
 module.exports = {
     resetRandomStream,
     setDevices,
     getDevices,
+    rcclInfo,
     Column,
     DataTable,
     addon,

@@ -8,6 +8,8 @@
  * Exports (js/index.js wraps them in the reference's signatures):
  *   version() -> number                       st_abi_version
  *   deviceCount() -> number                   st_device_count
+ *   rcclInfo() -> {version, path}             st_rccl_info (the RCCL the collectives run on)
+ *   lastHostReuse() -> {columns, bytes}       st_ctx_last_host_reuse (readPly's resident columns)
  *   transform(cols, names, t[3], r[4], s)     st_transform_params_make + st_transform
  *                                             (transform.ts:12-65)
  *   quatFromEuler(ex, ey, ez) -> [x,y,z,w]    Quat.setFromEulerAngles (process.ts:75-79)
@@ -282,6 +284,41 @@ static napi_value make_num(napi_env env, double d) {
 static napi_value js_version(napi_env env, napi_callback_info info) {
     (void)info;
     return make_num(env, st_abi_version());
+}
+
+/* rcclInfo() -> {version, path}: the RCCL the library's collectives run on (st_rccl_info) */
+static napi_value js_rccl_info(napi_env env, napi_callback_info info) {
+    (void)info;
+    int32_t v = 0;
+    char path[4096];
+    napi_value out, s;
+    const int rc = st_rccl_info(&v, path, sizeof path);
+    if (rc != ST_OK) return throw_st(env, rc);
+    NAPI_OK(napi_create_object(env, &out));
+    set_named(env, out, "version", make_num(env, v));
+    NAPI_OK(napi_create_string_utf8(env, path, NAPI_AUTO_LENGTH, &s));
+    set_named(env, out, "path", s);
+    return out;
+fail:
+    return NULL;
+}
+
+/* lastHostReuse() -> {columns, bytes}: how much of the last writeSog host form ran from readPly's
+ * resident device columns (st_ctx_last_host_reuse; 0 = uploaded) */
+static napi_value js_last_host_reuse(napi_env env, napi_callback_info info) {
+    (void)info;
+    st_ctx *ctx;
+    uint64_t cols = 0, bytes = 0;
+    napi_value out;
+    if (!get_ctx(env, &ctx)) return NULL;
+    const int rc = st_ctx_last_host_reuse(ctx, &cols, &bytes);
+    if (rc != ST_OK) return throw_st(env, rc);
+    NAPI_OK(napi_create_object(env, &out));
+    set_named(env, out, "columns", make_num(env, (double)cols));
+    set_named(env, out, "bytes", make_num(env, (double)bytes));
+    return out;
+fail:
+    return NULL;
 }
 
 static napi_value js_device_count(napi_env env, napi_callback_info info) {
@@ -1568,6 +1605,8 @@ static napi_value init(napi_env env, napi_value exports) {
         napi_callback fn;
     } fns[] = {{"version", js_version},
                {"deviceCount", js_device_count},
+               {"rcclInfo", js_rccl_info},
+               {"lastHostReuse", js_last_host_reuse},
                {"quatFromEuler", js_quat_from_euler},
                {"transform", js_transform},
                {"filterFinite", js_filter_finite},

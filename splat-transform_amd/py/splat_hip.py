@@ -102,7 +102,7 @@ EXPORTS = [
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
     'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_init_host', 'st_comm_destroy',
-    'st_comm_count',
+    'st_comm_count', 'st_rccl_info', 'st_ctx_last_host_reuse',
     'st_dev_sog_sharded', 'st_group_create', 'st_group_destroy', 'st_group_sog', 'st_group_sog_bundle',
     'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
@@ -507,6 +507,15 @@ def ply_parse_header(data):
     return h
 
 
+def rccl_info():
+    """(version, path) of the RCCL the library's collectives run on (st_rccl_info: loaded by path,
+    /opt/rocm/lib/librccl.so.1 unless ST_RCCL says otherwise; no GPU needed)"""
+    v = ctypes.c_int32(0)
+    buf = ctypes.create_string_buffer(4096)
+    check(lib().st_rccl_info(ctypes.byref(v), buf, ctypes.c_uint64(len(buf))))
+    return v.value, buf.value.decode()
+
+
 def device_count():
     n = ctypes.c_int32(0)
     check(lib().st_device_count(ctypes.byref(n)))
@@ -567,6 +576,28 @@ class Context:
 
     def timings(self):
         return lib().st_ctx_last_timings(self.h).decode()
+
+    def host_reuse(self):
+        """(columns, bytes) the last writeSog host form ran from st_ply_read's resident copy
+        (st_ctx_last_host_reuse; (0, 0): it uploaded them)"""
+        cols, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(lib().st_ctx_last_host_reuse(self.h, ctypes.byref(cols), ctypes.byref(nb)))
+        return cols.value, nb.value
+
+    def sog_file(self, cols, iters, draws, path, dos_time=0, dos_date=0):
+        """writeSog of a host table into a file (st_sog_file): (used, size).  The file is opened
+        without O_TRUNC (st_sog_file cuts it to the archive's length)"""
+        keep = {k: np.ascontiguousarray(v, np.float32) for k, v in cols.items()}
+        t = make_table(keep)
+        used, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            check(lib().st_sog_file(self.h, ctypes.byref(t), ctypes.c_int32(iters), _vp(draws),
+                                    ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.c_int32(fd),
+                                    ctypes.c_uint16(dos_time), ctypes.c_uint16(dos_date), ctypes.byref(size)))
+        finally:
+            os.close(fd)
+        return used.value, size.value
 
     def kmeans_stats(self):
         """the last N-D k-means' assign classification (st_ctx_last_kmeans_stats) as a dict"""

@@ -110,3 +110,66 @@ def test_st_num_gpus_rejects_a_bad_value():
     assert rc == sh.ST_ERR_ARG and n == 0 and 'ST_NUM_GPUS' in msg
     rc, _, msg = _get_devices_with_env('0')
     assert rc == sh.ST_ERR_ARG and 'ST_NUM_GPUS' in msg
+
+
+def _rccl_python(env_value=None, torch_first=True):
+    """st_rccl_info in a fresh Python process (torch imported first, as the bench does)"""
+    import json
+    import subprocess
+    import sys
+    code = (('import torch; ' if torch_first else '') +
+            'import json, sys; sys.path.insert(0, %r); import splat_hip as sh; '
+            'print(json.dumps(sh.rccl_info()))' % os.path.join(ROOT, 'splat-transform_amd', 'py'))
+    env = dict(os.environ)
+    env.pop('ST_RCCL', None)
+    if env_value is not None:
+        env['ST_RCCL'] = env_value
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return tuple(json.loads(r.stdout.strip().splitlines()[-1]))
+
+
+def test_rccl_is_the_same_file_under_python_and_node():
+    """the library binds RCCL at run time by path (st_rccl.h): under the Python host -- where torch
+    has already mapped its own librccl.so.1 (2.26.x) -- and under the Node host (no torch) the
+    collectives run on the same file, /opt/rocm/lib/librccl.so.1, and report the same version"""
+    import shutil
+    import subprocess
+    v, path = _rccl_python()
+    assert os.path.realpath(path) == os.path.realpath('/opt/rocm/lib/librccl.so.1'), path
+    assert v >= 22700, v
+    node = shutil.which('node')
+    addon = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
+    if not node or not os.path.exists(addon):
+        pytest.skip('node or the N-API addon absent')
+    js = ("const h = require(%r); console.log(JSON.stringify(h.rcclInfo()));" %
+          os.path.join(ROOT, 'splat-transform_amd', 'js'))
+    env = dict(os.environ)
+    env.pop('ST_RCCL', None)
+    r = subprocess.run([node, '-e', js], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    nj = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (nj['version'], nj['path']) == (v, path)
+
+
+def test_rccl_process_mode_binds_the_loaded_copy():
+    """ST_RCCL=process: the copy of soname librccl.so.1 already in the process (torch's), the
+    binding before round 6 -- a different version than the ROCm install's"""
+    import torch
+    v, path = _rccl_python('process')
+    assert os.path.realpath(path) == os.path.realpath(os.path.join(os.path.dirname(torch.__file__), 'lib',
+                                                                   'librccl.so'))
+    assert v != _rccl_python()[0]
+
+
+def test_rccl_bad_path_fails_loudly():
+    import subprocess
+    import sys
+    code = ('import sys; sys.path.insert(0, %r); import splat_hip as sh\n'
+            'try:\n    sh.rccl_info(); print("loaded")\nexcept sh.StError as e:\n    print("error", e)'
+            % os.path.join(ROOT, 'splat-transform_amd', 'py'))
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True,
+                       env=dict(os.environ, ST_RCCL='/nonexistent/librccl.so.1'), timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith('error') and 'ST_RCCL' in r.stdout, r.stdout

@@ -42,7 +42,7 @@ def test_addon_exports(addon_built):
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
                                        'process', 'compressedPlyFromFile', 'sogBundleFromFile',
                                        'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped',
-                                       'sogFile'])
+                                       'sogFile', 'rcclInfo', 'lastHostReuse'])
     assert ver == '1'
 
 

@@ -68,6 +68,16 @@ def test_read_ply_vs_oracle(ctx, tmp_path, monkeypatch, n, shc, odd, chunk):
         assert wn == gn and list(wc) == list(gc)
         for k in wc:
             assert same(gc[k].cpu().numpy(), wc[k]), k
+    # the host form: its device-to-host copies overlap the later chunks' reads, in groups of rows
+    # (ST_PLY_D2H_ROWS: many ragged groups) -- every byte as the oracle's
+    for rows in (None, 7_777):
+        if rows:
+            monkeypatch.setenv('ST_PLY_D2H_ROWS', str(rows))
+        _, got = ctx.read_ply(str(p))
+        for (wn, wc), (gn, gc) in zip(want, got):
+            assert wn == gn and list(wc) == list(gc)
+            for k in wc:
+                assert same(gc[k], wc[k]), (k, rows)
 
 
 def test_read_ply_truncated_file_raises(ctx, tmp_path):

@@ -57,35 +57,52 @@ def test_sog_file_equals_the_bundle(ctx, tmp_path, n, C):
 
 
 def test_sog_file_write_error_is_reported(ctx, tmp_path):
-    import ctypes
-
+    """a descriptor that takes writes but fails them (/dev/full: ENOSPC) ends the call with
+    ST_ERR_ARG 'write failed' after the step, and the context still works afterwards"""
     import torch
 
     import bench
     import splat_hip as sh
+    if not os.path.exists('/dev/full'):
+        pytest.skip('no /dev/full')
     dev = torch.device('cuda', 0)
     n = 70_000
     cols = bench.synth_table(n, 5, dev)
     tex = _textures(sh, n, 15, dev)
     draws = np.random.default_rng(3).random(2 * 65536 * 8)
-    path = str(tmp_path / 'ro.sog')
-    open(path, 'wb').close()
-    fd = os.open(path, os.O_RDONLY)
+    fd = os.open('/dev/full', os.O_WRONLY)
     try:
-        t = sh.make_table(cols)
-        out = sh.SogTextures(*[(tex[k].data_ptr() if k in tex else None) for k in
-                               ('means_l', 'means_u', 'quats', 'scales', 'sh0', 'shN_centroids', 'shN_labels')])
-        meta, used, size = sh.SogMeta(), ctypes.c_uint64(0), ctypes.c_uint64(0)
-        rc = sh.lib().st_dev_sog_file(ctx.h, ctypes.byref(t), ctypes.c_int32(2), sh._vp(draws),
-                                      ctypes.c_uint64(len(draws)), ctypes.byref(used), ctypes.byref(meta),
-                                      ctypes.byref(out), ctypes.c_int32(fd), ctypes.c_uint16(0), ctypes.c_uint16(0),
-                                      ctypes.byref(size))
+        rc, _ = _sog_file_fd(ctx, cols, tex, draws, fd)
     finally:
         os.close(fd)
     assert rc == sh.ST_ERR_ARG and b'write failed' in sh.lib().st_last_error()
-    # the context still works afterwards
     meta, used, size = ctx.dev_sog_file(cols, 2, draws, tex, str(tmp_path / 'ok.sog'))
     assert size == os.path.getsize(str(tmp_path / 'ok.sog'))
+
+
+@pytest.mark.parametrize('flags,msg', [(os.O_RDONLY, b'open for writing'),
+                                       (os.O_WRONLY | os.O_APPEND, b'O_APPEND')], ids=['rdonly', 'append'])
+def test_sog_file_refuses_unusable_descriptors_up_front(ctx, tmp_path, flags, msg):
+    """pwrite on an O_APPEND descriptor ignores the offset (Linux) and a read-only one fails only
+    at the first write: both are refused with ST_ERR_ARG before any work, the file untouched"""
+    import torch
+
+    import bench
+    import splat_hip as sh
+    dev = torch.device('cuda', 0)
+    n = 20_000
+    cols = bench.synth_table(n, 5, dev)
+    tex = _textures(sh, n, 15, dev)
+    draws = np.random.default_rng(3).random(2 * 65536 * 8)
+    path = str(tmp_path / 'x.sog')
+    open(path, 'wb').write(b'keep')
+    fd = os.open(path, flags)
+    try:
+        rc, _ = _sog_file_fd(ctx, cols, tex, draws, fd)
+    finally:
+        os.close(fd)
+    assert rc == sh.ST_ERR_ARG and msg in sh.lib().st_last_error()
+    assert open(path, 'rb').read() == b'keep'
 
 
 def _sog_file_fd(ctx, cols, tex, draws, fd, iters=2):
