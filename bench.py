@@ -447,7 +447,8 @@ def node_end_to_end(ctx, src, dst, n, iters, reps, draws, tex, meta):
     dfile = dst + '.draws.f64'
     np.asarray(draws, '<f8').tofile(dfile)
     try:
-        r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(max(3, reps)), str(iters),
+        r = subprocess.run([node, '--expose-gc', os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, str(max(3, reps)),
+                            str(iters),
                             dfile, json.dumps(NODE_CLOCK)], capture_output=True, text=True, timeout=600)
     finally:
         os.remove(dfile)
@@ -462,7 +463,8 @@ def node_end_to_end(ctx, src, dst, n, iters, reps, draws, tex, meta):
     med = runs[len(runs) // 2]
     return {'what': 'node tools/bench_node.js: readPly(FileHandle) -> host DataTable -> writeSogFile(FileHandle) '
                     '(js/index.js over napi/addon.node: st_ply_read + st_sog_file), median of the timed reps; '
-                    'Math.random = the bench\'s draw stream, Date pinned',
+                    'Math.random = the bench\'s draw stream, Date pinned; global.gc() between reps (untimed), so '
+                    'every rep\'s columns reuse the addon\'s faulted-in blocks',
             'ms': med['total'], 'Msplats_per_s': n / med['total'] / 1e3,
             'split_ms': {'readPly': med['readPly'], 'writeSogFile': med['writeSogFile']},
             'rows': out['rows'], 'sog_bytes': out['sog_bytes'], 'reps': len(runs),

@@ -179,6 +179,8 @@ struct st_ctx {
         const void *dev;
     };
     std::vector<HostMirror> mirrors;
+    void *shadow = nullptr;  // the mirrors' host twins (pageable, huge pages, grow-only)
+    size_t shadow_bytes = 0;
     // set while a host form runs on mirrors: the compare raises *spec_abort on a mismatch (the
     // N-D k-means checks it every iteration), spec_verdict waits for the compare (true = equal)
     std::atomic<bool> *spec_abort = nullptr;
@@ -211,6 +213,8 @@ void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs);
 void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs);
 // host-side copy over the context's copy threads (large copies split; small ones inline)
 void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes);
+// fn(t, nt) on each of the context's nt copy threads; returns when all are done
+void host_parallel(st_ctx *c, const std::function<void(int, int)> &fn);
 // a speculative host form's gate before it writes anything outside the device: throws SpecAbort
 // when the compare found the host columns changed (waits for the compare)
 inline void spec_gate(st_ctx *c) {
@@ -340,9 +344,17 @@ uint64_t cluster1d_pair_dev(st_ctx *c, st_ctx *side, const float *const *a, cons
                             uint8_t *lab_b);
 
 // PLY ingest / compressed-PLY reader (st_ply.hip)
-// (after_chunk: called once each chunk's transpose is queued on c->stream, with its rows)
+// a host consumer of the PLY reader's pinned row chunks (st_ply_read's host transpose)
+struct ChunkSink {
+    virtual ~ChunkSink() = default;
+    // rows [row, row + nrows) of the element are in the pinned chunk buffer b (0 / 1): consume
+    // them asynchronously
+    virtual void take(int b, const uint8_t *rows, uint64_t row, uint64_t nrows) = 0;
+    // before buffer b is refilled: returns once the host is done with its last chunk
+    virtual void wait(int b) = 0;
+};
 void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols,
-                  const std::function<void(uint64_t row, uint64_t nrows)> &after_chunk = {});
+                  ChunkSink *sink = nullptr);
 // st_ply_read: into the caller's host columns, and the element's mirrors (st_ctx::HostMirror)
 void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols);
 void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,

@@ -17,6 +17,10 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <immintrin.h>
+#include <sys/mman.h>
+
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -304,10 +308,9 @@ void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const 
     }
 }
 
-// one element of a PLY file (fd) into device columns, streamed through pinned chunks; after_chunk
-// (if set) is called on this thread once each chunk's transpose is queued on c->stream
-void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols,
-                  const std::function<void(uint64_t row, uint64_t nrows)> &after_chunk) {
+// one element of a PLY file (fd) into device columns, streamed through pinned chunks; a sink
+// (st_ply_read) also gets every chunk on the host
+void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols, ChunkSink *sink) {
     ST_REQUIRE(element >= 0 && element < h.nelements, ST_ERR_ARG, "ply: element index out of range");
     uint64_t off = h.header_bytes;
     for (int e = 0; e < element; ++e) off += h.elements[e].count * row_bytes(h.elements[e]);
@@ -335,6 +338,7 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
             const uint64_t bytes = nr * R;
             uint8_t *hb = pin + b * (chunk_bytes + 64);
             if (pending[b]) ST_HIP(hipEventSynchronize(ev[b]));  // the copy out of hb is done
+            if (sink) sink->wait(b);                              // and the host's pass over it
             // page-cache copies are per-thread memcpy bound: several readers per chunk
             const uint64_t base = off + row * R;
             const int nt = bytes >= (8ull << 20) ? kReaders : 1;
@@ -365,7 +369,7 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
             ST_HIP(hipEventRecord(ev[b], c->stream));
             pending[b] = true;
             tp.run(stage[b], nr, row);
-            if (after_chunk) after_chunk(row, nr);
+            if (sink) sink->take(b, hb, row, nr);
             row += nr;
         }
         ST_HIP(hipStreamSynchronize(c->stream));
@@ -379,132 +383,203 @@ void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *
     (void)hipEventDestroy(ev[1]);
 }
 
-// st_ply_read: the element into device columns (ply_read_dev), and their bytes out to the
-// caller's host columns while later chunks are still read: every ~256 MiB of rows, once their
-// transpose is done, a second stream copies the columns' new rows into one pinned block (the
-// element's pinned twin, column after column) and a host thread copies them on into the caller's
-// columns -- host-to-device reads and device-to-host writes on the link at once, instead of the
-// whole element up and then the whole element down.  The device columns and the pinned twin
-// stay: they are the mirrors the writeSog host forms run on while the host columns are
-// unchanged (st_ctx::HostMirror).
-void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols) {
-    c->mirrors.clear();  // their device slots and pinned twin are overwritten below
-    const st_ply_element &el = h.elements[element];
-    const int np = el.nprops;
-    std::vector<void *> dcols(np);
-    std::vector<uint64_t> sz(np), off(np);
-    uint64_t total = 0;
-    for (int p = 0; p < np; ++p) {
-        sz[p] = (uint64_t)type_size(el.props[p].type);
-        dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * sz[p] + 8);
-        off[p] = total;
-        total += (el.count * sz[p] + 63) / 64 * 64;
+// ---- st_ply_read: the host columns transposed on the host ------------------------------------
+// The rows of every pinned chunk go up to HBM and are transposed there (ply_read_dev: the device
+// columns, kept as the mirrors of st_ctx::HostMirror), and the same pinned rows are transposed
+// into the caller's host columns by the host's copy threads while the next chunk is read -- the
+// columns never cross the link back.  A float-only element (every 3DGS PLY) moves in 8 x 8
+// blocks of AVX2 registers; other property types one value at a time.  The host transpose also
+// writes the columns' pristine twin (c->shadow) that the writeSog host forms compare against.
+namespace {
+
+struct Props {
+    std::vector<uint32_t> off, sz;  // byte offset in the row, size
+    uint32_t R = 0;
+    bool all4 = true;
+};
+
+// rows [i0, i1) of the chunk (row r of the element at chunk row r - row0) into dst (+ dst2)
+void transpose_scalar(const uint8_t *rows, uint64_t row0, uint64_t i0, uint64_t i1, const Props &P,
+                      void *const *dst, void *const *dst2) {
+    const int np = (int)P.sz.size();
+    for (uint64_t i = i0; i < i1; ++i) {
+        const uint8_t *src = rows + i * P.R;
+        const uint64_t r = row0 + i;
+        for (int p = 0; p < np; ++p) {
+            const uint32_t z = P.sz[p];
+            for (int k = 0; k < 2; ++k) {
+                void *d = k ? (dst2 ? dst2[p] : nullptr) : dst[p];
+                if (!d) continue;
+                std::memcpy(static_cast<uint8_t *>(d) + r * z, src + P.off[p], z);
+            }
+        }
     }
-    if (!el.count || !np) {
-        ply_read_dev(c, fd, h, element, dcols.data(), {});
-        return;
+}
+
+__attribute__((target("avx2"))) void transpose_f32_avx2(const uint8_t *rows, uint64_t row0, uint64_t i0, uint64_t i1,
+                                                        const Props &P, void *const *dst, void *const *dst2) {
+    const int np = (int)P.sz.size(), nb = np / 8;
+    uint64_t i = i0;
+    for (; i + 8 <= i1; i += 8) {
+        const float *src = reinterpret_cast<const float *>(rows + i * P.R);
+        const uint64_t stride = P.R / 4, r = row0 + i;
+        for (int j = 0; j < nb; ++j) {
+            const float *s0 = src + 8 * j;
+            __m256 r0 = _mm256_loadu_ps(s0), r1 = _mm256_loadu_ps(s0 + stride), r2 = _mm256_loadu_ps(s0 + 2 * stride),
+                   r3 = _mm256_loadu_ps(s0 + 3 * stride), r4 = _mm256_loadu_ps(s0 + 4 * stride),
+                   r5 = _mm256_loadu_ps(s0 + 5 * stride), r6 = _mm256_loadu_ps(s0 + 6 * stride),
+                   r7 = _mm256_loadu_ps(s0 + 7 * stride);
+            const __m256 t0 = _mm256_unpacklo_ps(r0, r1), t1 = _mm256_unpackhi_ps(r0, r1);
+            const __m256 t2 = _mm256_unpacklo_ps(r2, r3), t3 = _mm256_unpackhi_ps(r2, r3);
+            const __m256 t4 = _mm256_unpacklo_ps(r4, r5), t5 = _mm256_unpackhi_ps(r4, r5);
+            const __m256 t6 = _mm256_unpacklo_ps(r6, r7), t7 = _mm256_unpackhi_ps(r6, r7);
+            const __m256 u0 = _mm256_shuffle_ps(t0, t2, 0x44), u1 = _mm256_shuffle_ps(t0, t2, 0xEE);
+            const __m256 u2 = _mm256_shuffle_ps(t1, t3, 0x44), u3 = _mm256_shuffle_ps(t1, t3, 0xEE);
+            const __m256 u4 = _mm256_shuffle_ps(t4, t6, 0x44), u5 = _mm256_shuffle_ps(t4, t6, 0xEE);
+            const __m256 u6 = _mm256_shuffle_ps(t5, t7, 0x44), u7 = _mm256_shuffle_ps(t5, t7, 0xEE);
+            const __m256 c[8] = {_mm256_permute2f128_ps(u0, u4, 0x20), _mm256_permute2f128_ps(u1, u5, 0x20),
+                                 _mm256_permute2f128_ps(u2, u6, 0x20), _mm256_permute2f128_ps(u3, u7, 0x20),
+                                 _mm256_permute2f128_ps(u0, u4, 0x31), _mm256_permute2f128_ps(u1, u5, 0x31),
+                                 _mm256_permute2f128_ps(u2, u6, 0x31), _mm256_permute2f128_ps(u3, u7, 0x31)};
+            for (int k = 0; k < 8; ++k) {
+                _mm256_storeu_ps(static_cast<float *>(dst[8 * j + k]) + r, c[k]);
+                if (dst2) _mm256_storeu_ps(static_cast<float *>(dst2[8 * j + k]) + r, c[k]);
+            }
+        }
+        for (int p = 8 * nb; p < np; ++p)  // the last np % 8 columns
+            for (int k = 0; k < 8; ++k) {
+                const float v = src[k * stride + p];
+                static_cast<float *>(dst[p])[r + k] = v;
+                if (dst2) static_cast<float *>(dst2[p])[r + k] = v;
+            }
     }
-    auto *shadow = static_cast<uint8_t *>(pinned_slot(c, "plyh.shadow", total));
-    hipStream_t s2 = side_stream(c);
-    struct Group {
-        uint64_t row, nr;
-        hipEvent_t ev;
-    };
+    transpose_scalar(rows, row0, i, i1, P, dst, dst2);
+}
+
+bool has_avx2() {
+    static const bool yes = __builtin_cpu_supports("avx2");
+    return yes;
+}
+
+// the copy threads transpose each chunk while the reader fills the other buffer
+struct HostTranspose : ChunkSink {
+    st_ctx *c;
+    const Props &P;
+    void *const *dst;
+    void *const *dst2;
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<Group> q;
-    bool fin = false;
-    std::exception_ptr err;
-    // the drain thread: waits for a group's device-to-host copy, then copies it on
-    std::thread drain([&] {
-        try {
-            use_device(c);
-            for (;;) {
-                Group g;
-                {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return fin || !q.empty(); });
-                    if (q.empty()) return;
-                    g = q.front();
-                    q.pop_front();
-                }
-                const hipError_t e = hipEventSynchronize(g.ev);
-                (void)hipEventDestroy(g.ev);
-                ST_HIP(e);
-                for (int p = 0; p < np; ++p)
-                    host_copy(c, static_cast<char *>(host_cols[p]) + g.row * sz[p],
-                              reinterpret_cast<const char *>(shadow + off[p] + g.row * sz[p]), g.nr * sz[p]);
-            }
-        } catch (...) {
-            std::lock_guard<std::mutex> lk(mu);
-            err = std::current_exception();
-            // drop the queued groups' events (their copies are never waited for)
-            for (auto &g : q) (void)hipEventDestroy(g.ev);
-            q.clear();
-        }
-    });
-    uint64_t row_bytes_all = 0;
-    for (int p = 0; p < np; ++p) row_bytes_all += sz[p];
-    uint64_t group_rows = std::max<uint64_t>(1, (256ull << 20) / row_bytes_all);
-    if (const char *e = std::getenv("ST_PLY_D2H_ROWS")) group_rows = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
-    uint64_t g0 = 0;  // first row not yet sent down
-    auto send = [&](uint64_t upto) {
-        if (upto <= g0) return;
-        hipEvent_t ev;
-        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ST_HIP(hipEventRecord(ev, c->stream));
-        ST_HIP(hipStreamWaitEvent(s2, ev, 0));
-        ST_HIP(hipEventDestroy(ev));
-        const uint64_t nr = upto - g0;
-        for (int p = 0; p < np; ++p)
-            ST_HIP(hipMemcpyAsync(shadow + off[p] + g0 * sz[p], static_cast<char *>(dcols[p]) + g0 * sz[p], nr * sz[p],
-                                  hipMemcpyDeviceToHost, s2));
-        hipEvent_t done;
-        ST_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        ST_HIP(hipEventRecord(done, s2));
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            if (err) {
-                (void)hipEventDestroy(done);
-            } else {
-                q.push_back({g0, nr, done});
-            }
-        }
-        cv.notify_one();
-        g0 = upto;
+    struct Job {
+        int b;
+        const uint8_t *rows;
+        uint64_t row, nr;
     };
-    struct Finish {  // the drain thread ends on every path out of here
-        std::mutex &mu;
-        std::condition_variable &cv;
-        bool &fin;
-        std::thread &th;
-        hipStream_t s2;
-        ~Finish() {
+    std::deque<Job> q;
+    bool busy[2] = {false, false}, fin = false;
+    std::exception_ptr err;
+    std::thread th;
+    HostTranspose(st_ctx *ctx, const Props &p, void *const *d, void *const *d2) : c(ctx), P(p), dst(d), dst2(d2) {
+        th = std::thread([this] { loop(); });
+    }
+    void loop() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return fin || !q.empty(); });
+                if (q.empty()) return;
+                j = q.front();
+                q.pop_front();
+            }
+            try {
+                const bool vec = P.all4 && P.R == 4 * P.sz.size() && has_avx2();
+                host_parallel(c, [&](int t, int nt) {
+                    // 8-row aligned shares (the AVX2 blocks), the remainder to the last thread
+                    const uint64_t blocks = j.nr / 8, a = blocks * t / nt * 8,
+                                   e = (t == nt - 1) ? j.nr : blocks * (t + 1) / nt * 8;
+                    if (vec) transpose_f32_avx2(j.rows, j.row, a, e, P, dst, dst2);
+                    else transpose_scalar(j.rows, j.row, a, e, P, dst, dst2);
+                });
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+            }
             {
                 std::lock_guard<std::mutex> lk(mu);
-                fin = true;
+                busy[j.b] = false;
             }
-            cv.notify_one();
-            if (th.joinable()) th.join();
-            (void)hipStreamSynchronize(s2);
+            cv.notify_all();
         }
-    } finish{mu, cv, fin, drain, s2};
-    ply_read_dev(c, fd, h, element, dcols.data(), [&](uint64_t row, uint64_t nr) {
-        if (row + nr - g0 >= group_rows) send(row + nr);
-    });
-    send(el.count);
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        fin = true;
     }
-    cv.notify_one();
-    drain.join();
-    ST_HIP(hipStreamSynchronize(s2));
-    if (err) std::rethrow_exception(err);
+    void take(int b, const uint8_t *rows, uint64_t row, uint64_t nr) override {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            busy[b] = true;
+            q.push_back({b, rows, row, nr});
+        }
+        cv.notify_all();
+    }
+    void wait(int b) override {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !busy[b]; });
+    }
+    void finish() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            fin = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+    }
+    ~HostTranspose() override { finish(); }
+};
+
+}  // namespace
+
+void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols) {
+    c->mirrors.clear();  // their device slots and host twins are overwritten below
+    const st_ply_element &el = h.elements[element];
+    const int np = el.nprops;
+    Props P;
+    std::vector<void *> dcols(np), twins(np);
+    std::vector<uint64_t> toff(np);
+    uint64_t total = 0;
+    for (int p = 0; p < np; ++p) {
+        const uint32_t z = (uint32_t)type_size(el.props[p].type);
+        P.off.push_back(P.R);
+        P.sz.push_back(z);
+        P.R += z;
+        P.all4 = P.all4 && z == 4;
+        dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * z + 8);
+        toff[p] = total;
+        total += (el.count * z + 63) / 64 * 64;
+    }
     const char *mo = std::getenv("ST_HOST_MIRROR");
-    if (!(mo && std::strcmp(mo, "0") == 0))
-        for (int p = 0; p < np; ++p)
-            c->mirrors.push_back({host_cols[p], el.count * sz[p], shadow + off[p], dcols[p]});
+    const bool mirror = !(mo && std::strcmp(mo, "0") == 0) && el.count && np;
+    if (mirror && c->shadow_bytes < total) {
+        std::free(c->shadow);
+        c->shadow = nullptr;
+        c->shadow_bytes = 0;
+        const size_t huge = 2u << 20, len = (total + huge - 1) / huge * huge;
+        ST_REQUIRE(posix_memalign(&c->shadow, huge, len) == 0, ST_ERR_NOMEM, "ply: host twin allocation failed");
+        madvise(c->shadow, len, MADV_HUGEPAGE);
+        c->shadow_bytes = len;
+    }
+    for (int p = 0; p < np; ++p) twins[p] = mirror ? static_cast<uint8_t *>(c->shadow) + toff[p] : nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    {
+        HostTranspose sink(c, P, host_cols, mirror ? twins.data() : nullptr);
+        ply_read_dev(c, fd, h, element, dcols.data(), el.count ? &sink : nullptr);
+        sink.finish();
+        if (sink.err) std::rethrow_exception(sink.err);
+    }
+    if (std::getenv("ST_DEBUG"))
+        fprintf(stderr, "[st ply read] %.1f MB: device and host columns %.1f ms (%s host transpose)\n", total / 1e6,
+                std::chrono::duration<double, std::milli>(clk::now() - t0).count(),
+                P.all4 && P.R == 4 * (uint32_t)np && has_avx2() ? "AVX2" : "scalar");
+    if (mirror)
+        for (int p = 0; p < np; ++p) c->mirrors.push_back({host_cols[p], el.count * P.sz[p], twins[p], dcols[p]});
 }
 
 }  // namespace st
@@ -555,7 +630,7 @@ int st_dev_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t eleme
     return guard([&] {
         ST_REQUIRE(c && h && cols && fd >= 0, ST_ERR_ARG, "bad argument");
         use_device(c);
-        ply_read_dev(c, fd, *h, element, cols, {});
+        ply_read_dev(c, fd, *h, element, cols);
     });
 }
 

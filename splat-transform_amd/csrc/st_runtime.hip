@@ -199,6 +199,11 @@ void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes) {
     });
 }
 
+void host_parallel(st_ctx *c, const std::function<void(int, int)> &fn) {
+    if (!c->xfer_pool) c->xfer_pool = new CopyPool(XF_THREADS);
+    static_cast<CopyPool *>(c->xfer_pool)->run([&fn](int t) { fn(t, XF_THREADS); });
+}
+
 // ST_XFER_PRINT=1: bytes and rate of every staged copy on stderr
 struct XferLog {
     const char *what;
@@ -430,6 +435,7 @@ void st_ctx_destroy(st_ctx *c) {
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->archive) (void)hipHostFree(c->archive);
     if (c->io) (void)hipHostFree(c->io);
+    std::free(c->shadow);
     if (c->xfer) (void)hipHostFree(c->xfer);
     for (auto &kv : c->pinned_slots)
         if (kv.second.first) (void)hipHostFree(kv.second.first);

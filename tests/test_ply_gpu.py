@@ -68,16 +68,19 @@ def test_read_ply_vs_oracle(ctx, tmp_path, monkeypatch, n, shc, odd, chunk):
         assert wn == gn and list(wc) == list(gc)
         for k in wc:
             assert same(gc[k].cpu().numpy(), wc[k]), k
-    # the host form: its device-to-host copies overlap the later chunks' reads, in groups of rows
-    # (ST_PLY_D2H_ROWS: many ragged groups) -- every byte as the oracle's
-    for rows in (None, 7_777):
-        if rows:
-            monkeypatch.setenv('ST_PLY_D2H_ROWS', str(rows))
+    # the host form: the pinned chunks transposed on the host (AVX2 8 x 8 blocks for float-only
+    # rows, value by value otherwise) beside the device ingest, with and without the columns'
+    # host twins -- every byte as the oracle's
+    for env in (None, 'ST_HOST_MIRROR'):
+        if env:
+            monkeypatch.setenv(env, '0')
         _, got = ctx.read_ply(str(p))
+        if env:
+            monkeypatch.delenv(env)
         for (wn, wc), (gn, gc) in zip(want, got):
             assert wn == gn and list(wc) == list(gc)
             for k in wc:
-                assert same(gc[k], wc[k]), (k, rows)
+                assert same(gc[k], wc[k]), (k, env)
 
 
 def test_read_ply_truncated_file_raises(ctx, tmp_path):

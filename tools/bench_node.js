@@ -37,6 +37,11 @@ const ms = (a, b) => Number(b - a) / 1e6;
     let size = 0;
     let rows = 0;
     for (let r = 0; r <= reps; ++r) {
+        // the last rep's table is garbage: collected here (node --expose-gc), outside the timed
+        // region, its column blocks go back to the addon's pool -- every timed readPly writes
+        // into faulted-in pages, as in the rep after a collection (a CLI process reads once, into
+        // fresh pages: ~+40 ms at 10M splats)
+        if (typeof global.gc === 'function') global.gc();
         if (draws) {  // the same stream for every rep (outside the timed region)
             let i = 0;
             Math.random = () => {

@@ -25,7 +25,7 @@ with open(src, 'wb') as f:
         rows[:, 3:6] = 0
         f.write(rows.tobytes())
 env = dict(os.environ, ST_XFER_PRINT='1', ST_DEBUG='1')
-r = subprocess.run(['node', os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, '4', '10'], capture_output=True,
+r = subprocess.run(['node', '--expose-gc', os.path.join(ROOT, 'tools', 'bench_node.js'), src, dst, '4', '10'], capture_output=True,
                    text=True, env=env, timeout=600)
 print(r.stdout)
 print('\n'.join(ln for ln in r.stderr.splitlines() if ln.startswith(('[st xfer]', '[st sog file]', '[addon]'))))
