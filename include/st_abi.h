@@ -44,6 +44,8 @@
  *   st_process                              processDataTable(dataTable, actions) process.ts:64-145
  *   st_ply_compressed_ply / st_ply_sog_bundle  readPly + processDataTable + writer, resident
  *                                           (the CLI's one-input path)           index.ts:463-496
+ *   st_ply_compressed_ply_file /            the same + the output file written   write-compressed-ply.ts:31-115,
+ *   st_compressed_ply_file                  at offsets as it leaves HBM          index.ts:101-154
  *   st_compressed_ply / st_dev_...          processDataTable + writeCompressedPly
  *                                           (CLI: in.ply [actions] out.compressed.ply) index.ts:463-496,
  *                                                                               write-compressed-ply.ts:31-115
@@ -303,6 +305,22 @@ int st_dev_compressed_ply(st_ctx *ctx, const st_ttable *src, const st_action *ac
 int st_ply_compressed_ply(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
                           int32_t nactions, float *chunk, uint32_t *vertex, uint8_t *sh, uint64_t *out_m,
                           int32_t *out_sh_coeffs);
+/* writeCompressedPly into a file (write-compressed-ply.ts:31-115 and the CLI's write of the
+ * output, index.ts:101-154): st_ply_compressed_ply / st_compressed_ply's chain, then the header
+ * (the reference's text, "comment Generated by splat-transform <version>"; version NULL =
+ * "0.10.1") and the chunk / vertex / sh arrays written to out_fd at offsets from its current
+ * position (where the reference's FileHandle.write calls would go; the CLI's fresh output: 0)
+ * as they come down from HBM through pinned slots (a host thread writes one slot while the next
+ * one copies); the descriptor's position ends after the output and a longer file is cut there,
+ * so a reused output needs no O_TRUNC.  out_fd must be a seekable descriptor open for writing
+ * and not O_APPEND (ST_ERR_ARG before any work).  *size = the bytes written.
+ * st_compressed_ply_file takes a host table (uploaded once). */
+int st_ply_compressed_ply_file(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element,
+                               const st_action *actions, int32_t nactions, int32_t out_fd, const char *version,
+                               uint64_t *out_m, int32_t *out_sh_coeffs, uint64_t *size);
+int st_compressed_ply_file(st_ctx *ctx, const st_ttable *src, const st_action *actions, int32_t nactions,
+                           int32_t out_fd, const char *version, uint64_t *out_m, int32_t *out_sh_coeffs,
+                           uint64_t *size);
 int st_ply_sog_bundle(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, const st_action *actions,
                       int32_t nactions, int32_t iters, const double *draws, uint64_t ndraws, uint64_t *used,
                       uint16_t dos_time, uint16_t dos_date, uint8_t **out, uint64_t *out_size);

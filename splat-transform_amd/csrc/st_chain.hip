@@ -7,8 +7,15 @@
 // updates float32 columns in place; a filter gathers the survivors into the other of two
 // workspace generations (ping-pong), so a long action list needs at most two copies of the
 // table beside the input.
+#include <unistd.h>
+
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
+#include <mutex>
+#include <thread>
 
 #include "st_internal.h"
 #include "st_typed.h"
@@ -257,6 +264,140 @@ st_sog_textures sog_textures(st_ctx *c, uint64_t n, int C, uint64_t *tex_bytes, 
 
 
 
+// ---- writeCompressedPly into a file (write-compressed-ply.ts:31-115 + the CLI's write) --------
+// the header text of write-compressed-ply.ts:35-54
+std::string compressed_ply_header(uint64_t m, int C, const char *version) {
+    static const char *chunk_props[18] = {"min_x", "min_y", "min_z", "max_x", "max_y", "max_z",
+                                          "min_scale_x", "min_scale_y", "min_scale_z", "max_scale_x", "max_scale_y",
+                                          "max_scale_z", "min_r", "min_g", "min_b", "max_r", "max_g", "max_b"};
+    static const char *vertex_props[4] = {"packed_position", "packed_rotation", "packed_scale", "packed_color"};
+    std::string h = "ply\nformat binary_little_endian 1.0\ncomment Generated by splat-transform ";
+    h += (version && *version) ? version : "0.10.1";
+    h += "\nelement chunk " + std::to_string((m + 255) / 256) + "\n";
+    for (auto *p : chunk_props) h += std::string("property float ") + p + "\n";
+    h += "element vertex " + std::to_string(m) + "\n";
+    for (auto *p : vertex_props) h += std::string("property uint ") + p + "\n";
+    if (C) {
+        h += "element sh " + std::to_string(m) + "\n";
+        for (int i = 0; i < 3 * C; ++i) h += "property uchar f_rest_" + std::to_string(i) + "\n";
+    }
+    return h + "end_header\n";
+}
+
+// the device arrays to fd at offsets from its position: pinned slots filled by device-to-host copies on
+// the context's stream while a host thread writes the slot before (ext4 / xfs serialise buffered
+// writes to one file, so one writer); the file ends at the last byte
+uint64_t compressed_ply_to_file(st_ctx *c, uint64_t m, int C, const float *dchunk, const uint32_t *dvert,
+                                const uint8_t *dsh, int fd, const char *version) {
+    const std::string head = compressed_ply_header(m, C, version);
+    // from the descriptor's position, as the reference's FileHandle.write calls go (the CLI's
+    // fresh output: 0), which is left at the end of what was written
+    const off_t pos = lseek(fd, 0, SEEK_CUR);
+    ST_REQUIRE(pos >= 0, ST_ERR_ARG, "compressed ply file: the descriptor has no position");
+    const uint64_t base = (uint64_t)pos;
+    write_at(fd, reinterpret_cast<const uint8_t *>(head.data()), head.size(), base);
+    const uint64_t nch = (m + 255) / 256;
+    struct Region {
+        const uint8_t *dev;
+        uint64_t bytes, off;
+    };
+    std::vector<Region> rs;
+    uint64_t off = base + head.size();
+    for (const Region &r : {Region{reinterpret_cast<const uint8_t *>(dchunk), nch * 72, 0},
+                            Region{reinterpret_cast<const uint8_t *>(dvert), m * 16, 0},
+                            Region{dsh, C ? m * 3 * (uint64_t)C : 0, 0}}) {
+        if (r.bytes) rs.push_back({r.dev, r.bytes, off});
+        off += r.bytes;
+    }
+    const uint64_t total = off;
+    constexpr int SLOTS = 4;
+    uint64_t slot = 32ull << 20;
+    if (const char *e = std::getenv("ST_CPF_SLOT_MB")) slot = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    auto *ring = static_cast<uint8_t *>(pinned_slot(c, "cpf.ring", SLOTS * slot));
+    struct Piece {
+        int s;
+        uint64_t bytes, off;
+        hipEvent_t ev;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Piece> q;
+    bool busy[SLOTS] = {}, fin = false;
+    std::exception_ptr err;
+    std::thread writer([&] {
+        for (;;) {
+            Piece p;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return fin || !q.empty(); });
+                if (q.empty()) return;
+                p = q.front();
+                q.pop_front();
+            }
+            try {
+                const hipError_t e = hipEventSynchronize(p.ev);
+                (void)hipEventDestroy(p.ev);
+                ST_HIP(e);
+                bool skip;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    skip = (bool)err;
+                }
+                if (!skip) write_at(fd, ring + p.s * slot, p.bytes, p.off);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err) err = std::current_exception();
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                busy[p.s] = false;
+            }
+            cv.notify_all();
+        }
+    });
+    auto stop = [&] {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            fin = true;
+        }
+        cv.notify_all();
+        if (writer.joinable()) writer.join();
+    };
+    try {
+        int k = 0;
+        for (const Region &r : rs)
+            for (uint64_t o = 0; o < r.bytes; o += slot, ++k) {
+                const int sidx = k % SLOTS;
+                const uint64_t nb = std::min(slot, r.bytes - o);
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return !busy[sidx] || err; });
+                    if (err) break;
+                    busy[sidx] = true;
+                }
+                hipEvent_t ev;
+                ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                ST_HIP(hipMemcpyAsync(ring + sidx * slot, r.dev + o, nb, hipMemcpyDeviceToHost, c->stream));
+                ST_HIP(hipEventRecord(ev, c->stream));
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    q.push_back({sidx, nb, r.off + o, ev});
+                }
+                cv.notify_all();
+            }
+    } catch (...) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
+    }
+    stop();
+    if (err) std::rethrow_exception(err);
+    sog_file_truncate(fd, total);
+    ST_REQUIRE(lseek(fd, (off_t)total, SEEK_SET) == (off_t)total, ST_ERR_ARG, "compressed ply file: lseek failed");
+    return total - base;
+}
+
 #define ST_REQUIRE_RC(cond, msg)           \
     do {                                   \
         if (!(cond)) {                     \
@@ -461,6 +602,52 @@ int st_ply_compressed_ply(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t
             if (C) down.push_back(HostXfer{sh, dsh, m * 3 * (uint64_t)C});
         }
         staged_d2h(c, down);
+        *out_m = m;
+        *out_sh_coeffs = C;
+    });
+}
+
+int st_ply_compressed_ply_file(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element,
+                               const st_action *actions, int32_t nactions, int32_t out_fd, const char *version,
+                               uint64_t *out_m, int32_t *out_sh_coeffs, uint64_t *size) {
+    return guard([&] {
+        ST_REQUIRE(c && h && fd >= 0 && out_m && out_sh_coeffs && size && (actions || nactions == 0), ST_ERR_ARG,
+                   "NULL argument");
+        sog_file_check(out_fd);
+        use_device(c);
+        Chain ch{c};
+        ply_chain(c, fd, h, element, ch);
+        run_actions(ch, actions, nactions);
+        const uint64_t m = ch.n, nch = (m + 255) / 256;
+        auto *dchunk = wsT<float>(c, "chain.chunk", nch * 18);
+        auto *dvert = wsT<uint32_t>(c, "chain.vert", m * 4);
+        auto *dsh = wsT<uint8_t>(c, "chain.sh", m * 3 * (uint64_t)band_coeffs(ch.cols) + 1);
+        int32_t C = 0;
+        compressed_tail(ch, dchunk, dvert, dsh, &C);
+        *size = compressed_ply_to_file(c, m, C, dchunk, dvert, dsh, out_fd, version);
+        *out_m = m;
+        *out_sh_coeffs = C;
+    });
+}
+
+int st_compressed_ply_file(st_ctx *c, const st_ttable *src, const st_action *actions, int32_t nactions, int32_t out_fd,
+                           const char *version, uint64_t *out_m, int32_t *out_sh_coeffs, uint64_t *size) {
+    return guard([&] {
+        ST_REQUIRE(c && src && out_m && out_sh_coeffs && size && (actions || nactions == 0), ST_ERR_ARG,
+                   "NULL argument");
+        check_src(src);
+        sog_file_check(out_fd);
+        use_device(c);
+        Chain ch{c};
+        upload_chain(c, src, ch);
+        run_actions(ch, actions, nactions);
+        const uint64_t m = ch.n, nch = (m + 255) / 256;
+        auto *dchunk = wsT<float>(c, "chain.chunk", nch * 18);
+        auto *dvert = wsT<uint32_t>(c, "chain.vert", m * 4);
+        auto *dsh = wsT<uint8_t>(c, "chain.sh", m * 3 * (uint64_t)band_coeffs(ch.cols) + 1);
+        int32_t C = 0;
+        compressed_tail(ch, dchunk, dvert, dsh, &C);
+        *size = compressed_ply_to_file(c, m, C, dchunk, dvert, dsh, out_fd, version);
         *out_m = m;
         *out_sh_coeffs = C;
     });

@@ -14,7 +14,8 @@
 //   packCompressed(dataTable)               write-compressed-ply.ts:56-109 (the chunk loop)
 //   processDataTable(dataTable, actions)    process.ts:64-145 (one upload for the whole list)
 //   writeCompressedPly(fh, dataTable[, actions])  write-compressed-ply.ts:31-115 (actions first,
-//                                           same device call: the CLI's config-3 path)
+//                                           same device call: the CLI's config-3 path; a real
+//                                           FileHandle is written as the arrays leave HBM)
 //   compressPlyFile(inFh, outFh, actions)   readPly + processDataTable + writeCompressedPly, the rows
 //   sogFromPlyFile(inFh, actions, iters)    resident in HBM (the CLI's one-input paths, index.ts:463-496)
 //   kmeans(points, k, iterations)           k-means.ts:137-201 (--no-gpu results)
@@ -302,7 +303,16 @@ const VERTEX_PROPS_OUT = ['packed_position', 'packed_rotation', 'packed_scale', 
 // write-compressed-ply.ts:31-115: header + chunk + vertex + sh writes.  With processActions the
 // actions run first in the same device call (the CLI's `in.ply [actions] out.compressed.ply`:
 // the table crosses PCIe once each way).  version: the package version of the header comment.
+// A real fs.promises FileHandle (a numeric fd) takes the streamed form: the library writes the
+// header and the arrays at the handle's position as they leave HBM (st_compressed_ply_file) and
+// leaves the position after them; any other handle gets the reference's four write() calls.
+const hasFd = h => h && typeof h.fd === 'number' && h.fd >= 0;
 const writeCompressedPly = async (fileHandle, dataTable, processActions, version) => {
+    if (hasFd(fileHandle)) {
+        addon.compressedPlyTableToFile(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+            normaliseActions(processActions || []), fileHandle.fd, version || '0.10.1');
+        return;
+    }
     const res = addon.compressedPly(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
         normaliseActions(processActions || []));
     await fileHandle.write(Buffer.from(compressedPlyHeader(res.numRows, res.shCoeffs, version), 'utf8'));
@@ -325,6 +335,11 @@ const compressedPlyHeader = (numSplats, outputSHCoeffs, version) => {
 };
 
 const compressPlyFile = async (inHandle, outHandle, processActions, version) => {
+    if (hasFd(outHandle)) {  // streamed into the file as the arrays leave HBM (st_ply_compressed_ply_file)
+        addon.compressedPlyToFile(inHandle.fd, normaliseActions(processActions || []), outHandle.fd,
+            version || '0.10.1');
+        return;
+    }
     const res = addon.compressedPlyFromFile(inHandle.fd, normaliseActions(processActions || []));
     await outHandle.write(Buffer.from(compressedPlyHeader(res.numRows, res.shCoeffs, version), 'utf8'));
     await outHandle.write(new Uint8Array(res.chunk.buffer));

@@ -42,6 +42,11 @@
  *   compressedPlyFromFile(fd, actions)        readPly + processDataTable + writeCompressedPly's
  *        -> {numRows, shCoeffs, chunk,        arrays, the rows resident in HBM (index.ts:463-496)
  *            vertex, sh}
+ *   compressedPlyToFile(inFd, actions,        readPly + processDataTable + writeCompressedPly into
+ *        outFd, version) -> {numRows,         outFd, written as the arrays leave HBM
+ *        shCoeffs, size}                      (st_ply_compressed_ply_file)
+ *   compressedPlyTableToFile(cols, names,     processDataTable + writeCompressedPly of a host table
+ *        actions, outFd, version)             into outFd (st_compressed_ply_file)
  *   sogBundleFromFile(fd, actions, iters,     readPly + processDataTable + writeSog -> .sog bytes,
  *        draws, dosTime, dosDate)             resident
  *        -> {archive, used}
@@ -718,6 +723,94 @@ static napi_value js_compressed_ply_file(napi_env env, napi_callback_info info) 
     return out;
 fail:
     free(chunk); free(vertex); free(sh); free(h);
+    chain_free(&a);
+    return NULL;
+}
+
+/* compressedPlyToFile(inFd, actions, outFd, version) -> {numRows, shCoeffs, size}: readPly +
+ * processDataTable + writeCompressedPly into outFd (st_ply_compressed_ply_file: the arrays written
+ * at offsets as they leave HBM) */
+static napi_value js_compressed_ply_to_file(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4], out = NULL;
+    chain_args a;
+    st_ctx *ctx;
+    st_ply_header *h = NULL;
+    char *version = NULL;
+    memset(&a, 0, sizeof a);
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (napi_get_array_length(env, argv[1], &a.na) != napi_ok || !parse_actions(env, argv[1], &a)) goto fail;
+    if (argc > 3 && !(version = dup_str(env, argv[3], "splat-hip: version must be a string"))) goto fail;
+    if (!get_ctx(env, &ctx)) goto fail;
+    h = (st_ply_header *)calloc(1, sizeof *h);
+    {
+        const int32_t fd = (int32_t)num(env, argv[0]), ofd = (int32_t)num(env, argv[2]);
+        int rc = st_ply_read_header(fd, h), el = -1;
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        for (int e = 0; e < h->nelements && el < 0; ++e)
+            if (strcmp(h->elements[e].name, "vertex") == 0) el = e;
+        if (el < 0) {
+            napi_throw_error(env, NULL, "splat-hip: no vertex element");
+            goto fail;
+        }
+        uint64_t m = 0, size = 0;
+        int32_t C = 0;
+        rc = st_ply_compressed_ply_file(ctx, fd, h, el, a.acts, (int32_t)a.na, ofd, version, &m, &C, &size);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "numRows", make_num(env, (double)m));
+        set_named(env, out, "shCoeffs", make_num(env, C));
+        set_named(env, out, "size", make_num(env, (double)size));
+    }
+    free(h);
+    free(version);
+    chain_free(&a);
+    return out;
+fail:
+    free(h);
+    free(version);
+    chain_free(&a);
+    return NULL;
+}
+
+/* compressedPlyTableToFile(columns, names, actions, outFd, version) -> {numRows, shCoeffs, size}:
+ * processDataTable + writeCompressedPly of a host table into outFd (st_compressed_ply_file) */
+static napi_value js_compressed_ply_table_to_file(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5], out = NULL;
+    chain_args a;
+    st_ctx *ctx;
+    char *version = NULL;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (!chain_parse(env, argv[0], argv[1], argv[2], &a)) goto fail;
+    if (argc > 4 && !(version = dup_str(env, argv[4], "splat-hip: version must be a string"))) goto fail;
+    if (!get_ctx(env, &ctx)) goto fail;
+    {
+        st_ttable ts = {a.n, (int32_t)a.m, (const char *const *)a.names, a.types, a.cols};
+        uint64_t m = 0, size = 0;
+        int32_t C = 0;
+        const int rc = st_compressed_ply_file(ctx, &ts, a.acts, (int32_t)a.na, (int32_t)num(env, argv[3]), version,
+                                              &m, &C, &size);
+        if (rc != ST_OK) {
+            throw_st(env, rc);
+            goto fail;
+        }
+        if (napi_create_object(env, &out) != napi_ok) goto fail;
+        set_named(env, out, "numRows", make_num(env, (double)m));
+        set_named(env, out, "shCoeffs", make_num(env, C));
+        set_named(env, out, "size", make_num(env, (double)size));
+    }
+    free(version);
+    chain_free(&a);
+    return out;
+fail:
+    free(version);
     chain_free(&a);
     return NULL;
 }
@@ -1626,6 +1719,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"decompressPly", js_decompress_ply},
                {"compressedPly", js_compressed_ply},
                {"compressedPlyFromFile", js_compressed_ply_file},
+               {"compressedPlyToFile", js_compressed_ply_to_file},
+               {"compressedPlyTableToFile", js_compressed_ply_table_to_file},
                {"sogBundleFromFile", js_sog_bundle_file},
                {"process", js_process},
                {"sogProcess", js_sog_process},

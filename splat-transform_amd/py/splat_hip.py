@@ -102,7 +102,8 @@ EXPORTS = [
     'st_dev_transform', 'st_dev_filter_finite', 'st_dev_permute_rows', 'st_dev_concat_rows', 'st_dev_morton_order',
     'st_dev_pack_compressed', 'st_dev_kmeans', 'st_dev_cluster1d', 'st_dev_sog',
     'st_set_devices', 'st_get_devices', 'st_comm_unique_id', 'st_comm_init_rank', 'st_comm_init_host', 'st_comm_destroy',
-    'st_comm_count', 'st_rccl_info', 'st_ctx_last_host_reuse',
+    'st_comm_count', 'st_rccl_info', 'st_ctx_last_host_reuse', 'st_ply_compressed_ply_file',
+    'st_compressed_ply_file',
     'st_dev_sog_sharded', 'st_group_create', 'st_group_destroy', 'st_group_sog', 'st_group_sog_bundle',
     'st_filter_nan', 'st_dev_filter_finite_t', 'st_dev_permute_rows_t', 'st_combine_layout', 'st_dev_combine',
     'st_dev_minmax', 'st_dev_kmeans_init_rows', 'st_dev_gather_rows', 'st_dev_kmeans_prepare',
@@ -974,6 +975,45 @@ class Context:
             os.close(fd)
         m, C = m.value, C.value
         return m, chunk[:(m + 255) // 256 * 18], vertex[:m * 4], sh[:m * 3 * C]
+
+    def ply_compressed_ply_file(self, path, actions, out_path, version=None, element=-1):
+        """readPly + processDataTable + writeCompressedPly into out_path (st_ply_compressed_ply_file:
+        the arrays written at offsets as they leave HBM; the file opened without O_TRUNC, cut to
+        length by the library): (m, sh_coeffs, file bytes)"""
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = PlyHeader()
+            check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+            acts = make_actions(actions)
+            m, C, size = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_uint64()
+            ofd = os.open(out_path, os.O_WRONLY | os.O_CREAT, 0o644)
+            try:
+                check(lib().st_ply_compressed_ply_file(self.h, ctypes.c_int32(fd), ctypes.byref(h),
+                                                       ctypes.c_int32(element), acts, ctypes.c_int32(len(actions)),
+                                                       ctypes.c_int32(ofd), version.encode() if version else None,
+                                                       ctypes.byref(m), ctypes.byref(C), ctypes.byref(size)))
+            finally:
+                os.close(ofd)
+        finally:
+            os.close(fd)
+        return m.value, C.value, size.value
+
+    def compressed_ply_file(self, cols, actions, out_path, version=None):
+        """processDataTable + writeCompressedPly of a host table into out_path (st_compressed_ply_file):
+        (m, sh_coeffs, file bytes)"""
+        items = list(cols.items()) if isinstance(cols, dict) else list(cols)
+        n = len(items[0][1]) if items else 0
+        ts = make_ttable(items, n)
+        acts = make_actions(actions)
+        m, C, size = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_uint64()
+        ofd = os.open(out_path, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            check(lib().st_compressed_ply_file(self.h, ctypes.byref(ts), acts, ctypes.c_int32(len(actions)),
+                                               ctypes.c_int32(ofd), version.encode() if version else None,
+                                               ctypes.byref(m), ctypes.byref(C), ctypes.byref(size)))
+        finally:
+            os.close(ofd)
+        return m.value, C.value, size.value
 
     def ply_sog_bundle(self, path, actions, iters, draws, dos_time, dos_date, element=-1):
         """readPly + processDataTable + writeSog to .sog bytes from the file (st_ply_sog_bundle):

@@ -58,9 +58,27 @@ const tableOf = c => new host.DataTable(man.meta[`${c}_in_columns`].map(n => new
         await host.compressPlyFile(inH, { write: async (d) => { w3.push(Buffer.from(d.buffer, d.byteOffset, d.byteLength)); } },
             actionsOf(c));
         await inH.close();
+        r.file = w3.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => w3[i].equals(bytes(arr(`${c}_${k}`))));
+        // real FileHandles: the streamed writers (the arrays written at offsets as they leave HBM),
+        // into a file that held longer content and at a handle position past 0
+        const want = Buffer.concat(['header', 'chunk', 'vertex', 'sh'].map(k => bytes(arr(`${c}_${k}`))));
+        const inH2 = await fs.promises.open(path.join(dir, 'in.ply'), 'r');
+        const outP = path.join(dir, 'out.compressed.ply');
+        fs.writeFileSync(outP, Buffer.alloc(want.length + 4096, 7));
+        let oh = await fs.promises.open(outP, fs.constants.O_WRONLY);
+        await host.compressPlyFile(inH2, oh, actionsOf(c));
+        await oh.close();
+        await inH2.close();
+        r.fileFd = fs.readFileSync(outP).equals(want);
+        oh = await fs.promises.open(outP, 'w');
+        await oh.write(Buffer.from('prefix'));
+        await host.writeCompressedPly(oh, tableOf(c), actionsOf(c));
+        await oh.write(Buffer.from('suffix'));
+        await oh.close();
+        r.tableFd = fs.readFileSync(outP).equals(Buffer.concat([Buffer.from('prefix'), want, Buffer.from('suffix')]));
+        fs.unlinkSync(outP);
         fs.unlinkSync(path.join(dir, 'in.ply'));
         fs.rmdirSync(dir);
-        r.file = w3.length === 4 && ['header', 'chunk', 'vertex', 'sh'].every((k, i) => w3[i].equals(bytes(arr(`${c}_${k}`))));
         out[c] = r;
     }
     console.log(JSON.stringify(out));

@@ -42,7 +42,8 @@ def test_addon_exports(addon_built):
                                        'webpLossless', 'sogBundle', 'readPly', 'decompressPly', 'compressedPly',
                                        'process', 'compressedPlyFromFile', 'sogBundleFromFile',
                                        'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped',
-                                       'sogFile', 'rcclInfo', 'lastHostReuse'])
+                                       'sogFile', 'rcclInfo', 'lastHostReuse', 'compressedPlyToFile',
+                                       'compressedPlyTableToFile'])
     assert ver == '1'
 
 

@@ -126,3 +126,55 @@ def test_pack_then_decompress_large_vs_oracle(ctx):
                            out)
     for k in want:
         assert same(out[k].cpu().numpy(), want[k]), k
+
+
+@pytest.mark.parametrize('slot_mb', [None, '1'])
+def test_compressed_ply_file_equals_the_arrays(ctx, tmp_path, monkeypatch, slot_mb):
+    """st_ply_compressed_ply_file / st_compressed_ply_file (the CLI's `in.ply -r 0,45,0 --filterNaN
+    out.compressed.ply`, write-compressed-ply.ts:31-115): the file is the reference's header + the
+    chunk / vertex / sh arrays of the one-call form, byte for byte -- into a file that held longer
+    content, with 1 MiB slots too (many pieces through the ring)"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tools'))
+    import bench_paths
+    if slot_mb:
+        monkeypatch.setenv('ST_CPF_SLOT_MB', slot_mb)
+    n = 300_001
+    data = bytearray(_gs_file(n, 15, 11))
+    src = tmp_path / 'in.ply'
+    src.write_bytes(bytes(data))
+    _, els = ctx.read_ply(str(src))
+    cols = dict(els)['vertex']
+    cols['x'][::997] = np.nan  # rows filterNaN drops
+    src.write_bytes(data[:data.index(b'end_header\n') + 11] + np.stack(list(cols.values()), 1).astype('<f4').tobytes())
+    acts = [{'kind': 'rotate', 'value': (0, 45, 0)}, {'kind': 'filterNaN'}]
+    m, chunk, vertex, shb = ctx.ply_compressed_ply(str(src), acts)
+    want = bench_paths.compressed_ply_header(m, 15) + chunk.tobytes() + vertex.tobytes() + shb.tobytes()
+    out = tmp_path / 'out.compressed.ply'
+    out.write_bytes(b'\x07' * (len(want) + 12345))
+    mm, C, size = ctx.ply_compressed_ply_file(str(src), acts, str(out))
+    assert (mm, C, size) == (m, 15, len(want)) and m < n
+    assert out.read_bytes() == want
+    mm, C, size = ctx.compressed_ply_file(list(cols.items()), acts, str(out), version='9.9.9')
+    assert out.read_bytes() == want.replace(b'splat-transform 0.10.1', b'splat-transform 9.9.9')
+
+
+def test_compressed_ply_file_refuses_append(ctx, tmp_path):
+    src = tmp_path / 'in.ply'
+    src.write_bytes(_gs_file(1000, 0, 3))
+    out = tmp_path / 'o.ply'
+    out.write_bytes(b'keep')
+    import ctypes
+    fd, ofd = os.open(str(src), os.O_RDONLY), os.open(str(out), os.O_WRONLY | os.O_APPEND)
+    try:
+        h = sh.PlyHeader()
+        sh.check(sh.lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
+        m, C, size = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_uint64()
+        rc = sh.lib().st_ply_compressed_ply_file(ctx.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(-1), None,
+                                                 ctypes.c_int32(0), ctypes.c_int32(ofd), None, ctypes.byref(m),
+                                                 ctypes.byref(C), ctypes.byref(size))
+    finally:
+        os.close(fd)
+        os.close(ofd)
+    assert rc == sh.ST_ERR_ARG and b'O_APPEND' in sh.lib().st_last_error()
+    assert out.read_bytes() == b'keep'

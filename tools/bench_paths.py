@@ -152,16 +152,42 @@ def measure(ctx, stream, dev, n=10_000_000, reps=5):
     return out
 
 
-def file_path(ctx, host, acts, ref, reps=2):
-    """the CLI's `in.ply -r 0,45,0 --filterNaN out.compressed.ply` from the file in one resident
-    call (st_ply_compressed_ply: page cache -> pinned -> HBM, the chain, the packed arrays back),
-    plus writing the output file; the table written once as a binary PLY (untimed)"""
+CHUNK_PROPS = ['min_x', 'min_y', 'min_z', 'max_x', 'max_y', 'max_z', 'min_scale_x', 'min_scale_y', 'min_scale_z',
+               'max_scale_x', 'max_scale_y', 'max_scale_z', 'min_r', 'min_g', 'min_b', 'max_r', 'max_g', 'max_b']
+VERTEX_PROPS = ['packed_position', 'packed_rotation', 'packed_scale', 'packed_color']
+
+
+def compressed_ply_header(m, C, version='0.10.1'):
+    """write-compressed-ply.ts:35-54's header text"""
+    lines = ['ply', 'format binary_little_endian 1.0', f'comment Generated by splat-transform {version}',
+             f'element chunk {(m + 255) // 256}'] + [f'property float {p}' for p in CHUNK_PROPS] + \
+        [f'element vertex {m}'] + [f'property uint {p}' for p in VERTEX_PROPS]
+    if C:
+        lines += [f'element sh {m}'] + [f'property uchar f_rest_{i}' for i in range(3 * C)]
+    return ('\n'.join(lines + ['end_header']) + '\n').encode()
+
+
+def file_path(ctx, host, acts, ref, reps=3):
+    """the CLI's `in.ply -r 0,45,0 --filterNaN out.compressed.ply` from the file to the file:
+    st_ply_compressed_ply_file (page cache -> pinned -> HBM, the chain, the arrays written at their
+    offsets as they leave HBM), each rep into a FRESH output file (the reference's CLI writes a new
+    'wx' file, index.ts:107-112); and the same job through the Node drop-in host
+    (tools/bench_node_c3.js: compressPlyFile(inHandle, outHandle, actions) over the addon).  The
+    table is written once as a binary PLY (untimed); every output file must equal the reference's
+    header + the host one-call arrays byte for byte"""
+    import hashlib
+    import shutil
+    import subprocess
     import tempfile
 
     import numpy as np
     n = len(host[0][1])
+    m, chunk, vertex, shb = ref
+    C = shb.size // max(1, 3 * m)
+    want = compressed_ply_header(m, C) + chunk.tobytes() + vertex.tobytes() + shb.tobytes()
+    want_sha = hashlib.sha256(want).hexdigest()
     d = tempfile.mkdtemp(prefix='st_c3_', dir=os.environ.get('TMPDIR', '/tmp'))
-    src, dst = os.path.join(d, 'in.ply'), os.path.join(d, 'out.compressed.ply')
+    src = os.path.join(d, 'in.ply')
     try:
         head = ('ply\nformat binary_little_endian 1.0\n' + f'element vertex {n}\n' +
                 ''.join(f'property float {k}\n' for k, _ in host) + 'end_header\n').encode()
@@ -170,32 +196,39 @@ def file_path(ctx, host, acts, ref, reps=2):
             step = 1 << 22
             for a in range(0, n, step):
                 f.write(np.stack([v[a:a + step] for _, v in host], 1).tobytes())
-        times, calls, same = [], [], True
+        times, same = [], True
         for r in range(reps + 1):  # rep 0 warms the page cache and the buffers
+            dst = os.path.join(d, f'out{r}.compressed.ply')
             t0 = time.perf_counter()
-            m, chunk, vertex, shb = ctx.ply_compressed_ply(src, acts)
-            tc = time.perf_counter() - t0
-            with open(dst, 'wb') as f:
-                f.write(b'ply header\n')  # the header text is the host's (a few hundred bytes)
-                f.write(chunk.tobytes())
-                f.write(vertex.tobytes())
-                f.write(shb.tobytes())
+            mm, CC, size = ctx.ply_compressed_ply_file(src, acts, dst)
+            t1 = time.perf_counter()
             if r:
-                times.append(time.perf_counter() - t0)
-                calls.append(tc)
-            same = same and m == ref[0] and all(np.array_equal(a.view(np.uint8), b.view(np.uint8))
-                                                for a, b in zip((chunk, vertex, shb), ref[1:]))
+                times.append(t1 - t0)
+            same = same and mm == m and CC == C and size == len(want) and \
+                hashlib.sha256(open(dst, 'rb').read()).hexdigest() == want_sha
+            os.remove(dst)
         ms = sorted(times)[len(times) // 2] * 1e3
-        mc = sorted(calls)[len(calls) // 2] * 1e3
-        return {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'call_ms': mc, 'call_Msplats_per_s': n / mc / 1e3,
-                'ply_bytes': os.path.getsize(src),
-                'equals_host_one_call': same,
-                'what': 'st_ply_compressed_ply from a PLY file in the page cache + the output file written'}
+        out = {'ms': ms, 'Msplats_per_s': n / (ms / 1e3) / 1e6, 'reps': reps, 'ply_bytes': os.path.getsize(src),
+               'out_bytes': len(want), 'equals_host_one_call': same,
+               'what': 'st_ply_compressed_ply_file: PLY file (page cache) -> HBM -> rotate + filterNaN + Morton + '
+                       'chunk pack -> a fresh .compressed.ply written at offsets as the arrays leave HBM'}
+        node = shutil.which('node')
+        addon = os.path.join(ROOT, 'splat-transform_amd', 'napi', 'build', 'addon.node')
+        if node and os.path.exists(addon):
+            r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node_c3.js'), src, d, str(reps)],
+                               capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                out['node_host'] = {'error': r.stderr[-2000:]}
+            else:
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+                nms = sorted(res['ms'])[len(res['ms']) // 2]
+                out['node_host'] = {'ms': nms, 'Msplats_per_s': n / (nms / 1e3) / 1e6, 'reps': len(res['ms']),
+                                    'equals_host_one_call': all(h == want_sha for h in res['sha256']),
+                                    'what': 'node tools/bench_node_c3.js: compressPlyFile(inHandle, outHandle '
+                                            "('wx', fresh), [rotate 0,45,0, filterNaN]) over napi/addon.node"}
+        return out
     finally:
-        for f in (src, dst):
-            if os.path.exists(f):
-                os.remove(f)
-        os.rmdir(d)
+        shutil.rmtree(d, ignore_errors=True)
 
 
 if __name__ == '__main__':
