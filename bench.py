@@ -335,6 +335,36 @@ def cpu_baseline(args):
     }, all_cores
 
 
+def realistic_table(n, seed, device, zero_frac=0.3, clumps=20_000, clump_frac=0.8):
+    """north_star's table shape with the distributions trained scenes bring:
+    SH rows heavy-tailed and correlated -- Student-t (nu = 3) through a fixed mixing matrix, the
+    t3 rows of tests/test_gpu_parity.py -- with `zero_frac` of them all zero (splats whose SH
+    never trained: exact duplicates), and `clump_frac` of the positions in `clumps` tight clumps
+    (Morton recursion, equal keys).  The other columns as synth_table."""
+    import torch
+    cols = synth_table(n, seed, device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 7)
+    f = dict(device=device, dtype=torch.float32)
+    cid = torch.randint(0, clumps, (n,), generator=g, device=device)
+    inclump = torch.rand(n, generator=g, **f) < clump_frac
+    for a in 'xyz':
+        centre = torch.randn(clumps, generator=g, **f) * 10
+        cols[a] = torch.where(inclump, centre[cid] + torch.randn(n, generator=g, **f) * 1e-3, cols[a]).contiguous()
+    D = 45
+    m = torch.eye(D, device=device) + 0.5 * torch.randn(D, D, generator=g, **f) / D ** 0.5
+    zero = torch.rand(n, generator=g, **f) < zero_frac
+    for a in range(0, n, 1 << 21):
+        b = min(n, a + (1 << 21))
+        t = torch.randn(b - a, D, generator=g, **f)
+        chi = (torch.randn(b - a, 3, generator=g, **f) ** 2).sum(1, keepdim=True) / 3
+        sh = (t / chi.sqrt()) @ m.T * 0.1
+        sh[zero[a:b]] = 0
+        for i in range(D):
+            cols[f'f_rest_{i}'][a:b] = sh[:, i]
+    return cols
+
+
 PLY_ORDER = (['x', 'y', 'z', 'nx', 'ny', 'nz', 'f_dc_0', 'f_dc_1', 'f_dc_2'] + [f'f_rest_{i}' for i in range(45)] +
              ['opacity', 'scale_0', 'scale_1', 'scale_2', 'rot_0', 'rot_1', 'rot_2', 'rot_3'])
 
@@ -993,6 +1023,22 @@ def main(args):
                                             textures_equal_main=sha1 == main_sha, parallelism='rowshard1-native')
             comm1.close()
             del tex1
+            # the same shape with heavy-tailed correlated SH, 30% all-zero SH rows and clumped
+            # positions: the assign's window on data like trained scenes, every label verified
+            progress('extra record: realistic 10M')
+            rt = realistic_table(total, SEED + 77, dev)
+            rstep, rtex, _ = make_step([rt], total)
+            el_r, meta_r, _ = timed(rstep, ks, kw)
+            rstats = ctx.kmeans_stats() or None
+            rver = None if args.no_verify else verify_step(ctx, rt, rtex, rstep, all_labels=not args.verify_sample)
+            extras['realistic_10M'] = dict(
+                record(f'writeSog SH3 of one {total / 1e6:g}M-splat table: heavy-tailed correlated SH (Student-t nu=3 '
+                       'through a mixing matrix), 30% all-zero SH rows, 80% of the positions in 20,000 clumps; '
+                       f'{args.iters} k-means iters', total, el_r, 'strong', textures_digest(rtex, meta_r)),
+                vs_main_step=(el_r / ks) / (elapsed / args.steps), sh_kmeans_assign=rstats, verified=rver['ok'] if rver
+                else None, verification=rver)
+            del rt, rstep, rtex
+            torch.cuda.empty_cache()
         # BASELINE config 4: one 50M-splat table, split over the ranks like the main table
         progress('extra record: config 4 (50M)')
         lo4, hi4 = CONFIG4_SPLATS * rank // world, CONFIG4_SPLATS * (rank + 1) // world
