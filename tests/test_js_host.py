@@ -91,7 +91,7 @@ def test_js_typed_columns_match_reference(addon_built):
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout)
     assert out.pop('transform_f64') is True
-    bad = {c: v for c, v in out.items() if not all(v.values())}
+    bad = {c: [k for k, ok in v.items() if not ok] for c, v in out.items() if not all(v.values())}
     assert not bad, bad
 
 
@@ -112,7 +112,7 @@ def test_js_process_and_compressed_ply_match_reference(addon_built):
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout)
-    bad = {c: v for c, v in out.items() if not all(v.values())}
+    bad = {c: [k for k, ok in v.items() if not ok] for c, v in out.items() if not all(v.values())}
     assert not bad, bad
 
 
