@@ -1778,7 +1778,13 @@ __global__ void k_big_prefix(const uint32_t *__restrict__ start, uint32_t cap, c
     *nlist = m;
 }
 
-// slice s of the listed clusters: 4 waves, lane = dimension; (sum, sum|x|, min ulp exponent)
+// slice s of the listed clusters: 4 waves, lane = dimension; (sum, sum|x|, min ulp exponent),
+// and each wave's members whose row is not all zero, in order (nzl: SB_SLICE / 4 per wave, nzc
+// their count): the sequential fallback of k_big_final walks only those.  Adding +-0 leaves an
+// f64 running sum unchanged (it starts at +0 and never becomes -0 under round-to-nearest), so
+// the walk over the nonzero rows IS the chain over all members -- a cluster of the table's
+// all-zero rows (30% of a scene's rows can be untrained SH) costs its nonzero members only.
+constexpr uint32_t SB_WAVE = 1024;  // SB_SLICE / 4
 template <typename T>
 __global__ __launch_bounds__(256) void k_big_partial(const T *__restrict__ aos, int d,
                                                      const uint32_t *__restrict__ members,
@@ -1786,7 +1792,8 @@ __global__ __launch_bounds__(256) void k_big_partial(const T *__restrict__ aos, 
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ soff,
                                                      const uint32_t *__restrict__ nlist, double *__restrict__ psum,
-                                                     double *__restrict__ pabs, int *__restrict__ pemin) {
+                                                     double *__restrict__ pabs, int *__restrict__ pemin,
+                                                     uint32_t *__restrict__ nzl, uint32_t *__restrict__ nzc) {
     __shared__ double ls[4][64], la[4][64];
     __shared__ int le[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1806,10 +1813,16 @@ __global__ __launch_bounds__(256) void k_big_partial(const T *__restrict__ aos, 
         const uint32_t a = s0 + min(s1 - s0, w * per), b = s0 + min(s1 - s0, (w + 1) * per);
         double sum = 0, sabs = 0;
         int emin = 0x7fffffff;
-        auto take = [&](T x) {
+        uint32_t *nz = nzl + ((uint64_t)sl * 4 + w) * SB_WAVE;
+        uint32_t cnt = 0;  // the same on every active lane
+        auto take = [&](T x, uint32_t mem) {
             sum += (double)x;
             sabs += __builtin_fabs((double)x);
             if (x != 0) emin = min(emin, ulp_exp(x));
+            if (__ballot(x != 0)) {  // the row is not all zero (the active lanes are lane < d)
+                if (lane == 0) nz[cnt] = mem;
+                ++cnt;
+            }
         };
         if (lane < d) {
             constexpr int U = 32;  // member rows in flight, as k_sumnd
@@ -1819,9 +1832,10 @@ __global__ __launch_bounds__(256) void k_big_partial(const T *__restrict__ aos, 
 #pragma unroll
                 for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
 #pragma unroll
-                for (int u = 0; u < U; ++u) take(v[u]);
+                for (int u = 0; u < U; ++u) take(v[u], members[j + u]);
             }
-            for (; j < b; ++j) take(aos[(uint64_t)members[j] * ld + lane]);
+            for (; j < b; ++j) take(aos[(uint64_t)members[j] * ld + lane], members[j]);
+            if (lane == 0) nzc[(uint64_t)sl * 4 + w] = cnt;
         }
         ls[w][lane] = sum;
         la[w][lane] = sabs;
@@ -1845,6 +1859,7 @@ __global__ __launch_bounds__(64) void k_big_final(const T *__restrict__ aos, int
                                                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ soff,
                                                   const uint32_t *__restrict__ nlist, const double *__restrict__ psum,
                                                   const double *__restrict__ pabs, const int *__restrict__ pemin,
+                                                  const uint32_t *__restrict__ nzl, const uint32_t *__restrict__ nzc,
                                                   float *__restrict__ cen) {
     const int lane = threadIdx.x;
     const int ld = aos_ld(d);
@@ -1860,18 +1875,26 @@ __global__ __launch_bounds__(64) void k_big_final(const T *__restrict__ aos, int
             E = min(E, pemin[(uint64_t)sl * 64 + lane]);
         }
         if (!sum_is_exact(A, E)) {
+            // the sequential chain (k-means.ts:41-63) over the members' nonzero rows, slice by
+            // slice, wave part by wave part: the members' order
             S = 0;
             constexpr int U = 32;
-            uint32_t j = s0;
-            for (; j + U <= s1; j += U) {
-                T v[U];
+            for (uint64_t part = (uint64_t)soff[i] * 4; part < (uint64_t)soff[i + 1] * 4; ++part) {
+                const uint32_t *mem = nzl + part * SB_WAVE;
+                const uint32_t c = nzc[part];
+                uint32_t j = 0;
+                for (; j + U <= c; j += U) {
+                    T v[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)members[j + u] * ld + lane];
+                    for (int u = 0; u < U; ++u) v[u] = aos[(uint64_t)mem[j + u] * ld + lane];
 #pragma unroll
-                for (int u = 0; u < U; ++u) S += (double)v[u];
+                    for (int u = 0; u < U; ++u) S += (double)v[u];
+                }
+                for (; j < c; ++j) S += (double)aos[(uint64_t)mem[j] * ld + lane];
             }
-            for (; j < s1; ++j) S += (double)aos[(uint64_t)members[j] * ld + lane];
         }
+        (void)members;
+        (void)s0;
         cen[(uint64_t)lane * k + cl] = (float)(S / (double)m);
     }
 }
@@ -1886,6 +1909,26 @@ __global__ __launch_bounds__(256) void k_aos64(const double *const *cols, int d,
     }
 }
 
+// the clusters k_sumnd listed as huge (list / nlist, at most cap): sliced partials, then the
+// certified sums or the sequential chain over their nonzero rows
+template <typename T>
+void big_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32_t *members, const uint32_t *start,
+              float *cen, uint32_t cap, uint32_t *list, uint32_t *nlist) {
+    const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
+    auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
+    auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
+    auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
+    auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
+    auto *nzl = wsT<uint32_t>(c, "kn.bnzl", slices * 4 * SB_WAVE);
+    auto *nzc = wsT<uint32_t>(c, "kn.bnzc", slices * 4);
+    hipLaunchKernelGGL(k_big_prefix, dim3(1), dim3(64), 0, c->stream, start, cap, list, soff, nlist);
+    hipLaunchKernelGGL(k_big_partial<T>, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d, members,
+                       start, list, soff, nlist, psum, pabs, pemin, nzl, nzc);
+    hipLaunchKernelGGL(k_big_final<T>, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d, members,
+                       start, k, list, soff, nlist, psum, pabs, pemin, nzl, nzc, cen);
+    ST_LAUNCH_CHECK();
+}
+
 template <typename T>
 void launch_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32_t *members, const uint32_t *start,
                  float *cen) {
@@ -1896,18 +1939,7 @@ void launch_sums(st_ctx *c, const T *aos, int d, uint64_t n, int k, const uint32
     ST_HIP(hipMemsetAsync(nlist, 0, 4, c->stream));
     hipLaunchKernelGGL(k_sumnd<T>, dim3((k + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen, big,
                        cap, list, nlist, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
-    if (n > big) {
-        const uint64_t slices = n / SB_SLICE + cap;  // bound on the listed clusters' slices
-        auto *soff = wsT<uint32_t>(c, "kn.bsoff", (size_t)cap + 1);
-        auto *psum = wsT<double>(c, "kn.bsum", slices * 64);
-        auto *pabs = wsT<double>(c, "kn.babs", slices * 64);
-        auto *pemin = wsT<int>(c, "kn.bemin", slices * 64);
-        hipLaunchKernelGGL(k_big_prefix, dim3(1), dim3(64), 0, c->stream, start, cap, list, soff, nlist);
-        hipLaunchKernelGGL(k_big_partial<T>, dim3(grid_for(slices, 1, 2048)), dim3(256), 0, c->stream, aos, d, members,
-                           start, list, soff, nlist, psum, pabs, pemin);
-        hipLaunchKernelGGL(k_big_final<T>, dim3(std::min<unsigned>(cap, 1024u)), dim3(64), 0, c->stream, aos, d,
-                           members, start, k, list, soff, nlist, psum, pabs, pemin, cen);
-    }
+    if (n > big) big_sums(c, aos, d, n, k, members, start, cen, cap, list, nlist);
     ST_LAUNCH_CHECK();
 }
 
@@ -2402,10 +2434,17 @@ bool nd_big_sums(st_ctx *c, int d, uint64_t n, int k, const uint32_t *labels, fl
     auto *members = wsT<uint32_t>(c, "kn.members", n);
     auto *start = wsT<uint32_t>(c, "kn.start", (size_t)k + 1);
     member_sort(c, labels, n, k, sorted_labels, members, start);
+    // the listed clusters: one wave each up to sumnd_big() members, the huge ones (a cluster of
+    // the table's all-zero rows) sliced over the chip (big_sums)
+    const uint32_t big = sumnd_big();
+    const uint32_t cap = (uint32_t)(n / ((uint64_t)big + 1) + 1);
+    auto *list = wsT<uint32_t>(c, "kn.blist", cap);
+    auto *nlist = wsT<uint32_t>(c, "kn.bn", 1);
+    ST_HIP(hipMemsetAsync(nlist, 0, 4, c->stream));
     hipLaunchKernelGGL(k_sumnd<float>, dim3((nbig + 3) / 4), dim3(256), 0, c->stream, aos, d, members, start, k, cen,
-                       0xffffffffu, 0u, (uint32_t *)nullptr, (uint32_t *)nullptr, wsT<uint32_t>(c, "kn.big", (size_t)k),
-                       wsT<uint32_t>(c, "kn.nflag", 2) + 1);
+                       big, cap, list, nlist, wsT<uint32_t>(c, "kn.big", (size_t)k), wsT<uint32_t>(c, "kn.nflag", 2) + 1);
     ST_LAUNCH_CHECK();
+    if (n > big) big_sums(c, aos, d, n, k, members, start, cen, cap, list, nlist);
     return true;
 }
 }  // namespace

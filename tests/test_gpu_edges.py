@@ -267,18 +267,25 @@ def test_kmeans_duplicated_rows_vs_oracle(ctx, monkeypatch, n, d, k, zero_frac, 
     same_bits(cent, ocent)
 
 
-@pytest.mark.parametrize('big,tiny', [(24, 0.0), (24, 0.02), (1, 0.0)])
-def test_kmeans_split_cluster_sums_vs_oracle(ctx, monkeypatch, big, tiny):
+@pytest.mark.parametrize('big,tiny,zero', [(24, 0.0, 0.0), (24, 0.02, 0.0), (1, 0.0, 0.0), (24, 0.02, 0.3),
+                                           (1, 0.02, 0.3), (24, 0.02, -0.3)])
+def test_kmeans_split_cluster_sums_vs_oracle(ctx, monkeypatch, big, tiny, zero):
     """calcAverage (k-means.ts:41-63) for clusters above the split threshold (ST_SUMND_BIG lowers
     the default 16,384): slices summed in parallel under the exactness certificate, and the
-    sequential chain where tiny members break the certificate.  big = 1 splits every cluster
-    with more than one member."""
+    sequential chain where tiny members break the certificate -- which walks the members' rows
+    that are not all zero (adding +-0 leaves the running sum as it is): zero = the fraction of
+    all-zero rows (negative: their zeros are -0.0 and +0.0 at random).  big = 1 splits every
+    cluster with more than one member."""
     n, d, k = 6000, 9, 64
-    rng = np.random.default_rng(big + int(tiny * 100))
+    rng = np.random.default_rng(big + int(tiny * 100) + int(zero * 1000))
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(d)]
+    zr = rng.random(n) < abs(zero)
     for c in cols:
         t = rng.random(n) < tiny
         c[t] *= np.float32(1e-12)
+        c[zr] = 0.0
+        if zero < 0:
+            c[zr & (rng.random(n) < 0.5)] = np.float32(-0.0)
     draws = oracle.mulberry32(9, 1 << 12)
     monkeypatch.setenv('ST_SUMND_BIG', str(big))
     cent, labels, used = ctx.kmeans(cols, k, 3, draws)
