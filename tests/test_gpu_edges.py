@@ -277,7 +277,7 @@ def test_kmeans_split_cluster_sums_vs_oracle(ctx, monkeypatch, big, tiny, zero):
     all-zero rows (negative: their zeros are -0.0 and +0.0 at random).  big = 1 splits every
     cluster with more than one member."""
     n, d, k = 6000, 9, 64
-    rng = np.random.default_rng(big + int(tiny * 100) + int(zero * 1000))
+    rng = np.random.default_rng(big + int(tiny * 100) + int(abs(zero) * 1000) + (7 if zero < 0 else 0))
     cols = [rng.normal(0, 1, n).astype(np.float32) for _ in range(d)]
     zr = rng.random(n) < abs(zero)
     for c in cols:
