@@ -1084,6 +1084,16 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
 // exact ties) are summed by k_nd_combine from a short label sort; clusters failing the
 // certificate take the sequential sum over their members in point order (k_nd_seq).
 constexpr uint32_t FA_SL = 4096;  // decided points per slice (a workgroup's unit of work)
+// a cluster's other members above which k_heavy_* sum them, and others per k_others_partial
+// record (ST_OTHERS_SPLIT / ST_OTHERS_CHUNK: test hooks that send small clusters this way)
+uint32_t others_split() {
+    const char *e = getenv("ST_OTHERS_SPLIT");  // read per call (tests set it around one call)
+    return e ? (uint32_t)std::max(1L, atol(e)) : 8192u;
+}
+uint32_t others_chunk() {
+    const char *e = getenv("ST_OTHERS_CHUNK");
+    return e ? (uint32_t)std::max(1L, atol(e)) : 4096u;
+}
 // accumulator slot of dimension j inside a cluster's LD slots (the layout k_nd_combine reads)
 template <int LD>
 __host__ __device__ inline int fa_slot(int j) { return (j & 3) * (LD / 4) + (j >> 2); }
@@ -1465,10 +1475,16 @@ __global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ ao
                                                     const uint32_t *__restrict__ ostart,
                                                     const uint32_t *__restrict__ ovals, float *__restrict__ cen,
                                                     uint32_t *__restrict__ counts, uint32_t *__restrict__ flagged,
-                                                    uint32_t *__restrict__ nflagged) {
+                                                    uint32_t *__restrict__ nflagged, uint32_t *__restrict__ heavy,
+                                                    uint32_t *__restrict__ nheavy, uint32_t os_split) {
     const int lane = threadIdx.x & 63;
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;  // uniform per wave
+    const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
+    if (o1 - o0 > os_split) {  // many others: summed over the chip (k_others_partial + k_heavy_final)
+        if (lane == 0) heavy[atomicAdd(nheavy, 1u)] = cl;
+        return;
+    }
     const uint32_t code = code_of(cl), loc = code_local(cl);
     double sum = 0, sabs = 0;
     int emin = 1 << 20;
@@ -1482,7 +1498,6 @@ __global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ ao
         }
         cnt += pcnt[(uint64_t)sl * 16 + loc];
     }
-    const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
     others_sum<LD>(aos, ovals, o0, o1, lane, sum, sabs, emin);
     cnt += o1 - o0;
     if (lane == 0) counts[cl] = cnt;
@@ -1506,10 +1521,15 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
                                                      const uint32_t *__restrict__ ostart,
                                                      const uint32_t *__restrict__ ovals, double *__restrict__ sums,
                                                      double *__restrict__ sabs_out, int32_t *__restrict__ emin_out,
-                                                     uint32_t *__restrict__ counts) {
+                                                     uint32_t *__restrict__ counts, uint32_t *__restrict__ heavy,
+                                                     uint32_t *__restrict__ nheavy, uint32_t os_split) {
     const int lane = threadIdx.x & 63;
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;  // uniform per wave
+    if (ostart[cl + 1] - ostart[cl] > os_split) {  // many others: k_others_partial + k_heavy_final
+        if (lane == 0) heavy[atomicAdd(nheavy, 1u)] = cl;
+        return;
+    }
     const uint32_t code = code_of(cl), loc = code_local(cl);
     double sum = 0, sabs = 0;
     int emin = 1 << 20;
@@ -1532,6 +1552,123 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
         sums[o] = sum;
         sabs_out[o] = sabs;
         emin_out[o] = emin;
+    }
+}
+
+// ---- clusters with many other members (others_split()): a cluster of the table's all-zero rows sits
+// on a near-tie with another centroid every other iteration, and its millions of pair points were
+// one wave's sequential loop inside k_nd_combine (100 ms per update at 10M).  Their others are
+// cut into others_chunk()-row chunks summed by the whole chip (sum, sum|x|, smallest ulp exponent per
+// dimension), then one wave per such cluster adds its slices' and its chunks' partials.  Under
+// the certificate every partial sum is exact, so the order of these additions does not matter;
+// a cluster the certificate fails is flagged as in k_nd_combine (the sequential sum over its
+// members in point order decides it).
+__global__ void k_heavy_prefix(const uint32_t *__restrict__ ostart, const uint32_t *__restrict__ heavy,
+                               const uint32_t *__restrict__ nheavy, uint32_t *__restrict__ hoff, uint32_t os_chunk) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t m = *nheavy;
+    uint32_t o = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        hoff[i] = o;
+        o += (ostart[heavy[i] + 1] - ostart[heavy[i]] + os_chunk - 1) / os_chunk;
+    }
+    hoff[m] = o;
+}
+
+// chunk j of the heavy clusters' others: 4 waves, lane = dimension; record j = (sum, sabs, emin)
+template <int LD>
+__global__ __launch_bounds__(256) void k_others_partial(const float *__restrict__ aos,
+                                                        const uint32_t *__restrict__ ostart,
+                                                        const uint32_t *__restrict__ ovals,
+                                                        const uint32_t *__restrict__ heavy,
+                                                        const uint32_t *__restrict__ nheavy,
+                                                        const uint32_t *__restrict__ hoff, double *__restrict__ rsum,
+                                                        double *__restrict__ rabs, int *__restrict__ remin,
+                                                        uint32_t os_chunk) {
+    __shared__ double ls[4][64], la[4][64];
+    __shared__ int le[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t nh = *nheavy, total = hoff[nh];
+    for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
+        uint32_t lo = 0, hi = nh;  // the heavy cluster whose chunks hold j
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (hoff[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t cl = heavy[lo];
+        const uint32_t c0 = ostart[cl] + (j - hoff[lo]) * os_chunk, c1 = min(ostart[cl + 1], c0 + os_chunk);
+        const uint32_t per = (c1 - c0 + 3) / 4;
+        const uint32_t a = c0 + min(c1 - c0, w * per), b = c0 + min(c1 - c0, (w + 1) * per);
+        double sum = 0, sabs = 0;
+        int emin = 1 << 20;
+        others_sum<LD>(aos, ovals, a, b, lane, sum, sabs, emin);
+        ls[w][lane] = sum;
+        la[w][lane] = sabs;
+        le[w][lane] = emin;
+        __syncthreads();
+        if (w == 0) {
+            rsum[(uint64_t)j * 64 + lane] = ((ls[0][lane] + ls[1][lane]) + ls[2][lane]) + ls[3][lane];
+            rabs[(uint64_t)j * 64 + lane] = ((la[0][lane] + la[1][lane]) + la[2][lane]) + la[3][lane];
+            remin[(uint64_t)j * 64 + lane] = min(min(le[0][lane], le[1][lane]), min(le[2][lane], le[3][lane]));
+        }
+        __syncthreads();
+    }
+}
+
+// one wave per heavy cluster: its tile-half's slice partials + its chunks' records; SHARD: the
+// sharded writer's partials (k_nd_partials' outputs), else the certified centroid or the flag
+template <int LD, bool SHARD>
+__global__ __launch_bounds__(64) void k_heavy_final(int d, int k, const uint32_t *__restrict__ soff,
+                                                    const double *__restrict__ psum, const double *__restrict__ pabs,
+                                                    const int *__restrict__ pemin, const uint32_t *__restrict__ pcnt,
+                                                    const uint32_t *__restrict__ ostart,
+                                                    const uint32_t *__restrict__ heavy,
+                                                    const uint32_t *__restrict__ nheavy,
+                                                    const uint32_t *__restrict__ hoff, const double *__restrict__ rsum,
+                                                    const double *__restrict__ rabs, const int *__restrict__ remin,
+                                                    float *__restrict__ cen, uint32_t *__restrict__ counts,
+                                                    uint32_t *__restrict__ flagged, uint32_t *__restrict__ nflagged,
+                                                    double *__restrict__ sums, double *__restrict__ sabs_out,
+                                                    int32_t *__restrict__ emin_out) {
+    const int lane = threadIdx.x;
+    const uint32_t nh = *nheavy;
+    for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+        const uint32_t cl = heavy[i], code = code_of(cl), loc = code_local(cl);
+        double sum = 0, sabs = 0;
+        int emin = 1 << 20;
+        uint32_t cnt = 0;
+        for (uint32_t sl = soff[code]; sl < soff[code + 1]; ++sl) {
+            if (lane < LD) {
+                const uint64_t e = (uint64_t)sl * 16 * LD + loc * LD + fa_slot<LD>(lane);
+                sum += psum[e];
+                sabs += pabs[e];
+                emin = min(emin, pemin[e]);
+            }
+            cnt += pcnt[(uint64_t)sl * 16 + loc];
+        }
+        for (uint32_t j = hoff[i]; j < hoff[i + 1]; ++j) {
+            sum += rsum[(uint64_t)j * 64 + lane];
+            sabs += rabs[(uint64_t)j * 64 + lane];
+            emin = min(emin, remin[(uint64_t)j * 64 + lane]);
+        }
+        cnt += ostart[cl + 1] - ostart[cl];
+        if (lane == 0) counts[cl] = cnt;
+        if constexpr (SHARD) {
+            if (lane < d) {
+                const uint64_t o = (uint64_t)lane * k + cl;
+                sums[o] = sum;
+                sabs_out[o] = sabs;
+                emin_out[o] = emin;
+            }
+        } else {
+            const bool exact = lane >= d || sum_is_exact(sabs, emin);
+            if (__ballot(!exact) == 0) {
+                if (lane < d) cen[(uint64_t)lane * k + cl] = (float)(sum / (double)cnt);
+            } else if (lane == 0) {
+                flagged[atomicAdd(nflagged, 1u)] = cl;
+            }
+        }
     }
 }
 
@@ -2375,6 +2512,47 @@ namespace {
 // the update after a fused fix-up: the other points' sums by label, the certified centroids,
 // the sequential sums of the clusters the certificate fails.  Returns false when a flagged
 // cluster has more members than k_nd_seq takes: those are summed over the member sort.
+// the clusters k_nd_combine / k_nd_partials listed as heavy (heavy / nheavy on the device): their
+// others' chunk records, then one wave each (no host sync)
+template <int LD, bool SHARD>
+void heavy_pass_t(st_ctx *c, int d, uint64_t n, int k, uint32_t m, const float *aos, const uint32_t *soff,
+                  const double *psum, const double *pabs, const int *pemin, const uint32_t *pcnt,
+                  const uint32_t *ostart, const uint32_t *ovals, const uint32_t *heavy, const uint32_t *nheavy,
+                  float *cen, uint32_t *counts, uint32_t *flagged, uint32_t *nflagged, double *sums, double *sabs,
+                  int32_t *emin) {
+    (void)n;
+    const uint32_t split = others_split(), chunk = others_chunk();
+    const uint64_t chunks = m / chunk + m / split + 2;  // bound: every heavy cluster holds > split others
+    auto *hoff = wsT<uint32_t>(c, "kn.hoff", (size_t)m / split + 2);
+    auto *rsum = wsT<double>(c, "kn.hrsum", chunks * 64);
+    auto *rabs = wsT<double>(c, "kn.hrabs", chunks * 64);
+    auto *remin = wsT<int>(c, "kn.hremin", chunks * 64);
+    hipLaunchKernelGGL(k_heavy_prefix, dim3(1), dim3(64), 0, c->stream, ostart, heavy, nheavy, hoff, chunk);
+    hipLaunchKernelGGL(k_others_partial<LD>, dim3(grid_for(chunks, 1, 2048)), dim3(256), 0, c->stream, aos, ostart,
+                       ovals, heavy, nheavy, hoff, rsum, rabs, remin, chunk);
+    hipLaunchKernelGGL((k_heavy_final<LD, SHARD>), dim3(std::min<uint64_t>(m / split + 1, 1024)), dim3(64), 0,
+                       c->stream, d, k, soff, psum, pabs, pemin, pcnt, ostart, heavy, nheavy, hoff, rsum, rabs, remin,
+                       cen, counts, flagged, nflagged, sums, sabs, emin);
+    ST_LAUNCH_CHECK();
+}
+
+template <bool SHARD>
+void heavy_pass(st_ctx *c, int ld, int d, uint64_t n, int k, uint32_t m, const float *aos, const uint32_t *soff,
+                const double *psum, const double *pabs, const int *pemin, const uint32_t *pcnt, const uint32_t *ostart,
+                const uint32_t *ovals, const uint32_t *heavy, const uint32_t *nheavy, float *cen, uint32_t *counts,
+                uint32_t *flagged, uint32_t *nflagged, double *sums, double *sabs, int32_t *emin) {
+    if (m <= others_split()) return;  // no cluster can hold more others than there are
+    if (ld == 48)
+        heavy_pass_t<48, SHARD>(c, d, n, k, m, aos, soff, psum, pabs, pemin, pcnt, ostart, ovals, heavy, nheavy, cen,
+                                counts, flagged, nflagged, sums, sabs, emin);
+    else if (ld == 24)
+        heavy_pass_t<24, SHARD>(c, d, n, k, m, aos, soff, psum, pabs, pemin, pcnt, ostart, ovals, heavy, nheavy, cen,
+                                counts, flagged, nflagged, sums, sabs, emin);
+    else
+        heavy_pass_t<12, SHARD>(c, d, n, k, m, aos, soff, psum, pabs, pemin, pcnt, ostart, ovals, heavy, nheavy, cen,
+                                counts, flagged, nflagged, sums, sabs, emin);
+}
+
 bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, const uint32_t *labels, float *cen,
                      uint32_t *counts, State *dstate) {
     KTimer kt(c, "kn.sumnd");
@@ -2390,19 +2568,23 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
     auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
     auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
     auto *flagged = wsT<uint32_t>(c, "kn.flagged", (size_t)k);
-    auto *nflag = wsT<uint32_t>(c, "kn.nflag", 2);  // [0] flagged clusters, [1] collect overflow
-    ST_HIP(hipMemsetAsync(nflag, 0, 8, c->stream));
+    auto *nflag = wsT<uint32_t>(c, "kn.nflag", 3);  // [0] flagged clusters, [1] collect overflow, [2] heavy
+    const uint32_t split = others_split();
+    auto *heavy = wsT<uint32_t>(c, "kn.heavy", (size_t)m / split + 2);
+    ST_HIP(hipMemsetAsync(nflag, 0, 12, c->stream));
     const dim3 g((k + 3) / 4);
     if (ld == 48)
         hipLaunchKernelGGL(k_nd_combine<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, cen, counts, flagged, nflag);
+                           ostart, ovals, cen, counts, flagged, nflag, heavy, nflag + 2, split);
     else if (ld == 24)
         hipLaunchKernelGGL(k_nd_combine<24>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, cen, counts, flagged, nflag);
+                           ostart, ovals, cen, counts, flagged, nflag, heavy, nflag + 2, split);
     else
         hipLaunchKernelGGL(k_nd_combine<12>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, cen, counts, flagged, nflag);
+                           ostart, ovals, cen, counts, flagged, nflag, heavy, nflag + 2, split);
     ST_LAUNCH_CHECK();
+    heavy_pass<false>(c, ld, d, n, k, m, aos, soff, psum, pabs, pemin, pcnt, ostart, ovals, heavy, nflag + 2, cen,
+                      counts, flagged, nflag, nullptr, nullptr, nullptr);
     // the clusters the certificate fails: their members in point order, the sequential sums
     // (grid-stride over the flagged list; none: every workgroup returns at once)
     auto *big = wsT<uint32_t>(c, "kn.big", (size_t)k);
@@ -2463,17 +2645,23 @@ void nd_fused_partials(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, c
     const uint32_t m = others_sort(c, n, k, fz, labels);
     auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
     auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
+    auto *nheavy = wsT<uint32_t>(c, "kn.pnheavy", 1);
+    const uint32_t split = others_split();
+    auto *heavy = wsT<uint32_t>(c, "kn.heavy", (size_t)m / split + 2);
+    ST_HIP(hipMemsetAsync(nheavy, 0, 4, c->stream));
     const dim3 g((k + 3) / 4);
     if (ld == 48)
         hipLaunchKernelGGL(k_nd_partials<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, sums, sabs, emin, counts);
+                           ostart, ovals, sums, sabs, emin, counts, heavy, nheavy, split);
     else if (ld == 24)
         hipLaunchKernelGGL(k_nd_partials<24>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, sums, sabs, emin, counts);
+                           ostart, ovals, sums, sabs, emin, counts, heavy, nheavy, split);
     else
         hipLaunchKernelGGL(k_nd_partials<12>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
-                           ostart, ovals, sums, sabs, emin, counts);
+                           ostart, ovals, sums, sabs, emin, counts, heavy, nheavy, split);
     ST_LAUNCH_CHECK();
+    heavy_pass<true>(c, ld, d, n, k, m, aos, soff, psum, pabs, pemin, pcnt, ostart, ovals, heavy, nheavy, nullptr,
+                     counts, nullptr, nullptr, sums, sabs, emin);
 }
 
 void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcols, int d, uint64_t n, int k,

@@ -183,6 +183,28 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
         assert st['pairs'] + st['ambiguous'] <= st['points']
 
 
+@pytest.mark.parametrize('n,d,k,iters,dist,split,chunk', [(20_000, 45, 1024, 3, 'gauss', 4, 16),
+                                                         (20_000, 45, 1024, 3, 't3', 1, 1),
+                                                         (30_000, 24, 2048, 2, 'gauss', 8, 5),
+                                                         (30_000, 9, 2048, 2, 't3', 2, 64)])
+def test_kmeans_heavy_others_vs_oracle(ctx, monkeypatch, n, d, k, iters, dist, split, chunk):
+    """clusters with many pair / ambiguous points (a cluster of all-zero rows on a near-tie: millions
+    at 10M) are summed over the chip in chunks (k_others_partial + k_heavy_final): ST_OTHERS_SPLIT /
+    ST_OTHERS_CHUNK lower the threshold (8,192) and the chunk (4,096) so every such cluster here
+    takes that path; labels, centroids and draws equal the reference's"""
+    monkeypatch.setenv('ST_OTHERS_SPLIT', str(split))
+    monkeypatch.setenv('ST_OTHERS_CHUNK', str(chunk))
+    rng = np.random.default_rng(n + d + 7)
+    cols = ([rng.normal(0, 0.1, n).astype(np.float32) for _ in range(d)] if dist == 'gauss'
+            else heavy_tailed(rng, n, d))
+    draws = oracle.mulberry32(n + k + 1, 4 * k * (iters + 1) + 64)
+    cent, labels, used = ctx.kmeans(cols, k, iters, draws)
+    rc, ocent, olabels, oused = oracle.kmeans(cols, k, iters, draws)
+    assert rc == 0 and used == oused
+    same_bits(labels, olabels)
+    same_bits(cent, ocent)
+
+
 K1_MODES = ['', 'ST_K1_SYNC', 'ST_K1_TILES', 'ST_K1_SORT', 'ST_K1_FF_MAX=0', 'ST_REPLAY_CAP=0',
             'ST_REPLAY_CAP=2']
 

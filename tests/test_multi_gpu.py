@@ -109,8 +109,15 @@ def test_group_cluster1d_reseeds_equal_single_device(ctx, who):
         g.close()
 
 
-@pytest.mark.parametrize('world,splits,adv', [(2, None, False), (3, 'empty0', False), (4, 'ragged', True)])
-def test_group_host_staged_equals_single_device(ctx, world, splits, adv):
+@pytest.mark.parametrize('world,splits,adv,heavy', [(2, None, False, False), (3, 'empty0', False, False),
+                                                     (4, 'ragged', True, False), (3, 'ragged', True, True)])
+def test_group_host_staged_equals_single_device(ctx, monkeypatch, world, splits, adv, heavy):
+    """heavy: ST_OTHERS_SPLIT / _CHUNK send every cluster with more than 2 pair / ambiguous points
+    through the chip-wide others sums (k_others_partial + k_heavy_final), in the single-device
+    update and in the sharded partials"""
+    if heavy:
+        monkeypatch.setenv('ST_OTHERS_SPLIT', '2')
+        monkeypatch.setenv('ST_OTHERS_CHUNK', '3')
     n = 30_011
     cols = _table(n, 40 + world, adversarial=adv)
     draws = np.random.default_rng(7).random(1 << 18)

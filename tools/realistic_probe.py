@@ -21,7 +21,7 @@ import splat_hip as sh
 KERNELS = ('kn.sweep', 'kn.collect', 'kn.fixrow', 'kn.fixpair', 'kn.exact', 'kn.sumnd', 'k1.assign', 'k1.sum')
 
 
-def main(n=10_000_000):
+def main(n=10_000_000, only=None):
     dev = torch.device('cuda', 0)
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
@@ -41,6 +41,8 @@ def main(n=10_000_000):
     }
     out = {}
     for name, make in cases.items():
+        if only and name not in only:
+            continue
         cols = make()
         torch.cuda.synchronize()
         ctx.dev_sog(cols, 10, draws, tex)  # warm
@@ -80,4 +82,4 @@ def zero_only(n, dev):
 
 
 if __name__ == '__main__':
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000, sys.argv[2].split(',') if len(sys.argv) > 2 else None)
