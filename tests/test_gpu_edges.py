@@ -522,3 +522,27 @@ def test_kmeans_labels_buffer_unaligned(ctx):
         assert used == oused
         same_bits(lab.cpu().numpy().astype(np.uint32), np.asarray(olabels, dtype=np.uint32))
         same_bits(cen.cpu().numpy(), np.asarray(ocent, dtype=np.float32).reshape(-1))
+
+
+@pytest.mark.parametrize('who', ['scales', 'colours', 'both', 'neither'])
+def test_sog_cluster1d_draws_move_the_sh_cursor_vs_oracle(ctx, who):
+    """writeSog's SH palette k-means starts at draw 0 beside the two cluster1d (a 1-D k-means
+    takes draws only to re-seed empty clusters) and reruns at the cursor they leave when they did
+    take draws (write-sog.ts:245-313): columns of four distinct values leave 252 of 256 clusters
+    empty, so the scales' / the colours' cluster1d (or both) take draws; textures, codebooks and
+    the draws used equal the reference's"""
+    n, C = 20_011, 3
+    cols = _table(n, C, 4242)
+    rng = np.random.default_rng(77)
+    groups = {'scales': ['scale_0', 'scale_1', 'scale_2'], 'colours': ['f_dc_0', 'f_dc_1', 'f_dc_2'],
+              'both': ['scale_0', 'scale_1', 'scale_2', 'f_dc_0', 'f_dc_1', 'f_dc_2'], 'neither': []}[who]
+    for k in groups:
+        cols[k] = (rng.integers(0, 4, n) * 0.25 - 5).astype(np.float32)
+    draws = oracle.mulberry32(31, 1 << 16)
+    tex, meta, used = ctx.sog(cols, 3, draws)
+    rc, otex, ometa, oused = oracle.sog(cols, C, 3, draws)
+    assert rc == 0 and used == oused
+    for k in otex:
+        same_bits(tex[k], otex[k])
+    for f in ('scales_codebook', 'sh0_codebook', 'shn_codebook'):
+        same_bits(np.array(getattr(meta, f)[:]), np.array(getattr(ometa, f)[:]))
