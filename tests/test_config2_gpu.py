@@ -57,7 +57,12 @@ def test_config2_1M_sh3_10_iterations():
         # the CLI's in.ply -> out.sog: the file path gives the in-memory step's archive
         addr, size = ctx.dev_sog_bundle_view(meta, N, tex, 0, 0)
         ref = bytes(bench.ctypes_char_array(size).from_address(addr))
-        e2e = bench.end_to_end(ctx, cols, 10, draws, tex, ref, reps=1)
+        e2e = bench.end_to_end(ctx, cols, 10, draws, tex, ref, meta, reps=1)
         assert e2e['archive_equals_in_memory_step'], e2e
+        # the Node drop-in (readPly -> writeSogFile over the addon, Math.random = the same draws,
+        # Date pinned): every rep's file is the library's archive of this step
+        nh = e2e['node_host']
+        if nh is not None:
+            assert nh.get('archive_equals_library') and nh['resident_columns_reused'] == 59, nh
     finally:
         ctx.close()
