@@ -441,41 +441,25 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
     for (uint8_t *p : {out->means_l, out->means_u, out->quats, out->scales, out->sh0})
         ST_HIP(hipMemsetAsync(p, 0, texels * 4, c->stream));
 
-    // The 1-D block and the SH palette k-means side by side.  The reference runs cluster1d of the
-    // scales, then of the colours, then the SH k-means, each starting at the Math.random cursor
-    // the one before left (write-sog.ts:245-313); a 1-D k-means takes draws only to re-seed
-    // empty clusters, so both cluster1d normally leave the cursor at 0.  The SH k-means therefore
-    // starts at once at draw 0 on this context, while a host thread on the context mc clusters
-    // the scales, then -- once the colours' thread on the context aux is done -- orders the rows
-    // (Morton) and writes the five textures beside the first sweeps; the colours' cluster1d runs
-    // from draw 0 too.  When a cluster1d did take draws, the colours rerun at the scales' cursor
-    // and the SH k-means reruns at the cursor both leave: the output is bit-identical either way.
+    // cluster1d of the colours (write-sog.ts:253-268) runs on a side context from its own host
+    // thread while this one orders, packs means / quats and clusters the scales.  Its draws
+    // start where the scales' k-means stops taking them (re-seeds of empty clusters only), so
+    // it starts at the scales' cursor 0 and is kept only if the scales took no draw; otherwise
+    // it reruns here at the right cursor (bit-identical either way)
     if (!c->aux) ST_REQUIRE(st_ctx_create(c->device, &c->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
     st_ctx *aux = c->aux;
-    if (!aux->aux) ST_REQUIRE(st_ctx_create(c->device, &aux->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
-    st_ctx *mc = aux->aux;
-    if (c->sog_early && !mc->aux)
-        ST_REQUIRE(st_ctx_create(c->device, &mc->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
-    // every buffer the threads share, allocated here (a context's workspace is not thread-safe)
     auto *lab_c = wsT<uint8_t>(aux, "sog.lab_c", n * 3);
     auto *cb_c = wsT<float>(aux, "sog.cb_c", 256);
-    auto *lab = wsT<uint8_t>(mc, "sog.lab", n * 3);
-    auto *cb = wsT<float>(mc, "sog.cb", 256);
-    auto *lab_s2 = wsT<uint8_t>(mc, "sog.lab_s", n * 3);
-    auto *pos = wsT<uint32_t>(c, "sog.pos", n);
-    const unsigned g = grid_for(n, 256, 8192);
-    hipEvent_t ev_pos;
-    ST_HIP(hipEventCreateWithFlags(&ev_pos, hipEventDisableTiming));
-    for (st_ctx *x : {aux, mc}) {
-        // the caller's columns and the textures' clears above: whatever was queued on c->stream
+    uint64_t used_c = 0;
+    std::exception_ptr err_c;
+    {
+        // the colour columns are the caller's: whatever the caller queued on c->stream first
         hipEvent_t ev;
         ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         ST_HIP(hipEventRecord(ev, c->stream));
-        ST_HIP(hipStreamWaitEvent(x->stream, ev, 0));
+        ST_HIP(hipStreamWaitEvent(aux->stream, ev, 0));
         ST_HIP(hipEventDestroy(ev));
     }
-    uint64_t used_c = 0;
-    std::exception_ptr err_c;
     std::thread colours([&] {
         try {
             use_device(aux);
@@ -485,31 +469,36 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
             err_c = std::current_exception();
         }
     });
-    uint64_t used_1d = 0;  // the draws both cluster1d took
-    std::exception_ptr err_1d;
-    auto block_1d = [&] {
+    struct Joiner {
+        std::thread &th;
+        ~Joiner() {
+            if (th.joinable()) th.join();
+        }
+    } joiner{colours};
+
+    // Morton order, extents and the five textures on a third context from their own host
+    // thread (c->aux->aux), started once both cluster1d are done so that the 1-D block runs
+    // alone and the Morton passes overlap the SH k-means' sweep instead: only the shN texture
+    // writes wait for the texel positions
+    auto *pos = wsT<uint32_t>(c, "sog.pos", n);
+    const unsigned g = grid_for(n, 256, 8192);
+    if (!aux->aux) ST_REQUIRE(st_ctx_create(c->device, &aux->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    st_ctx *mc = aux->aux;
+    hipEvent_t ev_pos, ev_lab;
+    ST_HIP(hipEventCreateWithFlags(&ev_pos, hipEventDisableTiming));
+    ST_HIP(hipEventCreateWithFlags(&ev_lab, hipEventDisableTiming));
+    {
+        hipEvent_t ev;  // the textures' clears above and the caller's columns
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ST_HIP(hipEventRecord(ev, c->stream));
+        ST_HIP(hipStreamWaitEvent(mc->stream, ev, 0));
+        ST_HIP(hipEventDestroy(ev));
+    }
+    std::exception_ptr err_m;
+    const uint8_t *lab_s_ = nullptr, *clab_ = nullptr;  // the labels the texture writes read
+    auto order_fn = [&] {
         try {
             use_device(mc);
-            // scales (write-sog.ts:245-251)
-            const uint64_t used_s = cluster1d_dev(mc, m + 3, 3, n, iters, draws, ndraws, cb, lab);
-            ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, mc->stream));
-            // colour + opacity (write-sog.ts:253-268)
-            colours.join();
-            const uint8_t *clab = lab_c, *lab_s = lab;
-            const float *ccb = cb_c;
-            uint64_t used = used_s;
-            if (used_s == 0) {
-                if (err_c) std::rethrow_exception(err_c);
-                used += used_c;
-            } else {  // the scales took draws: the colours' k-means starts after them
-                ST_HIP(hipMemcpyAsync(lab_s2, lab, n * 3, hipMemcpyDeviceToDevice, mc->stream));
-                lab_s = lab_s2;
-                used += cluster1d_dev(mc, m + 6, 3, n, iters, draws + used_s, ndraws - used_s, cb, lab);
-                clab = lab;
-                ccb = cb;
-            }
-            ST_HIP(hipMemcpyAsync(meta->sh0_codebook, ccb, 256 * 4, hipMemcpyDeviceToHost, mc->stream));
-            used_1d = used;
             // Morton order (write-sog.ts:42-49)
             auto *idx = wsT<uint32_t>(mc, "sog.idx", n);
             iota_u32(mc, idx, n);
@@ -569,42 +558,73 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
                 hipLaunchKernelGGL(k_quats_tex<float>, dim3(g), dim3(256), 0, mc->stream, m[10], m[11], m[12], m[13],
                                    (const uint32_t *)nullptr, pos, n, (uint32_t *)out->quats);
             ST_LAUNCH_CHECK();
-            // the scales / sh0 texels (the labels are final on this stream)
-            hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, lab_s, lab_s + n, lab_s + 2 * n,
-                               (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
-            if (src.op64)
-                hipLaunchKernelGGL(k_table_tex<double>, dim3(g), dim3(256), 0, mc->stream, clab, clab + n, clab + 2 * n,
-                                   src.op64, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
-            else
-                hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, clab, clab + n, clab + 2 * n,
-                                   m[9], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
-            ST_LAUNCH_CHECK();
+            {  // the scales / sh0 texels, once the labels are in place
+                ST_HIP(hipStreamWaitEvent(mc->stream, ev_lab, 0));
+                hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, lab_s_, lab_s_ + n, lab_s_ + 2 * n,
+                                   (const float *)nullptr, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->scales);
+                if (src.op64)
+                    hipLaunchKernelGGL(k_table_tex<double>, dim3(g), dim3(256), 0, mc->stream, clab_, clab_ + n,
+                                       clab_ + 2 * n, src.op64, (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+                else
+                    hipLaunchKernelGGL(k_table_tex<float>, dim3(g), dim3(256), 0, mc->stream, clab_, clab_ + n,
+                                       clab_ + 2 * n, m[9], (const uint32_t *)nullptr, pos, n, (uint32_t *)out->sh0);
+                ST_LAUNCH_CHECK();
+            }
             ST_HIP(hipEventRecord(ev_pos, mc->stream));
             if (c->sog_early) c->sog_early(mc);  // the five textures are final on mc->stream
             ST_HIP(hipStreamSynchronize(mc->stream));
         } catch (...) {
-            err_1d = std::current_exception();
+            err_m = std::current_exception();
         }
-        if (colours.joinable()) colours.join();
     };
-    std::thread th_1d(block_1d);
-    struct Joiner {
-        std::thread &a, &b;
-        hipEvent_t ev;
-        ~Joiner() {
-            if (a.joinable()) a.join();
-            if (b.joinable()) b.join();
+    std::thread order_th;
+    struct Joiner2 {
+        std::thread &th;
+        hipEvent_t ev, ev2;
+        ~Joiner2() {
+            if (th.joinable()) th.join();
             (void)hipEventDestroy(ev);
+            (void)hipEventDestroy(ev2);
         }
-    } joiner{th_1d, colours, ev_pos};
-    // the 1-D block ends before anything reads its results (texel positions, codebooks) here
-    auto join_1d = [&] {
-        if (!th_1d.joinable()) return;
-        th_1d.join();
-        if (err_1d) std::rethrow_exception(err_1d);
+    } joiner2{order_th, ev_pos, ev_lab};
+
+    uint64_t cursor = 0;
+    auto *lab = wsT<uint8_t>(c, "sog.lab", n * 3);
+    auto *cb = wsT<float>(c, "sog.cb", 256);
+    // scales (write-sog.ts:245-251)
+    cursor += cluster1d_dev(c, m + 3, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
+    ST_HIP(hipMemcpyAsync(meta->scales_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    // colour + opacity (write-sog.ts:253-268)
+    colours.join();
+    const uint8_t *clab = lab_c;
+    const float *ccb = cb_c;
+    uint8_t *lab_s = lab;
+    if (cursor == 0) {
+        if (err_c) std::rethrow_exception(err_c);
+        cursor += used_c;
+    } else {  // the scales took draws: the colours' k-means starts after them
+        lab_s = wsT<uint8_t>(c, "sog.lab_s", n * 3);
+        ST_HIP(hipMemcpyAsync(lab_s, lab, n * 3, hipMemcpyDeviceToDevice, c->stream));
+        cursor += cluster1d_dev(c, m + 6, 3, n, iters, draws + cursor, ndraws - cursor, cb, lab);
+        clab = lab;
+        ccb = cb;
+    }
+    ST_HIP(hipMemcpyAsync(meta->sh0_codebook, ccb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    mark(c, "sog.cluster1d");
+    // the Morton order and the five textures beside the SH k-means (order_fn)
+    lab_s_ = lab_s;
+    clab_ = clab;
+    ST_HIP(hipEventRecord(ev_lab, c->stream));
+    if (c->sog_early && !mc->aux)
+        ST_REQUIRE(st_ctx_create(c->device, &mc->aux) == ST_OK, ST_ERR_HIP, "sog: side context");
+    order_th = std::thread(order_fn);
+    // the texture thread ends before anything reads the texel positions on this stream
+    auto join_late = [&] {
+        if (!order_th.joinable()) return;
+        order_th.join();
+        if (err_m) std::rethrow_exception(err_m);
         ST_HIP(hipStreamWaitEvent(c->stream, ev_pos, 0));
     };
-    uint64_t cursor = 0;
 
     meta->sh_bands = C == 15 ? 3 : C == 8 ? 2 : C == 3 ? 1 : 0;
     if (C > 0) {
@@ -615,24 +635,10 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         const int D = 3 * C;
         auto *cen = wsT<float>(c, "sog.shcen", (size_t)pal * D);
         auto *labels = wsT<uint32_t>(c, "sog.shlab", n);
-        // from draw 0, beside the 1-D block; again at the cursor the cluster1d left if they took draws
-        uint64_t used_sh = 0;
-        std::exception_ptr err_sh;
-        try {
-            used_sh = kmeans_dev(c, src.sh, D, n, pal, iters, draws, ndraws, cen, labels, false,
-                                 src.sh64[0] ? src.sh64 : nullptr);
-        } catch (...) {
-            err_sh = std::current_exception();
-        }
-        join_1d();  // the reference's order: an error of the 1-D block comes first
-        if (used_1d != 0) {
-            used_sh = kmeans_dev(c, src.sh, D, n, pal, iters, draws + used_1d, ndraws - used_1d, cen, labels, false,
-                                 src.sh64[0] ? src.sh64 : nullptr);
-        } else if (err_sh) {
-            std::rethrow_exception(err_sh);
-        }
-        cursor = used_1d + used_sh;
+        cursor += kmeans_dev(c, src.sh, D, n, pal, iters, draws + cursor, ndraws - cursor, cen, labels, false,
+                             src.sh64[0] ? src.sh64 : nullptr);
         mark(c, "sog.shkmeans");
+        join_late();
         // the shN labels texels (random 4-byte stores at the Morton positions) do not wait for
         // the codebook: they run on the side stream beside its latency-bound 1-D iterations,
         // on few workgroups so that those kernels still find free CUs
@@ -648,18 +654,17 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         std::vector<const float *> ccols(D);
         for (int i = 0; i < D; ++i) ccols[i] = cen + (uint64_t)i * pal;
         auto *cl = wsT<uint8_t>(c, "sog.cl", (size_t)pal * D);
-        auto *cbn = wsT<float>(c, "sog.cbn", 256);
         try {
             // the SH centroids are initial rows, means of finite rows or re-seeded rows: finite
             c->km_finite_known = true;
-            cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cbn, cl);
+            cursor += cluster1d_dev(c, ccols.data(), D, (uint64_t)pal, iters, draws + cursor, ndraws - cursor, cb, cl);
             c->km_finite_known = false;
         } catch (...) {
             c->km_finite_known = false;
             (void)hipStreamWaitEvent(c->stream, c->side_ev[1], 0);
             throw;
         }
-        ST_HIP(hipMemcpyAsync(meta->shn_codebook, cbn, 256 * 4, hipMemcpyDeviceToHost, c->stream));
+        ST_HIP(hipMemcpyAsync(meta->shn_codebook, cb, 256 * 4, hipMemcpyDeviceToHost, c->stream));
         ST_HIP(hipMemsetAsync(out->shn_centroids, 0, (size_t)cw * chh * 4, c->stream));
         hipLaunchKernelGGL(k_shn_centroids_tex, dim3(grid_for((uint64_t)pal * C, 256, 4096)), dim3(256), 0, c->stream,
                            cl, C, pal, (uint32_t *)out->shn_centroids);
@@ -667,8 +672,7 @@ uint64_t sog_impl(st_ctx *c, const SogSrc &src, int iters, const double *draws, 
         ST_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
         mark(c, "sog.shn");
     }
-    join_1d();
-    if (C == 0) cursor = used_1d;
+    join_late();
     ST_HIP(hipStreamSynchronize(c->stream));
     return cursor;
 }
