@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(256) void k_fixrow_b(const float *__restrict__ aos,
 // exact ties) are summed by k_nd_combine from a short label sort; clusters failing the
 // certificate take the sequential sum over their members in point order (k_nd_seq).
 constexpr uint32_t FA_SL = 4096;  // decided points per slice (a workgroup's unit of work)
-// a cluster's other members above which k_heavy_* sum them, and others per k_others_partial
+// a cluster's other members above which k_heavy sums them, and others per k_heavy record
 // record (ST_OTHERS_SPLIT / ST_OTHERS_CHUNK: test hooks that send small clusters this way)
 uint32_t others_split() {
     const char *e = getenv("ST_OTHERS_SPLIT");  // read per call (tests set it around one call)
@@ -1481,7 +1481,7 @@ __global__ __launch_bounds__(256) void k_nd_combine(const float *__restrict__ ao
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;  // uniform per wave
     const uint32_t o0 = ostart[cl], o1 = ostart[cl + 1];
-    if (o1 - o0 > os_split) {  // many others: summed over the chip (k_others_partial + k_heavy_final)
+    if (o1 - o0 > os_split) {  // many others: summed over the chip (k_heavy)
         if (lane == 0) heavy[atomicAdd(nheavy, 1u)] = cl;
         return;
     }
@@ -1526,7 +1526,7 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
     const int lane = threadIdx.x & 63;
     const uint32_t cl = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cl >= (uint32_t)k) return;  // uniform per wave
-    if (ostart[cl + 1] - ostart[cl] > os_split) {  // many others: k_others_partial + k_heavy_final
+    if (ostart[cl + 1] - ostart[cl] > os_split) {  // many others: k_heavy
         if (lane == 0) heavy[atomicAdd(nheavy, 1u)] = cl;
         return;
     }
@@ -1563,41 +1563,52 @@ __global__ __launch_bounds__(256) void k_nd_partials(const float *__restrict__ a
 // the certificate every partial sum is exact, so the order of these additions does not matter;
 // a cluster the certificate fails is flagged as in k_nd_combine (the sequential sum over its
 // members in point order decides it).
-__global__ void k_heavy_prefix(const uint32_t *__restrict__ ostart, const uint32_t *__restrict__ heavy,
-                               const uint32_t *__restrict__ nheavy, uint32_t *__restrict__ hoff, uint32_t os_chunk) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const uint32_t m = *nheavy;
+// chunk j of the heavy clusters' others -> (cluster index i in the heavy list, its first chunk);
+// the list is short (none, usually; at most m / others_split()): a linear scan
+__device__ inline uint32_t heavy_of_chunk(const uint32_t *__restrict__ ostart, const uint32_t *__restrict__ heavy,
+                                          uint32_t nh, uint32_t os_chunk, uint32_t j, uint32_t *first) {
     uint32_t o = 0;
-    for (uint32_t i = 0; i < m; ++i) {
-        hoff[i] = o;
-        o += (ostart[heavy[i] + 1] - ostart[heavy[i]] + os_chunk - 1) / os_chunk;
+    for (uint32_t i = 0; i < nh; ++i) {
+        const uint32_t c = (ostart[heavy[i] + 1] - ostart[heavy[i]] + os_chunk - 1) / os_chunk;
+        if (j < o + c) {
+            *first = o;
+            return i;
+        }
+        o += c;
     }
-    hoff[m] = o;
+    *first = o;
+    return nh;
 }
 
-// chunk j of the heavy clusters' others: 4 waves, lane = dimension; record j = (sum, sabs, emin)
-template <int LD>
-__global__ __launch_bounds__(256) void k_others_partial(const float *__restrict__ aos,
-                                                        const uint32_t *__restrict__ ostart,
-                                                        const uint32_t *__restrict__ ovals,
-                                                        const uint32_t *__restrict__ heavy,
-                                                        const uint32_t *__restrict__ nheavy,
-                                                        const uint32_t *__restrict__ hoff, double *__restrict__ rsum,
-                                                        double *__restrict__ rabs, int *__restrict__ remin,
-                                                        uint32_t os_chunk) {
+// One launch: every workgroup sums chunks of the heavy clusters' others (4 waves, lane =
+// dimension; record j = (sum, sum|x|, smallest ulp exponent)); the workgroup that finishes last
+// then adds, one wave per heavy cluster, its tile-half's slice partials and its chunk records:
+// SHARD, the sharded writer's partials (k_nd_partials' outputs), else the certified centroid or
+// the flag.  done: zeroed before the launch.  No heavy cluster: every workgroup returns at once.
+template <int LD, bool SHARD>
+__global__ __launch_bounds__(256) void k_heavy(const float *__restrict__ aos, int d, int k,
+                                               const uint32_t *__restrict__ soff, const double *__restrict__ psum,
+                                               const double *__restrict__ pabs, const int *__restrict__ pemin,
+                                               const uint32_t *__restrict__ pcnt, const uint32_t *__restrict__ ostart,
+                                               const uint32_t *__restrict__ ovals, const uint32_t *__restrict__ heavy,
+                                               const uint32_t *__restrict__ nheavy, uint32_t *__restrict__ done,
+                                               uint32_t os_chunk, double *__restrict__ rsum, double *__restrict__ rabs,
+                                               int *__restrict__ remin, float *__restrict__ cen,
+                                               uint32_t *__restrict__ counts, uint32_t *__restrict__ flagged,
+                                               uint32_t *__restrict__ nflagged, double *__restrict__ sums,
+                                               double *__restrict__ sabs_out, int32_t *__restrict__ emin_out) {
     __shared__ double ls[4][64], la[4][64];
     __shared__ int le[4][64];
+    __shared__ bool last;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t nh = *nheavy, total = hoff[nh];
+    const uint32_t nh = *nheavy;
+    if (nh == 0) return;
+    uint32_t total;
+    heavy_of_chunk(ostart, heavy, nh, os_chunk, 0xffffffffu, &total);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
-        uint32_t lo = 0, hi = nh;  // the heavy cluster whose chunks hold j
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (hoff[mid] <= j) lo = mid;
-            else hi = mid;
-        }
-        const uint32_t cl = heavy[lo];
-        const uint32_t c0 = ostart[cl] + (j - hoff[lo]) * os_chunk, c1 = min(ostart[cl + 1], c0 + os_chunk);
+        uint32_t first;
+        const uint32_t cl = heavy[heavy_of_chunk(ostart, heavy, nh, os_chunk, j, &first)];
+        const uint32_t c0 = ostart[cl] + (j - first) * os_chunk, c1 = min(ostart[cl + 1], c0 + os_chunk);
         const uint32_t per = (c1 - c0 + 3) / 4;
         const uint32_t a = c0 + min(c1 - c0, w * per), b = c0 + min(c1 - c0, (w + 1) * per);
         double sum = 0, sabs = 0;
@@ -1614,27 +1625,17 @@ __global__ __launch_bounds__(256) void k_others_partial(const float *__restrict_
         }
         __syncthreads();
     }
-}
-
-// one wave per heavy cluster: its tile-half's slice partials + its chunks' records; SHARD: the
-// sharded writer's partials (k_nd_partials' outputs), else the certified centroid or the flag
-template <int LD, bool SHARD>
-__global__ __launch_bounds__(64) void k_heavy_final(int d, int k, const uint32_t *__restrict__ soff,
-                                                    const double *__restrict__ psum, const double *__restrict__ pabs,
-                                                    const int *__restrict__ pemin, const uint32_t *__restrict__ pcnt,
-                                                    const uint32_t *__restrict__ ostart,
-                                                    const uint32_t *__restrict__ heavy,
-                                                    const uint32_t *__restrict__ nheavy,
-                                                    const uint32_t *__restrict__ hoff, const double *__restrict__ rsum,
-                                                    const double *__restrict__ rabs, const int *__restrict__ remin,
-                                                    float *__restrict__ cen, uint32_t *__restrict__ counts,
-                                                    uint32_t *__restrict__ flagged, uint32_t *__restrict__ nflagged,
-                                                    double *__restrict__ sums, double *__restrict__ sabs_out,
-                                                    int32_t *__restrict__ emin_out) {
-    const int lane = threadIdx.x;
-    const uint32_t nh = *nheavy;
-    for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    __threadfence();  // this workgroup's records, before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // every other workgroup's records, after the last ticket
+    for (uint32_t i = w; i < nh; i += 4) {
         const uint32_t cl = heavy[i], code = code_of(cl), loc = code_local(cl);
+        uint32_t j0 = 0;
+        for (uint32_t t = 0; t < i; ++t) j0 += (ostart[heavy[t] + 1] - ostart[heavy[t]] + os_chunk - 1) / os_chunk;
+        const uint32_t j1 = j0 + (ostart[cl + 1] - ostart[cl] + os_chunk - 1) / os_chunk;
         double sum = 0, sabs = 0;
         int emin = 1 << 20;
         uint32_t cnt = 0;
@@ -1647,10 +1648,10 @@ __global__ __launch_bounds__(64) void k_heavy_final(int d, int k, const uint32_t
             }
             cnt += pcnt[(uint64_t)sl * 16 + loc];
         }
-        for (uint32_t j = hoff[i]; j < hoff[i + 1]; ++j) {
-            sum += rsum[(uint64_t)j * 64 + lane];
-            sabs += rabs[(uint64_t)j * 64 + lane];
-            emin = min(emin, remin[(uint64_t)j * 64 + lane]);
+        for (uint32_t j = j0; j < j1; ++j) {
+            sum += __builtin_nontemporal_load(&rsum[(uint64_t)j * 64 + lane]);
+            sabs += __builtin_nontemporal_load(&rabs[(uint64_t)j * 64 + lane]);
+            emin = min(emin, __builtin_nontemporal_load(&remin[(uint64_t)j * 64 + lane]));
         }
         cnt += ostart[cl + 1] - ostart[cl];
         if (lane == 0) counts[cl] = cnt;
@@ -2523,15 +2524,11 @@ void heavy_pass_t(st_ctx *c, int d, uint64_t n, int k, uint32_t m, const float *
     (void)n;
     const uint32_t split = others_split(), chunk = others_chunk();
     const uint64_t chunks = m / chunk + m / split + 2;  // bound: every heavy cluster holds > split others
-    auto *hoff = wsT<uint32_t>(c, "kn.hoff", (size_t)m / split + 2);
     auto *rsum = wsT<double>(c, "kn.hrsum", chunks * 64);
     auto *rabs = wsT<double>(c, "kn.hrabs", chunks * 64);
     auto *remin = wsT<int>(c, "kn.hremin", chunks * 64);
-    hipLaunchKernelGGL(k_heavy_prefix, dim3(1), dim3(64), 0, c->stream, ostart, heavy, nheavy, hoff, chunk);
-    hipLaunchKernelGGL(k_others_partial<LD>, dim3(grid_for(chunks, 1, 2048)), dim3(256), 0, c->stream, aos, ostart,
-                       ovals, heavy, nheavy, hoff, rsum, rabs, remin, chunk);
-    hipLaunchKernelGGL((k_heavy_final<LD, SHARD>), dim3(std::min<uint64_t>(m / split + 1, 1024)), dim3(64), 0,
-                       c->stream, d, k, soff, psum, pabs, pemin, pcnt, ostart, heavy, nheavy, hoff, rsum, rabs, remin,
+    hipLaunchKernelGGL((k_heavy<LD, SHARD>), dim3(grid_for(chunks, 1, 2048)), dim3(256), 0, c->stream, aos, d, k, soff,
+                       psum, pabs, pemin, pcnt, ostart, ovals, heavy, nheavy, const_cast<uint32_t *>(nheavy) + 1, chunk, rsum, rabs, remin,
                        cen, counts, flagged, nflagged, sums, sabs, emin);
     ST_LAUNCH_CHECK();
 }
@@ -2568,10 +2565,11 @@ bool nd_fused_update(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, con
     auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
     auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
     auto *flagged = wsT<uint32_t>(c, "kn.flagged", (size_t)k);
-    auto *nflag = wsT<uint32_t>(c, "kn.nflag", 3);  // [0] flagged clusters, [1] collect overflow, [2] heavy
+    // [0] flagged clusters, [1] collect overflow, [2] heavy clusters, [3] k_heavy's finished workgroups
+    auto *nflag = wsT<uint32_t>(c, "kn.nflag", 4);
     const uint32_t split = others_split();
     auto *heavy = wsT<uint32_t>(c, "kn.heavy", (size_t)m / split + 2);
-    ST_HIP(hipMemsetAsync(nflag, 0, 12, c->stream));
+    ST_HIP(hipMemsetAsync(nflag, 0, 16, c->stream));
     const dim3 g((k + 3) / 4);
     if (ld == 48)
         hipLaunchKernelGGL(k_nd_combine<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,
@@ -2645,10 +2643,10 @@ void nd_fused_partials(st_ctx *c, int d, uint64_t n, int k, const NdFused &fz, c
     const uint32_t m = others_sort(c, n, k, fz, labels);
     auto *ovals = wsT<uint32_t>(c, "kn.ovals", (size_t)m + 1);
     auto *ostart = wsT<uint32_t>(c, "kn.ostart", (size_t)k + 1);
-    auto *nheavy = wsT<uint32_t>(c, "kn.pnheavy", 1);
+    auto *nheavy = wsT<uint32_t>(c, "kn.pnheavy", 2);  // [0] heavy clusters, [1] k_heavy's finished workgroups
     const uint32_t split = others_split();
     auto *heavy = wsT<uint32_t>(c, "kn.heavy", (size_t)m / split + 2);
-    ST_HIP(hipMemsetAsync(nheavy, 0, 4, c->stream));
+    ST_HIP(hipMemsetAsync(nheavy, 0, 8, c->stream));
     const dim3 g((k + 3) / 4);
     if (ld == 48)
         hipLaunchKernelGGL(k_nd_partials<48>, g, dim3(256), 0, c->stream, aos, d, k, soff, psum, pabs, pemin, pcnt,

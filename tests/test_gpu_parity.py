@@ -189,7 +189,7 @@ def test_kmeans_vs_oracle(ctx, n, d, k, iters, dist):
                                                          (30_000, 9, 2048, 2, 't3', 2, 64)])
 def test_kmeans_heavy_others_vs_oracle(ctx, monkeypatch, n, d, k, iters, dist, split, chunk):
     """clusters with many pair / ambiguous points (a cluster of all-zero rows on a near-tie: millions
-    at 10M) are summed over the chip in chunks (k_others_partial + k_heavy_final): ST_OTHERS_SPLIT /
+    at 10M) are summed over the chip in chunks (k_heavy): ST_OTHERS_SPLIT /
     ST_OTHERS_CHUNK lower the threshold (8,192) and the chunk (4,096) so every such cluster here
     takes that path; labels, centroids and draws equal the reference's"""
     monkeypatch.setenv('ST_OTHERS_SPLIT', str(split))

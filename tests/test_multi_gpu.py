@@ -113,7 +113,7 @@ def test_group_cluster1d_reseeds_equal_single_device(ctx, who):
                                                      (4, 'ragged', True, False), (4, 'ragged', True, True)])
 def test_group_host_staged_equals_single_device(ctx, monkeypatch, world, splits, adv, heavy):
     """heavy: ST_OTHERS_SPLIT / _CHUNK send every cluster with more than 2 pair / ambiguous points
-    through the chip-wide others sums (k_others_partial + k_heavy_final), in the single-device
+    through the chip-wide others sums (k_heavy), in the single-device
     update and in the sharded partials"""
     if heavy:
         monkeypatch.setenv('ST_OTHERS_SPLIT', '2')
