@@ -144,7 +144,8 @@ struct PropSlot {
 };
 
 constexpr uint32_t LDS_ROWS_BYTES = 48 * 1024;
-constexpr int kReaders = 8;  // pread threads per file chunk
+// pread threads per file chunk (ST_PLY_READERS: tuning experiments)
+const int kReaders = std::max(1, std::min(32, std::getenv("ST_PLY_READERS") ? std::atoi(std::getenv("ST_PLY_READERS")) : 8));
 
 // rows [0, nrows) of the staged chunk -> columns at rows [row0, row0 + nrows)
 __global__ __launch_bounds__(256) void k_ply_cols(const uint8_t *__restrict__ rows, uint64_t nrows, uint32_t R,
@@ -416,42 +417,91 @@ void transpose_scalar(const uint8_t *rows, uint64_t row0, uint64_t i0, uint64_t 
     }
 }
 
+// 8 rows x 8 float columns (row stride `stride` floats) -> c[k] = column k of the 8 rows
+__attribute__((target("avx2"))) inline void t8x8(const float *s0, uint64_t stride, __m256 c[8]) {
+    const __m256 r0 = _mm256_loadu_ps(s0), r1 = _mm256_loadu_ps(s0 + stride), r2 = _mm256_loadu_ps(s0 + 2 * stride),
+                 r3 = _mm256_loadu_ps(s0 + 3 * stride), r4 = _mm256_loadu_ps(s0 + 4 * stride),
+                 r5 = _mm256_loadu_ps(s0 + 5 * stride), r6 = _mm256_loadu_ps(s0 + 6 * stride),
+                 r7 = _mm256_loadu_ps(s0 + 7 * stride);
+    const __m256 t0 = _mm256_unpacklo_ps(r0, r1), t1 = _mm256_unpackhi_ps(r0, r1);
+    const __m256 t2 = _mm256_unpacklo_ps(r2, r3), t3 = _mm256_unpackhi_ps(r2, r3);
+    const __m256 t4 = _mm256_unpacklo_ps(r4, r5), t5 = _mm256_unpackhi_ps(r4, r5);
+    const __m256 t6 = _mm256_unpacklo_ps(r6, r7), t7 = _mm256_unpackhi_ps(r6, r7);
+    const __m256 u0 = _mm256_shuffle_ps(t0, t2, 0x44), u1 = _mm256_shuffle_ps(t0, t2, 0xEE);
+    const __m256 u2 = _mm256_shuffle_ps(t1, t3, 0x44), u3 = _mm256_shuffle_ps(t1, t3, 0xEE);
+    const __m256 u4 = _mm256_shuffle_ps(t4, t6, 0x44), u5 = _mm256_shuffle_ps(t4, t6, 0xEE);
+    const __m256 u6 = _mm256_shuffle_ps(t5, t7, 0x44), u7 = _mm256_shuffle_ps(t5, t7, 0xEE);
+    c[0] = _mm256_permute2f128_ps(u0, u4, 0x20);
+    c[1] = _mm256_permute2f128_ps(u1, u5, 0x20);
+    c[2] = _mm256_permute2f128_ps(u2, u6, 0x20);
+    c[3] = _mm256_permute2f128_ps(u3, u7, 0x20);
+    c[4] = _mm256_permute2f128_ps(u0, u4, 0x31);
+    c[5] = _mm256_permute2f128_ps(u1, u5, 0x31);
+    c[6] = _mm256_permute2f128_ps(u2, u6, 0x31);
+    c[7] = _mm256_permute2f128_ps(u3, u7, 0x31);
+}
+
+// Every column 64-B aligned (the addon's column blocks, the host twins): 16 rows at a time, each
+// column's 64 bytes of them one whole cache line written with two streaming stores -- no read
+// for ownership of the 2.5 GB of columns, no cache pollution.  Otherwise 8 rows at a time with
+// ordinary stores.  The last np % 8 columns and the rows outside whole groups go value by value.
 __attribute__((target("avx2"))) void transpose_f32_avx2(const uint8_t *rows, uint64_t row0, uint64_t i0, uint64_t i1,
                                                         const Props &P, void *const *dst, void *const *dst2) {
     const int np = (int)P.sz.size(), nb = np / 8;
+    const uint64_t stride = P.R / 4;
+    bool aligned = true;
+    for (int p = 0; p < np; ++p) {
+        aligned = aligned && ((uintptr_t)dst[p] & 63) == 0;
+        if (dst2) aligned = aligned && ((uintptr_t)dst2[p] & 63) == 0;
+    }
     uint64_t i = i0;
-    for (; i + 8 <= i1; i += 8) {
-        const float *src = reinterpret_cast<const float *>(rows + i * P.R);
-        const uint64_t stride = P.R / 4, r = row0 + i;
-        for (int j = 0; j < nb; ++j) {
-            const float *s0 = src + 8 * j;
-            __m256 r0 = _mm256_loadu_ps(s0), r1 = _mm256_loadu_ps(s0 + stride), r2 = _mm256_loadu_ps(s0 + 2 * stride),
-                   r3 = _mm256_loadu_ps(s0 + 3 * stride), r4 = _mm256_loadu_ps(s0 + 4 * stride),
-                   r5 = _mm256_loadu_ps(s0 + 5 * stride), r6 = _mm256_loadu_ps(s0 + 6 * stride),
-                   r7 = _mm256_loadu_ps(s0 + 7 * stride);
-            const __m256 t0 = _mm256_unpacklo_ps(r0, r1), t1 = _mm256_unpackhi_ps(r0, r1);
-            const __m256 t2 = _mm256_unpacklo_ps(r2, r3), t3 = _mm256_unpackhi_ps(r2, r3);
-            const __m256 t4 = _mm256_unpacklo_ps(r4, r5), t5 = _mm256_unpackhi_ps(r4, r5);
-            const __m256 t6 = _mm256_unpacklo_ps(r6, r7), t7 = _mm256_unpackhi_ps(r6, r7);
-            const __m256 u0 = _mm256_shuffle_ps(t0, t2, 0x44), u1 = _mm256_shuffle_ps(t0, t2, 0xEE);
-            const __m256 u2 = _mm256_shuffle_ps(t1, t3, 0x44), u3 = _mm256_shuffle_ps(t1, t3, 0xEE);
-            const __m256 u4 = _mm256_shuffle_ps(t4, t6, 0x44), u5 = _mm256_shuffle_ps(t4, t6, 0xEE);
-            const __m256 u6 = _mm256_shuffle_ps(t5, t7, 0x44), u7 = _mm256_shuffle_ps(t5, t7, 0xEE);
-            const __m256 c[8] = {_mm256_permute2f128_ps(u0, u4, 0x20), _mm256_permute2f128_ps(u1, u5, 0x20),
-                                 _mm256_permute2f128_ps(u2, u6, 0x20), _mm256_permute2f128_ps(u3, u7, 0x20),
-                                 _mm256_permute2f128_ps(u0, u4, 0x31), _mm256_permute2f128_ps(u1, u5, 0x31),
-                                 _mm256_permute2f128_ps(u2, u6, 0x31), _mm256_permute2f128_ps(u3, u7, 0x31)};
-            for (int k = 0; k < 8; ++k) {
-                _mm256_storeu_ps(static_cast<float *>(dst[8 * j + k]) + r, c[k]);
-                if (dst2) _mm256_storeu_ps(static_cast<float *>(dst2[8 * j + k]) + r, c[k]);
+    __m256 c[8], e[8];
+    if (aligned) {
+        const uint64_t head = std::min(i1, i0 + ((16 - ((row0 + i0) & 15)) & 15));  // to a 16-row boundary
+        transpose_scalar(rows, row0, i0, head, P, dst, dst2);
+        for (i = head; i + 16 <= i1; i += 16) {
+            const float *src = reinterpret_cast<const float *>(rows + i * P.R);
+            const uint64_t r = row0 + i;
+            for (int j = 0; j < nb; ++j) {
+                t8x8(src + 8 * j, stride, c);
+                t8x8(src + 8 * stride + 8 * j, stride, e);
+                for (int k = 0; k < 8; ++k) {
+                    float *d = static_cast<float *>(dst[8 * j + k]) + r;
+                    _mm256_stream_ps(d, c[k]);
+                    _mm256_stream_ps(d + 8, e[k]);
+                    if (dst2) {
+                        float *d2 = static_cast<float *>(dst2[8 * j + k]) + r;
+                        _mm256_stream_ps(d2, c[k]);
+                        _mm256_stream_ps(d2 + 8, e[k]);
+                    }
+                }
             }
+            for (int p = 8 * nb; p < np; ++p)  // the last np % 8 columns
+                for (int k = 0; k < 16; ++k) {
+                    const float v = src[k * stride + p];
+                    static_cast<float *>(dst[p])[r + k] = v;
+                    if (dst2) static_cast<float *>(dst2[p])[r + k] = v;
+                }
         }
-        for (int p = 8 * nb; p < np; ++p)  // the last np % 8 columns
-            for (int k = 0; k < 8; ++k) {
-                const float v = src[k * stride + p];
-                static_cast<float *>(dst[p])[r + k] = v;
-                if (dst2) static_cast<float *>(dst2[p])[r + k] = v;
+        _mm_sfence();  // the streaming stores are visible before the copy thread reports done
+    } else {
+        for (; i + 8 <= i1; i += 8) {
+            const float *src = reinterpret_cast<const float *>(rows + i * P.R);
+            const uint64_t r = row0 + i;
+            for (int j = 0; j < nb; ++j) {
+                t8x8(src + 8 * j, stride, c);
+                for (int k = 0; k < 8; ++k) {
+                    _mm256_storeu_ps(static_cast<float *>(dst[8 * j + k]) + r, c[k]);
+                    if (dst2) _mm256_storeu_ps(static_cast<float *>(dst2[8 * j + k]) + r, c[k]);
+                }
             }
+            for (int p = 8 * nb; p < np; ++p)
+                for (int k = 0; k < 8; ++k) {
+                    const float v = src[k * stride + p];
+                    static_cast<float *>(dst[p])[r + k] = v;
+                    if (dst2) static_cast<float *>(dst2[p])[r + k] = v;
+                }
+        }
     }
     transpose_scalar(rows, row0, i, i1, P, dst, dst2);
 }
@@ -494,9 +544,9 @@ struct HostTranspose : ChunkSink {
             try {
                 const bool vec = P.all4 && P.R == 4 * P.sz.size() && has_avx2();
                 host_parallel(c, [&](int t, int nt) {
-                    // 8-row aligned shares (the AVX2 blocks), the remainder to the last thread
-                    const uint64_t blocks = j.nr / 8, a = blocks * t / nt * 8,
-                                   e = (t == nt - 1) ? j.nr : blocks * (t + 1) / nt * 8;
+                    // 16-row shares (the AVX2 blocks' cache lines), the remainder to the last thread
+                    const uint64_t blocks = j.nr / 16, a = blocks * t / nt * 16,
+                                   e = (t == nt - 1) ? j.nr : blocks * (t + 1) / nt * 16;
                     if (vec) transpose_f32_avx2(j.rows, j.row, a, e, P, dst, dst2);
                     else transpose_scalar(j.rows, j.row, a, e, P, dst, dst2);
                 });
