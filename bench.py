@@ -1119,7 +1119,7 @@ def main(args):
     # at this launch shape; tools/pmc_traffic.sh) -- PMC counters cannot be read from inside this run
     traffic, tsrc = None, None
     def latest(name):  # the newest round's committed profile of that name
-        for rnd in ('r05', 'r04', 'r03', 'r02', 'r01'):
+        for rnd in ('r06', 'r05', 'r04', 'r03', 'r02', 'r01'):
             f = os.path.join(ROOT, 'profiles', rnd, name)
             if os.path.exists(f):
                 return f
