@@ -68,6 +68,11 @@ def parse(argv=None):
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1 (nccl = RCCL; gloo with '
                     '--dist-python rehearses several ranks on one GPU)')
+    ap.add_argument('--torch-backend', default='auto', choices=('auto', 'gloo', 'nccl'),
+                    help='the process group of bench.py\'s own between-step duties (barriers, the unique id\'s '
+                         'broadcast, the max-over-ranks timer, the verification\'s reductions); auto: gloo, except '
+                         'nccl for --dist-python (its collectives are the step\'s), so that the library\'s RCCL is the '
+                         'only one a rank initialises')
     ap.add_argument('--cpu-assign-sample', type=int, default=20_000,
                     help='points of the 1-thread KdTree assign sample (cpu_baseline)')
     ap.add_argument('--cpu-assign-sample-mt', type=int, default=100_000,
@@ -832,6 +837,17 @@ def heartbeat(period=30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+def torch_backend(args):
+    """the torch.distributed backend of a sharded run: the library carries every collective of the step
+    (its own RCCL communicators, or host shared memory under --backend gloo), so torch's process
+    group only serves bench.py between steps and runs on gloo -- torch's bundled RCCL is then
+    loaded but never initialised, and each rank runs one RCCL (st_rccl.cpp's).  --dist-python's
+    step is torch.distributed collectives: --backend there."""
+    if args.torch_backend != 'auto':
+        return args.torch_backend
+    return args.backend if args.dist_python else 'gloo'
+
+
 def main(args):
     import numpy as np
     import torch
@@ -859,7 +875,7 @@ def main(args):
     if sharded:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29533')
-        dist.init_process_group(args.backend, init_method='env://', rank=rank, world_size=world)
+        dist.init_process_group(torch_backend(args), init_method='env://', rank=rank, world_size=world)
     dev = torch.device('cuda', local)
 
     # one real stream for the library and the torch glue (st_ctx_set_stream(NULL) would select the
@@ -943,7 +959,7 @@ def main(args):
         transport = comm.transport
     else:
         rccl_ranks = world if sharded and args.backend == 'nccl' else None
-        transport = ('torch.distributed ' + args.backend) if sharded else None
+        transport = ('torch.distributed ' + torch_backend(args)) if sharded else None
     devices = None
     if sharded:
         devs = [None] * world
@@ -1194,6 +1210,7 @@ def main(args):
         'rccl_version': rccl_version,
         'rccl_path': rccl_path,
         'rccl_torch_version': rccl_torch,
+        'torch_backend': torch_backend(args) if sharded else None,
         'transport': transport,
         'side_channel': (os.environ.get('ST_SIDE_CHANNEL') != '0') if comm else None,
         'distinct_devices': devices if sharded else 1,

@@ -117,6 +117,18 @@ def test_workload_is_the_same_at_every_n():
     assert w1[0] == w8[0] and (w1[1], w8[1]) == (10_000_000, 80_000_000) and w8[2] == 'weak'
 
 
+def test_torch_process_group_is_gloo_beside_the_librarys_rccl():
+    """torch.distributed only serves bench.py between steps (barriers, the unique id, the timer, the
+    verification), so it runs on gloo and each rank initialises one RCCL: the library's
+    (st_rccl.cpp).  The torch harness (--dist-python) steps through torch collectives: its backend."""
+    import bench
+    for argv in (['--gpus', '8'], ['--gpus', '8', '--backend', 'gloo'], ['--dist'], ['--gpus', '2', '--merge', '4']):
+        assert bench.torch_backend(bench.parse(argv)) == 'gloo', argv
+    assert bench.torch_backend(bench.parse(['--gpus', '2', '--dist-python'])) == 'nccl'
+    assert bench.torch_backend(bench.parse(['--gpus', '2', '--dist-python', '--backend', 'gloo'])) == 'gloo'
+    assert bench.torch_backend(bench.parse(['--gpus', '8', '--torch-backend', 'nccl'])) == 'nccl'
+
+
 def test_table_rows_independent_of_the_split():
     """rows [lo, hi) of a T-row table built from fixed-seed blocks: any split concatenates to the
     same table (small blocks here; the bench uses 10M-row blocks)"""

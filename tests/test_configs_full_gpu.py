@@ -1,14 +1,15 @@
 """BASELINE configs 3, 4 and 5 at their full sizes on the GPU.
 
-* config 4 (write-sog.ts:110-370): ONE 50M-splat SH-3 table -> .sog with its rows sharded over 4
-  rank processes -- `bench.py --gpus 4 --backend gloo`, i.e. the launcher, one process per rank and
-  st_dev_sog_sharded over the library's host shared-memory transport (the calls of the 8-GPU job,
-  with host memory carrying the bytes RCCL would) -- against st_dev_sog of the whole table on one
-  device in this process;
+* config 4 (write-sog.ts:110-370): ONE 50M-splat SH-3 table -> .sog with its rows sharded over 8
+  rank processes (the driver's N = 8) -- `bench.py --gpus 8 --backend gloo`, i.e. the launcher, one
+  process per rank and st_dev_sog_sharded over the library's host shared-memory transport (the
+  calls of the 8-GPU job, with host memory carrying the bytes RCCL would; both channels issued in
+  RCCL's program order, ST_SIDE_INLINE=1, and the eight ranks' collective sequences identical) --
+  against st_dev_sog of the whole table on one device in this process;
 * config 5 (index.ts:158-210 + write-sog.ts): four 10M-splat inputs (seeds 5001..5004) combined
-  in file order, Morton-ordered and written as one .sog, its 40M rows split over 3 rank processes
-  so that ranks cut across the input files -- against combine (st_dev_combine) + st_dev_sog on
-  one device;
+  in file order, Morton-ordered and written as one .sog, its 40M rows split over 8 rank processes
+  (5M each: odd ranks end inside an input file, even ranks on a file boundary) -- against combine
+  (st_dev_combine) + st_dev_sog on one device;
 * config 3 (process.ts:64-145, write-compressed-ply.ts:56-114): 10M SH-3 splats, -r 0,45,0 then
   filterNaN (0.1% of the rows non-finite), Morton order and chunk pack through
   st_dev_compressed_ply, bit-exact against the oracle's chain (oracle/st_oracle.c).
@@ -91,10 +92,30 @@ def _check_one_device(ver, total):
     assert ver['labels_wrong'] == 0 and ver['centroid_values_wrong'] == 0, ver
 
 
-def test_config4_50m_in_four_processes_matches_one_gpu():
+WORLD = 8
+
+
+def _bench_traced(args, tmp_path, monkeypatch):
+    """`bench.py --gpus 8 --backend gloo` + args with both channels issued from the main thread
+    (RCCL's program order) and each rank's collective sequence logged; returns the line and
+    asserts that the eight sequences are identical"""
+    d = tmp_path / 'trace'
+    d.mkdir()
+    monkeypatch.setenv('ST_SIDE_INLINE', '1')
+    monkeypatch.setenv('ST_COLL_TRACE', str(d))
+    res = _bench(['--gpus', str(WORLD), '--backend', 'gloo'] + args)
+    monkeypatch.delenv('ST_COLL_TRACE')
+    monkeypatch.delenv('ST_SIDE_INLINE')
+    tr = [open(d / f'coll_rank{r}.txt').read().splitlines() for r in range(WORLD)]
+    assert tr[0] and all(t == tr[0] for t in tr), [len(t) for t in tr]
+    return res
+
+
+def test_config4_50m_in_eight_processes_matches_one_gpu(tmp_path, monkeypatch):
     T = 50_000_000
-    four = _bench(['--gpus', '4', '--backend', 'gloo', '--total-splats', str(T)])
-    _check_sharded(four, 4, T)
+    eight = _bench_traced(['--total-splats', str(T)], tmp_path, monkeypatch)
+    _check_sharded(eight, WORLD, T)
+    assert eight['config']['splats_rank0'] == T // WORLD
     import torch
 
     import bench
@@ -102,15 +123,15 @@ def test_config4_50m_in_four_processes_matches_one_gpu():
     sha, ver = _one_device(table)
     del table
     _check_one_device(ver, T)
-    assert sha == four['textures_sha256']
+    assert sha == eight['textures_sha256']
 
 
-def test_config5_merge_4x10m_in_three_processes_matches_one_gpu():
+def test_config5_merge_4x10m_in_eight_processes_matches_one_gpu(tmp_path, monkeypatch):
     F, S = 4, 10_000_000
-    three = _bench(['--gpus', '3', '--backend', 'gloo', '--merge', str(F)])
-    _check_sharded(three, 3, F * S)
-    # rank r holds rows [40M r / 3, 40M (r + 1) / 3): ranks 0 and 1 each end inside an input file
-    assert three['config']['splats_rank0'] == F * S // 3
+    eight = _bench_traced(['--merge', str(F)], tmp_path, monkeypatch)
+    _check_sharded(eight, WORLD, F * S)
+    # rank r holds rows [5M r, 5M (r + 1)): the odd ranks end inside an input file
+    assert eight['config']['splats_rank0'] == F * S // WORLD
     import torch
 
     import bench
@@ -131,7 +152,7 @@ def test_config5_merge_4x10m_in_three_processes_matches_one_gpu():
     sha, ver = _one_device(dict(dst))
     del dst
     _check_one_device(ver, F * S)
-    assert sha == three['textures_sha256']
+    assert sha == eight['textures_sha256']
 
 
 def test_config3_10m_compressed_ply_vs_oracle():

@@ -12,9 +12,12 @@
 #   configs  BASELINE configs 3/4/5 at full size and the world-8 rehearsal (shared memory)
 #   dist     st_dev_sog against the sharded path at world 1 (--dist), interleaved, at an 8-way
 #            rank's 1.25M rows and at 10M (wall time per step)
+#   dist1    the sharded path at world 1 (one-rank RCCL communicator, torch's process group on gloo)
+#            at an 8-way rank's 1.25M rows, verified
 #   stats    the N-D assign classification on Gaussian and heavy-tailed SH at 10M (kn_bench)
 #   quick    a k-means test selection + kn_bench timings (a quick check of a kernel change)
-#   ab       interleaved bench steps of tools/var/base.so against tools/var/new.so (ST_LIB)
+#   ab       interleaved bench steps of tools/ab/base.so against tools/ab/new.so (ST_LIB; $AB_ARGS
+#            extra bench.py arguments, e.g. --total-splats 1250000)
 #   node     the Node drop-in's PLY -> .sog job with phase stamps (tools/node_probe.py)
 #   read     readPly's host form under its settings (tools/read_probe.py)
 #   paths    the config-3 stage table and file paths (tools/bench_paths.py)
@@ -71,6 +74,12 @@ print('realistic', rr.get('ms_per_step'), rr.get('vs_main_step'), rr.get('verifi
         done
       done
     done ;;
+  dist1)
+    timeout -k 10 300 python3 bench.py --dist --total-splats 1250000 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+      --no-paths --no-extra > ${O}_dist1.json 2> ${O}_dist1.err || fail dist1 ${O}_dist1.err
+    python3 -c "
+import json; r = json.load(open('${O}_dist1.json'))
+print('dist1', round(r['ms_per_step'], 2), r['transport'], r['torch_backend'], r['rccl_version'], r['verified'])" ;;
   stats)
     for d in gauss t3; do
       timeout -k 10 300 python3 tools/kn_bench.py --n 10000000 --iters 3 --dist $d > ${O}_stats_$d.txt 2>&1 \
@@ -90,9 +99,9 @@ print('realistic', rr.get('ms_per_step'), rr.get('vs_main_step'), rr.get('verifi
   ab)
     for i in 1 2 3 4; do
       for v in base new; do
-        ST_LIB=tools/var/$v.so timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
-          --no-paths --no-extra --no-verify > ${O}_ab_$v$i.json 2> ${O}_ab_$v$i.err || fail ab ${O}_ab_$v$i.err
-        python3 -c "import json; b=json.load(open('${O}_ab_$v$i.json')); print('$v', $i, round(b['ms_per_step'], 2), b['textures_sha256'][:12])"
+        ST_LIB=tools/ab/$v.so timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
+          --no-paths --no-extra --no-verify $AB_ARGS > ${O}_ab_$v$i.json 2> ${O}_ab_$v$i.err || fail ab ${O}_ab_$v$i.err
+        python3 -c "import json; b=json.load(open('${O}_ab_$v$i.json')); k=b['kernels']; print('$v', $i, round(b['ms_per_step'], 2), b['textures_sha256'][:12], 'fixrow', round(k['kn.fixrow']['avg_ms'], 3), 'sweep', round(k['kn.sweep']['avg_ms'], 2))"
       done
     done ;;
   node)
