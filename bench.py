@@ -497,7 +497,8 @@ def node_end_to_end(ctx, src, dst, n, iters, reps, draws, tex, meta):
     runs = sorted(out['runs'], key=lambda x: x['total'])
     med = runs[len(runs) // 2]
     return {'what': 'node tools/bench_node.js: readPly(FileHandle) -> host DataTable -> writeSogFile(FileHandle) '
-                    '(js/index.js over napi/addon.node: st_ply_read + st_sog_file), median of the timed reps; '
+                    '(js/index.js over napi/addon.node: st_ply_read_resident + st_sog_file; the columns JS never reads stay '
+                    'in HBM), median of the timed reps; '
                     'Math.random = the bench\'s draw stream, Date pinned; global.gc() between reps (untimed), so '
                     'every rep\'s columns reuse the addon\'s faulted-in blocks',
             'ms': med['total'], 'Msplats_per_s': n / med['total'] / 1e3,

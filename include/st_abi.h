@@ -39,6 +39,8 @@
  *   st_sog_bundle / st_dev_sog_bundle       writeSog to a .sog bundle           write-sog.ts:110-140,361-366
  *   st_ply_read_header / _parse_header      readPly header search + parseHeader readers/read-ply.ts:54-137
  *   st_ply_read / st_dev_ply_read           readPly element rows -> columns     read-ply.ts:139-188
+ *   st_ply_read_resident (+ _materialize,   readPly, the values left in HBM     read-ply.ts:111-191
+ *     _forget)                              until the host asks for them
  *   st_dev_ply_transpose                    (the same, rows already in HBM)     read-ply.ts:165-182
  *   st_decompress_ply / st_dev_...          decompressPly                       readers/decompress-ply.ts:82-232
  *   st_process                              processDataTable(dataTable, actions) process.ts:64-145
@@ -540,6 +542,19 @@ int st_dev_ply_transpose(st_ctx *ctx, const st_ply_header *h, int32_t element, c
 int st_dev_ply_read(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, void *const *cols);
 /* the same into host columns (readPly's TypedArrays) */
 int st_ply_read(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, void *const *host_cols);
+/* readPly with the values left in HBM (replaces read-ply.ts:111-191 for a host that defers the
+ * host copy): element `element` goes to the device columns only, and host_cols are registered
+ * as that element's lazy columns -- their memory is NOT written until st_ply_materialize.  The
+ * writeSog host forms (st_sog, st_sog_bundle, st_sog_file) given a lazy column run on its device
+ * copy directly; every other host form copies it down first.  Each lazy column holds a device
+ * block of its own until it is materialized or st_ply_forget-ten (later reads do not touch it);
+ * the caller keeps the host column alive until then. */
+int st_ply_read_resident(st_ctx *ctx, int32_t fd, const st_ply_header *h, int32_t element, void *const *host_cols);
+/* a lazy column's values copied into its host memory (then an ordinary host column: the caller
+ * may change it); no-op for any other pointer */
+int st_ply_materialize(st_ctx *ctx, const void *host_col);
+/* drop the lazy or mirrored column at host_col without copying (its memory is being released) */
+int st_ply_forget(st_ctx *ctx, const void *host_col);
 /* decompressPly: chunk = the 18 float columns min_x..max_b in decompress-ply.ts:14-33 order,
  * vertex = packed_position, packed_rotation, packed_scale, packed_color; sh = nsh (0/9/24/45)
  * uint8 f_rest columns; out = x y z f_dc_0..2 opacity rot_0..3 scale_0..2 then f_rest_0.. */

@@ -21,6 +21,7 @@ struct DevTable {
     std::vector<const char *> cnames;
     std::vector<float *> cols;
     st_table t{};
+    uint64_t resident = 0;  // columns read where they already were in HBM (resident_table)
 };
 
 // host <-> device transfers of one call, moved together through the staged copies
@@ -96,13 +97,17 @@ std::vector<std::string> transform_columns() {
     return v;
 }
 
-// ---- writeSog host forms on st_ply_read's mirrors --------------------------------------------
-// A host table whose every column writeSog reads is one st_ply_read filled (st_ctx::HostMirror)
-// is not uploaded: the step runs on the resident device columns at once, while host threads
-// compare the caller's columns with their pinned twins byte for byte (memcmp, ~4.7 GB read at
-// 10M splats, beside the step).  Nothing leaves the device (no file write, no host output) until
-// the compare has said "equal"; a changed byte raises spec_abort (the SH k-means stops at its
-// next iteration), the call waits for its queued work, uploads the columns and runs again.
+// ---- writeSog host forms on resident columns (st_ctx::HostMirror) ---------------------------
+// A column writeSog reads that is resident in HBM is not uploaded:
+//  * a lazy column (st_ply_read_resident: its host memory was never filled) is read on the
+//    device as it is -- its values exist nowhere else;
+//  * a mirrored column (st_ply_read filled it and a host twin) is read on the device while host
+//    threads compare the caller's column with the twin byte for byte (memcmp, ~4.7 GB read at
+//    10M splats, beside the step).  Nothing leaves the device (no file write, no host output) until
+//    the compare has said "equal"; a changed byte raises spec_abort (the SH k-means stops at its
+//    next iteration), the call waits for its queued work and runs again with those columns
+//    uploaded.
+// Every other column is uploaded.
 struct Spec {
     st_ctx *c;
     std::atomic<bool> abort{false};
@@ -125,58 +130,102 @@ struct Spec {
     }
 };
 
-const st_ctx::HostMirror *find_mirror(st_ctx *c, const void *host, uint64_t bytes) {
-    for (const auto &m : c->mirrors)
-        if (m.host == host && m.bytes == bytes) return &m;
-    return nullptr;
-}
-
-// the wanted float columns of h, all mirrored: d holds their device twins and the compare runs
-// on sp's threads; false (nothing started) when any one is not a mirror
-bool mirror_table(st_ctx *c, const st_table *h, const std::vector<std::string> &want, DevTable &d, Spec &sp) {
+// the wanted float columns of h on the device: resident ones as they are (mirrored ones under sp's
+// compare; without sp they are uploaded like the rest), the others uploaded into `tag` slots.
+// False (nothing done) when none is resident.  d.resident counts the columns not uploaded.
+bool resident_table(st_ctx *c, const st_table *h, const std::vector<std::string> &want, DevTable &d, Spec *sp,
+                    const std::string &tag) {
     const char *mo = getenv("ST_HOST_MIRROR");
-    if ((mo && std::strcmp(mo, "0") == 0) || c->mirrors.empty() || !h->n) return false;
-    std::vector<const st_ctx::HostMirror *> ms;
+    const bool compare_ok = sp && !(mo && std::strcmp(mo, "0") == 0);
+    std::lock_guard<std::mutex> lk(c->mirror_mu);
+    if (c->mirrors.empty() || !h->n) return false;
+    std::vector<int> src;
+    std::vector<st_ctx::HostMirror> ms;  // copies: the list may change once the lock is released
+    bool any = false;
     for (int i = 0; i < h->ncol; ++i) {
         bool hit = want.empty();
         for (auto &w : want) hit = hit || (w == h->names[i]);
         if (!hit) continue;
-        const auto *m = find_mirror(c, h->cols[i], h->n * sizeof(float));
-        if (!m) return false;
-        d.names.push_back(h->names[i]);
-        d.cols.push_back(static_cast<float *>(const_cast<void *>(m->dev)));
+        st_ctx::HostMirror m{};
+        for (const auto &x : c->mirrors)
+            if (x.host == h->cols[i] && x.bytes == h->n * sizeof(float) && (x.lazy || compare_ok)) m = x;
+        any = any || m.host;
+        src.push_back(i);
         ms.push_back(m);
+    }
+    if (!any) return false;
+    // a column read from host memory that lies inside a lazy one (a view of it) is copied down first
+    {
+        std::vector<HostXfer> down;
+        std::vector<const void *> gone;
+        for (size_t j = 0; j < src.size(); ++j) {
+            if (ms[j].host) continue;
+            const char *a = static_cast<const char *>(static_cast<const void *>(h->cols[src[j]]));
+            for (const auto &x : c->mirrors) {
+                const char *b = static_cast<const char *>(x.host);
+                if (x.lazy && a < b + x.bytes && b < a + h->n * sizeof(float)) {
+                    down.push_back(HostXfer{const_cast<void *>(x.host), const_cast<void *>(x.dev), (size_t)x.bytes});
+                    gone.push_back(x.host);
+                }
+            }
+        }
+        if (!down.empty()) {
+            staged_d2h_raw(c, down);
+            drop_mirrors_locked(c, [&](const st_ctx::HostMirror &x) {
+                return std::find(gone.begin(), gone.end(), x.host) != gone.end();
+            });
+        }
+    }
+    Batch up{c};
+    std::vector<std::pair<const char *, const char *>> blocks;  // the compare: 1 MiB blocks
+    std::vector<uint64_t> lens;
+    constexpr uint64_t BLK = 1ull << 20;
+    for (size_t j = 0; j < src.size(); ++j) {
+        d.names.push_back(h->names[src[j]]);
+        const auto &m = ms[j];
+        if (!m.host) {
+            float *p = wsT<float>(c, tag + std::to_string(j), h->n);
+            up.v.push_back(HostXfer{static_cast<void *>(h->cols[src[j]]), p, h->n * sizeof(float)});
+            d.cols.push_back(p);
+            continue;
+        }
+        d.cols.push_back(static_cast<float *>(const_cast<void *>(m.dev)));
+        ++d.resident;
+        if (!m.lazy)
+            for (uint64_t o = 0; o < m.bytes; o += BLK) {
+                blocks.emplace_back(static_cast<const char *>(m.host) + o, static_cast<const char *>(m.shadow) + o);
+                lens.push_back(std::min(BLK, m.bytes - o));
+            }
+    }
+    if (!up.v.empty()) {
+        std::vector<HostXfer> v;
+        v.swap(up.v);
+        // (the lock is held: staged_h2d's own bookkeeping would take it again, and these sources are
+        // not lazy -- the lazy ones are read on the device)
+        staged_h2d_raw(c, v);
     }
     for (auto &s : d.names) d.cnames.push_back(s.c_str());
     d.t.n = h->n;
     d.t.ncol = (int32_t)d.names.size();
     d.t.names = d.cnames.data();
     d.t.cols = d.cols.data();
-    // the compare: the columns' bytes cut into 1 MiB blocks dealt round-robin to the threads
-    constexpr uint64_t BLK = 1ull << 20;
-    std::vector<std::pair<const char *, const char *>> blocks;
-    std::vector<uint64_t> lens;
-    for (const auto *m : ms)
-        for (uint64_t o = 0; o < m->bytes; o += BLK) {
-            blocks.emplace_back(static_cast<const char *>(m->host) + o, static_cast<const char *>(m->shadow) + o);
-            lens.push_back(std::min(BLK, m->bytes - o));
-        }
+    if (blocks.empty()) return true;
     const int nt = std::max(1, std::min(16, getenv("ST_MIRROR_THREADS") ? atoi(getenv("ST_MIRROR_THREADS")) : 8));
     auto shared = std::make_shared<std::pair<decltype(blocks), decltype(lens)>>(std::move(blocks), std::move(lens));
     for (int t = 0; t < nt; ++t)
-        sp.th.emplace_back([&sp, shared, t, nt] {
+        sp->th.emplace_back([sp, shared, t, nt] {
             const auto &bl = shared->first;
             const auto &ln = shared->second;
             for (size_t b = (size_t)t; b < bl.size(); b += (size_t)nt) {
-                if (sp.abort.load(std::memory_order_relaxed)) return;
+                if (sp->abort.load(std::memory_order_relaxed)) return;
                 if (std::memcmp(bl[b].first, bl[b].second, ln[b]) != 0) {
-                    sp.abort.store(true);
+                    sp->abort.store(true);
                     return;
                 }
             }
         });
-    c->spec_abort = &sp.abort;
-    c->spec_verdict = [&sp] { return sp.verdict(); };
+    c->spec_abort = &sp->abort;
+    c->spec_verdict = [sp] { return sp->verdict(); };
     return true;
 }
 
@@ -189,15 +238,15 @@ void drain_ctx(st_ctx *c) {
     }
 }
 
-// body(dev_table) on the mirrors when possible (spec_gate inside body before any output leaves
-// the device), else -- or when the host columns changed -- on an upload
+// body(dev_table) on the resident columns when there are any (spec_gate inside body before any
+// output leaves the device), else -- or when a mirrored column changed -- with those uploaded
 template <typename F>
 void run_host_sog(st_ctx *c, const st_table *t, const std::vector<std::string> &want, const std::string &tag, F &&body) {
     c->last_reuse_cols = c->last_reuse_bytes = 0;
     {
         DevTable d;
         Spec sp(c);
-        if (mirror_table(c, t, want, d, sp)) {
+        if (resident_table(c, t, want, d, &sp, tag)) {
             std::exception_ptr err;
             try {
                 body(&d.t);
@@ -206,11 +255,20 @@ void run_host_sog(st_ctx *c, const st_table *t, const std::vector<std::string> &
             }
             if (sp.verdict()) {
                 if (err) std::rethrow_exception(err);
-                c->last_reuse_cols = d.cols.size();
-                c->last_reuse_bytes = d.cols.size() * t->n * sizeof(float);
+                c->last_reuse_cols = d.resident;
+                c->last_reuse_bytes = d.resident * t->n * sizeof(float);
                 return;
             }
             drain_ctx(c);
+        }
+    }
+    {
+        DevTable d;
+        if (resident_table(c, t, want, d, nullptr, tag)) {  // lazy columns still from HBM
+            body(&d.t);
+            c->last_reuse_cols = d.resident;
+            c->last_reuse_bytes = d.resident * t->n * sizeof(float);
+            return;
         }
     }
     DevTable d = upload(c, t, want, tag);

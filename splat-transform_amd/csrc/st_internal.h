@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -167,18 +168,31 @@ struct st_ctx {
     bool verify = false;
     int vf_d = 0, vf_k = 0;
     uint64_t vf_n = 0;
-    // the host columns the last st_ply_read filled, with their device columns (workspace slots
-    // "plyh.c<p>", still resident) and pinned host twins (every byte as the device copy has it).
-    // The writeSog host forms run on `dev` when every column they read is here, while other
-    // threads compare `host` with `shadow` (exact: memcmp); a changed byte sends the call back to
-    // an upload (st_host_api.hip).  Dropped by the next st_ply_read.  ST_HOST_MIRROR=0: off.
+    // host columns whose values are also resident in HBM (workspace slots "plyh.e<element>.c<p>"):
+    //  * st_ply_read filled `host` and a host twin `shadow` (every byte as the device copy has it):
+    //    the writeSog host forms run on `dev` while other threads compare `host` with `shadow`
+    //    (exact: memcmp); a changed byte sends the call back to an upload (st_host_api.hip).  The
+    //    twins share one buffer: dropped by the next st_ply_read.  ST_HOST_MIRROR=0: off.
+    //  * st_ply_read_resident left `host` unfilled (`lazy`): the values exist only in `dev`, a device
+    //    block of the mirror's own (`dev_bytes`), until st_ply_materialize copies them down (the
+    //    mirror is then dropped: the caller may change them).  The writeSog host forms read `dev`
+    //    directly; every other host form materializes first (the staged copies' bookkeeping).
+    //    st_ply_forget drops one whose host memory goes away.  A dropped mirror's block goes to
+    //    dev_pool for the next resident read's columns of the same size (freed with the context).
+    // mirror_mu guards the list and the pool (the Node addon's finalizers call st_ply_forget from
+    // any thread).
     struct HostMirror {
         const void *host;
         uint64_t bytes;
-        const void *shadow;
+        const void *shadow;  // null when lazy
         const void *dev;
+        int element;
+        bool lazy;
+        uint64_t dev_bytes;  // > 0: dev is this mirror's own block (lazy), returned to dev_pool when dropped
     };
     std::vector<HostMirror> mirrors;
+    std::vector<std::pair<void *, uint64_t>> dev_pool;
+    std::mutex mirror_mu;
     void *shadow = nullptr;  // the mirrors' host twins (pageable, huge pages, grow-only)
     size_t shadow_bytes = 0;
     // set while a host form runs on mirrors: the compare raises *spec_abort on a mismatch (the
@@ -211,6 +225,12 @@ struct HostXfer {
 };
 void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs);
 void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs);
+void staged_h2d_raw(st_ctx *c, const std::vector<HostXfer> &xs);  // without the mirrors' bookkeeping
+void staged_d2h_raw(st_ctx *c, const std::vector<HostXfer> &xs);  // without the mirrors' bookkeeping
+// st_ctx::HostMirror bookkeeping of the staged copies (st_ply.hip): lazy sources are copied down
+// before an upload reads them; overwritten destinations stop being mirrors
+void mirrors_before_h2d(st_ctx *c, const std::vector<HostXfer> &xs);
+void mirrors_before_d2h(st_ctx *c, const std::vector<HostXfer> &xs);
 // host-side copy over the context's copy threads (large copies split; small ones inline)
 void host_copy(st_ctx *c, char *dst, const char *src, size_t bytes);
 // fn(t, nt) on each of the context's nt copy threads; returns when all are done
@@ -356,7 +376,12 @@ struct ChunkSink {
 void ply_read_dev(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *cols,
                   ChunkSink *sink = nullptr);
 // st_ply_read: into the caller's host columns, and the element's mirrors (st_ctx::HostMirror)
-void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols);
+void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols, bool lazy = false);
+// st_ply_materialize: the lazy mirrors among these host columns copied down and dropped (upload()
+// calls it first: no host form reads an unfilled column)
+void materialize_lazy(st_ctx *c, const void *const *host, int n);
+// (mirror_mu held) the mirrors `pick` selects removed, their own device blocks pooled
+void drop_mirrors_locked(st_ctx *c, const std::function<bool(const st_ctx::HostMirror &)> &pick);
 void decompress_ply_dev(st_ctx *c, uint64_t n, const float *const *chunk, const uint32_t *const *vertex,
                         const uint8_t *const *sh, int nsh, float *const *out);
 

@@ -586,13 +586,96 @@ struct HostTranspose : ChunkSink {
 
 }  // namespace
 
-void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols) {
-    c->mirrors.clear();  // their device slots and host twins are overwritten below
+// the mirrors `pick` selects dropped, the lazy ones among them first copied down into their host
+// columns
+void materialize_where(st_ctx *c, const std::function<bool(const st_ctx::HostMirror &)> &pick) {
+    std::vector<HostXfer> xs;
+    std::lock_guard<std::mutex> lk(c->mirror_mu);
+    if (c->mirrors.empty()) return;
+    for (const auto &m : c->mirrors)
+        if (pick(m) && m.lazy && m.bytes)
+            xs.push_back(HostXfer{const_cast<void *>(m.host), const_cast<void *>(m.dev), (size_t)m.bytes});
+    if (!xs.empty()) staged_d2h_raw(c, xs);
+    drop_mirrors_locked(c, pick);
+}
+
+// (mirror_mu held) the mirrors `pick` selects removed; their own device blocks go to the pool
+void drop_mirrors_locked(st_ctx *c, const std::function<bool(const st_ctx::HostMirror &)> &pick) {
+    std::vector<st_ctx::HostMirror> keep;
+    for (const auto &m : c->mirrors) {
+        if (!pick(m)) {
+            keep.push_back(m);
+            continue;
+        }
+        if (m.dev_bytes) c->dev_pool.emplace_back(const_cast<void *>(m.dev), m.dev_bytes);
+    }
+    c->mirrors.swap(keep);
+}
+
+// (mirror_mu held) a device block of `bytes` for a resident column: a pooled one of that size, or
+// a new one (the pool is trimmed to ST_PLY_POOL_MB, default 16384, first)
+void *resident_block_locked(st_ctx *c, uint64_t bytes) {
+    for (size_t i = c->dev_pool.size(); i-- > 0;)
+        if (c->dev_pool[i].second == bytes) {
+            void *p = c->dev_pool[i].first;
+            c->dev_pool.erase(c->dev_pool.begin() + (long)i);
+            return p;
+        }
+    static const uint64_t cap = (uint64_t)(getenv("ST_PLY_POOL_MB") ? atoll(getenv("ST_PLY_POOL_MB")) : 16384) << 20;
+    uint64_t held = 0;
+    for (auto &b : c->dev_pool) held += b.second;
+    while (!c->dev_pool.empty() && held + bytes > cap) {
+        held -= c->dev_pool.front().second;
+        ST_HIP(hipFree(c->dev_pool.front().first));
+        c->dev_pool.erase(c->dev_pool.begin());
+    }
+    void *p = nullptr;
+    ST_HIP(hipMalloc(&p, bytes));
+    return p;
+}
+
+bool overlaps(const st_ctx::HostMirror &m, const void *p, size_t bytes) {
+    const char *a = static_cast<const char *>(m.host), *b = static_cast<const char *>(p);
+    return bytes && m.bytes && b < a + m.bytes && a < b + bytes;
+}
+
+void materialize_lazy(st_ctx *c, const void *const *host, int n) {
+    materialize_where(c, [&](const st_ctx::HostMirror &m) {
+        if (!m.lazy) return false;
+        for (int i = 0; i < n; ++i)
+            if (host[i] == m.host) return true;
+        return false;
+    });
+}
+
+// staged_h2d's sources: a lazy column about to be read from host memory is copied down first
+void mirrors_before_h2d(st_ctx *c, const std::vector<HostXfer> &xs) {
+    materialize_where(c, [&](const st_ctx::HostMirror &m) {
+        if (!m.lazy) return false;
+        for (const auto &x : xs)
+            if (overlaps(m, x.host, x.bytes)) return true;
+        return false;
+    });
+}
+
+// staged_d2h's destinations: a host column about to be overwritten is no longer its device copy's
+// mirror (lazy or not: dropped without copying)
+void mirrors_before_d2h(st_ctx *c, const std::vector<HostXfer> &xs) {
+    std::lock_guard<std::mutex> lk(c->mirror_mu);
+    if (c->mirrors.empty()) return;
+    drop_mirrors_locked(c, [&](const st_ctx::HostMirror &m) {
+        for (const auto &x : xs)
+            if (overlaps(m, x.host, x.bytes)) return true;
+        return false;
+    });
+}
+
+void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void *const *host_cols, bool lazy) {
     const st_ply_element &el = h.elements[element];
     const int np = el.nprops;
     Props P;
     std::vector<void *> dcols(np), twins(np);
-    std::vector<uint64_t> toff(np);
+    std::vector<uint64_t> toff(np), dbytes(np);
     uint64_t total = 0;
     for (int p = 0; p < np; ++p) {
         const uint32_t z = (uint32_t)type_size(el.props[p].type);
@@ -600,10 +683,57 @@ void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void 
         P.sz.push_back(z);
         P.R += z;
         P.all4 = P.all4 && z == 4;
-        dcols[p] = ws(c, "plyh.c" + std::to_string(p), el.count * z + 8);
+        dbytes[p] = el.count * z + 8;
         toff[p] = total;
         total += (el.count * z + 63) / 64 * 64;
     }
+    if (lazy) {
+        // the rows go up and are transposed in HBM only, into blocks of the columns' own (no other
+        // read reuses them); the host columns stay unfilled until st_ply_materialize (or a host form
+        // other than writeSog's) asks for them
+        {
+            std::lock_guard<std::mutex> lk(c->mirror_mu);
+            for (int p = 0; p < np; ++p) dcols[p] = el.count ? resident_block_locked(c, dbytes[p]) : nullptr;
+        }
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        try {
+            if (el.count) ply_read_dev(c, fd, h, element, dcols.data(), nullptr);
+            ST_HIP(hipStreamSynchronize(c->stream));
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(c->mirror_mu);
+            for (int p = 0; p < np; ++p)
+                if (dcols[p]) c->dev_pool.emplace_back(dcols[p], dbytes[p]);
+            throw;
+        }
+        if (std::getenv("ST_DEBUG"))
+            fprintf(stderr, "[st ply read] %.1f MB: device columns %.1f ms (host columns resident)\n", total / 1e6,
+                    std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+        std::lock_guard<std::mutex> lk(c->mirror_mu);
+        // a host column registered before at the same address (its memory reused) is not that one
+        drop_mirrors_locked(c, [&](const st_ctx::HostMirror &m) {
+            for (int p = 0; p < np; ++p)
+                if (m.host == host_cols[p]) return true;
+            return false;
+        });
+        for (int p = 0; p < np; ++p)
+            c->mirrors.push_back({host_cols[p], el.count * P.sz[p], nullptr, dcols[p], element, true,
+                                  dcols[p] ? dbytes[p] : 0});
+        return;
+    }
+    // an eager read overwrites this element's device slots and the shared host twins: every other
+    // eager mirror goes (the resident ones keep blocks of their own)
+    {
+        std::lock_guard<std::mutex> lk(c->mirror_mu);
+        drop_mirrors_locked(c, [&](const st_ctx::HostMirror &m) {
+            if (!m.lazy) return true;
+            for (int p = 0; p < np; ++p)
+                if (m.host == host_cols[p]) return true;
+            return false;
+        });
+    }
+    for (int p = 0; p < np; ++p)
+        dcols[p] = ws(c, "plyh.e" + std::to_string(element) + ".c" + std::to_string(p), dbytes[p]);
     const char *mo = std::getenv("ST_HOST_MIRROR");
     const bool mirror = !(mo && std::strcmp(mo, "0") == 0) && el.count && np;
     if (mirror && c->shadow_bytes < total) {
@@ -628,8 +758,11 @@ void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void 
         fprintf(stderr, "[st ply read] %.1f MB: device and host columns %.1f ms (%s host transpose)\n", total / 1e6,
                 std::chrono::duration<double, std::milli>(clk::now() - t0).count(),
                 P.all4 && P.R == 4 * (uint32_t)np && has_avx2() ? "AVX2" : "scalar");
-    if (mirror)
-        for (int p = 0; p < np; ++p) c->mirrors.push_back({host_cols[p], el.count * P.sz[p], twins[p], dcols[p]});
+    if (mirror) {
+        std::lock_guard<std::mutex> lk(c->mirror_mu);
+        for (int p = 0; p < np; ++p)
+            c->mirrors.push_back({host_cols[p], el.count * P.sz[p], twins[p], dcols[p], element, false});
+    }
 }
 
 }  // namespace st
@@ -690,6 +823,33 @@ int st_ply_read(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, 
                    "bad argument");
         use_device(c);
         ply_read_host(c, fd, *h, element, host_cols);
+    });
+}
+
+int st_ply_read_resident(st_ctx *c, int32_t fd, const st_ply_header *h, int32_t element, void *const *host_cols) {
+    return guard([&] {
+        ST_REQUIRE(c && h && host_cols && fd >= 0 && element >= 0 && element < h->nelements, ST_ERR_ARG,
+                   "bad argument");
+        for (int32_t p = 0; p < h->elements[element].nprops; ++p)
+            ST_REQUIRE(host_cols[p] || !h->elements[element].count, ST_ERR_ARG, "ply: NULL host column");
+        use_device(c);
+        ply_read_host(c, fd, *h, element, host_cols, true);
+    });
+}
+
+int st_ply_materialize(st_ctx *c, const void *host_col) {
+    return guard([&] {
+        ST_REQUIRE(c, ST_ERR_ARG, "NULL context");
+        use_device(c);
+        if (host_col) materialize_lazy(c, &host_col, 1);
+    });
+}
+
+int st_ply_forget(st_ctx *c, const void *host_col) {
+    return guard([&] {
+        ST_REQUIRE(c, ST_ERR_ARG, "NULL context");
+        std::lock_guard<std::mutex> lk(c->mirror_mu);
+        drop_mirrors_locked(c, [&](const st_ctx::HostMirror &m) { return m.host == host_col; });
     });
 }
 

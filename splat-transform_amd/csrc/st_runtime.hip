@@ -219,6 +219,11 @@ struct XferLog {
 };
 
 void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs) {
+    mirrors_before_h2d(c, xs);
+    staged_h2d_raw(c, xs);
+}
+
+void staged_h2d_raw(st_ctx *c, const std::vector<HostXfer> &xs) {
     XferLog log{"h2d", xs};
     std::vector<Piece> ps = pieces_of(c, xs, true);
     if (!ps.empty()) {
@@ -238,6 +243,11 @@ void staged_h2d(st_ctx *c, const std::vector<HostXfer> &xs) {
 }
 
 void staged_d2h(st_ctx *c, const std::vector<HostXfer> &xs) {
+    mirrors_before_d2h(c, xs);
+    staged_d2h_raw(c, xs);
+}
+
+void staged_d2h_raw(st_ctx *c, const std::vector<HostXfer> &xs) {
     XferLog log{"d2h", xs};
     std::vector<Piece> ps = pieces_of(c, xs, false);
     if (!ps.empty()) {
@@ -436,6 +446,9 @@ void st_ctx_destroy(st_ctx *c) {
     if (c->archive) (void)hipHostFree(c->archive);
     if (c->io) (void)hipHostFree(c->io);
     std::free(c->shadow);
+    for (auto &m : c->mirrors)
+        if (m.dev_bytes) (void)hipFree(const_cast<void *>(m.dev));
+    for (auto &b : c->dev_pool) (void)hipFree(b.first);
     if (c->xfer) (void)hipHostFree(c->xfer);
     for (auto &kv : c->pinned_slots)
         if (kv.second.first) (void)hipHostFree(kv.second.first);

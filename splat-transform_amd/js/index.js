@@ -43,17 +43,47 @@ class Column {
     }
 }
 
+// A readPly column whose values are still only in HBM (the addon's resident read): its memory is
+// allocated but unfilled, and `data` copies the values down on first access (addon.materialize),
+// after which it is an ordinary own property.  Until then nothing in JS holds the array, so it is
+// unchanged by construction and writeSogFile runs on the device copy (st_sog_file: no upload, no
+// compare).  Assigning `data` drops the resident copy.
+const kResident = Symbol('splat-hip resident column');
+const residentColumn = (name, ta) => {
+    const c = new Column(name, ta);
+    const settle = (v) => {
+        delete c[kResident];
+        Object.defineProperty(c, 'data', { value: v, writable: true, enumerable: true, configurable: true });
+    };
+    c[kResident] = ta;
+    Object.defineProperty(c, 'data', {
+        enumerable: true,
+        configurable: true,
+        get() {
+            addon.materialize(ta);
+            settle(ta);
+            return ta;
+        },
+        set(v) { settle(v); }
+    });
+    return c;
+};
+// the column's array without copying a resident one down (only for writeSogFile, which reads
+// resident columns on the device; every other host form would copy them down anyway)
+const deviceOrHost = c => (c[kResident] !== undefined ? c[kResident] : c.data);
+const rowsOf = c => deviceOrHost(c).length;
+
 class DataTable {
     constructor(columns) {
         if (columns.length === 0) throw new Error('DataTable must have at least one column');
         for (let i = 1; i < columns.length; ++i) {
-            if (columns[i].data.length !== columns[0].data.length) {
+            if (rowsOf(columns[i]) !== rowsOf(columns[0])) {
                 throw new Error(`Column ${columns[i].name} has a different number of rows`);
             }
         }
         this.columns = columns;
     }
-    get numRows() { return this.columns[0].data.length; }
+    get numRows() { return rowsOf(this.columns[0]); }
     get numColumns() { return this.columns.length; }
     getColumn(i) { return this.columns[i]; }
     getColumnByName(name) { return this.columns.find(c => c.name === name); }
@@ -416,27 +446,29 @@ const writeSogBundle = (dataTable, iterations, processActions) => {
 // archive is streamed into the file while the SH palette k-means runs (st_sog_file); the file
 // holds writeSogBundle's bytes and is cut to their length.  The handle must be a seekable file
 // (the archive is written at absolute offsets): a pipe's handle throws before any work.  Float32
-// columns.
+// columns; readPly's columns that JS has not read are taken from HBM where they are.
 const writeSogFile = (fileHandle, dataTable, iterations) => {
     const k = 65536;
     const date = new Date();
     const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
     const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
     const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
-        draws => addon.sogFile(fileHandle.fd, dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name),
+        draws => addon.sogFile(fileHandle.fd, dataTable.columns.map(deviceOrHost), dataTable.columns.map(c => c.name),
             iterations, draws, dosTime, dosDate));
     return Promise.resolve(res.size);
 };
 
 // readers/read-ply.ts:111-191: {comments, elements: [{name, dataTable}]} from an open FileHandle
-// (rows stream through pinned memory into HBM and are transposed to columns there)
+// (rows stream through pinned memory into HBM and are transposed to columns there; the columns
+// stay there until JS first reads a column's `data` -- residentColumn above)
 const readPly = (fileHandle) => {
     const r = addon.readPly(fileHandle.fd);
     return Promise.resolve({
         comments: r.comments,
         elements: r.elements.map(e => ({
             name: e.name,
-            dataTable: new DataTable(e.columns.map(c => new Column(c.name, c.data)))
+            dataTable: new DataTable(e.columns.map(c => (c.lazy ? residentColumn(c.name, c.data) :
+                new Column(c.name, c.data))))
         }))
     });
 };

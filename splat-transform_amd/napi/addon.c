@@ -30,8 +30,10 @@
  *           draws, dosTime, dosDate)        while the SH k-means runs; {used, size}
  *        -> {archive: Buffer, used}           writeSog to a .sog (write-sog.ts:110-370 +
  *                                             serialize/zip-writer.ts)
- *   readPly(fd) -> {comments, elements:       readPly (readers/read-ply.ts:111-191)
- *        [{name, columns: [{name, data}]}]}
+ *   readPly(fd) -> {comments, elements:       readPly (readers/read-ply.ts:111-191); the values
+ *        [{name, columns: [{name, data,       stay in HBM (st_ply_read_resident) and `data` is
+ *          lazy}]}]}                          unfilled while `lazy` (ST_READ_RESIDENT=0: filled)
+ *   materialize(typedArray)                   a lazy column's values copied down (st_ply_materialize)
  *   decompressPly(chunk[18], vertex[4], sh[]) decompressPly (readers/decompress-ply.ts:82-232)
  *        -> Float32Array[14 + sh.length]
  *   compressedPly(cols, names, actions)       processDataTable + writeCompressedPly's arrays, one
@@ -234,6 +236,8 @@ static void free_column(napi_env env, void *data, void *hint) {
     int64_t adj;
     const size_t bytes = (size_t)hint, huge = (size_t)2 << 20, len = (bytes + huge - 1) / huge * huge;
     napi_adjust_external_memory(env, -(int64_t)bytes, &adj);
+    /* a resident readPly column (or a mirrored one) stops being one before its memory is reused */
+    if (g_ctx) st_ply_forget(g_ctx, data);
     pthread_mutex_lock(&g_pool_mu);
     if (g_pool_n < POOL_MAX && g_pool_bytes + len <= pool_cap()) {
         g_pool[g_pool_n].p = data;
@@ -247,9 +251,10 @@ static void free_column(napi_env env, void *data, void *hint) {
     free(data);
 }
 
-static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t elems, size_t esize, void **data) {
+/* always the external form (a resident readPly column needs the finalizer whatever its size) */
+static napi_value new_typed_ext(napi_env env, napi_typedarray_type type, size_t elems, size_t esize, void **data) {
     const size_t bytes = elems * esize, huge = (size_t)2 << 20;
-    if (bytes < ((size_t)8 << 20)) return new_typed(env, type, elems, esize, data);
+    if (!bytes) return new_typed(env, type, elems, esize, data);
     void *p = NULL;
     const size_t len = (bytes + huge - 1) / huge * huge;
     pthread_mutex_lock(&g_pool_mu);
@@ -277,6 +282,11 @@ static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t 
     if (napi_create_typedarray(env, type, elems, ab, 0, &ta) != napi_ok) return NULL;
     *data = p;
     return ta;
+}
+
+static napi_value new_typed_big(napi_env env, napi_typedarray_type type, size_t elems, size_t esize, void **data) {
+    if (elems * esize < ((size_t)8 << 20)) return new_typed(env, type, elems, esize, data);
+    return new_typed_ext(env, type, elems, esize, data);
 }
 
 static napi_value make_num(napi_env env, double d) {
@@ -1542,11 +1552,17 @@ fail:
     return NULL;
 }
 
+/* readPly(fd) -> {comments, elements: [{name, columns: [{name, data, lazy}]}]}.  By default the
+ * values stay in HBM (st_ply_read_resident): `data` is allocated but unfilled, `lazy` is true, and
+ * js/index.js hands it out only through materialize(); ST_READ_RESIDENT=0 fills every column
+ * here (st_ply_read). */
 static napi_value js_read_ply(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1], out, els, comments;
     st_ctx *ctx;
     st_ply_header *h = NULL;
+    const char *rm = getenv("ST_READ_RESIDENT");
+    const int lazy = !(rm && strcmp(rm, "0") == 0);
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     {
         const int32_t fd = (int32_t)num(env, argv[0]);
@@ -1587,17 +1603,20 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
             set_named(env, eo, "name", nm);
             napi_create_array_with_length(env, (size_t)el->nprops, &cols);
             for (int32_t p = 0; p < el->nprops; ++p) {
-                napi_value co, pn, ta = new_typed_big(env, tt[el->props[p].type], (size_t)el->count,
-                                                      ts[el->props[p].type], &ptrs[p]);
+                napi_value co, pn, lz,
+                    ta = lazy ? new_typed_ext(env, tt[el->props[p].type], (size_t)el->count, ts[el->props[p].type], &ptrs[p])
+                              : new_typed_big(env, tt[el->props[p].type], (size_t)el->count, ts[el->props[p].type], &ptrs[p]);
                 if (!ta) goto fail;
                 napi_create_object(env, &co);
                 napi_create_string_utf8(env, el->props[p].name, NAPI_AUTO_LENGTH, &pn);
                 set_named(env, co, "name", pn);
                 set_named(env, co, "data", ta);
+                napi_get_boolean(env, lazy && el->count > 0, &lz);
+                set_named(env, co, "lazy", lz);
                 napi_set_element(env, cols, (uint32_t)p, co);
             }
             const double t1 = now_ms();
-            rc = st_ply_read(ctx, fd, h, ei, ptrs);
+            rc = lazy ? st_ply_read_resident(ctx, fd, h, ei, ptrs) : st_ply_read(ctx, fd, h, ei, ptrs);
             t_alloc += t1 - t0;
             t_read += now_ms() - t1;
             if (rc != ST_OK) {
@@ -1616,6 +1635,31 @@ static napi_value js_read_ply(napi_env env, napi_callback_info info) {
     return out;
 fail:
     free(h);
+    return NULL;
+}
+
+/* materialize(typedArray): a resident readPly column's values copied down from HBM (st_ply_materialize;
+ * no-op for any other array) */
+static napi_value js_materialize(napi_env env, napi_callback_info info) {
+    size_t argc = 1, length = 0, off = 0;
+    napi_value argv[1], ab;
+    bool is_ta = false;
+    napi_typedarray_type type;
+    void *data = NULL;
+    st_ctx *ctx;
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 1 || napi_is_typedarray(env, argv[0], &is_ta) != napi_ok || !is_ta ||
+        napi_get_typedarray_info(env, argv[0], &type, &length, &data, &ab, &off) != napi_ok) {
+        napi_throw_type_error(env, NULL, "splat-hip: materialize takes a TypedArray");
+        return NULL;
+    }
+    if (!get_ctx(env, &ctx)) return NULL;
+    {
+        const int rc = st_ply_materialize(ctx, data);
+        if (rc != ST_OK) return throw_st(env, rc);
+    }
+    return argv[0];
+fail:
     return NULL;
 }
 
@@ -1716,6 +1760,7 @@ static napi_value init(napi_env env, napi_value exports) {
                {"sogBundle", js_sog_bundle},
                {"sogFile", js_sog_file},
                {"readPly", js_read_ply},
+               {"materialize", js_materialize},
                {"decompressPly", js_decompress_ply},
                {"compressedPly", js_compressed_ply},
                {"compressedPlyFromFile", js_compressed_ply_file},

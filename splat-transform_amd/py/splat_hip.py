@@ -6,6 +6,7 @@ their device pointers, running on torch's current stream.  There is no CPU
 fallback: constructing a Context without a gfx950 device raises.
 """
 import ctypes
+import weakref
 import os
 import subprocess
 import sys
@@ -114,12 +115,19 @@ EXPORTS = [
     'st_sog_meta_json', 'st_dev_sog_bundle', 'st_dev_sog_bundle_view', 'st_dev_sog_file', 'st_sog_file', 'st_sog_bundle',
     'st_free',
     'st_ply_parse_header', 'st_ply_read_header', 'st_ply_row_bytes', 'st_dev_ply_transpose', 'st_dev_ply_read',
-    'st_ply_read', 'st_dev_decompress_ply', 'st_decompress_ply',
+    'st_ply_read', 'st_ply_read_resident', 'st_ply_materialize', 'st_ply_forget', 'st_dev_decompress_ply', 'st_decompress_ply',
     'st_process', 'st_compressed_ply', 'st_dev_compressed_ply', 'st_ply_compressed_ply', 'st_ply_sog_bundle',
     'st_group_sog_bundle_process',
     'st_transform_t', 'st_dev_transform_t', 'st_morton_order_t', 'st_dev_morton_order_t', 'st_sog_process',
     'st_sog_bundle_process', 'st_dev_sog_t',
 ]
+
+
+def _forget_column(ctx_ref, ptr):
+    """a resident read's column is being freed: the context (if still open) drops it (st_ply_forget)"""
+    c = ctx_ref()
+    if c is not None and c.h:
+        lib().st_ply_forget(c.h, ctypes.c_void_p(ptr))
 
 
 def build(jobs=8):
@@ -766,21 +774,37 @@ class Context:
                                      ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size)
 
-    def read_ply(self, path):
-        """readPly (read-ply.ts:111-191) -> (comments, [(element, {prop: numpy column})]); rows go through HBM"""
+    def read_ply(self, path, resident=False):
+        """readPly (read-ply.ts:111-191) -> (comments, [(element, {prop: numpy column})]); rows go through HBM.
+        resident: st_ply_read_resident -- the numpy columns stay unfilled (the values live in HBM) until
+        materialize(column) or a host form other than writeSog's reads them; keep them alive until then,
+        or forget() them"""
         fd = os.open(path, os.O_RDONLY)
         try:
             h = PlyHeader()
             check(lib().st_ply_read_header(ctypes.c_int32(fd), ctypes.byref(h)))
             out = []
+            read = lib().st_ply_read_resident if resident else lib().st_ply_read
             for ei, (name, count, props) in enumerate(h.layout()):
                 cols = {pn: np.empty(count, dt) for pn, dt in props}
                 ptrs = (ctypes.c_void_p * max(len(props), 1))(*[cols[pn].ctypes.data for pn, _ in props])
-                check(lib().st_ply_read(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(ei), ptrs))
+                check(read(self.h, ctypes.c_int32(fd), ctypes.byref(h), ctypes.c_int32(ei), ptrs))
+                if resident:  # st_ply_read_resident's contract: forgotten before the memory goes away
+                    for a in cols.values():
+                        weakref.finalize(a, _forget_column, weakref.ref(self), a.ctypes.data)
                 out.append((name, cols))
             return h.comment_list(), out
         finally:
             os.close(fd)
+
+    def materialize(self, col):
+        """a resident read's column filled from HBM (st_ply_materialize); no-op for any other array"""
+        check(lib().st_ply_materialize(self.h, ctypes.c_void_p(col.ctypes.data)))
+        return col
+
+    def forget(self, col):
+        """drop a resident or mirrored column without copying it (st_ply_forget)"""
+        check(lib().st_ply_forget(self.h, ctypes.c_void_p(col.ctypes.data)))
 
     def decompress_ply(self, chunk, vertex, sh):
         """decompressPly (decompress-ply.ts:82-232): chunk/vertex dicts of numpy columns, sh list of uint8

@@ -1,5 +1,10 @@
-"""The writeSog host forms on st_ply_read's resident columns (st_ctx::HostMirror,
-st_host_api.hip run_host_sog): readPly -> writeSog (index.ts:433-510 -> write-sog.ts:110-370)
+"""The writeSog host forms on resident columns (st_ctx::HostMirror, st_host_api.hip run_host_sog).
+
+st_ply_read_resident (the Node host's readPly): the host columns stay unfilled and the values live
+in HBM until st_ply_materialize -- writeSog reads them on the device, every other host form copies
+them down first, and a second read of the element copies them down before it reuses their slots.
+
+st_ply_read: readPly -> writeSog (index.ts:433-510 -> write-sog.ts:110-370)
 without uploading a table the device already holds, and only while the caller's columns are
 byte for byte what st_ply_read wrote.
 
@@ -121,3 +126,95 @@ def test_a_second_read_replaces_the_mirrors(ctx, tmp_path, monkeypatch):
     wa, _, _ = _file(ctx, ca, out, monkeypatch, False)
     wb, _, _ = _file(ctx, cb, out, monkeypatch, False)
     assert ga == wa and gb == wb and ga != gb
+
+
+def _read_resident(ctx, path):
+    _, els = ctx.read_ply(path, resident=True)
+    return dict(els)['vertex']
+
+
+def test_resident_read_sog_file_runs_on_the_device_copy(ctx, tmp_path, monkeypatch):
+    """st_ply_read_resident + st_sog_file: no column copied down or uploaded (59 reused), the
+    archive equal to the eager read's uploaded one; the unfilled host columns stay untouched"""
+    src = str(tmp_path / 'in.ply')
+    _ply(src, N, 11)
+    ref = _read(ctx, src)
+    cols = _read_resident(ctx, src)
+    mark = np.float32(-12345.5)
+    for v in cols.values():
+        v[:] = mark  # the library must never read these bytes
+    out = str(tmp_path / 'out.sog')
+    got, used, reuse = _file(ctx, cols, out, monkeypatch, True)
+    assert reuse == (59, 59 * N * 4), reuse
+    assert all(np.all(v == mark) for v in cols.values())
+    want, wused, _ = _file(ctx, ref, out, monkeypatch, False)
+    assert got == want and used == wused
+
+
+def test_resident_read_materialize_and_forget(ctx, tmp_path, monkeypatch):
+    """st_ply_materialize fills a column with the read's values (then an ordinary host column:
+    uploaded, so a change to it shows in the output); st_ply_forget drops one without copying"""
+    src = str(tmp_path / 'in.ply')
+    _ply(src, N, 12)
+    ref = _read(ctx, src)
+    cols = _read_resident(ctx, src)
+    ctx.materialize(cols['f_rest_5'])
+    ctx.materialize(cols['f_rest_5'])  # no-op the second time
+    assert np.array_equal(cols['f_rest_5'].view(np.uint32), ref['f_rest_5'].view(np.uint32))
+    ctx.forget(cols['y'])
+    cols['y'][:] = ref['y']  # the caller's own values now
+    cols['f_rest_5'][3] += np.float32(0.25)
+    ref['f_rest_5'][3] += np.float32(0.25)
+    out = str(tmp_path / 'out.sog')
+    got, _, reuse = _file(ctx, cols, out, monkeypatch, True)
+    assert reuse[0] == 57, reuse
+    want, _, _ = _file(ctx, ref, out, monkeypatch, False)
+    assert got == want
+
+
+def test_resident_read_other_host_forms_copy_down_first(ctx, tmp_path, monkeypatch):
+    """a host form other than writeSog's (st_transform in place, st_filter_nan) given unfilled
+    resident columns reads the read's values (copied down first); the columns it wrote are the
+    caller's afterwards, the untouched ones stay resident"""
+    src = str(tmp_path / 'in.ply')
+    _ply(src, N, 13)
+    ref = _read(ctx, src)
+    cols = _read_resident(ctx, src)
+    kept = ctx.filter_nan([('opacity', cols['opacity'])])
+    assert np.array_equal(kept[0][1].view(np.uint32), ref['opacity'].view(np.uint32))
+    p = sh.transform_params((1.0, -2.0, 0.5), (0.0, 0.0, 0.0, 1.0), 2.0)
+    moved = ('x', 'y', 'z', 'rot_0', 'rot_1', 'rot_2', 'rot_3', 'scale_0', 'scale_1', 'scale_2')
+    ctx.transform({k: cols[k] for k in moved}, p)
+    ctx.transform({k: ref[k] for k in moved}, p)
+    for k in moved + ('opacity',):
+        assert np.array_equal(cols[k].view(np.uint32), ref[k].view(np.uint32)), k
+    out = str(tmp_path / 'out.sog')
+    got, _, reuse = _file(ctx, cols, out, monkeypatch, True)
+    assert reuse[0] == 59 - 11, reuse  # the ten transformed columns and the filtered opacity came down
+    want, _, _ = _file(ctx, ref, out, monkeypatch, False)
+    assert got == want
+
+
+def test_resident_reads_keep_their_own_device_copies(ctx, tmp_path, monkeypatch):
+    """each resident read's columns hold device blocks of their own: a second read (same element,
+    another file) leaves the first table resident -- both run from HBM and give their own output;
+    a forgotten table's blocks serve the next read"""
+    a, b = str(tmp_path / 'a.ply'), str(tmp_path / 'b.ply')
+    _ply(a, N, 14)
+    _ply(b, N, 15)
+    ra, rb = _read(ctx, a), _read(ctx, b)
+    ca = _read_resident(ctx, a)
+    cb = _read_resident(ctx, b)
+    out = str(tmp_path / 'o.sog')
+    ga, _, xa = _file(ctx, ca, out, monkeypatch, True)
+    gb, _, xb = _file(ctx, cb, out, monkeypatch, True)
+    assert xa[0] == 59 and xb[0] == 59, (xa, xb)
+    wa, _, _ = _file(ctx, ra, out, monkeypatch, False)
+    wb, _, _ = _file(ctx, rb, out, monkeypatch, False)
+    assert ga == wa and gb == wb and ga != gb
+    for k in ra:
+        assert np.array_equal(ctx.materialize(ca[k]).view(np.uint32), ra[k].view(np.uint32)), k
+    del cb  # its finalizers forget the columns: their blocks go to the pool
+    cc = _read_resident(ctx, b)
+    gc, _, xc = _file(ctx, cc, out, monkeypatch, True)
+    assert xc[0] == 59 and gc == wb

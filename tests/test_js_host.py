@@ -43,7 +43,7 @@ def test_addon_exports(addon_built):
                                        'process', 'compressedPlyFromFile', 'sogBundleFromFile',
                                        'sogProcess', 'sogBundleProcess', 'transformTyped', 'mortonOrderTyped',
                                        'sogFile', 'rcclInfo', 'lastHostReuse', 'compressedPlyToFile',
-                                       'compressedPlyTableToFile'])
+                                       'compressedPlyTableToFile', 'materialize'])
     assert ver == '1'
 
 
@@ -246,3 +246,37 @@ def test_js_sog_file_equals_bundle(addon_built, tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         assert f'sog {mode} ok' in r.stdout
     assert (tmp_path / 'out_file.sog').read_bytes() == (tmp_path / 'out_bundle.sog').read_bytes()
+
+
+@pytest.mark.gpu
+def test_js_resident_read_columns_through_write_sog_file(addon_built, tmp_path):
+    """readPly leaves the columns in HBM (st_ply_read_resident) until JS reads a column's `data`:
+    writeSogFile of an untouched table reads all 59 writeSog columns where they are, a table whose
+    columns JS read or changed uploads exactly those columns -- every archive equal to the upload
+    path's for the same values; two tables read from one file each keep their own device copy
+    (tests/js/resident_read.js: same draws, pinned clock)"""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 300_000
+    cols = {k: v.numpy() for k, v in bench.synth_table(n, 4242, 'cpu').items()}
+    src = tmp_path / 'in.ply'
+    head = ('ply\nformat binary_little_endian 1.0\n' + f'element vertex {n}\n' +
+            ''.join(f'property float {k}\n' for k in bench.PLY_ORDER) + 'end_header\n').encode()
+    rows = np.stack([cols[k] if k in cols else np.zeros(n, np.float32) for k in bench.PLY_ORDER], 1)
+    src.write_bytes(head + rows.astype('<f4').tobytes())
+    r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'resident_read.js'), str(src), str(tmp_path), '3'],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    sha = out['untouched']['sha']
+    assert out['untouched']['reused'] == 59, out
+    assert out['read'] == {'sha': sha, 'reused': 0, 'finite': True}, out
+    assert out['changed']['reused'] == 58 and out['changed_ref']['reused'] == 0, out
+    assert out['changed']['sha'] == out['changed_ref']['sha'] != sha, out
+    assert out['first'] == {'sha': sha, 'reused': 59} and out['second'] == {'sha': sha, 'reused': 59}, out
+    assert out['meta'] == {'sha': sha, 'reused': 59} and out['numRows'] == n and out['columns'] == 62, out
+    assert out['hasRot'], out
+    got = np.fromfile(tmp_path / 'first_f_rest_44.bin', np.float32)
+    assert np.array_equal(got.view(np.uint32), cols['f_rest_44'].view(np.uint32))
+    got = np.fromfile(tmp_path / 'meta_x.bin', np.float32)
+    assert np.array_equal(got.view(np.uint32), cols['x'].view(np.uint32))
