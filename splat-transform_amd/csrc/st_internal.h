@@ -122,7 +122,7 @@ struct st_ctx {
     hipStream_t side = nullptr;
     hipEvent_t side_ev[2] = {nullptr, nullptr};
     // the N-D assign's read-backs: behind the sweep, behind the fix-up (created on first use)
-    hipEvent_t kn_ev[2] = {nullptr, nullptr};
+    hipEvent_t kn_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     st::Workspace ws;
     // pinned host staging for small readbacks
     void *pinned = nullptr;
@@ -200,6 +200,9 @@ struct st_ctx {
     std::atomic<bool> *spec_abort = nullptr;
     std::function<bool()> spec_verdict;
     uint64_t last_reuse_cols = 0, last_reuse_bytes = 0;  // st_ctx_last_host_reuse
+    // set by the one-device N-D k-means loop: an assign's pair / ambiguous fix-ups run on the side
+    // stream beside the decided points' fix-up (nd_assign_core); ST_FIX_SERIAL=1: one stream
+    bool fix_overlap = false;
 };
 
 namespace st {
@@ -248,7 +251,8 @@ struct KTimer {
     st_ctx *c;
     hipEvent_t a = nullptr, b = nullptr;
     const char *name;
-    KTimer(st_ctx *ctx, const char *nm);
+    hipStream_t s;  // the stream the timed kernels run on (the context's unless given)
+    KTimer(st_ctx *ctx, const char *nm, hipStream_t stream = nullptr);
     ~KTimer();
 };
 

@@ -2099,14 +2099,14 @@ struct Sweep {
     }
     static void collect(st_ctx *c, const uint4 *afrag, uint32_t atiles, uint32_t namb, const uint4 *cfrag,
                         uint32_t ctiles, const Bound &bnd, float *thr_slot, uint32_t *cand_cnt, uint32_t *cand,
-                        uint32_t cap) {
+                        uint32_t cap, hipStream_t s) {
         const uint32_t per_block = NW * PT;
         const uint32_t blocks = (atiles + per_block - 1) / per_block;
         // enough workgroups to cover the chip twice over
         const uint32_t split = std::max(1u, std::min(ctiles / CT_STAGE, (2048u + blocks - 1) / blocks));
         const dim3 grid(blocks, split);
-        KTimer kt(c, "kn.collect");
-        hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, c->stream, afrag, atiles, namb, cfrag, ctiles,
+        KTimer kt(c, "kn.collect", s);
+        hipLaunchKernelGGL((k_sweep<KS, 1>), grid, dim3(WG), 0, s, afrag, atiles, namb, cfrag, ctiles,
                            (const float *)nullptr, (const float *)nullptr, (const uint32_t *)nullptr,
                            (const float *)nullptr, (const float *)nullptr, (const float *)nullptr, bnd,
                            (uint32_t *)nullptr, thr_slot,
@@ -2294,7 +2294,8 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     for (auto &e : c->kn_ev)
         if (!e) ST_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    hipEvent_t ev_sw = c->kn_ev[0], ev_fix = c->kn_ev[1];
+    hipEvent_t ev_sw = c->kn_ev[0], ev_fix = c->kn_ev[1], ev_grp = c->kn_ev[2], ev_side = c->kn_ev[3];
+    bool grouped_ev = false;
     ST_HIP(hipEventRecord(ev_sw, c->stream));
     if (grouped_fix) {
         // group the decided points by tile-half, then settle them with register-resident rows
@@ -2332,6 +2333,9 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
                                    ncodes, cursor, grouped);
         }
         ST_LAUNCH_CHECK();
+        // the grouping has read every label: the pair / ambiguous fix-ups may write theirs from here
+        ST_HIP(hipEventRecord(ev_grp, c->stream));
+        grouped_ev = true;
         const dim3 g((unsigned)(((n + FB_RUN - 1) / FB_RUN * 16 + 255) / 256));
         if (fused) {
             // the fix-up with the decided points' sums (k_fixrow_lp), slices shared out over the workgroups
@@ -2375,33 +2379,38 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
     ST_HIP(hipEventRecord(ev_fix, c->stream));
     ST_HIP(hipEventSynchronize(ev_sw));
     const uint32_t npair = h->pairs;
+    const uint32_t namb = h->amb;
+    // The pair and ambiguous points' fix-ups, on the side stream beside the decided points' one
+    // when the one-device loop asks for it (c->fix_overlap) and the grouping has read the labels
+    // (ev_grp): their ties go to a list and counters of their own (kn.ties2, kn.state2), appended to
+    // the fix-up's list afterwards -- the same list, in the same order, as one stream gives.
+    const bool overlap = c->fix_overlap && grouped_ev && (npair || namb) && !getenv("ST_FIX_SERIAL");
+    const hipStream_t fs = overlap ? side_stream(c) : c->stream;
+    State *ds = overlap ? static_cast<State *>(ws(c, "kn.state2", sizeof(State))) : dstate;
+    uint32_t *tl = overlap ? wsT<uint32_t>(c, "kn.ties2", n) : ties;
+    auto *hs = overlap ? static_cast<State *>(pinned_slot(c, "kn.hside", sizeof(State))) : h;
+    if (overlap) {
+        ST_HIP(hipStreamWaitEvent(fs, ev_grp, 0));
+        ST_HIP(hipMemsetAsync(ds, 0, sizeof(State), fs));
+    }
     if (npair) {
-        KTimer kt(c, "kn.fixpair");
+        KTimer kt(c, "kn.fixpair", fs);
         const dim3 g((npair * 32 + 255) / 256);
         if (ld == 48)
-            hipLaunchKernelGGL(k_fixpair_b<48>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
-                               pair_codes, npair, labels, ties, dstate);
+            hipLaunchKernelGGL(k_fixpair_b<48>, g, dim3(256), 0, fs, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, tl, ds);
         else if (ld == 24)
-            hipLaunchKernelGGL(k_fixpair_b<24>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
-                               pair_codes, npair, labels, ties, dstate);
+            hipLaunchKernelGGL(k_fixpair_b<24>, g, dim3(256), 0, fs, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, tl, ds);
         else if (ld == 12)
-            hipLaunchKernelGGL(k_fixpair_b<12>, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts,
-                               pair_codes, npair, labels, ties, dstate);
+            hipLaunchKernelGGL(k_fixpair_b<12>, g, dim3(256), 0, fs, aos, d, cfix, caos, k, pair_pts,
+                               pair_codes, npair, labels, tl, ds);
         else
-            hipLaunchKernelGGL(k_fixpair, g, dim3(256), 0, c->stream, aos, d, cfix, caos, k, pair_pts, pair_codes,
-                               npair, labels, ties, dstate);
+            hipLaunchKernelGGL(k_fixpair, g, dim3(256), 0, fs, aos, d, cfix, caos, k, pair_pts, pair_codes,
+                               npair, labels, tl, ds);
         ST_LAUNCH_CHECK();
     }
     mark(c, "kn.assign");
-    const uint32_t namb = h->amb;
-    // the fix-up's read-back (the pairs' kernel already queued behind it); h is the latest from here
-    ST_HIP(hipEventSynchronize(ev_fix));
-    *h = *h_fix;
-    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
-        fz->nties_fix = h->ties;
-        fz->npair = npair;
-        fz->namb = namb;
-    }
     uint32_t ovf1 = 0;  // first lists that overflowed (collected again with CAND_CAP2)
     if (namb) {
         const uint32_t atiles = (namb + 31) / 32;
@@ -2409,26 +2418,26 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
         auto *thr_slot = wsT<float>(c, "kn.thrslot", (size_t)atiles * 32);
         auto *cand_cnt = wsT<uint32_t>(c, "kn.ccnt", (size_t)atiles * 32);
         auto *cand = wsT<uint32_t>(c, "kn.cand", (size_t)namb * CAND_CAP);
-        hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)atiles * 32, 256, 4096)), dim3(256), 0, fs,
                            pfrag, amb, thr, namb, ks, afrag, thr_slot, cand_cnt);
         ST_LAUNCH_CHECK();
         auto *ovf = wsT<uint32_t>(c, "kn.ovf", namb);
         ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag, atiles, namb, cfrag, ctiles, bnd, thr_slot, cand_cnt, cand,
-                                               (uint32_t)CAND_CAP)));
+                                               (uint32_t)CAND_CAP, fs)));
         {
-            KTimer kt(c, "kn.exact");
-            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, c->stream, aos, d, caos, k, amb, namb,
-                               cand_cnt, cand, (uint32_t)CAND_CAP, labels, ties, ovf, dstate);
+            KTimer kt(c, "kn.exact", fs);
+            hipLaunchKernelGGL(k_exact, dim3((namb + 3) / 4), dim3(256), 0, fs, aos, d, caos, k, amb, namb,
+                               cand_cnt, cand, (uint32_t)CAND_CAP, labels, tl, ovf, ds);
             ST_LAUNCH_CHECK();
         }
-        ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
-        ovf1 = h->overflow;
-        if (h->overflow) {
+        ST_HIP(hipMemcpyAsync(hs, ds, sizeof(State), hipMemcpyDeviceToHost, fs));
+        ST_HIP(hipStreamSynchronize(fs));
+        ovf1 = hs->overflow;
+        if (hs->overflow) {
             // points whose window holds more than CAND_CAP rows (wide windows: outlying points of
             // heavy-tailed data): collected again with lists of CAND_CAP2, in batches; only those
             // that overflow these too take the KdTree walk
-            const uint32_t nov = h->overflow, batch = std::min(nov, (uint32_t)OVF_BATCH);
+            const uint32_t nov = hs->overflow, batch = std::min(nov, (uint32_t)OVF_BATCH);
             const uint32_t btiles = (batch + 31) / 32;
             auto *afrag2 = wsT<uint4>(c, "kn.afrag2", (size_t)btiles * ks * 64);
             auto *thr2 = wsT<float>(c, "kn.thrslot2", (size_t)btiles * 32);
@@ -2436,18 +2445,18 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
             auto *cand2 = wsT<uint32_t>(c, "kn.cand2", (size_t)batch * CAND_CAP2);
             for (uint32_t b0 = 0; b0 < nov; b0 += batch) {
                 const uint32_t m = std::min(batch, nov - b0), mt = (m + 31) / 32;
-                hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)mt * 32, 256, 4096)), dim3(256), 0,
-                                   c->stream, pfrag, ovf + b0, thr, m, ks, afrag2, thr2, cnt2);
+                hipLaunchKernelGGL(k_gather_amb, dim3(grid_for((uint64_t)mt * 32, 256, 4096)), dim3(256), 0, fs,
+                                   pfrag, ovf + b0, thr, m, ks, afrag2, thr2, cnt2);
                 ST_LAUNCH_CHECK();
                 ST_KS_DISPATCH(ks, (Sweep<KS>::collect(c, afrag2, mt, m, cfrag, ctiles, bnd, thr2, cnt2, cand2,
-                                                       (uint32_t)CAND_CAP2)));
-                KTimer kt(c, "kn.exact");
-                hipLaunchKernelGGL(k_exact, dim3((m + 3) / 4), dim3(256), 0, c->stream, aos, d, caos, k, ovf + b0, m,
-                                   cnt2, cand2, (uint32_t)CAND_CAP2, labels, ties, (uint32_t *)nullptr, dstate);
+                                                       (uint32_t)CAND_CAP2, fs)));
+                KTimer kt(c, "kn.exact", fs);
+                hipLaunchKernelGGL(k_exact, dim3((m + 3) / 4), dim3(256), 0, fs, aos, d, caos, k, ovf + b0, m,
+                                   cnt2, cand2, (uint32_t)CAND_CAP2, labels, tl, (uint32_t *)nullptr, ds);
                 ST_LAUNCH_CHECK();
             }
-            ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-            ST_HIP(hipStreamSynchronize(c->stream));
+            ST_HIP(hipMemcpyAsync(hs, ds, sizeof(State), hipMemcpyDeviceToHost, fs));
+            ST_HIP(hipStreamSynchronize(fs));
         }
         if (getenv("ST_DEBUG")) {  // candidate-count histogram of the ambiguous points
             std::vector<uint32_t> cc(namb);
@@ -2458,10 +2467,31 @@ uint32_t nd_assign_core(st_ctx *c, const float *const *dcols, int d, uint64_t n,
                     (unsigned long long)hist[0], (unsigned long long)hist[1], (unsigned long long)hist[2],
                     (unsigned long long)hist[3], (unsigned long long)hist[4], (unsigned long long)hist[5]);
         }
+    } else if (npair) {  // the pairs' ties and counters
+        ST_HIP(hipMemcpyAsync(hs, ds, sizeof(State), hipMemcpyDeviceToHost, fs));
+        ST_HIP(hipStreamSynchronize(fs));
     }
-    if (npair && !namb) {  // the tie count read before k_fixpair_b: its exact ties count too
-        ST_HIP(hipMemcpyAsync(h, dstate, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-        ST_HIP(hipStreamSynchronize(c->stream));
+    // the decided points' fix-up (its read-back was queued behind it)
+    ST_HIP(hipEventSynchronize(ev_fix));
+    const uint32_t nties_fix = h_fix->ties;
+    if (overlap) {
+        // join: the side stream's ties follow the fix-up's in one list (kn.ties), as one stream
+        // would have listed them; its overflow count is the assign's
+        ST_HIP(hipEventRecord(ev_side, fs));
+        ST_HIP(hipStreamWaitEvent(c->stream, ev_side, 0));
+        if (hs->ties)
+            ST_HIP(hipMemcpyAsync(ties + nties_fix, tl, (size_t)hs->ties * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        *h = *h_fix;
+        h->ties = nties_fix + hs->ties;
+        h->overflow = hs->overflow;
+    } else if (!npair && !namb) {
+        *h = *h_fix;
+    }
+    if (fz && fz->valid) {  // the fix-up's own ties are listed first; pairs and ambiguous come next
+        fz->nties_fix = nties_fix;
+        fz->npair = npair;
+        fz->namb = namb;
     }
     if (getenv("ST_DEBUG"))
         fprintf(stderr, "[st kmeans] n=%llu k=%d pairs=%u ambiguous=%u ties=%u overflow=%u sigma=%g\n",
@@ -2666,6 +2696,13 @@ void kmeansnd_loop(st_ctx *c, const float *const *cols, const float *const *dcol
                    int iters, const double *ddraws, uint64_t ndraws, km::State *dstate, float *cen, uint32_t *labels,
                    const double *const *sum64) {
     (void)cols;
+    // one device: the assign's pair / ambiguous fix-ups overlap the decided points' (nd_assign_core)
+    struct Overlap {
+        st_ctx *c;
+        bool was;
+        ~Overlap() { c->fix_overlap = was; }
+    } overlap{c, c->fix_overlap};
+    c->fix_overlap = true;
     auto *aos = wsT<float>(c, "kn.aos", n * (size_t)aos_ld(d));
     double *aos64 = nullptr;
     if (sum64) {  // the members' float64 numbers for the sums

@@ -293,16 +293,16 @@ static hipEvent_t pool_event(st_ctx *c) {
     return e;
 }
 
-KTimer::KTimer(st_ctx *ctx, const char *nm) : c(ctx), name(nm) {
+KTimer::KTimer(st_ctx *ctx, const char *nm, hipStream_t stream) : c(ctx), name(nm), s(stream ? stream : ctx->stream) {
     if (!c->profiling) return;
     a = pool_event(c);
     b = pool_event(c);
-    ST_HIP(hipEventRecord(a, c->stream));
+    ST_HIP(hipEventRecord(a, s));
 }
 
 KTimer::~KTimer() {
     if (!a) return;
-    if (hipEventRecord(b, c->stream) == hipSuccess) c->kevents.push_back({name, a, b});
+    if (hipEventRecord(b, s) == hipSuccess) c->kevents.push_back({name, a, b});
 }
 
 static void begin_timing(st_ctx *c) {

@@ -18,6 +18,7 @@
 #   quick    a k-means test selection + kn_bench timings (a quick check of a kernel change)
 #   ab       interleaved bench steps of tools/ab/base.so against tools/ab/new.so (ST_LIB; $AB_ARGS
 #            extra bench.py arguments, e.g. --total-splats 1250000)
+#   abenv    interleaved bench steps of this library with and without $AB_ENV (VAR=value) ($AB_ARGS)
 #   node     the Node drop-in's PLY -> .sog job with phase stamps (tools/node_probe.py)
 #   read     readPly's host form under its settings (tools/read_probe.py)
 #   paths    the config-3 stage table and file paths (tools/bench_paths.py)
@@ -102,6 +103,16 @@ print('dist1', round(r['ms_per_step'], 2), r['transport'], r['torch_backend'], r
         ST_LIB=tools/ab/$v.so timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
           --no-paths --no-extra --no-verify $AB_ARGS > ${O}_ab_$v$i.json 2> ${O}_ab_$v$i.err || fail ab ${O}_ab_$v$i.err
         python3 -c "import json; b=json.load(open('${O}_ab_$v$i.json')); k=b['kernels']; print('$v', $i, round(b['ms_per_step'], 2), b['textures_sha256'][:12], 'fixrow', round(k['kn.fixrow']['avg_ms'], 3), 'sweep', round(k['kn.sweep']['avg_ms'], 2))"
+      done
+    done ;;
+  abenv)
+    # the same library with and without $AB_ENV (e.g. ST_FIX_SERIAL=1), interleaved; $AB_ARGS as for ab
+    for i in 1 2 3 4; do
+      for v in base env; do
+        e=""; [ $v = env ] && e="$AB_ENV"
+        env $e timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
+          --no-paths --no-extra --no-verify $AB_ARGS > ${O}_abe_$v$i.json 2> ${O}_abe_$v$i.err || fail abenv ${O}_abe_$v$i.err
+        python3 -c "import json; b=json.load(open('${O}_abe_$v$i.json')); k=b['kernels']; print('$v', $i, round(b['ms_per_step'], 2), b['textures_sha256'][:12], 'fixrow', round(k['kn.fixrow']['avg_ms'], 3), 'sweep', round(k['kn.sweep']['avg_ms'], 2))"
       done
     done ;;
   node)
