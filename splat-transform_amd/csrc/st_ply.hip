@@ -716,9 +716,9 @@ void ply_read_host(st_ctx *c, int fd, const st_ply_header &h, int element, void 
                 if (m.host == host_cols[p]) return true;
             return false;
         });
-        for (int p = 0; p < np; ++p)
-            c->mirrors.push_back({host_cols[p], el.count * P.sz[p], nullptr, dcols[p], element, true,
-                                  dcols[p] ? dbytes[p] : 0});
+        if (el.count)  // (an empty element has nothing to keep)
+            for (int p = 0; p < np; ++p)
+                c->mirrors.push_back({host_cols[p], el.count * P.sz[p], nullptr, dcols[p], element, true, dbytes[p]});
         return;
     }
     // an eager read overwrites this element's device slots and the shared host twins: every other
