@@ -436,9 +436,14 @@ const writeSogBundle = (dataTable, iterations, processActions) => {
     const dosTime = (date.getHours() << 11) | (date.getMinutes() << 5) | Math.floor(date.getSeconds() / 2);
     const dosDate = ((date.getFullYear() - 1980) << 9) | ((date.getMonth() + 1) << 5) | date.getDate();
     const acts = normaliseActions(processActions || []);
+    // no actions and float32 columns only: st_sog_bundle, which reads readPly's untouched columns
+    // where they are in HBM (deviceOrHost: nothing copied down); otherwise the typed chain
+    const plain = acts.length === 0 && dataTable.columns.every(c => deviceOrHost(c) instanceof Float32Array);
     const res = withDraws(4 * 256 * (iterations + 1) + k * (iterations + 1) + 4096,
-        draws => addon.sogBundleProcess(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name), acts,
-            iterations, draws, dosTime, dosDate));
+        draws => (plain ? addon.sogBundle(dataTable.columns.map(deviceOrHost), dataTable.columns.map(c => c.name),
+            iterations, draws, dosTime, dosDate) :
+            addon.sogBundleProcess(dataTable.columns.map(c => c.data), dataTable.columns.map(c => c.name), acts,
+                iterations, draws, dosTime, dosDate)));
     return Promise.resolve(res.archive);
 };
 

@@ -7,6 +7,7 @@
 //   changed        one value of f_rest_3 changed: that column uploaded, the other 58 from HBM
 //   changed_ref    the same change after reading every column: all uploaded
 //   first, second  two reads of the file, both tables alive: each keeps its own device copy
+//   bundle         writeSogBundle of an untouched table (st_sog_bundle): the same bytes, from HBM
 //   meta           numRows / names / getColumnByName only: still from HBM
 // Prints one JSON line {case: {sha, reused}, ..., numRows}.
 //   node resident_read.js <in.ply> <dir> <iters>
@@ -72,6 +73,12 @@ const write = async (table, name) => {
     const t2 = await read();
     res.first = await write(t1, 'e.sog');
     res.second = await write(t2, 'f.sog');
+
+    // writeSogBundle of an untouched table: the same archive from HBM
+    t = await read();
+    fixDraws();
+    const bundle = await host.writeSogBundle(t, iters);
+    res.bundle = { sha: crypto.createHash('sha256').update(bundle).digest('hex'), reused: host.addon.lastHostReuse().columns };
 
     t = await read();
     res.numRows = t.numRows;

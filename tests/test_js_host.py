@@ -275,6 +275,7 @@ def test_js_resident_read_columns_through_write_sog_file(addon_built, tmp_path):
     assert out['changed']['sha'] == out['changed_ref']['sha'] != sha, out
     assert out['first'] == {'sha': sha, 'reused': 59} and out['second'] == {'sha': sha, 'reused': 59}, out
     assert out['meta'] == {'sha': sha, 'reused': 59} and out['numRows'] == n and out['columns'] == 62, out
+    assert out['bundle'] == {'sha': sha, 'reused': 59}, out
     assert out['hasRot'], out
     got = np.fromfile(tmp_path / 'first_f_rest_44.bin', np.float32)
     assert np.array_equal(got.view(np.uint32), cols['f_rest_44'].view(np.uint32))
