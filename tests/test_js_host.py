@@ -202,7 +202,10 @@ def test_js_sog_bundle_matches_reference(addon_built, tmp_path):
 
 
 @pytest.mark.gpu
-def test_js_read_ply_and_decompress_match_reference(addon_built, tmp_path):
+@pytest.mark.parametrize('resident', ['1', '0'])
+def test_js_read_ply_and_decompress_match_reference(addon_built, tmp_path, resident):
+    """readPly (resident columns copied down as JS reads them, or -- ST_READ_RESIDENT=0 -- filled by
+    the read) and decompressPly against the reference's readers' outputs"""
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     from golden_io import Golden
     from test_ply_cpu import compressed_file
@@ -210,7 +213,7 @@ def test_js_read_ply_and_decompress_match_reference(addon_built, tmp_path):
     (tmp_path / 'mixed.ply').write_bytes(g['mixed_file'].tobytes())
     (tmp_path / 'comp.ply').write_bytes(compressed_file('sh3'))
     r = subprocess.run([NODE, os.path.join(ROOT, 'tests', 'js', 'ply_read.js'), str(tmp_path)],
-                       capture_output=True, text=True, timeout=600)
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, ST_READ_RESIDENT=resident))
     assert r.returncode == 0, r.stdout + r.stderr
     summ = json.loads((tmp_path / 'summary.json').read_text())
     assert summ['mixed']['comments'] == g.meta['mixed']['comments']
