@@ -17,6 +17,8 @@
 #include <mutex>
 #include <thread>
 
+#include <chrono>
+
 #include "st_internal.h"
 #include "st_typed.h"
 #include "st_webp.h"
@@ -615,8 +617,12 @@ int st_ply_compressed_ply_file(st_ctx *c, int32_t fd, const st_ply_header *h, in
                    "NULL argument");
         sog_file_check(out_fd);
         use_device(c);
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         Chain ch{c};
         ply_chain(c, fd, h, element, ch);
+        ST_HIP(hipStreamSynchronize(c->stream));  // (ST_DEBUG's stamps: the ingest alone)
+        const auto t1 = clk::now();
         run_actions(ch, actions, nactions);
         const uint64_t m = ch.n, nch = (m + 255) / 256;
         auto *dchunk = wsT<float>(c, "chain.chunk", nch * 18);
@@ -624,9 +630,18 @@ int st_ply_compressed_ply_file(st_ctx *c, int32_t fd, const st_ply_header *h, in
         auto *dsh = wsT<uint8_t>(c, "chain.sh", m * 3 * (uint64_t)band_coeffs(ch.cols) + 1);
         int32_t C = 0;
         compressed_tail(ch, dchunk, dvert, dsh, &C);
+        ST_HIP(hipStreamSynchronize(c->stream));
+        const auto t2 = clk::now();
         *size = compressed_ply_to_file(c, m, C, dchunk, dvert, dsh, out_fd, version);
         *out_m = m;
         *out_sh_coeffs = C;
+        if (std::getenv("ST_DEBUG")) {
+            const auto ms = [](clk::time_point a, clk::time_point b) {
+                return std::chrono::duration<double, std::milli>(b - a).count();
+            };
+            fprintf(stderr, "[st cply file] ingest %.1f ms, chain %.1f ms, file %.1f ms (%llu rows)\n", ms(t0, t1),
+                    ms(t1, t2), ms(t2, clk::now()), (unsigned long long)m);
+        }
     });
 }
 

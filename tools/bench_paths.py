@@ -217,6 +217,8 @@ def file_path(ctx, host, acts, ref, reps=3):
         if node and os.path.exists(addon):
             r = subprocess.run([node, os.path.join(ROOT, 'tools', 'bench_node_c3.js'), src, d, str(reps)],
                                capture_output=True, text=True, timeout=600)
+            if os.environ.get('ST_DEBUG'):  # the addon's phase stamps
+                sys.stderr.write(r.stderr)
             if r.returncode != 0:
                 out['node_host'] = {'error': r.stderr[-2000:]}
             else:
