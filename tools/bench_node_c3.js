@@ -17,19 +17,26 @@ const host = require(path.join(__dirname, '..', 'splat-transform_amd', 'js'));
     const reps = parseInt(process.argv[4] || '3', 10);
     const actions = [{ kind: 'rotate', value: { x: 0, y: 45, z: 0 } }, { kind: 'filterNaN' }];
     const ms = [];
+    const split = [];
     const sha = [];
+    const d = (a, b) => Number(b - a) / 1e6;
     for (let r = 0; r <= reps; ++r) {
         const dst = path.join(dir, `node${r}.compressed.ply`);
         const t0 = process.hrtime.bigint();
         const inH = await fs.promises.open(src, 'r');
         const outH = await fs.promises.open(dst, 'wx');
+        const t1 = process.hrtime.bigint();
         await host.compressPlyFile(inH, outH, actions);
+        const t2 = process.hrtime.bigint();
         await outH.close();
         await inH.close();
-        const t1 = process.hrtime.bigint();
-        if (r) ms.push(Number(t1 - t0) / 1e6);
+        const t3 = process.hrtime.bigint();
+        if (r) {
+            ms.push(d(t0, t3));
+            split.push({ open: d(t0, t1), call: d(t1, t2), close: d(t2, t3) });
+        }
         sha.push(crypto.createHash('sha256').update(fs.readFileSync(dst)).digest('hex'));
         fs.unlinkSync(dst);
     }
-    console.log(JSON.stringify({ ms, sha256: sha }));
+    console.log(JSON.stringify({ ms, split, sha256: sha }));
 })().catch((e) => { console.error(e); process.exit(1); });

@@ -225,6 +225,7 @@ def file_path(ctx, host, acts, ref, reps=3):
                 res = json.loads(r.stdout.strip().splitlines()[-1])
                 nms = sorted(res['ms'])[len(res['ms']) // 2]
                 out['node_host'] = {'ms': nms, 'Msplats_per_s': n / (nms / 1e3) / 1e6, 'reps': len(res['ms']),
+                                    'split_ms': res.get('split'),
                                     'equals_host_one_call': all(h == want_sha for h in res['sha256']),
                                     'what': 'node tools/bench_node_c3.js: compressPlyFile(inHandle, outHandle '
                                             "('wx', fresh), [rotate 0,45,0, filterNaN]) over napi/addon.node"}
